@@ -1,0 +1,236 @@
+/*
+ * contivcls.h -- C ABI of the MI355X batched first-match ACL classifier.
+ *
+ * This is the drop-in boundary for the Contiv-VPP policy verdict backend.
+ * In the reference the verdict backend is the Go test engine
+ * mock/aclengine/aclengine_mock.go (MockACLEngine); in production it is VPP's
+ * acl-plugin (external C binary, not in the reference tree).  Every entry
+ * point below names the reference interface it replaces (file:line relative to
+ * the reference root).  A Go (cgo) binding of these entry points is shown in
+ * INTEGRATION.md.
+ *
+ * Conventions
+ *  - All functions return 0 (CLS_OK) or a negative CLS_E_* code; the detail is
+ *    available from cls_last_error().  Per-packet semantic failures are
+ *    VERDICTS (CLS_ACL_FAILURE / CLS_CONN_FAILURE), never error codes.
+ *  - The caller owns every buffer.  The engine retains no caller pointer after
+ *    a call returns (cgo rule); rule tables are deep-copied by cls_table_put.
+ *  - Enum values keep the reference's numeric values.
+ *  - IPv4 addresses in the 4-byte SoA are host-order uint32 (a.b.c.d =
+ *    a<<24|b<<16|c<<8|d).  16-byte addresses are network-order bytes; an
+ *    IPv4-mapped address (::ffff:a.b.c.d) is an IPv4 packet, exactly like Go's
+ *    net.IP.To4().
+ */
+#ifndef CONTIVCLS_H
+#define CONTIVCLS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CLS_ABI_VERSION 1
+
+/* ---- status codes ------------------------------------------------------ */
+enum {
+    CLS_OK = 0,
+    CLS_E_INVAL = -1,    /* bad argument / malformed rule (would panic in Go) */
+    CLS_E_NOMEM = -2,
+    CLS_E_HIP = -3,      /* HIP runtime error */
+    CLS_E_RCCL = -4,     /* reserved: collective error */
+    CLS_E_NOTFOUND = -5, /* unknown table / ACL name */
+    CLS_E_NODEV = -6     /* no usable gfx950 device */
+};
+
+/* ---- reference enums ----------------------------------------------------- */
+/* vpp_acl.AclAction (acl.proto:4-8); any other int32 is carried verbatim. */
+enum { CLS_ACTION_DENY = 0, CLS_ACTION_PERMIT = 1, CLS_ACTION_REFLECT = 2 };
+
+/* ACLAction returned by evalACL (aclengine_mock.go:63-77). */
+enum {
+    CLS_ACL_DENY = 0,
+    CLS_ACL_PERMIT = 1,
+    CLS_ACL_REFLECT = 2,
+    CLS_ACL_FAILURE = 3
+};
+
+/* ConnectionAction returned by Connection* (aclengine_mock.go:46-60). */
+enum {
+    CLS_CONN_DENY_SYN = 0,
+    CLS_CONN_DENY_SYN_ACK = 1,
+    CLS_CONN_ALLOW = 2,
+    CLS_CONN_FAILURE = 3
+};
+
+/* ProtocolType (aclengine_mock.go:80-91).  Any other value takes evalACL's
+ * `switch protocol` fall-through (no case): networks alone decide. */
+enum { CLS_PROTO_TCP = 0, CLS_PROTO_UDP = 1, CLS_PROTO_ICMP = 2 };
+
+/* ---- one ACL rule, as the vpp_acl protobuf carries it --------------------
+ * Mirrors AccessLists_Acl_Rule (acl.pb.go / acl.proto:17-146).  Presence bits
+ * stand for the nil-ness of each protobuf sub-message, because evalACL's
+ * semantics depend on it (aclengine_mock.go:481-664).  Networks are the CIDR
+ * STRINGS of the protobuf; the engine parses them with Go 1.9 net.ParseCIDR
+ * semantics, so a string that fails to parse yields the same FAILURE verdicts
+ * the Go engine returns.  NULL or "" means "no network" (match all).
+ */
+enum {
+    CLS_R_MATCHES = 1u << 0,     /* rule.Matches != nil (nil would panic: rejected) */
+    CLS_R_MACIP = 1u << 1,       /* Matches.MacipRule != nil */
+    CLS_R_IPRULE = 1u << 2,      /* Matches.IpRule != nil */
+    CLS_R_IP = 1u << 3,          /* IpRule.Ip != nil */
+    CLS_R_OTHER = 1u << 4,       /* IpRule.Other != nil */
+    CLS_R_TCP = 1u << 5,         /* IpRule.Tcp != nil */
+    CLS_R_TCP_SRC = 1u << 6,     /* Tcp.SourcePortRange != nil */
+    CLS_R_TCP_DST = 1u << 7,     /* Tcp.DestinationPortRange != nil */
+    CLS_R_UDP = 1u << 8,         /* IpRule.Udp != nil */
+    CLS_R_UDP_SRC = 1u << 9,
+    CLS_R_UDP_DST = 1u << 10,
+    CLS_R_ICMP = 1u << 11,       /* IpRule.Icmp != nil */
+    CLS_R_ICMP_CODE = 1u << 12,  /* Icmp.IcmpCodeRange != nil */
+    CLS_R_ICMP_TYPE = 1u << 13,  /* Icmp.IcmpTypeRange != nil */
+    CLS_R_ICMPV6 = 1u << 14,     /* Icmp.Icmpv6 == true */
+    CLS_R_ACTIONS = 1u << 15     /* rule.Actions != nil */
+};
+
+typedef struct cls_rule {
+    uint32_t flags;             /* CLS_R_* */
+    int32_t acl_action;         /* Actions.AclAction (vpp_acl.AclAction) */
+    const char* src_network;    /* IpRule.Ip.SourceNetwork */
+    const char* dst_network;    /* IpRule.Ip.DestinationNetwork */
+    uint32_t tcp_src_lo, tcp_src_hi, tcp_dst_lo, tcp_dst_hi;
+    uint32_t udp_src_lo, udp_src_hi, udp_dst_lo, udp_dst_hi;
+    uint32_t icmp_code_first, icmp_code_last, icmp_type_first, icmp_type_last;
+} cls_rule;
+
+/* ---- packet batches (structure of arrays) -------------------------------- */
+enum { CLS_AF_V4 = 4, CLS_AF_V16 = 16 };
+
+typedef struct cls_pkt_soa {
+    uint32_t af;               /* CLS_AF_V4: src4/dst4; CLS_AF_V16: src16/dst16 */
+    const uint32_t* src4;      /* host-order IPv4 */
+    const uint32_t* dst4;
+    const uint8_t* src16;      /* n x 16 bytes */
+    const uint8_t* dst16;
+    const uint16_t* sport;     /* used by the connection path only (SYN-ACK) */
+    const uint16_t* dport;
+    const uint8_t* proto;      /* ProtocolType */
+} cls_pkt_soa;
+
+/* cls_classify / cls_connect_batch flags */
+enum {
+    CLS_F_DEVICE = 1u << 0,       /* every pointer is device memory on this engine's GPU */
+    CLS_F_NO_VERDICT = 1u << 1,   /* verdict_out may be NULL (counters only) */
+    CLS_F_ACCUMULATE = 1u << 2,   /* add to counters_out instead of overwriting */
+    CLS_F_FORCE_LINEAR = 1u << 3, /* use the linear (ballot) kernel: GPU cross-check */
+    CLS_F_TIMING = 1u << 4        /* record HIP events around the classify kernel */
+};
+
+typedef struct cls_engine cls_engine;
+
+typedef struct cls_config {
+    int device;                /* HIP device ordinal; -1 = current device */
+    uint32_t reserved[7];
+} cls_config;
+
+/* ---- engine lifetime ---------------------------------------------------- */
+/* Replaces NewMockACLEngine (aclengine_mock.go:124). */
+int cls_engine_create(const cls_config* cfg, cls_engine** out);
+void cls_engine_destroy(cls_engine* e);
+const char* cls_last_error(const cls_engine* e);
+int cls_abi_version(void);
+
+/* ---- rule tables (one compiled, device-resident ACL) -------------------
+ * cls_table_put compiles an ACL's rules (evalACL semantics,
+ * aclengine_mock.go:473-668) into the engine's device layout and uploads it.
+ * Replaces the per-evaluation re-parse of acl.Rules (aclengine_mock.go:480-524).
+ */
+int cls_table_put(cls_engine* e, const char* name, const cls_rule* rules,
+                  uint32_t n_rules, uint32_t* table_id);
+int cls_table_del(cls_engine* e, uint32_t table_id);
+
+typedef struct cls_table_info {
+    uint32_t n_rules;          /* R: counters_out has R+1 entries */
+    uint32_t kernel;           /* 0 = linear (ballot) kernel, 1 = compiled classifier */
+    uint32_t lds_bytes;        /* LDS image of the compiled classifier (v4) */
+    uint32_t n_intervals;      /* elementary source intervals (v4) */
+    uint32_t n_classes;        /* distinct source-prefix classes (v4) */
+    uint32_t n_templates;      /* distinct (dst, port range, result) tuples (v4) */
+    uint32_t n_slots;          /* flattened candidate slots (v4) */
+    uint32_t lds_resident;     /* 1 if the classifier fits LDS, else global memory */
+    uint32_t reserved[8];
+} cls_table_info;
+int cls_table_get_info(cls_engine* e, uint32_t table_id, cls_table_info* info);
+
+/* ---- batched first-match -------------------------------------------------
+ * verdict_out[i] = evalACL(acl, pkt i) (ACLAction, aclengine_mock.go:473-668).
+ * counters_out[k] (k < R) = packets whose evaluation terminated at rule k,
+ * counters_out[R] = packets that fell through to the default DENY (:667).
+ * `stream` is a hipStream_t (NULL: the engine's own stream).  The call is
+ * synchronous with respect to the host unless CLS_F_DEVICE is set, in which
+ * case work is only enqueued on `stream`.
+ */
+int cls_classify(cls_engine* e, uint32_t table_id, const cls_pkt_soa* pkts,
+                 uint64_t n, uint8_t* verdict_out, uint64_t* counters_out,
+                 uint32_t flags, void* stream);
+
+/* Milliseconds of the last classify kernel (CLS_F_TIMING), measured with HIP
+ * events on the launch stream.  Blocks until that kernel has finished. */
+int cls_last_kernel_ms(cls_engine* e, float* ms);
+
+/* ---- ACL configuration (ACLConfig, aclengine_mock.go:110-121,671-728) --- */
+/* PutACL semantics (:699-728): requires >=1 interface; re-putting a name
+ * replaces it without counting an extra change; last writer wins per
+ * interface direction. */
+int cls_acl_put(cls_engine* e, const char* acl_name, const cls_rule* rules,
+                uint32_t n_rules, const char* const* ingress_ifs, uint32_t n_ingress,
+                const char* const* egress_ifs, uint32_t n_egress);
+/* DelACL semantics (:680-696). */
+int cls_acl_del(cls_engine* e, const char* acl_name);
+/* GetNumOfACLs (:209), GetNumOfACLChanges (:237). */
+int cls_acl_counts(cls_engine* e, uint32_t* n_acls, uint32_t* n_changes);
+/* Interface id used by cls_conn_batch; ids are stable for the engine's life. */
+int cls_if_id(cls_engine* e, const char* if_name, uint32_t* id);
+/* Table id of the inbound/outbound ACL on an interface, -1 if none
+ * (GetInboundACL / GetOutboundACL, :215-225). */
+int cls_if_acls(cls_engine* e, uint32_t if_id, int32_t* in_table, int32_t* out_table);
+
+/* ---- batched connection verdicts (testConnection, :394-471) -------------
+ * For each connection i: SYN through src_if inbound then dst_if outbound
+ * with (src->dst, dport); SYN-ACK through dst_if inbound then src_if outbound
+ * with (dst->src, sport); REFLECT marks sides reflected exactly as the
+ * reference does.  Interface->ACL bindings are snapshotted at the call.
+ */
+typedef struct cls_conn_soa {
+    cls_pkt_soa pkt;           /* src/dst/sport/dport/proto of the SYN */
+    const uint32_t* src_if;    /* interface ids (cls_if_id) */
+    const uint32_t* dst_if;
+} cls_conn_soa;
+int cls_connect_batch(cls_engine* e, const cls_conn_soa* conns, uint64_t n,
+                      uint8_t* conn_verdict_out, uint32_t flags, void* stream);
+
+/* ---- synthetic traffic (BASELINE.md / SURVEY 8(d) generator) -----------
+ * Generates packets i in [first, first+n) of the counter-based splitmix64
+ * stream directly into device memory (no PCIe).  Pools: pod IPs, rule
+ * destination prefixes (addr, prefix length) and ports drawn from the table.
+ */
+typedef struct cls_traffic_spec {
+    uint64_t seed;
+    uint32_t pct_pod_src;      /* % of packets whose src is a pod IP (60) */
+    uint32_t pct_rule_dst;     /* % whose dst lies in a rule dst prefix (50) */
+    uint32_t pct_table_port;   /* % whose dport is one of the table ports (50) */
+    uint32_t pct_icmp;         /* % ICMP (0 or 10); the rest split TCP/UDP evenly */
+    const uint32_t* pod_ips; uint32_t n_pod_ips;
+    const uint32_t* dst_addrs; const uint8_t* dst_lens; uint32_t n_dst;
+    const uint16_t* ports; uint32_t n_ports;
+} cls_traffic_spec;
+int cls_gen_traffic_v4(cls_engine* e, const cls_traffic_spec* spec, uint64_t first,
+                       uint64_t n, uint32_t* src4, uint32_t* dst4, uint16_t* sport,
+                       uint16_t* dport, uint8_t* proto, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CONTIVCLS_H */
