@@ -1,0 +1,188 @@
+#!/usr/bin/env python3
+"""Benchmark: Mpps classified at 10k ACL rules per MI355X, and % of HBM roofline.
+
+Workload (BASELINE.json configs[2]): the ~10k-rule
+global ACL of a 1000-pod render (vpp_amd/workload.py), 256 Mi synthetic IPv4
+TCP/UDP packets per GPU generated in HBM by the splitmix64 stream (seed
+0xC0175EED03, rank r generates packets [r*N, (r+1)*N)).  A step = one
+classify pass over the batch (verdict per packet + per-rule hit counters),
+plus, at N>1 GPUs, the RCCL all-reduce of the hit counters (the only
+collective: packets shard across ranks, the table is replicated).
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+N>1 is launched by torch.distributed.run, one rank per GPU.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBPS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
+BYTES_PER_PKT = 12              # src 4 + dst 4 + dport 2 + proto 1 + verdict 1
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", type=int, default=3, choices=[2, 3])
+    ap.add_argument("--packets", type=int, default=0, help="packets per GPU (default: config's)")
+    ap.add_argument("--cpu-sample", type=int, default=1 << 21,
+                    help="packets timed on the host for the CPU baseline (0: skip)")
+    ap.add_argument("--faithful-sample", type=int, default=4096)
+    return ap.parse_args()
+
+
+def cpu_baseline(acl, spec, sample: int, faithful_sample: int):
+    """Oracle CPU port on the host cores (OpenMP), and the faithful Go-style
+    evaluator (string re-parse per rule, one thread) on a smaller prefix."""
+    import oracle
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    tr = oracle.gen_traffic_v4(spec, 0, sample)
+    cr = oracle.rules_to_c(acl.rules)
+    ft = oracle.FastTable(cr)
+    ft.classify(tr["src"][:1024], tr["dst"][:1024], tr["dport"][:1024], tr["proto"][:1024],
+                nthreads=threads)
+    t0 = time.perf_counter()
+    ft.classify(tr["src"], tr["dst"], tr["dport"], tr["proto"], nthreads=threads)
+    dt = time.perf_counter() - t0
+    out = {"value": round(sample / dt / 1e6, 4), "unit": "Mpps", "cores": threads, "kind": "port",
+           "sample": "%d packets of the same config stream (oracle/aclengine_ref.c orc_classify_fast, "
+                     "rules pre-parsed, OpenMP %d threads), %.1f s" % (sample, threads, dt)}
+    if faithful_sample:
+        f = {k: v[:faithful_sample] for k, v in tr.items()}
+        t0 = time.perf_counter()
+        oracle.classify_faithful(cr, f["src"], f["dst"], f["dport"], f["proto"])
+        dt2 = time.perf_counter() - t0
+        out["faithful"] = {"value": round(faithful_sample / dt2 / 1e6, 6), "unit": "Mpps", "cores": 1,
+                           "sample": "%d packets, evalACL restated literally (CIDR strings re-parsed "
+                                     "per rule per packet, aclengine_mock.go:500,514), %.1f s"
+                                     % (faithful_sample, dt2)}
+    return out
+
+
+def pmc_traffic(cfg: int, n: int):
+    """Per-launch HBM bytes of the classify kernel from the committed rocprofv3
+    PMC summary (profiles/pmc_*.json, written by tools/pmc_traffic.py)."""
+    import glob
+    best = None
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json"))):
+        try:
+            d = json.load(open(p))
+        except Exception:
+            continue
+        if d.get("config") == cfg and d.get("packets") == n:
+            best = d
+    return None if best is None else best.get("hbm_bytes_per_launch")
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+
+    from vpp_amd import workload
+    from vpp_amd.engine import Engine
+
+    acl, spec, n_default = workload.config(args.config)
+    n = args.packets or n_default
+    eng = Engine(torch.cuda.current_device())
+    table = eng.put_table("contiv/vpp-policy-GLOBAL", acl.rules)
+    info = table.info()
+    R = table.n_rules
+
+    dev = torch.device("cuda", torch.cuda.current_device())
+    pk = {k: torch.empty(n, dtype=dt, device=dev) for k, dt in
+          (("src", torch.int32), ("dst", torch.int32), ("dport", torch.int16), ("proto", torch.uint8))}
+    eng.gen_traffic_v4(spec, rank * n, pk)
+    verdict = torch.empty(n, dtype=torch.uint8, device=dev)
+    counters = torch.zeros(R + 1, dtype=torch.int64, device=dev)
+    torch.cuda.synchronize()
+
+    def step(timing):
+        eng.classify(table, pk["src"], pk["dst"], pk["dport"], pk["proto"], verdict=verdict,
+                     counters=counters, timing=timing)
+        if world > 1:
+            dist.all_reduce(counters)      # RCCL over xGMI: merge per-rule hit counters
+
+    for _ in range(args.warmup):
+        step(False)
+    torch.cuda.synchronize()
+    eng.kernel_times(reset=True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    kms = eng.kernel_times(reset=True)
+    t = torch.tensor([wall], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    wall = float(t.item())
+
+    if rank == 0:
+        total = n * world * args.steps
+        mpps = total / wall / 1e6
+        avg_k = float(np.mean(kms)) if kms else float("nan")
+        alg_bytes = n * BYTES_PER_PKT + (R + 1) * 8
+        achieved = alg_bytes / (avg_k / 1e3) / 1e9
+        traffic = pmc_traffic(args.config, n)
+        cpu = None
+        if world == 1 and args.cpu_sample:
+            cpu = cpu_baseline(acl, spec, args.cpu_sample, args.faithful_sample)
+        line = {
+            "metric": "Mpps classified at 10k ACL rules, 1/8 GPU; % of HBM roofline",
+            "value": round(mpps, 2),
+            "unit": "Mpps",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(wall / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic (splitmix64 stream generated in HBM, seed %#x; rules rendered from a "
+                    "synthetic 1000-pod policy set)" % spec["seed"],
+            "config": {"workload": "config%d: %d-rule global ACL (%d pods), %d IPv4 TCP/UDP packets per GPU"
+                                   % (args.config, R, len(spec["pod_ips"]), n),
+                       "rules": R, "packets_per_gpu": n, "layout": "IPv4 SoA, 12 B/packet",
+                       "kernel": "classifier" if info["kernel"] == 1 else "linear",
+                       "lds_bytes": info["lds_bytes"], "parallelism": "dp%d" % world},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                         "traffic": traffic,
+                         "kernel_ms_avg": round(avg_k, 4),
+                         "algorithmic_bytes_per_launch": alg_bytes},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -179,6 +179,11 @@ int cls_classify(cls_engine* e, uint32_t table_id, const cls_pkt_soa* pkts,
 /* Milliseconds of the last classify kernel (CLS_F_TIMING), measured with HIP
  * events on the launch stream.  Blocks until that kernel has finished. */
 int cls_last_kernel_ms(cls_engine* e, float* ms);
+/* Every classify kernel timed (CLS_F_TIMING) since the last reset: up to `cap`
+ * durations in launch order; *count = number recorded.  Recording enqueues
+ * only events (no host synchronisation); reading blocks on the last one. */
+int cls_kernel_times(cls_engine* e, float* ms, uint32_t cap, uint32_t* count);
+int cls_kernel_times_reset(cls_engine* e);
 
 /* ---- ACL configuration (ACLConfig, aclengine_mock.go:110-121,671-728) --- */
 /* PutACL semantics (:699-728): requires >=1 interface; re-putting a name
@@ -189,6 +194,8 @@ int cls_acl_put(cls_engine* e, const char* acl_name, const cls_rule* rules,
                 const char* const* egress_ifs, uint32_t n_egress);
 /* DelACL semantics (:680-696). */
 int cls_acl_del(cls_engine* e, const char* acl_name);
+/* Table id of the installed ACL `acl_name` (GetACLByName, :228-234). */
+int cls_acl_table(cls_engine* e, const char* acl_name, uint32_t* table_id);
 /* GetNumOfACLs (:209), GetNumOfACLChanges (:237). */
 int cls_acl_counts(cls_engine* e, uint32_t* n_acls, uint32_t* n_changes);
 /* Interface id used by cls_conn_batch; ids are stable for the engine's life. */
@@ -229,6 +236,25 @@ typedef struct cls_traffic_spec {
 int cls_gen_traffic_v4(cls_engine* e, const cls_traffic_spec* spec, uint64_t first,
                        uint64_t n, uint32_t* src4, uint32_t* dst4, uint16_t* sport,
                        uint16_t* dport, uint8_t* proto, void* stream);
+
+/* ---- offline compilation (no device needed) -----------------------------
+ * Compiles an ACL exactly as cls_table_put does and writes the IPv4 device
+ * layouts into `blob`: a cls_image_v4_header followed by the classifier image,
+ * the slot->rule map and the linear rules.  With cap too small (or blob NULL)
+ * only *need is set.  Used for inspection and CPU-side verification of the
+ * compiler.
+ */
+typedef struct cls_image_v4_header {
+    uint32_t magic;            /* 0x434C5334 "CLS4" */
+    uint32_t version;
+    uint32_t n_rules, n_lin, has_cls;
+    uint32_t img_bytes, off_bounds, off_iclass, off_cells, off_lists, off_tmpl;
+    uint32_t n_bounds, search_top, n_classes, n_tmpl, n_list_entries, n_ctr, lds_bytes;
+    uint32_t off_image, off_ctr_rule, off_lin;   /* byte offsets inside the blob */
+    uint32_t total_bytes;
+} cls_image_v4_header;
+int cls_compile_v4(const cls_rule* rules, uint32_t n_rules, void* blob, uint64_t cap,
+                   uint64_t* need);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,133 @@
+"""Random ACL and traffic generators for parity tests (test infrastructure).
+
+``random_acl`` produces adversarial rule lists that exercise every branch of
+evalACL (mock/aclengine/aclengine_mock.go:480-667): nested and disjoint
+prefixes of every length, IPv6 and IPv4-mapped strings, malformed CIDRs,
+missing/extra protocol sections and port ranges, non-full source ranges,
+reversed and wide destination ranges (with uint16 truncation), ICMP
+code/type ranges, Icmpv6, MAC-IP / Other sections, unknown actions.
+"""
+from __future__ import annotations
+
+import random
+
+import numpy as np
+
+from vpp_amd import model as M
+
+
+def _v4(a):
+    return "%d.%d.%d.%d" % ((a >> 24) & 255, (a >> 16) & 255, (a >> 8) & 255, a & 255)
+
+
+class PrefixPool:
+    def __init__(self, rng: random.Random, n=24):
+        self.rng = rng
+        self.v4 = []
+        base = [rng.getrandbits(32) for _ in range(max(2, n // 4))]
+        for _ in range(n):
+            b = rng.choice(base)
+            ln = rng.choice([0, 1, 8, 12, 16, 20, 24, 24, 28, 30, 31, 32, 32, 32])
+            b ^= rng.getrandbits(32) >> max(ln, 1) if rng.random() < 0.5 else 0
+            mask = (0xFFFFFFFF << (32 - ln)) & 0xFFFFFFFF if ln else 0
+            self.v4.append((b & mask, ln))
+
+    def cidr(self, allow_weird=True) -> str:
+        rng = self.rng
+        r = rng.random()
+        if not allow_weird or r < 0.80:
+            a, ln = rng.choice(self.v4)
+            if rng.random() < 0.1:                       # host bits set: ParseCIDR masks them
+                a |= rng.getrandbits(32) & ((1 << (32 - ln)) - 1 if ln < 32 else 0)
+            return "%s/%d" % (_v4(a), ln)
+        if r < 0.86:                                      # IPv4-mapped IPv6 spelling
+            a, ln = rng.choice(self.v4)
+            return "::ffff:%s/%d" % (_v4(a), 96 + ln)
+        if r < 0.90:
+            return rng.choice(["fd00:10::/64", "::/0", "2001:db8::1/128", "::ffff:0:0/95"])
+        return rng.choice(["10.0.0.0/33", "10.0.0/8", "garbage", "1.2.3.4", "300.1.1.1/8",
+                           "10.0.0.0/", "/8", "::ffff:10.0.0.0/95", "010.001.0.0/16"])
+
+
+def random_rule(rng: random.Random, pool: PrefixPool, weird: float = 0.15) -> M.Rule:
+    w = lambda: rng.random() < weird
+    action = rng.choice([M.DENY, M.PERMIT, M.PERMIT, M.REFLECT])
+    if w():
+        action = rng.choice([3, -1, 7])
+    actions = None if w() and rng.random() < 0.3 else M.Actions(action)
+    if w() and rng.random() < 0.15:
+        return M.Rule(actions=actions, matches=M.Matches(macip_rule=M.MacIpRule()))
+    if w() and rng.random() < 0.1:
+        return M.Rule(actions=actions, matches=M.Matches())
+    ip = M.Ip(source_network=pool.cidr(weird > 0) if rng.random() < 0.7 else "",
+              destination_network=pool.cidr(weird > 0) if rng.random() < 0.6 else "")
+    ipr = M.IpRule(ip=None if (w() and rng.random() < 0.1) else ip)
+    kind = rng.choice(["tcp", "udp", "tcp", "udp", "icmp"] + (["none", "both", "other"] if w() else []))
+
+    def prange(src=False):
+        if src:
+            if w():
+                return rng.choice([None, M.PortRange(0, 1000), M.PortRange(1, 65535)])
+            return M.PortRange(0, 65535)
+        r = rng.random()
+        if r < 0.35:
+            return M.PortRange(0, 65535)
+        if r < 0.75:
+            p = rng.choice([22, 53, 80, 161, 443, 8080, rng.randint(1, 65535)])
+            return M.PortRange(p, p)
+        lo = rng.randint(0, 65535)
+        hi = rng.randint(lo, 65535)
+        if w():
+            return rng.choice([None, M.PortRange(hi, lo), M.PortRange(70000, 80000),
+                               M.PortRange(65536 + 80, 65536 + 90)])
+        return M.PortRange(lo, hi)
+
+    if kind in ("tcp", "both"):
+        ipr.tcp = M.Tcp(destination_port_range=prange(), source_port_range=prange(True))
+    if kind in ("udp", "both"):
+        ipr.udp = M.Udp(destination_port_range=prange(), source_port_range=prange(True))
+    if kind == "icmp":
+        code = M.IcmpRange(0, 5) if not w() else rng.choice([None, M.IcmpRange(0, 4)])
+        typ = M.IcmpRange(0, 16) if not w() else rng.choice([None, M.IcmpRange(1, 16)])
+        ipr.icmp = M.Icmp(icmpv6=w() and rng.random() < 0.3, icmp_code_range=code,
+                          icmp_type_range=typ)
+    if kind == "other":
+        ipr.other = M.Other(protocol=47)
+    return M.Rule(actions=actions, matches=M.Matches(ip_rule=ipr))
+
+
+def random_acl(seed: int, n_rules: int, weird: float = 0.15, n_prefixes: int = 24):
+    rng = random.Random(seed)
+    pool = PrefixPool(rng, n_prefixes)
+    return [random_rule(rng, pool, weird) for _ in range(n_rules)], pool
+
+
+def random_traffic(seed: int, n: int, pool: PrefixPool, other_proto: bool = True):
+    """IPv4 packets biased towards the prefixes' edges."""
+    rng = np.random.default_rng(seed)
+    pfx = np.array([a for a, _ in pool.v4], np.uint64)
+    size = np.array([(1 << (32 - ln)) for _, ln in pool.v4], np.uint64)
+
+    def addrs():
+        choice = rng.integers(0, 5, n)
+        i = rng.integers(0, len(pfx), n)
+        inside = (pfx[i] + rng.integers(0, 1 << 62, n, dtype=np.uint64) % size[i]) & 0xFFFFFFFF
+        first = pfx[i]
+        last = (pfx[i] + size[i] - 1) & 0xFFFFFFFF
+        past = (pfx[i] + size[i]) & 0xFFFFFFFF
+        uni = rng.integers(0, 1 << 32, n, dtype=np.uint64)
+        out = np.select([choice == 0, choice == 1, choice == 2, choice == 3],
+                        [inside, first, last, past], uni)
+        edge = rng.random(n) < 0.01
+        out[edge] = rng.choice(np.array([0, 0xFFFFFFFF], np.uint64), edge.sum())
+        return out.astype(np.uint32)
+
+    src, dst = addrs(), addrs()
+    ports = np.array([0, 1, 22, 53, 79, 80, 81, 161, 443, 8080, 65535], np.uint16)
+    dport = np.where(rng.random(n) < 0.6, rng.choice(ports, n),
+                     rng.integers(0, 65536, n)).astype(np.uint16)
+    pvals = [0, 1, 2, 3, 17] if other_proto else [0, 1, 2]
+    pw = [0.4, 0.4, 0.14, 0.03, 0.03] if other_proto else [0.43, 0.43, 0.14]
+    proto = rng.choice(np.array(pvals, np.uint8), n, p=pw)
+    sport = rng.integers(1024, 65536, n).astype(np.uint16)
+    return dict(src=src, dst=dst, dport=dport, proto=proto, sport=sport)

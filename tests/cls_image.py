@@ -1,0 +1,120 @@
+"""CPU interpreter of the compiled IPv4 device layouts (test infrastructure).
+
+Reads the blob of ``cls_compile_v4`` (include/contivcls.h) and evaluates it
+exactly as the gfx950 kernels do (vpp_amd/csrc/kernels.hip: classify4_cls's
+branch-free interval search -> class -> cell -> template scan; linear_one
+for protocols > 2), so the rule compiler can be checked against the oracle
+without a GPU.  Never used by the product.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from vpp_amd import _abi
+
+
+def compile_blob(crules) -> bytes:
+    L = _abi.lib()
+    need = C.c_uint64(0)
+    rc = L.cls_compile_v4(crules.ptr(), crules.n, None, 0, C.byref(need))
+    if rc != 0:
+        raise RuntimeError("cls_compile_v4 rc=%d" % rc)
+    buf = C.create_string_buffer(need.value)
+    rc = L.cls_compile_v4(crules.ptr(), crules.n, buf, need.value, C.byref(need))
+    if rc != 0:
+        raise RuntimeError("cls_compile_v4 rc=%d" % rc)
+    return buf.raw
+
+
+class Image:
+    def __init__(self, blob: bytes):
+        h = _abi.ImageHeader.from_buffer_copy(blob)
+        assert h.magic == 0x434C5334
+        self.h = h
+        self.n_rules = h.n_rules
+        lin = np.frombuffer(blob, np.uint32, count=h.n_lin * 12, offset=h.off_lin).reshape(-1, 12)
+        self.lin = lin
+        self.has_cls = bool(h.has_cls)
+        if self.has_cls:
+            img = blob[h.off_image:h.off_image + h.img_bytes]
+            top = h.search_top
+            self.bounds = np.frombuffer(img, np.uint32, count=2 * top, offset=h.off_bounds)
+            self.iclass = np.frombuffer(img, np.uint16, count=2 * top, offset=h.off_iclass)
+            self.cells = np.frombuffer(img, np.uint32, count=h.n_classes * 6,
+                                       offset=h.off_cells).reshape(-1, 2)
+            self.lists = np.frombuffer(img, np.uint16, count=h.n_list_entries, offset=h.off_lists)
+            self.tmpl = np.frombuffer(img, np.uint32, count=h.n_tmpl * 4,
+                                      offset=h.off_tmpl).reshape(-1, 4)
+            self.ctr_rule = np.frombuffer(blob, np.uint32, count=h.n_ctr, offset=h.off_ctr_rule)
+
+    @staticmethod
+    def _port_in(dport, pw):
+        return ((dport.astype(np.uint32) - (pw & 0xFFFF)) & 0xFFFF) <= (pw >> 16)
+
+    def linear(self, src, dst, dport, proto):
+        n = len(src)
+        p = np.where(proto <= 2, proto, 3).astype(np.uint32)
+        res = np.zeros(n, np.uint32)
+        rule = np.full(n, self.n_rules, np.int64)
+        done = np.zeros(n, bool)
+        for r in self.lin:
+            meta = (r[8] >> (8 * p)) & 0xFF
+            pw = r[4 + p]
+            m = (~done & ((meta & 0x80) != 0) & (((src ^ r[0]) & r[1]) == 0) &
+                 (((dst ^ r[2]) & r[3]) == 0) & self._port_in(dport, pw))
+            res[m] = meta[m] & 3
+            rule[m] = r[9]
+            done |= m
+            if done.all():
+                break
+        return res, rule
+
+    def classify(self, src, dst, dport, proto):
+        """Returns (verdict u8[n], counters u64[R+1])."""
+        src = np.asarray(src, np.uint32)
+        dst = np.asarray(dst, np.uint32)
+        dport = np.asarray(dport, np.uint16)
+        proto = np.asarray(proto, np.uint8)
+        n = len(src)
+        counters = np.zeros(self.n_rules + 1, np.uint64)
+        if not self.has_cls:
+            res, rule = self.linear(src, dst, dport, proto)
+            np.add.at(counters, rule, 1)
+            return res.astype(np.uint8), counters
+        h = self.h
+        k = np.zeros(n, np.int64)
+        s = h.search_top
+        while s:
+            c = k + s
+            k = np.where(self.bounds[c] <= src, c, k)
+            s >>= 1
+        cls = self.iclass[k].astype(np.int64)
+        pr = np.minimum(proto, 2).astype(np.int64)
+        cell = self.cells[cls * 3 + pr]
+        start = (cell[:, 0] & 0xFFFF).astype(np.int64)
+        ln = (cell[:, 0] >> 16).astype(np.int64)
+        base = cell[:, 1].astype(np.int64)
+        res = np.zeros(n, np.uint32)
+        slot = np.zeros(n, np.int64)
+        done = np.zeros(n, bool)
+        for j in range(int(ln.max()) if n else 0):
+            act = ~done & (j < ln)
+            if not act.any():
+                break
+            tid = self.lists[np.where(act, start + j, 0)]
+            tm = self.tmpl[tid]
+            m = act & (((dst ^ tm[:, 0]) & tm[:, 1]) == 0) & self._port_in(dport, tm[:, 2])
+            res[m] = tm[m, 3]
+            slot[m] = base[m] + j
+            done |= m
+        np.add.at(counters, self.ctr_rule[slot].astype(np.int64), 1)
+        other = proto > 2
+        if other.any():
+            r2, rule2 = self.linear(src[other], dst[other], dport[other], proto[other])
+            res[other] = r2
+            # undo the slot count made above for these packets, use the rule path
+            np.subtract.at(counters, self.ctr_rule[slot[other]].astype(np.int64), 1)
+            np.add.at(counters, rule2, 1)
+        return res.astype(np.uint8), counters

@@ -1,0 +1,42 @@
+"""CPU checks of the drop-in boundary: the gfx950 library loads and exports
+every entry point include/contivcls.h declares (no compute calls here)."""
+import os
+import re
+
+from vpp_amd import _abi
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_symbols():
+    text = open(os.path.join(ROOT, "include", "contivcls.h")).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:int|void|const char\*)\s+(cls_\w+)\s*\(", text, re.M)))
+
+
+def test_library_exports_every_declared_symbol():
+    L = _abi.lib()
+    decl = declared_symbols()
+    assert len(decl) >= 18
+    for sym in decl:
+        assert hasattr(L, sym), sym
+    assert sorted(_abi.SYMBOLS) == decl
+
+
+def test_abi_version():
+    assert _abi.lib().cls_abi_version() == 1
+
+
+def test_engine_create_without_gpu_fails_loudly():
+    import torch
+    if torch.cuda.is_available():
+        return
+    import pytest
+    from vpp_amd.engine import Engine
+    with pytest.raises(_abi.ClsError):
+        Engine()
+
+
+def test_library_is_gfx950_code_object():
+    data = open(_abi.LIB_PATH, "rb").read()
+    assert b"gfx950" in data

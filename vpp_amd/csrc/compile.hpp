@@ -1,0 +1,99 @@
+// Rule-set compiler: ACL rules (cls_rule) -> device layouts.
+//
+// Stage 1 (semantic): every rule is reduced, per packet address family, to
+// the decision evalACL makes for it (mock/aclengine/aclengine_mock.go:480-664):
+//   src prefix | ANY, dst prefix | ANY, and per packet protocol
+//   (TCP, UDP, ICMP, OTHER) either SKIP (the `continue` branches) or
+//   TERM(port range, result) where result is DENY/PERMIT/REFLECT/FAILURE.
+//   Unconditional failures (MacipRule, missing IpRule/Ip, Other section, src
+//   parse error) become an ANY/ANY rule that terminates every protocol with
+//   FAILURE; a dst parse error does the same once the src prefix matched.
+//   Rules after an unconditional terminator are unreachable and dropped.
+//
+// Stage 2a (linear): the semantic rules in order, 48 B each -- the table of the
+//   ballot kernel (small tables, GPU cross-check, OTHER-protocol fallback).
+// Stage 2b (classifier, IPv4): first-match is decided per packet by
+//   (1) the source address's elementary interval (binary search over the
+//       sorted boundaries of every source prefix), which fixes the set of
+//       source prefixes covering it (they nest: a laminar family) -> class;
+//   (2) the cell (class, protocol) -> the ordered candidate list of rules that
+//       cover that class and do not SKIP that protocol, truncated after the
+//       first rule that matches every packet of the cell;
+//   (3) a scan of the candidate list comparing only dst prefix and dst port.
+//   Candidates are stored as 16-bit ids of deduplicated templates
+//   (dst, port range, result); identical lists are stored once.  Hit counters
+//   are one u32 per (cell, position) "slot", mapped back to rule indices
+//   after the kernel (slot 0 = default DENY = counter R).
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/contivcls.h"
+#include "goparse.hpp"
+
+namespace cls {
+
+enum : uint8_t { RES_DENY = 0, RES_PERMIT = 1, RES_REFLECT = 2, RES_FAIL = 3 };
+enum : int { P_TCP = 0, P_UDP = 1, P_ICMP = 2, P_OTHER = 3, NPROTO = 4 };
+
+struct Term {
+    bool term = false;     // false = SKIP (rule never matches this protocol)
+    uint16_t lo = 0, hi = 0xFFFF;
+    uint8_t res = RES_DENY;
+};
+
+struct SemRule {
+    uint32_t index = 0;    // rule index in the ACL
+    bool src_any = true;
+    Prefix src;
+    bool dst_any = true;
+    Prefix dst;
+    Term t[NPROTO];
+};
+
+// Reduce the ACL for packets of family `fam` (4 or 16).  Returns CLS_OK or
+// CLS_E_INVAL (a rule with nil Matches: Go would panic).
+int semantic_rules(const cls_rule* rules, uint32_t n, int fam, std::vector<SemRule>& out,
+                   std::string& err);
+
+// ---- linear table (device layout, 48 B per rule) ---------------------------
+struct alignas(16) LinRule4 {
+    uint32_t src_addr, src_mask, dst_addr, dst_mask;
+    uint32_t port[NPROTO];   // lo | (hi - lo) << 16
+    uint32_t meta;           // byte p: bit7 = TERM, bits0-1 = result
+    uint32_t index;          // rule index in the ACL
+    uint32_t pad[2];
+};
+static_assert(sizeof(LinRule4) == 48, "LinRule4 layout");
+
+struct alignas(16) LinRule16 {
+    uint8_t src_addr[16], dst_addr[16];
+    uint8_t src_len, dst_len, src_any, dst_any;
+    uint32_t port[NPROTO];
+    uint32_t meta;
+    uint32_t index;
+    uint32_t pad[1];
+};
+static_assert(sizeof(LinRule16) == 64, "LinRule16 layout");
+
+std::vector<LinRule4> linear4(const std::vector<SemRule>& sem);
+std::vector<LinRule16> linear16(const std::vector<SemRule>& sem);
+
+// ---- IPv4 classifier image -------------------------------------------------
+struct Cls4Image {
+    std::vector<uint32_t> words;   // read-only LDS image, 16 B aligned sections
+    uint32_t off_bounds = 0, off_iclass = 0, off_cells = 0, off_lists = 0, off_tmpl = 0;
+    uint32_t img_bytes = 0;        // size of the read-only image
+    uint32_t n_bounds = 0, n_classes = 0, n_tmpl = 0, n_list_entries = 0, n_ctr = 0;
+    uint32_t search_top = 0;       // largest power of two <= n_bounds
+    uint32_t lds_bytes = 0;        // image + counters (u32 per slot), 16 B aligned
+    std::vector<uint32_t> ctr_rule;  // slot -> rule index (R = default DENY)
+};
+
+// Build the image; returns false (with reason) if the table does not fit the
+// 16-bit list / template indices.
+bool build_cls4(const std::vector<SemRule>& sem, uint32_t n_rules, Cls4Image& img,
+                std::string& why);
+
+}  // namespace cls

@@ -1,0 +1,608 @@
+// C ABI of the classifier engine (include/contivcls.h).
+//
+// Host side of the MI355X verdict backend: ACL configuration (the
+// MockACLEngine's ACLConfig, mock/aclengine/aclengine_mock.go:110-121,
+// 671-728), table compilation + upload, and the launch sequence of the
+// classify / connection / traffic kernels on one gfx950 device.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/contivcls.h"
+#include "compile.hpp"
+#include "kernels.hpp"
+
+using namespace cls;
+
+namespace {
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    ~DevBuf() { if (p) (void)hipFree(p); }
+    hipError_t ensure(size_t n) {
+        if (n <= bytes) return hipSuccess;
+        if (p) { (void)hipFree(p); p = nullptr; bytes = 0; }
+        hipError_t e = hipMalloc(&p, n < 256 ? 256 : n);
+        if (e == hipSuccess) bytes = n < 256 ? 256 : n;
+        return e;
+    }
+    template <typename T> T* as() const { return static_cast<T*>(p); }
+};
+
+struct Table {
+    std::string name;
+    uint32_t n_rules = 0;
+    // linear (ballot) table, also the protocol>2 fallback
+    std::vector<LinRule4> lin4;
+    DevBuf d_lin4;
+    // IPv4 classifier
+    bool has_cls = false;
+    Cls4Image img;
+    DevBuf d_img;
+    // counters: slots [0, n_ctr) of the classifier + [n_ctr, n_ctr + R + 1) direct rule slots
+    uint32_t n_slots = 0;
+    DevBuf d_slot, d_map, d_out;
+    int kernel = 0;            // 0 linear, 1 classifier
+    bool lds_resident = false;
+};
+
+struct AclEntry {
+    uint32_t table_id = 0;
+    std::vector<uint32_t> ingress, egress;
+};
+
+}  // namespace
+
+struct cls_engine {
+    int device = 0;
+    int n_cu = 256;
+    hipStream_t stream = nullptr;
+    std::mutex mu;
+    std::string err;
+    std::map<uint32_t, std::shared_ptr<Table>> tables;
+    uint32_t next_table = 1;
+    // ACLConfig
+    std::map<std::string, AclEntry> acls;
+    std::unordered_map<std::string, uint32_t> if_ids;
+    std::vector<std::string> if_names;
+    std::vector<std::pair<int32_t, int32_t>> if_acl;   // per if id: (inbound, outbound) table id
+    uint32_t changes = 0;
+    // scratch for host-pointer batches
+    DevBuf s_src, s_dst, s_sport, s_dport, s_proto, s_verdict, s_if_a, s_if_b, s_desc, s_ifs;
+    DevBuf s_pool;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    bool timed = false;
+    // per-launch timing (CLS_F_TIMING): event pairs, recycled after a reset
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pool;
+    size_t ev_used = 0;
+};
+
+static int fail(cls_engine* e, int code, const char* fmt, ...) {
+    if (e) {
+        char buf[512];
+        va_list ap;
+        va_start(ap, fmt);
+        vsnprintf(buf, sizeof buf, fmt, ap);
+        va_end(ap);
+        e->err = buf;
+    }
+    return code;
+}
+
+#define HIPC(e, expr)                                                                    \
+    do {                                                                                 \
+        hipError_t _h = (expr);                                                          \
+        if (_h != hipSuccess)                                                            \
+            return fail((e), CLS_E_HIP, "%s: %s (%s:%d)", #expr, hipGetErrorString(_h),  \
+                        __FILE__, __LINE__);                                             \
+    } while (0)
+
+extern "C" {
+
+int cls_abi_version(void) { return CLS_ABI_VERSION; }
+
+int cls_engine_create(const cls_config* cfg, cls_engine** out) {
+    if (!out) return CLS_E_INVAL;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return CLS_E_NODEV;
+    int dev = cfg && cfg->device >= 0 ? cfg->device : -1;
+    if (dev < 0 && hipGetDevice(&dev) != hipSuccess) return CLS_E_NODEV;
+    if (dev >= ndev) return CLS_E_NODEV;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return CLS_E_NODEV;
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return CLS_E_NODEV;
+    auto* e = new (std::nothrow) cls_engine();
+    if (!e) return CLS_E_NOMEM;
+    e->device = dev;
+    e->n_cu = prop.multiProcessorCount;
+    if (hipSetDevice(dev) != hipSuccess || hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete e;
+        return CLS_E_HIP;
+    }
+    *out = e;
+    return CLS_OK;
+}
+
+void cls_engine_destroy(cls_engine* e) {
+    if (!e) return;
+    (void)hipSetDevice(e->device);
+    (void)hipDeviceSynchronize();
+    e->tables.clear();
+    for (auto& pr : e->ev_pool) {
+        (void)hipEventDestroy(pr.first);
+        (void)hipEventDestroy(pr.second);
+    }
+    if (e->stream) (void)hipStreamDestroy(e->stream);
+    delete e;
+}
+
+const char* cls_last_error(const cls_engine* e) { return e ? e->err.c_str() : "null engine"; }
+
+// ---------------------------------------------------------------------------
+static int table_put_locked(cls_engine* e, const char* name, const cls_rule* rules, uint32_t n,
+                            uint32_t* table_id) {
+    if (n && !rules) return fail(e, CLS_E_INVAL, "rules is NULL");
+    auto t = std::make_shared<Table>();
+    t->name = name ? name : "";
+    t->n_rules = n;
+    std::vector<SemRule> sem;
+    std::string why;
+    int rc = semantic_rules(rules, n, 4, sem, why);
+    if (rc != CLS_OK) return fail(e, rc, "%s", why.c_str());
+    t->lin4 = linear4(sem);
+    HIPC(e, hipSetDevice(e->device));
+    HIPC(e, t->d_lin4.ensure(std::max<size_t>(1, t->lin4.size()) * sizeof(LinRule4)));
+    if (!t->lin4.empty())
+        HIPC(e, hipMemcpy(t->d_lin4.p, t->lin4.data(), t->lin4.size() * sizeof(LinRule4), hipMemcpyHostToDevice));
+    // classifier for anything but tiny tables
+    t->kernel = 0;
+    if (sem.size() > 8) {
+        if (build_cls4(sem, n, t->img, why)) {
+            t->has_cls = true;
+            t->kernel = 1;
+            t->lds_resident = t->img.lds_bytes <= uint32_t(max_lds_bytes());
+            HIPC(e, t->d_img.ensure(t->img.img_bytes));
+            HIPC(e, hipMemcpy(t->d_img.p, t->img.words.data(), t->img.img_bytes, hipMemcpyHostToDevice));
+        }
+    }
+    const uint32_t n_cls_slots = t->has_cls ? t->img.n_ctr : 0;
+    t->n_slots = n_cls_slots + n + 1;
+    std::vector<uint32_t> map(t->n_slots);
+    for (uint32_t i = 0; i < n_cls_slots; ++i) map[i] = t->img.ctr_rule[i];
+    for (uint32_t i = 0; i <= n; ++i) map[n_cls_slots + i] = i;
+    HIPC(e, t->d_slot.ensure(size_t(t->n_slots) * 8));
+    HIPC(e, t->d_map.ensure(size_t(t->n_slots) * 4));
+    HIPC(e, t->d_out.ensure(size_t(n + 1) * 8));
+    HIPC(e, hipMemcpy(t->d_map.p, map.data(), map.size() * 4, hipMemcpyHostToDevice));
+    const uint32_t id = e->next_table++;
+    e->tables[id] = t;
+    if (table_id) *table_id = id;
+    return CLS_OK;
+}
+
+int cls_table_put(cls_engine* e, const char* name, const cls_rule* rules, uint32_t n_rules,
+                  uint32_t* table_id) {
+    if (!e) return CLS_E_INVAL;
+    std::lock_guard<std::mutex> g(e->mu);
+    return table_put_locked(e, name, rules, n_rules, table_id);
+}
+
+int cls_table_del(cls_engine* e, uint32_t table_id) {
+    if (!e) return CLS_E_INVAL;
+    std::lock_guard<std::mutex> g(e->mu);
+    if (!e->tables.erase(table_id)) return fail(e, CLS_E_NOTFOUND, "no table %u", table_id);
+    return CLS_OK;
+}
+
+int cls_table_get_info(cls_engine* e, uint32_t table_id, cls_table_info* info) {
+    if (!e || !info) return CLS_E_INVAL;
+    std::lock_guard<std::mutex> g(e->mu);
+    auto it = e->tables.find(table_id);
+    if (it == e->tables.end()) return fail(e, CLS_E_NOTFOUND, "no table %u", table_id);
+    const Table& t = *it->second;
+    std::memset(info, 0, sizeof *info);
+    info->n_rules = t.n_rules;
+    info->kernel = uint32_t(t.kernel);
+    if (t.has_cls) {
+        info->lds_bytes = t.img.lds_bytes;
+        info->n_intervals = t.img.n_bounds;
+        info->n_classes = t.img.n_classes;
+        info->n_templates = t.img.n_tmpl;
+        info->n_slots = t.img.n_ctr;
+        info->lds_resident = t.lds_resident ? 1 : 0;
+    }
+    return CLS_OK;
+}
+
+// ---------------------------------------------------------------------------
+static bool aligned(const void* p, size_t a) { return (reinterpret_cast<uintptr_t>(p) % a) == 0; }
+
+int cls_classify(cls_engine* e, uint32_t table_id, const cls_pkt_soa* pk, uint64_t n,
+                 uint8_t* verdict_out, uint64_t* counters_out, uint32_t flags, void* stream) {
+    if (!e || !pk) return CLS_E_INVAL;
+    std::lock_guard<std::mutex> g(e->mu);
+    auto it = e->tables.find(table_id);
+    if (it == e->tables.end()) return fail(e, CLS_E_NOTFOUND, "no table %u", table_id);
+    std::shared_ptr<Table> t = it->second;
+    if (pk->af != CLS_AF_V4) return fail(e, CLS_E_INVAL, "only CLS_AF_V4 batches are supported");
+    if (n && (!pk->src4 || !pk->dst4 || !pk->dport || !pk->proto))
+        return fail(e, CLS_E_INVAL, "missing packet arrays");
+    if (!verdict_out && !(flags & CLS_F_NO_VERDICT) && n)
+        return fail(e, CLS_E_INVAL, "verdict_out is NULL (set CLS_F_NO_VERDICT)");
+    HIPC(e, hipSetDevice(e->device));
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : e->stream;
+    const bool dev = flags & CLS_F_DEVICE;
+
+    Pkts4 p{pk->src4, pk->dst4, pk->dport, pk->proto, n};
+    uint8_t* d_verdict = verdict_out;
+    if (!dev && n) {
+        HIPC(e, e->s_src.ensure(n * 4));
+        HIPC(e, e->s_dst.ensure(n * 4));
+        HIPC(e, e->s_dport.ensure(n * 2));
+        HIPC(e, e->s_proto.ensure(n));
+        HIPC(e, hipMemcpyAsync(e->s_src.p, pk->src4, n * 4, hipMemcpyHostToDevice, s));
+        HIPC(e, hipMemcpyAsync(e->s_dst.p, pk->dst4, n * 4, hipMemcpyHostToDevice, s));
+        HIPC(e, hipMemcpyAsync(e->s_dport.p, pk->dport, n * 2, hipMemcpyHostToDevice, s));
+        HIPC(e, hipMemcpyAsync(e->s_proto.p, pk->proto, n, hipMemcpyHostToDevice, s));
+        p = Pkts4{e->s_src.as<uint32_t>(), e->s_dst.as<uint32_t>(), e->s_dport.as<uint16_t>(),
+                  e->s_proto.as<uint8_t>(), n};
+        d_verdict = nullptr;
+        if (verdict_out) {
+            HIPC(e, e->s_verdict.ensure(n));
+            d_verdict = e->s_verdict.as<uint8_t>();
+        }
+    }
+    HIPC(e, hipMemsetAsync(t->d_slot.p, 0, size_t(t->n_slots) * 8, s));
+
+    const bool vec = aligned(p.src, 16) && aligned(p.dst, 16) && aligned(p.dport, 8) &&
+                     aligned(p.proto, 4) && (!d_verdict || aligned(d_verdict, 4));
+    LaunchCfg cfg;
+    cfg.stream = s;
+    const bool use_cls = t->has_cls && !(flags & CLS_F_FORCE_LINEAR);
+    int per_cu = 2;
+    if (use_cls && t->lds_resident)
+        per_cu = std::max(1, std::min(2, int(max_lds_bytes() / std::max<uint32_t>(1, t->img.lds_bytes))));
+    const uint64_t want = (n + 4ull * 1024 - 1) / (4ull * 1024);
+    cfg.grid = int(std::max<uint64_t>(1, std::min<uint64_t>(uint64_t(e->n_cu) * per_cu, want)));
+
+    const bool timing = flags & CLS_F_TIMING;
+    if (timing) {
+        if (e->ev_used == e->ev_pool.size()) {
+            hipEvent_t a, b;
+            HIPC(e, hipEventCreate(&a));
+            HIPC(e, hipEventCreate(&b));
+            e->ev_pool.push_back({a, b});
+        }
+        e->ev0 = e->ev_pool[e->ev_used].first;
+        e->ev1 = e->ev_pool[e->ev_used].second;
+        e->ev_used++;
+        HIPC(e, hipEventRecord(e->ev0, s));
+    }
+    if (n) {
+        if (use_cls) {
+            Cls4Dev cd;
+            cd.img = t->d_img.as<uint32_t>();
+            cd.img_bytes = t->img.img_bytes;
+            cd.off_bounds = t->img.off_bounds;
+            cd.off_iclass = t->img.off_iclass;
+            cd.off_cells = t->img.off_cells;
+            cd.off_lists = t->img.off_lists;
+            cd.off_tmpl = t->img.off_tmpl;
+            cd.search_top = t->img.search_top;
+            cd.n_ctr = t->img.n_ctr;
+            cd.lds_bytes = t->img.lds_bytes;
+            cd.lin = t->d_lin4.as<LinRule4>();
+            cd.n_lin = uint32_t(t->lin4.size());
+            cd.n_rules = t->n_rules;
+            HIPC(e, launch_classify4_cls(cd, p, d_verdict, t->d_slot.as<unsigned long long>(),
+                                         t->lds_resident, vec, cfg));
+        } else {
+            const uint32_t base = t->has_cls ? t->img.n_ctr : 0;
+            HIPC(e, launch_classify4_linear(t->d_lin4.as<LinRule4>(), uint32_t(t->lin4.size()), t->n_rules, p,
+                                            d_verdict, t->d_slot.as<unsigned long long>() + base, cfg));
+        }
+    }
+    if (timing) {
+        HIPC(e, hipEventRecord(e->ev1, s));
+        e->timed = true;
+    }
+    // slot counters -> rule counters
+    unsigned long long* out = dev && counters_out ? reinterpret_cast<unsigned long long*>(counters_out)
+                                                  : t->d_out.as<unsigned long long>();
+    if (counters_out || !dev) {
+        if (!(dev && (flags & CLS_F_ACCUMULATE)))
+            HIPC(e, hipMemsetAsync(out, 0, size_t(t->n_rules + 1) * 8, s));
+        HIPC(e, launch_remap(t->d_slot.as<unsigned long long>(), t->d_map.as<uint32_t>(), t->n_slots, out, s));
+    }
+    if (!dev) {
+        if (verdict_out && n) HIPC(e, hipMemcpyAsync(verdict_out, d_verdict, n, hipMemcpyDeviceToHost, s));
+        std::vector<uint64_t> tmp;
+        if (counters_out) {
+            tmp.resize(t->n_rules + 1);
+            HIPC(e, hipMemcpyAsync(tmp.data(), out, tmp.size() * 8, hipMemcpyDeviceToHost, s));
+        }
+        HIPC(e, hipStreamSynchronize(s));
+        if (counters_out) {
+            for (size_t i = 0; i < tmp.size(); ++i)
+                counters_out[i] = (flags & CLS_F_ACCUMULATE) ? counters_out[i] + tmp[i] : tmp[i];
+        }
+    }
+    return CLS_OK;
+}
+
+int cls_last_kernel_ms(cls_engine* e, float* ms) {
+    if (!e || !ms) return CLS_E_INVAL;
+    if (!e->timed) return fail(e, CLS_E_INVAL, "no timed classify recorded");
+    HIPC(e, hipEventSynchronize(e->ev1));
+    HIPC(e, hipEventElapsedTime(ms, e->ev0, e->ev1));
+    return CLS_OK;
+}
+
+int cls_kernel_times(cls_engine* e, float* ms, uint32_t cap, uint32_t* count) {
+    if (!e || !count) return CLS_E_INVAL;
+    std::lock_guard<std::mutex> g(e->mu);
+    *count = uint32_t(e->ev_used);
+    if (e->ev_used == 0) return CLS_OK;
+    HIPC(e, hipEventSynchronize(e->ev_pool[e->ev_used - 1].second));
+    for (size_t i = 0; i < e->ev_used && i < cap && ms; ++i)
+        HIPC(e, hipEventElapsedTime(&ms[i], e->ev_pool[i].first, e->ev_pool[i].second));
+    return CLS_OK;
+}
+
+int cls_kernel_times_reset(cls_engine* e) {
+    if (!e) return CLS_E_INVAL;
+    std::lock_guard<std::mutex> g(e->mu);
+    if (e->ev_used) HIPC(e, hipEventSynchronize(e->ev_pool[e->ev_used - 1].second));
+    e->ev_used = 0;
+    return CLS_OK;
+}
+
+// ---------------------------------------------------------------------------
+// ACLConfig
+static uint32_t if_id_locked(cls_engine* e, const std::string& name) {
+    auto it = e->if_ids.find(name);
+    if (it != e->if_ids.end()) return it->second;
+    const uint32_t id = uint32_t(e->if_names.size());
+    e->if_ids[name] = id;
+    e->if_names.push_back(name);
+    e->if_acl.push_back({-1, -1});
+    return id;
+}
+
+static int acl_del_locked(cls_engine* e, const std::string& name) {
+    auto it = e->acls.find(name);
+    if (it == e->acls.end()) return fail(e, CLS_E_NOTFOUND, "cannot find ACL: %s", name.c_str());
+    const int32_t tid = int32_t(it->second.table_id);
+    for (auto& b : e->if_acl) {
+        if (b.first == tid) b.first = -1;
+        if (b.second == tid) b.second = -1;
+    }
+    e->tables.erase(it->second.table_id);
+    e->acls.erase(it);
+    e->changes++;
+    return CLS_OK;
+}
+
+int cls_acl_put(cls_engine* e, const char* acl_name, const cls_rule* rules, uint32_t n_rules,
+                const char* const* ingress_ifs, uint32_t n_ingress, const char* const* egress_ifs,
+                uint32_t n_egress) {
+    if (!e || !acl_name) return CLS_E_INVAL;
+    std::lock_guard<std::mutex> g(e->mu);
+    if (n_ingress + n_egress == 0) return fail(e, CLS_E_INVAL, "ACL with empty interfaces");
+    uint32_t tid;
+    int rc = table_put_locked(e, acl_name, rules, n_rules, &tid);
+    if (rc != CLS_OK) return rc;
+    const std::string name(acl_name);
+    if (e->acls.count(name)) {          // PutACL: delete the original first, not a change
+        acl_del_locked(e, name);
+        e->changes--;
+    }
+    AclEntry a;
+    a.table_id = tid;
+    for (uint32_t i = 0; i < n_ingress; ++i) {
+        const uint32_t id = if_id_locked(e, ingress_ifs[i]);
+        a.ingress.push_back(id);
+        e->if_acl[id].first = int32_t(tid);
+    }
+    for (uint32_t i = 0; i < n_egress; ++i) {
+        const uint32_t id = if_id_locked(e, egress_ifs[i]);
+        a.egress.push_back(id);
+        e->if_acl[id].second = int32_t(tid);
+    }
+    e->acls[name] = a;
+    e->changes++;
+    return CLS_OK;
+}
+
+int cls_acl_del(cls_engine* e, const char* acl_name) {
+    if (!e || !acl_name) return CLS_E_INVAL;
+    std::lock_guard<std::mutex> g(e->mu);
+    return acl_del_locked(e, acl_name);
+}
+
+int cls_acl_table(cls_engine* e, const char* acl_name, uint32_t* table_id) {
+    if (!e || !acl_name || !table_id) return CLS_E_INVAL;
+    std::lock_guard<std::mutex> g(e->mu);
+    auto it = e->acls.find(acl_name);
+    if (it == e->acls.end()) return fail(e, CLS_E_NOTFOUND, "cannot find ACL: %s", acl_name);
+    *table_id = it->second.table_id;
+    return CLS_OK;
+}
+
+int cls_acl_counts(cls_engine* e, uint32_t* n_acls, uint32_t* n_changes) {
+    if (!e) return CLS_E_INVAL;
+    std::lock_guard<std::mutex> g(e->mu);
+    if (n_acls) *n_acls = uint32_t(e->acls.size());
+    if (n_changes) *n_changes = e->changes;
+    return CLS_OK;
+}
+
+int cls_if_id(cls_engine* e, const char* if_name, uint32_t* id) {
+    if (!e || !if_name || !id) return CLS_E_INVAL;
+    std::lock_guard<std::mutex> g(e->mu);
+    *id = if_id_locked(e, if_name);
+    return CLS_OK;
+}
+
+int cls_if_acls(cls_engine* e, uint32_t if_id, int32_t* in_table, int32_t* out_table) {
+    if (!e) return CLS_E_INVAL;
+    std::lock_guard<std::mutex> g(e->mu);
+    if (if_id >= e->if_acl.size()) return fail(e, CLS_E_NOTFOUND, "no interface %u", if_id);
+    if (in_table) *in_table = e->if_acl[if_id].first;
+    if (out_table) *out_table = e->if_acl[if_id].second;
+    return CLS_OK;
+}
+
+int cls_connect_batch(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t* out,
+                      uint32_t flags, void* stream) {
+    if (!e || !c || (n && !out)) return CLS_E_INVAL;
+    std::lock_guard<std::mutex> g(e->mu);
+    const cls_pkt_soa& pk = c->pkt;
+    if (pk.af != CLS_AF_V4) return fail(e, CLS_E_INVAL, "only CLS_AF_V4 connections are supported");
+    if (n && (!pk.src4 || !pk.dst4 || !pk.sport || !pk.dport || !pk.proto || !c->src_if || !c->dst_if))
+        return fail(e, CLS_E_INVAL, "missing connection arrays");
+    HIPC(e, hipSetDevice(e->device));
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : e->stream;
+    // snapshot the bindings: descriptor per table, (in, out) per interface
+    std::vector<AclDesc> desc;
+    std::unordered_map<int32_t, int32_t> slot;
+    auto desc_of = [&](int32_t tid) -> int32_t {
+        if (tid < 0) return -1;
+        auto f = slot.find(tid);
+        if (f != slot.end()) return f->second;
+        auto t = e->tables.find(uint32_t(tid));
+        if (t == e->tables.end()) return -1;
+        AclDesc d{t->second->d_lin4.as<LinRule4>(), uint32_t(t->second->lin4.size()), 1u};
+        desc.push_back(d);
+        slot[tid] = int32_t(desc.size() - 1);
+        return int32_t(desc.size() - 1);
+    };
+    std::vector<IfAcls> ifs(std::max<size_t>(1, e->if_acl.size()));
+    for (size_t i = 0; i < e->if_acl.size(); ++i)
+        ifs[i] = IfAcls{desc_of(e->if_acl[i].first), desc_of(e->if_acl[i].second)};
+    if (desc.empty()) desc.push_back(AclDesc{nullptr, 0, 0});
+    if (!(flags & CLS_F_DEVICE))
+        for (uint64_t i = 0; i < n; ++i)
+            if (c->src_if[i] >= e->if_acl.size() || c->dst_if[i] >= e->if_acl.size())
+                return fail(e, CLS_E_INVAL, "connection %llu: unknown interface id", (unsigned long long)i);
+    HIPC(e, e->s_desc.ensure(desc.size() * sizeof(AclDesc)));
+    HIPC(e, e->s_ifs.ensure(ifs.size() * sizeof(IfAcls)));
+    HIPC(e, hipMemcpyAsync(e->s_desc.p, desc.data(), desc.size() * sizeof(AclDesc), hipMemcpyHostToDevice, s));
+    HIPC(e, hipMemcpyAsync(e->s_ifs.p, ifs.data(), ifs.size() * sizeof(IfAcls), hipMemcpyHostToDevice, s));
+    const uint32_t *src = pk.src4, *dst = pk.dst4, *sif = c->src_if, *dif = c->dst_if;
+    const uint16_t *sp = pk.sport, *dp = pk.dport;
+    const uint8_t* pr = pk.proto;
+    uint8_t* o = out;
+    const bool dev = flags & CLS_F_DEVICE;
+    if (!dev && n) {
+        HIPC(e, e->s_src.ensure(n * 4)); HIPC(e, e->s_dst.ensure(n * 4));
+        HIPC(e, e->s_if_a.ensure(n * 4)); HIPC(e, e->s_if_b.ensure(n * 4));
+        HIPC(e, e->s_sport.ensure(n * 2)); HIPC(e, e->s_dport.ensure(n * 2));
+        HIPC(e, e->s_proto.ensure(n)); HIPC(e, e->s_verdict.ensure(n));
+        HIPC(e, hipMemcpyAsync(e->s_src.p, src, n * 4, hipMemcpyHostToDevice, s));
+        HIPC(e, hipMemcpyAsync(e->s_dst.p, dst, n * 4, hipMemcpyHostToDevice, s));
+        HIPC(e, hipMemcpyAsync(e->s_if_a.p, sif, n * 4, hipMemcpyHostToDevice, s));
+        HIPC(e, hipMemcpyAsync(e->s_if_b.p, dif, n * 4, hipMemcpyHostToDevice, s));
+        HIPC(e, hipMemcpyAsync(e->s_sport.p, sp, n * 2, hipMemcpyHostToDevice, s));
+        HIPC(e, hipMemcpyAsync(e->s_dport.p, dp, n * 2, hipMemcpyHostToDevice, s));
+        HIPC(e, hipMemcpyAsync(e->s_proto.p, pr, n, hipMemcpyHostToDevice, s));
+        src = e->s_src.as<uint32_t>(); dst = e->s_dst.as<uint32_t>();
+        sif = e->s_if_a.as<uint32_t>(); dif = e->s_if_b.as<uint32_t>();
+        sp = e->s_sport.as<uint16_t>(); dp = e->s_dport.as<uint16_t>();
+        pr = e->s_proto.as<uint8_t>(); o = e->s_verdict.as<uint8_t>();
+    }
+    HIPC(e, launch_connect4(e->s_desc.as<AclDesc>(), e->s_ifs.as<IfAcls>(), sif, dif, src, dst, sp, dp, pr,
+                            n, o, s));
+    if (!dev) {
+        if (n) HIPC(e, hipMemcpyAsync(out, o, n, hipMemcpyDeviceToHost, s));
+        HIPC(e, hipStreamSynchronize(s));
+    } else {
+        // descriptor buffers are engine scratch: finish before they can be reused
+        HIPC(e, hipStreamSynchronize(s));
+    }
+    return CLS_OK;
+}
+
+// ---------------------------------------------------------------------------
+int cls_gen_traffic_v4(cls_engine* e, const cls_traffic_spec* sp, uint64_t first, uint64_t n,
+                       uint32_t* src4, uint32_t* dst4, uint16_t* sport, uint16_t* dport,
+                       uint8_t* proto, void* stream) {
+    if (!e || !sp) return CLS_E_INVAL;
+    std::lock_guard<std::mutex> g(e->mu);
+    HIPC(e, hipSetDevice(e->device));
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : e->stream;
+    const size_t bp = size_t(sp->n_pod_ips) * 4, bd = size_t(sp->n_dst) * 4, bl = sp->n_dst,
+                 bq = size_t(sp->n_ports) * 2;
+    auto al = [](size_t x) { return (x + 15) & ~size_t(15); };
+    HIPC(e, e->s_pool.ensure(al(bp) + al(bd) + al(bl) + al(bq) + 16));
+    uint8_t* base = e->s_pool.as<uint8_t>();
+    TrafficDev t;
+    t.seed = sp->seed;
+    t.pct_pod = sp->pct_pod_src; t.pct_dst = sp->pct_rule_dst;
+    t.pct_port = sp->pct_table_port; t.pct_icmp = sp->pct_icmp;
+    t.pods = reinterpret_cast<const uint32_t*>(base); t.n_pods = sp->n_pod_ips;
+    t.dst_addrs = reinterpret_cast<const uint32_t*>(base + al(bp));
+    t.dst_lens = base + al(bp) + al(bd); t.n_dst = sp->n_dst;
+    t.ports = reinterpret_cast<const uint16_t*>(base + al(bp) + al(bd) + al(bl)); t.n_ports = sp->n_ports;
+    if (bp) HIPC(e, hipMemcpyAsync(base, sp->pod_ips, bp, hipMemcpyHostToDevice, s));
+    if (bd) HIPC(e, hipMemcpyAsync(base + al(bp), sp->dst_addrs, bd, hipMemcpyHostToDevice, s));
+    if (bl) HIPC(e, hipMemcpyAsync(base + al(bp) + al(bd), sp->dst_lens, bl, hipMemcpyHostToDevice, s));
+    if (bq) HIPC(e, hipMemcpyAsync(base + al(bp) + al(bd) + al(bl), sp->ports, bq, hipMemcpyHostToDevice, s));
+    HIPC(e, launch_gen4(t, first, n, src4, dst4, sport, dport, proto, s));
+    HIPC(e, hipStreamSynchronize(s));   // the pools are engine scratch
+    return CLS_OK;
+}
+
+int cls_compile_v4(const cls_rule* rules, uint32_t n, void* blob, uint64_t cap, uint64_t* need) {
+    if ((n && !rules) || !need) return CLS_E_INVAL;
+    std::vector<SemRule> sem;
+    std::string why;
+    int rc = semantic_rules(rules, n, 4, sem, why);
+    if (rc != CLS_OK) return rc;
+    std::vector<LinRule4> lin = linear4(sem);
+    Cls4Image img;
+    const bool has = sem.size() > 8 && build_cls4(sem, n, img, why);
+    cls_image_v4_header h;
+    std::memset(&h, 0, sizeof h);
+    h.magic = 0x434C5334u;
+    h.version = 1;
+    h.n_rules = n;
+    h.n_lin = uint32_t(lin.size());
+    h.has_cls = has ? 1u : 0u;
+    if (has) {
+        h.img_bytes = img.img_bytes; h.off_bounds = img.off_bounds; h.off_iclass = img.off_iclass;
+        h.off_cells = img.off_cells; h.off_lists = img.off_lists; h.off_tmpl = img.off_tmpl;
+        h.n_bounds = img.n_bounds; h.search_top = img.search_top; h.n_classes = img.n_classes;
+        h.n_tmpl = img.n_tmpl; h.n_list_entries = img.n_list_entries; h.n_ctr = img.n_ctr;
+        h.lds_bytes = img.lds_bytes;
+    }
+    auto al = [](uint64_t x) { return (x + 15) & ~uint64_t(15); };
+    h.off_image = uint32_t(al(sizeof h));
+    h.off_ctr_rule = uint32_t(al(h.off_image + h.img_bytes));
+    h.off_lin = uint32_t(al(h.off_ctr_rule + uint64_t(h.n_ctr) * 4));
+    h.total_bytes = uint32_t(h.off_lin + lin.size() * sizeof(LinRule4));
+    *need = h.total_bytes;
+    if (!blob || cap < h.total_bytes) return CLS_OK;
+    uint8_t* b = static_cast<uint8_t*>(blob);
+    std::memset(b, 0, h.total_bytes);
+    std::memcpy(b, &h, sizeof h);
+    if (has) {
+        std::memcpy(b + h.off_image, img.words.data(), img.img_bytes);
+        std::memcpy(b + h.off_ctr_rule, img.ctr_rule.data(), size_t(h.n_ctr) * 4);
+    }
+    if (!lin.empty()) std::memcpy(b + h.off_lin, lin.data(), lin.size() * sizeof(LinRule4));
+    return CLS_OK;
+}
+
+}  // extern "C"

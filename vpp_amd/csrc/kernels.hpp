@@ -1,0 +1,74 @@
+// Launch interface of the gfx950 kernels (kernels.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "compile.hpp"
+
+namespace cls {
+
+// IPv4 packet batch in device memory (structure of arrays)
+struct Pkts4 {
+    const uint32_t* src;
+    const uint32_t* dst;
+    const uint16_t* dport;
+    const uint8_t* proto;
+    uint64_t n;
+};
+
+struct Cls4Dev {
+    const uint32_t* img;       // classifier image (device)
+    uint32_t img_bytes;
+    uint32_t off_bounds, off_iclass, off_cells, off_lists, off_tmpl;
+    uint32_t search_top;       // power of two; bounds padded to 2*search_top
+    uint32_t n_ctr;            // slot counters in the image's LDS tail
+    uint32_t lds_bytes;
+    const LinRule4* lin;       // linear rules: fallback for protocols outside TCP/UDP/ICMP
+    uint32_t n_lin;
+    uint32_t n_rules;          // R: direct rule slots start at n_ctr
+};
+
+struct LaunchCfg {
+    int grid;                  // workgroups (persistent, grid-stride)
+    hipStream_t stream;
+};
+
+// verdict may be null; gslot: u64 slot counters (added to)
+hipError_t launch_classify4_cls(const Cls4Dev& t, const Pkts4& p, uint8_t* verdict,
+                                unsigned long long* gslot, bool lds_resident, bool vec,
+                                const LaunchCfg& cfg);
+hipError_t launch_classify4_linear(const LinRule4* rules, uint32_t n_lin, uint32_t n_rules,
+                                   const Pkts4& p, uint8_t* verdict, unsigned long long* gslot,
+                                   const LaunchCfg& cfg);
+// out[map[i]] += slot[i]
+hipError_t launch_remap(const unsigned long long* slot, const uint32_t* map, uint32_t n,
+                        unsigned long long* out, hipStream_t s);
+
+struct AclDesc {                 // one installed ACL for the connection kernel
+    const LinRule4* rules;
+    uint32_t n;
+    uint32_t valid;              // 0 = nil ACL (PERMIT)
+};
+struct IfAcls {                  // interface -> (inbound, outbound) AclDesc index, -1 = nil
+    int32_t in, out;
+};
+hipError_t launch_connect4(const AclDesc* acls, const IfAcls* ifs, const uint32_t* src_if,
+                           const uint32_t* dst_if, const uint32_t* src, const uint32_t* dst,
+                           const uint16_t* sport, const uint16_t* dport, const uint8_t* proto,
+                           uint64_t n, uint8_t* out, hipStream_t s);
+
+struct TrafficDev {
+    uint64_t seed;
+    uint32_t pct_pod, pct_dst, pct_port, pct_icmp;
+    const uint32_t* pods; uint32_t n_pods;
+    const uint32_t* dst_addrs; const uint8_t* dst_lens; uint32_t n_dst;
+    const uint16_t* ports; uint32_t n_ports;
+};
+hipError_t launch_gen4(const TrafficDev& t, uint64_t first, uint64_t n, uint32_t* src,
+                       uint32_t* dst, uint16_t* sport, uint16_t* dport, uint8_t* proto,
+                       hipStream_t s);
+
+int max_lds_bytes();             // per-workgroup LDS the classify kernel may use
+
+}  // namespace cls

@@ -1,0 +1,362 @@
+"""Host layer of the GPU verdict backend (Python stand-in for the Go host).
+
+``Engine`` wraps the C ABI (include/contivcls.h): compiled rule tables,
+batched classification of packet batches resident in HBM (torch tensors) or
+host memory (numpy), the device traffic generator.
+
+``ACLEngine`` is the drop-in for the reference's MockACLEngine
+(mock/aclengine/aclengine_mock.go:94-471) with the same method set:
+RegisterPod, ApplyTxn, DumpACLs, GetNumOfACLs, GetInboundACL,
+GetOutboundACL, GetACLByName, GetNumOfACLChanges and the three Connection*
+entry points -- plus ``connection_batch`` which evaluates many connections in
+one GPU launch.  ACL configuration (interfaces, replace-on-put, change
+counting) lives in the C++ engine; this layer keeps only what the Go host
+would: the protobuf ACLs by name, pods and interface names.
+"""
+from __future__ import annotations
+
+import copy
+import ctypes as C
+from typing import Optional
+
+import numpy as np
+
+from . import _abi, gonet
+from ._abi import ClsError
+
+ACL_KEY_PREFIX = "vpp/config/v1/acl/"
+# ConnectionAction (aclengine_mock.go:46-60)
+CONN_DENY_SYN, CONN_DENY_SYN_ACK, CONN_ALLOW, CONN_FAILURE = 0, 1, 2, 3
+# ProtocolType (aclengine_mock.go:80-91)
+TCP, UDP, ICMP = 0, 1, 2
+
+
+def _is_torch(x) -> bool:
+    return type(x).__module__.startswith("torch")
+
+
+def _ptr(x):
+    if x is None:
+        return None
+    if _is_torch(x):
+        return x.data_ptr()
+    return x.ctypes.data
+
+
+class Table:
+    def __init__(self, engine: "Engine", tid: int, n_rules: int, name: str):
+        self.engine = engine
+        self.id = tid
+        self.n_rules = n_rules
+        self.name = name
+
+    def info(self) -> dict:
+        inf = _abi.TableInfo()
+        self.engine._check(_abi.lib().cls_table_get_info(self.engine.h, self.id, C.byref(inf)))
+        return {k: getattr(inf, k) for k, _ in _abi.TableInfo._fields_ if k != "reserved"}
+
+
+class Engine:
+    """One gfx950 device."""
+
+    def __init__(self, device: int = -1):
+        L = _abi.lib()
+        cfg = _abi.Config(device)
+        h = C.c_void_p()
+        rc = L.cls_engine_create(C.byref(cfg), C.byref(h))
+        if rc != 0:
+            raise ClsError("cls_engine_create failed (rc=%d): no usable gfx950 device" % rc)
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None):
+            _abi.lib().cls_engine_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc: int):
+        if rc != 0:
+            raise ClsError("rc=%d: %s" % (rc, _abi.lib().cls_last_error(self.h).decode()))
+
+    # -- tables -----------------------------------------------------------
+    def put_table(self, name: str, rules) -> Table:
+        cr = rules if isinstance(rules, _abi.CRules) else _abi.CRules(rules)
+        tid = C.c_uint32(0)
+        self._check(_abi.lib().cls_table_put(self.h, name.encode(), cr.ptr(), cr.n, C.byref(tid)))
+        return Table(self, tid.value, cr.n, name)
+
+    def del_table(self, table: Table):
+        self._check(_abi.lib().cls_table_del(self.h, table.id))
+
+    # -- classify ---------------------------------------------------------
+    def classify(self, table: Table, src, dst, dport, proto, verdict=None, counters=None,
+                 force_linear=False, timing=False, accumulate=False, stream=None):
+        """IPv4 batch.  numpy inputs: synchronous, returns (verdict, counters)
+        as numpy arrays.  torch device tensors: enqueued on ``stream`` (a
+        torch.cuda.Stream or raw handle; default torch's current stream);
+        ``verdict`` (uint8[n]) and ``counters`` (int64[R+1]) are written."""
+        n = int(len(dport))
+        dev = _is_torch(src)
+        flags = 0
+        if force_linear:
+            flags |= _abi.F_FORCE_LINEAR
+        if timing:
+            flags |= _abi.F_TIMING
+        if accumulate:
+            flags |= _abi.F_ACCUMULATE
+        if dev:
+            import torch
+            flags |= _abi.F_DEVICE
+            if verdict is None:
+                flags |= _abi.F_NO_VERDICT
+            if stream is None:
+                stream = torch.cuda.current_stream()
+            s = stream.cuda_stream if hasattr(stream, "cuda_stream") else stream
+            pk = _abi.PktSoa(_abi.AF_V4, _ptr(src), _ptr(dst), None, None, None, _ptr(dport), _ptr(proto))
+            self._check(_abi.lib().cls_classify(self.h, table.id, C.byref(pk), n, _ptr(verdict),
+                                                _ptr(counters), flags, s))
+            return verdict, counters
+        src = np.ascontiguousarray(src, np.uint32)
+        dst = np.ascontiguousarray(dst, np.uint32)
+        dport = np.ascontiguousarray(dport, np.uint16)
+        proto = np.ascontiguousarray(proto, np.uint8)
+        v = np.zeros(n, np.uint8) if verdict is None else verdict
+        c = np.zeros(table.n_rules + 1, np.uint64) if counters is None else counters
+        pk = _abi.PktSoa(_abi.AF_V4, _ptr(src), _ptr(dst), None, None, None, _ptr(dport), _ptr(proto))
+        self._check(_abi.lib().cls_classify(self.h, table.id, C.byref(pk), n, _ptr(v), _ptr(c),
+                                            flags, None))
+        return v, c
+
+    def last_kernel_ms(self) -> float:
+        ms = C.c_float(0)
+        self._check(_abi.lib().cls_last_kernel_ms(self.h, C.byref(ms)))
+        return ms.value
+
+    def kernel_times(self, reset: bool = True):
+        """Durations (ms) of every kernel timed since the last reset."""
+        n = C.c_uint32(0)
+        self._check(_abi.lib().cls_kernel_times(self.h, None, 0, C.byref(n)))
+        buf = (C.c_float * max(1, n.value))()
+        self._check(_abi.lib().cls_kernel_times(self.h, buf, n.value, C.byref(n)))
+        out = [buf[i] for i in range(n.value)]
+        if reset:
+            self._check(_abi.lib().cls_kernel_times_reset(self.h))
+        return out
+
+    # -- traffic ------------------------------------------------------------
+    def gen_traffic_v4(self, spec: dict, first: int, out: dict, stream=None):
+        """Generate packets [first, first+n) of the synthetic stream into the
+        device tensors of ``out`` (src, dst, sport, dport, proto)."""
+        pods = np.ascontiguousarray(spec.get("pod_ips", []), np.uint32)
+        da = np.ascontiguousarray(spec.get("dst_addrs", []), np.uint32)
+        dl = np.ascontiguousarray(spec.get("dst_lens", []), np.uint8)
+        ports = np.ascontiguousarray(spec.get("ports", []), np.uint16)
+        ts = _abi.TrafficSpec(spec["seed"], spec.get("pct_pod_src", 60), spec.get("pct_rule_dst", 50),
+                              spec.get("pct_table_port", 50), spec.get("pct_icmp", 0),
+                              pods.ctypes.data, len(pods), da.ctypes.data, dl.ctypes.data, len(da),
+                              ports.ctypes.data, len(ports))
+        n = int(len(out["dport"]))
+        s = None
+        if stream is not None:
+            s = stream.cuda_stream if hasattr(stream, "cuda_stream") else stream
+        self._check(_abi.lib().cls_gen_traffic_v4(
+            self.h, C.byref(ts), first, n, _ptr(out.get("src")), _ptr(out.get("dst")),
+            _ptr(out.get("sport")), _ptr(out.get("dport")), _ptr(out.get("proto")), s))
+
+    # -- ACL configuration (ACLConfig) ---------------------------------------
+    def acl_put(self, name: str, rules, ingress, egress):
+        cr = _abi.CRules(rules)
+        ing = (C.c_char_p * max(1, len(ingress)))(*[x.encode() for x in ingress])
+        eg = (C.c_char_p * max(1, len(egress)))(*[x.encode() for x in egress])
+        return _abi.lib().cls_acl_put(self.h, name.encode(), cr.ptr(), cr.n, ing, len(ingress),
+                                      eg, len(egress))
+
+    def acl_del(self, name: str):
+        return _abi.lib().cls_acl_del(self.h, name.encode())
+
+    def acl_table(self, name: str) -> int:
+        t = C.c_uint32(0)
+        rc = _abi.lib().cls_acl_table(self.h, name.encode(), C.byref(t))
+        return int(t.value) if rc == 0 else -1
+
+    def acl_counts(self):
+        a, c = C.c_uint32(0), C.c_uint32(0)
+        self._check(_abi.lib().cls_acl_counts(self.h, C.byref(a), C.byref(c)))
+        return a.value, c.value
+
+    def if_id(self, name: str) -> int:
+        i = C.c_uint32(0)
+        self._check(_abi.lib().cls_if_id(self.h, name.encode(), C.byref(i)))
+        return i.value
+
+    def if_acls(self, if_id: int):
+        a, b = C.c_int32(0), C.c_int32(0)
+        self._check(_abi.lib().cls_if_acls(self.h, if_id, C.byref(a), C.byref(b)))
+        return a.value, b.value
+
+    def connect_batch(self, src_if, dst_if, src, dst, proto, sport, dport) -> np.ndarray:
+        arrs = [np.ascontiguousarray(src_if, np.uint32), np.ascontiguousarray(dst_if, np.uint32),
+                np.ascontiguousarray(src, np.uint32), np.ascontiguousarray(dst, np.uint32),
+                np.ascontiguousarray(proto, np.uint8), np.ascontiguousarray(sport, np.uint16),
+                np.ascontiguousarray(dport, np.uint16)]
+        si, di, s, d, p, sp, dp = arrs
+        n = len(s)
+        out = np.zeros(n, np.uint8)
+        pk = _abi.PktSoa(_abi.AF_V4, _ptr(s), _ptr(d), None, None, _ptr(sp), _ptr(dp), _ptr(p))
+        cs = _abi.ConnSoa(pk, _ptr(si), _ptr(di))
+        self._check(_abi.lib().cls_connect_batch(self.h, C.byref(cs), n, _ptr(out), 0, None))
+        return out
+
+
+def _ip4(ip: Optional[bytes]) -> Optional[int]:
+    if ip is None:
+        return None
+    x = gonet.to4(ip)
+    if x is None:
+        return None
+    return int.from_bytes(x, "big")
+
+
+class ACLEngine:
+    """MockACLEngine drop-in over the GPU engine (aclengine_mock.go:94-471)."""
+
+    def __init__(self, contiv, engine: Optional[Engine] = None):
+        self.contiv = contiv
+        self.engine = engine or Engine()
+        self.pods = {}              # PodID -> (net.IP bytes | None, another_node)
+        self.by_name = {}           # ACL name -> Acl (the protobuf the host keeps)
+
+    # RegisterPod (:144-148)
+    def register_pod(self, pod, pod_ip: str, another_node: bool):
+        self.pods[pod] = (gonet.parse_ip(pod_ip), another_node)
+
+    # ApplyTxn (:151-198): returns an error string or None
+    def apply_txn(self, ops):
+        for key, value in ops:
+            if not key.startswith(ACL_KEY_PREFIX):
+                return "non-ACL changed in txn"
+            name = key[len(ACL_KEY_PREFIX):]
+            if value is not None:
+                acl = copy.deepcopy(value)
+                ifs = acl.interfaces
+                rc = self.engine.acl_put(acl.acl_name, acl.rules,
+                                         ifs.ingress if ifs else [], ifs.egress if ifs else [])
+                if rc != 0:
+                    return _abi.lib().cls_last_error(self.engine.h).decode()
+                self.by_name[acl.acl_name] = acl
+            else:
+                rc = self.engine.acl_del(name)
+                if rc != 0:
+                    return _abi.lib().cls_last_error(self.engine.h).decode()
+                self.by_name.pop(name, None)
+        return None
+
+    def dump_acls(self):
+        return list(self.by_name.values())
+
+    def get_num_of_acls(self) -> int:
+        return self.engine.acl_counts()[0]
+
+    def get_num_of_acl_changes(self) -> int:
+        return self.engine.acl_counts()[1]
+
+    def _acl_of_table(self, tid: int):
+        """The protobuf ACL whose compiled table the engine bound (-1: nil)."""
+        if tid < 0:
+            return None
+        for name, acl in self.by_name.items():
+            if self.engine.acl_table(name) == tid:
+                return acl
+        return None
+
+    def get_inbound_acl(self, if_name: str):
+        i, _ = self.engine.if_acls(self.engine.if_id(if_name))
+        return self._acl_of_table(i)
+
+    def get_outbound_acl(self, if_name: str):
+        _, o = self.engine.if_acls(self.engine.if_id(if_name))
+        return self._acl_of_table(o)
+
+    def get_acl_by_name(self, name: str):
+        return self.by_name.get(name)
+
+    # -- Connection* (:243-390), resolved on the host, evaluated on the GPU --
+    def _node_output_if(self):
+        ifn = self.contiv.get_vxlan_bvi_if_name()
+        return ifn if ifn != "" else self.contiv.get_main_physical_if_name()
+
+    def _pod_if(self, pod, cfg):
+        if cfg[1]:
+            ifn = self._node_output_if()
+            return ifn if ifn != "" else None
+        ifn, ok = self.contiv.get_if_name(pod.namespace, pod.name)
+        return ifn if ok else None
+
+    def resolve(self, fn: str, args):
+        """Returns (src_if, src_ip, dst_if, dst_ip, proto, sport, dport) or
+        CONN_FAILURE when the reference fails before testConnection."""
+        if fn == "ConnectionPodToPod":
+            sp, dp, proto, sport, dport = args
+            s, d = self.pods.get(sp), self.pods.get(dp)
+            if s is None or d is None:
+                return CONN_FAILURE
+            sif, dif = self._pod_if(sp, s), self._pod_if(dp, d)
+            if sif is None or dif is None:
+                return CONN_FAILURE
+            return sif, s[0], dif, d[0], proto, sport, dport
+        if fn == "ConnectionPodToInternet":
+            sp, dst_ip, proto, sport, dport = args
+            s = self.pods.get(sp)
+            if s is None or s[1]:
+                return CONN_FAILURE
+            sif, ok = self.contiv.get_if_name(sp.namespace, sp.name)
+            dif = self._node_output_if()
+            ip = gonet.parse_ip(dst_ip)
+            if not ok or dif == "" or ip is None:
+                return CONN_FAILURE
+            return sif, s[0], dif, ip, proto, sport, dport
+        src_ip, dp, proto, sport, dport = args
+        d = self.pods.get(dp)
+        if d is None or d[1]:
+            return CONN_FAILURE
+        sif = self._node_output_if()
+        ip = gonet.parse_ip(src_ip)
+        dif, ok = self.contiv.get_if_name(dp.namespace, dp.name)
+        if sif == "" or ip is None or not ok:
+            return CONN_FAILURE
+        return sif, ip, dif, d[0], proto, sport, dport
+
+    def connection_batch(self, calls):
+        """calls: list of (fn name, args).  One GPU launch for all of them."""
+        out = [None] * len(calls)
+        rows = []
+        for i, (fn, args) in enumerate(calls):
+            r = self.resolve(fn, args)
+            if r == CONN_FAILURE:
+                out[i] = CONN_FAILURE
+                continue
+            sif, sip, dif, dip, proto, sport, dport = r
+            s4, d4 = _ip4(sip), _ip4(dip)
+            if s4 is None or d4 is None:
+                raise ClsError("connection path supports IPv4 endpoints only")
+            rows.append((i, self.engine.if_id(sif), self.engine.if_id(dif), s4, d4, proto, sport, dport))
+        if rows:
+            a = np.array([r[1:] for r in rows], np.int64)
+            res = self.engine.connect_batch(a[:, 0], a[:, 1], a[:, 2], a[:, 3], a[:, 4], a[:, 5], a[:, 6])
+            for (i, *_), v in zip(rows, res):
+                out[i] = int(v)
+        return out
+
+    def connection_pod_to_pod(self, src_pod, dst_pod, proto, sport, dport):
+        return self.connection_batch([("ConnectionPodToPod", (src_pod, dst_pod, proto, sport, dport))])[0]
+
+    def connection_pod_to_internet(self, src_pod, dst_ip, proto, sport, dport):
+        return self.connection_batch([("ConnectionPodToInternet", (src_pod, dst_ip, proto, sport, dport))])[0]
+
+    def connection_internet_to_pod(self, src_ip, dst_pod, proto, sport, dport):
+        return self.connection_batch([("ConnectionInternetToPod", (src_ip, dst_pod, proto, sport, dport))])[0]
