@@ -90,16 +90,11 @@ def main():
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(0)
-
+    from vpp_amd import dist as D
     from vpp_amd import workload
+    rank, world, local = D.world()
+    D.init("nccl")
+    torch.cuda.set_device(local if world > 1 else 0)
     from vpp_amd.engine import Engine
 
     acl, spec, n_default = workload.config(args.config)
@@ -112,7 +107,8 @@ def main():
     dev = torch.device("cuda", torch.cuda.current_device())
     pk = {k: torch.empty(n, dtype=dt, device=dev) for k, dt in
           (("src", torch.int32), ("dst", torch.int32), ("dport", torch.int16), ("proto", torch.uint8))}
-    eng.gen_traffic_v4(spec, rank * n, pk)
+    first, _ = D.shard(rank, n)
+    eng.gen_traffic_v4(spec, first, pk)
     verdict = torch.empty(n, dtype=torch.uint8, device=dev)
     counters = torch.zeros(R + 1, dtype=torch.int64, device=dev)
     torch.cuda.synchronize()
@@ -120,8 +116,7 @@ def main():
     def step(timing):
         eng.classify(table, pk["src"], pk["dst"], pk["dport"], pk["proto"], verdict=verdict,
                      counters=counters, timing=timing)
-        if world > 1:
-            dist.all_reduce(counters)      # RCCL over xGMI: merge per-rule hit counters
+        D.merge_counters(counters)         # RCCL over xGMI: merge per-rule hit counters
 
     for _ in range(args.warmup):
         step(False)
@@ -138,10 +133,7 @@ def main():
         dist.barrier()
     wall = time.perf_counter() - t0
     kms = eng.kernel_times(reset=True)
-    t = torch.tensor([wall], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    wall = float(t.item())
+    wall = D.max_over_ranks(wall, dev)
 
     if rank == 0:
         total = n * world * args.steps

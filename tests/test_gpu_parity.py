@@ -50,9 +50,10 @@ def _assert_same(got, want):
 def test_reference_scenarios_on_gpu(eng, test):
     """The 221 Connection* KATs of acl_renderer_test.go, verdicts from the GPU
     connection kernel (one launch per phase)."""
-    from vpp_amd.engine import ACLEngine
+    from vpp_amd.engine import ACLEngine, Engine
 
-    checked, failures = replay(test, lambda contiv: ACLEngine(contiv, eng),
+    # a fresh engine per scenario, as NewMockACLEngine is called per test
+    checked, failures = replay(test, lambda contiv: ACLEngine(contiv, Engine()),
                                check_conn=lambda engine, calls: engine.connection_batch(calls))
     assert not failures, "\n".join(failures)
     assert checked > 0

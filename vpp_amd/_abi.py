@@ -94,6 +94,13 @@ def lib():
     if not os.path.exists(LIB_PATH):
         raise ClsError("libcontivcls.so not built (run __graft_entry__.build() or "
                        "make -C vpp_amd/csrc); the product has no CPU fallback")
+    # One HIP runtime per process: PyTorch ships its own libamdhip64.so.7.
+    # Load it first so that our NEEDED libamdhip64.so.7 resolves to the same
+    # already-loaded runtime (two runtimes in one process cannot share the GPU).
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = C.CDLL(LIB_PATH)
     vp, u32, u64, i32 = C.c_void_p, C.c_uint32, C.c_uint64, C.c_int32
     sig = {
