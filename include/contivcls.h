@@ -252,6 +252,12 @@ typedef struct cls_image_v4_header {
     uint32_t n_bounds, search_top, n_classes, n_tmpl, n_list_entries, n_ctr, lds_bytes;
     uint32_t off_image, off_ctr_rule, off_lin;   /* byte offsets inside the blob */
     uint32_t total_bytes;
+    uint32_t mode;             /* source lookup: 0 interval search, 1 hash LPM */
+    uint32_t default_class;    /* hash LPM: class when no hashed prefix matches */
+    uint32_t n_hash;           /* hashed prefix lengths (ascending) */
+    uint32_t hash_mask[3], hash_shift[3], hash_cap[3], off_hash[3];
+    uint32_t list_mode;        /* candidate lists: 0 template scan, 1 bit vectors */
+    uint32_t off_bv, bv_steps_d, bv_steps_p;
 } cls_image_v4_header;
 int cls_compile_v4(const cls_rule* rules, uint32_t n_rules, void* blob, uint64_t cap,
                    uint64_t* need);

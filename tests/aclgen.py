@@ -102,6 +102,25 @@ def random_acl(seed: int, n_rules: int, weird: float = 0.15, n_prefixes: int = 2
     return [random_rule(rng, pool, weird) for _ in range(n_rules)], pool
 
 
+def long_list_acl(seed: int, n_rules: int = 300, n_src: int = 3):
+    """Rules with few source prefixes and no catch-all: every cell's candidate
+    list is long (> 32), which selects the template-scan list mode."""
+    rng = random.Random(seed)
+    pool = PrefixPool(rng, 32)
+    srcs = [pool.v4[i] for i in range(n_src)]
+    rules = []
+    for _ in range(n_rules):
+        a, ln = rng.choice(srcs)
+        da, dl = rng.choice(pool.v4[n_src:])
+        dl = max(dl, 1)
+        proto = rng.choice(["tcp", "udp"])
+        p = rng.choice([22, 53, 80, 443, rng.randint(1, 65535)])
+        hi = p if rng.random() < 0.7 else min(65535, p + rng.randint(1, 1000))
+        rules.append(M.l4_rule(rng.choice([M.DENY, M.PERMIT, M.REFLECT]), "%s/%d" % (_v4(a), ln),
+                               "%s/%d" % (_v4(da), dl), proto, 0, 65535, p, hi))
+    return rules, pool
+
+
 def random_traffic(seed: int, n: int, pool: PrefixPool, other_proto: bool = True):
     """IPv4 packets biased towards the prefixes' edges."""
     rng = np.random.default_rng(seed)

@@ -39,19 +39,103 @@ class Image:
         self.has_cls = bool(h.has_cls)
         if self.has_cls:
             img = blob[h.off_image:h.off_image + h.img_bytes]
+            self._img = img
             top = h.search_top
-            self.bounds = np.frombuffer(img, np.uint32, count=2 * top, offset=h.off_bounds)
-            self.iclass = np.frombuffer(img, np.uint16, count=2 * top, offset=h.off_iclass)
+            if h.mode == 0:
+                self.bounds = np.frombuffer(img, np.uint32, count=2 * top, offset=h.off_bounds)
+                self.iclass = np.frombuffer(img, np.uint16, count=2 * top, offset=h.off_iclass)
             self.cells = np.frombuffer(img, np.uint32, count=h.n_classes * 6,
                                        offset=h.off_cells).reshape(-1, 2)
-            self.lists = np.frombuffer(img, np.uint16, count=h.n_list_entries, offset=h.off_lists)
-            self.tmpl = np.frombuffer(img, np.uint32, count=h.n_tmpl * 4,
-                                      offset=h.off_tmpl).reshape(-1, 4)
+            if h.list_mode == 0:
+                self.lists = np.frombuffer(img, np.uint16, count=h.n_list_entries, offset=h.off_lists)
+                self.tmpl = np.frombuffer(img, np.uint32, count=h.n_tmpl * 4,
+                                          offset=h.off_tmpl).reshape(-1, 4)
             self.ctr_rule = np.frombuffer(blob, np.uint32, count=h.n_ctr, offset=h.off_ctr_rule)
+            self.hash = []
+            for i in range(h.n_hash):
+                cap = h.hash_cap[i]
+                tab = np.frombuffer(img, np.uint32, count=4 * cap, offset=h.off_hash[i]).reshape(-1, 2)
+                self.hash.append((h.hash_mask[i], h.hash_shift[i], cap, tab))
+
+    @staticmethod
+    def _h0(k, shift):
+        return ((k.astype(np.uint64) * 0x9E3779B1) & 0xFFFFFFFF) >> np.uint64(shift)
+
+    @staticmethod
+    def _h1(k, shift):
+        return (((k.astype(np.uint64) ^ 0x5BD1E995) * 0xC2B2AE35) & 0xFFFFFFFF) >> np.uint64(shift)
+
+    def source_class(self, src):
+        h = self.h
+        if h.mode == 1:
+            cls = np.full(len(src), h.default_class, np.int64)
+            for mask, shift, cap, tab in self.hash:
+                key = src & np.uint32(mask)
+                e0 = tab[self._h0(key, shift).astype(np.int64)]
+                e1 = tab[cap + self._h1(key, shift).astype(np.int64)]
+                hit0 = e0[:, 0] == key
+                hit1 = e1[:, 0] == key
+                cls = np.where(hit0, e0[:, 1].astype(np.int64),
+                               np.where(hit1, e1[:, 1].astype(np.int64), cls))
+            return cls
+        k = np.zeros(len(src), np.int64)
+        s = h.search_top
+        while s:
+            c = k + s
+            k = np.where(self.bounds[c] <= src, c, k)
+            s >>= 1
+        return self.iclass[k].astype(np.int64)
 
     @staticmethod
     def _port_in(dport, pw):
         return ((dport.astype(np.uint32) - (pw & 0xFFFF)) & 0xFFFF) <= (pw >> 16)
+
+    def _classify_bv(self, cls, src, dst, dport, proto, counters):
+        """Bit-vector lists: per list, masks of the entries covering the dst
+        interval and the port interval; first match = lowest common bit."""
+        img = np.frombuffer(self._img, np.uint32)
+        pr = np.minimum(proto, 2).astype(np.int64)
+        cells1 = np.frombuffer(self._img, np.uint32, count=self.h.n_classes * 3,
+                               offset=self.h.off_cells)
+        cell = cells1[cls * 3 + pr]
+        cb = (cell >> 16).astype(np.int64)
+        d_off = ((cell & 0xFFFF).astype(np.int64) * 8) // 4
+        S = int(self.h.bv_steps_d)
+        sd = np.full(len(cls), S, np.int64)
+        sp = np.full(len(cls), S, np.int64)
+        p_off = d_off + 2 * (np.int64(1) << sd)
+        res_bits = img[d_off].astype(np.uint64) | (img[p_off].astype(np.uint64) << np.uint64(32))
+
+        def search(off, steps, x):
+            k = np.zeros(len(x), np.int64)
+            m = img[off + 1]
+            for i in range(int(steps.max()) if len(x) else 0, -1, -1):
+                st = np.where(i < steps, np.int64(1) << i, 0)
+                c = k + st
+                b = img[off + 2 * c]
+                take = b <= x
+                k = np.where(take, c, k)
+                m = np.where(take, img[off + 2 * c + 1], m)
+            return m
+
+        md = search(d_off, sd, dst.astype(np.uint32))
+        mp = search(p_off, sp, dport.astype(np.uint32))
+        m = (md & mp).astype(np.uint64)
+        found = (m != 0) & (proto <= 2)
+        low = m & (~m + np.uint64(1))
+        j = np.zeros(len(m), np.int64)
+        nz = low != 0
+        j[nz] = np.log2(low[nz].astype(np.float64)).astype(np.int64)
+        res = np.where(found, (res_bits >> (2 * j).astype(np.uint64)) & np.uint64(3), 0).astype(np.uint32)
+        slot = np.where(found, cb + j, 0)
+        np.add.at(counters, self.ctr_rule[slot].astype(np.int64), 1)
+        other = proto > 2
+        if other.any():
+            r2, rule2 = self.linear(src[other], dst[other], dport[other], proto[other])
+            res[other] = r2
+            np.subtract.at(counters, self.ctr_rule[slot[other]].astype(np.int64), 1)
+            np.add.at(counters, rule2, 1)
+        return res.astype(np.uint8), counters
 
     def linear(self, src, dst, dport, proto):
         n = len(src)
@@ -83,14 +167,9 @@ class Image:
             res, rule = self.linear(src, dst, dport, proto)
             np.add.at(counters, rule, 1)
             return res.astype(np.uint8), counters
-        h = self.h
-        k = np.zeros(n, np.int64)
-        s = h.search_top
-        while s:
-            c = k + s
-            k = np.where(self.bounds[c] <= src, c, k)
-            s >>= 1
-        cls = self.iclass[k].astype(np.int64)
+        cls = self.source_class(src)
+        if self.h.list_mode == 1:
+            return self._classify_bv(cls, src, dst, dport, proto, counters)
         pr = np.minimum(proto, 2).astype(np.int64)
         cell = self.cells[cls * 3 + pr]
         start = (cell[:, 0] & 0xFFFF).astype(np.int64)

@@ -33,6 +33,36 @@ def test_compiler_matches_oracle(seed, n_rules, weird):
     _check(rules, tr)
 
 
+@pytest.mark.parametrize("lens", [(32,), (32, 24), (32, 24, 16), (32, 0), (8, 16, 24, 32)])
+@pytest.mark.parametrize("seed", range(4))
+def test_hash_lpm_and_search_modes(seed, lens):
+    """Few distinct source prefix lengths -> cuckoo-hash LPM (mode 1); more ->
+    interval search (mode 0).  Both must be exact, incl. /0 and nesting."""
+    import random
+    from aclgen import PrefixPool, random_rule
+    rng = random.Random(seed)
+    pool = PrefixPool(rng, 40)
+    base = [rng.getrandbits(32) for _ in range(6)]
+    pool.v4 = []
+    for i in range(60):
+        ln = lens[i % len(lens)]
+        m = (0xFFFFFFFF << (32 - ln)) & 0xFFFFFFFF if ln else 0
+        pool.v4.append(((rng.choice(base) ^ (rng.getrandbits(12) << 4)) & m, ln))
+    rules = [random_rule(rng, pool, 0.0) for _ in range(120)]
+    img = _check(rules, random_traffic(seed, 4000, pool))
+    assert img.has_cls
+    assert img.h.mode == (1 if len([x for x in lens if x]) <= 3 else 0)
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_long_candidate_lists_use_scan_mode(seed):
+    """> 32 candidates in a cell: the template-scan list mode (list_mode 0)."""
+    from aclgen import long_list_acl
+    rules, pool = long_list_acl(seed + 500)
+    img = _check(rules, random_traffic(seed, 4000, pool))
+    assert img.has_cls and img.h.list_mode == 0
+
+
 def test_compiler_uses_classifier_for_larger_tables():
     rules, pool = random_acl(7, 120, 0.0)
     img = _check(rules, random_traffic(7, 2000, pool))

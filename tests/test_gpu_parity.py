@@ -69,6 +69,24 @@ def test_random_acls_both_kernels(eng, seed, n_rules, weird):
     _assert_same(_gpu(eng, rules, tr, force_linear=True), want)
 
 
+@pytest.mark.parametrize("seed", range(3))
+@pytest.mark.parametrize("kind", ["hash_bv", "search_bv", "hash_scan", "search_scan"])
+def test_all_kernel_variants(eng, seed, kind):
+    """The four classifier variants (hash-LPM / interval-search source lookup
+    x bit-vector / template-scan candidate lists) against the oracle."""
+    from aclgen import long_list_acl
+    from cls_image import Image, compile_blob
+    from vpp_amd import _abi
+    if kind.endswith("scan"):
+        rules, pool = long_list_acl(seed + 70, 300, n_src=3 if kind.startswith("hash") else 30)
+    else:
+        rules, pool = random_acl(seed * 31 + 7, 120, 0.0, n_prefixes=4 if kind.startswith("hash") else 24)
+    h = Image(compile_blob(_abi.CRules(rules))).h
+    assert (h.mode, h.list_mode) == (int(kind.startswith("hash")), int(kind.endswith("bv"))), kind
+    tr = random_traffic(seed + 11, 30000, pool)
+    _assert_same(_gpu(eng, rules, tr), _oracle(rules, tr))
+
+
 def test_misaligned_batch_uses_scalar_path(eng):
     rules, pool = random_acl(99, 200, 0.05)
     tr = random_traffic(5, 9001, pool)

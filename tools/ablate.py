@@ -1,0 +1,41 @@
+#!/usr/bin/env python3
+"""Diagnostics: time classify4_cls with stages ablated (CONTIVCLS_ABLATE bits:
+1 counters, 2 candidate scan, 4 source lookup, 8 verdict store).  Results of
+ablated runs are wrong by construction; only kernel times matter."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    import numpy as np
+    import torch
+    from vpp_amd import workload
+    from vpp_amd.engine import Engine
+    cfg = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+    acl, spec, n = workload.config(cfg)
+    eng = Engine(0)
+    t = eng.put_table("t", acl.rules)
+    print("info", t.info())
+    pk = {k: torch.empty(n, dtype=dt, device="cuda") for k, dt in
+          (("src", torch.int32), ("dst", torch.int32), ("dport", torch.int16), ("proto", torch.uint8))}
+    eng.gen_traffic_v4(spec, 0, pk)
+    verdict = torch.empty(n, dtype=torch.uint8, device="cuda")
+    counters = torch.zeros(t.n_rules + 1, dtype=torch.int64, device="cuda")
+    for ab in [0, 1, 2, 3, 4, 6, 7, 15]:
+        os.environ["CONTIVCLS_ABLATE"] = str(ab)
+        for _ in range(2):
+            eng.classify(t, pk["src"], pk["dst"], pk["dport"], pk["proto"], verdict=verdict, counters=counters)
+        eng.kernel_times(reset=True)
+        for _ in range(5):
+            eng.classify(t, pk["src"], pk["dst"], pk["dport"], pk["proto"], verdict=verdict,
+                         counters=counters, timing=True)
+        ms = float(np.mean(eng.kernel_times(reset=True)))
+        print("ablate=%2d kernel %.3f ms  %.1f Gpps  %.1f GB/s" % (ab, ms, n / ms / 1e6, n * 12 / ms / 1e6))
+    os.environ.pop("CONTIVCLS_ABLATE")
+
+
+if __name__ == "__main__":
+    main()

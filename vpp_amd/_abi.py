@@ -77,7 +77,11 @@ class ImageHeader(C.Structure):
         "magic", "version", "n_rules", "n_lin", "has_cls", "img_bytes", "off_bounds",
         "off_iclass", "off_cells", "off_lists", "off_tmpl", "n_bounds", "search_top",
         "n_classes", "n_tmpl", "n_list_entries", "n_ctr", "lds_bytes", "off_image",
-        "off_ctr_rule", "off_lin", "total_bytes")]
+        "off_ctr_rule", "off_lin", "total_bytes", "mode", "default_class", "n_hash")] + [
+        ("hash_mask", C.c_uint32 * 3), ("hash_shift", C.c_uint32 * 3),
+        ("hash_cap", C.c_uint32 * 3), ("off_hash", C.c_uint32 * 3),
+        ("list_mode", C.c_uint32), ("off_bv", C.c_uint32), ("bv_steps_d", C.c_uint32),
+        ("bv_steps_p", C.c_uint32)]
 
 
 _lib = None

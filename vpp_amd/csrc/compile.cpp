@@ -217,6 +217,120 @@ struct TmplHash {
 
 uint32_t align4(uint32_t w) { return (w + 3u) & ~3u; }
 
+// Two-table cuckoo hash of (key, class): table 0 at [0, cap), table 1 at
+// [cap, 2 cap); entry = key | (class + 1) << 32, 0 = empty.
+bool cuckoo_build(const std::vector<std::pair<uint32_t, uint32_t>>& keys, uint32_t cap,
+                  std::vector<uint64_t>& tab) {
+    const uint32_t shift = 32u - uint32_t(__builtin_ctz(cap));
+    std::vector<uint8_t> used(size_t(cap) * 2, 0);
+    tab.assign(size_t(cap) * 2, 0ull);
+    for (const auto& kv : keys) {
+        uint64_t cur = uint64_t(kv.first) | (uint64_t(kv.second) << 32);
+        bool cur_valid = true;
+        int side = 0;
+        for (int kick = 0; kick < 256 && cur_valid; ++kick) {
+            const uint32_t k = uint32_t(cur);
+            const size_t pos = side == 0 ? lpm_h0(k, shift) : size_t(cap) + lpm_h1(k, shift);
+            std::swap(cur, tab[pos]);
+            const bool was_used = used[pos];
+            used[pos] = 1;
+            cur_valid = was_used;
+            side ^= 1;
+        }
+        if (cur_valid) return false;
+    }
+    // Empty slots hold a key that never probes them, so the kernel's hit test
+    // is a plain key compare (no "occupied" bit, no branch).
+    for (size_t pos = 0; pos < tab.size(); ++pos) {
+        if (used[pos]) continue;
+        const bool t1 = pos >= cap;
+        const uint32_t slot = uint32_t(t1 ? pos - cap : pos);
+        uint32_t k = 0;
+        while ((t1 ? lpm_h1(k, shift) : lpm_h0(k, shift)) == slot) ++k;
+        tab[pos] = k;
+    }
+    return true;
+}
+
+// Bit-vector arrays of one candidate list (k <= 32 entries), appended to `out`:
+//   dst array:  2^S x {interval start, mask of entries whose dst prefix covers it}
+//   port array: 2^S x {interval start, mask of entries whose port range covers it}
+// S is the table-wide search depth, so every lane runs the same steps; the
+// arrays are padded with {0xFFFFFFFF, last mask} and never need a bound check.
+struct BvDesc {
+    uint32_t off_rel;          // byte offset of the dst array inside the BV section
+    uint64_t res;              // 2-bit result of entry j at bits 2j
+};
+
+void bv_bounds(const std::vector<TmplKey>& ents, std::vector<uint32_t>& db, std::vector<uint32_t>& pb) {
+    std::vector<uint64_t> d{0};
+    std::vector<uint32_t> p{0};
+    for (const TmplKey& t : ents) {
+        if (t.m) {
+            const uint64_t hi = uint64_t(t.a | ~t.m);
+            d.push_back(t.a);
+            if (hi < 0xFFFFFFFFull) d.push_back(hi + 1);
+        }
+        const uint32_t lo = t.pw & 0xFFFFu, phi = lo + (t.pw >> 16);
+        p.push_back(lo);
+        if (phi < 0xFFFFu) p.push_back(phi + 1);
+    }
+    std::sort(d.begin(), d.end());
+    d.erase(std::unique(d.begin(), d.end()), d.end());
+    std::sort(p.begin(), p.end());
+    p.erase(std::unique(p.begin(), p.end()), p.end());
+    db.assign(d.begin(), d.end());
+    pb = p;
+}
+
+BvDesc build_bv(const std::vector<TmplKey>& ents, uint32_t S, std::vector<uint32_t>& out) {
+    const size_t k = ents.size();
+    std::vector<uint32_t> db, pb;
+    bv_bounds(ents, db, pb);
+    uint64_t res = 0;
+    for (size_t j = 0; j < k; ++j) res |= uint64_t(ents[j].res & 3u) << (2 * j);
+    const BvDesc desc{uint32_t(out.size()) * 4, res};
+    const size_t n = size_t(1) << S;
+    uint32_t last = 0;
+    // Entry 0's bound is always 0 and the search never reads it (probes start
+    // at index >= 1): it carries the list's result bits instead (dst array:
+    // low word, port array: high word).
+    for (size_t i = 0; i < n; ++i) {
+        if (i < db.size()) {
+            const uint32_t x = db[i];
+            uint32_t m = 0;
+            for (size_t j = 0; j < k; ++j)
+                if (((x ^ ents[j].a) & ents[j].m) == 0) m |= 1u << j;
+            last = m;
+            out.push_back(i == 0 ? uint32_t(res) : x);
+        } else {
+            out.push_back(0xFFFFFFFFu);
+        }
+        out.push_back(last);
+    }
+    for (size_t i = 0; i < n; ++i) {
+        if (i < pb.size()) {
+            const uint32_t x = pb[i];
+            uint32_t m = 0;
+            for (size_t j = 0; j < k; ++j) {
+                const uint32_t lo = ents[j].pw & 0xFFFFu, hi = lo + (ents[j].pw >> 16);
+                if (x >= lo && x <= hi) m |= 1u << j;
+            }
+            last = m;
+            out.push_back(i == 0 ? uint32_t(res >> 32) : x);
+        } else {
+            out.push_back(0xFFFFFFFFu);
+        }
+        out.push_back(last);
+    }
+    // Blocks are 2^(S+4) bytes: without a stagger, probe i of every list would
+    // sit on the same LDS bank pair and the lanes of a wave (different lists,
+    // same step) would conflict 32-way.  One extra uint2 rotates the banks.
+    out.push_back(0u);
+    out.push_back(0u);
+    return desc;
+}
+
 }  // namespace
 
 bool build_cls4(const std::vector<SemRule>& sem, uint32_t n_rules, Cls4Image& img,
@@ -285,6 +399,47 @@ bool build_cls4(const std::vector<SemRule>& sem, uint32_t n_rules, Cls4Image& im
     }
     const uint32_t n_classes = uint32_t(class_pfx.size());
     const uint32_t n_real_bounds = uint32_t(bounds.size());
+
+    // Hash LPM (tuple space): when the classed prefixes use few distinct lengths
+    // (a rendered global table has only pod /32s), the class of an address is
+    // found by one cuckoo probe pair per length instead of the binary search.
+    std::vector<std::vector<uint64_t>> hash_tabs;
+    {
+        std::map<int, std::vector<std::pair<uint32_t, uint32_t>>> keys;  // len -> (addr, class)
+        int len0_class = -1;
+        for (size_t i = 0; i < pfx.size(); ++i) {
+            const int c = class_of_pfx[i + 1];
+            if (c < 0) continue;                     // never the longest match anywhere
+            if (pfx[i].len == 0) { len0_class = c; continue; }
+            keys[pfx[i].len].push_back({pfx[i].addr, uint32_t(c)});
+        }
+        uint32_t dflt = 0;
+        if (len0_class >= 0) dflt = uint32_t(len0_class);
+        else if (class_of_pfx[0] >= 0) dflt = uint32_t(class_of_pfx[0]);
+        if (keys.size() <= kMaxHashLens) {
+            img.mode = 1;
+            img.default_class = dflt;
+            for (const auto& kv : keys) {
+                const auto& ks = kv.second;
+                uint32_t cap = 16;
+                while (cap < ks.size()) cap *= 2;
+                std::vector<uint64_t> tab;
+                for (;;) {
+                    if (cuckoo_build(ks, cap, tab)) break;
+                    cap *= 2;
+                    if (cap > (1u << 16)) { img.mode = 0; break; }
+                }
+                if (img.mode == 0) break;
+                const uint32_t i = uint32_t(hash_tabs.size());
+                img.hash_mask[i] = v4_mask(kv.first);
+                img.hash_shift[i] = 32u - uint32_t(__builtin_ctz(cap));
+                img.hash_cap[i] = cap;
+                hash_tabs.push_back(std::move(tab));
+            }
+            img.n_hash = img.mode == 1 ? uint32_t(hash_tabs.size()) : 0u;
+            if (img.mode == 0) hash_tabs.clear();
+        }
+    }
     // pad to 2*top entries so the branch-free search never needs a bound check:
     // sentinel 0xFFFFFFFF keeps the class of the last interval (which holds it)
     uint32_t top = 1;
@@ -351,34 +506,124 @@ bool build_cls4(const std::vector<SemRule>& sem, uint32_t n_rules, Cls4Image& im
         }
     }
 
-    // serialise (u32 words, each section 16 B aligned)
-    std::vector<uint32_t>& w = img.words;
-    img.off_bounds = 0;
-    w.insert(w.end(), bounds.begin(), bounds.end());
-    w.resize(align4(uint32_t(w.size())));
-    img.off_iclass = uint32_t(w.size()) * 4;
-    w.resize(w.size() + (bounds.size() + 1) / 2);
-    std::memcpy(reinterpret_cast<uint8_t*>(w.data()) + img.off_iclass, iclass.data(), iclass.size() * 2);
-    w.resize(align4(uint32_t(w.size())));
-    img.off_cells = uint32_t(w.size()) * 4;
-    w.insert(w.end(), cells.begin(), cells.end());
-    w.resize(align4(uint32_t(w.size())));
-    img.off_lists = uint32_t(w.size()) * 4;
+    // the scan kernel reads list/template entries speculatively (clamped
+    // index): keep both sections non-empty
+    if (lists.empty()) lists.push_back(0);
+    if (tmpls.empty()) tmpls.push_back(TmplKey{0, 0, 0, 0});
+
+    // bit-vector form of every distinct candidate list (lists <= 32 entries):
+    // first match = ctz(mask of entries covering the dst interval & mask of
+    // entries covering the port interval)
+    std::vector<uint32_t> bv;
+    std::unordered_map<uint32_t, BvDesc> bv_desc;        // list (start | len << 16) -> arrays
+    bool all_bv = true;
+    uint32_t S = 0;                                       // table-wide search depth
+    std::vector<uint32_t> bv_lists;                       // distinct cell list keys
+    for (uint32_t c = 0; c < n_classes && all_bv; ++c)
+        for (int pr = 0; pr < 3; ++pr) {
+            const uint32_t x = cells[(size_t(c) * 3 + pr) * 2];
+            if ((x >> 16) > 32) { all_bv = false; break; }
+            bv_lists.push_back(x);
+        }
+    std::sort(bv_lists.begin(), bv_lists.end());
+    bv_lists.erase(std::unique(bv_lists.begin(), bv_lists.end()), bv_lists.end());
+    auto ents_of = [&](uint32_t x) {
+        std::vector<TmplKey> ents;
+        for (uint32_t j = 0; j < (x >> 16); ++j) ents.push_back(tmpls[lists[(x & 0xFFFFu) + j]]);
+        return ents;
+    };
+    if (all_bv) {
+        for (uint32_t x : bv_lists) {
+            std::vector<uint32_t> db, pb;
+            bv_bounds(ents_of(x), db, pb);
+            const size_t need = std::max(db.size(), pb.size());
+            while ((size_t(1) << S) < need) ++S;
+        }
+        for (uint32_t x : bv_lists) bv_desc[x] = build_bv(ents_of(x), S, bv);
+        // 16-bit fields of the u32 cell: array offset / 8 and counter base
+        const size_t worst = (bounds.size() * 3 + cells.size() + bv.size() + 64) * 4;
+        if (img.ctr_rule.size() > 0xFFFFu || worst / 8 > 0xFFFFu) {
+            all_bv = false;
+            bv.clear();
+            bv_desc.clear();
+        }
+    }
+    const uint32_t max_sd = S, max_sp = S;
+    // Hot slots: the first entry of each cell of the class covering most of the
+    // address space (random sources land there), and slot 0 (default DENY).
     {
-        const size_t base = w.size();
-        w.resize(base + (lists.size() + 1) / 2);
-        if (!lists.empty())
-            std::memcpy(reinterpret_cast<uint8_t*>(w.data() + base), lists.data(), lists.size() * 2);
+        std::vector<double> span(n_classes, 0.0);
+        for (uint32_t k = 0; k < n_real_bounds; ++k) {
+            const double hi = k + 1 < n_real_bounds ? double(bounds[k + 1]) : 4294967296.0;
+            span[iclass[k]] += hi - double(bounds[k]);
+        }
+        const uint32_t dc = uint32_t(std::max_element(span.begin(), span.end()) - span.begin());
+        uint32_t hot[4] = {0u, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+        for (int pr = 0; pr < 3; ++pr) {
+            const uint32_t x = cells[(size_t(dc) * 3 + pr) * 2], base = cells[(size_t(dc) * 3 + pr) * 2 + 1];
+            if ((x >> 16) == 0) continue;            // empty list: no slot of its own
+            hot[pr + 1] = base;                      // slots are distinct per (cell, position)
+        }
+        for (int i = 0; i < 4; ++i) img.hot_slot[i] = hot[i];
     }
-    w.resize(align4(uint32_t(w.size())));
-    img.off_tmpl = uint32_t(w.size()) * 4;
-    for (const auto& t : tmpls) {
-        w.push_back(t.a);
-        w.push_back(t.m);
-        w.push_back(t.pw);
-        w.push_back(t.res);
+    img.list_mode = all_bv ? 1u : 0u;
+    img.bv_steps_d = max_sd;
+    img.bv_steps_p = max_sp;
+
+    // serialise (u32 words, each section 16 B aligned); sections the chosen
+    // modes never read are left out of the LDS image
+    std::vector<uint32_t>& w = img.words;
+    if (img.mode == 0) {
+        img.off_bounds = 0;
+        w.insert(w.end(), bounds.begin(), bounds.end());
+        w.resize(align4(uint32_t(w.size())));
+        img.off_iclass = uint32_t(w.size()) * 4;
+        w.resize(w.size() + (bounds.size() + 1) / 2);
+        std::memcpy(reinterpret_cast<uint8_t*>(w.data()) + img.off_iclass, iclass.data(), iclass.size() * 2);
+        w.resize(align4(uint32_t(w.size())));
     }
-    w.resize(align4(uint32_t(w.size())));
+    img.off_cells = uint32_t(w.size()) * 4;
+    if (img.list_mode == 0) {
+        // scan cells: uint2 {list start | len << 16, counter base}
+        w.insert(w.end(), cells.begin(), cells.end());
+        w.resize(align4(uint32_t(w.size())));
+        img.off_lists = uint32_t(w.size()) * 4;
+        const size_t lbase = w.size();
+        w.resize(lbase + (lists.size() + 1) / 2);
+        std::memcpy(reinterpret_cast<uint8_t*>(w.data() + lbase), lists.data(), lists.size() * 2);
+        w.resize(align4(uint32_t(w.size())));
+        img.off_tmpl = uint32_t(w.size()) * 4;
+        for (const auto& t : tmpls) {
+            w.push_back(t.a);
+            w.push_back(t.m);
+            w.push_back(t.pw);
+            w.push_back(t.res);
+        }
+        w.resize(align4(uint32_t(w.size())));
+    } else {
+        // bit-vector cells: u32 {dst array offset / 8 | counter base << 16}
+        // (port array = dst array + 2^S entries; result bits in entry 0 of
+        // both arrays)
+        const size_t n_cells = size_t(n_classes) * 3;
+        const uint32_t off_bv = uint32_t(align4(uint32_t(w.size() + n_cells))) * 4;
+        img.off_bv = off_bv;
+        for (size_t i = 0; i < n_cells; ++i) {
+            const BvDesc& d = bv_desc.at(cells[2 * i]);
+            const uint32_t off = off_bv + d.off_rel;
+            w.push_back((off / 8) | (cells[2 * i + 1] << 16));
+        }
+        w.resize(align4(uint32_t(w.size())));
+        w.insert(w.end(), bv.begin(), bv.end());
+        w.resize(align4(uint32_t(w.size())));
+    }
+    for (uint32_t i = 0; i < img.n_hash; ++i) {
+        img.off_hash[i] = uint32_t(w.size()) * 4;
+        for (uint64_t e : hash_tabs[i]) {
+            w.push_back(uint32_t(e));
+            w.push_back(uint32_t(e >> 32));
+        }
+        w.resize(align4(uint32_t(w.size())));
+    }
     img.img_bytes = uint32_t(w.size()) * 4;
     img.n_bounds = n_real_bounds;
     img.n_classes = n_classes;

@@ -25,6 +25,8 @@
 //   are one u32 per (cell, position) "slot", mapped back to rule indices
 //   after the kernel (slot 0 = default DENY = counter R).
 #pragma once
+#include <hip/hip_runtime.h>
+
 #include <cstdint>
 #include <string>
 #include <vector>
@@ -33,6 +35,15 @@
 #include "goparse.hpp"
 
 namespace cls {
+
+// Cuckoo hash pair of the hash-LPM source lookup (shared by compiler and kernel).
+constexpr uint32_t kMaxHashLens = 3;
+__host__ __device__ inline uint32_t lpm_h0(uint32_t k, uint32_t shift) {
+    return (k * 0x9E3779B1u) >> shift;
+}
+__host__ __device__ inline uint32_t lpm_h1(uint32_t k, uint32_t shift) {
+    return ((k ^ 0x5BD1E995u) * 0xC2B2AE35u) >> shift;
+}
 
 enum : uint8_t { RES_DENY = 0, RES_PERMIT = 1, RES_REFLECT = 2, RES_FAIL = 3 };
 enum : int { P_TCP = 0, P_UDP = 1, P_ICMP = 2, P_OTHER = 3, NPROTO = 4 };
@@ -89,6 +100,19 @@ struct Cls4Image {
     uint32_t search_top = 0;       // largest power of two <= n_bounds
     uint32_t lds_bytes = 0;        // image + counters (u32 per slot), 16 B aligned
     std::vector<uint32_t> ctr_rule;  // slot -> rule index (R = default DENY)
+    // source lookup: mode 0 = interval binary search, 1 = hash LPM
+    uint32_t mode = 0;
+    uint32_t default_class = 0;    // hash mode: class of addresses no hashed prefix covers
+    uint32_t n_hash = 0;           // hashed prefix lengths, ascending
+    uint32_t hash_mask[kMaxHashLens] = {}, hash_shift[kMaxHashLens] = {};
+    uint32_t hash_cap[kMaxHashLens] = {}, off_hash[kMaxHashLens] = {};
+    // candidate lists: mode 0 = scan of template ids, 1 = bit vectors (all lists <= 32)
+    uint32_t list_mode = 0;
+    uint32_t off_bv = 0;
+    uint32_t bv_steps_d = 0, bv_steps_p = 0;   // largest search depths over the lists
+    // slots expected to take most hits (first entry of each cell of the
+    // default source class, default DENY): counted in registers, not LDS
+    uint32_t hot_slot[4] = {0, 0, 0, 0};
 };
 
 // Build the image; returns false (with reason) if the table does not fit the

@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -305,6 +306,22 @@ int cls_classify(cls_engine* e, uint32_t table_id, const cls_pkt_soa* pk, uint64
             cd.lin = t->d_lin4.as<LinRule4>();
             cd.n_lin = uint32_t(t->lin4.size());
             cd.n_rules = t->n_rules;
+            cd.mode = t->img.mode;
+            cd.default_class = t->img.default_class;
+            cd.n_hash = t->img.n_hash;
+            cd.list_mode = t->img.list_mode;
+            cd.bv_steps = std::max(t->img.bv_steps_d, t->img.bv_steps_p);
+            for (int i = 0; i < 4; ++i) cd.hot_slot[i] = t->img.hot_slot[i];
+            for (uint32_t i = 0; i < kMaxHashLens; ++i) {
+                cd.hash_mask[i] = t->img.hash_mask[i];
+                cd.hash_shift[i] = t->img.hash_shift[i];
+                cd.hash_cap[i] = t->img.hash_cap[i];
+                cd.off_hash[i] = t->img.off_hash[i];
+            }
+            // diagnostics: CONTIVCLS_ABLATE=bits skips kernel stages (1 counters,
+            // 2 candidate scan, 4 source lookup, 8 verdict store) -- results are wrong
+            const char* ab = std::getenv("CONTIVCLS_ABLATE");
+            cd.ablate = ab ? uint32_t(std::strtoul(ab, nullptr, 0)) : 0u;
             HIPC(e, launch_classify4_cls(cd, p, d_verdict, t->d_slot.as<unsigned long long>(),
                                          t->lds_resident, vec, cfg));
         } else {
@@ -586,6 +603,19 @@ int cls_compile_v4(const cls_rule* rules, uint32_t n, void* blob, uint64_t cap, 
         h.n_bounds = img.n_bounds; h.search_top = img.search_top; h.n_classes = img.n_classes;
         h.n_tmpl = img.n_tmpl; h.n_list_entries = img.n_list_entries; h.n_ctr = img.n_ctr;
         h.lds_bytes = img.lds_bytes;
+        h.mode = img.mode;
+        h.default_class = img.default_class;
+        h.n_hash = img.n_hash;
+        h.list_mode = img.list_mode;
+        h.off_bv = img.off_bv;
+        h.bv_steps_d = img.bv_steps_d;
+        h.bv_steps_p = img.bv_steps_p;
+        for (uint32_t i = 0; i < kMaxHashLens; ++i) {
+            h.hash_mask[i] = img.hash_mask[i];
+            h.hash_shift[i] = img.hash_shift[i];
+            h.hash_cap[i] = img.hash_cap[i];
+            h.off_hash[i] = img.off_hash[i];
+        }
     }
     auto al = [](uint64_t x) { return (x + 15) & ~uint64_t(15); };
     h.off_image = uint32_t(al(sizeof h));

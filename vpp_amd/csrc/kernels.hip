@@ -51,35 +51,201 @@ __device__ __forceinline__ void linear_one(const LinRule4* __restrict__ rules, u
     }
 }
 
-template <typename Base>
-__device__ __forceinline__ void cls4_one(Base base, const Cls4Dev& t, uint32_t src, uint32_t dst,
-                                         uint32_t dport, uint32_t proto, uint32_t& res,
-                                         uint32_t& slot) {
-    const uint32_t* __restrict__ b = reinterpret_cast<const uint32_t*>(base + t.off_bounds);
-    uint32_t k = 0;
+// Source class of N packets, interleaved (N independent LDS chains per lane).
+template <int N, int kMode>
+__device__ __forceinline__ void src_class(const uint8_t* base, const Cls4Dev& t,
+                                          const uint32_t (&src)[N], uint32_t (&cls)[N]) {
+    if constexpr (kMode == 1) {
+        // hash LPM: one cuckoo probe pair per prefix length, lengths ascending so
+        // the longest hit wins
+#pragma unroll
+        for (int q = 0; q < N; ++q) cls[q] = t.default_class;
 #pragma unroll 1
-    for (uint32_t s = t.search_top; s; s >>= 1) {
-        const uint32_t c = k + s;
-        k = (b[c] <= src) ? c : k;
+        for (uint32_t i = 0; i < t.n_hash; ++i) {
+            const uint2* __restrict__ tab = reinterpret_cast<const uint2*>(base + t.off_hash[i]);
+            const uint32_t mask = t.hash_mask[i], shift = t.hash_shift[i], cap = t.hash_cap[i];
+            uint2 e0[N], e1[N];
+            uint32_t key[N];
+#pragma unroll
+            for (int q = 0; q < N; ++q) {
+                key[q] = src[q] & mask;
+                e0[q] = tab[lpm_h0(key[q], shift)];
+                e1[q] = tab[cap + lpm_h1(key[q], shift)];
+            }
+#pragma unroll
+            for (int q = 0; q < N; ++q) {
+                // empty slots hold keys that never probe them: a key compare is
+                // the whole hit test; bit selects keep it branch-free
+                const uint32_t m0 = 0u - uint32_t(e0[q].x == key[q]);
+                const uint32_t m1 = 0u - uint32_t(e1[q].x == key[q]) & ~m0;
+                cls[q] = (e0[q].y & m0) | (e1[q].y & m1) | (cls[q] & ~(m0 | m1));
+            }
+        }
+    } else {
+        // branch-free binary search over the padded interval boundaries
+        const uint32_t* __restrict__ b = reinterpret_cast<const uint32_t*>(base + t.off_bounds);
+        uint32_t k[N];
+#pragma unroll
+        for (int q = 0; q < N; ++q) k[q] = 0;
+#pragma unroll 1
+        for (uint32_t s = t.search_top; s; s >>= 1) {
+#pragma unroll
+            for (int q = 0; q < N; ++q) {
+                const uint32_t c = k[q] + s;
+                k[q] = (b[c] <= src[q]) ? c : k[q];
+            }
+        }
+        const uint16_t* __restrict__ ic = reinterpret_cast<const uint16_t*>(base + t.off_iclass);
+#pragma unroll
+        for (int q = 0; q < N; ++q) cls[q] = ic[k[q]];
     }
-    const uint32_t cls = reinterpret_cast<const uint16_t*>(base + t.off_iclass)[k];
-    const uint2 cell = reinterpret_cast<const uint2*>(base + t.off_cells)[cls * 3u + proto];
-    const uint16_t* __restrict__ L = reinterpret_cast<const uint16_t*>(base + t.off_lists) + (cell.x & 0xFFFFu);
+}
+
+// First match of N packets (protocols 0-2) against their cells' candidate
+// lists.  The N scans advance in lockstep with predication: a finished packet
+// keeps re-reading a valid entry instead of branching, so the lane issues N
+// independent LDS reads per step.
+template <int N, int kMode, int kList>
+__device__ __forceinline__ void classify_n(const uint8_t* base, const Cls4Dev& t,
+                                           const uint32_t (&src)[N], const uint32_t (&dst)[N],
+                                           const uint32_t (&dport)[N], const uint32_t (&proto)[N],
+                                           uint32_t (&res)[N], uint32_t (&slot)[N]) {
+    uint32_t cls[N];
+    if (t.ablate & 4u) {
+#pragma unroll
+        for (int q = 0; q < N; ++q) cls[q] = src[q] & 1u;
+    } else {
+        src_class<N, kMode>(base, t, src, cls);
+    }
+    const uint2* __restrict__ cells = reinterpret_cast<const uint2*>(base + t.off_cells);
+    if constexpr (kList == 1) {
+        // Bit vectors: the entries of the cell's list that cover the packet's
+        // dst interval AND its port interval; the first such entry (lowest
+        // set bit) is the first match of the ordered list.  Both interval
+        // searches are branch-free and run t.bv_steps steps for every lane.
+        // cell = dst array offset / 8 | counter base << 16; entry 0 of the dst
+        // and port arrays = {result bits lo / hi, mask of interval 0}
+        const uint32_t* __restrict__ cells1 = reinterpret_cast<const uint32_t*>(base + t.off_cells);
+        uint32_t cb[N], rlo[N], rhi[N];
+        uint32_t kd[N], kp[N], md[N], mp[N];
+        const uint2* DA[N];
+        const uint2* PA[N];
+        const uint32_t S = t.bv_steps;       // table-wide depth: one uniform step size
+#pragma unroll
+        for (int q = 0; q < N; ++q) {
+            const uint32_t pp = proto[q] <= 2u ? proto[q] : 0u;
+            const uint32_t cell = cells1[cls[q] * 3u + pp];
+            cb[q] = cell >> 16;
+            DA[q] = reinterpret_cast<const uint2*>(base + (cell & 0xFFFFu) * 8u);
+            PA[q] = DA[q] + (1u << S);
+        }
+#pragma unroll
+        for (int q = 0; q < N; ++q) {
+            const uint2 d0 = DA[q][0], p0 = PA[q][0];
+            rlo[q] = d0.x;
+            rhi[q] = p0.x;
+            md[q] = d0.y;
+            mp[q] = p0.y;
+            kd[q] = 0u;
+            kp[q] = 0u;
+        }
+        if (!(t.ablate & 2u)) {
+#pragma unroll 1
+            for (uint32_t i = S; i-- > 0;) {
+                const uint32_t step = 1u << i;
+#pragma unroll
+                for (int q = 0; q < N; ++q) {
+                    const uint32_t cd = kd[q] + step;
+                    const uint32_t cp = kp[q] + step;
+                    const uint2 ed = DA[q][cd];
+                    const uint2 ep = PA[q][cp];
+                    const bool td = ed.x <= dst[q], tp = ep.x <= dport[q];
+                    kd[q] = td ? cd : kd[q];
+                    md[q] = td ? ed.y : md[q];
+                    kp[q] = tp ? cp : kp[q];
+                    mp[q] = tp ? ep.y : mp[q];
+                }
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < N; ++q) {
+            const uint32_t m = (proto[q] <= 2u) ? (md[q] & mp[q]) : 0u;
+            const uint32_t j = uint32_t(__builtin_ctz(m | 0x80000000u));   // m == 0 handled below
+            const uint32_t bits = j < 16u ? (rlo[q] >> (2u * j)) : (rhi[q] >> (2u * (j - 16u)));
+            res[q] = m ? (bits & 3u) : 0u;            // default DENY (aclengine_mock.go:667)
+            slot[q] = m ? cb[q] + j : 0u;
+        }
+        return;
+    }
+    const uint16_t* __restrict__ L = reinterpret_cast<const uint16_t*>(base + t.off_lists);
     const uint4* __restrict__ T = reinterpret_cast<const uint4*>(base + t.off_tmpl);
-    const uint32_t len = cell.x >> 16;
-    res = 0;
-    slot = 0;
-    for (uint32_t j = 0; j < len; ++j) {
-        const uint4 tm = T[L[j]];
-        if (((dst ^ tm.x) & tm.y) == 0 && port_in(dport, tm.z)) {
-            res = tm.w;
-            slot = cell.y + j;
-            break;
+    uint32_t start[N], len[N], cb[N];
+    bool act[N];
+#pragma unroll
+    for (int q = 0; q < N; ++q) {
+        const uint32_t pp = proto[q] <= 2u ? proto[q] : 0u;
+        const uint2 cell = cells[cls[q] * 3u + pp];
+        start[q] = cell.x & 0xFFFFu;
+        len[q] = proto[q] <= 2u ? (cell.x >> 16) : 0u;
+        cb[q] = cell.y;
+        res[q] = 0u;      // default DENY (aclengine_mock.go:667)
+        slot[q] = 0u;     // slot 0 = default DENY counter
+        act[q] = len[q] != 0u;
+    }
+    bool any = false;
+#pragma unroll
+    for (int q = 0; q < N; ++q) any |= act[q];
+    if (t.ablate & 2u) {
+#pragma unroll
+        for (int q = 0; q < N; ++q) res[q] = len[q] & 3u;
+        any = false;
+    }
+    for (uint32_t j = 0; any; ++j) {
+        any = false;
+#pragma unroll
+        for (int q = 0; q < N; ++q) {
+            const uint32_t idx = start[q] + (act[q] ? j : 0u);
+            const uint4 tm = T[L[idx]];
+            const bool m = act[q] && ((dst[q] ^ tm.x) & tm.y) == 0u && port_in(dport[q], tm.z);
+            res[q] = m ? tm.w : res[q];
+            slot[q] = m ? cb[q] + j : slot[q];
+            act[q] = act[q] && !m && (j + 1u < len[q]);
+            any |= act[q];
         }
     }
 }
 
-template <bool kLds, bool kVec>
+template <int N, bool kLds, int kMode>
+__device__ __forceinline__ void run_n(const uint8_t* base, const Cls4Dev& t, uint32_t* lctr,
+                                      unsigned long long* gslot, uint32_t (&hot)[4],
+                                      const uint32_t (&s)[N], const uint32_t (&d)[N],
+                                      const uint32_t (&dp)[N], const uint32_t (&pr)[N],
+                                      uint32_t (&res)[N]) {
+    uint32_t slot[N];
+    classify_n<N, (kMode & 1), (kMode >> 1)>(base, t, s, d, dp, pr, res, slot);
+    if (t.ablate & 1u) return;
+#pragma unroll
+    for (int q = 0; q < N; ++q) {
+        if (pr[q] <= 2u) {
+            // Hot slots (the allow-all of unmatched sources, default DENY) take
+            // a large share of packets; lanes adding to one LDS address would
+            // serialise, so those are counted in registers and flushed once.
+            const uint32_t m0 = slot[q] == t.hot_slot[0], m1 = slot[q] == t.hot_slot[1];
+            const uint32_t m2 = slot[q] == t.hot_slot[2], m3 = slot[q] == t.hot_slot[3];
+            hot[0] += m0; hot[1] += m1; hot[2] += m2; hot[3] += m3;
+            if (!(m0 | m1 | m2 | m3)) {
+                if constexpr (kLds) atomicAdd(&lctr[slot[q]], 1u);
+                else atomicAdd(&gslot[slot[q]], 1ull);
+            }
+        } else {                       // protocol outside TCP/UDP/ICMP: switch fall-through
+            uint32_t rule;
+            linear_one(t.lin, t.n_lin, t.n_rules, s[q], d[q], dp[q], 3u, res[q], rule);
+            atomicAdd(&gslot[t.n_ctr + rule], 1ull);
+        }
+    }
+}
+
+template <bool kLds, bool kVec, int kMode>
 __global__ __launch_bounds__(kBlock) void classify4_cls(Cls4Dev t, Pkts4 p, uint8_t* verdict,
                                                         unsigned long long* gslot) {
     extern __shared__ uint4 smem[];
@@ -97,52 +263,56 @@ __global__ __launch_bounds__(kBlock) void classify4_cls(Cls4Dev t, Pkts4 p, uint
         base = reinterpret_cast<const uint8_t*>(t.img);
     }
 
-    auto one = [&](uint32_t s, uint32_t d, uint32_t dp, uint32_t pr) -> uint32_t {
-        uint32_t res, slot;
-        if (pr <= 2u) {
-            if constexpr (kLds)
-                cls4_one(reinterpret_cast<const uint8_t*>(smem), t, s, d, dp, pr, res, slot);
-            else
-                cls4_one(base, t, s, d, dp, pr, res, slot);
-            if constexpr (kLds)
-                atomicAdd(&lctr[slot], 1u);
-            else
-                atomicAdd(&gslot[slot], 1ull);
-        } else {
-            uint32_t rule;
-            linear_one(t.lin, t.n_lin, t.n_rules, s, d, dp, 3u, res, rule);
-            atomicAdd(&gslot[t.n_ctr + rule], 1ull);
-        }
-        return res;
-    };
-
     const uint64_t nthreads = uint64_t(gridDim.x) * blockDim.x;
     const uint64_t tid = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    uint32_t hot[4] = {0u, 0u, 0u, 0u};
+    uint64_t tail_from = 0;
     if constexpr (kVec) {
+        // 4 packets per lane per step, next step's loads issued before this
+        // step's lookups (software pipelining of the HBM stream)
         const uint64_t ngroups = p.n / 4u;
-        for (uint64_t g = tid; g < ngroups; g += nthreads) {
-            const uint4 s = reinterpret_cast<const uint4*>(p.src)[g];
-            const uint4 d = reinterpret_cast<const uint4*>(p.dst)[g];
-            const uint2 dp = reinterpret_cast<const uint2*>(p.dport)[g];
-            const uint32_t pr = reinterpret_cast<const uint32_t*>(p.proto)[g];
-            const uint32_t v0 = one(s.x, d.x, dp.x & 0xFFFFu, pr & 0xFFu);
-            const uint32_t v1 = one(s.y, d.y, dp.x >> 16, (pr >> 8) & 0xFFu);
-            const uint32_t v2 = one(s.z, d.z, dp.y & 0xFFFFu, (pr >> 16) & 0xFFu);
-            const uint32_t v3 = one(s.w, d.w, dp.y >> 16, pr >> 24);
-            if (verdict)
-                reinterpret_cast<uint32_t*>(verdict)[g] = v0 | (v1 << 8) | (v2 << 16) | (v3 << 24);
+        const uint4* S = reinterpret_cast<const uint4*>(p.src);
+        const uint4* D = reinterpret_cast<const uint4*>(p.dst);
+        const uint2* DP = reinterpret_cast<const uint2*>(p.dport);
+        const uint32_t* PR = reinterpret_cast<const uint32_t*>(p.proto);
+        uint64_t g = tid;
+        uint4 s = make_uint4(0, 0, 0, 0), d = s;
+        uint2 dp = make_uint2(0, 0);
+        uint32_t pr = 0;
+        if (g < ngroups) { s = S[g]; d = D[g]; dp = DP[g]; pr = PR[g]; }
+        while (g < ngroups) {
+            const uint64_t gn = g + nthreads;
+            uint4 s2 = s, d2 = d;
+            uint2 dp2 = dp;
+            uint32_t pr2 = pr;
+            if (gn < ngroups) { s2 = S[gn]; d2 = D[gn]; dp2 = DP[gn]; pr2 = PR[gn]; }
+            const uint32_t sa[4] = {s.x, s.y, s.z, s.w};
+            const uint32_t da[4] = {d.x, d.y, d.z, d.w};
+            const uint32_t pa[4] = {dp.x & 0xFFFFu, dp.x >> 16, dp.y & 0xFFFFu, dp.y >> 16};
+            const uint32_t ra[4] = {pr & 0xFFu, (pr >> 8) & 0xFFu, (pr >> 16) & 0xFFu, pr >> 24};
+            uint32_t v[4];
+            run_n<4, kLds, kMode>(base, t, lctr, gslot, hot, sa, da, pa, ra, v);
+            if (verdict && !(t.ablate & 8u))
+                reinterpret_cast<uint32_t*>(verdict)[g] = v[0] | (v[1] << 8) | (v[2] << 16) | (v[3] << 24);
+            s = s2; d = d2; dp = dp2; pr = pr2;
+            g = gn;
         }
-        for (uint64_t i = ngroups * 4u + tid; i < p.n; i += nthreads) {
-            const uint32_t v = one(p.src[i], p.dst[i], p.dport[i], p.proto[i]);
-            if (verdict) verdict[i] = uint8_t(v);
-        }
-    } else {
-        for (uint64_t i = tid; i < p.n; i += nthreads) {
-            const uint32_t v = one(p.src[i], p.dst[i], p.dport[i], p.proto[i]);
-            if (verdict) verdict[i] = uint8_t(v);
-        }
+        tail_from = ngroups * 4u;
+    }
+    for (uint64_t i = tail_from + tid; i < p.n; i += nthreads) {
+        const uint32_t sa[1] = {p.src[i]}, da[1] = {p.dst[i]}, pa[1] = {p.dport[i]}, ra[1] = {p.proto[i]};
+        uint32_t v[1];
+        run_n<1, kLds, kMode>(base, t, lctr, gslot, hot, sa, da, pa, ra, v);
+        if (verdict) verdict[i] = uint8_t(v[0]);
     }
 
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+        if (hot[h]) {
+            if constexpr (kLds) atomicAdd(&lctr[t.hot_slot[h]], hot[h]);
+            else atomicAdd(&gslot[t.hot_slot[h]], (unsigned long long)hot[h]);
+        }
+    }
     if constexpr (kLds) {
         __syncthreads();
         for (uint32_t i = threadIdx.x; i < t.n_ctr; i += blockDim.x) {
@@ -313,27 +483,35 @@ __global__ void gen4_kernel(TrafficDev t, uint64_t first, uint64_t n, uint32_t* 
 
 int max_lds_bytes() { return kLdsMax; }
 
+template <bool kLds, bool kVec, int kMode>
+static void launch_cls(const Cls4Dev& t, const Pkts4& p, uint8_t* verdict, unsigned long long* gslot,
+                       const LaunchCfg& cfg) {
+    const size_t lds = kLds ? t.lds_bytes : 0;
+    if (kLds)
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(classify4_cls<kLds, kVec, kMode>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
+    hipLaunchKernelGGL((classify4_cls<kLds, kVec, kMode>), dim3(cfg.grid), dim3(kBlock), lds, cfg.stream,
+                       t, p, verdict, gslot);
+}
+
 hipError_t launch_classify4_cls(const Cls4Dev& t, const Pkts4& p, uint8_t* verdict,
                                 unsigned long long* gslot, bool lds_resident, bool vec,
                                 const LaunchCfg& cfg) {
-    dim3 grid(cfg.grid), block(kBlock);
-    if (lds_resident) {
-        const size_t lds = t.lds_bytes;
-        if (vec) {
-            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(classify4_cls<true, true>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
-            hipLaunchKernelGGL((classify4_cls<true, true>), grid, block, lds, cfg.stream, t, p, verdict, gslot);
-        } else {
-            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(classify4_cls<true, false>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
-            hipLaunchKernelGGL((classify4_cls<true, false>), grid, block, lds, cfg.stream, t, p, verdict, gslot);
-        }
-    } else {
-        if (vec)
-            hipLaunchKernelGGL((classify4_cls<false, true>), grid, block, 0, cfg.stream, t, p, verdict, gslot);
-        else
-            hipLaunchKernelGGL((classify4_cls<false, false>), grid, block, 0, cfg.stream, t, p, verdict, gslot);
+    // variant bits: 1 = hash LPM source lookup, 2 = bit-vector candidate lists
+    const int var = (t.mode == 1 ? 1 : 0) | (t.list_mode == 1 ? 2 : 0);
+#define CLS_DISPATCH(L, V)                                                       \
+    switch (var) {                                                               \
+    case 0: launch_cls<L, V, 0>(t, p, verdict, gslot, cfg); break;               \
+    case 1: launch_cls<L, V, 1>(t, p, verdict, gslot, cfg); break;               \
+    case 2: launch_cls<L, V, 2>(t, p, verdict, gslot, cfg); break;               \
+    default: launch_cls<L, V, 3>(t, p, verdict, gslot, cfg); break;              \
     }
+    if (lds_resident) {
+        if (vec) { CLS_DISPATCH(true, true) } else { CLS_DISPATCH(true, false) }
+    } else {
+        if (vec) { CLS_DISPATCH(false, true) } else { CLS_DISPATCH(false, false) }
+    }
+#undef CLS_DISPATCH
     return hipGetLastError();
 }
 

@@ -27,6 +27,15 @@ struct Cls4Dev {
     const LinRule4* lin;       // linear rules: fallback for protocols outside TCP/UDP/ICMP
     uint32_t n_lin;
     uint32_t n_rules;          // R: direct rule slots start at n_ctr
+    uint32_t mode;             // 0 interval search, 1 hash LPM
+    uint32_t default_class;
+    uint32_t n_hash;
+    uint32_t hash_mask[kMaxHashLens], hash_shift[kMaxHashLens], hash_cap[kMaxHashLens];
+    uint32_t off_hash[kMaxHashLens];
+    uint32_t ablate;           // diagnostics only (CONTIVCLS_ABLATE): skip stages, wrong results
+    uint32_t list_mode;        // 0 template scan, 1 bit vectors
+    uint32_t bv_steps;         // bit-vector search depth (max over lists, both dims)
+    uint32_t hot_slot[4];      // slots counted in registers (0xFFFFFFFF = unused)
 };
 
 struct LaunchCfg {
