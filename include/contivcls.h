@@ -256,8 +256,12 @@ typedef struct cls_image_v4_header {
     uint32_t default_class;    /* hash LPM: class when no hashed prefix matches */
     uint32_t n_hash;           /* hashed prefix lengths (ascending) */
     uint32_t hash_mask[3], hash_shift[3], hash_cap[3], off_hash[3];
-    uint32_t list_mode;        /* candidate lists: 0 template scan, 1 bit vectors */
+    uint32_t list_mode;        /* candidate lists: 0 template scan, 1 bit vectors,
+                                  2 bit vectors with global port classes */
     uint32_t off_bv, bv_steps_d, bv_steps_p;
+    uint32_t off_ptop;         /* list mode 2: port radix (256 x u32, then u8 sub-tables) */
+    uint32_t n_pclass;         /* list mode 2: global port classes */
+    uint32_t bv_wide;          /* some bit-vector list has more than 16 entries */
 } cls_image_v4_header;
 int cls_compile_v4(const cls_rule* rules, uint32_t n_rules, void* blob, uint64_t cap,
                    uint64_t* need);

@@ -121,6 +121,32 @@ def long_list_acl(seed: int, n_rules: int = 300, n_src: int = 3):
     return rules, pool
 
 
+def many_ports_acl(seed: int, n_rules: int = 400, n_src: int = 40, host_src: bool = True):
+    """Short candidate lists over many distinct port ranges: more than 256
+    global port classes, which selects bit vectors with per-list port search
+    (list_mode 1).  host_src: /32 sources (hash LPM), else the pool's mixed
+    prefix lengths (interval search)."""
+    rng = random.Random(seed)
+    pool = PrefixPool(rng, 48)
+    if host_src:
+        srcs = [(a | rng.randint(0, 255) if ln <= 24 else a, 32) for a, ln in pool.v4[:n_src]]
+    else:                                   # 5 lengths, random (rarely nested) prefixes
+        lens = (16, 20, 24, 28, 32)
+        srcs = [(rng.getrandbits(32) & ((0xFFFFFFFF << (32 - lens[i % 5])) & 0xFFFFFFFF), lens[i % 5])
+                for i in range(n_src)]
+        pool.v4 = srcs + pool.v4[n_src:]
+    rules = []
+    for _ in range(n_rules):
+        a, ln = rng.choice(srcs)
+        da, dl = rng.choice(pool.v4[n_src:])
+        proto = rng.choice(["tcp", "udp"])
+        lo = rng.randint(0, 64000)
+        hi = lo + rng.randint(0, 1500)
+        rules.append(M.l4_rule(rng.choice([M.DENY, M.PERMIT, M.REFLECT]), "%s/%d" % (_v4(a), ln),
+                               "%s/%d" % (_v4(da), max(dl, 1)), proto, 0, 65535, lo, hi))
+    return rules, pool
+
+
 def random_traffic(seed: int, n: int, pool: PrefixPool, other_proto: bool = True):
     """IPv4 packets biased towards the prefixes' edges."""
     rng = np.random.default_rng(seed)

@@ -105,6 +105,13 @@ class Image:
         sp = np.full(len(cls), S, np.int64)
         p_off = d_off + 2 * (np.int64(1) << sd)
         res_bits = img[d_off].astype(np.uint64) | (img[p_off].astype(np.uint64) << np.uint64(32))
+        lm2 = self.h.list_mode == 2
+        if lm2:
+            # global port class: top[p >> 8] = sub offset | base << 20
+            b8 = np.frombuffer(self._img, np.uint8)
+            dp = dport.astype(np.int64)
+            tp = img[self.h.off_ptop // 4 + (dp >> 8)].astype(np.int64)
+            pc = (tp >> 20) + b8[(tp & 0xFFFFF) + (dp & 0xFF)].astype(np.int64)
 
         def search(off, steps, x):
             k = np.zeros(len(x), np.int64)
@@ -119,7 +126,10 @@ class Image:
             return m
 
         md = search(d_off, sd, dst.astype(np.uint32))
-        mp = search(p_off, sp, dport.astype(np.uint32))
+        if lm2:
+            mp = img[p_off + 1 + pc]
+        else:
+            mp = search(p_off, sp, dport.astype(np.uint32))
         m = (md & mp).astype(np.uint64)
         found = (m != 0) & (proto <= 2)
         low = m & (~m + np.uint64(1))
@@ -168,7 +178,7 @@ class Image:
             np.add.at(counters, rule, 1)
             return res.astype(np.uint8), counters
         cls = self.source_class(src)
-        if self.h.list_mode == 1:
+        if self.h.list_mode >= 1:
             return self._classify_bv(cls, src, dst, dport, proto, counters)
         pr = np.minimum(proto, 2).astype(np.int64)
         cell = self.cells[cls * 3 + pr]

@@ -63,6 +63,41 @@ def test_long_candidate_lists_use_scan_mode(seed):
     assert img.has_cls and img.h.list_mode == 0
 
 
+@pytest.mark.parametrize("seed", range(4))
+@pytest.mark.parametrize("host_src", [True, False])
+def test_many_port_ranges_use_per_list_port_search(seed, host_src):
+    """> 256 global port classes: bit vectors with per-list port search
+    (list_mode 1); few port ranges: global port classes (list_mode 2)."""
+    from aclgen import many_ports_acl
+    rules, pool = many_ports_acl(seed + 900, 400, 40, host_src=host_src)
+    img = _check(rules, random_traffic(seed, 6000, pool))
+    assert img.has_cls and img.h.list_mode == 1
+    assert img.h.mode == (1 if host_src else 0)
+    rules, pool = random_acl(seed + 77, 150, 0.0)
+    img = _check(rules, random_traffic(seed, 6000, pool))
+    assert img.has_cls and img.h.list_mode == 2 and img.h.n_pclass <= 256
+
+
+def test_port_class_radix_edges():
+    """Port classes at chunk edges (255/256, 65535) and ranges inside one
+    256-port chunk: every port of every boundary checked against the oracle."""
+    from vpp_amd import model as M
+    edges = [(0, 0), (255, 256), (256, 511), (300, 300), (301, 302), (1023, 1024),
+             (65534, 65535), (65535, 65535), (80, 80), (8080, 8081)]
+    rules = [M.l4_rule(M.PERMIT if i % 2 else M.REFLECT, "10.0.%d.0/24" % i, "", "tcp", 0, 65535,
+                       lo, hi) for i, (lo, hi) in enumerate(edges)]
+    rules += [M.l4_rule(M.DENY, "10.0.0.0/16", "", "udp", 0, 65535, lo, hi) for lo, hi in edges]
+    ports = sorted({x for lo, hi in edges for x in (lo - 1, lo, hi, hi + 1) if 0 <= x <= 65535})
+    n = len(ports) * 40
+    rng = np.random.default_rng(5)
+    tr = dict(src=(np.uint32(0x0A000000) + rng.integers(0, 12 << 8, n)).astype(np.uint32),
+              dst=rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32),
+              dport=np.tile(np.array(ports, np.uint16), 40),
+              proto=rng.choice(np.array([0, 1, 2], np.uint8), n))
+    img = _check(rules, tr)
+    assert img.h.list_mode == 2
+
+
 def test_compiler_uses_classifier_for_larger_tables():
     rules, pool = random_acl(7, 120, 0.0)
     img = _check(rules, random_traffic(7, 2000, pool))

@@ -69,20 +69,32 @@ def test_random_acls_both_kernels(eng, seed, n_rules, weird):
     _assert_same(_gpu(eng, rules, tr, force_linear=True), want)
 
 
+VARIANTS = {  # kind -> (source lookup mode, list mode)
+    "hash_pc": (1, 2), "search_pc": (0, 2), "hash_bv": (1, 1), "search_bv": (0, 1),
+    "hash_scan": (1, 0), "search_scan": (0, 0)}
+
+
+def variant_acl(kind, seed):
+    from aclgen import long_list_acl, many_ports_acl
+    hashed = kind.startswith("hash")
+    if kind.endswith("scan"):
+        return long_list_acl(seed + 70, 300, n_src=3 if hashed else 30)
+    if kind.endswith("_bv"):
+        return many_ports_acl(seed + 5, 400, 40, host_src=hashed)
+    return random_acl(seed * 31 + 7, 120, 0.0, n_prefixes=4 if hashed else 24)
+
+
 @pytest.mark.parametrize("seed", range(3))
-@pytest.mark.parametrize("kind", ["hash_bv", "search_bv", "hash_scan", "search_scan"])
+@pytest.mark.parametrize("kind", sorted(VARIANTS))
 def test_all_kernel_variants(eng, seed, kind):
-    """The four classifier variants (hash-LPM / interval-search source lookup
-    x bit-vector / template-scan candidate lists) against the oracle."""
-    from aclgen import long_list_acl
+    """The six classifier variants (hash-LPM / interval-search source lookup
+    x bit vectors with global port classes / bit vectors with per-list port
+    search / template scan) against the oracle."""
     from cls_image import Image, compile_blob
     from vpp_amd import _abi
-    if kind.endswith("scan"):
-        rules, pool = long_list_acl(seed + 70, 300, n_src=3 if kind.startswith("hash") else 30)
-    else:
-        rules, pool = random_acl(seed * 31 + 7, 120, 0.0, n_prefixes=4 if kind.startswith("hash") else 24)
+    rules, pool = variant_acl(kind, seed)
     h = Image(compile_blob(_abi.CRules(rules))).h
-    assert (h.mode, h.list_mode) == (int(kind.startswith("hash")), int(kind.endswith("bv"))), kind
+    assert (h.mode, h.list_mode) == VARIANTS[kind], kind
     tr = random_traffic(seed + 11, 30000, pool)
     _assert_same(_gpu(eng, rules, tr), _oracle(rules, tr))
 

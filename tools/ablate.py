@@ -24,7 +24,8 @@ def main():
     eng.gen_traffic_v4(spec, 0, pk)
     verdict = torch.empty(n, dtype=torch.uint8, device="cuda")
     counters = torch.zeros(t.n_rules + 1, dtype=torch.int64, device="cuda")
-    for ab in [0, 1, 2, 3, 4, 6, 7, 15]:
+    abl = [int(x) for x in os.environ.get("ABL", "0,1,2,3,4,6,7,15").split(",")]
+    for ab in abl:
         os.environ["CONTIVCLS_ABLATE"] = str(ab)
         for _ in range(2):
             eng.classify(t, pk["src"], pk["dst"], pk["dport"], pk["proto"], verdict=verdict, counters=counters)
@@ -37,5 +38,20 @@ def main():
     os.environ.pop("CONTIVCLS_ABLATE")
 
 
+def ab_libs():
+    """tools/ablate.py CFG lib1.so lib2.so ...: A/B the kernel build variants
+    (vpp_amd/csrc/Makefile `variant`), one child process per library."""
+    import subprocess
+    for so in sys.argv[2:]:
+        print("==", so, flush=True)
+        env = dict(os.environ, CONTIVCLS_LIB=os.path.abspath(so))
+        r = subprocess.run([sys.executable, os.path.abspath(__file__), sys.argv[1]], env=env)
+        if r.returncode:
+            sys.exit(r.returncode)
+
+
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 2:
+        ab_libs()
+    else:
+        main()

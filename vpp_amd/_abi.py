@@ -11,7 +11,8 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libcontivcls.so")
+# CONTIVCLS_LIB: diagnostics only (A/B timing of kernel build variants)
+LIB_PATH = os.environ.get("CONTIVCLS_LIB") or os.path.join(_HERE, "libcontivcls.so")
 
 # status codes
 OK, E_INVAL, E_NOMEM, E_HIP, E_RCCL, E_NOTFOUND, E_NODEV = 0, -1, -2, -3, -4, -5, -6
@@ -81,7 +82,8 @@ class ImageHeader(C.Structure):
         ("hash_mask", C.c_uint32 * 3), ("hash_shift", C.c_uint32 * 3),
         ("hash_cap", C.c_uint32 * 3), ("off_hash", C.c_uint32 * 3),
         ("list_mode", C.c_uint32), ("off_bv", C.c_uint32), ("bv_steps_d", C.c_uint32),
-        ("bv_steps_p", C.c_uint32)]
+        ("bv_steps_p", C.c_uint32), ("off_ptop", C.c_uint32), ("n_pclass", C.c_uint32),
+        ("bv_wide", C.c_uint32)]
 
 
 _lib = None

@@ -331,6 +331,85 @@ BvDesc build_bv(const std::vector<TmplKey>& ents, uint32_t S, std::vector<uint32
     return desc;
 }
 
+// Global port classes (list mode 2): the elementary intervals of the port
+// ranges of every bit-vector list, G = sorted interval starts (G[0] = 0).
+std::vector<uint32_t> port_classes(const std::vector<std::vector<TmplKey>>& lists) {
+    std::vector<uint32_t> g{0};
+    for (const auto& ents : lists)
+        for (const TmplKey& t : ents) {
+            const uint32_t lo = t.pw & 0xFFFFu, hi = lo + (t.pw >> 16);
+            g.push_back(lo);
+            if (hi < 0xFFFFu) g.push_back(hi + 1);
+        }
+    std::sort(g.begin(), g.end());
+    g.erase(std::unique(g.begin(), g.end()), g.end());
+    return g;
+}
+
+// Block of one list in mode 2, appended to `out` (8-B aligned):
+//   dst array: 2^Sd x {interval start, mask} as in mode 1 (entry 0 = {result
+//              bits lo, mask of interval 0}),
+//   result bits hi (u32), then one mask per global port class (u32 x P),
+//   padded so the block is an odd number of 8-B units: lanes probing the same
+//   step of different lists then spread over all LDS bank pairs.
+BvDesc build_bv2(const std::vector<TmplKey>& ents, uint32_t Sd, const std::vector<uint32_t>& G,
+                 std::vector<uint32_t>& out) {
+    const size_t k = ents.size();
+    std::vector<uint32_t> db, pb;
+    bv_bounds(ents, db, pb);
+    uint64_t res = 0;
+    for (size_t j = 0; j < k; ++j) res |= uint64_t(ents[j].res & 3u) << (2 * j);
+    const size_t start = out.size();
+    const BvDesc desc{uint32_t(start) * 4, res};
+    uint32_t last = 0;
+    for (size_t i = 0; i < (size_t(1) << Sd); ++i) {
+        if (i < db.size()) {
+            const uint32_t x = db[i];
+            uint32_t m = 0;
+            for (size_t j = 0; j < k; ++j)
+                if (((x ^ ents[j].a) & ents[j].m) == 0) m |= 1u << j;
+            last = m;
+            out.push_back(i == 0 ? uint32_t(res) : x);
+        } else {
+            out.push_back(0xFFFFFFFFu);
+        }
+        out.push_back(last);
+    }
+    out.push_back(uint32_t(res >> 32));
+    for (uint32_t x : G) {
+        uint32_t m = 0;
+        for (size_t j = 0; j < k; ++j) {
+            const uint32_t lo = ents[j].pw & 0xFFFFu, hi = lo + (ents[j].pw >> 16);
+            if (x >= lo && x <= hi) m |= 1u << j;
+        }
+        out.push_back(m);
+    }
+    if ((out.size() - start) % 2) out.push_back(0u);
+    if (((out.size() - start) / 2) % 2 == 0) { out.push_back(0u); out.push_back(0u); }
+    return desc;
+}
+
+// Port -> class radix of mode 2: top[p >> 8] = sub-table byte offset (20 bits,
+// relative to the radix section) | base class << 20; class = base + sub[p & 255].
+// A 256-port chunk inside one class points at the shared all-zero sub-table.
+void port_radix(const std::vector<uint32_t>& G, std::vector<uint32_t>& top,
+                std::vector<uint8_t>& subs) {
+    top.assign(256, 0);
+    subs.assign(256, 0);                                   // sub-table 0: all zero
+    auto cls_of = [&](uint32_t p) {
+        return uint32_t(std::upper_bound(G.begin(), G.end(), p) - G.begin()) - 1u;
+    };
+    for (uint32_t h = 0; h < 256; ++h) {
+        const uint32_t c0 = cls_of(h << 8), c1 = cls_of((h << 8) | 255u);
+        uint32_t off = 0;
+        if (c1 != c0) {
+            off = uint32_t(subs.size());
+            for (uint32_t x = 0; x < 256; ++x) subs.push_back(uint8_t(cls_of((h << 8) | x) - c0));
+        }
+        top[h] = off | (c0 << 20);
+    }
+}
+
 }  // namespace
 
 bool build_cls4(const std::vector<SemRule>& sem, uint32_t n_rules, Cls4Image& img,
@@ -454,8 +533,22 @@ bool build_cls4(const std::vector<SemRule>& sem, uint32_t n_rules, Cls4Image& im
     std::vector<uint16_t> lists;
     std::vector<uint32_t> cells(size_t(n_classes) * 3 * 2);
     img.ctr_rule.assign(1, n_rules);  // slot 0: default DENY
+    // Hot class: the one covering most of the address space (random sources
+    // land there).  Its cells take the slots right after slot 0, so the
+    // kernel can tell the heavily hit slots by `slot < n_hot` and count them
+    // in per-lane LDS rows instead of one contended word.
+    uint32_t hot_class = 0;
+    {
+        std::vector<double> span(n_classes, 0.0);
+        for (uint32_t k = 0; k < n_real_bounds; ++k) {
+            const double hi = k + 1 < n_real_bounds ? double(bounds[k + 1]) : 4294967296.0;
+            span[iclass[k]] += hi - double(bounds[k]);
+        }
+        hot_class = uint32_t(std::max_element(span.begin(), span.end()) - span.begin());
+    }
     std::vector<uint32_t> cand;
-    for (uint32_t c = 0; c < n_classes; ++c) {
+    for (uint32_t ci = 0; ci < n_classes; ++ci) {
+        const uint32_t c = ci == 0 ? hot_class : (ci <= hot_class ? ci - 1 : ci);
         // merge candidate rule positions: chain of covering prefixes + ANY
         cand.clear();
         for (int p = class_pfx[c]; p >= 0; p = parent[p])
@@ -504,6 +597,7 @@ bool build_cls4(const std::vector<SemRule>& sem, uint32_t n_rules, Cls4Image& im
             cells[(size_t(c) * 3 + pr) * 2 + 0] = start | (uint32_t(seq.size()) << 16);
             cells[(size_t(c) * 3 + pr) * 2 + 1] = ctr_base;
         }
+        if (ci == 0) img.n_hot = std::min<uint32_t>(uint32_t(img.ctr_rule.size()), kMaxHot);
     }
 
     // the scan kernel reads list/template entries speculatively (clamped
@@ -517,7 +611,6 @@ bool build_cls4(const std::vector<SemRule>& sem, uint32_t n_rules, Cls4Image& im
     std::vector<uint32_t> bv;
     std::unordered_map<uint32_t, BvDesc> bv_desc;        // list (start | len << 16) -> arrays
     bool all_bv = true;
-    uint32_t S = 0;                                       // table-wide search depth
     std::vector<uint32_t> bv_lists;                       // distinct cell list keys
     for (uint32_t c = 0; c < n_classes && all_bv; ++c)
         for (int pr = 0; pr < 3; ++pr) {
@@ -532,106 +625,125 @@ bool build_cls4(const std::vector<SemRule>& sem, uint32_t n_rules, Cls4Image& im
         for (uint32_t j = 0; j < (x >> 16); ++j) ents.push_back(tmpls[lists[(x & 0xFFFFu) + j]]);
         return ents;
     };
+    // list mode: 2 = bit vectors with global port classes, 1 = bit vectors
+    // with per-list port search, 0 = template scan; the fastest mode whose
+    // image fits the workgroup's LDS (and the 16-bit cell fields) is chosen
+    std::vector<std::vector<TmplKey>> bv_ents;
+    uint32_t Sd = 0, Sp = 0;
+    std::vector<uint32_t> G, ptop;
+    std::vector<uint8_t> psub;
+    if (img.ctr_rule.size() > 0xFFFFu) all_bv = false;    // counter base: 16-bit cell field
     if (all_bv) {
         for (uint32_t x : bv_lists) {
+            bv_ents.push_back(ents_of(x));
             std::vector<uint32_t> db, pb;
-            bv_bounds(ents_of(x), db, pb);
-            const size_t need = std::max(db.size(), pb.size());
-            while ((size_t(1) << S) < need) ++S;
+            bv_bounds(bv_ents.back(), db, pb);
+            while ((size_t(1) << Sd) < db.size()) ++Sd;
+            while ((size_t(1) << Sp) < pb.size()) ++Sp;
         }
-        for (uint32_t x : bv_lists) bv_desc[x] = build_bv(ents_of(x), S, bv);
-        // 16-bit fields of the u32 cell: array offset / 8 and counter base
-        const size_t worst = (bounds.size() * 3 + cells.size() + bv.size() + 64) * 4;
-        if (img.ctr_rule.size() > 0xFFFFu || worst / 8 > 0xFFFFu) {
-            all_bv = false;
-            bv.clear();
-            bv_desc.clear();
-        }
+        G = port_classes(bv_ents);
+        port_radix(G, ptop, psub);
     }
-    const uint32_t max_sd = S, max_sp = S;
-    // Hot slots: the first entry of each cell of the class covering most of the
-    // address space (random sources land there), and slot 0 (default DENY).
-    {
-        std::vector<double> span(n_classes, 0.0);
-        for (uint32_t k = 0; k < n_real_bounds; ++k) {
-            const double hi = k + 1 < n_real_bounds ? double(bounds[k + 1]) : 4294967296.0;
-            span[iclass[k]] += hi - double(bounds[k]);
-        }
-        const uint32_t dc = uint32_t(std::max_element(span.begin(), span.end()) - span.begin());
-        uint32_t hot[4] = {0u, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
-        for (int pr = 0; pr < 3; ++pr) {
-            const uint32_t x = cells[(size_t(dc) * 3 + pr) * 2], base = cells[(size_t(dc) * 3 + pr) * 2 + 1];
-            if ((x >> 16) == 0) continue;            // empty list: no slot of its own
-            hot[pr + 1] = base;                      // slots are distinct per (cell, position)
-        }
-        for (int i = 0; i < 4; ++i) img.hot_slot[i] = hot[i];
-    }
-    img.list_mode = all_bv ? 1u : 0u;
-    img.bv_steps_d = max_sd;
-    img.bv_steps_p = max_sp;
+    uint32_t lmode = 0;
+    if (all_bv && Sd <= kMaxBvSteps && G.size() <= kMaxPortClasses) lmode = 2;
+    else if (all_bv && std::max(Sd, Sp) <= kMaxBvSteps) lmode = 1;
 
-    // serialise (u32 words, each section 16 B aligned); sections the chosen
-    // modes never read are left out of the LDS image
     std::vector<uint32_t>& w = img.words;
-    if (img.mode == 0) {
-        img.off_bounds = 0;
-        w.insert(w.end(), bounds.begin(), bounds.end());
-        w.resize(align4(uint32_t(w.size())));
-        img.off_iclass = uint32_t(w.size()) * 4;
-        w.resize(w.size() + (bounds.size() + 1) / 2);
-        std::memcpy(reinterpret_cast<uint8_t*>(w.data()) + img.off_iclass, iclass.data(), iclass.size() * 2);
-        w.resize(align4(uint32_t(w.size())));
-    }
-    img.off_cells = uint32_t(w.size()) * 4;
-    if (img.list_mode == 0) {
-        // scan cells: uint2 {list start | len << 16, counter base}
-        w.insert(w.end(), cells.begin(), cells.end());
-        w.resize(align4(uint32_t(w.size())));
-        img.off_lists = uint32_t(w.size()) * 4;
-        const size_t lbase = w.size();
-        w.resize(lbase + (lists.size() + 1) / 2);
-        std::memcpy(reinterpret_cast<uint8_t*>(w.data() + lbase), lists.data(), lists.size() * 2);
-        w.resize(align4(uint32_t(w.size())));
-        img.off_tmpl = uint32_t(w.size()) * 4;
-        for (const auto& t : tmpls) {
-            w.push_back(t.a);
-            w.push_back(t.m);
-            w.push_back(t.pw);
-            w.push_back(t.res);
+    auto serialise = [&](uint32_t lm) {
+        // lists
+        bv.clear();
+        bv_desc.clear();
+        const uint32_t S = std::max(Sd, Sp);
+        for (size_t i = 0; i < bv_lists.size(); ++i) {
+            if (lm == 2) bv_desc[bv_lists[i]] = build_bv2(bv_ents[i], Sd, G, bv);
+            else if (lm == 1) bv_desc[bv_lists[i]] = build_bv(bv_ents[i], S, bv);
         }
-        w.resize(align4(uint32_t(w.size())));
-    } else {
-        // bit-vector cells: u32 {dst array offset / 8 | counter base << 16}
-        // (port array = dst array + 2^S entries; result bits in entry 0 of
-        // both arrays)
-        const size_t n_cells = size_t(n_classes) * 3;
-        const uint32_t off_bv = uint32_t(align4(uint32_t(w.size() + n_cells))) * 4;
-        img.off_bv = off_bv;
-        for (size_t i = 0; i < n_cells; ++i) {
-            const BvDesc& d = bv_desc.at(cells[2 * i]);
-            const uint32_t off = off_bv + d.off_rel;
-            w.push_back((off / 8) | (cells[2 * i + 1] << 16));
+        img.list_mode = lm;
+        img.bv_steps_d = lm == 2 ? Sd : S;
+        img.bv_steps_p = lm == 2 ? 0u : S;
+        img.n_pclass = lm == 2 ? uint32_t(G.size()) : 0u;
+        img.bv_wide = 0;
+        for (const auto& e : bv_ents) img.bv_wide |= e.size() > 16 ? 1u : 0u;
+        // serialise (u32 words, each section 16 B aligned); sections the chosen
+        // modes never read are left out of the LDS image
+        w.clear();
+        img.off_bounds = img.off_iclass = img.off_lists = img.off_tmpl = img.off_bv = img.off_ptop = 0;
+        if (img.mode == 0) {
+            img.off_bounds = 0;
+            w.insert(w.end(), bounds.begin(), bounds.end());
+            w.resize(align4(uint32_t(w.size())));
+            img.off_iclass = uint32_t(w.size()) * 4;
+            w.resize(w.size() + (bounds.size() + 1) / 2);
+            std::memcpy(reinterpret_cast<uint8_t*>(w.data()) + img.off_iclass, iclass.data(), iclass.size() * 2);
+            w.resize(align4(uint32_t(w.size())));
         }
-        w.resize(align4(uint32_t(w.size())));
-        w.insert(w.end(), bv.begin(), bv.end());
-        w.resize(align4(uint32_t(w.size())));
-    }
-    for (uint32_t i = 0; i < img.n_hash; ++i) {
-        img.off_hash[i] = uint32_t(w.size()) * 4;
-        for (uint64_t e : hash_tabs[i]) {
-            w.push_back(uint32_t(e));
-            w.push_back(uint32_t(e >> 32));
+        img.off_cells = uint32_t(w.size()) * 4;
+        if (lm == 0) {
+            // scan cells: uint2 {list start | len << 16, counter base}
+            w.insert(w.end(), cells.begin(), cells.end());
+            w.resize(align4(uint32_t(w.size())));
+            img.off_lists = uint32_t(w.size()) * 4;
+            const size_t lbase = w.size();
+            w.resize(lbase + (lists.size() + 1) / 2);
+            std::memcpy(reinterpret_cast<uint8_t*>(w.data() + lbase), lists.data(), lists.size() * 2);
+            w.resize(align4(uint32_t(w.size())));
+            img.off_tmpl = uint32_t(w.size()) * 4;
+            for (const auto& t : tmpls) {
+                w.push_back(t.a);
+                w.push_back(t.m);
+                w.push_back(t.pw);
+                w.push_back(t.res);
+            }
+            w.resize(align4(uint32_t(w.size())));
+        } else {
+            // bit-vector cells: u32 {list block offset / 8 | counter base << 16}
+            const size_t n_cells = size_t(n_classes) * 3;
+            const uint32_t off_bv = uint32_t(align4(uint32_t(w.size() + n_cells))) * 4;
+            img.off_bv = off_bv;
+            for (size_t i = 0; i < n_cells; ++i) {
+                const BvDesc& d = bv_desc.at(cells[2 * i]);
+                const uint32_t off = off_bv + d.off_rel;
+                w.push_back((off / 8) | (cells[2 * i + 1] << 16));
+            }
+            w.resize(align4(uint32_t(w.size())));
+            w.insert(w.end(), bv.begin(), bv.end());
+            w.resize(align4(uint32_t(w.size())));
+            if (lm == 2) {
+                // port radix: top (256 x u32), then the u8 sub-tables
+                img.off_ptop = uint32_t(w.size()) * 4;
+                const uint32_t sub0 = img.off_ptop + 256u * 4u;
+                for (uint32_t x : ptop) w.push_back(((x & 0xFFFFFu) + sub0) | (x & ~0xFFFFFu));
+                const size_t sbase = w.size();
+                w.resize(sbase + (psub.size() + 3) / 4);
+                std::memcpy(reinterpret_cast<uint8_t*>(w.data() + sbase), psub.data(), psub.size());
+                w.resize(align4(uint32_t(w.size())));
+            }
         }
-        w.resize(align4(uint32_t(w.size())));
+        for (uint32_t i = 0; i < img.n_hash; ++i) {
+            img.off_hash[i] = uint32_t(w.size()) * 4;
+            for (uint64_t e : hash_tabs[i]) {
+                w.push_back(uint32_t(e));
+                w.push_back(uint32_t(e >> 32));
+            }
+            w.resize(align4(uint32_t(w.size())));
+        }
+        img.img_bytes = uint32_t(w.size()) * 4;
+        img.n_bounds = n_real_bounds;
+        img.n_classes = n_classes;
+        img.n_tmpl = uint32_t(tmpls.size());
+        img.n_list_entries = uint32_t(lists.size());
+        img.n_ctr = uint32_t(img.ctr_rule.size());
+        img.search_top = top;
+        img.off_hot = img.img_bytes + ((img.n_ctr * 4 + 15u) & ~15u);
+        img.lds_bytes = img.off_hot + img.n_hot * 64u * 4u;
+    };
+    for (;;) {
+        serialise(lmode);
+        if (lmode == 0) break;
+        const bool cell_ok = img.img_bytes / 8u <= 0xFFFFu;   // 16-bit block offset field
+        if (cell_ok && (lmode == 1 || img.lds_bytes <= kLdsBudget)) break;
+        lmode = (lmode == 2 && std::max(Sd, Sp) <= kMaxBvSteps) ? 1u : 0u;
     }
-    img.img_bytes = uint32_t(w.size()) * 4;
-    img.n_bounds = n_real_bounds;
-    img.n_classes = n_classes;
-    img.n_tmpl = uint32_t(tmpls.size());
-    img.n_list_entries = uint32_t(lists.size());
-    img.n_ctr = uint32_t(img.ctr_rule.size());
-    img.search_top = top;
-    img.lds_bytes = img.img_bytes + ((img.n_ctr * 4 + 15u) & ~15u);
     return true;
 }
 

@@ -38,6 +38,10 @@ namespace cls {
 
 // Cuckoo hash pair of the hash-LPM source lookup (shared by compiler and kernel).
 constexpr uint32_t kMaxHashLens = 3;
+constexpr uint32_t kMaxHot = 16;       // hot slots counted in per-lane LDS rows
+constexpr uint32_t kMaxBvSteps = 7;    // bit-vector search depth (lists <= 32 entries)
+constexpr uint32_t kMaxPortClasses = 256;  // list mode 2: global port classes
+constexpr uint32_t kLdsBudget = 160 * 1024;  // LDS of one classify workgroup
 __host__ __device__ inline uint32_t lpm_h0(uint32_t k, uint32_t shift) {
     return (k * 0x9E3779B1u) >> shift;
 }
@@ -106,13 +110,18 @@ struct Cls4Image {
     uint32_t n_hash = 0;           // hashed prefix lengths, ascending
     uint32_t hash_mask[kMaxHashLens] = {}, hash_shift[kMaxHashLens] = {};
     uint32_t hash_cap[kMaxHashLens] = {}, off_hash[kMaxHashLens] = {};
-    // candidate lists: mode 0 = scan of template ids, 1 = bit vectors (all lists <= 32)
+    // candidate lists: mode 0 = scan of template ids, 1 = bit vectors (all lists
+    // <= 32) with per-list port search, 2 = bit vectors with global port classes
     uint32_t list_mode = 0;
     uint32_t off_bv = 0;
     uint32_t bv_steps_d = 0, bv_steps_p = 0;   // largest search depths over the lists
-    // slots expected to take most hits (first entry of each cell of the
-    // default source class, default DENY): counted in registers, not LDS
-    uint32_t hot_slot[4] = {0, 0, 0, 0};
+    // list mode 2: global port classes (radix at off_ptop), result-hi word used
+    uint32_t off_ptop = 0, n_pclass = 0, bv_wide = 0;
+    // slots [0, n_hot) -- default DENY and the cells of the class covering
+    // most of the address space -- are counted in per-lane LDS rows
+    // (n_hot x 64 u32 at off_hot, after the slot counters)
+    uint32_t n_hot = 1;
+    uint32_t off_hot = 0;
 };
 
 // Build the image; returns false (with reason) if the table does not fit the

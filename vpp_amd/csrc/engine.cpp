@@ -310,8 +310,11 @@ int cls_classify(cls_engine* e, uint32_t table_id, const cls_pkt_soa* pk, uint64
             cd.default_class = t->img.default_class;
             cd.n_hash = t->img.n_hash;
             cd.list_mode = t->img.list_mode;
-            cd.bv_steps = std::max(t->img.bv_steps_d, t->img.bv_steps_p);
-            for (int i = 0; i < 4; ++i) cd.hot_slot[i] = t->img.hot_slot[i];
+            cd.bv_steps = std::max(t->img.bv_steps_d, t->img.bv_steps_p);  // mode 2: Sd
+            cd.n_hot = t->img.n_hot;
+            cd.off_ptop = t->img.off_ptop;
+            cd.bv_wide = t->img.bv_wide;
+            cd.off_hot = t->img.off_hot;
             for (uint32_t i = 0; i < kMaxHashLens; ++i) {
                 cd.hash_mask[i] = t->img.hash_mask[i];
                 cd.hash_shift[i] = t->img.hash_shift[i];
@@ -610,6 +613,9 @@ int cls_compile_v4(const cls_rule* rules, uint32_t n, void* blob, uint64_t cap, 
         h.off_bv = img.off_bv;
         h.bv_steps_d = img.bv_steps_d;
         h.bv_steps_p = img.bv_steps_p;
+        h.off_ptop = img.off_ptop;
+        h.n_pclass = img.n_pclass;
+        h.bv_wide = img.bv_wide;
         for (uint32_t i = 0; i < kMaxHashLens; ++i) {
             h.hash_mask[i] = img.hash_mask[i];
             h.hash_shift[i] = img.hash_shift[i];

@@ -60,8 +60,13 @@ __device__ __forceinline__ void src_class(const uint8_t* base, const Cls4Dev& t,
         // the longest hit wins
 #pragma unroll
         for (int q = 0; q < N; ++q) cls[q] = t.default_class;
-#pragma unroll 1
-        for (uint32_t i = 0; i < t.n_hash; ++i) {
+        // Constant indices into the kernel arguments: the parameters are loaded
+        // into SGPRs once, outside the packet loop.  (A runtime index would
+        // re-issue s_load + s_waitcnt lgkmcnt(0) every step, which also drains
+        // the previous step's LDS counter atomics.)
+#pragma unroll
+        for (uint32_t i = 0; i < kMaxHashLens; ++i) {
+            if (i >= t.n_hash) break;
             const uint2* __restrict__ tab = reinterpret_cast<const uint2*>(base + t.off_hash[i]);
             const uint32_t mask = t.hash_mask[i], shift = t.hash_shift[i], cap = t.hash_cap[i];
             uint2 e0[N], e1[N];
@@ -75,10 +80,9 @@ __device__ __forceinline__ void src_class(const uint8_t* base, const Cls4Dev& t,
 #pragma unroll
             for (int q = 0; q < N; ++q) {
                 // empty slots hold keys that never probe them: a key compare is
-                // the whole hit test; bit selects keep it branch-free
-                const uint32_t m0 = 0u - uint32_t(e0[q].x == key[q]);
-                const uint32_t m1 = 0u - uint32_t(e1[q].x == key[q]) & ~m0;
-                cls[q] = (e0[q].y & m0) | (e1[q].y & m1) | (cls[q] & ~(m0 | m1));
+                // the whole hit test (two compares, two selects)
+                cls[q] = e1[q].x == key[q] ? e1[q].y : cls[q];
+                cls[q] = e0[q].x == key[q] ? e0[q].y : cls[q];
             }
         }
     } else {
@@ -110,6 +114,18 @@ __device__ __forceinline__ void classify_n(const uint8_t* base, const Cls4Dev& t
                                            const uint32_t (&src)[N], const uint32_t (&dst)[N],
                                            const uint32_t (&dport)[N], const uint32_t (&proto)[N],
                                            uint32_t (&res)[N], uint32_t (&slot)[N]) {
+    uint32_t pc[N];
+    if constexpr (kList == 2) {
+        // global port class (list mode 2): top[port >> 8] = sub-table offset |
+        // base class << 20, class = base + sub[port & 255].  Independent of the
+        // source lookup: these reads go out together with the hash probes.
+        const uint32_t* __restrict__ ptop = reinterpret_cast<const uint32_t*>(base + t.off_ptop);
+        uint32_t tp[N];
+#pragma unroll
+        for (int q = 0; q < N; ++q) tp[q] = ptop[dport[q] >> 8];
+#pragma unroll
+        for (int q = 0; q < N; ++q) pc[q] = (tp[q] >> 20) + base[(tp[q] & 0xFFFFFu) + (dport[q] & 0xFFu)];
+    }
     uint32_t cls[N];
     if (t.ablate & 4u) {
 #pragma unroll
@@ -118,60 +134,79 @@ __device__ __forceinline__ void classify_n(const uint8_t* base, const Cls4Dev& t
         src_class<N, kMode>(base, t, src, cls);
     }
     const uint2* __restrict__ cells = reinterpret_cast<const uint2*>(base + t.off_cells);
-    if constexpr (kList == 1) {
+    if constexpr (kList >= 1) {
         // Bit vectors: the entries of the cell's list that cover the packet's
         // dst interval AND its port interval; the first such entry (lowest
         // set bit) is the first match of the ordered list.  Both interval
-        // searches are branch-free and run t.bv_steps steps for every lane.
-        // cell = dst array offset / 8 | counter base << 16; entry 0 of the dst
-        // and port arrays = {result bits lo / hi, mask of interval 0}
+        // searches are branch-free, t.bv_steps steps for every lane, and
+        // track the byte address of the current interval: the step sizes
+        // are compile-time constants (unrolled, uniform guard), so a probe
+        // is one ds_read_b64 {bound, mask} with an immediate offset (b64 and
+        // b32 reads cost the same LDS cycles on gfx950: 2 x 32 lanes).
+        // cell = dst array offset / 8 | counter base << 16; an array is 2^S
+        // {bound, mask} pairs, the port array follows the dst array; the bound
+        // word of entry 0 (never probed) holds the result bits, lo / hi
         const uint32_t* __restrict__ cells1 = reinterpret_cast<const uint32_t*>(base + t.off_cells);
-        uint32_t cb[N], rlo[N], rhi[N];
-        uint32_t kd[N], kp[N], md[N], mp[N];
-        const uint2* DA[N];
-        const uint2* PA[N];
-        const uint32_t S = t.bv_steps;       // table-wide depth: one uniform step size
+        const uint32_t S = t.bv_steps;
+        uint32_t cb[N], ad[N], ap[N], rlo[N], rhi[N], md[N], mp[N];
 #pragma unroll
         for (int q = 0; q < N; ++q) {
-            const uint32_t pp = proto[q] <= 2u ? proto[q] : 0u;
-            const uint32_t cell = cells1[cls[q] * 3u + pp];
+            const uint32_t cell = cells1[cls[q] * 3u + min(proto[q], 2u)];
             cb[q] = cell >> 16;
-            DA[q] = reinterpret_cast<const uint2*>(base + (cell & 0xFFFFu) * 8u);
-            PA[q] = DA[q] + (1u << S);
+            ad[q] = (cell & 0xFFFFu) * 8u;
+            ap[q] = ad[q] + (8u << S);
         }
+        if constexpr (kList == 1) {
 #pragma unroll
-        for (int q = 0; q < N; ++q) {
-            const uint2 d0 = DA[q][0], p0 = PA[q][0];
-            rlo[q] = d0.x;
-            rhi[q] = p0.x;
-            md[q] = d0.y;
-            mp[q] = p0.y;
-            kd[q] = 0u;
-            kp[q] = 0u;
+            for (int q = 0; q < N; ++q) {
+                const uint2 d0 = *reinterpret_cast<const uint2*>(base + ad[q]);
+                const uint2 p0 = *reinterpret_cast<const uint2*>(base + ap[q]);
+                rlo[q] = d0.x;
+                md[q] = d0.y;
+                rhi[q] = p0.x;
+                mp[q] = p0.y;
+            }
+        } else {
+            // mode 2: after the dst array, the result-hi word and one mask per
+            // global port class
+#pragma unroll
+            for (int q = 0; q < N; ++q) {
+                const uint2 d0 = *reinterpret_cast<const uint2*>(base + ad[q]);
+                rlo[q] = d0.x;
+                md[q] = d0.y;
+                mp[q] = *reinterpret_cast<const uint32_t*>(base + ap[q] + 4u + pc[q] * 4u);
+                rhi[q] = 0u;
+            }
+            if (t.bv_wide) {
+#pragma unroll
+                for (int q = 0; q < N; ++q) rhi[q] = *reinterpret_cast<const uint32_t*>(base + ap[q]);
+            }
         }
         if (!(t.ablate & 2u)) {
-#pragma unroll 1
-            for (uint32_t i = S; i-- > 0;) {
-                const uint32_t step = 1u << i;
+#pragma unroll
+            for (int i = int(kMaxBvSteps) - 1; i >= 0; --i) {
+                if (uint32_t(i) >= S) continue;
+                const uint32_t step = 8u << i;
 #pragma unroll
                 for (int q = 0; q < N; ++q) {
-                    const uint32_t cd = kd[q] + step;
-                    const uint32_t cp = kp[q] + step;
-                    const uint2 ed = DA[q][cd];
-                    const uint2 ep = PA[q][cp];
-                    const bool td = ed.x <= dst[q], tp = ep.x <= dport[q];
-                    kd[q] = td ? cd : kd[q];
+                    const uint2 ed = *reinterpret_cast<const uint2*>(base + ad[q] + step);
+                    const bool td = ed.x <= dst[q];
+                    ad[q] = td ? ad[q] + step : ad[q];
                     md[q] = td ? ed.y : md[q];
-                    kp[q] = tp ? cp : kp[q];
-                    mp[q] = tp ? ep.y : mp[q];
+                    if constexpr (kList == 1) {
+                        const uint2 ep = *reinterpret_cast<const uint2*>(base + ap[q] + step);
+                        const bool tp = ep.x <= dport[q];
+                        ap[q] = tp ? ap[q] + step : ap[q];
+                        mp[q] = tp ? ep.y : mp[q];
+                    }
                 }
             }
         }
 #pragma unroll
         for (int q = 0; q < N; ++q) {
-            const uint32_t m = (proto[q] <= 2u) ? (md[q] & mp[q]) : 0u;
-            const uint32_t j = uint32_t(__builtin_ctz(m | 0x80000000u));   // m == 0 handled below
-            const uint32_t bits = j < 16u ? (rlo[q] >> (2u * j)) : (rhi[q] >> (2u * (j - 16u)));
+            const uint32_t m = md[q] & mp[q];
+            const uint32_t j = uint32_t(__ffs(m)) - 1u;               // m == 0 handled below
+            const uint32_t bits = uint32_t(((uint64_t(rhi[q]) << 32) | rlo[q]) >> ((2u * j) & 63u));
             res[q] = m ? (bits & 3u) : 0u;            // default DENY (aclengine_mock.go:667)
             slot[q] = m ? cb[q] + j : 0u;
         }
@@ -217,33 +252,51 @@ __device__ __forceinline__ void classify_n(const uint8_t* base, const Cls4Dev& t
 
 template <int N, bool kLds, int kMode>
 __device__ __forceinline__ void run_n(const uint8_t* base, const Cls4Dev& t, uint32_t* lctr,
-                                      unsigned long long* gslot, uint32_t (&hot)[4],
-                                      const uint32_t (&s)[N], const uint32_t (&d)[N],
-                                      const uint32_t (&dp)[N], const uint32_t (&pr)[N],
-                                      uint32_t (&res)[N]) {
+                                      unsigned long long* gslot, uint32_t hot_lane,
+                                      uint32_t& hot0, const uint32_t (&s)[N],
+                                      const uint32_t (&d)[N], const uint32_t (&dp)[N],
+                                      const uint32_t (&pr)[N], uint32_t (&res)[N]) {
     uint32_t slot[N];
     classify_n<N, (kMode & 1), (kMode >> 1)>(base, t, s, d, dp, pr, res, slot);
     if (t.ablate & 1u) return;
+    // One LDS atomic per packet, no branch.  Hot slots (< n_hot: default DENY
+    // and the cells of the widest source class) would have many lanes adding
+    // to one word -- serialised -- so they are counted in this lane's own
+    // row (hot_lane + slot * 64: one bank per lane) and folded at the end.
+    uint32_t idx[N];
 #pragma unroll
     for (int q = 0; q < N; ++q) {
-        if (pr[q] <= 2u) {
-            // Hot slots (the allow-all of unmatched sources, default DENY) take
-            // a large share of packets; lanes adding to one LDS address would
-            // serialise, so those are counted in registers and flushed once.
-            const uint32_t m0 = slot[q] == t.hot_slot[0], m1 = slot[q] == t.hot_slot[1];
-            const uint32_t m2 = slot[q] == t.hot_slot[2], m3 = slot[q] == t.hot_slot[3];
-            hot[0] += m0; hot[1] += m1; hot[2] += m2; hot[3] += m3;
-            if (!(m0 | m1 | m2 | m3)) {
-                if constexpr (kLds) atomicAdd(&lctr[slot[q]], 1u);
-                else atomicAdd(&gslot[slot[q]], 1ull);
+        if constexpr (kLds) {
+            idx[q] = slot[q] < t.n_hot ? hot_lane + slot[q] * 64u : slot[q];
+            atomicAdd(&lctr[idx[q]], 1u);
+        } else if (pr[q] <= 2u) {
+            if (slot[q] == 0u) ++hot0;
+            else atomicAdd(&gslot[slot[q]], 1ull);
+        }
+    }
+    // Protocols outside TCP/UDP/ICMP fall through evalACL's switch
+    // (aclengine_mock.go:508-664): networks alone decide.  Rare; taken per
+    // wave only when some lane holds such a packet.
+    bool other = false;
+#pragma unroll
+    for (int q = 0; q < N; ++q) other |= pr[q] > 2u;
+    if (__any(other)) {
+#pragma unroll
+        for (int q = 0; q < N; ++q) {
+            if (pr[q] > 2u) {
+                if constexpr (kLds) atomicSub(&lctr[idx[q]], 1u);   // undo the cell count
+                uint32_t rule;
+                linear_one(t.lin, t.n_lin, t.n_rules, s[q], d[q], dp[q], 3u, res[q], rule);
+                atomicAdd(&gslot[t.n_ctr + rule], 1ull);
             }
-        } else {                       // protocol outside TCP/UDP/ICMP: switch fall-through
-            uint32_t rule;
-            linear_one(t.lin, t.n_lin, t.n_rules, s[q], d[q], dp[q], 3u, res[q], rule);
-            atomicAdd(&gslot[t.n_ctr + rule], 1ull);
         }
     }
 }
+
+#ifndef CLS_GROUPS
+#define CLS_GROUPS 1
+#endif
+constexpr int kG = CLS_GROUPS;     // 16-B packet groups per lane per step
 
 template <bool kLds, bool kVec, int kMode>
 __global__ __launch_bounds__(kBlock) void classify4_cls(Cls4Dev t, Pkts4 p, uint8_t* verdict,
@@ -256,7 +309,7 @@ __global__ __launch_bounds__(kBlock) void classify4_cls(Cls4Dev t, Pkts4 p, uint
         const uint32_t n4 = t.img_bytes / 16u;
         for (uint32_t i = threadIdx.x; i < n4; i += blockDim.x) smem[i] = src4[i];
         lctr = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(smem) + t.img_bytes);
-        for (uint32_t i = threadIdx.x; i < t.n_ctr; i += blockDim.x) lctr[i] = 0u;
+        for (uint32_t i = threadIdx.x; i < (t.lds_bytes - t.img_bytes) / 4u; i += blockDim.x) lctr[i] = 0u;
         __syncthreads();
         base = reinterpret_cast<const uint8_t*>(smem);
     } else {
@@ -265,55 +318,88 @@ __global__ __launch_bounds__(kBlock) void classify4_cls(Cls4Dev t, Pkts4 p, uint
 
     const uint64_t nthreads = uint64_t(gridDim.x) * blockDim.x;
     const uint64_t tid = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-    uint32_t hot[4] = {0u, 0u, 0u, 0u};
+    uint32_t hot0 = 0;                                     // global-image variant only
+    const uint32_t hot_lane = (t.off_hot - t.img_bytes) / 4u + (threadIdx.x & 63u);
     uint64_t tail_from = 0;
     if constexpr (kVec) {
-        // 4 packets per lane per step, next step's loads issued before this
-        // step's lookups (software pipelining of the HBM stream)
-        const uint64_t ngroups = p.n / 4u;
+        // kG x 4 packets per lane per step (kG contiguous 16-B groups), next
+        // step's loads issued before this step's lookups (software pipelining
+        // of the HBM stream)
+        constexpr int kN = 4 * kG;
+        const uint64_t nsteps = p.n / kN;
         const uint4* S = reinterpret_cast<const uint4*>(p.src);
         const uint4* D = reinterpret_cast<const uint4*>(p.dst);
         const uint2* DP = reinterpret_cast<const uint2*>(p.dport);
         const uint32_t* PR = reinterpret_cast<const uint32_t*>(p.proto);
         uint64_t g = tid;
-        uint4 s = make_uint4(0, 0, 0, 0), d = s;
-        uint2 dp = make_uint2(0, 0);
-        uint32_t pr = 0;
-        if (g < ngroups) { s = S[g]; d = D[g]; dp = DP[g]; pr = PR[g]; }
-        while (g < ngroups) {
+        uint4 s[kG], d[kG];
+        uint2 dp[kG];
+        uint32_t pr[kG];
+#pragma unroll
+        for (int k = 0; k < kG; ++k) {
+            s[k] = make_uint4(0, 0, 0, 0); d[k] = s[k]; dp[k] = make_uint2(0, 0); pr[k] = 0;
+        }
+        if (g < nsteps) {
+#pragma unroll
+            for (int k = 0; k < kG; ++k) {
+                s[k] = S[g * kG + k]; d[k] = D[g * kG + k]; dp[k] = DP[g * kG + k]; pr[k] = PR[g * kG + k];
+            }
+        }
+        while (g < nsteps) {
             const uint64_t gn = g + nthreads;
-            uint4 s2 = s, d2 = d;
-            uint2 dp2 = dp;
-            uint32_t pr2 = pr;
-            if (gn < ngroups) { s2 = S[gn]; d2 = D[gn]; dp2 = DP[gn]; pr2 = PR[gn]; }
-            const uint32_t sa[4] = {s.x, s.y, s.z, s.w};
-            const uint32_t da[4] = {d.x, d.y, d.z, d.w};
-            const uint32_t pa[4] = {dp.x & 0xFFFFu, dp.x >> 16, dp.y & 0xFFFFu, dp.y >> 16};
-            const uint32_t ra[4] = {pr & 0xFFu, (pr >> 8) & 0xFFu, (pr >> 16) & 0xFFu, pr >> 24};
-            uint32_t v[4];
-            run_n<4, kLds, kMode>(base, t, lctr, gslot, hot, sa, da, pa, ra, v);
-            if (verdict && !(t.ablate & 8u))
-                reinterpret_cast<uint32_t*>(verdict)[g] = v[0] | (v[1] << 8) | (v[2] << 16) | (v[3] << 24);
-            s = s2; d = d2; dp = dp2; pr = pr2;
+            uint4 s2[kG], d2[kG];
+            uint2 dp2[kG];
+            uint32_t pr2[kG];
+#pragma unroll
+            for (int k = 0; k < kG; ++k) { s2[k] = s[k]; d2[k] = d[k]; dp2[k] = dp[k]; pr2[k] = pr[k]; }
+            if (gn < nsteps) {
+#pragma unroll
+                for (int k = 0; k < kG; ++k) {
+                    s2[k] = S[gn * kG + k]; d2[k] = D[gn * kG + k]; dp2[k] = DP[gn * kG + k]; pr2[k] = PR[gn * kG + k];
+                }
+            }
+            uint32_t sa[kN], da[kN], pa[kN], ra[kN];
+#pragma unroll
+            for (int k = 0; k < kG; ++k) {
+                sa[4 * k + 0] = s[k].x; sa[4 * k + 1] = s[k].y; sa[4 * k + 2] = s[k].z; sa[4 * k + 3] = s[k].w;
+                da[4 * k + 0] = d[k].x; da[4 * k + 1] = d[k].y; da[4 * k + 2] = d[k].z; da[4 * k + 3] = d[k].w;
+                pa[4 * k + 0] = dp[k].x & 0xFFFFu; pa[4 * k + 1] = dp[k].x >> 16;
+                pa[4 * k + 2] = dp[k].y & 0xFFFFu; pa[4 * k + 3] = dp[k].y >> 16;
+                ra[4 * k + 0] = pr[k] & 0xFFu; ra[4 * k + 1] = (pr[k] >> 8) & 0xFFu;
+                ra[4 * k + 2] = (pr[k] >> 16) & 0xFFu; ra[4 * k + 3] = pr[k] >> 24;
+            }
+            uint32_t v[kN];
+            run_n<kN, kLds, kMode>(base, t, lctr, gslot, hot_lane, hot0, sa, da, pa, ra, v);
+            if (verdict && !(t.ablate & 8u)) {
+#pragma unroll
+                for (int k = 0; k < kG; ++k)
+                    reinterpret_cast<uint32_t*>(verdict)[g * kG + k] =
+                        v[4 * k] | (v[4 * k + 1] << 8) | (v[4 * k + 2] << 16) | (v[4 * k + 3] << 24);
+            }
+#pragma unroll
+            for (int k = 0; k < kG; ++k) { s[k] = s2[k]; d[k] = d2[k]; dp[k] = dp2[k]; pr[k] = pr2[k]; }
             g = gn;
         }
-        tail_from = ngroups * 4u;
+        tail_from = nsteps * kN;
     }
     for (uint64_t i = tail_from + tid; i < p.n; i += nthreads) {
         const uint32_t sa[1] = {p.src[i]}, da[1] = {p.dst[i]}, pa[1] = {p.dport[i]}, ra[1] = {p.proto[i]};
         uint32_t v[1];
-        run_n<1, kLds, kMode>(base, t, lctr, gslot, hot, sa, da, pa, ra, v);
+        run_n<1, kLds, kMode>(base, t, lctr, gslot, hot_lane, hot0, sa, da, pa, ra, v);
         if (verdict) verdict[i] = uint8_t(v[0]);
     }
 
-#pragma unroll
-    for (int h = 0; h < 4; ++h) {
-        if (hot[h]) {
-            if constexpr (kLds) atomicAdd(&lctr[t.hot_slot[h]], hot[h]);
-            else atomicAdd(&gslot[t.hot_slot[h]], (unsigned long long)hot[h]);
-        }
+    if constexpr (!kLds) {
+        if (hot0) atomicAdd(&gslot[0], (unsigned long long)hot0);
     }
     if constexpr (kLds) {
+        __syncthreads();
+        // fold the per-lane hot rows into their slots
+        const uint32_t* hrow = lctr + (t.off_hot - t.img_bytes) / 4u;
+        for (uint32_t i = threadIdx.x; i < t.n_hot * 64u; i += blockDim.x) {
+            const uint32_t v = hrow[i];
+            if (v) atomicAdd(&lctr[i >> 6], v);
+        }
         __syncthreads();
         for (uint32_t i = threadIdx.x; i < t.n_ctr; i += blockDim.x) {
             const uint32_t v = lctr[i];
@@ -498,13 +584,15 @@ hipError_t launch_classify4_cls(const Cls4Dev& t, const Pkts4& p, uint8_t* verdi
                                 unsigned long long* gslot, bool lds_resident, bool vec,
                                 const LaunchCfg& cfg) {
     // variant bits: 1 = hash LPM source lookup, 2 = bit-vector candidate lists
-    const int var = (t.mode == 1 ? 1 : 0) | (t.list_mode == 1 ? 2 : 0);
+    const int var = (t.mode == 1 ? 1 : 0) | (int(t.list_mode) << 1);
 #define CLS_DISPATCH(L, V)                                                       \
     switch (var) {                                                               \
     case 0: launch_cls<L, V, 0>(t, p, verdict, gslot, cfg); break;               \
     case 1: launch_cls<L, V, 1>(t, p, verdict, gslot, cfg); break;               \
     case 2: launch_cls<L, V, 2>(t, p, verdict, gslot, cfg); break;               \
-    default: launch_cls<L, V, 3>(t, p, verdict, gslot, cfg); break;              \
+    case 3: launch_cls<L, V, 3>(t, p, verdict, gslot, cfg); break;               \
+    case 4: launch_cls<L, V, 4>(t, p, verdict, gslot, cfg); break;               \
+    default: launch_cls<L, V, 5>(t, p, verdict, gslot, cfg); break;              \
     }
     if (lds_resident) {
         if (vec) { CLS_DISPATCH(true, true) } else { CLS_DISPATCH(true, false) }
