@@ -44,8 +44,9 @@ class Image:
             if h.mode == 0:
                 self.bounds = np.frombuffer(img, np.uint32, count=2 * top, offset=h.off_bounds)
                 self.iclass = np.frombuffer(img, np.uint16, count=2 * top, offset=h.off_iclass)
-            self.cells = np.frombuffer(img, np.uint32, count=h.n_classes * 6,
-                                       offset=h.off_cells).reshape(-1, 2)
+            if h.list_mode == 0:                   # uint2 cells
+                self.cells = np.frombuffer(img, np.uint32, count=h.n_classes * 6,
+                                           offset=h.off_cells).reshape(-1, 2)
             if h.list_mode == 0:
                 self.lists = np.frombuffer(img, np.uint16, count=h.n_list_entries, offset=h.off_lists)
                 self.tmpl = np.frombuffer(img, np.uint32, count=h.n_tmpl * 4,
@@ -55,29 +56,29 @@ class Image:
             for i in range(h.n_hash):
                 cap = h.hash_cap[i]
                 tab = np.frombuffer(img, np.uint32, count=4 * cap, offset=h.off_hash[i]).reshape(-1, 2)
-                self.hash.append((h.hash_mask[i], h.hash_shift[i], cap, tab))
+                self.hash.append((h.hash_mask[i], h.hash_shift[i], cap, tab, h.hash_mul[i]))
 
     @staticmethod
-    def _h0(k, shift):
-        return ((k.astype(np.uint64) * 0x9E3779B1) & 0xFFFFFFFF) >> np.uint64(shift)
+    def _h0(k, mul, shift):
+        return ((k.astype(np.uint64) * mul) & 0xFFFFFFFF) >> np.uint64(shift)
 
     @staticmethod
-    def _h1(k, shift):
-        return (((k.astype(np.uint64) ^ 0x5BD1E995) * 0xC2B2AE35) & 0xFFFFFFFF) >> np.uint64(shift)
+    def _h1(k, mul, shift):
+        L = 32 - shift
+        return (((k.astype(np.uint64) * mul) & 0xFFFFFFFF) >> np.uint64(32 - 2 * L)) & ((1 << L) - 1)
 
     def source_class(self, src):
         h = self.h
         if h.mode == 1:
-            cls = np.full(len(src), h.default_class, np.int64)
-            for mask, shift, cap, tab in self.hash:
+            # entries hold the byte address of the class's cell row
+            row = np.full(len(src), h.default_row, np.int64)
+            for mask, shift, cap, tab, mul in self.hash:
                 key = src & np.uint32(mask)
-                e0 = tab[self._h0(key, shift).astype(np.int64)]
-                e1 = tab[cap + self._h1(key, shift).astype(np.int64)]
-                hit0 = e0[:, 0] == key
-                hit1 = e1[:, 0] == key
-                cls = np.where(hit0, e0[:, 1].astype(np.int64),
-                               np.where(hit1, e1[:, 1].astype(np.int64), cls))
-            return cls
+                e0 = tab[self._h0(key, mul, shift).astype(np.int64)]
+                e1 = tab[cap + self._h1(key, mul, shift).astype(np.int64)]
+                row = np.where(e0[:, 0] == key, e0[:, 1].astype(np.int64),
+                               np.where(e1[:, 0] == key, e1[:, 1].astype(np.int64), row))
+            return (row - h.off_cells) // h.row_bytes
         k = np.zeros(len(src), np.int64)
         s = h.search_top
         while s:
@@ -107,11 +108,7 @@ class Image:
         res_bits = img[d_off].astype(np.uint64) | (img[p_off].astype(np.uint64) << np.uint64(32))
         lm2 = self.h.list_mode == 2
         if lm2:
-            # global port class: top[p >> 8] = sub offset | base << 20
-            b8 = np.frombuffer(self._img, np.uint8)
-            dp = dport.astype(np.int64)
-            tp = img[self.h.off_ptop // 4 + (dp >> 8)].astype(np.int64)
-            pc = (tp >> 20) + b8[(tp & 0xFFFFF) + (dp & 0xFF)].astype(np.int64)
+            pc = self._port_class(dport)
 
         def search(off, steps, x):
             k = np.zeros(len(x), np.int64)
@@ -138,6 +135,41 @@ class Image:
         j[nz] = np.log2(low[nz].astype(np.float64)).astype(np.int64)
         res = np.where(found, (res_bits >> (2 * j).astype(np.uint64)) & np.uint64(3), 0).astype(np.uint32)
         slot = np.where(found, cb + j, 0)
+        np.add.at(counters, self.ctr_rule[slot].astype(np.int64), 1)
+        other = proto > 2
+        if other.any():
+            r2, rule2 = self.linear(src[other], dst[other], dport[other], proto[other])
+            res[other] = r2
+            np.subtract.at(counters, self.ctr_rule[slot[other]].astype(np.int64), 1)
+            np.add.at(counters, rule2, 1)
+        return res.astype(np.uint8), counters
+
+    def _port_class(self, dport):
+        """Global port class: top[p >> 8] = byte address of a 256-byte window
+        of classes (x 4 in list mode 3)."""
+        img = np.frombuffer(self._img, np.uint32)
+        b8 = np.frombuffer(self._img, np.uint8)
+        dp = dport.astype(np.int64)
+        tp = img[self.h.off_ptop // 4 + (dp >> 8)].astype(np.int64)
+        return b8[tp + (dp & 0xFF)].astype(np.int64)
+
+    def _classify_bv3(self, cls, src, dst, dport, proto, counters):
+        """List mode 3 (port-filtered sublists): cell u32 {pointer table byte
+        offset | counter base << 16}; table[port class] = initial state
+        {outcome | entry slot << 16} (state >> 13 = entry byte address);
+        entries {start - 1, state}, a probe of step i reads 8 << i bytes on and
+        moves the state when start - 1 < dst; outcome = result | (j + 1) << 2."""
+        img = np.frombuffer(self._img, np.uint32).astype(np.int64)
+        pr = np.minimum(proto, 2).astype(np.int64)
+        cell = img[(self.h.off_cells + cls * 12 + pr * 4) // 4]
+        pc4 = self._port_class(dport)                 # class x 4 in mode 3
+        st = img[((cell & 0xFFFF) + pc4) // 4]
+        d = dst.astype(np.int64)
+        for i in range(int(self.h.bv_steps_d) - 1, -1, -1):
+            a = ((st >> 13) + (8 << i)) // 4
+            st = np.where(img[a] < d, img[a + 1], st)
+        res = np.where(proto <= 2, st & 3, 0).astype(np.uint32)
+        slot = (cell >> 16) + ((st >> 2) & 63)       # the cell's no-match slot when j + 1 == 0
         np.add.at(counters, self.ctr_rule[slot].astype(np.int64), 1)
         other = proto > 2
         if other.any():
@@ -178,6 +210,8 @@ class Image:
             np.add.at(counters, rule, 1)
             return res.astype(np.uint8), counters
         cls = self.source_class(src)
+        if self.h.list_mode == 3:
+            return self._classify_bv3(cls, src, dst, dport, proto, counters)
         if self.h.list_mode >= 1:
             return self._classify_bv(cls, src, dst, dport, proto, counters)
         pr = np.minimum(proto, 2).astype(np.int64)

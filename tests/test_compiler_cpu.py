@@ -75,10 +75,11 @@ def test_many_port_ranges_use_per_list_port_search(seed, host_src):
     assert img.h.mode == (1 if host_src else 0)
     rules, pool = random_acl(seed + 77, 150, 0.0)
     img = _check(rules, random_traffic(seed, 6000, pool))
-    assert img.has_cls and img.h.list_mode == 2 and img.h.n_pclass <= 256
+    assert img.has_cls and img.h.list_mode in (2, 3) and img.h.n_pclass <= 256
 
 
-def test_port_class_radix_edges():
+@pytest.mark.parametrize("max_mode", [2, 3])
+def test_port_class_radix_edges(monkeypatch, max_mode):
     """Port classes at chunk edges (255/256, 65535) and ranges inside one
     256-port chunk: every port of every boundary checked against the oracle."""
     from vpp_amd import model as M
@@ -94,8 +95,9 @@ def test_port_class_radix_edges():
               dst=rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32),
               dport=np.tile(np.array(ports, np.uint16), 40),
               proto=rng.choice(np.array([0, 1, 2], np.uint8), n))
+    monkeypatch.setenv("CONTIVCLS_LIST_MODE_MAX", str(max_mode))
     img = _check(rules, tr)
-    assert img.h.list_mode == 2
+    assert img.h.list_mode <= max_mode
 
 
 def test_compiler_uses_classifier_for_larger_tables():
@@ -107,3 +109,28 @@ def test_compiler_uses_classifier_for_larger_tables():
 def test_empty_acl_denies_everything():
     img = _check([], random_traffic(1, 100, random_acl(1, 1)[1]))
     assert not img.has_cls
+
+
+@pytest.mark.parametrize("seed", range(6))
+@pytest.mark.parametrize("max_mode", [1, 2])
+def test_capped_list_modes_match_oracle(monkeypatch, seed, max_mode):
+    """The lower bit-vector list modes (what tables with > 16-entry lists or
+    too many port classes get) stay exact when selected explicitly."""
+    monkeypatch.setenv("CONTIVCLS_LIST_MODE_MAX", str(max_mode))
+    rules, pool = random_acl(seed * 7 + 3, 150, 0.0, n_prefixes=4 if seed % 2 else 24)
+    img = _check(rules, random_traffic(seed, 5000, pool))
+    assert img.h.list_mode <= max_mode
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_compact_lists_edge_addresses(seed):
+    """List mode 3 at the address-space edges (0.0.0.0, 255.255.255.255 hit the
+    padding of shallow lists) and /32 sources outside the probe filter."""
+    rules, pool = random_acl(seed * 11 + 5, 60, 0.0, n_prefixes=6)
+    tr = random_traffic(seed, 4000, pool)
+    n = len(tr["dst"])
+    tr["dst"][: n // 4] = np.uint32(0xFFFFFFFF)
+    tr["dst"][n // 4: n // 2] = np.uint32(0)
+    tr["src"][::7] = np.uint32(0xFFFFFFFF)
+    img = _check(rules, tr)
+    assert img.h.list_mode in (2, 3)

@@ -70,6 +70,7 @@ def test_random_acls_both_kernels(eng, seed, n_rules, weird):
 
 
 VARIANTS = {  # kind -> (source lookup mode, list mode)
+    "hash_cbv": (1, 3), "search_cbv": (0, 3),
     "hash_pc": (1, 2), "search_pc": (0, 2), "hash_bv": (1, 1), "search_bv": (0, 1),
     "hash_scan": (1, 0), "search_scan": (0, 0)}
 
@@ -81,15 +82,18 @@ def variant_acl(kind, seed):
         return long_list_acl(seed + 70, 300, n_src=3 if hashed else 30)
     if kind.endswith("_bv"):
         return many_ports_acl(seed + 5, 400, 40, host_src=hashed)
-    return random_acl(seed * 31 + 7, 120, 0.0, n_prefixes=4 if hashed else 24)
+    return random_acl(seed * 31 + 7, 60 if kind.endswith("cbv") else 120, 0.0,
+                      n_prefixes=4 if hashed else 24)
 
 
 @pytest.mark.parametrize("seed", range(3))
 @pytest.mark.parametrize("kind", sorted(VARIANTS))
-def test_all_kernel_variants(eng, seed, kind):
-    """The six classifier variants (hash-LPM / interval-search source lookup
-    x bit vectors with global port classes / bit vectors with per-list port
-    search / template scan) against the oracle."""
+def test_all_kernel_variants(eng, seed, kind, monkeypatch):
+    """The eight classifier variants (hash-LPM / interval-search source lookup
+    x compact bit vectors / bit vectors with global port classes / bit vectors
+    with per-list port search / template scan) against the oracle."""
+    if kind.endswith("_pc"):
+        monkeypatch.setenv("CONTIVCLS_LIST_MODE_MAX", "2")
     from cls_image import Image, compile_blob
     from vpp_amd import _abi
     rules, pool = variant_acl(kind, seed)

@@ -1,7 +1,12 @@
 #!/usr/bin/env python3
-"""Diagnostics: time classify4_cls with stages ablated (CONTIVCLS_ABLATE bits:
-1 counters, 2 candidate scan, 4 source lookup, 8 verdict store).  Results of
-ablated runs are wrong by construction; only kernel times matter."""
+"""Diagnostics: time classify4_cls builds A/B.
+
+  tools/ablate.py CFG lib1.so lib2.so ...   one child process per library
+  (build them with `make -C vpp_amd/csrc variant V=name F=...`; stage ablation
+  is a build flag, F=-DCLS_ABLATE=bits: 1 counters, 2 candidate scan, 4 source
+  lookup, 8 verdict store -- results of ablated builds are wrong by
+  construction; only kernel times matter).  tools/build_ablate.sh builds the
+  usual set."""
 import os
 import sys
 
@@ -16,6 +21,7 @@ def main():
     from vpp_amd.engine import Engine
     cfg = int(sys.argv[1]) if len(sys.argv) > 1 else 3
     acl, spec, n = workload.config(cfg)
+    n = int(os.environ.get("PKTS", n))
     eng = Engine(0)
     t = eng.put_table("t", acl.rules)
     print("info", t.info())
@@ -24,18 +30,16 @@ def main():
     eng.gen_traffic_v4(spec, 0, pk)
     verdict = torch.empty(n, dtype=torch.uint8, device="cuda")
     counters = torch.zeros(t.n_rules + 1, dtype=torch.int64, device="cuda")
-    abl = [int(x) for x in os.environ.get("ABL", "0,1,2,3,4,6,7,15").split(",")]
-    for ab in abl:
-        os.environ["CONTIVCLS_ABLATE"] = str(ab)
-        for _ in range(2):
+    for rep in range(2):       # the first round warms clocks up
+        for _ in range(3):
             eng.classify(t, pk["src"], pk["dst"], pk["dport"], pk["proto"], verdict=verdict, counters=counters)
         eng.kernel_times(reset=True)
-        for _ in range(5):
+        for _ in range(10):
             eng.classify(t, pk["src"], pk["dst"], pk["dport"], pk["proto"], verdict=verdict,
                          counters=counters, timing=True)
-        ms = float(np.mean(eng.kernel_times(reset=True)))
-        print("ablate=%2d kernel %.3f ms  %.1f Gpps  %.1f GB/s" % (ab, ms, n / ms / 1e6, n * 12 / ms / 1e6))
-    os.environ.pop("CONTIVCLS_ABLATE")
+        ks = eng.kernel_times(reset=True)
+        ms = float(np.median(ks))
+        print("kernel median %.3f ms (min %.3f)  %.1f Gpps  %.1f GB/s" % (ms, min(ks), n / ms / 1e6, n * 12 / ms / 1e6))
 
 
 def ab_libs():

@@ -12,7 +12,7 @@ cd /tmp
 B="$ROOT/bench.py --config $CFG --steps 2 --warmup 1 --cpu-sample 0"
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $OUT/fetch -o run --output-format csv -- python3 $B > $OUT/fetch.log 2>&1
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $OUT/write -o run --output-format csv -- python3 $B > $OUT/write.log 2>&1
-N=$(python3 -c "import json,sys; print(json.loads(open('$OUT/fetch.log').read().strip().splitlines()[-1])['config']['packets_per_gpu'])")
+N=$(grep '^{"metric"' $OUT/fetch.log | python3 -c "import json,sys; print(json.loads(sys.stdin.readline())['config']['packets_per_gpu'])")
 python3 $ROOT/tools/pmc_traffic.py pmc $(find $OUT/fetch -name "*counter_collection.csv") $(find $OUT/write -name "*counter_collection.csv") $CFG $N $OUT/pmc.json
 cd $ROOT
 timeout -k 10 120 python3 tools/ablate.py $CFG > $OUT/ablate.log 2>&1

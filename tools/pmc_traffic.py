@@ -56,6 +56,7 @@ def pmc(fetch_csv, write_csv, config, packets, out):
     wk = sum(w) / len(w)
     read_bytes = 2.0 * fk * 1024        # gfx950 FETCH_SIZE half-count correction
     write_bytes = wk * 1024
+    packets = int(packets)
     alg_read = packets * 11
     alg_write = packets * 1
     d = {"config": int(config), "packets": int(packets), "kernel": KERNEL,

@@ -2,6 +2,7 @@
 #include "compile.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <unordered_map>
@@ -218,10 +219,10 @@ struct TmplHash {
 uint32_t align4(uint32_t w) { return (w + 3u) & ~3u; }
 
 // Two-table cuckoo hash of (key, class): table 0 at [0, cap), table 1 at
-// [cap, 2 cap); entry = key | (class + 1) << 32, 0 = empty.
-bool cuckoo_build(const std::vector<std::pair<uint32_t, uint32_t>>& keys, uint32_t cap,
+// [cap, 2 cap); entry = key | class << 32.
+bool cuckoo_build(const std::vector<std::pair<uint32_t, uint32_t>>& keys, uint32_t cap, uint32_t mul,
                   std::vector<uint64_t>& tab) {
-    const uint32_t shift = 32u - uint32_t(__builtin_ctz(cap));
+    const uint32_t L = uint32_t(__builtin_ctz(cap));
     std::vector<uint8_t> used(size_t(cap) * 2, 0);
     tab.assign(size_t(cap) * 2, 0ull);
     for (const auto& kv : keys) {
@@ -230,7 +231,7 @@ bool cuckoo_build(const std::vector<std::pair<uint32_t, uint32_t>>& keys, uint32
         int side = 0;
         for (int kick = 0; kick < 256 && cur_valid; ++kick) {
             const uint32_t k = uint32_t(cur);
-            const size_t pos = side == 0 ? lpm_h0(k, shift) : size_t(cap) + lpm_h1(k, shift);
+            const size_t pos = side == 0 ? lpm_h0(k, mul, L) : size_t(cap) + lpm_h1(k, mul, L);
             std::swap(cur, tab[pos]);
             const bool was_used = used[pos];
             used[pos] = 1;
@@ -246,11 +247,15 @@ bool cuckoo_build(const std::vector<std::pair<uint32_t, uint32_t>>& keys, uint32
         const bool t1 = pos >= cap;
         const uint32_t slot = uint32_t(t1 ? pos - cap : pos);
         uint32_t k = 0;
-        while ((t1 ? lpm_h1(k, shift) : lpm_h0(k, shift)) == slot) ++k;
+        while ((t1 ? lpm_h1(k, mul, L) : lpm_h0(k, mul, L)) == slot) ++k;
         tab[pos] = k;
     }
     return true;
 }
+
+// odd multipliers tried in order by the hash-LPM builder
+constexpr uint32_t kHashMuls[] = {0x9E3779B1u, 0x85EBCA77u, 0xC2B2AE3Du, 0x27D4EB2Fu, 0x165667B1u,
+                                  0xD3A2646Du, 0xFD7046C5u, 0xB55A4F09u};
 
 // Bit-vector arrays of one candidate list (k <= 32 entries), appended to `out`:
 //   dst array:  2^S x {interval start, mask of entries whose dst prefix covers it}
@@ -392,22 +397,93 @@ BvDesc build_bv2(const std::vector<TmplKey>& ents, uint32_t Sd, const std::vecto
 // Port -> class radix of mode 2: top[p >> 8] = sub-table byte offset (20 bits,
 // relative to the radix section) | base class << 20; class = base + sub[p & 255].
 // A 256-port chunk inside one class points at the shared all-zero sub-table.
-void port_radix(const std::vector<uint32_t>& G, std::vector<uint32_t>& top,
-                std::vector<uint8_t>& subs) {
-    top.assign(256, 0);
-    subs.assign(256, 0);                                   // sub-table 0: all zero
+// Port -> class radix (list modes 2, 3): per 256-port chunk h, the byte offset
+// of a 256-byte window holding class x `scale` for each port of the chunk.
+// Chunks inside one class point into any run of 256 equal bytes (shared).
+void port_radix(const std::vector<uint32_t>& G, std::vector<uint32_t>& toff,
+                std::vector<uint8_t>& subs, uint32_t scale) {
+    toff.assign(256, 0);
+    subs.clear();
     auto cls_of = [&](uint32_t p) {
         return uint32_t(std::upper_bound(G.begin(), G.end(), p) - G.begin()) - 1u;
     };
+    std::vector<int> uni(256, -1);
     for (uint32_t h = 0; h < 256; ++h) {
         const uint32_t c0 = cls_of(h << 8), c1 = cls_of((h << 8) | 255u);
-        uint32_t off = 0;
         if (c1 != c0) {
-            off = uint32_t(subs.size());
-            for (uint32_t x = 0; x < 256; ++x) subs.push_back(uint8_t(cls_of((h << 8) | x) - c0));
+            toff[h] = uint32_t(subs.size());
+            for (uint32_t x = 0; x < 256; ++x) subs.push_back(uint8_t(cls_of((h << 8) | x) * scale));
+        } else {
+            uni[h] = int(c0 * scale);
         }
-        top[h] = off | (c0 << 20);
     }
+    for (uint32_t h = 0; h < 256; ++h) {
+        if (uni[h] < 0) continue;
+        const uint8_t v = uint8_t(uni[h]);
+        size_t at = SIZE_MAX, run = 0;
+        for (size_t i = 0; i < subs.size(); ++i) {
+            run = subs[i] == v ? run + 1 : 0;
+            if (run == 256) { at = i + 1 - 256; break; }
+        }
+        if (at == SIZE_MAX) {                      // extend the tail run to 256
+            size_t tail = 0;
+            while (tail < subs.size() && subs[subs.size() - 1 - tail] == v) ++tail;
+            at = subs.size() - tail;
+            subs.resize(at + 256, v);
+        }
+        toff[h] = uint32_t(at);
+    }
+}
+
+// List mode 3: port-filtered sublists.  For a list and a global port class,
+// the entries whose port range covers the class decide first-match by the dst
+// address alone: the elementary dst intervals of the list each get an outcome
+// o = result | (j + 1) << 2 (j = first matching entry, 0 = no entry matches:
+// default DENY), adjacent intervals with equal outcomes merge.
+struct Sublist {
+    std::vector<uint32_t> start;   // interval starts, start[0] = 0
+    std::vector<uint32_t> out;     // outcome per interval
+    bool operator==(const Sublist& o) const { return start == o.start && out == o.out; }
+};
+struct SublistHash {
+    size_t operator()(const Sublist& s) const {
+        uint64_t h = 1469598103934665603ull;
+        for (size_t i = 0; i < s.start.size(); ++i) {
+            h = (h ^ s.start[i]) * 1099511628211ull;
+            h = (h ^ s.out[i]) * 1099511628211ull;
+        }
+        return size_t(h);
+    }
+};
+std::vector<Sublist> port_sublists(const std::vector<TmplKey>& ents, const std::vector<uint32_t>& G) {
+    std::vector<uint32_t> db, pb;
+    bv_bounds(ents, db, pb);
+    std::vector<uint64_t> dm(db.size(), 0);
+    for (size_t k = 0; k < db.size(); ++k)
+        for (size_t j = 0; j < ents.size(); ++j)
+            if (((db[k] ^ ents[j].a) & ents[j].m) == 0) dm[k] |= 1ull << j;
+    std::vector<Sublist> res(G.size());
+    for (size_t p = 0; p < G.size(); ++p) {
+        uint64_t pm = 0;
+        for (size_t j = 0; j < ents.size(); ++j) {
+            const uint32_t lo = ents[j].pw & 0xFFFFu, hi = lo + (ents[j].pw >> 16);
+            if (G[p] >= lo && G[p] <= hi) pm |= 1ull << j;
+        }
+        Sublist& sl = res[p];
+        for (size_t k = 0; k < db.size(); ++k) {
+            const uint64_t m = dm[k] & pm;
+            uint32_t o = 0;
+            if (m) {
+                const uint32_t j = uint32_t(__builtin_ctzll(m));
+                o = (ents[j].res & 3u) | ((j + 1u) << 2);
+            }
+            if (sl.out.empty() || sl.out.back() != o) {
+                sl.start.push_back(db[k]);
+                sl.out.push_back(o);
+            }
+        }
+    }
+    return res;
 }
 
 }  // namespace
@@ -500,18 +576,20 @@ bool build_cls4(const std::vector<SemRule>& sem, uint32_t n_rules, Cls4Image& im
             img.default_class = dflt;
             for (const auto& kv : keys) {
                 const auto& ks = kv.second;
-                uint32_t cap = 16;
+                uint32_t cap = 16, mul = 0;
                 while (cap < ks.size()) cap *= 2;
                 std::vector<uint64_t> tab;
-                for (;;) {
-                    if (cuckoo_build(ks, cap, tab)) break;
-                    cap *= 2;
+                for (bool ok = false; !ok;) {
+                    for (uint32_t m : kHashMuls)
+                        if (cuckoo_build(ks, cap, m, tab)) { ok = true; mul = m; break; }
+                    if (!ok) cap *= 2;
                     if (cap > (1u << 16)) { img.mode = 0; break; }
                 }
                 if (img.mode == 0) break;
                 const uint32_t i = uint32_t(hash_tabs.size());
                 img.hash_mask[i] = v4_mask(kv.first);
                 img.hash_shift[i] = 32u - uint32_t(__builtin_ctz(cap));
+                img.hash_mul[i] = mul;
                 img.hash_cap[i] = cap;
                 hash_tabs.push_back(std::move(tab));
             }
@@ -630,7 +708,7 @@ bool build_cls4(const std::vector<SemRule>& sem, uint32_t n_rules, Cls4Image& im
     // image fits the workgroup's LDS (and the 16-bit cell fields) is chosen
     std::vector<std::vector<TmplKey>> bv_ents;
     uint32_t Sd = 0, Sp = 0;
-    std::vector<uint32_t> G, ptop;
+    std::vector<uint32_t> G, toff;
     std::vector<uint8_t> psub;
     if (img.ctr_rule.size() > 0xFFFFu) all_bv = false;    // counter base: 16-bit cell field
     if (all_bv) {
@@ -642,14 +720,63 @@ bool build_cls4(const std::vector<SemRule>& sem, uint32_t n_rules, Cls4Image& im
             while ((size_t(1) << Sp) < pb.size()) ++Sp;
         }
         G = port_classes(bv_ents);
-        port_radix(G, ptop, psub);
     }
     uint32_t lmode = 0;
     if (all_bv && Sd <= kMaxBvSteps && G.size() <= kMaxPortClasses) lmode = 2;
     else if (all_bv && std::max(Sd, Sp) <= kMaxBvSteps) lmode = 1;
+    // list mode 3: port-filtered sublists (needs <= 64 port classes: the radix
+    // yields the class x 4 in a byte)
+    std::vector<std::vector<uint32_t>> sub_of;           // list -> sublist id per port class
+    std::vector<Sublist> subs;
+    uint32_t D = 0;
+    if (lmode == 2 && G.size() <= kMaxPortClasses3) {
+        std::unordered_map<Sublist, uint32_t, SublistHash> sid;
+        for (const auto& ents : bv_ents) {
+            std::vector<uint32_t> ids;
+            for (Sublist& sl : port_sublists(ents, G)) {
+                auto it = sid.find(sl);
+                if (it == sid.end()) {
+                    it = sid.emplace(sl, uint32_t(subs.size())).first;
+                    while ((size_t(1) << D) < sl.start.size()) ++D;
+                    subs.push_back(std::move(sl));
+                }
+                ids.push_back(it->second);
+            }
+            sub_of.push_back(std::move(ids));
+        }
+        if (D <= kMaxBvSteps) lmode = 3;
+    }
+    // diagnostics / tests: cap the list mode (CONTIVCLS_LIST_MODE_MAX)
+    if (const char* mx = std::getenv("CONTIVCLS_LIST_MODE_MAX")) {
+        const uint32_t cap = uint32_t(std::strtoul(mx, nullptr, 0));
+        if (lmode > cap)
+            lmode = cap >= 2 && lmode >= 2 ? 2u : (cap >= 1 && std::max(Sd, Sp) <= kMaxBvSteps ? 1u : 0u);
+    }
+
+    // mode 3 gives every cell its own "no entry matched" slot (rule R, default
+    // DENY) in front of its entry slots, so the kernel's slot is cell base +
+    // (j + 1) with no select; same cell order, so the hot class stays first
+    const std::vector<uint32_t> ctr_base_rule = img.ctr_rule;
+    const uint32_t hot_base = img.n_hot;
+    std::vector<uint32_t> ctr3(1, n_rules), cb3(size_t(n_classes) * 3);
+    uint32_t hot3 = 1;
+    for (uint32_t ci = 0; ci < n_classes; ++ci) {
+        const uint32_t c = ci == 0 ? hot_class : (ci <= hot_class ? ci - 1 : ci);
+        for (int pr = 0; pr < 3; ++pr) {
+            const size_t k = size_t(c) * 3 + pr;
+            cb3[k] = uint32_t(ctr3.size());
+            ctr3.push_back(n_rules);
+            const uint32_t len = cells[2 * k] >> 16, b = cells[2 * k + 1];
+            for (uint32_t j = 0; j < len; ++j) ctr3.push_back(ctr_base_rule[b + j]);
+        }
+        if (ci == 0) hot3 = std::min<uint32_t>(uint32_t(ctr3.size()), kMaxHot);
+    }
+    if (lmode == 3 && ctr3.size() > 0xFFFFu) lmode = 2;   // 16-bit cell field
 
     std::vector<uint32_t>& w = img.words;
     auto serialise = [&](uint32_t lm) {
+        img.ctr_rule = lm == 3 ? ctr3 : ctr_base_rule;
+        img.n_hot = lm == 3 ? hot3 : hot_base;
         // lists
         bv.clear();
         bv_desc.clear();
@@ -659,17 +786,40 @@ bool build_cls4(const std::vector<SemRule>& sem, uint32_t n_rules, Cls4Image& im
             else if (lm == 1) bv_desc[bv_lists[i]] = build_bv(bv_ents[i], S, bv);
         }
         img.list_mode = lm;
-        img.bv_steps_d = lm == 2 ? Sd : S;
-        img.bv_steps_p = lm == 2 ? 0u : S;
-        img.n_pclass = lm == 2 ? uint32_t(G.size()) : 0u;
+        img.bv_steps_d = lm == 3 ? D : lm == 2 ? Sd : S;
+        img.bv_steps_p = lm >= 2 ? 0u : S;
+        img.n_pclass = lm >= 2 ? uint32_t(G.size()) : 0u;
         img.bv_wide = 0;
         for (const auto& e : bv_ents) img.bv_wide |= e.size() > 16 ? 1u : 0u;
         // serialise (u32 words, each section 16 B aligned); sections the chosen
         // modes never read are left out of the LDS image
         w.clear();
         img.off_bounds = img.off_iclass = img.off_lists = img.off_tmpl = img.off_bv = img.off_ptop = 0;
+        if (lm >= 2) {
+            // port radix at LDS address 0 (the kernel indexes it without a base):
+            // top (256 x u32 = byte address of the chunk's window), then windows
+            port_radix(G, toff, psub, lm == 3 ? 4u : 1u);   // mode 3: class x 4
+            img.off_ptop = 0;
+            for (uint32_t h = 0; h < 256; ++h) w.push_back(1024u + toff[h]);
+            w.resize(256 + (psub.size() + 3) / 4);
+            std::memcpy(reinterpret_cast<uint8_t*>(w.data() + 256), psub.data(), psub.size());
+            w.resize(align4(uint32_t(w.size())));
+        }
+        std::unordered_map<uint32_t, uint32_t> ptr_off;  // list key -> byte offset of its pointer table
+        std::vector<uint32_t> state0;                      // sublist -> initial state, region-relative
+        std::vector<uint32_t> ptr_at;                      // word index of each list's pointer table
+        if (lm == 3) {
+            // pointer tables first: their byte offsets live in the cell's low 16 bits
+            for (size_t i = 0; i < bv_lists.size(); ++i) {
+                ptr_off[bv_lists[i]] = uint32_t(w.size()) * 4;
+                ptr_at.push_back(uint32_t(w.size()));
+                w.resize(w.size() + G.size(), 0u);           // filled once the region is placed
+            }
+            w.resize(align4(uint32_t(w.size())));
+            img.sub_bytes = uint32_t(w.size()) * 4;
+        }
         if (img.mode == 0) {
-            img.off_bounds = 0;
+            img.off_bounds = uint32_t(w.size()) * 4;
             w.insert(w.end(), bounds.begin(), bounds.end());
             w.resize(align4(uint32_t(w.size())));
             img.off_iclass = uint32_t(w.size()) * 4;
@@ -678,6 +828,8 @@ bool build_cls4(const std::vector<SemRule>& sem, uint32_t n_rules, Cls4Image& im
             w.resize(align4(uint32_t(w.size())));
         }
         img.off_cells = uint32_t(w.size()) * 4;
+        img.row_bytes = lm == 0 ? 24u : 12u;          // 3 cells of uint2 (scan) / u32
+        img.default_row = img.off_cells + img.default_class * img.row_bytes;
         if (lm == 0) {
             // scan cells: uint2 {list start | len << 16, counter base}
             w.insert(w.end(), cells.begin(), cells.end());
@@ -695,6 +847,12 @@ bool build_cls4(const std::vector<SemRule>& sem, uint32_t n_rules, Cls4Image& im
                 w.push_back(t.res);
             }
             w.resize(align4(uint32_t(w.size())));
+        } else if (lm == 3) {
+            // sublist cells: u32 {pointer table byte offset | counter base << 16},
+            // the base being the cell's own no-match slot
+            const size_t n_cells = size_t(n_classes) * 3;
+            for (size_t i = 0; i < n_cells; ++i) w.push_back(ptr_off.at(cells[2 * i]) | (cb3[i] << 16));
+            w.resize(align4(uint32_t(w.size())));
         } else {
             // bit-vector cells: u32 {list block offset / 8 | counter base << 16}
             const size_t n_cells = size_t(n_classes) * 3;
@@ -708,23 +866,83 @@ bool build_cls4(const std::vector<SemRule>& sem, uint32_t n_rules, Cls4Image& im
             w.resize(align4(uint32_t(w.size())));
             w.insert(w.end(), bv.begin(), bv.end());
             w.resize(align4(uint32_t(w.size())));
-            if (lm == 2) {
-                // port radix: top (256 x u32), then the u8 sub-tables
-                img.off_ptop = uint32_t(w.size()) * 4;
-                const uint32_t sub0 = img.off_ptop + 256u * 4u;
-                for (uint32_t x : ptop) w.push_back(((x & 0xFFFFFu) + sub0) | (x & ~0xFFFFFu));
-                const size_t sbase = w.size();
-                w.resize(sbase + (psub.size() + 3) / 4);
-                std::memcpy(reinterpret_cast<uint8_t*>(w.data() + sbase), psub.data(), psub.size());
-                w.resize(align4(uint32_t(w.size())));
-            }
         }
         for (uint32_t i = 0; i < img.n_hash; ++i) {
             img.off_hash[i] = uint32_t(w.size()) * 4;
+            // entry {key, byte address of the class's cell row}
             for (uint64_t e : hash_tabs[i]) {
                 w.push_back(uint32_t(e));
-                w.push_back(uint32_t(e >> 32));
+                w.push_back(img.off_cells + uint32_t(e >> 32) * img.row_bytes);
             }
+            w.resize(align4(uint32_t(w.size())));
+        }
+        if (lm == 3) {
+            // Sublist region, 8-B slots.  A sublist of n intervals and depth s
+            // (2^s >= n) sits at slot A: entries 1 .. n-1 in slots A+1 .. A+n-1
+            // as {start - 1, outcome | (A + c) << 16}; the slots a probe may
+            // read beyond them -- A+n .. A+2^s-1 and A + 2^i for s <= i < D --
+            // must hold a never-taken sentinel {0xFFFFFFFF, 0} (the kernel
+            // tests start - 1 < dst).  Sentinel slots are shared between
+            // sublists; greedy first fit, deepest first.
+            const uint32_t r0 = uint32_t(w.size()) / 2u + (w.size() & 1u);   // region slot base
+            std::vector<uint8_t> kind;                    // 0 free, 1 entry, 2 sentinel
+            std::vector<uint32_t> A(subs.size());
+            std::vector<size_t> order(subs.size());
+            for (size_t k = 0; k < order.size(); ++k) order[k] = k;
+            std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) {
+                return subs[a].start.size() > subs[b].start.size();
+            });
+            std::vector<uint32_t> need_e, need_s;
+            uint32_t hint1 = 0;                           // first fit for single-interval sublists
+            for (size_t k : order) {
+                const uint32_t n = uint32_t(subs[k].start.size());
+                uint32_t sd = 0;
+                while ((1u << sd) < n) ++sd;
+                need_e.clear();
+                need_s.clear();
+                for (uint32_t c = 1; c < n; ++c) need_e.push_back(c);
+                for (uint32_t c = n; c < (1u << sd); ++c) need_s.push_back(c);
+                for (uint32_t i2 = std::max(sd, n > 1 ? sd : 0u); i2 < D; ++i2) need_s.push_back(1u << i2);
+                uint32_t a = n == 1 ? hint1 : 0u;
+                for (;; ++a) {
+                    bool ok = true;
+                    for (uint32_t c : need_e) {
+                        if (a + c < kind.size() && kind[a + c] != 0) { ok = false; break; }
+                    }
+                    if (ok)
+                        for (uint32_t c : need_s) {
+                            if (a + c < kind.size() && kind[a + c] == 1) { ok = false; break; }
+                        }
+                    if (ok) break;
+                }
+                if (n == 1) hint1 = a;
+                const uint32_t top_slot = a + std::max<uint32_t>(1u << std::max(sd, D > 0 ? D - 1 : 0u), n) + 1;
+                if (kind.size() < top_slot) kind.resize(top_slot, 0);
+                for (uint32_t c : need_e) kind[a + c] = 1;
+                for (uint32_t c : need_s) kind[a + c] = 2;
+                A[k] = a;
+            }
+            if (kind.empty()) kind.resize(1, 0);
+            w.resize(size_t(r0) * 2, 0u);
+            const size_t reg = w.size();
+            w.resize(reg + kind.size() * 2);
+            for (size_t sl = 0; sl < kind.size(); ++sl) {
+                w[reg + 2 * sl] = 0xFFFFFFFFu;
+                w[reg + 2 * sl + 1] = 0u;
+            }
+            state0.resize(subs.size());
+            for (size_t k = 0; k < subs.size(); ++k) {
+                const uint32_t base_slot = r0 + A[k];
+                for (uint32_t c = 1; c < subs[k].start.size(); ++c) {
+                    w[reg + 2 * (A[k] + c)] = subs[k].start[c] - 1u;
+                    w[reg + 2 * (A[k] + c) + 1] = subs[k].out[c] | ((base_slot + c) << 16);
+                }
+                state0[k] = subs[k].out[0] | (base_slot << 16);
+            }
+            img.off_bv = uint32_t(reg) * 4;
+            if (r0 + kind.size() > 0x10000u) img.sub_bytes = 0xFFFFFFFFu;   // 16-bit slot field
+            for (size_t i = 0; i < bv_lists.size(); ++i)
+                for (size_t p = 0; p < G.size(); ++p) w[ptr_at[i] + p] = state0[sub_of[i][p]];
             w.resize(align4(uint32_t(w.size())));
         }
         img.img_bytes = uint32_t(w.size()) * 4;
@@ -740,9 +958,11 @@ bool build_cls4(const std::vector<SemRule>& sem, uint32_t n_rules, Cls4Image& im
     for (;;) {
         serialise(lmode);
         if (lmode == 0) break;
-        const bool cell_ok = img.img_bytes / 8u <= 0xFFFFu;   // 16-bit block offset field
+        // block offset field: 16 bits in 8-B units (modes 1, 2); mode 3: the
+        // pointer tables in the first 64 KiB, sublist slots below 2^16
+        const bool cell_ok = lmode == 3 ? img.sub_bytes <= 0x10000u : img.img_bytes / 8u <= 0xFFFFu;
         if (cell_ok && (lmode == 1 || img.lds_bytes <= kLdsBudget)) break;
-        lmode = (lmode == 2 && std::max(Sd, Sp) <= kMaxBvSteps) ? 1u : 0u;
+        lmode = lmode == 3 ? 2u : (lmode == 2 && std::max(Sd, Sp) <= kMaxBvSteps) ? 1u : 0u;
     }
     return true;
 }

@@ -40,13 +40,18 @@ namespace cls {
 constexpr uint32_t kMaxHashLens = 3;
 constexpr uint32_t kMaxHot = 16;       // hot slots counted in per-lane LDS rows
 constexpr uint32_t kMaxBvSteps = 7;    // bit-vector search depth (lists <= 32 entries)
-constexpr uint32_t kMaxPortClasses = 256;  // list mode 2: global port classes
+constexpr uint32_t kMaxPortClasses = 256;  // list modes 2, 3: global port classes
+constexpr uint32_t kPortUniform = 1u << 19;  // port radix: chunk inside one class
+constexpr uint32_t kMaxPortClasses3 = 64;   // list mode 3: class x 4 fits the radix byte
 constexpr uint32_t kLdsBudget = 160 * 1024;  // LDS of one classify workgroup
-__host__ __device__ inline uint32_t lpm_h0(uint32_t k, uint32_t shift) {
-    return (k * 0x9E3779B1u) >> shift;
+// One multiply per key: p = key x mul; table 0 takes the top L bits of p,
+// table 1 the next L bits (L = log2 cap <= 16).  The compiler picks mul from a
+// fixed list until the cuckoo build succeeds.
+__host__ __device__ inline uint32_t lpm_h0(uint32_t k, uint32_t mul, uint32_t L) {
+    return (k * mul) >> (32u - L);
 }
-__host__ __device__ inline uint32_t lpm_h1(uint32_t k, uint32_t shift) {
-    return ((k ^ 0x5BD1E995u) * 0xC2B2AE35u) >> shift;
+__host__ __device__ inline uint32_t lpm_h1(uint32_t k, uint32_t mul, uint32_t L) {
+    return ((k * mul) >> (32u - 2u * L)) & ((1u << L) - 1u);
 }
 
 enum : uint8_t { RES_DENY = 0, RES_PERMIT = 1, RES_REFLECT = 2, RES_FAIL = 3 };
@@ -108,11 +113,19 @@ struct Cls4Image {
     uint32_t mode = 0;
     uint32_t default_class = 0;    // hash mode: class of addresses no hashed prefix covers
     uint32_t n_hash = 0;           // hashed prefix lengths, ascending
-    uint32_t hash_mask[kMaxHashLens] = {}, hash_shift[kMaxHashLens] = {};
+    uint32_t hash_mask[kMaxHashLens] = {}, hash_shift[kMaxHashLens] = {};  // shift = 32 - L
+    uint32_t hash_mul[kMaxHashLens] = {};
     uint32_t hash_cap[kMaxHashLens] = {}, off_hash[kMaxHashLens] = {};
+    // class rows: a class's 3 cells (TCP, UDP, ICMP) at off_cells + class x
+    // row_bytes; hash entries hold that byte address, not the class index
+    uint32_t row_bytes = 12;
+    uint32_t default_row = 0;      // hash mode: row of default_class
     // candidate lists: mode 0 = scan of template ids, 1 = bit vectors (all lists
-    // <= 32) with per-list port search, 2 = bit vectors with global port classes
+    // <= 32) with per-list port search, 2 = bit vectors with global port
+    // classes, 3 = port-filtered sublists (per list and port class, the dst
+    // intervals with their first-match outcome; searched with one state word)
     uint32_t list_mode = 0;
+    uint32_t sub_bytes = 0;        // mode 3: end of the pointer tables (< 64 KiB)
     uint32_t off_bv = 0;
     uint32_t bv_steps_d = 0, bv_steps_p = 0;   // largest search depths over the lists
     // list mode 2: global port classes (radix at off_ptop), result-hi word used

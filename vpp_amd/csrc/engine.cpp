@@ -227,6 +227,8 @@ int cls_table_get_info(cls_engine* e, uint32_t table_id, cls_table_info* info) {
 }
 
 // ---------------------------------------------------------------------------
+constexpr uint64_t kClsChunk = 1ull << 30;   // packets per classify launch (32-bit offsets)
+
 static bool aligned(const void* p, size_t a) { return (reinterpret_cast<uintptr_t>(p) % a) == 0; }
 
 int cls_classify(cls_engine* e, uint32_t table_id, const cls_pkt_soa* pk, uint64_t n,
@@ -272,8 +274,14 @@ int cls_classify(cls_engine* e, uint32_t table_id, const cls_pkt_soa* pk, uint64
     cfg.stream = s;
     const bool use_cls = t->has_cls && !(flags & CLS_F_FORCE_LINEAR);
     int per_cu = 2;
-    if (use_cls && t->lds_resident)
-        per_cu = std::max(1, std::min(2, int(max_lds_bytes() / std::max<uint32_t>(1, t->img.lds_bytes))));
+    if (use_cls) {
+        const int by_threads = 2048 / cls_block();
+        per_cu = by_threads;
+        if (t->lds_resident)
+            per_cu = std::max(1, std::min(by_threads, int(max_lds_bytes() / std::max<uint32_t>(1, t->img.lds_bytes))));
+        if (const char* w = std::getenv("CONTIVCLS_WG_PER_CU"))   // diagnostics
+            per_cu = std::max(1, std::atoi(w));
+    }
     const uint64_t want = (n + 4ull * 1024 - 1) / (4ull * 1024);
     cfg.grid = int(std::max<uint64_t>(1, std::min<uint64_t>(uint64_t(e->n_cu) * per_cu, want)));
 
@@ -307,7 +315,8 @@ int cls_classify(cls_engine* e, uint32_t table_id, const cls_pkt_soa* pk, uint64
             cd.n_lin = uint32_t(t->lin4.size());
             cd.n_rules = t->n_rules;
             cd.mode = t->img.mode;
-            cd.default_class = t->img.default_class;
+            cd.default_row = t->img.default_row;
+            cd.row_bytes = t->img.row_bytes;
             cd.n_hash = t->img.n_hash;
             cd.list_mode = t->img.list_mode;
             cd.bv_steps = std::max(t->img.bv_steps_d, t->img.bv_steps_p);  // mode 2: Sd
@@ -319,14 +328,18 @@ int cls_classify(cls_engine* e, uint32_t table_id, const cls_pkt_soa* pk, uint64
                 cd.hash_mask[i] = t->img.hash_mask[i];
                 cd.hash_shift[i] = t->img.hash_shift[i];
                 cd.hash_cap[i] = t->img.hash_cap[i];
+                cd.hash_mul[i] = t->img.hash_mul[i];
+                cd.hash_shift1[i] = 32u - 2u * (32u - t->img.hash_shift[i]);
                 cd.off_hash[i] = t->img.off_hash[i];
             }
-            // diagnostics: CONTIVCLS_ABLATE=bits skips kernel stages (1 counters,
-            // 2 candidate scan, 4 source lookup, 8 verdict store) -- results are wrong
-            const char* ab = std::getenv("CONTIVCLS_ABLATE");
-            cd.ablate = ab ? uint32_t(std::strtoul(ab, nullptr, 0)) : 0u;
-            HIPC(e, launch_classify4_cls(cd, p, d_verdict, t->d_slot.as<unsigned long long>(),
-                                         t->lds_resident, vec, cfg));
+            // the kernel indexes packets with 32-bit offsets: chunks of 2^30
+            for (uint64_t off = 0; off < n; off += kClsChunk) {
+                const uint64_t m = std::min<uint64_t>(kClsChunk, n - off);
+                const Pkts4 pc{p.src + off, p.dst + off, p.dport + off, p.proto + off, m};
+                HIPC(e, launch_classify4_cls(cd, pc, d_verdict ? d_verdict + off : nullptr,
+                                             t->d_slot.as<unsigned long long>(), t->lds_resident, vec,
+                                             cfg));
+            }
         } else {
             const uint32_t base = t->has_cls ? t->img.n_ctr : 0;
             HIPC(e, launch_classify4_linear(t->d_lin4.as<LinRule4>(), uint32_t(t->lin4.size()), t->n_rules, p,
@@ -596,7 +609,7 @@ int cls_compile_v4(const cls_rule* rules, uint32_t n, void* blob, uint64_t cap, 
     cls_image_v4_header h;
     std::memset(&h, 0, sizeof h);
     h.magic = 0x434C5334u;
-    h.version = 1;
+    h.version = 2;
     h.n_rules = n;
     h.n_lin = uint32_t(lin.size());
     h.has_cls = has ? 1u : 0u;
@@ -616,10 +629,15 @@ int cls_compile_v4(const cls_rule* rules, uint32_t n, void* blob, uint64_t cap, 
         h.off_ptop = img.off_ptop;
         h.n_pclass = img.n_pclass;
         h.bv_wide = img.bv_wide;
+        h.row_bytes = img.row_bytes;
+        h.default_row = img.default_row;
+        h.n_hot = img.n_hot;
+        h.off_hot = img.off_hot;
         for (uint32_t i = 0; i < kMaxHashLens; ++i) {
             h.hash_mask[i] = img.hash_mask[i];
             h.hash_shift[i] = img.hash_shift[i];
             h.hash_cap[i] = img.hash_cap[i];
+            h.hash_mul[i] = img.hash_mul[i];
             h.off_hash[i] = img.off_hash[i];
         }
     }

@@ -4,12 +4,21 @@
 //   workgroup stages the read-only classifier image (compile.hpp, Cls4Image)
 //   into LDS once with 16-B loads, zeroes its LDS slot counters, then streams
 //   packets: 4 packets per lane per step with 16-B (src, dst), 8-B (dport) and
-//   4-B (proto) coalesced loads and one 4-B verdict store.  Per packet:
-//   branch-free binary search of the source boundaries (LDS) -> class ->
-//   (class, protocol) cell -> scan of the cell's candidate templates (dst
-//   prefix + port range) to the first match.  One LDS atomic per packet
-//   counts the terminating slot; counters are flushed to global u64 slots
-//   once per workgroup.  Integer compare work only -- no MFMA.
+//   4-B (proto) coalesced non-temporal loads and one 4-B verdict store, the
+//   next step's loads in flight during this step's lookups.  Per packet:
+//   source lookup (cuckoo hash LPM or interval search) -> the (class,
+//   protocol) cell -> the cell's candidate list evaluated against dst address
+//   and dst port (list modes 0-3, compile.hpp) -> verdict and the terminating
+//   slot.  One LDS atomic per packet counts the slot; counters are flushed to
+//   global u64 slots once per workgroup.  Integer compare work only -- no MFMA.
+//
+//   Cost model (measured on MI355X, config 3): the kernel is bound by VALU
+//   issue plus LDS bank conflicts, ~0.006 ms per VALU op per packet and
+//   ~0.03 ms per LDS read per packet at 256 Mi packets, both above the HBM
+//   stream's 0.53 ms floor.  So LDS is addressed with absolute 32-bit
+//   addresses (no base add), table values are stored pre-scaled to the byte
+//   addresses the next lookup needs, and list mode 3 searches with a single
+//   state word per packet.
 // classify4_linear -- the ballot kernel: every lane walks the rule list in
 //   order with wave-uniform (scalar) rule loads and the wave leaves as soon
 //   as the ballot of unfinished lanes is empty.  Small tables, GPU cross-check,
@@ -24,9 +33,74 @@ namespace cls {
 
 namespace {
 
-constexpr int kBlock = 1024;
+constexpr int kBlock = 1024;      // linear kernel
+#ifndef CLS_BLOCK
+#define CLS_BLOCK 1024
+#endif
+constexpr int kClsBlock = CLS_BLOCK;   // classifier workgroup (one LDS image per workgroup)
 constexpr int kLdsMax = 160 * 1024;
 constexpr uint32_t kLinLdsCounters = 16384;  // linear kernel: LDS counters up to R+1 <= this
+
+// Streamed packet fields are read once and verdicts written once: non-temporal
+// loads/stores keep them from churning L2 / the Infinity Cache (measured on
+// MI355X with tools/stream_bench.hip: 0.53 ms vs 0.61 ms for 256 Mi packets).
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+typedef uint32_t v2u __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint4 ldnt(const uint4* p) {
+    const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ uint2 ldnt(const uint2* p) {
+    const v2u v = __builtin_nontemporal_load(reinterpret_cast<const v2u*>(p));
+    return make_uint2(v.x, v.y);
+}
+__device__ __forceinline__ uint32_t ldnt(const uint32_t* p) { return __builtin_nontemporal_load(p); }
+__device__ __forceinline__ void stnt(uint32_t v, uint32_t* p) { __builtin_nontemporal_store(v, p); }
+// element i of a streamed array by 32-bit byte offset: SGPR base + VGPR offset
+template <typename T>
+__device__ __forceinline__ const T* at(const T* base, uint32_t i) {
+    return reinterpret_cast<const T*>(reinterpret_cast<const char*>(base) + i * uint32_t(sizeof(T)));
+}
+
+// The classifier image, read either from LDS (staged at LDS address 0: the
+// kernel has no static __shared__ data, so its dynamic LDS starts there) by
+// absolute 32-bit address -- ds_read with no base add -- or, for images too
+// large for LDS, from global memory.
+#pragma clang diagnostic ignored "-Wint-to-pointer-cast"   // 32-bit LDS addresses
+typedef const __attribute__((address_space(3))) uint8_t* lds8_t;
+typedef const __attribute__((address_space(3))) uint16_t* lds16_t;
+typedef const __attribute__((address_space(3))) uint32_t* lds32_t;
+typedef const __attribute__((address_space(3))) v2u* lds64_t;
+typedef const __attribute__((address_space(3))) v4u* lds128_t;
+template <bool kLds>
+struct Img {
+    const uint8_t* g;
+    __device__ __forceinline__ uint32_t u8(uint32_t a) const {
+        if constexpr (kLds) return *lds8_t(a); else return g[a];
+    }
+    __device__ __forceinline__ uint32_t u16(uint32_t a) const {
+        if constexpr (kLds) return *lds16_t(a); else return *reinterpret_cast<const uint16_t*>(g + a);
+    }
+    __device__ __forceinline__ uint32_t u32(uint32_t a) const {
+        if constexpr (kLds) return *lds32_t(a); else return *reinterpret_cast<const uint32_t*>(g + a);
+    }
+    __device__ __forceinline__ uint2 u64(uint32_t a) const {
+        if constexpr (kLds) {
+            const v2u v = *lds64_t(a);
+            return make_uint2(v.x, v.y);
+        } else {
+            return *reinterpret_cast<const uint2*>(g + a);
+        }
+    }
+    __device__ __forceinline__ uint4 u128(uint32_t a) const {
+        if constexpr (kLds) {
+            const v4u v = *lds128_t(a);
+            return make_uint4(v.x, v.y, v.z, v.w);
+        } else {
+            return *reinterpret_cast<const uint4*>(g + a);
+        }
+    }
+};
 
 __device__ __forceinline__ bool port_in(uint32_t dport, uint32_t pw) {
     return ((dport - (pw & 0xFFFFu)) & 0xFFFFu) <= (pw >> 16);
@@ -51,43 +125,43 @@ __device__ __forceinline__ void linear_one(const LinRule4* __restrict__ rules, u
     }
 }
 
-// Source class of N packets, interleaved (N independent LDS chains per lane).
-template <int N, int kMode>
-__device__ __forceinline__ void src_class(const uint8_t* base, const Cls4Dev& t,
-                                          const uint32_t (&src)[N], uint32_t (&cls)[N]) {
+// Source lookup of N packets, interleaved (N independent LDS chains per lane).
+// Result: the byte address of the packet's class row of cells.
+template <int N, bool kLds, int kMode>
+__device__ __forceinline__ void src_row(const Img<kLds>& im, const Cls4Dev& t,
+                                        const uint32_t (&src)[N], uint32_t (&row)[N]) {
     if constexpr (kMode == 1) {
-        // hash LPM: one cuckoo probe pair per prefix length, lengths ascending so
-        // the longest hit wins
+        // Hash LPM: one cuckoo probe pair per prefix length, lengths ascending
+        // so the longest hit wins.  Entries {key, row}; empty slots hold keys
+        // that never probe them, so a key compare is the whole hit test.  The
+        // parameters are indexed by constants: loaded into SGPRs once.
 #pragma unroll
-        for (int q = 0; q < N; ++q) cls[q] = t.default_class;
-        // Constant indices into the kernel arguments: the parameters are loaded
-        // into SGPRs once, outside the packet loop.  (A runtime index would
-        // re-issue s_load + s_waitcnt lgkmcnt(0) every step, which also drains
-        // the previous step's LDS counter atomics.)
+        for (int q = 0; q < N; ++q) row[q] = t.default_row;
 #pragma unroll
         for (uint32_t i = 0; i < kMaxHashLens; ++i) {
             if (i >= t.n_hash) break;
-            const uint2* __restrict__ tab = reinterpret_cast<const uint2*>(base + t.off_hash[i]);
-            const uint32_t mask = t.hash_mask[i], shift = t.hash_shift[i], cap = t.hash_cap[i];
+            // one multiply per key: table 0 probes the top L bits of key x
+            // mul, table 1 the next L bits (compile.hpp lpm_h0 / lpm_h1)
+            const uint32_t tab = t.off_hash[i], mask = t.hash_mask[i], mul = t.hash_mul[i];
+            const uint32_t s0 = t.hash_shift[i], s1 = t.hash_shift1[i], L = 32u - s0;
+            const uint32_t tab1 = __builtin_amdgcn_readfirstlane(tab + 8u * t.hash_cap[i]);
             uint2 e0[N], e1[N];
             uint32_t key[N];
 #pragma unroll
             for (int q = 0; q < N; ++q) {
                 key[q] = src[q] & mask;
-                e0[q] = tab[lpm_h0(key[q], shift)];
-                e1[q] = tab[cap + lpm_h1(key[q], shift)];
+                const uint32_t h = key[q] * mul;
+                e0[q] = im.u64(tab + 8u * (h >> s0));
+                e1[q] = im.u64(tab1 + 8u * __builtin_amdgcn_ubfe(h, s1, L));
             }
 #pragma unroll
             for (int q = 0; q < N; ++q) {
-                // empty slots hold keys that never probe them: a key compare is
-                // the whole hit test (two compares, two selects)
-                cls[q] = e1[q].x == key[q] ? e1[q].y : cls[q];
-                cls[q] = e0[q].x == key[q] ? e0[q].y : cls[q];
+                row[q] = e1[q].x == key[q] ? e1[q].y : row[q];
+                row[q] = e0[q].x == key[q] ? e0[q].y : row[q];
             }
         }
     } else {
         // branch-free binary search over the padded interval boundaries
-        const uint32_t* __restrict__ b = reinterpret_cast<const uint32_t*>(base + t.off_bounds);
         uint32_t k[N];
 #pragma unroll
         for (int q = 0; q < N; ++q) k[q] = 0;
@@ -96,109 +170,115 @@ __device__ __forceinline__ void src_class(const uint8_t* base, const Cls4Dev& t,
 #pragma unroll
             for (int q = 0; q < N; ++q) {
                 const uint32_t c = k[q] + s;
-                k[q] = (b[c] <= src[q]) ? c : k[q];
+                k[q] = (im.u32(t.off_bounds + 4u * c) <= src[q]) ? c : k[q];
             }
         }
-        const uint16_t* __restrict__ ic = reinterpret_cast<const uint16_t*>(base + t.off_iclass);
 #pragma unroll
-        for (int q = 0; q < N; ++q) cls[q] = ic[k[q]];
+        for (int q = 0; q < N; ++q)
+            row[q] = t.off_cells + im.u16(t.off_iclass + 2u * k[q]) * t.row_bytes;
     }
 }
 
 // First match of N packets (protocols 0-2) against their cells' candidate
-// lists.  The N scans advance in lockstep with predication: a finished packet
-// keeps re-reading a valid entry instead of branching, so the lane issues N
-// independent LDS reads per step.
-template <int N, int kMode, int kList>
-__device__ __forceinline__ void classify_n(const uint8_t* base, const Cls4Dev& t,
+// lists: verdict (ACLAction) and the terminating counter slot (0 = default
+// DENY, aclengine_mock.go:667).
+template <int N, bool kLds, int kMode, int kList>
+__device__ __forceinline__ void classify_n(const Img<kLds>& im, const Cls4Dev& t,
                                            const uint32_t (&src)[N], const uint32_t (&dst)[N],
                                            const uint32_t (&dport)[N], const uint32_t (&proto)[N],
                                            uint32_t (&res)[N], uint32_t (&slot)[N]) {
     uint32_t pc[N];
-    if constexpr (kList == 2) {
-        // global port class (list mode 2): top[port >> 8] = sub-table offset |
-        // base class << 20, class = base + sub[port & 255].  Independent of the
-        // source lookup: these reads go out together with the hash probes.
-        const uint32_t* __restrict__ ptop = reinterpret_cast<const uint32_t*>(base + t.off_ptop);
+    if constexpr (kList >= 2) {
+        // Global port class from the radix at image address 0: top[port >> 8]
+        // = byte address of a 256-byte window, class = window[port & 255]
+        // (class x 4 in mode 3).  Independent of the source lookup: these
+        // reads go out with the probes.
         uint32_t tp[N];
 #pragma unroll
-        for (int q = 0; q < N; ++q) tp[q] = ptop[dport[q] >> 8];
+        for (int q = 0; q < N; ++q) tp[q] = im.u32(((dport[q] >> 8) & 0xFFu) * 4u);
 #pragma unroll
-        for (int q = 0; q < N; ++q) pc[q] = (tp[q] >> 20) + base[(tp[q] & 0xFFFFFu) + (dport[q] & 0xFFu)];
+        for (int q = 0; q < N; ++q) pc[q] = im.u8(tp[q] + (dport[q] & 0xFFu));
     }
-    uint32_t cls[N];
-    if (t.ablate & 4u) {
+    uint32_t row[N];
+    src_row<N, kLds, kMode>(im, t, src, row);
+
+    if constexpr (kList == 3) {
+        // Port-filtered sublists.  cell = {pointer table byte address | counter
+        // base << 16} (slot base + 0: the cell's own no-match slot, counted as
+        // default DENY); the pointer table holds, per global port
+        // class, the initial search state of the sublist deciding first-match
+        // for that class: state = outcome | 8-B slot of the current entry << 16,
+        // outcome = result | (j + 1) << 2 (0: no entry, default DENY), so
+        // state >> 13 is the entry's byte address.  A probe of step i reads
+        // {start - 1, state} 8 << i bytes further and the state moves to the
+        // entry when start - 1 < dst: one shift, one compare, one select.
+        uint32_t cell[N], st[N];
 #pragma unroll
-        for (int q = 0; q < N; ++q) cls[q] = src[q] & 1u;
-    } else {
-        src_class<N, kMode>(base, t, src, cls);
-    }
-    const uint2* __restrict__ cells = reinterpret_cast<const uint2*>(base + t.off_cells);
-    if constexpr (kList >= 1) {
-        // Bit vectors: the entries of the cell's list that cover the packet's
-        // dst interval AND its port interval; the first such entry (lowest
-        // set bit) is the first match of the ordered list.  Both interval
-        // searches are branch-free, t.bv_steps steps for every lane, and
-        // track the byte address of the current interval: the step sizes
-        // are compile-time constants (unrolled, uniform guard), so a probe
-        // is one ds_read_b64 {bound, mask} with an immediate offset (b64 and
-        // b32 reads cost the same LDS cycles on gfx950: 2 x 32 lanes).
-        // cell = dst array offset / 8 | counter base << 16; an array is 2^S
-        // {bound, mask} pairs, the port array follows the dst array; the bound
-        // word of entry 0 (never probed) holds the result bits, lo / hi
-        const uint32_t* __restrict__ cells1 = reinterpret_cast<const uint32_t*>(base + t.off_cells);
+        for (int q = 0; q < N; ++q) cell[q] = im.u32(row[q] + 4u * min(proto[q], 2u));
+#pragma unroll
+        for (int q = 0; q < N; ++q) st[q] = im.u32((cell[q] & 0xFFFFu) + pc[q]);
+#pragma unroll
+        for (int i = int(kMaxBvSteps) - 1; i >= 0; --i) {
+            if (uint32_t(i) >= t.bv_steps) continue;
+            uint2 e[N];
+#pragma unroll
+            for (int q = 0; q < N; ++q) e[q] = im.u64((st[q] >> 13) + (8u << i));
+#pragma unroll
+            for (int q = 0; q < N; ++q) st[q] = e[q].x < dst[q] ? e[q].y : st[q];
+        }
+#pragma unroll
+        for (int q = 0; q < N; ++q) {
+            res[q] = st[q] & 3u;                                      // DENY when no entry
+            slot[q] = (cell[q] >> 16) + ((st[q] >> 2) & 63u);         // base + j + 1 (0: no entry)
+        }
+    } else if constexpr (kList >= 1) {
+        // Bit vectors: the entries of the cell's list covering the packet's dst
+        // interval AND its port interval; the lowest set bit is the first match.
+        // cell = block / 8 | counter base << 16.  Block: dst array of 2^S
+        // {interval start, mask} (entry 0, never probed, = {result bits lo,
+        // mask of interval 0}), then mode 1: the port array likewise (entry 0 =
+        // {result bits hi, mask}); mode 2: result bits hi, one mask per global
+        // port class.  The searches track the byte address of the current
+        // entry; the steps are constants, so a probe is one ds_read_b64 with an
+        // immediate offset.
         const uint32_t S = t.bv_steps;
         uint32_t cb[N], ad[N], ap[N], rlo[N], rhi[N], md[N], mp[N];
 #pragma unroll
         for (int q = 0; q < N; ++q) {
-            const uint32_t cell = cells1[cls[q] * 3u + min(proto[q], 2u)];
+            const uint32_t cell = im.u32(row[q] + 4u * min(proto[q], 2u));
             cb[q] = cell >> 16;
             ad[q] = (cell & 0xFFFFu) * 8u;
             ap[q] = ad[q] + (8u << S);
         }
-        if constexpr (kList == 1) {
 #pragma unroll
-            for (int q = 0; q < N; ++q) {
-                const uint2 d0 = *reinterpret_cast<const uint2*>(base + ad[q]);
-                const uint2 p0 = *reinterpret_cast<const uint2*>(base + ap[q]);
-                rlo[q] = d0.x;
-                md[q] = d0.y;
+        for (int q = 0; q < N; ++q) {
+            const uint2 d0 = im.u64(ad[q]);
+            rlo[q] = d0.x;
+            md[q] = d0.y;
+            if constexpr (kList == 1) {
+                const uint2 p0 = im.u64(ap[q]);
                 rhi[q] = p0.x;
                 mp[q] = p0.y;
-            }
-        } else {
-            // mode 2: after the dst array, the result-hi word and one mask per
-            // global port class
-#pragma unroll
-            for (int q = 0; q < N; ++q) {
-                const uint2 d0 = *reinterpret_cast<const uint2*>(base + ad[q]);
-                rlo[q] = d0.x;
-                md[q] = d0.y;
-                mp[q] = *reinterpret_cast<const uint32_t*>(base + ap[q] + 4u + pc[q] * 4u);
-                rhi[q] = 0u;
-            }
-            if (t.bv_wide) {
-#pragma unroll
-                for (int q = 0; q < N; ++q) rhi[q] = *reinterpret_cast<const uint32_t*>(base + ap[q]);
+            } else {
+                mp[q] = im.u32(ap[q] + 4u + pc[q] * 4u);
+                rhi[q] = t.bv_wide ? im.u32(ap[q]) : 0u;
             }
         }
-        if (!(t.ablate & 2u)) {
 #pragma unroll
-            for (int i = int(kMaxBvSteps) - 1; i >= 0; --i) {
-                if (uint32_t(i) >= S) continue;
-                const uint32_t step = 8u << i;
+        for (int i = int(kMaxBvSteps) - 1; i >= 0; --i) {
+            if (uint32_t(i) >= S) continue;
+            const uint32_t step = 8u << i;
 #pragma unroll
-                for (int q = 0; q < N; ++q) {
-                    const uint2 ed = *reinterpret_cast<const uint2*>(base + ad[q] + step);
-                    const bool td = ed.x <= dst[q];
-                    ad[q] = td ? ad[q] + step : ad[q];
-                    md[q] = td ? ed.y : md[q];
-                    if constexpr (kList == 1) {
-                        const uint2 ep = *reinterpret_cast<const uint2*>(base + ap[q] + step);
-                        const bool tp = ep.x <= dport[q];
-                        ap[q] = tp ? ap[q] + step : ap[q];
-                        mp[q] = tp ? ep.y : mp[q];
-                    }
+            for (int q = 0; q < N; ++q) {
+                const uint2 ed = im.u64(ad[q] + step);
+                const bool td = ed.x <= dst[q];
+                ad[q] = td ? ad[q] + step : ad[q];
+                md[q] = td ? ed.y : md[q];
+                if constexpr (kList == 1) {
+                    const uint2 ep = im.u64(ap[q] + step);
+                    const bool tq = ep.x <= dport[q];
+                    ap[q] = tq ? ap[q] + step : ap[q];
+                    mp[q] = tq ? ep.y : mp[q];
                 }
             }
         }
@@ -207,68 +287,66 @@ __device__ __forceinline__ void classify_n(const uint8_t* base, const Cls4Dev& t
             const uint32_t m = md[q] & mp[q];
             const uint32_t j = uint32_t(__ffs(m)) - 1u;               // m == 0 handled below
             const uint32_t bits = uint32_t(((uint64_t(rhi[q]) << 32) | rlo[q]) >> ((2u * j) & 63u));
-            res[q] = m ? (bits & 3u) : 0u;            // default DENY (aclengine_mock.go:667)
+            res[q] = m ? (bits & 3u) : 0u;
             slot[q] = m ? cb[q] + j : 0u;
         }
-        return;
-    }
-    const uint16_t* __restrict__ L = reinterpret_cast<const uint16_t*>(base + t.off_lists);
-    const uint4* __restrict__ T = reinterpret_cast<const uint4*>(base + t.off_tmpl);
-    uint32_t start[N], len[N], cb[N];
-    bool act[N];
-#pragma unroll
-    for (int q = 0; q < N; ++q) {
-        const uint32_t pp = proto[q] <= 2u ? proto[q] : 0u;
-        const uint2 cell = cells[cls[q] * 3u + pp];
-        start[q] = cell.x & 0xFFFFu;
-        len[q] = proto[q] <= 2u ? (cell.x >> 16) : 0u;
-        cb[q] = cell.y;
-        res[q] = 0u;      // default DENY (aclengine_mock.go:667)
-        slot[q] = 0u;     // slot 0 = default DENY counter
-        act[q] = len[q] != 0u;
-    }
-    bool any = false;
-#pragma unroll
-    for (int q = 0; q < N; ++q) any |= act[q];
-    if (t.ablate & 2u) {
-#pragma unroll
-        for (int q = 0; q < N; ++q) res[q] = len[q] & 3u;
-        any = false;
-    }
-    for (uint32_t j = 0; any; ++j) {
-        any = false;
+    } else {
+        // Template scan (lists > 32 entries): cell = {list start | length << 16,
+        // counter base}; entries are 16-bit ids of 16-B templates {dst, dst
+        // mask, port lo | width << 16, result}.  The N scans advance in
+        // lockstep with predication.
+        uint32_t start[N], len[N], cb[N];
+        bool act[N];
 #pragma unroll
         for (int q = 0; q < N; ++q) {
-            const uint32_t idx = start[q] + (act[q] ? j : 0u);
-            const uint4 tm = T[L[idx]];
-            const bool m = act[q] && ((dst[q] ^ tm.x) & tm.y) == 0u && port_in(dport[q], tm.z);
-            res[q] = m ? tm.w : res[q];
-            slot[q] = m ? cb[q] + j : slot[q];
-            act[q] = act[q] && !m && (j + 1u < len[q]);
-            any |= act[q];
+            const uint2 cell = im.u64(row[q] + 8u * min(proto[q], 2u));
+            start[q] = cell.x & 0xFFFFu;
+            len[q] = cell.x >> 16;
+            cb[q] = cell.y;
+            res[q] = 0u;
+            slot[q] = 0u;
+            act[q] = len[q] != 0u;
+        }
+        bool any = false;
+#pragma unroll
+        for (int q = 0; q < N; ++q) any |= act[q];
+        for (uint32_t j = 0; any; ++j) {
+            any = false;
+#pragma unroll
+            for (int q = 0; q < N; ++q) {
+                const uint32_t idx = start[q] + (act[q] ? j : 0u);
+                const uint4 tm = im.u128(t.off_tmpl + 16u * im.u16(t.off_lists + 2u * idx));
+                const bool m = act[q] && ((dst[q] ^ tm.x) & tm.y) == 0u && port_in(dport[q], tm.z);
+                res[q] = m ? tm.w : res[q];
+                slot[q] = m ? cb[q] + j : slot[q];
+                act[q] = act[q] && !m && (j + 1u < len[q]);
+                any |= act[q];
+            }
         }
     }
 }
 
-template <int N, bool kLds, int kMode>
-__device__ __forceinline__ void run_n(const uint8_t* base, const Cls4Dev& t, uint32_t* lctr,
-                                      unsigned long long* gslot, uint32_t hot_lane,
-                                      uint32_t& hot0, const uint32_t (&s)[N],
-                                      const uint32_t (&d)[N], const uint32_t (&dp)[N],
-                                      const uint32_t (&pr)[N], uint32_t (&res)[N]) {
+// Classify N packets and count their slots.  pr_any: some packet of the
+// group has a protocol outside TCP/UDP/ICMP.
+template <int N, bool kLds, int kMode, int kList>
+__device__ __forceinline__ void run_n(const Img<kLds>& im, const Cls4Dev& t, uint32_t hot_lane,
+                                      unsigned long long* gslot, uint32_t& hot0,
+                                      const uint32_t (&s)[N], const uint32_t (&d)[N],
+                                      const uint32_t (&dp)[N], const uint32_t (&pr)[N],
+                                      bool pr_any, uint32_t (&res)[N]) {
     uint32_t slot[N];
-    classify_n<N, (kMode & 1), (kMode >> 1)>(base, t, s, d, dp, pr, res, slot);
-    if (t.ablate & 1u) return;
+    classify_n<N, kLds, kMode, kList>(im, t, s, d, dp, pr, res, slot);
     // One LDS atomic per packet, no branch.  Hot slots (< n_hot: default DENY
     // and the cells of the widest source class) would have many lanes adding
-    // to one word -- serialised -- so they are counted in this lane's own
-    // row (hot_lane + slot * 64: one bank per lane) and folded at the end.
-    uint32_t idx[N];
+    // to one word -- serialised -- so they are counted in this lane's own row
+    // (hot_lane + slot * 256 bytes: one bank per lane) and folded at the end.
+    typedef __attribute__((address_space(3))) uint32_t* lctr_t;
+    uint32_t addr[N];
 #pragma unroll
     for (int q = 0; q < N; ++q) {
         if constexpr (kLds) {
-            idx[q] = slot[q] < t.n_hot ? hot_lane + slot[q] * 64u : slot[q];
-            atomicAdd(&lctr[idx[q]], 1u);
+            addr[q] = slot[q] < t.n_hot ? hot_lane + slot[q] * 256u : t.img_bytes + slot[q] * 4u;
+            __hip_atomic_fetch_add(lctr_t(addr[q]), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         } else if (pr[q] <= 2u) {
             if (slot[q] == 0u) ++hot0;
             else atomicAdd(&gslot[slot[q]], 1ull);
@@ -277,14 +355,13 @@ __device__ __forceinline__ void run_n(const uint8_t* base, const Cls4Dev& t, uin
     // Protocols outside TCP/UDP/ICMP fall through evalACL's switch
     // (aclengine_mock.go:508-664): networks alone decide.  Rare; taken per
     // wave only when some lane holds such a packet.
-    bool other = false;
-#pragma unroll
-    for (int q = 0; q < N; ++q) other |= pr[q] > 2u;
-    if (__any(other)) {
+    if (__any(pr_any)) {
 #pragma unroll
         for (int q = 0; q < N; ++q) {
             if (pr[q] > 2u) {
-                if constexpr (kLds) atomicSub(&lctr[idx[q]], 1u);   // undo the cell count
+                if constexpr (kLds)                                   // undo the cell count
+                    __hip_atomic_fetch_add(lctr_t(addr[q]), ~0u, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_WORKGROUP);
                 uint32_t rule;
                 linear_one(t.lin, t.n_lin, t.n_rules, s[q], d[q], dp[q], 3u, res[q], rule);
                 atomicAdd(&gslot[t.n_ctr + rule], 1ull);
@@ -293,99 +370,77 @@ __device__ __forceinline__ void run_n(const uint8_t* base, const Cls4Dev& t, uin
     }
 }
 
-#ifndef CLS_GROUPS
-#define CLS_GROUPS 1
-#endif
-constexpr int kG = CLS_GROUPS;     // 16-B packet groups per lane per step
-
-template <bool kLds, bool kVec, int kMode>
-__global__ __launch_bounds__(kBlock) void classify4_cls(Cls4Dev t, Pkts4 p, uint8_t* verdict,
-                                                        unsigned long long* gslot) {
+template <bool kLds, bool kVec, int kMode, int kList>
+__global__ __launch_bounds__(kClsBlock) void classify4_cls(Cls4Dev t, Pkts4 p, uint8_t* verdict,
+                                                           unsigned long long* gslot) {
     extern __shared__ uint4 smem[];
-    const uint8_t* base;
-    uint32_t* lctr = nullptr;
+    Img<kLds> im{reinterpret_cast<const uint8_t*>(t.img)};
     if constexpr (kLds) {
         const uint4* src4 = reinterpret_cast<const uint4*>(t.img);
         const uint32_t n4 = t.img_bytes / 16u;
         for (uint32_t i = threadIdx.x; i < n4; i += blockDim.x) smem[i] = src4[i];
-        lctr = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(smem) + t.img_bytes);
+        uint32_t* lctr = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(smem) + t.img_bytes);
         for (uint32_t i = threadIdx.x; i < (t.lds_bytes - t.img_bytes) / 4u; i += blockDim.x) lctr[i] = 0u;
         __syncthreads();
-        base = reinterpret_cast<const uint8_t*>(smem);
-    } else {
-        base = reinterpret_cast<const uint8_t*>(t.img);
     }
 
-    const uint64_t nthreads = uint64_t(gridDim.x) * blockDim.x;
-    const uint64_t tid = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    const uint32_t nthreads = gridDim.x * blockDim.x;
+    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t hot0 = 0;                                     // global-image variant only
-    const uint32_t hot_lane = (t.off_hot - t.img_bytes) / 4u + (threadIdx.x & 63u);
-    uint64_t tail_from = 0;
+    const uint32_t hot_lane = t.off_hot + 4u * (threadIdx.x & 63u);
+    uint32_t tail_from = 0;
     if constexpr (kVec) {
-        // kG x 4 packets per lane per step (kG contiguous 16-B groups), next
-        // step's loads issued before this step's lookups (software pipelining
-        // of the HBM stream)
-        constexpr int kN = 4 * kG;
-        const uint64_t nsteps = p.n / kN;
+        // 4 packets per lane per step, the next step's loads issued before this
+        // step's lookups.  32-bit indices: the host splits batches at 2^30.
+        const uint32_t nsteps = uint32_t(p.n / 4u);
         const uint4* S = reinterpret_cast<const uint4*>(p.src);
         const uint4* D = reinterpret_cast<const uint4*>(p.dst);
         const uint2* DP = reinterpret_cast<const uint2*>(p.dport);
         const uint32_t* PR = reinterpret_cast<const uint32_t*>(p.proto);
-        uint64_t g = tid;
-        uint4 s[kG], d[kG];
-        uint2 dp[kG];
-        uint32_t pr[kG];
-#pragma unroll
-        for (int k = 0; k < kG; ++k) {
-            s[k] = make_uint4(0, 0, 0, 0); d[k] = s[k]; dp[k] = make_uint2(0, 0); pr[k] = 0;
-        }
-        if (g < nsteps) {
-#pragma unroll
-            for (int k = 0; k < kG; ++k) {
-                s[k] = S[g * kG + k]; d[k] = D[g * kG + k]; dp[k] = DP[g * kG + k]; pr[k] = PR[g * kG + k];
+        struct Buf {
+            uint4 s, d;
+            uint2 dp;
+            uint32_t pr;
+        };
+        auto load = [&](Buf& b, uint32_t g) {
+            if (g < nsteps) {
+                b.s = ldnt(at(S, g)); b.d = ldnt(at(D, g)); b.dp = ldnt(at(DP, g)); b.pr = ldnt(at(PR, g));
             }
-        }
+        };
+        auto step = [&](const Buf& b, uint32_t g) {
+            const uint32_t sa[4] = {b.s.x, b.s.y, b.s.z, b.s.w}, da[4] = {b.d.x, b.d.y, b.d.z, b.d.w};
+            const uint32_t pa[4] = {b.dp.x & 0xFFFFu, b.dp.x >> 16, b.dp.y & 0xFFFFu, b.dp.y >> 16};
+            const uint32_t pr = b.pr;
+            const uint32_t ra[4] = {pr & 0xFFu, (pr >> 8) & 0xFFu, (pr >> 16) & 0xFFu, pr >> 24};
+            // some protocol byte > 2 (SWAR: bit 7 of each byte of x + 125,
+            // computed without inter-byte carries)
+            const bool other = ((pr | ((pr & 0x7F7F7F7Fu) + 0x7D7D7D7Du)) & 0x80808080u) != 0u;
+            uint32_t v[4];
+            run_n<4, kLds, kMode, kList>(im, t, hot_lane, gslot, hot0, sa, da, pa, ra, other, v);
+            if (verdict)
+                stnt(v[0] | (v[1] << 8) | (v[2] << 16) | (v[3] << 24),
+                     const_cast<uint32_t*>(at(reinterpret_cast<const uint32_t*>(verdict), g)));
+        };
+        // two buffers in turn: the next step's loads are in flight during this
+        // step's lookups, with no register copies between steps
+        Buf a, b;
+        uint32_t g = tid;
+        load(a, g);
         while (g < nsteps) {
-            const uint64_t gn = g + nthreads;
-            uint4 s2[kG], d2[kG];
-            uint2 dp2[kG];
-            uint32_t pr2[kG];
-#pragma unroll
-            for (int k = 0; k < kG; ++k) { s2[k] = s[k]; d2[k] = d[k]; dp2[k] = dp[k]; pr2[k] = pr[k]; }
-            if (gn < nsteps) {
-#pragma unroll
-                for (int k = 0; k < kG; ++k) {
-                    s2[k] = S[gn * kG + k]; d2[k] = D[gn * kG + k]; dp2[k] = DP[gn * kG + k]; pr2[k] = PR[gn * kG + k];
-                }
-            }
-            uint32_t sa[kN], da[kN], pa[kN], ra[kN];
-#pragma unroll
-            for (int k = 0; k < kG; ++k) {
-                sa[4 * k + 0] = s[k].x; sa[4 * k + 1] = s[k].y; sa[4 * k + 2] = s[k].z; sa[4 * k + 3] = s[k].w;
-                da[4 * k + 0] = d[k].x; da[4 * k + 1] = d[k].y; da[4 * k + 2] = d[k].z; da[4 * k + 3] = d[k].w;
-                pa[4 * k + 0] = dp[k].x & 0xFFFFu; pa[4 * k + 1] = dp[k].x >> 16;
-                pa[4 * k + 2] = dp[k].y & 0xFFFFu; pa[4 * k + 3] = dp[k].y >> 16;
-                ra[4 * k + 0] = pr[k] & 0xFFu; ra[4 * k + 1] = (pr[k] >> 8) & 0xFFu;
-                ra[4 * k + 2] = (pr[k] >> 16) & 0xFFu; ra[4 * k + 3] = pr[k] >> 24;
-            }
-            uint32_t v[kN];
-            run_n<kN, kLds, kMode>(base, t, lctr, gslot, hot_lane, hot0, sa, da, pa, ra, v);
-            if (verdict && !(t.ablate & 8u)) {
-#pragma unroll
-                for (int k = 0; k < kG; ++k)
-                    reinterpret_cast<uint32_t*>(verdict)[g * kG + k] =
-                        v[4 * k] | (v[4 * k + 1] << 8) | (v[4 * k + 2] << 16) | (v[4 * k + 3] << 24);
-            }
-#pragma unroll
-            for (int k = 0; k < kG; ++k) { s[k] = s2[k]; d[k] = d2[k]; dp[k] = dp2[k]; pr[k] = pr2[k]; }
-            g = gn;
+            load(b, g + nthreads);
+            step(a, g);
+            g += nthreads;
+            if (g >= nsteps) break;
+            load(a, g + nthreads);
+            step(b, g);
+            g += nthreads;
         }
-        tail_from = nsteps * kN;
+        tail_from = nsteps * 4u;
     }
-    for (uint64_t i = tail_from + tid; i < p.n; i += nthreads) {
+    for (uint32_t i = tail_from + tid; i < uint32_t(p.n); i += nthreads) {
         const uint32_t sa[1] = {p.src[i]}, da[1] = {p.dst[i]}, pa[1] = {p.dport[i]}, ra[1] = {p.proto[i]};
         uint32_t v[1];
-        run_n<1, kLds, kMode>(base, t, lctr, gslot, hot_lane, hot0, sa, da, pa, ra, v);
+        run_n<1, kLds, kMode, kList>(im, t, hot_lane, gslot, hot0, sa, da, pa, ra, ra[0] > 2u, v);
         if (verdict) verdict[i] = uint8_t(v[0]);
     }
 
@@ -395,7 +450,8 @@ __global__ __launch_bounds__(kBlock) void classify4_cls(Cls4Dev t, Pkts4 p, uint
     if constexpr (kLds) {
         __syncthreads();
         // fold the per-lane hot rows into their slots
-        const uint32_t* hrow = lctr + (t.off_hot - t.img_bytes) / 4u;
+        uint32_t* lctr = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(smem) + t.img_bytes);
+        const uint32_t* hrow = reinterpret_cast<const uint32_t*>(reinterpret_cast<uint8_t*>(smem) + t.off_hot);
         for (uint32_t i = threadIdx.x; i < t.n_hot * 64u; i += blockDim.x) {
             const uint32_t v = hrow[i];
             if (v) atomicAdd(&lctr[i >> 6], v);
@@ -568,38 +624,45 @@ __global__ void gen4_kernel(TrafficDev t, uint64_t first, uint64_t n, uint32_t* 
 }  // namespace
 
 int max_lds_bytes() { return kLdsMax; }
+int cls_block() { return kClsBlock; }
 
-template <bool kLds, bool kVec, int kMode>
+template <bool kLds, bool kVec, int kMode, int kList>
 static void launch_cls(const Cls4Dev& t, const Pkts4& p, uint8_t* verdict, unsigned long long* gslot,
                        const LaunchCfg& cfg) {
     const size_t lds = kLds ? t.lds_bytes : 0;
     if (kLds)
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(classify4_cls<kLds, kVec, kMode>),
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(classify4_cls<kLds, kVec, kMode, kList>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
-    hipLaunchKernelGGL((classify4_cls<kLds, kVec, kMode>), dim3(cfg.grid), dim3(kBlock), lds, cfg.stream,
-                       t, p, verdict, gslot);
+    hipLaunchKernelGGL((classify4_cls<kLds, kVec, kMode, kList>), dim3(cfg.grid), dim3(kClsBlock), lds,
+                       cfg.stream, t, p, verdict, gslot);
+}
+
+template <bool kLds, bool kVec>
+static void dispatch_cls(const Cls4Dev& t, const Pkts4& p, uint8_t* verdict, unsigned long long* gslot,
+                         const LaunchCfg& cfg) {
+    const int var = (t.mode == 1 ? 1 : 0) | (int(t.list_mode) << 1);
+    switch (var) {
+    case 0: launch_cls<kLds, kVec, 0, 0>(t, p, verdict, gslot, cfg); break;
+    case 1: launch_cls<kLds, kVec, 1, 0>(t, p, verdict, gslot, cfg); break;
+    case 2: launch_cls<kLds, kVec, 0, 1>(t, p, verdict, gslot, cfg); break;
+    case 3: launch_cls<kLds, kVec, 1, 1>(t, p, verdict, gslot, cfg); break;
+    case 4: launch_cls<kLds, kVec, 0, 2>(t, p, verdict, gslot, cfg); break;
+    case 5: launch_cls<kLds, kVec, 1, 2>(t, p, verdict, gslot, cfg); break;
+    case 6: launch_cls<kLds, kVec, 0, 3>(t, p, verdict, gslot, cfg); break;
+    default: launch_cls<kLds, kVec, 1, 3>(t, p, verdict, gslot, cfg); break;
+    }
 }
 
 hipError_t launch_classify4_cls(const Cls4Dev& t, const Pkts4& p, uint8_t* verdict,
                                 unsigned long long* gslot, bool lds_resident, bool vec,
                                 const LaunchCfg& cfg) {
-    // variant bits: 1 = hash LPM source lookup, 2 = bit-vector candidate lists
-    const int var = (t.mode == 1 ? 1 : 0) | (int(t.list_mode) << 1);
-#define CLS_DISPATCH(L, V)                                                       \
-    switch (var) {                                                               \
-    case 0: launch_cls<L, V, 0>(t, p, verdict, gslot, cfg); break;               \
-    case 1: launch_cls<L, V, 1>(t, p, verdict, gslot, cfg); break;               \
-    case 2: launch_cls<L, V, 2>(t, p, verdict, gslot, cfg); break;               \
-    case 3: launch_cls<L, V, 3>(t, p, verdict, gslot, cfg); break;               \
-    case 4: launch_cls<L, V, 4>(t, p, verdict, gslot, cfg); break;               \
-    default: launch_cls<L, V, 5>(t, p, verdict, gslot, cfg); break;              \
-    }
     if (lds_resident) {
-        if (vec) { CLS_DISPATCH(true, true) } else { CLS_DISPATCH(true, false) }
+        if (vec) dispatch_cls<true, true>(t, p, verdict, gslot, cfg);
+        else dispatch_cls<true, false>(t, p, verdict, gslot, cfg);
     } else {
-        if (vec) { CLS_DISPATCH(false, true) } else { CLS_DISPATCH(false, false) }
+        if (vec) dispatch_cls<false, true>(t, p, verdict, gslot, cfg);
+        else dispatch_cls<false, false>(t, p, verdict, gslot, cfg);
     }
-#undef CLS_DISPATCH
     return hipGetLastError();
 }
 

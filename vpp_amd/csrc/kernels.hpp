@@ -28,17 +28,18 @@ struct Cls4Dev {
     uint32_t n_lin;
     uint32_t n_rules;          // R: direct rule slots start at n_ctr
     uint32_t mode;             // 0 interval search, 1 hash LPM
-    uint32_t default_class;
+    uint32_t default_row;      // source lookup miss: byte address of the default class's cells
     uint32_t n_hash;
     uint32_t hash_mask[kMaxHashLens], hash_shift[kMaxHashLens], hash_cap[kMaxHashLens];
     uint32_t off_hash[kMaxHashLens];
-    uint32_t ablate;           // diagnostics only (CONTIVCLS_ABLATE): skip stages, wrong results
+    uint32_t hash_mul[kMaxHashLens], hash_shift1[kMaxHashLens];   // shift1 = 32 - 2 L
     uint32_t list_mode;        // 0 template scan, 1 bit vectors, 2 + global port classes
     uint32_t bv_steps;         // bit-vector search depth (max over lists, both dims)
     uint32_t n_hot;            // slots [0, n_hot) are counted in per-lane LDS rows
     uint32_t off_hot;          // byte offset of the rows (n_hot x 64 u32) in LDS
     uint32_t off_ptop;         // list mode 2: port radix
     uint32_t bv_wide;          // some list > 16 entries: result bits need the hi word
+    uint32_t row_bytes;        // cells per class row x cell size (interval search scales by it)
 };
 
 struct LaunchCfg {
@@ -82,5 +83,6 @@ hipError_t launch_gen4(const TrafficDev& t, uint64_t first, uint64_t n, uint32_t
                        hipStream_t s);
 
 int max_lds_bytes();             // per-workgroup LDS the classify kernel may use
+int cls_block();                 // classify workgroup size
 
 }  // namespace cls
