@@ -176,3 +176,23 @@ def random_traffic(seed: int, n: int, pool: PrefixPool, other_proto: bool = True
     proto = rng.choice(np.array(pvals, np.uint8), n, p=pw)
     sport = rng.integers(1024, 65536, n).astype(np.uint16)
     return dict(src=src, dst=dst, dport=dport, proto=proto, sport=sport)
+
+
+def single_port_acl(seed: int, n_rules: int = 120, n_prefixes: int = 8):
+    """Rules in renderACL's shape (acl_renderer.go:342-374): dst port a single
+    port or any (ContivRule.DestPort, 0 = any), no source port.  Port classes
+    then merge into few, and the compiler picks the hashed port lookup (list
+    mode 4)."""
+    rng = random.Random(seed)
+    pool = PrefixPool(rng, n_prefixes)
+    ports = [22, 53, 80, 161, 443, 8080, rng.randint(1, 65535), rng.randint(1, 65535)]
+    rules = []
+    for _ in range(n_rules):
+        a, ln = rng.choice(pool.v4)
+        src = "%s/%d" % (_v4(a), ln) if rng.random() < 0.8 else ""
+        da, dl = rng.choice(pool.v4)
+        dst = "%s/%d" % (_v4(da), dl) if rng.random() < 0.7 else ""
+        p = rng.choice(ports) if rng.random() < 0.7 else 0
+        rules.append(M.l4_rule(rng.choice([M.DENY, M.PERMIT, M.REFLECT]), src, dst,
+                               rng.choice(["tcp", "udp"]), 0, 65535, p, p if p else 65535))
+    return rules, pool

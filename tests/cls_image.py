@@ -153,6 +153,15 @@ class Image:
         tp = img[self.h.off_ptop // 4 + (dp >> 8)].astype(np.int64)
         return b8[tp + (dp & 0xFF)].astype(np.int64)
 
+    def _port_class4(self, dport):
+        """List modes 3, 4: merged port class x 4 (mode 4: perfect hash at 0)."""
+        if self.h.list_mode == 3:
+            return self._port_class(dport)
+        img = np.frombuffer(self._img, np.uint32).astype(np.int64)
+        dp = dport.astype(np.int64)
+        e = img[((dp * self.h.port_mul) & 0xFFFFFFFF) >> self.h.port_shift]
+        return np.where((e & 0xFFFF) == dp, e >> 16, self.h.port_dflt)
+
     def _classify_bv3(self, cls, src, dst, dport, proto, counters):
         """List mode 3 (port-filtered sublists): cell u32 {pointer table byte
         offset | counter base << 16}; table[port class] = initial state
@@ -162,7 +171,7 @@ class Image:
         img = np.frombuffer(self._img, np.uint32).astype(np.int64)
         pr = np.minimum(proto, 2).astype(np.int64)
         cell = img[(self.h.off_cells + cls * 12 + pr * 4) // 4]
-        pc4 = self._port_class(dport)                 # class x 4 in mode 3
+        pc4 = self._port_class4(dport)                # class x 4
         st = img[((cell & 0xFFFF) + pc4) // 4]
         d = dst.astype(np.int64)
         for i in range(int(self.h.bv_steps_d) - 1, -1, -1):
@@ -210,7 +219,7 @@ class Image:
             np.add.at(counters, rule, 1)
             return res.astype(np.uint8), counters
         cls = self.source_class(src)
-        if self.h.list_mode == 3:
+        if self.h.list_mode >= 3:
             return self._classify_bv3(cls, src, dst, dport, proto, counters)
         if self.h.list_mode >= 1:
             return self._classify_bv(cls, src, dst, dport, proto, counters)

@@ -134,3 +134,17 @@ def test_compact_lists_edge_addresses(seed):
     tr["src"][::7] = np.uint32(0xFFFFFFFF)
     img = _check(rules, tr)
     assert img.h.list_mode in (2, 3)
+
+
+@pytest.mark.parametrize("seed", range(6))
+@pytest.mark.parametrize("max_mode", [3, 4])
+def test_single_port_tables_hash_port_classes(monkeypatch, seed, max_mode):
+    """Rendered-shape tables (single dst ports): merged port classes, the
+    perfect-hash port lookup (list mode 4) and, capped, the radix (mode 3)."""
+    from aclgen import single_port_acl
+    monkeypatch.setenv("CONTIVCLS_LIST_MODE_MAX", str(max_mode))
+    rules, pool = single_port_acl(seed + 31, 70, n_prefixes=6 if seed % 2 else 20)
+    tr = random_traffic(seed, 5000, pool)
+    img = _check(rules, tr)
+    assert img.h.list_mode == max_mode
+    assert img.h.n_pclass <= 10

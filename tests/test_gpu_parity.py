@@ -70,14 +70,17 @@ def test_random_acls_both_kernels(eng, seed, n_rules, weird):
 
 
 VARIANTS = {  # kind -> (source lookup mode, list mode)
+    "hash_sph": (1, 4), "search_sph": (0, 4),
     "hash_cbv": (1, 3), "search_cbv": (0, 3),
     "hash_pc": (1, 2), "search_pc": (0, 2), "hash_bv": (1, 1), "search_bv": (0, 1),
     "hash_scan": (1, 0), "search_scan": (0, 0)}
 
 
 def variant_acl(kind, seed):
-    from aclgen import long_list_acl, many_ports_acl
+    from aclgen import long_list_acl, many_ports_acl, single_port_acl
     hashed = kind.startswith("hash")
+    if kind.endswith("_sph"):
+        return single_port_acl(seed * 13 + 1, 90, n_prefixes=3 if hashed else 24)
     if kind.endswith("scan"):
         return long_list_acl(seed + 70, 300, n_src=3 if hashed else 30)
     if kind.endswith("_bv"):
@@ -89,9 +92,10 @@ def variant_acl(kind, seed):
 @pytest.mark.parametrize("seed", range(3))
 @pytest.mark.parametrize("kind", sorted(VARIANTS))
 def test_all_kernel_variants(eng, seed, kind, monkeypatch):
-    """The eight classifier variants (hash-LPM / interval-search source lookup
-    x compact bit vectors / bit vectors with global port classes / bit vectors
-    with per-list port search / template scan) against the oracle."""
+    """The ten classifier variants (hash-LPM / interval-search source lookup
+    x port-filtered sublists with hashed / radix port classes / bit vectors
+    with global port classes / bit vectors with per-list port search /
+    template scan) against the oracle."""
     if kind.endswith("_pc"):
         monkeypatch.setenv("CONTIVCLS_LIST_MODE_MAX", "2")
     from cls_image import Image, compile_blob

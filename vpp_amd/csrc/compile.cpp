@@ -394,23 +394,23 @@ BvDesc build_bv2(const std::vector<TmplKey>& ents, uint32_t Sd, const std::vecto
     return desc;
 }
 
-// Port -> class radix of mode 2: top[p >> 8] = sub-table byte offset (20 bits,
-// relative to the radix section) | base class << 20; class = base + sub[p & 255].
-// A 256-port chunk inside one class points at the shared all-zero sub-table.
 // Port -> class radix (list modes 2, 3): per 256-port chunk h, the byte offset
 // of a 256-byte window holding class x `scale` for each port of the chunk.
 // Chunks inside one class point into any run of 256 equal bytes (shared).
-void port_radix(const std::vector<uint32_t>& G, std::vector<uint32_t>& toff,
-                std::vector<uint8_t>& subs, uint32_t scale) {
+void port_radix(const std::vector<uint32_t>& G, const std::vector<uint32_t>& cmap,
+                std::vector<uint32_t>& toff, std::vector<uint8_t>& subs, uint32_t scale) {
     toff.assign(256, 0);
     subs.clear();
-    auto cls_of = [&](uint32_t p) {
-        return uint32_t(std::upper_bound(G.begin(), G.end(), p) - G.begin()) - 1u;
+    auto cls_of = [&](uint32_t p) {   // cmap: global class -> stored class
+        return cmap[uint32_t(std::upper_bound(G.begin(), G.end(), p) - G.begin()) - 1u];
     };
     std::vector<int> uni(256, -1);
     for (uint32_t h = 0; h < 256; ++h) {
-        const uint32_t c0 = cls_of(h << 8), c1 = cls_of((h << 8) | 255u);
-        if (c1 != c0) {
+        // merged classes are not intervals: uniform means every port of the chunk
+        const uint32_t c0 = cls_of(h << 8);
+        bool uniform = true;
+        for (uint32_t x = 1; x < 256 && uniform; ++x) uniform = cls_of((h << 8) | x) == c0;
+        if (!uniform) {
             toff[h] = uint32_t(subs.size());
             for (uint32_t x = 0; x < 256; ++x) subs.push_back(uint8_t(cls_of((h << 8) | x) * scale));
         } else {
@@ -724,16 +724,42 @@ bool build_cls4(const std::vector<SemRule>& sem, uint32_t n_rules, Cls4Image& im
     uint32_t lmode = 0;
     if (all_bv && Sd <= kMaxBvSteps && G.size() <= kMaxPortClasses) lmode = 2;
     else if (all_bv && std::max(Sd, Sp) <= kMaxBvSteps) lmode = 1;
-    // list mode 3: port-filtered sublists (needs <= 64 port classes: the radix
-    // yields the class x 4 in a byte)
-    std::vector<std::vector<uint32_t>> sub_of;           // list -> sublist id per port class
+    // List modes 3, 4 work on merged port classes: global classes no list tells
+    // apart collapse (rendered ContivRules have single ports or "any", so every
+    // port between the table's ports lands in one class).  <= 64 merged classes:
+    // the port lookup yields class x 4 in a byte.
+    std::vector<uint32_t> pmerge, prep;                  // class -> merged, merged -> a port
+    std::vector<uint32_t> ident(G.size());
+    for (size_t p = 0; p < G.size(); ++p) ident[p] = uint32_t(p);
+    if (lmode == 2) {
+        std::map<std::vector<uint64_t>, uint32_t> sig_id;
+        for (size_t p = 0; p < G.size(); ++p) {
+            std::vector<uint64_t> sig;
+            sig.reserve(bv_ents.size());
+            for (const auto& ents : bv_ents) {
+                uint64_t m = 0;
+                for (size_t j = 0; j < ents.size(); ++j) {
+                    const uint32_t lo = ents[j].pw & 0xFFFFu, hi = lo + (ents[j].pw >> 16);
+                    if (G[p] >= lo && G[p] <= hi) m |= 1ull << j;
+                }
+                sig.push_back(m);
+            }
+            auto it = sig_id.find(sig);
+            if (it == sig_id.end()) {
+                it = sig_id.emplace(std::move(sig), uint32_t(prep.size())).first;
+                prep.push_back(G[p]);
+            }
+            pmerge.push_back(it->second);
+        }
+    }
+    std::vector<std::vector<uint32_t>> sub_of;           // list -> sublist id per merged class
     std::vector<Sublist> subs;
     uint32_t D = 0;
-    if (lmode == 2 && G.size() <= kMaxPortClasses3) {
+    if (lmode == 2 && prep.size() <= kMaxPortClasses3) {
         std::unordered_map<Sublist, uint32_t, SublistHash> sid;
         for (const auto& ents : bv_ents) {
             std::vector<uint32_t> ids;
-            for (Sublist& sl : port_sublists(ents, G)) {
+            for (Sublist& sl : port_sublists(ents, prep)) {
                 auto it = sid.find(sl);
                 if (it == sid.end()) {
                     it = sid.emplace(sl, uint32_t(subs.size())).first;
@@ -746,11 +772,62 @@ bool build_cls4(const std::vector<SemRule>& sem, uint32_t n_rules, Cls4Image& im
         }
         if (D <= kMaxBvSteps) lmode = 3;
     }
+    // List mode 4 = mode 3 with the port lookup as one probe of a perfect hash
+    // of the ports outside the most common merged class (<= kMaxPortHash such
+    // ports: rendered tables), instead of the two-level radix.
+    std::vector<uint32_t> phash;                          // entries {port | class x 4 << 16}
+    uint32_t phash_mul = 0, phash_shift = 0, phash_dflt = 0;
+    if (lmode == 3) {
+        auto mcls = [&](uint32_t x) {
+            return pmerge[uint32_t(std::upper_bound(G.begin(), G.end(), x) - G.begin()) - 1u];
+        };
+        std::vector<uint32_t> count(prep.size(), 0);
+        for (uint32_t x = 0; x < 65536; ++x) ++count[mcls(x)];
+        const uint32_t d = uint32_t(std::max_element(count.begin(), count.end()) - count.begin());
+        std::vector<uint32_t> special;
+        for (uint32_t x = 0; x < 65536 && special.size() <= kMaxPortHash; ++x)
+            if (mcls(x) != d) special.push_back(x);
+        if (special.size() <= kMaxPortHash) {
+            uint64_t z = 0x243F6A8885A308D3ull;           // splitmix64 stream of odd multipliers
+            for (uint32_t L = 4; L <= 11 && !phash_mul; ++L) {
+                if ((1u << L) < 2 * special.size()) continue;
+                for (int tries = 0; tries < 256 && !phash_mul; ++tries) {
+                    z += 0x9E3779B97F4A7C15ull;
+                    uint64_t m = z;
+                    m = (m ^ (m >> 30)) * 0xBF58476D1CE4E5B9ull;
+                    m = (m ^ (m >> 27)) * 0x94D049BB133111EBull;
+                    const uint32_t mul = uint32_t(m ^ (m >> 31)) | 1u;
+                    std::vector<uint8_t> used(size_t(1) << L, 0);
+                    bool ok = true;
+                    for (uint32_t x : special) {
+                        const uint32_t h = (x * mul) >> (32u - L);
+                        if (used[h]) { ok = false; break; }
+                        used[h] = 1;
+                    }
+                    if (!ok) continue;
+                    phash_mul = mul;
+                    phash_shift = 32u - L;
+                    phash.assign(size_t(1) << L, 0);
+                    for (uint32_t hslot = 0; hslot < (1u << L); ++hslot) {
+                        uint32_t y = 0;                   // a port that never probes this slot
+                        while (((y * mul) >> (32u - L)) == hslot) ++y;
+                        phash[hslot] = y;
+                    }
+                    for (uint32_t x : special) phash[(x * mul) >> (32u - L)] = x | ((mcls(x) * 4u) << 16);
+                }
+            }
+            if (phash_mul) {
+                phash_dflt = d * 4u;
+                lmode = 4;
+            }
+        }
+    }
     // diagnostics / tests: cap the list mode (CONTIVCLS_LIST_MODE_MAX)
     if (const char* mx = std::getenv("CONTIVCLS_LIST_MODE_MAX")) {
         const uint32_t cap = uint32_t(std::strtoul(mx, nullptr, 0));
         if (lmode > cap)
-            lmode = cap >= 2 && lmode >= 2 ? 2u : (cap >= 1 && std::max(Sd, Sp) <= kMaxBvSteps ? 1u : 0u);
+            lmode = cap >= 3 && lmode >= 3 ? 3u
+                  : cap >= 2 && lmode >= 2 ? 2u : (cap >= 1 && std::max(Sd, Sp) <= kMaxBvSteps ? 1u : 0u);
     }
 
     // mode 3 gives every cell its own "no entry matched" slot (rule R, default
@@ -771,12 +848,12 @@ bool build_cls4(const std::vector<SemRule>& sem, uint32_t n_rules, Cls4Image& im
         }
         if (ci == 0) hot3 = std::min<uint32_t>(uint32_t(ctr3.size()), kMaxHot);
     }
-    if (lmode == 3 && ctr3.size() > 0xFFFFu) lmode = 2;   // 16-bit cell field
+    if (lmode >= 3 && ctr3.size() > 0xFFFFu) lmode = 2;   // 16-bit cell field
 
     std::vector<uint32_t>& w = img.words;
     auto serialise = [&](uint32_t lm) {
-        img.ctr_rule = lm == 3 ? ctr3 : ctr_base_rule;
-        img.n_hot = lm == 3 ? hot3 : hot_base;
+        img.ctr_rule = lm >= 3 ? ctr3 : ctr_base_rule;
+        img.n_hot = lm >= 3 ? hot3 : hot_base;
         // lists
         bv.clear();
         bv_desc.clear();
@@ -786,19 +863,28 @@ bool build_cls4(const std::vector<SemRule>& sem, uint32_t n_rules, Cls4Image& im
             else if (lm == 1) bv_desc[bv_lists[i]] = build_bv(bv_ents[i], S, bv);
         }
         img.list_mode = lm;
-        img.bv_steps_d = lm == 3 ? D : lm == 2 ? Sd : S;
+        img.bv_steps_d = lm >= 3 ? D : lm == 2 ? Sd : S;
         img.bv_steps_p = lm >= 2 ? 0u : S;
-        img.n_pclass = lm >= 2 ? uint32_t(G.size()) : 0u;
+        img.n_pclass = lm >= 3 ? uint32_t(prep.size()) : lm == 2 ? uint32_t(G.size()) : 0u;
         img.bv_wide = 0;
         for (const auto& e : bv_ents) img.bv_wide |= e.size() > 16 ? 1u : 0u;
         // serialise (u32 words, each section 16 B aligned); sections the chosen
         // modes never read are left out of the LDS image
         w.clear();
         img.off_bounds = img.off_iclass = img.off_lists = img.off_tmpl = img.off_bv = img.off_ptop = 0;
-        if (lm >= 2) {
+        img.port_mul = img.port_shift = img.port_dflt = 0;
+        if (lm == 4) {
+            // port perfect hash at LDS address 0
+            w.assign(phash.begin(), phash.end());
+            w.resize(align4(uint32_t(w.size())));
+            img.port_mul = phash_mul;
+            img.port_shift = phash_shift;
+            img.port_dflt = phash_dflt;
+        } else if (lm >= 2) {
             // port radix at LDS address 0 (the kernel indexes it without a base):
             // top (256 x u32 = byte address of the chunk's window), then windows
-            port_radix(G, toff, psub, lm == 3 ? 4u : 1u);   // mode 3: class x 4
+            // of classes (mode 2: global classes; mode 3: merged classes x 4)
+            port_radix(G, lm == 3 ? pmerge : ident, toff, psub, lm == 3 ? 4u : 1u);
             img.off_ptop = 0;
             for (uint32_t h = 0; h < 256; ++h) w.push_back(1024u + toff[h]);
             w.resize(256 + (psub.size() + 3) / 4);
@@ -808,12 +894,12 @@ bool build_cls4(const std::vector<SemRule>& sem, uint32_t n_rules, Cls4Image& im
         std::unordered_map<uint32_t, uint32_t> ptr_off;  // list key -> byte offset of its pointer table
         std::vector<uint32_t> state0;                      // sublist -> initial state, region-relative
         std::vector<uint32_t> ptr_at;                      // word index of each list's pointer table
-        if (lm == 3) {
-            // pointer tables first: their byte offsets live in the cell's low 16 bits
+        if (lm >= 3) {
+            // pointer tables next: their byte offsets live in the cell's low 16 bits
             for (size_t i = 0; i < bv_lists.size(); ++i) {
                 ptr_off[bv_lists[i]] = uint32_t(w.size()) * 4;
                 ptr_at.push_back(uint32_t(w.size()));
-                w.resize(w.size() + G.size(), 0u);           // filled once the region is placed
+                w.resize(w.size() + prep.size(), 0u);        // filled once the region is placed
             }
             w.resize(align4(uint32_t(w.size())));
             img.sub_bytes = uint32_t(w.size()) * 4;
@@ -847,7 +933,7 @@ bool build_cls4(const std::vector<SemRule>& sem, uint32_t n_rules, Cls4Image& im
                 w.push_back(t.res);
             }
             w.resize(align4(uint32_t(w.size())));
-        } else if (lm == 3) {
+        } else if (lm >= 3) {
             // sublist cells: u32 {pointer table byte offset | counter base << 16},
             // the base being the cell's own no-match slot
             const size_t n_cells = size_t(n_classes) * 3;
@@ -876,7 +962,7 @@ bool build_cls4(const std::vector<SemRule>& sem, uint32_t n_rules, Cls4Image& im
             }
             w.resize(align4(uint32_t(w.size())));
         }
-        if (lm == 3) {
+        if (lm >= 3) {
             // Sublist region, 8-B slots.  A sublist of n intervals and depth s
             // (2^s >= n) sits at slot A: entries 1 .. n-1 in slots A+1 .. A+n-1
             // as {start - 1, outcome | (A + c) << 16}; the slots a probe may
@@ -942,7 +1028,7 @@ bool build_cls4(const std::vector<SemRule>& sem, uint32_t n_rules, Cls4Image& im
             img.off_bv = uint32_t(reg) * 4;
             if (r0 + kind.size() > 0x10000u) img.sub_bytes = 0xFFFFFFFFu;   // 16-bit slot field
             for (size_t i = 0; i < bv_lists.size(); ++i)
-                for (size_t p = 0; p < G.size(); ++p) w[ptr_at[i] + p] = state0[sub_of[i][p]];
+                for (size_t p = 0; p < prep.size(); ++p) w[ptr_at[i] + p] = state0[sub_of[i][p]];
             w.resize(align4(uint32_t(w.size())));
         }
         img.img_bytes = uint32_t(w.size()) * 4;
@@ -960,9 +1046,9 @@ bool build_cls4(const std::vector<SemRule>& sem, uint32_t n_rules, Cls4Image& im
         if (lmode == 0) break;
         // block offset field: 16 bits in 8-B units (modes 1, 2); mode 3: the
         // pointer tables in the first 64 KiB, sublist slots below 2^16
-        const bool cell_ok = lmode == 3 ? img.sub_bytes <= 0x10000u : img.img_bytes / 8u <= 0xFFFFu;
+        const bool cell_ok = lmode >= 3 ? img.sub_bytes <= 0x10000u : img.img_bytes / 8u <= 0xFFFFu;
         if (cell_ok && (lmode == 1 || img.lds_bytes <= kLdsBudget)) break;
-        lmode = lmode == 3 ? 2u : (lmode == 2 && std::max(Sd, Sp) <= kMaxBvSteps) ? 1u : 0u;
+        lmode = lmode >= 3 ? 2u : (lmode == 2 && std::max(Sd, Sp) <= kMaxBvSteps) ? 1u : 0u;
     }
     return true;
 }

@@ -42,7 +42,8 @@ constexpr uint32_t kMaxHot = 16;       // hot slots counted in per-lane LDS rows
 constexpr uint32_t kMaxBvSteps = 7;    // bit-vector search depth (lists <= 32 entries)
 constexpr uint32_t kMaxPortClasses = 256;  // list modes 2, 3: global port classes
 constexpr uint32_t kPortUniform = 1u << 19;  // port radix: chunk inside one class
-constexpr uint32_t kMaxPortClasses3 = 64;   // list mode 3: class x 4 fits the radix byte
+constexpr uint32_t kMaxPortClasses3 = 64;   // list modes 3, 4: class x 4 fits a byte
+constexpr uint32_t kMaxPortHash = 64;       // list mode 4: ports outside the default class
 constexpr uint32_t kLdsBudget = 160 * 1024;  // LDS of one classify workgroup
 // One multiply per key: p = key x mul; table 0 takes the top L bits of p,
 // table 1 the next L bits (L = log2 cap <= 16).  The compiler picks mul from a
@@ -125,7 +126,10 @@ struct Cls4Image {
     // classes, 3 = port-filtered sublists (per list and port class, the dst
     // intervals with their first-match outcome; searched with one state word)
     uint32_t list_mode = 0;
-    uint32_t sub_bytes = 0;        // mode 3: end of the pointer tables (< 64 KiB)
+    uint32_t sub_bytes = 0;        // modes 3, 4: end of the pointer tables (< 64 KiB)
+    // mode 4: port perfect hash at LDS 0: e = table[(port x mul) >> shift],
+    // class x 4 = (e & 0xFFFF) == port ? e >> 16 : port_dflt
+    uint32_t port_mul = 0, port_shift = 0, port_dflt = 0;
     uint32_t off_bv = 0;
     uint32_t bv_steps_d = 0, bv_steps_p = 0;   // largest search depths over the lists
     // list mode 2: global port classes (radix at off_ptop), result-hi word used

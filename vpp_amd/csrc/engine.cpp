@@ -317,6 +317,9 @@ int cls_classify(cls_engine* e, uint32_t table_id, const cls_pkt_soa* pk, uint64
             cd.mode = t->img.mode;
             cd.default_row = t->img.default_row;
             cd.row_bytes = t->img.row_bytes;
+            cd.port_mul = t->img.port_mul;
+            cd.port_shift = t->img.port_shift;
+            cd.port_dflt = t->img.port_dflt;
             cd.n_hash = t->img.n_hash;
             cd.list_mode = t->img.list_mode;
             cd.bv_steps = std::max(t->img.bv_steps_d, t->img.bv_steps_p);  // mode 2: Sd
@@ -630,6 +633,9 @@ int cls_compile_v4(const cls_rule* rules, uint32_t n, void* blob, uint64_t cap, 
         h.n_pclass = img.n_pclass;
         h.bv_wide = img.bv_wide;
         h.row_bytes = img.row_bytes;
+        h.port_mul = img.port_mul;
+        h.port_shift = img.port_shift;
+        h.port_dflt = img.port_dflt;
         h.default_row = img.default_row;
         h.n_hot = img.n_hot;
         h.off_hot = img.off_hot;

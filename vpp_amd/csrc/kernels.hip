@@ -188,7 +188,16 @@ __device__ __forceinline__ void classify_n(const Img<kLds>& im, const Cls4Dev& t
                                            const uint32_t (&dport)[N], const uint32_t (&proto)[N],
                                            uint32_t (&res)[N], uint32_t (&slot)[N]) {
     uint32_t pc[N];
-    if constexpr (kList >= 2) {
+    if constexpr (kList == 4) {
+        // Port class from the perfect hash at image address 0: one probe,
+        // e = {port | class x 4 << 16}; ports absent from it are in the
+        // default class (rendered tables: every port not named by a rule).
+#pragma unroll
+        for (int q = 0; q < N; ++q) {
+            const uint32_t e = im.u32(((dport[q] * t.port_mul) >> t.port_shift) * 4u);
+            pc[q] = (e & 0xFFFFu) == dport[q] ? e >> 16 : t.port_dflt;
+        }
+    } else if constexpr (kList >= 2) {
         // Global port class from the radix at image address 0: top[port >> 8]
         // = byte address of a 256-byte window, class = window[port & 255]
         // (class x 4 in mode 3).  Independent of the source lookup: these
@@ -202,7 +211,7 @@ __device__ __forceinline__ void classify_n(const Img<kLds>& im, const Cls4Dev& t
     uint32_t row[N];
     src_row<N, kLds, kMode>(im, t, src, row);
 
-    if constexpr (kList == 3) {
+    if constexpr (kList >= 3) {
         // Port-filtered sublists.  cell = {pointer table byte address | counter
         // base << 16} (slot base + 0: the cell's own no-match slot, counted as
         // default DENY); the pointer table holds, per global port
@@ -649,7 +658,9 @@ static void dispatch_cls(const Cls4Dev& t, const Pkts4& p, uint8_t* verdict, uns
     case 4: launch_cls<kLds, kVec, 0, 2>(t, p, verdict, gslot, cfg); break;
     case 5: launch_cls<kLds, kVec, 1, 2>(t, p, verdict, gslot, cfg); break;
     case 6: launch_cls<kLds, kVec, 0, 3>(t, p, verdict, gslot, cfg); break;
-    default: launch_cls<kLds, kVec, 1, 3>(t, p, verdict, gslot, cfg); break;
+    case 7: launch_cls<kLds, kVec, 1, 3>(t, p, verdict, gslot, cfg); break;
+    case 8: launch_cls<kLds, kVec, 0, 4>(t, p, verdict, gslot, cfg); break;
+    default: launch_cls<kLds, kVec, 1, 4>(t, p, verdict, gslot, cfg); break;
     }
 }
 

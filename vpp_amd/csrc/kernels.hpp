@@ -33,13 +33,15 @@ struct Cls4Dev {
     uint32_t hash_mask[kMaxHashLens], hash_shift[kMaxHashLens], hash_cap[kMaxHashLens];
     uint32_t off_hash[kMaxHashLens];
     uint32_t hash_mul[kMaxHashLens], hash_shift1[kMaxHashLens];   // shift1 = 32 - 2 L
-    uint32_t list_mode;        // 0 template scan, 1 bit vectors, 2 + global port classes
+    uint32_t list_mode;        // 0 template scan, 1 bit vectors, 2 + global port classes,
+                               // 3 port-filtered sublists, 4 + hashed port classes
     uint32_t bv_steps;         // bit-vector search depth (max over lists, both dims)
     uint32_t n_hot;            // slots [0, n_hot) are counted in per-lane LDS rows
     uint32_t off_hot;          // byte offset of the rows (n_hot x 64 u32) in LDS
     uint32_t off_ptop;         // list mode 2: port radix
     uint32_t bv_wide;          // some list > 16 entries: result bits need the hi word
     uint32_t row_bytes;        // cells per class row x cell size (interval search scales by it)
+    uint32_t port_mul, port_shift, port_dflt;   // list mode 4: port perfect hash at LDS 0
 };
 
 struct LaunchCfg {
