@@ -268,8 +268,8 @@ typedef struct cls_image_v4_header {
     uint32_t row_bytes;        /* a class's 3 cells at off_cells + class x row_bytes */
     uint32_t default_row;      /* hash LPM: cell row of default_class (hash entries hold rows) */
     uint32_t hash_mul[3];      /* hash LPM: p = key x mul; h0 = p >> shift, h1 = next log2(cap) bits */
-    uint32_t port_mul, port_shift, port_dflt;  /* list mode 4: e = u32 at ((port x mul) >> shift) x 4,
-                                  class x 4 = (e & 0xFFFF) == port ? e >> 16 : port_dflt */
+    uint32_t port_mul, port_mask4, port_dflt;  /* list mode 4: e = u32 at byte mulhi(port, mul) &
+                                  mask4, class x 4 = (e & 0xFFFF) == port ? e >> 16 : port_dflt */
     uint32_t n_hot, off_hot;   /* per-lane counter rows of the hot slots (LDS offsets) */
 } cls_image_v4_header;
 int cls_compile_v4(const cls_rule* rules, uint32_t n_rules, void* blob, uint64_t cap,

@@ -159,7 +159,7 @@ class Image:
             return self._port_class(dport)
         img = np.frombuffer(self._img, np.uint32).astype(np.int64)
         dp = dport.astype(np.int64)
-        e = img[((dp * self.h.port_mul) & 0xFFFFFFFF) >> self.h.port_shift]
+        e = img[(((dp * self.h.port_mul) >> 32) & self.h.port_mask4) // 4]
         return np.where((e & 0xFFFF) == dp, e >> 16, self.h.port_dflt)
 
     def _classify_bv3(self, cls, src, dst, dport, proto, counters):

@@ -84,7 +84,7 @@ class ImageHeader(C.Structure):
         ("list_mode", C.c_uint32), ("off_bv", C.c_uint32), ("bv_steps_d", C.c_uint32),
         ("bv_steps_p", C.c_uint32), ("off_ptop", C.c_uint32), ("n_pclass", C.c_uint32),
         ("bv_wide", C.c_uint32), ("row_bytes", C.c_uint32), ("default_row", C.c_uint32),
-        ("hash_mul", C.c_uint32 * 3), ("port_mul", C.c_uint32), ("port_shift", C.c_uint32),
+        ("hash_mul", C.c_uint32 * 3), ("port_mul", C.c_uint32), ("port_mask4", C.c_uint32),
         ("port_dflt", C.c_uint32),
         ("n_hot", C.c_uint32), ("off_hot", C.c_uint32)]
 

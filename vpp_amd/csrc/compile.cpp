@@ -776,7 +776,7 @@ bool build_cls4(const std::vector<SemRule>& sem, uint32_t n_rules, Cls4Image& im
     // of the ports outside the most common merged class (<= kMaxPortHash such
     // ports: rendered tables), instead of the two-level radix.
     std::vector<uint32_t> phash;                          // entries {port | class x 4 << 16}
-    uint32_t phash_mul = 0, phash_shift = 0, phash_dflt = 0;
+    uint32_t phash_mul = 0, phash_mask4 = 0, phash_dflt = 0;
     if (lmode == 3) {
         auto mcls = [&](uint32_t x) {
             return pmerge[uint32_t(std::upper_bound(G.begin(), G.end(), x) - G.begin()) - 1u];
@@ -796,24 +796,27 @@ bool build_cls4(const std::vector<SemRule>& sem, uint32_t n_rules, Cls4Image& im
                     uint64_t m = z;
                     m = (m ^ (m >> 30)) * 0xBF58476D1CE4E5B9ull;
                     m = (m ^ (m >> 27)) * 0x94D049BB133111EBull;
-                    const uint32_t mul = uint32_t(m ^ (m >> 31)) | 1u;
+                    const uint32_t mul = uint32_t(m ^ (m >> 31));
+                    const uint32_t mask4 = (4u << L) - 4u;
+                    // slot of port x: (mulhi(x, mul) & mask4) / 4
+                    auto slot = [&](uint32_t x) { return uint32_t((uint64_t(x) * mul) >> 32) & mask4; };
                     std::vector<uint8_t> used(size_t(1) << L, 0);
                     bool ok = true;
                     for (uint32_t x : special) {
-                        const uint32_t h = (x * mul) >> (32u - L);
+                        const uint32_t h = slot(x) / 4u;
                         if (used[h]) { ok = false; break; }
                         used[h] = 1;
                     }
                     if (!ok) continue;
                     phash_mul = mul;
-                    phash_shift = 32u - L;
+                    phash_mask4 = mask4;
                     phash.assign(size_t(1) << L, 0);
                     for (uint32_t hslot = 0; hslot < (1u << L); ++hslot) {
                         uint32_t y = 0;                   // a port that never probes this slot
-                        while (((y * mul) >> (32u - L)) == hslot) ++y;
+                        while (slot(y) / 4u == hslot) ++y;
                         phash[hslot] = y;
                     }
-                    for (uint32_t x : special) phash[(x * mul) >> (32u - L)] = x | ((mcls(x) * 4u) << 16);
+                    for (uint32_t x : special) phash[slot(x) / 4u] = x | ((mcls(x) * 4u) << 16);
                 }
             }
             if (phash_mul) {
@@ -872,13 +875,13 @@ bool build_cls4(const std::vector<SemRule>& sem, uint32_t n_rules, Cls4Image& im
         // modes never read are left out of the LDS image
         w.clear();
         img.off_bounds = img.off_iclass = img.off_lists = img.off_tmpl = img.off_bv = img.off_ptop = 0;
-        img.port_mul = img.port_shift = img.port_dflt = 0;
+        img.port_mul = img.port_mask4 = img.port_dflt = 0;
         if (lm == 4) {
             // port perfect hash at LDS address 0
             w.assign(phash.begin(), phash.end());
             w.resize(align4(uint32_t(w.size())));
             img.port_mul = phash_mul;
-            img.port_shift = phash_shift;
+            img.port_mask4 = phash_mask4;
             img.port_dflt = phash_dflt;
         } else if (lm >= 2) {
             // port radix at LDS address 0 (the kernel indexes it without a base):

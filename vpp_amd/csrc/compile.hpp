@@ -127,9 +127,9 @@ struct Cls4Image {
     // intervals with their first-match outcome; searched with one state word)
     uint32_t list_mode = 0;
     uint32_t sub_bytes = 0;        // modes 3, 4: end of the pointer tables (< 64 KiB)
-    // mode 4: port perfect hash at LDS 0: e = table[(port x mul) >> shift],
-    // class x 4 = (e & 0xFFFF) == port ? e >> 16 : port_dflt
-    uint32_t port_mul = 0, port_shift = 0, port_dflt = 0;
+    // mode 4: port perfect hash at LDS 0: e = u32 at byte mulhi(port, mul) &
+    // mask4, class x 4 = (e & 0xFFFF) == port ? e >> 16 : port_dflt
+    uint32_t port_mul = 0, port_mask4 = 0, port_dflt = 0;
     uint32_t off_bv = 0;
     uint32_t bv_steps_d = 0, bv_steps_p = 0;   // largest search depths over the lists
     // list mode 2: global port classes (radix at off_ptop), result-hi word used

@@ -53,6 +53,7 @@ struct Table {
     // counters: slots [0, n_ctr) of the classifier + [n_ctr, n_ctr + R + 1) direct rule slots
     uint32_t n_slots = 0;
     DevBuf d_slot, d_map, d_out;
+    DevBuf d_part;                 // per-workgroup slot counters of the LDS-resident kernel
     int kernel = 0;            // 0 linear, 1 classifier
     bool lds_resident = false;
 };
@@ -318,7 +319,7 @@ int cls_classify(cls_engine* e, uint32_t table_id, const cls_pkt_soa* pk, uint64
             cd.default_row = t->img.default_row;
             cd.row_bytes = t->img.row_bytes;
             cd.port_mul = t->img.port_mul;
-            cd.port_shift = t->img.port_shift;
+            cd.port_mask4 = t->img.port_mask4;
             cd.port_dflt = t->img.port_dflt;
             cd.n_hash = t->img.n_hash;
             cd.list_mode = t->img.list_mode;
@@ -327,6 +328,11 @@ int cls_classify(cls_engine* e, uint32_t table_id, const cls_pkt_soa* pk, uint64
             cd.off_ptop = t->img.off_ptop;
             cd.bv_wide = t->img.bv_wide;
             cd.off_hot = t->img.off_hot;
+            cd.part = nullptr;
+            if (t->lds_resident) {
+                HIPC(e, t->d_part.ensure(size_t(cfg.grid) * t->img.n_ctr * 4));
+                cd.part = t->d_part.as<uint32_t>();
+            }
             for (uint32_t i = 0; i < kMaxHashLens; ++i) {
                 cd.hash_mask[i] = t->img.hash_mask[i];
                 cd.hash_shift[i] = t->img.hash_shift[i];
@@ -342,6 +348,10 @@ int cls_classify(cls_engine* e, uint32_t table_id, const cls_pkt_soa* pk, uint64
                 HIPC(e, launch_classify4_cls(cd, pc, d_verdict ? d_verdict + off : nullptr,
                                              t->d_slot.as<unsigned long long>(), t->lds_resident, vec,
                                              cfg));
+                if (t->lds_resident && timing && off + m >= n) HIPC(e, hipEventRecord(e->ev1, s));
+                if (t->lds_resident)
+                    HIPC(e, launch_fold(cd.part, uint32_t(cfg.grid), t->img.n_ctr,
+                                        t->d_slot.as<unsigned long long>(), s));
             }
         } else {
             const uint32_t base = t->has_cls ? t->img.n_ctr : 0;
@@ -350,7 +360,9 @@ int cls_classify(cls_engine* e, uint32_t table_id, const cls_pkt_soa* pk, uint64
         }
     }
     if (timing) {
-        HIPC(e, hipEventRecord(e->ev1, s));
+        // ev1 brackets the classify kernel itself (recorded above, before the
+        // fold of the workgroup partials, when the image is LDS-resident)
+        if (!(n && use_cls && t->lds_resident)) HIPC(e, hipEventRecord(e->ev1, s));
         e->timed = true;
     }
     // slot counters -> rule counters
@@ -634,7 +646,7 @@ int cls_compile_v4(const cls_rule* rules, uint32_t n, void* blob, uint64_t cap, 
         h.bv_wide = img.bv_wide;
         h.row_bytes = img.row_bytes;
         h.port_mul = img.port_mul;
-        h.port_shift = img.port_shift;
+        h.port_mask4 = img.port_mask4;
         h.port_dflt = img.port_dflt;
         h.default_row = img.default_row;
         h.n_hot = img.n_hot;

@@ -29,6 +29,12 @@
 
 #include "kernels.hpp"
 
+// Diagnostics builds only (tools/build_ablate.sh): skip stages while keeping
+// their inputs live -- 1 slot counting, 2 sublist probes, 4 source lookup.
+#ifndef CLS_ABLATE
+#define CLS_ABLATE 0
+#endif
+
 namespace cls {
 
 namespace {
@@ -125,12 +131,25 @@ __device__ __forceinline__ void linear_one(const LinRule4* __restrict__ rules, u
     }
 }
 
+// One probe step I of the sublist search for N packets (list modes 3, 4).
+template <int I, int N, bool kLds>
+__device__ __forceinline__ void sub_step(const Img<kLds>& im, const uint32_t (&dst)[N],
+                                         uint32_t (&st)[N]) {
+    uint2 e[N];
+#pragma unroll
+    for (int q = 0; q < N; ++q) e[q] = im.u64((st[q] >> 13) + (8u << I));
+#pragma unroll
+    for (int q = 0; q < N; ++q) st[q] = e[q].x < dst[q] ? e[q].y : st[q];
+}
+
 // Source lookup of N packets, interleaved (N independent LDS chains per lane).
-// Result: the byte address of the packet's class row of cells.
+// Result: the byte address of the packet's class row of cells.  kMode: 0
+// interval search, 1 hash LPM over t.n_hash prefix lengths, 2 hash LPM over
+// exactly one length (pod /32s: the common rendered table; fewer live SGPRs).
 template <int N, bool kLds, int kMode>
 __device__ __forceinline__ void src_row(const Img<kLds>& im, const Cls4Dev& t,
                                         const uint32_t (&src)[N], uint32_t (&row)[N]) {
-    if constexpr (kMode == 1) {
+    if constexpr (kMode >= 1) {
         // Hash LPM: one cuckoo probe pair per prefix length, lengths ascending
         // so the longest hit wins.  Entries {key, row}; empty slots hold keys
         // that never probe them, so a key compare is the whole hit test.  The
@@ -138,8 +157,8 @@ __device__ __forceinline__ void src_row(const Img<kLds>& im, const Cls4Dev& t,
 #pragma unroll
         for (int q = 0; q < N; ++q) row[q] = t.default_row;
 #pragma unroll
-        for (uint32_t i = 0; i < kMaxHashLens; ++i) {
-            if (i >= t.n_hash) break;
+        for (uint32_t i = 0; i < (kMode == 2 ? 1u : kMaxHashLens); ++i) {
+            if (kMode == 1 && i >= t.n_hash) break;
             // one multiply per key: table 0 probes the top L bits of key x
             // mul, table 1 the next L bits (compile.hpp lpm_h0 / lpm_h1)
             const uint32_t tab = t.off_hash[i], mask = t.hash_mask[i], mul = t.hash_mul[i];
@@ -182,20 +201,25 @@ __device__ __forceinline__ void src_row(const Img<kLds>& im, const Cls4Dev& t,
 // First match of N packets (protocols 0-2) against their cells' candidate
 // lists: verdict (ACLAction) and the terminating counter slot (0 = default
 // DENY, aclengine_mock.go:667).
-template <int N, bool kLds, int kMode, int kList>
+template <int N, bool kLds, int kMode, int kList, int kD>
 __device__ __forceinline__ void classify_n(const Img<kLds>& im, const Cls4Dev& t,
                                            const uint32_t (&src)[N], const uint32_t (&dst)[N],
                                            const uint32_t (&dport)[N], const uint32_t (&proto)[N],
                                            uint32_t (&res)[N], uint32_t (&slot)[N]) {
     uint32_t pc[N];
     if constexpr (kList == 4) {
-        // Port class from the perfect hash at image address 0: one probe,
-        // e = {port | class x 4 << 16}; ports absent from it are in the
-        // default class (rendered tables: every port not named by a rule).
+        // Port class from the perfect hash at image address 0: one probe at
+        // byte address mulhi(port, mul) & mask4, e = {port | class x 4 << 16};
+        // ports absent from it are in the default class (rendered tables:
+        // every port no rule names).
 #pragma unroll
         for (int q = 0; q < N; ++q) {
-            const uint32_t e = im.u32(((dport[q] * t.port_mul) >> t.port_shift) * 4u);
-            pc[q] = (e & 0xFFFFu) == dport[q] ? e >> 16 : t.port_dflt;
+            if constexpr (CLS_ABLATE & 8) {
+                pc[q] = dport[q] & 0xFCu;
+            } else {
+                const uint32_t e = im.u32(__umulhi(dport[q], t.port_mul) & t.port_mask4);
+                pc[q] = (e & 0xFFFFu) == dport[q] ? e >> 16 : t.port_dflt;
+            }
         }
     } else if constexpr (kList >= 2) {
         // Global port class from the radix at image address 0: top[port >> 8]
@@ -209,7 +233,14 @@ __device__ __forceinline__ void classify_n(const Img<kLds>& im, const Cls4Dev& t
         for (int q = 0; q < N; ++q) pc[q] = im.u8(tp[q] + (dport[q] & 0xFFu));
     }
     uint32_t row[N];
-    src_row<N, kLds, kMode>(im, t, src, row);
+    if constexpr (CLS_ABLATE & 4) {
+#pragma unroll
+        for (int q = 0; q < N; ++q) row[q] = t.default_row + ((src[q] & 1u) ? 0u : 0u) + (src[q] & 0u);
+#pragma unroll
+        for (int q = 0; q < N; ++q) asm volatile("" :: "v"(src[q]));
+    } else {
+        src_row<N, kLds, kMode>(im, t, src, row);
+    }
 
     if constexpr (kList >= 3) {
         // Port-filtered sublists.  cell = {pointer table byte address | counter
@@ -222,18 +253,43 @@ __device__ __forceinline__ void classify_n(const Img<kLds>& im, const Cls4Dev& t
         // {start - 1, state} 8 << i bytes further and the state moves to the
         // entry when start - 1 < dst: one shift, one compare, one select.
         uint32_t cell[N], st[N];
+        if constexpr (CLS_ABLATE & 8) {
 #pragma unroll
-        for (int q = 0; q < N; ++q) cell[q] = im.u32(row[q] + 4u * min(proto[q], 2u));
+            for (int q = 0; q < N; ++q) {
+                cell[q] = row[q] + proto[q] + pc[q];
+                st[q] = cell[q] & 0x3Fu;
+            }
+        } else {
 #pragma unroll
-        for (int q = 0; q < N; ++q) st[q] = im.u32((cell[q] & 0xFFFFu) + pc[q]);
+            for (int q = 0; q < N; ++q) cell[q] = im.u32(row[q] + 4u * min(proto[q], 2u));
 #pragma unroll
-        for (int i = int(kMaxBvSteps) - 1; i >= 0; --i) {
-            if (uint32_t(i) >= t.bv_steps) continue;
-            uint2 e[N];
+            for (int q = 0; q < N; ++q) st[q] = im.u32((cell[q] & 0xFFFFu) + pc[q]);
+        }
+        // kD >= 0: the table's depth is a template argument -- straight-line
+        // probes.  kD < 0 (scalar tail, global-image variants): guarded steps
+        // (the compiler materialises those uniform guards as lane masks, a
+        // few VALU ops per step).
+        static_assert(kMaxBvSteps == 7, "step chain below");
+        if constexpr (CLS_ABLATE & 2) {
 #pragma unroll
-            for (int q = 0; q < N; ++q) e[q] = im.u64((st[q] >> 13) + (8u << i));
-#pragma unroll
-            for (int q = 0; q < N; ++q) st[q] = e[q].x < dst[q] ? e[q].y : st[q];
+            for (int q = 0; q < N; ++q) st[q] ^= dst[q] & 0x10000000u;   // keep dst live
+        } else {
+        if constexpr (kD > 6) sub_step<6>(im, dst, st);
+        if constexpr (kD > 5) sub_step<5>(im, dst, st);
+        if constexpr (kD > 4) sub_step<4>(im, dst, st);
+        if constexpr (kD > 3) sub_step<3>(im, dst, st);
+        if constexpr (kD > 2) sub_step<2>(im, dst, st);
+        if constexpr (kD > 1) sub_step<1>(im, dst, st);
+        if constexpr (kD > 0) sub_step<0>(im, dst, st);
+        if constexpr (kD < 0) {
+            if (t.bv_steps > 6) sub_step<6>(im, dst, st);
+            if (t.bv_steps > 5) sub_step<5>(im, dst, st);
+            if (t.bv_steps > 4) sub_step<4>(im, dst, st);
+            if (t.bv_steps > 3) sub_step<3>(im, dst, st);
+            if (t.bv_steps > 2) sub_step<2>(im, dst, st);
+            if (t.bv_steps > 1) sub_step<1>(im, dst, st);
+            if (t.bv_steps > 0) sub_step<0>(im, dst, st);
+        }
         }
 #pragma unroll
         for (int q = 0; q < N; ++q) {
@@ -337,14 +393,14 @@ __device__ __forceinline__ void classify_n(const Img<kLds>& im, const Cls4Dev& t
 
 // Classify N packets and count their slots.  pr_any: some packet of the
 // group has a protocol outside TCP/UDP/ICMP.
-template <int N, bool kLds, int kMode, int kList>
+template <int N, bool kLds, int kMode, int kList, int kD>
 __device__ __forceinline__ void run_n(const Img<kLds>& im, const Cls4Dev& t, uint32_t hot_lane,
                                       unsigned long long* gslot, uint32_t& hot0,
                                       const uint32_t (&s)[N], const uint32_t (&d)[N],
                                       const uint32_t (&dp)[N], const uint32_t (&pr)[N],
                                       bool pr_any, uint32_t (&res)[N]) {
     uint32_t slot[N];
-    classify_n<N, kLds, kMode, kList>(im, t, s, d, dp, pr, res, slot);
+    classify_n<N, kLds, kMode, kList, kD>(im, t, s, d, dp, pr, res, slot);
     // One LDS atomic per packet, no branch.  Hot slots (< n_hot: default DENY
     // and the cells of the widest source class) would have many lanes adding
     // to one word -- serialised -- so they are counted in this lane's own row
@@ -355,7 +411,8 @@ __device__ __forceinline__ void run_n(const Img<kLds>& im, const Cls4Dev& t, uin
     for (int q = 0; q < N; ++q) {
         if constexpr (kLds) {
             addr[q] = slot[q] < t.n_hot ? hot_lane + slot[q] * 256u : t.img_bytes + slot[q] * 4u;
-            __hip_atomic_fetch_add(lctr_t(addr[q]), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if constexpr (CLS_ABLATE & 1) asm volatile("" :: "v"(addr[q]));
+            else __hip_atomic_fetch_add(lctr_t(addr[q]), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         } else if (pr[q] <= 2u) {
             if (slot[q] == 0u) ++hot0;
             else atomicAdd(&gslot[slot[q]], 1ull);
@@ -379,7 +436,12 @@ __device__ __forceinline__ void run_n(const Img<kLds>& im, const Cls4Dev& t, uin
     }
 }
 
-template <bool kLds, bool kVec, int kMode, int kList>
+#ifndef CLS_GROUPS
+#define CLS_GROUPS 1
+#endif
+constexpr int kG = CLS_GROUPS;     // 16-B packet groups per lane per step
+
+template <bool kLds, bool kVec, int kMode, int kList, int kD>
 __global__ __launch_bounds__(kClsBlock) void classify4_cls(Cls4Dev t, Pkts4 p, uint8_t* verdict,
                                                            unsigned long long* gslot) {
     extern __shared__ uint4 smem[];
@@ -406,50 +468,90 @@ __global__ __launch_bounds__(kClsBlock) void classify4_cls(Cls4Dev t, Pkts4 p, u
         const uint4* D = reinterpret_cast<const uint4*>(p.dst);
         const uint2* DP = reinterpret_cast<const uint2*>(p.dport);
         const uint32_t* PR = reinterpret_cast<const uint32_t*>(p.proto);
+        // A step takes kG 16-B groups (4 packets each) per lane, group k at
+        // index g + k * nthreads: every load instruction stays coalesced, and
+        // the lookups of the 4 kG packets interleave (more LDS reads in flight
+        // per wave; 16 waves per CU is the ceiling with one LDS image per CU).
         struct Buf {
-            uint4 s, d;
-            uint2 dp;
-            uint32_t pr;
+            uint4 s[kG], d[kG];
+            uint2 dp[kG];
+            uint32_t pr[kG];
         };
-        auto load = [&](Buf& b, uint32_t g) {
-            if (g < nsteps) {
-                b.s = ldnt(at(S, g)); b.d = ldnt(at(D, g)); b.dp = ldnt(at(DP, g)); b.pr = ldnt(at(PR, g));
+        auto load = [&](Buf& b, uint32_t g, bool ok) {
+            if (ok) {
+#pragma unroll
+                for (int k = 0; k < kG; ++k) {
+                    const uint32_t gi = g + uint32_t(k) * nthreads;
+                    b.s[k] = ldnt(at(S, gi)); b.d[k] = ldnt(at(D, gi));
+                    b.dp[k] = ldnt(at(DP, gi)); b.pr[k] = ldnt(at(PR, gi));
+                }
             }
         };
         auto step = [&](const Buf& b, uint32_t g) {
-            const uint32_t sa[4] = {b.s.x, b.s.y, b.s.z, b.s.w}, da[4] = {b.d.x, b.d.y, b.d.z, b.d.w};
-            const uint32_t pa[4] = {b.dp.x & 0xFFFFu, b.dp.x >> 16, b.dp.y & 0xFFFFu, b.dp.y >> 16};
-            const uint32_t pr = b.pr;
-            const uint32_t ra[4] = {pr & 0xFFu, (pr >> 8) & 0xFFu, (pr >> 16) & 0xFFu, pr >> 24};
-            // some protocol byte > 2 (SWAR: bit 7 of each byte of x + 125,
-            // computed without inter-byte carries)
-            const bool other = ((pr | ((pr & 0x7F7F7F7Fu) + 0x7D7D7D7Du)) & 0x80808080u) != 0u;
-            uint32_t v[4];
-            run_n<4, kLds, kMode, kList>(im, t, hot_lane, gslot, hot0, sa, da, pa, ra, other, v);
-            if (verdict)
-                stnt(v[0] | (v[1] << 8) | (v[2] << 16) | (v[3] << 24),
-                     const_cast<uint32_t*>(at(reinterpret_cast<const uint32_t*>(verdict), g)));
+            constexpr int kN = 4 * kG;
+            uint32_t sa[kN], da[kN], pa[kN], ra[kN];
+            bool other = false;
+#pragma unroll
+            for (int k = 0; k < kG; ++k) {
+                sa[4 * k + 0] = b.s[k].x; sa[4 * k + 1] = b.s[k].y; sa[4 * k + 2] = b.s[k].z; sa[4 * k + 3] = b.s[k].w;
+                da[4 * k + 0] = b.d[k].x; da[4 * k + 1] = b.d[k].y; da[4 * k + 2] = b.d[k].z; da[4 * k + 3] = b.d[k].w;
+                pa[4 * k + 0] = b.dp[k].x & 0xFFFFu; pa[4 * k + 1] = b.dp[k].x >> 16;
+                pa[4 * k + 2] = b.dp[k].y & 0xFFFFu; pa[4 * k + 3] = b.dp[k].y >> 16;
+                const uint32_t pr = b.pr[k];
+                ra[4 * k + 0] = pr & 0xFFu; ra[4 * k + 1] = (pr >> 8) & 0xFFu;
+                ra[4 * k + 2] = (pr >> 16) & 0xFFu; ra[4 * k + 3] = pr >> 24;
+                // some protocol byte > 2 (SWAR: bit 7 of each byte of x + 125,
+                // computed without inter-byte carries)
+                other |= ((pr | ((pr & 0x7F7F7F7Fu) + 0x7D7D7D7Du)) & 0x80808080u) != 0u;
+            }
+            uint32_t v[kN];
+            run_n<kN, kLds, kMode, kList, kD>(im, t, hot_lane, gslot, hot0, sa, da, pa, ra, other, v);
+            if (verdict) {
+#pragma unroll
+                for (int k = 0; k < kG; ++k)
+                    stnt(v[4 * k] | (v[4 * k + 1] << 8) | (v[4 * k + 2] << 16) | (v[4 * k + 3] << 24),
+                         const_cast<uint32_t*>(at(reinterpret_cast<const uint32_t*>(verdict),
+                                                  g + uint32_t(k) * nthreads)));
+            }
         };
-        // two buffers in turn: the next step's loads are in flight during this
-        // step's lookups, with no register copies between steps
+        // Full steps over groups [0, nfull), two buffers in turn: the next
+        // step's loads are in flight during this step's lookups, with no
+        // register copies between steps.
+        const uint32_t span = nthreads * uint32_t(kG);
+        const uint32_t nfull = nsteps / span * span;
         Buf a, b;
         uint32_t g = tid;
-        load(a, g);
-        while (g < nsteps) {
-            load(b, g + nthreads);
+        load(a, g, g < nfull);
+        while (g < nfull) {
+            load(b, g + span, g + span < nfull);
             step(a, g);
-            g += nthreads;
-            if (g >= nsteps) break;
-            load(a, g + nthreads);
+            g += span;
+            if (g >= nfull) break;
+            load(a, g + span, g + span < nfull);
             step(b, g);
-            g += nthreads;
+            g += span;
+        }
+        // leftover groups one at a time
+        for (uint32_t gi = nfull + tid; gi < nsteps; gi += nthreads) {
+            const uint4 s4 = ldnt(at(S, gi)), d4 = ldnt(at(D, gi));
+            const uint2 p2 = ldnt(at(DP, gi));
+            const uint32_t pr = ldnt(at(PR, gi));
+            const uint32_t sa[4] = {s4.x, s4.y, s4.z, s4.w}, da[4] = {d4.x, d4.y, d4.z, d4.w};
+            const uint32_t pa[4] = {p2.x & 0xFFFFu, p2.x >> 16, p2.y & 0xFFFFu, p2.y >> 16};
+            const uint32_t ra[4] = {pr & 0xFFu, (pr >> 8) & 0xFFu, (pr >> 16) & 0xFFu, pr >> 24};
+            uint32_t v[4];
+            run_n<4, kLds, kMode, kList, -1>(im, t, hot_lane, gslot, hot0, sa, da, pa, ra,
+                                             ((pr | ((pr & 0x7F7F7F7Fu) + 0x7D7D7D7Du)) & 0x80808080u) != 0u, v);
+            if (verdict)
+                stnt(v[0] | (v[1] << 8) | (v[2] << 16) | (v[3] << 24),
+                     const_cast<uint32_t*>(at(reinterpret_cast<const uint32_t*>(verdict), gi)));
         }
         tail_from = nsteps * 4u;
     }
     for (uint32_t i = tail_from + tid; i < uint32_t(p.n); i += nthreads) {
         const uint32_t sa[1] = {p.src[i]}, da[1] = {p.dst[i]}, pa[1] = {p.dport[i]}, ra[1] = {p.proto[i]};
         uint32_t v[1];
-        run_n<1, kLds, kMode, kList>(im, t, hot_lane, gslot, hot0, sa, da, pa, ra, ra[0] > 2u, v);
+        run_n<1, kLds, kMode, kList, -1>(im, t, hot_lane, gslot, hot0, sa, da, pa, ra, ra[0] > 2u, v);
         if (verdict) verdict[i] = uint8_t(v[0]);
     }
 
@@ -466,11 +568,30 @@ __global__ __launch_bounds__(kClsBlock) void classify4_cls(Cls4Dev t, Pkts4 p, u
             if (v) atomicAdd(&lctr[i >> 6], v);
         }
         __syncthreads();
-        for (uint32_t i = threadIdx.x; i < t.n_ctr; i += blockDim.x) {
-            const uint32_t v = lctr[i];
-            if (v) atomicAdd(&gslot[i], (unsigned long long)v);
-        }
+        // This workgroup's slot counters, stored plainly into its own row of
+        // the partials (fold_kernel sums the rows): no global atomics from
+        // every workgroup onto the same addresses at the end of the launch.
+        uint32_t* part = t.part + size_t(blockIdx.x) * t.n_ctr;
+        for (uint32_t i = threadIdx.x; i < t.n_ctr; i += blockDim.x) part[i] = lctr[i];
     }
+}
+
+// gslot[i] += sum over the grid's rows of part[w][i].  Thread (slot i, row
+// group blockIdx.y) sums kFoldRows rows with independent coalesced loads and
+// adds once: rows / kFoldRows atomics per slot instead of one per workgroup.
+constexpr uint32_t kFoldRows = 16;
+__global__ void fold_kernel(const uint32_t* __restrict__ part, uint32_t rows, uint32_t n,
+                            unsigned long long* __restrict__ gslot) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t w0 = blockIdx.y * kFoldRows;
+    unsigned long long s64 = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kFoldRows; ++k) {
+        const uint32_t w = w0 + k;
+        if (w < rows) s64 += part[size_t(w) * n + i];
+    }
+    if (s64) atomicAdd(&gslot[i], s64);
 }
 
 __global__ __launch_bounds__(kBlock) void classify4_linear(const LinRule4* __restrict__ rules,
@@ -635,33 +756,54 @@ __global__ void gen4_kernel(TrafficDev t, uint64_t first, uint64_t n, uint32_t* 
 int max_lds_bytes() { return kLdsMax; }
 int cls_block() { return kClsBlock; }
 
+template <bool kLds, bool kVec, int kMode, int kList, int kD>
+static void launch_d(const Cls4Dev& t, const Pkts4& p, uint8_t* verdict, unsigned long long* gslot,
+                     const LaunchCfg& cfg) {
+    const size_t lds = kLds ? t.lds_bytes : 0;
+    if (kLds)
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(classify4_cls<kLds, kVec, kMode, kList, kD>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
+    hipLaunchKernelGGL((classify4_cls<kLds, kVec, kMode, kList, kD>), dim3(cfg.grid), dim3(kClsBlock), lds,
+                       cfg.stream, t, p, verdict, gslot);
+}
+
+// The hot variants (LDS-resident image, vector loads, sublist lists) are
+// specialised on the search depth; the others take it at run time.
 template <bool kLds, bool kVec, int kMode, int kList>
 static void launch_cls(const Cls4Dev& t, const Pkts4& p, uint8_t* verdict, unsigned long long* gslot,
                        const LaunchCfg& cfg) {
-    const size_t lds = kLds ? t.lds_bytes : 0;
-    if (kLds)
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(classify4_cls<kLds, kVec, kMode, kList>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
-    hipLaunchKernelGGL((classify4_cls<kLds, kVec, kMode, kList>), dim3(cfg.grid), dim3(kClsBlock), lds,
-                       cfg.stream, t, p, verdict, gslot);
+    if constexpr (kLds && kVec && kList >= 3) {
+        switch (t.bv_steps) {
+        case 0: launch_d<kLds, kVec, kMode, kList, 0>(t, p, verdict, gslot, cfg); return;
+        case 1: launch_d<kLds, kVec, kMode, kList, 1>(t, p, verdict, gslot, cfg); return;
+        case 2: launch_d<kLds, kVec, kMode, kList, 2>(t, p, verdict, gslot, cfg); return;
+        case 3: launch_d<kLds, kVec, kMode, kList, 3>(t, p, verdict, gslot, cfg); return;
+        case 4: launch_d<kLds, kVec, kMode, kList, 4>(t, p, verdict, gslot, cfg); return;
+        case 5: launch_d<kLds, kVec, kMode, kList, 5>(t, p, verdict, gslot, cfg); return;
+        default: break;
+        }
+    }
+    launch_d<kLds, kVec, kMode, kList, -1>(t, p, verdict, gslot, cfg);
 }
 
 template <bool kLds, bool kVec>
 static void dispatch_cls(const Cls4Dev& t, const Pkts4& p, uint8_t* verdict, unsigned long long* gslot,
                          const LaunchCfg& cfg) {
-    const int var = (t.mode == 1 ? 1 : 0) | (int(t.list_mode) << 1);
-    switch (var) {
-    case 0: launch_cls<kLds, kVec, 0, 0>(t, p, verdict, gslot, cfg); break;
-    case 1: launch_cls<kLds, kVec, 1, 0>(t, p, verdict, gslot, cfg); break;
-    case 2: launch_cls<kLds, kVec, 0, 1>(t, p, verdict, gslot, cfg); break;
-    case 3: launch_cls<kLds, kVec, 1, 1>(t, p, verdict, gslot, cfg); break;
-    case 4: launch_cls<kLds, kVec, 0, 2>(t, p, verdict, gslot, cfg); break;
-    case 5: launch_cls<kLds, kVec, 1, 2>(t, p, verdict, gslot, cfg); break;
-    case 6: launch_cls<kLds, kVec, 0, 3>(t, p, verdict, gslot, cfg); break;
-    case 7: launch_cls<kLds, kVec, 1, 3>(t, p, verdict, gslot, cfg); break;
-    case 8: launch_cls<kLds, kVec, 0, 4>(t, p, verdict, gslot, cfg); break;
-    default: launch_cls<kLds, kVec, 1, 4>(t, p, verdict, gslot, cfg); break;
+    // source lookup: 0 interval search, 1 hash LPM, 2 hash LPM with one length
+    const int src = t.mode != 1 ? 0 : t.n_hash == 1 ? 2 : 1;
+#define CLS_SRC_CASES(L)                                                                   \
+    case 3 * L + 0: launch_cls<kLds, kVec, 0, L>(t, p, verdict, gslot, cfg); break;        \
+    case 3 * L + 1: launch_cls<kLds, kVec, 1, L>(t, p, verdict, gslot, cfg); break;        \
+    case 3 * L + 2: launch_cls<kLds, kVec, 2, L>(t, p, verdict, gslot, cfg); break;
+    switch (src + 3 * int(t.list_mode)) {
+        CLS_SRC_CASES(0)
+        CLS_SRC_CASES(1)
+        CLS_SRC_CASES(2)
+        CLS_SRC_CASES(3)
+        CLS_SRC_CASES(4)
+    default: break;
     }
+#undef CLS_SRC_CASES
 }
 
 hipError_t launch_classify4_cls(const Cls4Dev& t, const Pkts4& p, uint8_t* verdict,
@@ -682,6 +824,14 @@ hipError_t launch_classify4_linear(const LinRule4* rules, uint32_t n_lin, uint32
                                    const LaunchCfg& cfg) {
     hipLaunchKernelGGL(classify4_linear, dim3(cfg.grid), dim3(kBlock), 0, cfg.stream, rules, n_lin,
                        n_rules, p, verdict, gslot);
+    return hipGetLastError();
+}
+
+hipError_t launch_fold(const uint32_t* part, uint32_t rows, uint32_t n, unsigned long long* gslot,
+                       hipStream_t s) {
+    if (n == 0 || rows == 0) return hipSuccess;
+    hipLaunchKernelGGL(fold_kernel, dim3((n + 255) / 256, (rows + kFoldRows - 1) / kFoldRows), dim3(256), 0, s,
+                       part, rows, n, gslot);
     return hipGetLastError();
 }
 

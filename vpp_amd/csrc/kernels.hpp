@@ -41,7 +41,8 @@ struct Cls4Dev {
     uint32_t off_ptop;         // list mode 2: port radix
     uint32_t bv_wide;          // some list > 16 entries: result bits need the hi word
     uint32_t row_bytes;        // cells per class row x cell size (interval search scales by it)
-    uint32_t port_mul, port_shift, port_dflt;   // list mode 4: port perfect hash at LDS 0
+    uint32_t port_mul, port_mask4, port_dflt;   // list mode 4: port perfect hash at LDS 0
+    uint32_t* part;            // LDS-resident image: per-workgroup slot counters [grid][n_ctr]
 };
 
 struct LaunchCfg {
@@ -56,6 +57,9 @@ hipError_t launch_classify4_cls(const Cls4Dev& t, const Pkts4& p, uint8_t* verdi
 hipError_t launch_classify4_linear(const LinRule4* rules, uint32_t n_lin, uint32_t n_rules,
                                    const Pkts4& p, uint8_t* verdict, unsigned long long* gslot,
                                    const LaunchCfg& cfg);
+// gslot[i] += sum_w part[w * n + i], w < rows (the classify kernel's partials)
+hipError_t launch_fold(const uint32_t* part, uint32_t rows, uint32_t n, unsigned long long* gslot,
+                       hipStream_t s);
 // out[map[i]] += slot[i]
 hipError_t launch_remap(const unsigned long long* slot, const uint32_t* map, uint32_t n,
                         unsigned long long* out, hipStream_t s);
