@@ -97,6 +97,45 @@ __global__ __launch_bounds__(1024) void stream16(const uint4* S, const uint4* D,
     }
 }
 
+// D: the classify kernel's skeleton: 32-bit byte offsets from uniform bases
+// (saddr loads), two buffers in turn (next step's loads in flight), nt loads
+// and stores.  kPf = false: load and use in the same iteration.
+template <typename T>
+__device__ __forceinline__ const T* at(const T* base, uint32_t i) {
+    return reinterpret_cast<const T*>(reinterpret_cast<const char*>(base) + i * uint32_t(sizeof(T)));
+}
+struct Buf { uint4 s, d; uint2 dp; uint32_t pr; };
+template <bool kPf>
+__global__ __launch_bounds__(1024) void stream_pp(const uint4* S, const uint4* D, const uint2* DP,
+                                                  const uint32_t* PR, uint32_t* V, uint32_t nsteps,
+                                                  uint32_t salt) {
+    const uint32_t nthreads = gridDim.x * blockDim.x;
+    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+    auto load = [&](Buf& b, uint32_t g) {
+        if (g < nsteps) { b.s = ld(at(S, g), true); b.d = ld(at(D, g), true); b.dp = ld(at(DP, g), true); b.pr = ld(at(PR, g), true); }
+    };
+    auto step = [&](const Buf& b, uint32_t g) {
+        const uint32_t v = (b.s.x ^ b.d.x ^ b.s.y ^ b.d.y ^ b.s.z ^ b.d.z ^ b.s.w ^ b.d.w ^ b.dp.x ^ b.dp.y ^ b.pr ^ salt) & 0x03030303u;
+        __builtin_nontemporal_store(v, const_cast<uint32_t*>(at(const_cast<const uint32_t*>(V), g)));
+    };
+    if constexpr (kPf) {
+        Buf a, b;
+        uint32_t g = tid;
+        load(a, g);
+        while (g < nsteps) {
+            load(b, g + nthreads);
+            step(a, g);
+            g += nthreads;
+            if (g >= nsteps) break;
+            load(a, g + nthreads);
+            step(b, g);
+            g += nthreads;
+        }
+    } else {
+        for (uint32_t g = tid; g < nsteps; g += nthreads) { Buf a; load(a, g); step(a, g); }
+    }
+}
+
 // C: pure read 11 B/pkt (no store) and pure float4 copy for reference
 __global__ __launch_bounds__(1024) void copy16(const uint4* a, uint4* b, uint64_t n) {
     const uint64_t nt = uint64_t(gridDim.x) * blockDim.x;
@@ -158,6 +197,10 @@ int main(int argc, char** argv) {
         timeit(nm, [&] { stream16<NL, NS><<<GRID, 1024>>>((const uint4*)src, (const uint4*)dst, (const uint4*)dp, \
                                                        (const uint4*)pr, (uint4*)v, N / 1024, 7u); }, B12);  \
     }
+    timeit("stream_pp prefetch grid=256", [&] { stream_pp<true><<<256, 1024>>>((const uint4*)src, (const uint4*)dst, (const uint2*)dp, pr, v, N / 4, 7u); }, B12);
+    timeit("stream_pp no-prefetch grid=256", [&] { stream_pp<false><<<256, 1024>>>((const uint4*)src, (const uint4*)dst, (const uint2*)dp, pr, v, N / 4, 7u); }, B12);
+    timeit("stream_pp prefetch grid=512", [&] { stream_pp<true><<<512, 1024>>>((const uint4*)src, (const uint4*)dst, (const uint2*)dp, pr, v, N / 4, 7u); }, B12);
+    timeit("stream_pp no-prefetch grid=512", [&] { stream_pp<false><<<512, 1024>>>((const uint4*)src, (const uint4*)dst, (const uint2*)dp, pr, v, N / 4, 7u); }, B12);
     RUN16(false, false, 256);
     RUN16(false, false, 512);
     RUN16(false, false, 1024);

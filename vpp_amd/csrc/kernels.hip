@@ -439,6 +439,9 @@ __device__ __forceinline__ void run_n(const Img<kLds>& im, const Cls4Dev& t, uin
 #ifndef CLS_GROUPS
 #define CLS_GROUPS 1
 #endif
+#ifndef CLS_PREFETCH
+#define CLS_PREFETCH 1
+#endif
 constexpr int kG = CLS_GROUPS;     // 16-B packet groups per lane per step
 
 template <bool kLds, bool kVec, int kMode, int kList, int kD>
@@ -446,7 +449,7 @@ __global__ __launch_bounds__(kClsBlock) void classify4_cls(Cls4Dev t, Pkts4 p, u
                                                            unsigned long long* gslot) {
     extern __shared__ uint4 smem[];
     Img<kLds> im{reinterpret_cast<const uint8_t*>(t.img)};
-    if constexpr (kLds) {
+    if constexpr (kLds && !(CLS_ABLATE & 16)) {
         const uint4* src4 = reinterpret_cast<const uint4*>(t.img);
         const uint32_t n4 = t.img_bytes / 16u;
         for (uint32_t i = threadIdx.x; i < n4; i += blockDim.x) smem[i] = src4[i];
@@ -514,11 +517,15 @@ __global__ __launch_bounds__(kClsBlock) void classify4_cls(Cls4Dev t, Pkts4 p, u
                                                   g + uint32_t(k) * nthreads)));
             }
         };
-        // Full steps over groups [0, nfull), two buffers in turn: the next
-        // step's loads are in flight during this step's lookups, with no
-        // register copies between steps.
+        // Full steps over groups [0, nfull).  CLS_PREFETCH (default): two
+        // buffers in turn, the next step's loads in flight during this step's
+        // lookups.  Off: load and use, the CU's 16 waves overlapping stream and
+        // lookups -- the pure stream is faster that way (tools/stream_bench.hip:
+        // 0.527 vs 0.558 ms per 256 Mi packets) but with the lookups the two
+        // measure the same within noise on config 3 (0.605-0.626 ms).
         const uint32_t span = nthreads * uint32_t(kG);
         const uint32_t nfull = nsteps / span * span;
+#if CLS_PREFETCH
         Buf a, b;
         uint32_t g = tid;
         load(a, g, g < nfull);
@@ -531,6 +538,13 @@ __global__ __launch_bounds__(kClsBlock) void classify4_cls(Cls4Dev t, Pkts4 p, u
             step(b, g);
             g += span;
         }
+#else
+        for (uint32_t g = tid; g < nfull; g += span) {
+            Buf a;
+            load(a, g, true);
+            step(a, g);
+        }
+#endif
         // leftover groups one at a time
         for (uint32_t gi = nfull + tid; gi < nsteps; gi += nthreads) {
             const uint4 s4 = ldnt(at(S, gi)), d4 = ldnt(at(D, gi));
@@ -572,7 +586,8 @@ __global__ __launch_bounds__(kClsBlock) void classify4_cls(Cls4Dev t, Pkts4 p, u
         // the partials (fold_kernel sums the rows): no global atomics from
         // every workgroup onto the same addresses at the end of the launch.
         uint32_t* part = t.part + size_t(blockIdx.x) * t.n_ctr;
-        for (uint32_t i = threadIdx.x; i < t.n_ctr; i += blockDim.x) part[i] = lctr[i];
+        if constexpr (!(CLS_ABLATE & 16))
+            for (uint32_t i = threadIdx.x; i < t.n_ctr; i += blockDim.x) part[i] = lctr[i];
     }
 }
 
