@@ -26,7 +26,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
-BYTES_PER_PKT = 12              # src 4 + dst 4 + dport 2 + proto 1 + verdict 1
+BYTES_PER_PKT = {4: 12,         # src 4 + dst 4 + dport 2 + proto 1 + verdict 1
+                 16: 36}        # 16-byte layout (config 5): src 16 + dst 16 + 2 + 1 + 1
 
 
 def parse():
@@ -34,7 +35,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", type=int, default=3, choices=[2, 3])
+    ap.add_argument("--config", type=int, default=3, choices=[2, 3, 5])
     ap.add_argument("--packets", type=int, default=0, help="packets per GPU (default: config's)")
     ap.add_argument("--cpu-sample", type=int, default=1 << 21,
                     help="packets timed on the host for the CPU baseline (0: skip)")
@@ -47,13 +48,14 @@ def cpu_baseline(acl, spec, sample: int, faithful_sample: int):
     evaluator (string re-parse per rule, one thread) on a smaller prefix."""
     import oracle
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
-    tr = oracle.gen_traffic_v4(spec, 0, sample)
+    af = spec.get("layout", 4)
+    tr = (oracle.gen_traffic_v16 if af == 16 else oracle.gen_traffic_v4)(spec, 0, sample)
     cr = oracle.rules_to_c(acl.rules)
     ft = oracle.FastTable(cr)
     ft.classify(tr["src"][:1024], tr["dst"][:1024], tr["dport"][:1024], tr["proto"][:1024],
-                nthreads=threads)
+                af=af, nthreads=threads)
     t0 = time.perf_counter()
-    ft.classify(tr["src"], tr["dst"], tr["dport"], tr["proto"], nthreads=threads)
+    ft.classify(tr["src"], tr["dst"], tr["dport"], tr["proto"], af=af, nthreads=threads)
     dt = time.perf_counter() - t0
     out = {"value": round(sample / dt / 1e6, 4), "unit": "Mpps", "cores": threads, "kind": "port",
            "sample": "%d packets of the same config stream (oracle/aclengine_ref.c orc_classify_fast, "
@@ -61,7 +63,7 @@ def cpu_baseline(acl, spec, sample: int, faithful_sample: int):
     if faithful_sample:
         f = {k: v[:faithful_sample] for k, v in tr.items()}
         t0 = time.perf_counter()
-        oracle.classify_faithful(cr, f["src"], f["dst"], f["dport"], f["proto"])
+        oracle.classify_faithful(cr, f["src"], f["dst"], f["dport"], f["proto"], af=af)
         dt2 = time.perf_counter() - t0
         out["faithful"] = {"value": round(faithful_sample / dt2 / 1e6, 6), "unit": "Mpps", "cores": 1,
                            "sample": "%d packets, evalACL restated literally (CIDR strings re-parsed "
@@ -105,10 +107,13 @@ def main():
     R = table.n_rules
 
     dev = torch.device("cuda", torch.cuda.current_device())
-    pk = {k: torch.empty(n, dtype=dt, device=dev) for k, dt in
-          (("src", torch.int32), ("dst", torch.int32), ("dport", torch.int16), ("proto", torch.uint8))}
+    af = spec.get("layout", 4)
+    shape = (n, 16) if af == 16 else (n,)
+    adt = torch.uint8 if af == 16 else torch.int32
+    pk = {k: torch.empty(shape if k in ("src", "dst") else (n,), dtype=dt, device=dev) for k, dt in
+          (("src", adt), ("dst", adt), ("dport", torch.int16), ("proto", torch.uint8))}
     first, _ = D.shard(rank, n)
-    eng.gen_traffic_v4(spec, first, pk)
+    (eng.gen_traffic_v16 if af == 16 else eng.gen_traffic_v4)(spec, first, pk)
     verdict = torch.empty(n, dtype=torch.uint8, device=dev)
     counters = torch.zeros(R + 1, dtype=torch.int64, device=dev)
     torch.cuda.synchronize()
@@ -139,7 +144,7 @@ def main():
         total = n * world * args.steps
         mpps = total / wall / 1e6
         avg_k = float(np.mean(kms)) if kms else float("nan")
-        alg_bytes = n * BYTES_PER_PKT + (R + 1) * 8
+        alg_bytes = n * BYTES_PER_PKT[af] + (R + 1) * 8
         achieved = alg_bytes / (avg_k / 1e3) / 1e9
         traffic = pmc_traffic(args.config, n)
         cpu = None
@@ -159,11 +164,17 @@ def main():
             "dtype": "u32",
             "data": "synthetic (splitmix64 stream generated in HBM, seed %#x; rules rendered from a "
                     "synthetic 1000-pod policy set)" % spec["seed"],
-            "config": {"workload": "config%d: %d-rule global ACL (%d pods), %d IPv4 TCP/UDP packets per GPU"
-                                   % (args.config, R, len(spec["pod_ips"]), n),
-                       "rules": R, "packets_per_gpu": n, "layout": "IPv4 SoA, 12 B/packet",
+            "config": {"workload": ("config%d: %d-rule global ACL (%d pods), %d IPv4 TCP/UDP packets per GPU"
+                                    % (args.config, R, len(spec["pod_ips"]), n)) if af == 4 else
+                                   ("config%d: %d-rule global ACL (%d pods, half IPv6, dst port ranges), %d "
+                                    "mixed IPv4/IPv6 packets per GPU (10%% ICMP)" % (args.config, R,
+                                                                                   len(spec["pod_ips"]), n)),
+                       "rules": R, "packets_per_gpu": n,
+                       "layout": "IPv4 SoA, 12 B/packet" if af == 4 else "16-byte address SoA, 36 B/packet",
                        "kernel": "classifier" if info["kernel"] == 1 else "linear",
-                       "lds_bytes": info["lds_bytes"], "parallelism": "dp%d" % world},
+                       "lds_bytes": info["lds_bytes"] if af == 4 else info["lds_bytes_v16"],
+                       "lds_resident": info["lds_resident"] if af == 4 else info["lds_resident_v16"],
+                       "parallelism": "dp%d" % world},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
                          "traffic": traffic,

@@ -160,7 +160,10 @@ typedef struct cls_table_info {
     uint32_t n_templates;      /* distinct (dst, port range, result) tuples (v4) */
     uint32_t n_slots;          /* flattened candidate slots (v4) */
     uint32_t lds_resident;     /* 1 if the classifier fits LDS, else global memory */
-    uint32_t reserved[8];
+    uint32_t has_v16;          /* 1 if CLS_AF_V16 batches can be classified */
+    uint32_t lds_bytes_v16;    /* LDS image of the 16-byte layout's classifier */
+    uint32_t lds_resident_v16;
+    uint32_t reserved[5];
 } cls_table_info;
 int cls_table_get_info(cls_engine* e, uint32_t table_id, cls_table_info* info);
 
@@ -237,6 +240,24 @@ int cls_gen_traffic_v4(cls_engine* e, const cls_traffic_spec* spec, uint64_t fir
                        uint64_t n, uint32_t* src4, uint32_t* dst4, uint16_t* sport,
                        uint16_t* dport, uint8_t* proto, void* stream);
 
+/* The 16-byte stream (config 5, mixed families): pools of 16-byte network-
+ * order addresses (IPv4 as IPv4-mapped), destination prefix lengths 0..128.
+ * Packet i draws w_k = splitmix64(seed ^ ((8i + k) * golden)), k < 8, as the
+ * IPv4 stream does for protocol, ports and the pool choices; an address not
+ * drawn from a pool is IPv6 fd00::/64 + w_6 (src) or w_7 (dst) when bit 0 of
+ * the choice word's high half is set, else IPv4-mapped ::ffff:(u32)w_1 (src)
+ * or (u32)w_3 (dst); a pool prefix's host bits come from (w_3, w_7). */
+typedef struct cls_traffic_spec16 {
+    uint64_t seed;
+    uint32_t pct_pod_src, pct_rule_dst, pct_table_port, pct_icmp;
+    const uint8_t* pod_ips; uint32_t n_pod_ips;            /* n x 16 bytes */
+    const uint8_t* dst_addrs; const uint8_t* dst_lens; uint32_t n_dst;
+    const uint16_t* ports; uint32_t n_ports;
+} cls_traffic_spec16;
+int cls_gen_traffic_v16(cls_engine* e, const cls_traffic_spec16* spec, uint64_t first,
+                        uint64_t n, uint8_t* src16, uint8_t* dst16, uint16_t* sport,
+                        uint16_t* dport, uint8_t* proto, void* stream);
+
 /* ---- offline compilation (no device needed) -----------------------------
  * Compiles an ACL exactly as cls_table_put does and writes the IPv4 device
  * layouts into `blob`: a cls_image_v4_header followed by the classifier image,
@@ -274,6 +295,22 @@ typedef struct cls_image_v4_header {
 } cls_image_v4_header;
 int cls_compile_v4(const cls_rule* rules, uint32_t n_rules, void* blob, uint64_t cap,
                    uint64_t* need);
+
+/* The 16-byte layout's compiled form (what cls_classify runs for CLS_AF_V16
+ * batches): both address families are mapped to 32-bit representatives by a
+ * front end -- per side (0 src, 1 dst) fe_top 16-B keys at image offset
+ * fe_key (interval start - 1 as u64 hi, u64 lo in address order; padding all
+ * ones) and fe_n u32 representatives at fe_val -- and `core` is the IPv4
+ * classifier over the rules restated on representatives (magic 0x434C3136
+ * "CL16"; its linear rules are in representative space too).  Returns
+ * CLS_E_INVAL when the table has no 16-byte classifier.
+ */
+typedef struct cls_image_v16_header {
+    cls_image_v4_header core;
+    uint32_t fe_key[2], fe_val[2], fe_top[2], fe_n[2];
+} cls_image_v16_header;
+int cls_compile_v16(const cls_rule* rules, uint32_t n_rules, void* blob, uint64_t cap,
+                    uint64_t* need);
 
 #ifdef __cplusplus
 }

@@ -90,6 +90,8 @@ def lib():
         L.orc_parse_ip.argtypes = [C.c_char_p, C.c_char_p, C.POINTER(C.c_int)]
         L.orc_cidr_contains.restype = C.c_int
         L.orc_cidr_contains.argtypes = [C.c_char_p, C.c_char_p, C.c_int]
+        L.orc_gen_traffic_v16.restype = None
+        L.orc_gen_traffic_v16.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64] + [C.c_void_p] * 5
         L.orc_gen_traffic_v4.restype = None
         L.orc_gen_traffic_v4.argtypes = [C.POINTER(TrafficSpec), C.c_uint64, C.c_uint64] + [C.c_void_p] * 5
         _LIB = L
@@ -251,6 +253,31 @@ def gen_traffic_v4(spec: dict, first: int, n: int):
                proto=np.zeros(n, np.uint8))
     lib().orc_gen_traffic_v4(C.byref(ts), first, n, _p(out["src"]), _p(out["dst"]),
                              _p(out["sport"]), _p(out["dport"]), _p(out["proto"]))
+    return out
+
+
+class TrafficSpec16(C.Structure):
+    _fields_ = [("seed", C.c_uint64), ("pct_pod_src", C.c_uint32), ("pct_rule_dst", C.c_uint32),
+                ("pct_table_port", C.c_uint32), ("pct_icmp", C.c_uint32),
+                ("pod_ips", C.c_void_p), ("n_pod_ips", C.c_uint32),
+                ("dst_addrs", C.c_void_p), ("dst_lens", C.c_void_p), ("n_dst", C.c_uint32),
+                ("ports", C.c_void_p), ("n_ports", C.c_uint32)]
+
+
+def gen_traffic_v16(spec: dict, first: int, n: int):
+    """CPU reference of the 16-byte stream (include/contivcls.h cls_traffic_spec16)."""
+    pods = np.ascontiguousarray(spec.get("pod_ips", np.zeros((0, 16))), np.uint8)
+    da = np.ascontiguousarray(spec.get("dst_addrs", np.zeros((0, 16))), np.uint8)
+    dl = np.ascontiguousarray(spec.get("dst_lens", []), np.uint8)
+    ports = np.ascontiguousarray(spec.get("ports", []), np.uint16)
+    ts = TrafficSpec16(spec["seed"], spec.get("pct_pod_src", 60), spec.get("pct_rule_dst", 50),
+                       spec.get("pct_table_port", 50), spec.get("pct_icmp", 0),
+                       pods.ctypes.data, len(pods), da.ctypes.data, dl.ctypes.data, len(da),
+                       ports.ctypes.data, len(ports))
+    out = dict(src=np.zeros((n, 16), np.uint8), dst=np.zeros((n, 16), np.uint8),
+               sport=np.zeros(n, np.uint16), dport=np.zeros(n, np.uint16), proto=np.zeros(n, np.uint8))
+    lib().orc_gen_traffic_v16(C.byref(ts), first, n, _p(out["src"]), _p(out["dst"]),
+                              _p(out["sport"]), _p(out["dport"]), _p(out["proto"]))
     return out
 
 

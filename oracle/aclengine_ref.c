@@ -627,3 +627,63 @@ void orc_gen_traffic_v4(const cls_traffic_spec* sp, uint64_t first, uint64_t n,
         if (proto) proto[k] = pr;
     }
 }
+
+/* The 16-byte stream (include/contivcls.h cls_traffic_spec16): addresses as
+ * (hi, lo) u64 in address order, written as 16 network-order bytes. */
+static void put16(uint8_t* b, uint64_t hi, uint64_t lo) {
+    for (int k = 0; k < 8; k++) {
+        b[k] = (uint8_t)(hi >> (56 - 8 * k));
+        b[8 + k] = (uint8_t)(lo >> (56 - 8 * k));
+    }
+}
+static void get16(const uint8_t* b, uint64_t* hi, uint64_t* lo) {
+    *hi = *lo = 0;
+    for (int k = 0; k < 8; k++) {
+        *hi = (*hi << 8) | b[k];
+        *lo = (*lo << 8) | b[8 + k];
+    }
+}
+
+void orc_gen_traffic_v16(const cls_traffic_spec16* sp, uint64_t first, uint64_t n,
+                         uint8_t* src16, uint8_t* dst16, uint16_t* sport, uint16_t* dport,
+                         uint8_t* proto) {
+    const uint64_t fd00 = 0xFD00ull << 48, mapped = 0xFFFFull << 32;
+    for (uint64_t k = 0; k < n; k++) {
+        uint64_t i = first + k;
+        uint64_t w[8];
+        for (int j = 0; j < 8; j++) w[j] = mix64(sp->seed ^ ((8 * i + (uint64_t)j) * GOLDEN));
+        uint32_t a0 = (uint32_t)w[0], b0 = (uint32_t)(w[0] >> 32);
+        uint8_t pr;
+        if (a0 % 100u < sp->pct_icmp) pr = CLS_PROTO_ICMP;
+        else pr = (b0 & 1u) ? CLS_PROTO_UDP : CLS_PROTO_TCP;
+        uint64_t sh, sl;
+        uint32_t b1 = (uint32_t)(w[1] >> 32);
+        if (sp->n_pod_ips && ((b0 >> 1) % 100u) < sp->pct_pod_src)
+            get16(sp->pod_ips + 16 * (size_t)(b1 % sp->n_pod_ips), &sh, &sl);
+        else if (b1 & 1u) { sh = fd00; sl = w[6]; }
+        else { sh = 0; sl = mapped | (uint32_t)w[1]; }
+        uint32_t a2 = (uint32_t)w[2], b2 = (uint32_t)(w[2] >> 32);
+        uint64_t dh, dl;
+        if (sp->n_dst && (a2 % 100u) < sp->pct_rule_dst) {
+            uint32_t j = b2 % sp->n_dst;
+            uint32_t len = sp->dst_lens[j];
+            uint64_t mh = len == 0 ? 0 : len >= 64 ? ~0ull : ~0ull << (64 - len);
+            uint64_t ml = len <= 64 ? 0 : len >= 128 ? ~0ull : ~0ull << (128 - len);
+            uint64_t ph, pl;
+            get16(sp->dst_addrs + 16 * (size_t)j, &ph, &pl);
+            dh = (ph & mh) | (w[3] & ~mh);
+            dl = (pl & ml) | (w[7] & ~ml);
+        } else if (b2 & 1u) { dh = fd00; dl = w[7]; }
+        else { dh = 0; dl = mapped | (uint32_t)w[3]; }
+        uint32_t a4 = (uint32_t)w[4], b4 = (uint32_t)(w[4] >> 32);
+        uint16_t dp;
+        if (sp->n_ports && (a4 % 100u) < sp->pct_table_port) dp = sp->ports[b4 % sp->n_ports];
+        else dp = (uint16_t)w[5];
+        uint16_t spt = (uint16_t)(1024u + ((uint32_t)(w[5] >> 32) % 64512u));
+        if (src16) put16(src16 + 16 * k, sh, sl);
+        if (dst16) put16(dst16 + 16 * k, dh, dl);
+        if (sport) sport[k] = spt;
+        if (dport) dport[k] = dp;
+        if (proto) proto[k] = pr;
+    }
+}

@@ -196,3 +196,140 @@ def single_port_acl(seed: int, n_rules: int = 120, n_prefixes: int = 8):
         rules.append(M.l4_rule(rng.choice([M.DENY, M.PERMIT, M.REFLECT]), src, dst,
                                rng.choice(["tcp", "udp"]), 0, 65535, p, p if p else 65535))
     return rules, pool
+
+
+# ---------------------------------------------------------------------------
+# mixed-family tables and 16-byte traffic (the CLS_AF_V16 path)
+
+V4_MAPPED = 0xFFFF << 32
+
+
+def _v6(x: int) -> str:
+    import ipaddress
+    return str(ipaddress.IPv6Address(x))
+
+
+class PrefixPool16(PrefixPool):
+    """IPv4 prefixes (PrefixPool) plus IPv6 ones: nested /32../128 under a few
+    bases, IPv4-mapped and IPv4-compatible spellings, and the ranges around the
+    v4-mapped block (::ffff:0:0/96 is an IPv4 network for Go, /95 and /80 are
+    IPv6 networks that numerically contain it)."""
+
+    def __init__(self, rng: random.Random, n=24):
+        super().__init__(rng, n)
+        bases = [0xFD000010 << 96, 0xFD000020 << 96, 0x20010DB8 << 96, 0, V4_MAPPED]
+        self.v6 = []
+        for _ in range(n):
+            b = rng.choice(bases[:3])
+            ln = rng.choice([32, 48, 56, 64, 64, 96, 112, 120, 127, 128, 128, 128])
+            a = b | (rng.getrandbits(128 - 32) if ln > 32 else 0)
+            host = (1 << (128 - ln)) - 1
+            self.v6.append((a & ~host & ((1 << 128) - 1), ln))
+        self.v6 += [(0, 0), (0, 80), (V4_MAPPED & ~((1 << 33) - 1), 95), (0, 96), (1, 128)]
+
+    def cidr(self, allow_weird=True) -> str:
+        rng = self.rng
+        r = rng.random()
+        if r < 0.45:
+            a, ln = rng.choice(self.v6)
+            return "%s/%d" % (_v6(a), ln)
+        if r < 0.52:
+            return rng.choice(["::ffff:0:0/96", "::ffff:0.0.0.0/96", "::ffff:0:0/95", "::/0",
+                               "::ffff:10.1.0.0/112", "::10.1.2.3/128", "0.0.0.0/0"])
+        return super().cidr(allow_weird)
+
+    def addr16(self, np_rng, n):
+        """n addresses (as python ints) biased towards the prefixes' edges."""
+        out = []
+        for _ in range(n):
+            c = np_rng.integers(0, 10)
+            if c < 4:
+                a, ln = self.v4[np_rng.integers(0, len(self.v4))]
+                size = 1 << (32 - ln)
+                k = np_rng.integers(0, 4)
+                x = [a + int(np_rng.integers(0, size)), a, a + size - 1, a + size][k] & 0xFFFFFFFF
+                out.append(V4_MAPPED | x)
+            elif c < 8:
+                a, ln = self.v6[np_rng.integers(0, len(self.v6))]
+                size = 1 << (128 - ln)
+                k = np_rng.integers(0, 4)
+                off = int.from_bytes(np_rng.bytes(16), "big") % size
+                out.append([a + off, a, a + size - 1, a + size][k] & ((1 << 128) - 1))
+            elif c < 9:
+                out.append(int(np_rng.choice([0, 1, V4_MAPPED - 1, V4_MAPPED, V4_MAPPED | 0xFFFFFFFF,
+                                              (V4_MAPPED | 0xFFFFFFFF) + 1, (1 << 128) - 1,
+                                              0x0A010203])))
+            else:
+                out.append(int.from_bytes(np_rng.bytes(16), "big"))
+        return out
+
+
+def random_acl16(seed: int, n_rules: int, weird: float = 0.15, n_prefixes: int = 24):
+    rng = random.Random(seed)
+    pool = PrefixPool16(rng, n_prefixes)
+    return [random_rule(rng, pool, weird) for _ in range(n_rules)], pool
+
+
+def to16(addrs) -> np.ndarray:
+    return np.frombuffer(b"".join(int(a).to_bytes(16, "big") for a in addrs), np.uint8).reshape(-1, 16).copy()
+
+
+def random_traffic16(seed: int, n: int, pool: PrefixPool16, other_proto: bool = True):
+    rng = np.random.default_rng(seed)
+    src, dst = to16(pool.addr16(rng, n)), to16(pool.addr16(rng, n))
+    ports = np.array([0, 1, 22, 53, 79, 80, 81, 161, 443, 8080, 65535], np.uint16)
+    dport = np.where(rng.random(n) < 0.6, rng.choice(ports, n),
+                     rng.integers(0, 65536, n)).astype(np.uint16)
+    pvals = [0, 1, 2, 3, 17] if other_proto else [0, 1, 2]
+    pw = [0.4, 0.4, 0.14, 0.03, 0.03] if other_proto else [0.43, 0.43, 0.14]
+    proto = rng.choice(np.array(pvals, np.uint8), n, p=pw)
+    sport = rng.integers(1024, 65536, n).astype(np.uint16)
+    return dict(src=src, dst=dst, dport=dport, proto=proto, sport=sport)
+
+
+V6_TWIN = 0xFD000030 << 96          # fd00:30::/96 + IPv4 address: an IPv6 twin of the IPv4 space
+
+
+def _twin_cidr(c: str, rng: random.Random) -> str:
+    """a.b.c.d/n -> fd00:30::a.b.c.d/(96+n) (an IPv6 network of the same shape), other strings as is."""
+    import ipaddress
+    try:
+        net = ipaddress.IPv4Network(c, strict=False)
+        if "/" not in c or c.count(".") != 3 or rng.random() < 0.5:
+            return c
+        return "%s/%d" % (_v6(V6_TWIN | int(net.network_address)), 96 + net.prefixlen)
+    except ValueError:
+        return c
+
+
+def mix_families(rules, traffic, seed: int, frac: float = 0.5):
+    """A mixed-family version of an IPv4 table and batch: about `frac` of the
+    networks become their fd00:30::/96 twins, every packet address becomes
+    16 bytes -- its twin with probability frac, else IPv4-mapped -- so list
+    shapes (and the compiler's list modes) stay those of the IPv4 table."""
+    import copy
+    rng = random.Random(seed)
+    out = []
+    for r in rules:
+        r = copy.deepcopy(r)
+        ip = r.matches.ip_rule.ip if r.matches is not None and r.matches.ip_rule is not None else None
+        if ip is not None:
+            ip.source_network = _twin_cidr(ip.source_network, rng) if ip.source_network else ip.source_network
+            ip.destination_network = (_twin_cidr(ip.destination_network, rng) if ip.destination_network
+                                      else ip.destination_network)
+        out.append(r)
+    nrng = np.random.default_rng(seed)
+    n = len(traffic["src"])
+
+    def widen(a):
+        twin = nrng.random(n) < frac
+        hi = np.where(twin, np.uint64(V6_TWIN >> 64), np.uint64(0))
+        lo = np.where(twin, np.uint64(0), np.uint64(0xFFFF << 32)) | a.astype(np.uint64)
+        b = np.empty((n, 16), np.uint8)
+        b[:, :8] = hi.astype(">u8").view(np.uint8).reshape(n, 8)
+        b[:, 8:] = lo.astype(">u8").view(np.uint8).reshape(n, 8)
+        return b
+
+    tr = dict(traffic)
+    tr["src"], tr["dst"] = widen(traffic["src"]), widen(traffic["dst"])
+    return out, tr

@@ -15,23 +15,23 @@ import numpy as np
 from vpp_amd import _abi
 
 
-def compile_blob(crules) -> bytes:
-    L = _abi.lib()
+def compile_blob(crules, fn="cls_compile_v4") -> bytes:
+    f = getattr(_abi.lib(), fn)
     need = C.c_uint64(0)
-    rc = L.cls_compile_v4(crules.ptr(), crules.n, None, 0, C.byref(need))
+    rc = f(crules.ptr(), crules.n, None, 0, C.byref(need))
     if rc != 0:
-        raise RuntimeError("cls_compile_v4 rc=%d" % rc)
+        raise RuntimeError("%s rc=%d" % (fn, rc))
     buf = C.create_string_buffer(need.value)
-    rc = L.cls_compile_v4(crules.ptr(), crules.n, buf, need.value, C.byref(need))
+    rc = f(crules.ptr(), crules.n, buf, need.value, C.byref(need))
     if rc != 0:
-        raise RuntimeError("cls_compile_v4 rc=%d" % rc)
+        raise RuntimeError("%s rc=%d" % (fn, rc))
     return buf.raw
 
 
 class Image:
     def __init__(self, blob: bytes):
         h = _abi.ImageHeader.from_buffer_copy(blob)
-        assert h.magic == 0x434C5334
+        assert h.magic in (0x434C5334, 0x434C3136)
         self.h = h
         self.n_rules = h.n_rules
         lin = np.frombuffer(blob, np.uint32, count=h.n_lin * 12, offset=h.off_lin).reshape(-1, 12)
@@ -250,3 +250,41 @@ class Image:
             np.subtract.at(counters, self.ctr_rule[slot[other]].astype(np.int64), 1)
             np.add.at(counters, rule2, 1)
         return res.astype(np.uint8), counters
+
+
+class Image16:
+    """The 16-byte layout (cls_compile_v16): the front end's binary search
+    over 128-bit interval starts (kernels.hip fe_rep) maps each address to its
+    32-bit representative, then the core image classifies the reps."""
+
+    def __init__(self, blob: bytes):
+        h = _abi.Image16Header.from_buffer_copy(blob)
+        assert h.core.magic == 0x434C3136
+        self.h = h
+        self.core = Image(blob)
+        img = blob[h.core.off_image:h.core.off_image + h.core.img_bytes]
+        self.keys, self.vals = [], []
+        for sd in range(2):
+            k = np.frombuffer(img, np.uint32, count=4 * h.fe_top[sd], offset=h.fe_key[sd]).reshape(-1, 4)
+            hi = (k[:, 1].astype(object) << 32) | k[:, 0].astype(object)
+            lo = (k[:, 3].astype(object) << 32) | k[:, 2].astype(object)
+            self.keys.append([int(a) << 64 | int(b) for a, b in zip(hi, lo)])
+            self.vals.append(np.frombuffer(img, np.uint32, count=h.fe_n[sd], offset=h.fe_val[sd]))
+
+    def rep(self, sd: int, addrs) -> np.ndarray:
+        keys, vals, top = self.keys[sd], self.vals[sd], self.h.fe_top[sd]
+        out = np.empty(len(addrs), np.uint32)
+        for i, a in enumerate(addrs):
+            x = int.from_bytes(bytes(a), "big")
+            pos, s = 0, top >> 1
+            while s:
+                if keys[pos + s] < x:
+                    pos += s
+                s >>= 1
+            out[i] = vals[pos]
+        return out
+
+    def classify(self, src16, dst16, dport, proto):
+        src16 = np.asarray(src16, np.uint8).reshape(-1, 16)
+        dst16 = np.asarray(dst16, np.uint8).reshape(-1, 16)
+        return self.core.classify(self.rep(0, src16), self.rep(1, dst16), dport, proto)

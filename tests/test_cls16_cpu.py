@@ -1,0 +1,110 @@
+"""The 16-byte layout's compiler (cls_compile_v16: representatives + the IPv4
+classifier over them), checked on CPU against the oracle.
+
+tests/cls_image.py Image16 evaluates the blob exactly as classify16_cls does
+(front-end binary search over 128-bit interval starts, then the core image).
+Verdicts and counters must be bit-exact against the faithful evalACL
+restatement (oracle, af=16: Go 1.9 To4 / networkNumberAndMask semantics,
+aclengine_mock.go:499-524).  IPv6 and IPv4-mapped matching is not covered by
+the reference's own tests: parity here is against the
+oracle's restatement of the Go 1.9 net package, "parity unpinned" by
+reference fixtures.
+"""
+import numpy as np
+import pytest
+
+import oracle
+from aclgen import (mix_families, random_acl, random_acl16, random_traffic, random_traffic16)
+from cls_image import Image, Image16, compile_blob
+from vpp_amd import _abi
+
+
+def _img16(rules):
+    return Image16(compile_blob(_abi.CRules(rules), "cls_compile_v16"))
+
+
+def _check16(rules, tr):
+    img = _img16(rules)
+    v, c = img.classify(tr["src"], tr["dst"], tr["dport"], tr["proto"])
+    ov, oc = oracle.classify_faithful(oracle.rules_to_c(rules), tr["src"], tr["dst"], tr["dport"],
+                                      tr["proto"], af=16)
+    bad = np.nonzero(v != ov)[0]
+    assert len(bad) == 0, "verdict mismatch at %s: got %s want %s" % (bad[:5], v[bad[:5]], ov[bad[:5]])
+    np.testing.assert_array_equal(c, oc)
+    return img
+
+
+@pytest.mark.parametrize("seed", range(10))
+@pytest.mark.parametrize("n_rules,weird", [(5, 0.0), (40, 0.0), (40, 0.2), (150, 0.05)])
+def test_v16_compiler_matches_oracle(seed, n_rules, weird):
+    rules, pool = random_acl16(seed * 1000 + n_rules, n_rules, weird)
+    _check16(rules, random_traffic16(seed, 1500, pool))
+
+
+@pytest.mark.parametrize("seed", range(4))
+@pytest.mark.parametrize("cap", [0, 1, 2, 3, 4])
+def test_v16_list_modes(seed, cap, monkeypatch):
+    """Every list mode of the core, over mixed-family twins of IPv4 tables."""
+    from aclgen import long_list_acl, many_ports_acl, single_port_acl
+    monkeypatch.setenv("CONTIVCLS_LIST_MODE_MAX", str(cap))
+    gen = [single_port_acl(seed + 3, 120), random_acl(seed + 9, 120, 0.0), many_ports_acl(seed, 300, 30),
+           long_list_acl(seed + 1, 200)][seed % 4]
+    rules, pool = gen
+    rules, tr = mix_families(rules, random_traffic(seed, 2500, pool), seed)
+    img = _check16(rules, tr)
+    assert img.core.h.list_mode <= cap
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_v4_mapped_batch_equals_ipv4_batch(seed):
+    """An IPv4 batch spelled as IPv4-mapped 16-byte addresses (Go's To4)
+    classifies exactly as the 4-byte batch does."""
+    rules, pool = random_acl(seed + 40, 120, 0.1)
+    tr = random_traffic(seed, 3000, pool)
+    _, tr16 = mix_families(rules, tr, seed, frac=0.0)
+    v4, c4 = Image(compile_blob(_abi.CRules(rules))).classify(tr["src"], tr["dst"], tr["dport"], tr["proto"])
+    v16, c16 = _img16(rules).classify(tr16["src"], tr16["dst"], tr16["dport"], tr16["proto"])
+    np.testing.assert_array_equal(v4, v16)
+    np.testing.assert_array_equal(c4, c16)
+
+
+def test_v16_empty_and_any_tables():
+    import vpp_amd.model as M
+    pool_rules, pool = random_acl16(5, 10)
+    tr = random_traffic16(2, 500, pool)
+    _check16([], tr)
+    _check16([M.l4_rule(M.PERMIT, "", "", "tcp", 0, 65535, 0, 65535)], tr)
+    _check16([M.l4_rule(M.DENY, "::/0", "", "udp", 0, 65535, 53, 53),
+              M.l4_rule(M.REFLECT, "0.0.0.0/0", "::ffff:0:0/96", "tcp", 0, 65535, 0, 65535)], tr)
+
+
+def test_v16_representatives_preserve_containment():
+    """Nested IPv6 prefixes, IPv4 prefixes and the v4-mapped block's edges:
+    the interval table's reps must separate exactly what Contains separates."""
+    import vpp_amd.model as M
+    nets = ["fd00:10::/32", "fd00:10:1::/48", "fd00:10:1:2::/64", "fd00:10:1:2::7/128", "::ffff:0:0/95",
+            "::/80", "10.0.0.0/8", "10.1.0.0/16", "::ffff:10.1.2.0/120", "::/0", "0.0.0.0/0"]
+    rules = []
+    for k, a in enumerate(nets):
+        for b in nets[::-1]:
+            rules.append(M.l4_rule([M.DENY, M.PERMIT, M.REFLECT][k % 3], a, b, "tcp", 0, 65535, 0, 65535))
+    from aclgen import PrefixPool16, to16
+    import random
+    pool = PrefixPool16(random.Random(1), 8)
+    rng = np.random.default_rng(3)
+    tr = random_traffic16(4, 2000, pool)
+    edge = to16(pool.addr16(rng, 500) + [0xFD000010 << 96, (0xFD000010 << 96) - 1, (0xFD000011 << 96) - 1,
+                                         0xFFFF << 32, (0xFFFF << 32) - 1, 0x0A010203 | (0xFFFF << 32)])
+    n = len(edge)
+    tr = dict(src=edge, dst=edge[::-1].copy(), dport=np.full(n, 80, np.uint16), proto=np.zeros(n, np.uint8))
+    _check16(rules, tr)
+
+
+def test_oracle_fast_matches_faithful_v16():
+    rules, pool = random_acl16(77, 200, 0.1)
+    tr = random_traffic16(8, 3000, pool)
+    cr = oracle.rules_to_c(rules)
+    fv, fc = oracle.classify_fast(cr, tr["src"], tr["dst"], tr["dport"], tr["proto"], af=16)
+    ov, oc = oracle.classify_faithful(cr, tr["src"], tr["dst"], tr["dport"], tr["proto"], af=16)
+    np.testing.assert_array_equal(fv, ov)
+    np.testing.assert_array_equal(fc, oc)

@@ -30,7 +30,8 @@ SYMBOLS = ["cls_abi_version", "cls_engine_create", "cls_engine_destroy", "cls_la
            "cls_table_put", "cls_table_del", "cls_table_get_info", "cls_classify",
            "cls_last_kernel_ms", "cls_kernel_times", "cls_kernel_times_reset", "cls_acl_put", "cls_acl_del", "cls_acl_table", "cls_acl_counts",
            "cls_if_id",
-           "cls_if_acls", "cls_connect_batch", "cls_gen_traffic_v4", "cls_compile_v4"]
+           "cls_if_acls", "cls_connect_batch", "cls_gen_traffic_v4", "cls_compile_v4",
+           "cls_compile_v16", "cls_gen_traffic_v16"]
 
 
 class ClsRule(C.Structure):
@@ -62,10 +63,19 @@ class TableInfo(C.Structure):
     _fields_ = [("n_rules", C.c_uint32), ("kernel", C.c_uint32), ("lds_bytes", C.c_uint32),
                 ("n_intervals", C.c_uint32), ("n_classes", C.c_uint32),
                 ("n_templates", C.c_uint32), ("n_slots", C.c_uint32),
-                ("lds_resident", C.c_uint32), ("reserved", C.c_uint32 * 8)]
+                ("lds_resident", C.c_uint32), ("has_v16", C.c_uint32), ("lds_bytes_v16", C.c_uint32),
+                ("lds_resident_v16", C.c_uint32), ("reserved", C.c_uint32 * 5)]
 
 
 class TrafficSpec(C.Structure):
+    _fields_ = [("seed", C.c_uint64), ("pct_pod_src", C.c_uint32), ("pct_rule_dst", C.c_uint32),
+                ("pct_table_port", C.c_uint32), ("pct_icmp", C.c_uint32),
+                ("pod_ips", C.c_void_p), ("n_pod_ips", C.c_uint32),
+                ("dst_addrs", C.c_void_p), ("dst_lens", C.c_void_p), ("n_dst", C.c_uint32),
+                ("ports", C.c_void_p), ("n_ports", C.c_uint32)]
+
+
+class TrafficSpec16(C.Structure):
     _fields_ = [("seed", C.c_uint64), ("pct_pod_src", C.c_uint32), ("pct_rule_dst", C.c_uint32),
                 ("pct_table_port", C.c_uint32), ("pct_icmp", C.c_uint32),
                 ("pod_ips", C.c_void_p), ("n_pod_ips", C.c_uint32),
@@ -87,6 +97,12 @@ class ImageHeader(C.Structure):
         ("hash_mul", C.c_uint32 * 3), ("port_mul", C.c_uint32), ("port_mask4", C.c_uint32),
         ("port_dflt", C.c_uint32),
         ("n_hot", C.c_uint32), ("off_hot", C.c_uint32)]
+
+
+class Image16Header(C.Structure):
+    """cls_image_v16_header: the core (rep-space) header, then the front end."""
+    _fields_ = [("core", ImageHeader), ("fe_key", C.c_uint32 * 2), ("fe_val", C.c_uint32 * 2),
+                ("fe_top", C.c_uint32 * 2), ("fe_n", C.c_uint32 * 2)]
 
 
 _lib = None
@@ -135,6 +151,9 @@ def lib():
         "cls_gen_traffic_v4": (C.c_int, [vp, C.POINTER(TrafficSpec), u64, u64, vp, vp, vp, vp,
                                          vp, vp]),
         "cls_compile_v4": (C.c_int, [C.POINTER(ClsRule), u32, vp, u64, C.POINTER(u64)]),
+        "cls_compile_v16": (C.c_int, [C.POINTER(ClsRule), u32, vp, u64, C.POINTER(u64)]),
+        "cls_gen_traffic_v16": (C.c_int, [vp, C.POINTER(TrafficSpec16), u64, u64, vp, vp, vp, vp,
+                                          vp, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

@@ -113,14 +113,14 @@ int semantic_rules(const cls_rule* rules, uint32_t n, int fam, std::vector<SemRu
         if (nonempty(r.src_network)) {                       // :499-510
             s.src = parse_cidr(r.src_network);
             if (s.src.fam == 0) { out.push_back(terminator(k)); return CLS_OK; }
-            if (s.src.fam != fam) continue;                  // never Contains() this family
+            if (fam && s.src.fam != fam) continue;           // never Contains() this family
             s.src_any = false;
         }
         bool dst_fail = false;
         if (nonempty(r.dst_network)) {                       // :513-524
             s.dst = parse_cidr(r.dst_network);
             if (s.dst.fam == 0) dst_fail = true;
-            else if (s.dst.fam != fam) continue;
+            else if (fam && s.dst.fam != fam) continue;
             else s.dst_any = false;
         }
         if (dst_fail) {
@@ -489,7 +489,7 @@ std::vector<Sublist> port_sublists(const std::vector<TmplKey>& ents, const std::
 }  // namespace
 
 bool build_cls4(const std::vector<SemRule>& sem, uint32_t n_rules, Cls4Image& img,
-                std::string& why) {
+                std::string& why, const Cls4Opts* opt) {
     img = Cls4Image();
     // distinct source prefixes
     std::vector<Pfx> pfx;
@@ -623,6 +623,11 @@ bool build_cls4(const std::vector<SemRule>& sem, uint32_t n_rules, Cls4Image& im
             span[iclass[k]] += hi - double(bounds[k]);
         }
         hot_class = uint32_t(std::max_element(span.begin(), span.end()) - span.begin());
+        if (opt && opt->hot_addr >= 0) {
+            const uint32_t x = uint32_t(opt->hot_addr);
+            hot_class = iclass[uint32_t(std::upper_bound(bounds.begin(), bounds.begin() + n_real_bounds, x) -
+                                        bounds.begin()) - 1u];
+        }
     }
     std::vector<uint32_t> cand;
     for (uint32_t ci = 0; ci < n_classes; ++ci) {
@@ -1034,6 +1039,11 @@ bool build_cls4(const std::vector<SemRule>& sem, uint32_t n_rules, Cls4Image& im
                 for (size_t p = 0; p < prep.size(); ++p) w[ptr_at[i] + p] = state0[sub_of[i][p]];
             w.resize(align4(uint32_t(w.size())));
         }
+        img.off_tail = uint32_t(w.size()) * 4;
+        if (opt) {
+            w.insert(w.end(), opt->tail.begin(), opt->tail.end());
+            w.resize(align4(uint32_t(w.size())));
+        }
         img.img_bytes = uint32_t(w.size()) * 4;
         img.n_bounds = n_real_bounds;
         img.n_classes = n_classes;
@@ -1052,6 +1062,182 @@ bool build_cls4(const std::vector<SemRule>& sem, uint32_t n_rules, Cls4Image& im
         const bool cell_ok = lmode >= 3 ? img.sub_bytes <= 0x10000u : img.img_bytes / 8u <= 0xFFFFu;
         if (cell_ok && (lmode == 1 || img.lds_bytes <= kLdsBudget)) break;
         lmode = lmode >= 3 ? 2u : (lmode == 2 && std::max(Sd, Sp) <= kMaxBvSteps) ? 1u : 0u;
+    }
+    return true;
+}
+
+}  // namespace cls
+
+// ---------------------------------------------------------------------------
+// 16-byte classifier image (compile.hpp: representatives)
+// ---------------------------------------------------------------------------
+namespace cls {
+namespace {
+
+using u128 = unsigned __int128;
+constexpr u128 kAll = ~u128(0);
+constexpr u128 kV4Lo = u128(0xFFFFu) << 32;          // ::ffff:0.0.0.0, To4()-able addresses
+constexpr u128 kV4Hi = kV4Lo | 0xFFFFFFFFu;
+
+struct Range {
+    u128 lo, hi;
+    bool operator<(const Range& o) const { return lo != o.lo ? lo < o.lo : hi > o.hi; }  // containers first
+    bool operator==(const Range& o) const { return lo == o.lo && hi == o.hi; }
+};
+
+Range range_of(const Prefix& p) {
+    if (p.fam == 4) {
+        const uint32_t m = v4_mask(p.len);
+        const u128 lo = kV4Lo | (v4_word(p.addr) & m);
+        return {lo, lo | u128(~m)};
+    }
+    u128 a = 0;
+    for (int i = 0; i < 16; ++i) a = (a << 8) | p.addr[i];
+    const u128 host = p.len >= 128 ? u128(0) : (kAll >> p.len);
+    return {a & ~host, (a & ~host) | host};
+}
+
+// One address side (src or dst): the prefix tree of each family, its blocks
+// in rep space, and the front-end interval table.
+struct Side {
+    std::vector<Range> pf[2];          // 0 = IPv4, 1 = IPv6; sorted, distinct
+    std::vector<uint32_t> base[2];
+    std::vector<int> blen[2];
+    uint32_t root[2] = {0u, 0x80000000u};
+
+    int fam_of(const Prefix& p) const { return p.fam == 4 ? 0 : 1; }
+    size_t find(int f, const Range& r) const {
+        return size_t(std::lower_bound(pf[f].begin(), pf[f].end(), r) - pf[f].begin());
+    }
+    bool embed(std::string& why) {
+        for (int f = 0; f < 2; ++f) {
+            auto& P = pf[f];
+            std::sort(P.begin(), P.end());
+            P.erase(std::unique(P.begin(), P.end()), P.end());
+            std::vector<std::vector<uint32_t>> kids(P.size() + 1);   // last = family root
+            std::vector<uint32_t> stack;
+            for (uint32_t i = 0; i < P.size(); ++i) {
+                while (!stack.empty() && P[stack.back()].hi < P[i].lo) stack.pop_back();
+                kids[stack.empty() ? P.size() : stack.back()].push_back(i);
+                stack.push_back(i);
+            }
+            base[f].assign(P.size(), 0);
+            blen[f].assign(P.size(), 0);
+            auto assign = [&](const std::vector<uint32_t>& ks, uint32_t b, int l) {
+                if (ks.empty()) return true;
+                int bits = 0;
+                while ((size_t(1) << bits) < ks.size() + 1) ++bits;
+                if (l + bits > 32) return false;
+                for (size_t j = 0; j < ks.size(); ++j) {
+                    base[f][ks[j]] = b | uint32_t(uint64_t(j + 1) << (32 - l - bits));
+                    blen[f][ks[j]] = l + bits;
+                }
+                return true;
+            };
+            bool ok = assign(kids[P.size()], root[f], 1);
+            for (uint32_t i = 0; ok && i < P.size(); ++i) ok = assign(kids[i], base[f][i], blen[f][i]);
+            if (!ok) {
+                why = "prefix tree too deep for 32-bit representatives";
+                return false;
+            }
+        }
+        return true;
+    }
+    // interval table: starts (ascending, [0] = 0) and the rep of each interval
+    void intervals(std::vector<u128>& start, std::vector<uint32_t>& rep) const {
+        std::vector<u128> b{0, kV4Lo, kV4Hi + 1};
+        for (int f = 0; f < 2; ++f)
+            for (const auto& r : pf[f]) {
+                b.push_back(r.lo);
+                if (r.hi != kAll) b.push_back(r.hi + 1);
+            }
+        std::sort(b.begin(), b.end());
+        b.erase(std::unique(b.begin(), b.end()), b.end());
+        std::vector<int> lpm[2];
+        for (int f = 0; f < 2; ++f) {
+            lpm[f].assign(b.size(), -1);
+            std::vector<int> stack;
+            size_t next = 0;
+            for (size_t k = 0; k < b.size(); ++k) {
+                while (!stack.empty() && pf[f][stack.back()].hi < b[k]) stack.pop_back();
+                while (next < pf[f].size() && pf[f][next].lo == b[k]) stack.push_back(int(next++));
+                lpm[f][k] = stack.empty() ? -1 : stack.back();
+            }
+        }
+        start.clear();
+        rep.clear();
+        for (size_t k = 0; k < b.size(); ++k) {
+            const int f = (b[k] >= kV4Lo && b[k] <= kV4Hi) ? 0 : 1;
+            const uint32_t r = lpm[f][k] < 0 ? root[f] : base[f][lpm[f][k]];
+            if (!rep.empty() && rep.back() == r) continue;
+            start.push_back(b[k]);
+            rep.push_back(r);
+        }
+    }
+};
+
+void put_be32(uint8_t* a, uint32_t v) {
+    a[0] = uint8_t(v >> 24); a[1] = uint8_t(v >> 16); a[2] = uint8_t(v >> 8); a[3] = uint8_t(v);
+}
+
+}  // namespace
+
+bool build_cls16(const std::vector<SemRule>& sem, uint32_t n_rules, Cls16Image& img, std::string& why) {
+    img = Cls16Image();
+    Side side[2];                                         // 0 src, 1 dst
+    for (const SemRule& s : sem) {
+        if (!s.src_any) side[0].pf[side[0].fam_of(s.src)].push_back(range_of(s.src));
+        if (!s.dst_any) side[1].pf[side[1].fam_of(s.dst)].push_back(range_of(s.dst));
+    }
+    for (auto& sd : side)
+        if (!sd.embed(why)) return false;
+    // rules in rep space
+    img.sem.clear();
+    for (const SemRule& s : sem) {
+        SemRule r = s;
+        for (int sd = 0; sd < 2; ++sd) {
+            const bool any = sd == 0 ? r.src_any : r.dst_any;
+            if (any) continue;
+            Prefix& p = sd == 0 ? r.src : r.dst;
+            const int f = side[sd].fam_of(p);
+            const size_t id = side[sd].find(f, range_of(p));
+            Prefix q;
+            q.fam = 4;
+            put_be32(q.addr, side[sd].base[f][id]);
+            q.len = side[sd].blen[f][id];
+            p = q;
+        }
+        img.sem.push_back(r);
+    }
+    // front-end tables (image tail): per side, keys then reps
+    Cls4Opts opt;
+    uint32_t rel_key[2], rel_val[2];
+    for (int sd = 0; sd < 2; ++sd) {
+        std::vector<u128> start;
+        std::vector<uint32_t> rep;
+        side[sd].intervals(start, rep);
+        uint32_t K = 1;
+        while (K < start.size()) K *= 2;
+        img.fe_top[sd] = K;
+        img.fe_n[sd] = uint32_t(rep.size());
+        rel_key[sd] = uint32_t(opt.tail.size()) * 4;
+        for (uint32_t k = 0; k < K; ++k) {
+            const u128 key = (k >= 1 && k < start.size()) ? start[k] - 1 : kAll;
+            const uint64_t h = uint64_t(key >> 64), l = uint64_t(key);
+            opt.tail.push_back(uint32_t(h));
+            opt.tail.push_back(uint32_t(h >> 32));
+            opt.tail.push_back(uint32_t(l));
+            opt.tail.push_back(uint32_t(l >> 32));
+        }
+        rel_val[sd] = uint32_t(opt.tail.size()) * 4;
+        opt.tail.insert(opt.tail.end(), rep.begin(), rep.end());
+        opt.tail.resize(align4(uint32_t(opt.tail.size())));
+    }
+    opt.hot_addr = side[0].root[0];                       // IPv4 sources matching no prefix
+    if (!build_cls4(img.sem, n_rules, img.core, why, &opt)) return false;
+    for (int sd = 0; sd < 2; ++sd) {
+        img.fe_key[sd] = img.core.off_tail + rel_key[sd];
+        img.fe_val[sd] = img.core.off_tail + rel_val[sd];
     }
     return true;
 }

@@ -73,7 +73,8 @@ struct SemRule {
     Term t[NPROTO];
 };
 
-// Reduce the ACL for packets of family `fam` (4 or 16).  Returns CLS_OK or
+// Reduce the ACL for packets of family `fam` (4: both addresses IPv4; 0: each
+// address of either family -- networks of both families kept).  Returns CLS_OK or
 // CLS_E_INVAL (a rule with nil Matches: Go would panic).
 int semantic_rules(const cls_rule* rules, uint32_t n, int fam, std::vector<SemRule>& out,
                    std::string& err);
@@ -139,11 +140,47 @@ struct Cls4Image {
     // (n_hot x 64 u32 at off_hot, after the slot counters)
     uint32_t n_hot = 1;
     uint32_t off_hot = 0;
+    uint32_t off_tail = 0;         // Cls4Opts::tail words (read-only, after the sections above)
+};
+
+struct Cls4Opts {
+    std::vector<uint32_t> tail;    // extra read-only words appended to the image
+    int64_t hot_addr = -1;         // the hot class is this address's (default: the widest)
 };
 
 // Build the image; returns false (with reason) if the table does not fit the
 // 16-bit list / template indices.
 bool build_cls4(const std::vector<SemRule>& sem, uint32_t n_rules, Cls4Image& img,
-                std::string& why);
+                std::string& why, const Cls4Opts* opt = nullptr);
+
+// ---- 16-byte (IPv6 and IPv4-mapped) classifier image ----------------------
+// evalACL's Contains (Go 1.9 net.IPNet.Contains) reduces a v4-mapped packet
+// address to 4 bytes and never matches an address of one family against a
+// network of the other.  The 16-byte path maps both families into one 32-bit
+// space of *representatives* that preserves every containment the rule set
+// can observe, then runs the IPv4 classifier over it:
+//   - the prefixes of one side (src or dst) of one family form a tree (any
+//     two prefixes nest or are disjoint); each node gets a block (base, len)
+//     of the 32-bit space inside its parent's block -- children at sub-block
+//     indices 1..k of the parent's next ceil(log2(k+1)) bits, index 0 left to
+//     the node itself -- under a family root block (IPv4 0/1, IPv6 1/1);
+//   - a packet address maps to the base of its longest matching prefix's
+//     block (the family root's base when none matches), found by one binary
+//     search over the 128-bit elementary intervals of all prefixes (IPv4
+//     prefixes at ::ffff:a.b.c.d, the v4-mapped range holding IPv4 packets;
+//     inside it only IPv4 prefixes count, outside it only IPv6 prefixes);
+//   - a rule's prefix becomes its block: the rep of an address lies in a
+//     block iff the address lies in the prefix.
+// Front-end tables per side s (0 src, 1 dst), in the image's tail: fe_top[s]
+// keys of 16 B (interval start - 1 as u64 hi, u64 lo; padding all-ones),
+// then fe_n[s] u32 reps.
+struct Cls16Image {
+    Cls4Image core;                // classifier over the rules in rep space
+    std::vector<SemRule> sem;      // the rules in rep space (linear fallback)
+    uint32_t fe_key[2] = {}, fe_val[2] = {}, fe_top[2] = {}, fe_n[2] = {};
+};
+// sem: semantic_rules(..., fam 0, ...) -- a packet's src and dst may be of
+// different families (Contains tests each address on its own).
+bool build_cls16(const std::vector<SemRule>& sem, uint32_t n_rules, Cls16Image& img, std::string& why);
 
 }  // namespace cls

@@ -56,6 +56,16 @@ struct Table {
     DevBuf d_part;                 // per-workgroup slot counters of the LDS-resident kernel
     int kernel = 0;            // 0 linear, 1 classifier
     bool lds_resident = false;
+    // 16-byte layout (IPv6 / IPv4-mapped): classifier over 32-bit reps
+    struct {
+        bool ok = false;
+        std::string why;           // why there is none
+        Cls16Image img;
+        std::vector<LinRule4> lin; // rules in rep space (protocol > 2, FORCE_LINEAR)
+        DevBuf d_img, d_lin, d_slot, d_map, d_part;
+        uint32_t n_slots = 0;
+        bool lds_resident = false;
+    } p16;
 };
 
 struct AclEntry {
@@ -187,6 +197,33 @@ static int table_put_locked(cls_engine* e, const char* name, const cls_rule* rul
     HIPC(e, t->d_map.ensure(size_t(t->n_slots) * 4));
     HIPC(e, t->d_out.ensure(size_t(n + 1) * 8));
     HIPC(e, hipMemcpy(t->d_map.p, map.data(), map.size() * 4, hipMemcpyHostToDevice));
+    // 16-byte layout: both families' reductions over one rep space
+    {
+        auto& q = t->p16;
+        std::vector<SemRule> s16;
+        rc = semantic_rules(rules, n, 0, s16, why);
+        if (rc != CLS_OK) return fail(e, rc, "%s", why.c_str());
+        std::string why16;
+        q.ok = build_cls16(s16, n, q.img, why16);
+        q.why = why16;
+        if (q.ok) {
+            const Cls4Image& c = q.img.core;
+            q.lin = linear4(q.img.sem);
+            q.lds_resident = c.lds_bytes <= uint32_t(max_lds_bytes());
+            HIPC(e, q.d_img.ensure(c.img_bytes));
+            HIPC(e, hipMemcpy(q.d_img.p, c.words.data(), c.img_bytes, hipMemcpyHostToDevice));
+            HIPC(e, q.d_lin.ensure(std::max<size_t>(1, q.lin.size()) * sizeof(LinRule4)));
+            if (!q.lin.empty())
+                HIPC(e, hipMemcpy(q.d_lin.p, q.lin.data(), q.lin.size() * sizeof(LinRule4), hipMemcpyHostToDevice));
+            q.n_slots = c.n_ctr + n + 1;
+            std::vector<uint32_t> m16(q.n_slots);
+            for (uint32_t i = 0; i < c.n_ctr; ++i) m16[i] = c.ctr_rule[i];
+            for (uint32_t i = 0; i <= n; ++i) m16[c.n_ctr + i] = i;
+            HIPC(e, q.d_slot.ensure(size_t(q.n_slots) * 8));
+            HIPC(e, q.d_map.ensure(size_t(q.n_slots) * 4));
+            HIPC(e, hipMemcpy(q.d_map.p, m16.data(), m16.size() * 4, hipMemcpyHostToDevice));
+        }
+    }
     const uint32_t id = e->next_table++;
     e->tables[id] = t;
     if (table_id) *table_id = id;
@@ -224,6 +261,11 @@ int cls_table_get_info(cls_engine* e, uint32_t table_id, cls_table_info* info) {
         info->n_slots = t.img.n_ctr;
         info->lds_resident = t.lds_resident ? 1 : 0;
     }
+    info->has_v16 = t.p16.ok ? 1u : 0u;
+    if (t.p16.ok) {
+        info->lds_bytes_v16 = t.p16.img.core.lds_bytes;
+        info->lds_resident_v16 = t.p16.lds_resident ? 1u : 0u;
+    }
     return CLS_OK;
 }
 
@@ -232,6 +274,185 @@ constexpr uint64_t kClsChunk = 1ull << 30;   // packets per classify launch (32-
 
 static bool aligned(const void* p, size_t a) { return (reinterpret_cast<uintptr_t>(p) % a) == 0; }
 
+static int timing_begin(cls_engine* e, hipStream_t s) {
+    if (e->ev_used == e->ev_pool.size()) {
+        hipEvent_t a, b;
+        HIPC(e, hipEventCreate(&a));
+        HIPC(e, hipEventCreate(&b));
+        e->ev_pool.push_back({a, b});
+    }
+    e->ev0 = e->ev_pool[e->ev_used].first;
+    e->ev1 = e->ev_pool[e->ev_used].second;
+    e->ev_used++;
+    HIPC(e, hipEventRecord(e->ev0, s));
+    return CLS_OK;
+}
+
+static Cls4Dev cls4_dev(const Cls4Image& im, const DevBuf& d_img, const DevBuf& d_lin, uint32_t n_lin,
+                        uint32_t n_rules) {
+    Cls4Dev cd;
+    cd.img = d_img.as<uint32_t>();
+    cd.img_bytes = im.img_bytes;
+    cd.off_bounds = im.off_bounds;
+    cd.off_iclass = im.off_iclass;
+    cd.off_cells = im.off_cells;
+    cd.off_lists = im.off_lists;
+    cd.off_tmpl = im.off_tmpl;
+    cd.search_top = im.search_top;
+    cd.n_ctr = im.n_ctr;
+    cd.lds_bytes = im.lds_bytes;
+    cd.lin = d_lin.as<LinRule4>();
+    cd.n_lin = n_lin;
+    cd.n_rules = n_rules;
+    cd.mode = im.mode;
+    cd.default_row = im.default_row;
+    cd.row_bytes = im.row_bytes;
+    cd.port_mul = im.port_mul;
+    cd.port_mask4 = im.port_mask4;
+    cd.port_dflt = im.port_dflt;
+    cd.n_hash = im.n_hash;
+    cd.list_mode = im.list_mode;
+    cd.bv_steps = std::max(im.bv_steps_d, im.bv_steps_p);  // mode 2: Sd
+    cd.n_hot = im.n_hot;
+    cd.off_ptop = im.off_ptop;
+    cd.bv_wide = im.bv_wide;
+    cd.off_hot = im.off_hot;
+    cd.part = nullptr;
+    for (uint32_t i = 0; i < kMaxHashLens; ++i) {
+        cd.hash_mask[i] = im.hash_mask[i];
+        cd.hash_shift[i] = im.hash_shift[i];
+        cd.hash_cap[i] = im.hash_cap[i];
+        cd.hash_mul[i] = im.hash_mul[i];
+        cd.hash_shift1[i] = 32u - 2u * (32u - im.hash_shift[i]);
+        cd.off_hash[i] = im.off_hash[i];
+    }
+    return cd;
+}
+
+// Workgroups of a classify launch: persistent grid, as many per CU as LDS
+// and threads allow, no more than the batch needs.
+static int cls_grid(const cls_engine* e, bool use_cls, bool lds_resident, uint32_t lds_bytes, uint64_t n) {
+    int per_cu = 2;
+    if (use_cls) {
+        const int by_threads = 2048 / cls_block();
+        per_cu = by_threads;
+        if (lds_resident)
+            per_cu = std::max(1, std::min(by_threads, int(max_lds_bytes() / std::max<uint32_t>(1, lds_bytes))));
+        if (const char* w = std::getenv("CONTIVCLS_WG_PER_CU"))   // diagnostics
+            per_cu = std::max(1, std::atoi(w));
+    }
+    const uint64_t want = (n + 4ull * 1024 - 1) / (4ull * 1024);
+    return int(std::max<uint64_t>(1, std::min<uint64_t>(uint64_t(e->n_cu) * per_cu, want)));
+}
+
+// slot counters -> rule counters; host batches: copy verdicts and counters back
+static int finish_counts(cls_engine* e, Table& t, DevBuf& d_slot, DevBuf& d_map, uint32_t n_slots, uint64_t n,
+                         uint8_t* verdict_out, const uint8_t* d_verdict, uint64_t* counters_out,
+                         uint32_t flags, hipStream_t s) {
+    const bool dev = flags & CLS_F_DEVICE;
+    unsigned long long* out = dev && counters_out ? reinterpret_cast<unsigned long long*>(counters_out)
+                                                  : t.d_out.as<unsigned long long>();
+    if (counters_out || !dev) {
+        if (!(dev && (flags & CLS_F_ACCUMULATE)))
+            HIPC(e, hipMemsetAsync(out, 0, size_t(t.n_rules + 1) * 8, s));
+        HIPC(e, launch_remap(d_slot.as<unsigned long long>(), d_map.as<uint32_t>(), n_slots, out, s));
+    }
+    if (!dev) {
+        if (verdict_out && n) HIPC(e, hipMemcpyAsync(verdict_out, d_verdict, n, hipMemcpyDeviceToHost, s));
+        std::vector<uint64_t> tmp;
+        if (counters_out) {
+            tmp.resize(t.n_rules + 1);
+            HIPC(e, hipMemcpyAsync(tmp.data(), out, tmp.size() * 8, hipMemcpyDeviceToHost, s));
+        }
+        HIPC(e, hipStreamSynchronize(s));
+        if (counters_out) {
+            for (size_t i = 0; i < tmp.size(); ++i)
+                counters_out[i] = (flags & CLS_F_ACCUMULATE) ? counters_out[i] + tmp[i] : tmp[i];
+        }
+    }
+    return CLS_OK;
+}
+
+// cls_classify of a 16-byte batch (CLS_AF_V16): front end to reps, then the
+// classifier over the rep-space rules (compile.hpp Cls16Image).
+static int classify16_locked(cls_engine* e, std::shared_ptr<Table> t, const cls_pkt_soa* pk, uint64_t n,
+                             uint8_t* verdict_out, uint64_t* counters_out, uint32_t flags, void* stream) {
+    auto& q = t->p16;
+    if (!q.ok) return fail(e, CLS_E_INVAL, "no 16-byte classifier for this table: %s", q.why.c_str());
+    if (n && (!pk->src16 || !pk->dst16 || !pk->dport || !pk->proto))
+        return fail(e, CLS_E_INVAL, "missing packet arrays");
+    if (!verdict_out && !(flags & CLS_F_NO_VERDICT) && n)
+        return fail(e, CLS_E_INVAL, "verdict_out is NULL (set CLS_F_NO_VERDICT)");
+    HIPC(e, hipSetDevice(e->device));
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : e->stream;
+    const bool dev = flags & CLS_F_DEVICE;
+    const uint8_t *src = pk->src16, *dst = pk->dst16, *pr = pk->proto;
+    const uint16_t* dp = pk->dport;
+    uint8_t* d_verdict = verdict_out;
+    if (dev && n && (!aligned(src, 16) || !aligned(dst, 16)))
+        return fail(e, CLS_E_INVAL, "device src16/dst16 must be 16-byte aligned");
+    if (!dev && n) {
+        HIPC(e, e->s_src.ensure(n * 16));
+        HIPC(e, e->s_dst.ensure(n * 16));
+        HIPC(e, e->s_dport.ensure(n * 2));
+        HIPC(e, e->s_proto.ensure(n));
+        HIPC(e, hipMemcpyAsync(e->s_src.p, src, n * 16, hipMemcpyHostToDevice, s));
+        HIPC(e, hipMemcpyAsync(e->s_dst.p, dst, n * 16, hipMemcpyHostToDevice, s));
+        HIPC(e, hipMemcpyAsync(e->s_dport.p, dp, n * 2, hipMemcpyHostToDevice, s));
+        HIPC(e, hipMemcpyAsync(e->s_proto.p, pr, n, hipMemcpyHostToDevice, s));
+        src = e->s_src.as<uint8_t>();
+        dst = e->s_dst.as<uint8_t>();
+        dp = e->s_dport.as<uint16_t>();
+        pr = e->s_proto.as<uint8_t>();
+        d_verdict = nullptr;
+        if (verdict_out) {
+            HIPC(e, e->s_verdict.ensure(n));
+            d_verdict = e->s_verdict.as<uint8_t>();
+        }
+    }
+    HIPC(e, hipMemsetAsync(q.d_slot.p, 0, size_t(q.n_slots) * 8, s));
+    const Cls4Image& c = q.img.core;
+    const bool lin = flags & CLS_F_FORCE_LINEAR;
+    LaunchCfg cfg;
+    cfg.stream = s;
+    cfg.grid = cls_grid(e, true, q.lds_resident, c.lds_bytes, n);
+    const bool timing = flags & CLS_F_TIMING;
+    if (timing) {
+        const int rc = timing_begin(e, s);
+        if (rc != CLS_OK) return rc;
+    }
+    if (n) {
+        Cls4Dev cd = cls4_dev(c, q.d_img, q.d_lin, uint32_t(q.lin.size()), t->n_rules);
+        if (q.lds_resident) {
+            HIPC(e, q.d_part.ensure(size_t(cfg.grid) * c.n_ctr * 4));
+            cd.part = q.d_part.as<uint32_t>();
+        }
+        Fe16 fe;
+        for (int sd = 0; sd < 2; ++sd) {
+            fe.key[sd] = q.img.fe_key[sd];
+            fe.val[sd] = q.img.fe_val[sd];
+            fe.top[sd] = q.img.fe_top[sd];
+        }
+        for (uint64_t off = 0; off < n; off += kClsChunk) {
+            const uint64_t m = std::min<uint64_t>(kClsChunk, n - off);
+            Pkts16 pc{reinterpret_cast<const uint4*>(src + 16 * off), reinterpret_cast<const uint4*>(dst + 16 * off),
+                      dp + off, pr + off, m, 0u};
+            uint8_t* vo = d_verdict ? d_verdict + off : nullptr;
+            pc.vec = aligned(pc.dport, 8) && aligned(pc.proto, 4) && (!vo || aligned(vo, 4)) ? 1u : 0u;
+            HIPC(e, launch_classify16_cls(cd, fe, pc, vo, q.d_slot.as<unsigned long long>(), q.lds_resident, lin,
+                                          cfg));
+            if (timing && off + m >= n) HIPC(e, hipEventRecord(e->ev1, s));
+            if (q.lds_resident)
+                HIPC(e, launch_fold(cd.part, uint32_t(cfg.grid), c.n_ctr, q.d_slot.as<unsigned long long>(), s));
+        }
+    }
+    if (timing) {
+        if (!n) HIPC(e, hipEventRecord(e->ev1, s));
+        e->timed = true;
+    }
+    return finish_counts(e, *t, q.d_slot, q.d_map, q.n_slots, n, verdict_out, d_verdict, counters_out, flags, s);
+}
+
 int cls_classify(cls_engine* e, uint32_t table_id, const cls_pkt_soa* pk, uint64_t n,
                  uint8_t* verdict_out, uint64_t* counters_out, uint32_t flags, void* stream) {
     if (!e || !pk) return CLS_E_INVAL;
@@ -239,7 +460,8 @@ int cls_classify(cls_engine* e, uint32_t table_id, const cls_pkt_soa* pk, uint64
     auto it = e->tables.find(table_id);
     if (it == e->tables.end()) return fail(e, CLS_E_NOTFOUND, "no table %u", table_id);
     std::shared_ptr<Table> t = it->second;
-    if (pk->af != CLS_AF_V4) return fail(e, CLS_E_INVAL, "only CLS_AF_V4 batches are supported");
+    if (pk->af == CLS_AF_V16) return classify16_locked(e, t, pk, n, verdict_out, counters_out, flags, stream);
+    if (pk->af != CLS_AF_V4) return fail(e, CLS_E_INVAL, "af must be CLS_AF_V4 or CLS_AF_V16");
     if (n && (!pk->src4 || !pk->dst4 || !pk->dport || !pk->proto))
         return fail(e, CLS_E_INVAL, "missing packet arrays");
     if (!verdict_out && !(flags & CLS_F_NO_VERDICT) && n)
@@ -274,72 +496,20 @@ int cls_classify(cls_engine* e, uint32_t table_id, const cls_pkt_soa* pk, uint64
     LaunchCfg cfg;
     cfg.stream = s;
     const bool use_cls = t->has_cls && !(flags & CLS_F_FORCE_LINEAR);
-    int per_cu = 2;
-    if (use_cls) {
-        const int by_threads = 2048 / cls_block();
-        per_cu = by_threads;
-        if (t->lds_resident)
-            per_cu = std::max(1, std::min(by_threads, int(max_lds_bytes() / std::max<uint32_t>(1, t->img.lds_bytes))));
-        if (const char* w = std::getenv("CONTIVCLS_WG_PER_CU"))   // diagnostics
-            per_cu = std::max(1, std::atoi(w));
-    }
-    const uint64_t want = (n + 4ull * 1024 - 1) / (4ull * 1024);
-    cfg.grid = int(std::max<uint64_t>(1, std::min<uint64_t>(uint64_t(e->n_cu) * per_cu, want)));
+    cfg.grid = cls_grid(e, use_cls, t->lds_resident, t->img.lds_bytes, n);
 
     const bool timing = flags & CLS_F_TIMING;
     if (timing) {
-        if (e->ev_used == e->ev_pool.size()) {
-            hipEvent_t a, b;
-            HIPC(e, hipEventCreate(&a));
-            HIPC(e, hipEventCreate(&b));
-            e->ev_pool.push_back({a, b});
-        }
-        e->ev0 = e->ev_pool[e->ev_used].first;
-        e->ev1 = e->ev_pool[e->ev_used].second;
-        e->ev_used++;
-        HIPC(e, hipEventRecord(e->ev0, s));
+        const int rc = timing_begin(e, s);
+        if (rc != CLS_OK) return rc;
     }
     if (n) {
         if (use_cls) {
-            Cls4Dev cd;
-            cd.img = t->d_img.as<uint32_t>();
-            cd.img_bytes = t->img.img_bytes;
-            cd.off_bounds = t->img.off_bounds;
-            cd.off_iclass = t->img.off_iclass;
-            cd.off_cells = t->img.off_cells;
-            cd.off_lists = t->img.off_lists;
-            cd.off_tmpl = t->img.off_tmpl;
-            cd.search_top = t->img.search_top;
-            cd.n_ctr = t->img.n_ctr;
-            cd.lds_bytes = t->img.lds_bytes;
-            cd.lin = t->d_lin4.as<LinRule4>();
-            cd.n_lin = uint32_t(t->lin4.size());
-            cd.n_rules = t->n_rules;
-            cd.mode = t->img.mode;
-            cd.default_row = t->img.default_row;
-            cd.row_bytes = t->img.row_bytes;
-            cd.port_mul = t->img.port_mul;
-            cd.port_mask4 = t->img.port_mask4;
-            cd.port_dflt = t->img.port_dflt;
-            cd.n_hash = t->img.n_hash;
-            cd.list_mode = t->img.list_mode;
-            cd.bv_steps = std::max(t->img.bv_steps_d, t->img.bv_steps_p);  // mode 2: Sd
-            cd.n_hot = t->img.n_hot;
-            cd.off_ptop = t->img.off_ptop;
-            cd.bv_wide = t->img.bv_wide;
-            cd.off_hot = t->img.off_hot;
+            Cls4Dev cd = cls4_dev(t->img, t->d_img, t->d_lin4, uint32_t(t->lin4.size()), t->n_rules);
             cd.part = nullptr;
             if (t->lds_resident) {
                 HIPC(e, t->d_part.ensure(size_t(cfg.grid) * t->img.n_ctr * 4));
                 cd.part = t->d_part.as<uint32_t>();
-            }
-            for (uint32_t i = 0; i < kMaxHashLens; ++i) {
-                cd.hash_mask[i] = t->img.hash_mask[i];
-                cd.hash_shift[i] = t->img.hash_shift[i];
-                cd.hash_cap[i] = t->img.hash_cap[i];
-                cd.hash_mul[i] = t->img.hash_mul[i];
-                cd.hash_shift1[i] = 32u - 2u * (32u - t->img.hash_shift[i]);
-                cd.off_hash[i] = t->img.off_hash[i];
             }
             // the kernel indexes packets with 32-bit offsets: chunks of 2^30
             for (uint64_t off = 0; off < n; off += kClsChunk) {
@@ -365,28 +535,8 @@ int cls_classify(cls_engine* e, uint32_t table_id, const cls_pkt_soa* pk, uint64
         if (!(n && use_cls && t->lds_resident)) HIPC(e, hipEventRecord(e->ev1, s));
         e->timed = true;
     }
-    // slot counters -> rule counters
-    unsigned long long* out = dev && counters_out ? reinterpret_cast<unsigned long long*>(counters_out)
-                                                  : t->d_out.as<unsigned long long>();
-    if (counters_out || !dev) {
-        if (!(dev && (flags & CLS_F_ACCUMULATE)))
-            HIPC(e, hipMemsetAsync(out, 0, size_t(t->n_rules + 1) * 8, s));
-        HIPC(e, launch_remap(t->d_slot.as<unsigned long long>(), t->d_map.as<uint32_t>(), t->n_slots, out, s));
-    }
-    if (!dev) {
-        if (verdict_out && n) HIPC(e, hipMemcpyAsync(verdict_out, d_verdict, n, hipMemcpyDeviceToHost, s));
-        std::vector<uint64_t> tmp;
-        if (counters_out) {
-            tmp.resize(t->n_rules + 1);
-            HIPC(e, hipMemcpyAsync(tmp.data(), out, tmp.size() * 8, hipMemcpyDeviceToHost, s));
-        }
-        HIPC(e, hipStreamSynchronize(s));
-        if (counters_out) {
-            for (size_t i = 0; i < tmp.size(); ++i)
-                counters_out[i] = (flags & CLS_F_ACCUMULATE) ? counters_out[i] + tmp[i] : tmp[i];
-        }
-    }
-    return CLS_OK;
+    return finish_counts(e, *t, t->d_slot, t->d_map, t->n_slots, n, verdict_out, d_verdict, counters_out,
+                         flags, s);
 }
 
 int cls_last_kernel_ms(cls_engine* e, float* ms) {
@@ -612,6 +762,107 @@ int cls_gen_traffic_v4(cls_engine* e, const cls_traffic_spec* sp, uint64_t first
     return CLS_OK;
 }
 
+// Blob of cls_compile_v4 / cls_compile_v16: header (v4 header, then `extra`
+// bytes of a larger header), image, slot -> rule map, linear rules.
+static int write_blob(const Cls4Image* img, const std::vector<LinRule4>& lin, uint32_t n, uint32_t magic,
+                      const void* extra, size_t extra_bytes, void* blob, uint64_t cap, uint64_t* need) {
+    cls_image_v4_header h;
+    std::memset(&h, 0, sizeof h);
+    h.magic = magic;
+    h.version = 2;
+    h.n_rules = n;
+    h.n_lin = uint32_t(lin.size());
+    h.has_cls = img ? 1u : 0u;
+    if (img) {
+        const Cls4Image& im = *img;
+        h.img_bytes = im.img_bytes; h.off_bounds = im.off_bounds; h.off_iclass = im.off_iclass;
+        h.off_cells = im.off_cells; h.off_lists = im.off_lists; h.off_tmpl = im.off_tmpl;
+        h.n_bounds = im.n_bounds; h.search_top = im.search_top; h.n_classes = im.n_classes;
+        h.n_tmpl = im.n_tmpl; h.n_list_entries = im.n_list_entries; h.n_ctr = im.n_ctr;
+        h.lds_bytes = im.lds_bytes;
+        h.mode = im.mode;
+        h.default_class = im.default_class;
+        h.n_hash = im.n_hash;
+        h.list_mode = im.list_mode;
+        h.off_bv = im.off_bv;
+        h.bv_steps_d = im.bv_steps_d;
+        h.bv_steps_p = im.bv_steps_p;
+        h.off_ptop = im.off_ptop;
+        h.n_pclass = im.n_pclass;
+        h.bv_wide = im.bv_wide;
+        h.row_bytes = im.row_bytes;
+        h.port_mul = im.port_mul;
+        h.port_mask4 = im.port_mask4;
+        h.port_dflt = im.port_dflt;
+        h.default_row = im.default_row;
+        h.n_hot = im.n_hot;
+        h.off_hot = im.off_hot;
+        for (uint32_t i = 0; i < kMaxHashLens; ++i) {
+            h.hash_mask[i] = im.hash_mask[i];
+            h.hash_shift[i] = im.hash_shift[i];
+            h.hash_cap[i] = im.hash_cap[i];
+            h.hash_mul[i] = im.hash_mul[i];
+            h.off_hash[i] = im.off_hash[i];
+        }
+    }
+    auto al = [](uint64_t x) { return (x + 15) & ~uint64_t(15); };
+    h.off_image = uint32_t(al(sizeof h + extra_bytes));
+    h.off_ctr_rule = uint32_t(al(h.off_image + h.img_bytes));
+    h.off_lin = uint32_t(al(h.off_ctr_rule + uint64_t(h.n_ctr) * 4));
+    h.total_bytes = uint32_t(h.off_lin + lin.size() * sizeof(LinRule4));
+    *need = h.total_bytes;
+    if (!blob || cap < h.total_bytes) return CLS_OK;
+    uint8_t* b = static_cast<uint8_t*>(blob);
+    std::memset(b, 0, h.total_bytes);
+    std::memcpy(b, &h, sizeof h);
+    if (extra_bytes) std::memcpy(b + sizeof h, extra, extra_bytes);
+    if (img) {
+        std::memcpy(b + h.off_image, img->words.data(), img->img_bytes);
+        std::memcpy(b + h.off_ctr_rule, img->ctr_rule.data(), size_t(h.n_ctr) * 4);
+    }
+    if (!lin.empty()) std::memcpy(b + h.off_lin, lin.data(), lin.size() * sizeof(LinRule4));
+    return CLS_OK;
+}
+
+int cls_gen_traffic_v16(cls_engine* e, const cls_traffic_spec16* sp, uint64_t first, uint64_t n,
+                        uint8_t* src16, uint8_t* dst16, uint16_t* sport, uint16_t* dport, uint8_t* proto,
+                        void* stream) {
+    if (!e || !sp) return CLS_E_INVAL;
+    if ((src16 && !aligned(src16, 16)) || (dst16 && !aligned(dst16, 16)))
+        return fail(e, CLS_E_INVAL, "src16/dst16 must be 16-byte aligned");
+    std::lock_guard<std::mutex> g(e->mu);
+    HIPC(e, hipSetDevice(e->device));
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : e->stream;
+    // pools as (hi, lo) u64 pairs in address order
+    auto pairs = [](const uint8_t* b, uint32_t m) {
+        std::vector<uint64_t> v(size_t(m) * 2, 0);
+        for (uint32_t j = 0; j < m; ++j)
+            for (int k = 0; k < 16; ++k) v[2 * j + k / 8] = (v[2 * j + k / 8] << 8) | b[16 * size_t(j) + k];
+        return v;
+    };
+    const std::vector<uint64_t> pods = pairs(sp->pod_ips, sp->n_pod_ips), dsta = pairs(sp->dst_addrs, sp->n_dst);
+    const size_t bp = pods.size() * 8, bd = dsta.size() * 8, bl = sp->n_dst, bq = size_t(sp->n_ports) * 2;
+    auto al = [](size_t x) { return (x + 15) & ~size_t(15); };
+    HIPC(e, e->s_pool.ensure(al(bp) + al(bd) + al(bl) + al(bq) + 16));
+    uint8_t* base = e->s_pool.as<uint8_t>();
+    TrafficDev16 t;
+    t.seed = sp->seed;
+    t.pct_pod = sp->pct_pod_src; t.pct_dst = sp->pct_rule_dst;
+    t.pct_port = sp->pct_table_port; t.pct_icmp = sp->pct_icmp;
+    t.pods = reinterpret_cast<const uint64_t*>(base); t.n_pods = sp->n_pod_ips;
+    t.dst_addrs = reinterpret_cast<const uint64_t*>(base + al(bp));
+    t.dst_lens = base + al(bp) + al(bd); t.n_dst = sp->n_dst;
+    t.ports = reinterpret_cast<const uint16_t*>(base + al(bp) + al(bd) + al(bl)); t.n_ports = sp->n_ports;
+    if (bp) HIPC(e, hipMemcpyAsync(base, pods.data(), bp, hipMemcpyHostToDevice, s));
+    if (bd) HIPC(e, hipMemcpyAsync(base + al(bp), dsta.data(), bd, hipMemcpyHostToDevice, s));
+    if (bl) HIPC(e, hipMemcpyAsync(base + al(bp) + al(bd), sp->dst_lens, bl, hipMemcpyHostToDevice, s));
+    if (bq) HIPC(e, hipMemcpyAsync(base + al(bp) + al(bd) + al(bl), sp->ports, bq, hipMemcpyHostToDevice, s));
+    HIPC(e, launch_gen16(t, first, n, reinterpret_cast<uint4*>(src16), reinterpret_cast<uint4*>(dst16), sport, dport,
+                         proto, s));
+    HIPC(e, hipStreamSynchronize(s));   // the pools are engine scratch
+    return CLS_OK;
+}
+
 int cls_compile_v4(const cls_rule* rules, uint32_t n, void* blob, uint64_t cap, uint64_t* need) {
     if ((n && !rules) || !need) return CLS_E_INVAL;
     std::vector<SemRule> sem;
@@ -621,60 +872,28 @@ int cls_compile_v4(const cls_rule* rules, uint32_t n, void* blob, uint64_t cap, 
     std::vector<LinRule4> lin = linear4(sem);
     Cls4Image img;
     const bool has = sem.size() > 8 && build_cls4(sem, n, img, why);
-    cls_image_v4_header h;
-    std::memset(&h, 0, sizeof h);
-    h.magic = 0x434C5334u;
-    h.version = 2;
-    h.n_rules = n;
-    h.n_lin = uint32_t(lin.size());
-    h.has_cls = has ? 1u : 0u;
-    if (has) {
-        h.img_bytes = img.img_bytes; h.off_bounds = img.off_bounds; h.off_iclass = img.off_iclass;
-        h.off_cells = img.off_cells; h.off_lists = img.off_lists; h.off_tmpl = img.off_tmpl;
-        h.n_bounds = img.n_bounds; h.search_top = img.search_top; h.n_classes = img.n_classes;
-        h.n_tmpl = img.n_tmpl; h.n_list_entries = img.n_list_entries; h.n_ctr = img.n_ctr;
-        h.lds_bytes = img.lds_bytes;
-        h.mode = img.mode;
-        h.default_class = img.default_class;
-        h.n_hash = img.n_hash;
-        h.list_mode = img.list_mode;
-        h.off_bv = img.off_bv;
-        h.bv_steps_d = img.bv_steps_d;
-        h.bv_steps_p = img.bv_steps_p;
-        h.off_ptop = img.off_ptop;
-        h.n_pclass = img.n_pclass;
-        h.bv_wide = img.bv_wide;
-        h.row_bytes = img.row_bytes;
-        h.port_mul = img.port_mul;
-        h.port_mask4 = img.port_mask4;
-        h.port_dflt = img.port_dflt;
-        h.default_row = img.default_row;
-        h.n_hot = img.n_hot;
-        h.off_hot = img.off_hot;
-        for (uint32_t i = 0; i < kMaxHashLens; ++i) {
-            h.hash_mask[i] = img.hash_mask[i];
-            h.hash_shift[i] = img.hash_shift[i];
-            h.hash_cap[i] = img.hash_cap[i];
-            h.hash_mul[i] = img.hash_mul[i];
-            h.off_hash[i] = img.off_hash[i];
-        }
+    return write_blob(has ? &img : nullptr, lin, n, 0x434C5334u, nullptr, 0, blob, cap, need);
+}
+
+int cls_compile_v16(const cls_rule* rules, uint32_t n, void* blob, uint64_t cap, uint64_t* need) {
+    if ((n && !rules) || !need) return CLS_E_INVAL;
+    std::vector<SemRule> sem;
+    std::string why;
+    int rc = semantic_rules(rules, n, 0, sem, why);
+    if (rc != CLS_OK) return rc;
+    Cls16Image img;
+    if (!build_cls16(sem, n, img, why)) return CLS_E_INVAL;
+    cls_image_v16_header h16;
+    std::memset(&h16, 0, sizeof h16);
+    for (int sd = 0; sd < 2; ++sd) {
+        h16.fe_key[sd] = img.fe_key[sd];
+        h16.fe_val[sd] = img.fe_val[sd];
+        h16.fe_top[sd] = img.fe_top[sd];
+        h16.fe_n[sd] = img.fe_n[sd];
     }
-    auto al = [](uint64_t x) { return (x + 15) & ~uint64_t(15); };
-    h.off_image = uint32_t(al(sizeof h));
-    h.off_ctr_rule = uint32_t(al(h.off_image + h.img_bytes));
-    h.off_lin = uint32_t(al(h.off_ctr_rule + uint64_t(h.n_ctr) * 4));
-    h.total_bytes = uint32_t(h.off_lin + lin.size() * sizeof(LinRule4));
-    *need = h.total_bytes;
-    if (!blob || cap < h.total_bytes) return CLS_OK;
-    uint8_t* b = static_cast<uint8_t*>(blob);
-    std::memset(b, 0, h.total_bytes);
-    std::memcpy(b, &h, sizeof h);
-    if (has) {
-        std::memcpy(b + h.off_image, img.words.data(), img.img_bytes);
-        std::memcpy(b + h.off_ctr_rule, img.ctr_rule.data(), size_t(h.n_ctr) * 4);
-    }
-    if (!lin.empty()) std::memcpy(b + h.off_lin, lin.data(), lin.size() * sizeof(LinRule4));
-    return CLS_OK;
+    const size_t extra = sizeof h16 - sizeof h16.core;
+    return write_blob(&img.core, linear4(img.sem), n, 0x434C3136u, reinterpret_cast<const uint8_t*>(&h16) + sizeof h16.core,
+                      extra, blob, cap, need);
 }
 
 }  // extern "C"

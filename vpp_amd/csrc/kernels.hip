@@ -444,19 +444,40 @@ __device__ __forceinline__ void run_n(const Img<kLds>& im, const Cls4Dev& t, uin
 #endif
 constexpr int kG = CLS_GROUPS;     // 16-B packet groups per lane per step
 
+// Stage the read-only image into LDS (at address 0) and zero the counters.
+__device__ __forceinline__ void stage_lds(const Cls4Dev& t, uint4* smem) {
+    const uint4* src4 = reinterpret_cast<const uint4*>(t.img);
+    const uint32_t n4 = t.img_bytes / 16u;
+    for (uint32_t i = threadIdx.x; i < n4; i += blockDim.x) smem[i] = src4[i];
+    uint32_t* lctr = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(smem) + t.img_bytes);
+    for (uint32_t i = threadIdx.x; i < (t.lds_bytes - t.img_bytes) / 4u; i += blockDim.x) lctr[i] = 0u;
+    __syncthreads();
+}
+
+// End of an LDS-resident launch: fold the per-lane hot rows into their slots,
+// then store this workgroup's slot counters plainly into its own row of the
+// partials (fold_kernel sums the rows): no global atomics from every
+// workgroup onto the same addresses at the end of the launch.
+__device__ __forceinline__ void flush_lds(const Cls4Dev& t, uint4* smem) {
+    __syncthreads();
+    uint32_t* lctr = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(smem) + t.img_bytes);
+    const uint32_t* hrow = reinterpret_cast<const uint32_t*>(reinterpret_cast<uint8_t*>(smem) + t.off_hot);
+    for (uint32_t i = threadIdx.x; i < t.n_hot * 64u; i += blockDim.x) {
+        const uint32_t v = hrow[i];
+        if (v) atomicAdd(&lctr[i >> 6], v);
+    }
+    __syncthreads();
+    uint32_t* part = t.part + size_t(blockIdx.x) * t.n_ctr;
+    if constexpr (!(CLS_ABLATE & 16))
+        for (uint32_t i = threadIdx.x; i < t.n_ctr; i += blockDim.x) part[i] = lctr[i];
+}
+
 template <bool kLds, bool kVec, int kMode, int kList, int kD>
 __global__ __launch_bounds__(kClsBlock) void classify4_cls(Cls4Dev t, Pkts4 p, uint8_t* verdict,
                                                            unsigned long long* gslot) {
     extern __shared__ uint4 smem[];
     Img<kLds> im{reinterpret_cast<const uint8_t*>(t.img)};
-    if constexpr (kLds && !(CLS_ABLATE & 16)) {
-        const uint4* src4 = reinterpret_cast<const uint4*>(t.img);
-        const uint32_t n4 = t.img_bytes / 16u;
-        for (uint32_t i = threadIdx.x; i < n4; i += blockDim.x) smem[i] = src4[i];
-        uint32_t* lctr = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(smem) + t.img_bytes);
-        for (uint32_t i = threadIdx.x; i < (t.lds_bytes - t.img_bytes) / 4u; i += blockDim.x) lctr[i] = 0u;
-        __syncthreads();
-    }
+    if constexpr (kLds && !(CLS_ABLATE & 16)) stage_lds(t, smem);
 
     const uint32_t nthreads = gridDim.x * blockDim.x;
     const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
@@ -572,23 +593,138 @@ __global__ __launch_bounds__(kClsBlock) void classify4_cls(Cls4Dev t, Pkts4 p, u
     if constexpr (!kLds) {
         if (hot0) atomicAdd(&gslot[0], (unsigned long long)hot0);
     }
-    if constexpr (kLds) {
-        __syncthreads();
-        // fold the per-lane hot rows into their slots
-        uint32_t* lctr = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(smem) + t.img_bytes);
-        const uint32_t* hrow = reinterpret_cast<const uint32_t*>(reinterpret_cast<uint8_t*>(smem) + t.off_hot);
-        for (uint32_t i = threadIdx.x; i < t.n_hot * 64u; i += blockDim.x) {
-            const uint32_t v = hrow[i];
-            if (v) atomicAdd(&lctr[i >> 6], v);
-        }
-        __syncthreads();
-        // This workgroup's slot counters, stored plainly into its own row of
-        // the partials (fold_kernel sums the rows): no global atomics from
-        // every workgroup onto the same addresses at the end of the launch.
-        uint32_t* part = t.part + size_t(blockIdx.x) * t.n_ctr;
-        if constexpr (!(CLS_ABLATE & 16))
-            for (uint32_t i = threadIdx.x; i < t.n_ctr; i += blockDim.x) part[i] = lctr[i];
+    if constexpr (kLds) flush_lds(t, smem);
+}
+
+// ---------------------------------------------------------------------------
+// 16-byte path (IPv6 and IPv4-mapped addresses, compile.hpp Cls16Image): the
+// front end maps each 128-bit address to its 32-bit representative with one
+// branch-free binary search over the elementary intervals (16-B keys: interval
+// start - 1 as u64 hi, lo), then the IPv4 classifier runs on the reps.
+
+// 128-bit address as loaded (network-order bytes in little-endian words)
+// -> (hi, lo) u64 in address order
+__device__ __forceinline__ void addr128(const uint4& a, uint64_t& hi, uint64_t& lo) {
+    hi = (uint64_t(__builtin_bswap32(a.x)) << 32) | __builtin_bswap32(a.y);
+    lo = (uint64_t(__builtin_bswap32(a.z)) << 32) | __builtin_bswap32(a.w);
+}
+
+template <int N, bool kLds>
+__device__ __forceinline__ void fe_rep(const Img<kLds>& im, uint32_t off_key, uint32_t off_val,
+                                       uint32_t top, const uint4 (&a)[N], uint32_t (&rep)[N]) {
+    uint64_t kh[N], kl[N];
+    uint32_t pos[N];
+#pragma unroll
+    for (int q = 0; q < N; ++q) {
+        addr128(a[q], kh[q], kl[q]);
+        pos[q] = off_key;
     }
+#pragma unroll 1
+    for (uint32_t s = top >> 1; s; s >>= 1) {
+        const uint32_t step = 16u * s;
+        uint4 e[N];
+#pragma unroll
+        for (int q = 0; q < N; ++q) e[q] = im.u128(pos[q] + step);
+#pragma unroll
+        for (int q = 0; q < N; ++q) {
+            const uint64_t eh = (uint64_t(e[q].y) << 32) | e[q].x, el = (uint64_t(e[q].w) << 32) | e[q].z;
+            const bool lt = eh < kh[q] || (eh == kh[q] && el < kl[q]);      // start - 1 < addr
+            pos[q] = lt ? pos[q] + step : pos[q];
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < N; ++q) rep[q] = im.u32(off_val + ((pos[q] - off_key) >> 2));
+}
+
+// Linear first match over the rules in rep space (the 16-byte path's GPU
+// cross-check, CLS_F_FORCE_LINEAR): direct rule slots after the n_ctr slots.
+template <int N>
+__device__ __forceinline__ void lin_n(const Cls4Dev& t, unsigned long long* gslot, const uint32_t (&s)[N],
+                                      const uint32_t (&d)[N], const uint32_t (&dp)[N],
+                                      const uint32_t (&pr)[N], uint32_t (&res)[N]) {
+#pragma unroll
+    for (int q = 0; q < N; ++q) {
+        uint32_t rule;
+        linear_one(t.lin, t.n_lin, t.n_rules, s[q], d[q], dp[q], min(pr[q], 3u), res[q], rule);
+        atomicAdd(&gslot[t.n_ctr + rule], 1ull);
+    }
+}
+
+template <bool kLds, int kMode, int kList, int kD, bool kLin>
+__global__ __launch_bounds__(kClsBlock) void classify16_cls(Cls4Dev t, Fe16 fe, Pkts16 p, uint8_t* verdict,
+                                                            unsigned long long* gslot) {
+    extern __shared__ uint4 smem[];
+    Img<kLds> im{reinterpret_cast<const uint8_t*>(t.img)};
+    if constexpr (kLds) stage_lds(t, smem);
+    const uint32_t nthreads = gridDim.x * blockDim.x;
+    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t hot0 = 0;
+    const uint32_t hot_lane = t.off_hot + 4u * (threadIdx.x & 63u);
+    auto run = [&](auto& sa, auto& da, auto& pa, auto& ra, bool other, auto& v) {
+        if constexpr (kLin) lin_n(t, gslot, sa, da, pa, ra, v);
+        else run_n<sizeof(v) / 4, kLds, kMode, kList, kD>(im, t, hot_lane, gslot, hot0, sa, da, pa, ra, other, v);
+    };
+    // 4 packets per lane per step (vector dport / proto / verdict words),
+    // the next step's loads in flight during this step's lookups
+    const uint32_t nsteps = p.vec ? uint32_t(p.n / 4u) : 0u;
+    const uint2* DP = reinterpret_cast<const uint2*>(p.dport);
+    const uint32_t* PR = reinterpret_cast<const uint32_t*>(p.proto);
+    struct Buf {
+        uint4 s[4], d[4];
+        uint2 dp;
+        uint32_t pr;
+    };
+    auto load = [&](Buf& b, uint32_t g, bool ok) {
+        if (ok) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                b.s[k] = ldnt(at(p.src, 4u * g + k));
+                b.d[k] = ldnt(at(p.dst, 4u * g + k));
+            }
+            b.dp = ldnt(at(DP, g));
+            b.pr = ldnt(at(PR, g));
+        }
+    };
+    auto step = [&](const Buf& b, uint32_t g) {
+        uint32_t sa[4], da[4], v[4];
+        fe_rep<4, kLds>(im, fe.key[0], fe.val[0], fe.top[0], b.s, sa);
+        fe_rep<4, kLds>(im, fe.key[1], fe.val[1], fe.top[1], b.d, da);
+        const uint32_t pr = b.pr;
+        uint32_t pa[4] = {b.dp.x & 0xFFFFu, b.dp.x >> 16, b.dp.y & 0xFFFFu, b.dp.y >> 16};
+        uint32_t ra[4] = {pr & 0xFFu, (pr >> 8) & 0xFFu, (pr >> 16) & 0xFFu, pr >> 24};
+        run(sa, da, pa, ra, ((pr | ((pr & 0x7F7F7F7Fu) + 0x7D7D7D7Du)) & 0x80808080u) != 0u, v);
+        if (verdict)
+            stnt(v[0] | (v[1] << 8) | (v[2] << 16) | (v[3] << 24),
+                 const_cast<uint32_t*>(at(reinterpret_cast<const uint32_t*>(verdict), g)));
+    };
+    {
+        Buf a, b;
+        uint32_t g = tid;
+        load(a, g, g < nsteps);
+        while (g < nsteps) {
+            load(b, g + nthreads, g + nthreads < nsteps);
+            step(a, g);
+            g += nthreads;
+            if (g >= nsteps) break;
+            load(a, g + nthreads, g + nthreads < nsteps);
+            step(b, g);
+            g += nthreads;
+        }
+    }
+    for (uint32_t i = nsteps * 4u + tid; i < uint32_t(p.n); i += nthreads) {
+        const uint4 s1[1] = {ldnt(at(p.src, i))}, d1[1] = {ldnt(at(p.dst, i))};
+        uint32_t sa[1], da[1], v[1];
+        fe_rep<1, kLds>(im, fe.key[0], fe.val[0], fe.top[0], s1, sa);
+        fe_rep<1, kLds>(im, fe.key[1], fe.val[1], fe.top[1], d1, da);
+        uint32_t pa[1] = {p.dport[i]}, ra[1] = {p.proto[i]};
+        if constexpr (kLin) lin_n(t, gslot, sa, da, pa, ra, v);
+        else run_n<1, kLds, kMode, kList, -1>(im, t, hot_lane, gslot, hot0, sa, da, pa, ra, ra[0] > 2u, v);
+        if (verdict) verdict[i] = uint8_t(v[0]);
+    }
+    if constexpr (!kLds) {
+        if (hot0) atomicAdd(&gslot[0], (unsigned long long)hot0);
+    }
+    if constexpr (kLds) flush_lds(t, smem);
 }
 
 // gslot[i] += sum over the grid's rows of part[w][i].  Thread (slot i, row
@@ -766,6 +902,63 @@ __global__ void gen4_kernel(TrafficDev t, uint64_t first, uint64_t n, uint32_t* 
     }
 }
 
+// (hi, lo) address -> the 16 network-order bytes as stored (little-endian words)
+__device__ __forceinline__ uint4 store16(uint64_t hi, uint64_t lo) {
+    return make_uint4(__builtin_bswap32(uint32_t(hi >> 32)), __builtin_bswap32(uint32_t(hi)),
+                      __builtin_bswap32(uint32_t(lo >> 32)), __builtin_bswap32(uint32_t(lo)));
+}
+
+__global__ void gen16_kernel(TrafficDev16 t, uint64_t first, uint64_t n, uint4* src, uint4* dst,
+                             uint16_t* sport, uint16_t* dport, uint8_t* proto) {
+    const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
+    const uint64_t fd00 = 0xFD00ull << 48, mapped = 0xFFFFull << 32;
+    for (uint64_t k = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; k < n; k += stride) {
+        const uint64_t i = first + k;
+        uint64_t w[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) w[j] = mix64(t.seed ^ ((8ull * i + uint64_t(j)) * kGolden));
+        const uint32_t a0 = uint32_t(w[0]), b0 = uint32_t(w[0] >> 32);
+        uint8_t pr;
+        if (a0 % 100u < t.pct_icmp) pr = 2;
+        else pr = (b0 & 1u) ? 1 : 0;
+        uint64_t sh, sl;
+        const uint32_t b1 = uint32_t(w[1] >> 32);
+        if (t.n_pods && ((b0 >> 1) % 100u) < t.pct_pod) {
+            const uint32_t j = b1 % t.n_pods;
+            sh = t.pods[2 * j];
+            sl = t.pods[2 * j + 1];
+        } else if (b1 & 1u) {
+            sh = fd00; sl = w[6];
+        } else {
+            sh = 0; sl = mapped | uint32_t(w[1]);
+        }
+        const uint32_t a2 = uint32_t(w[2]), b2 = uint32_t(w[2] >> 32);
+        uint64_t dh, dl;
+        if (t.n_dst && (a2 % 100u) < t.pct_dst) {
+            const uint32_t j = b2 % t.n_dst;
+            const uint32_t len = t.dst_lens[j];
+            const uint64_t mh = len == 0 ? 0ull : len >= 64 ? ~0ull : ~0ull << (64 - len);
+            const uint64_t ml = len <= 64 ? 0ull : len >= 128 ? ~0ull : ~0ull << (128 - len);
+            dh = (t.dst_addrs[2 * j] & mh) | (w[3] & ~mh);
+            dl = (t.dst_addrs[2 * j + 1] & ml) | (w[7] & ~ml);
+        } else if (b2 & 1u) {
+            dh = fd00; dl = w[7];
+        } else {
+            dh = 0; dl = mapped | uint32_t(w[3]);
+        }
+        const uint32_t a4 = uint32_t(w[4]), b4 = uint32_t(w[4] >> 32);
+        uint16_t dp;
+        if (t.n_ports && (a4 % 100u) < t.pct_port) dp = t.ports[b4 % t.n_ports];
+        else dp = uint16_t(w[5]);
+        const uint16_t sp = uint16_t(1024u + (uint32_t(w[5] >> 32) % 64512u));
+        if (src) src[k] = store16(sh, sl);
+        if (dst) dst[k] = store16(dh, dl);
+        if (sport) sport[k] = sp;
+        if (dport) dport[k] = dp;
+        if (proto) proto[k] = pr;
+    }
+}
+
 }  // namespace
 
 int max_lds_bytes() { return kLdsMax; }
@@ -834,6 +1027,65 @@ hipError_t launch_classify4_cls(const Cls4Dev& t, const Pkts4& p, uint8_t* verdi
     return hipGetLastError();
 }
 
+template <bool kLds, int kMode, int kList, int kD, bool kLin>
+static void launch16_d(const Cls4Dev& t, const Fe16& fe, const Pkts16& p, uint8_t* verdict,
+                       unsigned long long* gslot, const LaunchCfg& cfg) {
+    const size_t lds = kLds ? t.lds_bytes : 0;
+    if (kLds)
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(classify16_cls<kLds, kMode, kList, kD, kLin>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
+    hipLaunchKernelGGL((classify16_cls<kLds, kMode, kList, kD, kLin>), dim3(cfg.grid), dim3(kClsBlock), lds,
+                       cfg.stream, t, fe, p, verdict, gslot);
+}
+
+template <bool kLds, int kMode, int kList>
+static void launch16_cls(const Cls4Dev& t, const Fe16& fe, const Pkts16& p, uint8_t* verdict,
+                         unsigned long long* gslot, const LaunchCfg& cfg) {
+    if constexpr (kLds && kList >= 3) {
+        switch (t.bv_steps) {
+        case 0: launch16_d<kLds, kMode, kList, 0, false>(t, fe, p, verdict, gslot, cfg); return;
+        case 1: launch16_d<kLds, kMode, kList, 1, false>(t, fe, p, verdict, gslot, cfg); return;
+        case 2: launch16_d<kLds, kMode, kList, 2, false>(t, fe, p, verdict, gslot, cfg); return;
+        case 3: launch16_d<kLds, kMode, kList, 3, false>(t, fe, p, verdict, gslot, cfg); return;
+        case 4: launch16_d<kLds, kMode, kList, 4, false>(t, fe, p, verdict, gslot, cfg); return;
+        case 5: launch16_d<kLds, kMode, kList, 5, false>(t, fe, p, verdict, gslot, cfg); return;
+        default: break;
+        }
+    }
+    launch16_d<kLds, kMode, kList, -1, false>(t, fe, p, verdict, gslot, cfg);
+}
+
+template <bool kLds>
+static void dispatch16(const Cls4Dev& t, const Fe16& fe, const Pkts16& p, uint8_t* verdict,
+                       unsigned long long* gslot, bool lin, const LaunchCfg& cfg) {
+    if (lin) {
+        launch16_d<kLds, 0, 0, -1, true>(t, fe, p, verdict, gslot, cfg);
+        return;
+    }
+    const int src = t.mode != 1 ? 0 : t.n_hash == 1 ? 2 : 1;
+#define CLS16_SRC_CASES(L)                                                                  \
+    case 3 * L + 0: launch16_cls<kLds, 0, L>(t, fe, p, verdict, gslot, cfg); break;         \
+    case 3 * L + 1: launch16_cls<kLds, 1, L>(t, fe, p, verdict, gslot, cfg); break;         \
+    case 3 * L + 2: launch16_cls<kLds, 2, L>(t, fe, p, verdict, gslot, cfg); break;
+    switch (src + 3 * int(t.list_mode)) {
+        CLS16_SRC_CASES(0)
+        CLS16_SRC_CASES(1)
+        CLS16_SRC_CASES(2)
+        CLS16_SRC_CASES(3)
+        CLS16_SRC_CASES(4)
+    default: break;
+    }
+#undef CLS16_SRC_CASES
+}
+
+hipError_t launch_classify16_cls(const Cls4Dev& t, const Fe16& fe, const Pkts16& p, uint8_t* verdict,
+                                 unsigned long long* gslot, bool lds_resident, bool lin,
+                                 const LaunchCfg& cfg) {
+    if (lds_resident) dispatch16<true>(t, fe, p, verdict, gslot, lin, cfg);
+    else dispatch16<false>(t, fe, p, verdict, gslot, lin, cfg);
+    return hipGetLastError();
+}
+
 hipError_t launch_classify4_linear(const LinRule4* rules, uint32_t n_lin, uint32_t n_rules,
                                    const Pkts4& p, uint8_t* verdict, unsigned long long* gslot,
                                    const LaunchCfg& cfg) {
@@ -864,6 +1116,16 @@ hipError_t launch_connect4(const AclDesc* acls, const IfAcls* ifs, const uint32_
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(connect4_kernel, dim3(uint32_t((n + 255) / 256)), dim3(256), 0, s, acls, ifs,
                        src_if, dst_if, src, dst, sport, dport, proto, n, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_gen16(const TrafficDev16& t, uint64_t first, uint64_t n, uint4* src, uint4* dst,
+                        uint16_t* sport, uint16_t* dport, uint8_t* proto, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    uint64_t blocks = (n + 255) / 256;
+    if (blocks > 65536) blocks = 65536;
+    hipLaunchKernelGGL(gen16_kernel, dim3(uint32_t(blocks)), dim3(256), 0, s, t, first, n, src, dst, sport,
+                       dport, proto);
     return hipGetLastError();
 }
 

@@ -17,6 +17,22 @@ struct Pkts4 {
     uint64_t n;
 };
 
+// 16-byte packet batch: network-order addresses (IPv4-mapped = IPv4 packet)
+struct Pkts16 {
+    const uint4* src;          // 16-B aligned
+    const uint4* dst;
+    const uint16_t* dport;
+    const uint8_t* proto;
+    uint64_t n;
+    uint32_t vec;              // dport 8-B, proto and verdict 4-B aligned: 4 packets per lane
+};
+
+// 16-byte front end (Cls16Image): per side (0 src, 1 dst) the key array's
+// and the rep array's LDS byte offsets and the padded key count
+struct Fe16 {
+    uint32_t key[2], val[2], top[2];
+};
+
 struct Cls4Dev {
     const uint32_t* img;       // classifier image (device)
     uint32_t img_bytes;
@@ -54,6 +70,10 @@ struct LaunchCfg {
 hipError_t launch_classify4_cls(const Cls4Dev& t, const Pkts4& p, uint8_t* verdict,
                                 unsigned long long* gslot, bool lds_resident, bool vec,
                                 const LaunchCfg& cfg);
+// lin: linear first match over the rep-space rules (t.lin) after the front end
+hipError_t launch_classify16_cls(const Cls4Dev& t, const Fe16& fe, const Pkts16& p, uint8_t* verdict,
+                                 unsigned long long* gslot, bool lds_resident, bool lin,
+                                 const LaunchCfg& cfg);
 hipError_t launch_classify4_linear(const LinRule4* rules, uint32_t n_lin, uint32_t n_rules,
                                    const Pkts4& p, uint8_t* verdict, unsigned long long* gslot,
                                    const LaunchCfg& cfg);
@@ -87,6 +107,17 @@ struct TrafficDev {
 hipError_t launch_gen4(const TrafficDev& t, uint64_t first, uint64_t n, uint32_t* src,
                        uint32_t* dst, uint16_t* sport, uint16_t* dport, uint8_t* proto,
                        hipStream_t s);
+
+// 16-byte stream (contivcls.h cls_traffic_spec16); pools as (hi, lo) u64 pairs
+struct TrafficDev16 {
+    uint64_t seed;
+    uint32_t pct_pod, pct_dst, pct_port, pct_icmp;
+    const uint64_t* pods; uint32_t n_pods;
+    const uint64_t* dst_addrs; const uint8_t* dst_lens; uint32_t n_dst;
+    const uint16_t* ports; uint32_t n_ports;
+};
+hipError_t launch_gen16(const TrafficDev16& t, uint64_t first, uint64_t n, uint4* src, uint4* dst,
+                        uint16_t* sport, uint16_t* dport, uint8_t* proto, hipStream_t s);
 
 int max_lds_bytes();             // per-workgroup LDS the classify kernel may use
 int cls_block();                 // classify workgroup size

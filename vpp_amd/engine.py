@@ -96,12 +96,21 @@ class Engine:
     # -- classify ---------------------------------------------------------
     def classify(self, table: Table, src, dst, dport, proto, verdict=None, counters=None,
                  force_linear=False, timing=False, accumulate=False, stream=None):
-        """IPv4 batch.  numpy inputs: synchronous, returns (verdict, counters)
-        as numpy arrays.  torch device tensors: enqueued on ``stream`` (a
-        torch.cuda.Stream or raw handle; default torch's current stream);
-        ``verdict`` (uint8[n]) and ``counters`` (int64[R+1]) are written."""
+        """A packet batch: IPv4 (src, dst: uint32[n], host order) or the
+        16-byte layout (src, dst: uint8[n, 16], network order; IPv4-mapped
+        addresses are IPv4 packets).  numpy inputs: synchronous, returns
+        (verdict, counters) as numpy arrays.  torch device tensors: enqueued on
+        ``stream`` (a torch.cuda.Stream or raw handle; default torch's current
+        stream); ``verdict`` (uint8[n]) and ``counters`` (int64[R+1]) are
+        written."""
         n = int(len(dport))
         dev = _is_torch(src)
+        v16 = (src.dim() if dev else np.ndim(src)) == 2
+
+        def soa(s_, d_, dp_, pr_):
+            if v16:
+                return _abi.PktSoa(_abi.AF_V16, None, None, _ptr(s_), _ptr(d_), None, _ptr(dp_), _ptr(pr_))
+            return _abi.PktSoa(_abi.AF_V4, _ptr(s_), _ptr(d_), None, None, None, _ptr(dp_), _ptr(pr_))
         flags = 0
         if force_linear:
             flags |= _abi.F_FORCE_LINEAR
@@ -117,17 +126,18 @@ class Engine:
             if stream is None:
                 stream = torch.cuda.current_stream()
             s = stream.cuda_stream if hasattr(stream, "cuda_stream") else stream
-            pk = _abi.PktSoa(_abi.AF_V4, _ptr(src), _ptr(dst), None, None, None, _ptr(dport), _ptr(proto))
+            pk = soa(src, dst, dport, proto)
             self._check(_abi.lib().cls_classify(self.h, table.id, C.byref(pk), n, _ptr(verdict),
                                                 _ptr(counters), flags, s))
             return verdict, counters
-        src = np.ascontiguousarray(src, np.uint32)
-        dst = np.ascontiguousarray(dst, np.uint32)
+        adt = np.uint8 if v16 else np.uint32
+        src = np.ascontiguousarray(src, adt)
+        dst = np.ascontiguousarray(dst, adt)
         dport = np.ascontiguousarray(dport, np.uint16)
         proto = np.ascontiguousarray(proto, np.uint8)
         v = np.zeros(n, np.uint8) if verdict is None else verdict
         c = np.zeros(table.n_rules + 1, np.uint64) if counters is None else counters
-        pk = _abi.PktSoa(_abi.AF_V4, _ptr(src), _ptr(dst), None, None, None, _ptr(dport), _ptr(proto))
+        pk = soa(src, dst, dport, proto)
         self._check(_abi.lib().cls_classify(self.h, table.id, C.byref(pk), n, _ptr(v), _ptr(c),
                                             flags, None))
         return v, c
@@ -165,6 +175,26 @@ class Engine:
         if stream is not None:
             s = stream.cuda_stream if hasattr(stream, "cuda_stream") else stream
         self._check(_abi.lib().cls_gen_traffic_v4(
+            self.h, C.byref(ts), first, n, _ptr(out.get("src")), _ptr(out.get("dst")),
+            _ptr(out.get("sport")), _ptr(out.get("dport")), _ptr(out.get("proto")), s))
+
+    def gen_traffic_v16(self, spec: dict, first: int, out: dict, stream=None):
+        """The 16-byte stream (cls_traffic_spec16) into device tensors: src,
+        dst uint8[n, 16] (16-B aligned), sport, dport, proto.  Pools:
+        pod_ips / dst_addrs uint8[m, 16], dst_lens 0..128, ports."""
+        pods = np.ascontiguousarray(spec.get("pod_ips", np.zeros((0, 16))), np.uint8)
+        da = np.ascontiguousarray(spec.get("dst_addrs", np.zeros((0, 16))), np.uint8)
+        dl = np.ascontiguousarray(spec.get("dst_lens", []), np.uint8)
+        ports = np.ascontiguousarray(spec.get("ports", []), np.uint16)
+        ts = _abi.TrafficSpec16(spec["seed"], spec.get("pct_pod_src", 60), spec.get("pct_rule_dst", 50),
+                                spec.get("pct_table_port", 50), spec.get("pct_icmp", 0),
+                                pods.ctypes.data, len(pods), da.ctypes.data, dl.ctypes.data, len(da),
+                                ports.ctypes.data, len(ports))
+        n = int(len(out["dport"]))
+        s = None
+        if stream is not None:
+            s = stream.cuda_stream if hasattr(stream, "cuda_stream") else stream
+        self._check(_abi.lib().cls_gen_traffic_v16(
             self.h, C.byref(ts), first, n, _ptr(out.get("src")), _ptr(out.get("dst")),
             _ptr(out.get("sport")), _ptr(out.get("dport")), _ptr(out.get("proto")), s))
 

@@ -12,6 +12,11 @@ cache_impl.go:638-673) and rendered by renderACL (acl_renderer.go:312-402),
 so R = #distinct (pod, rule) + 2 allow-all + 1 ICMP.
 
 Config 2: 100 pods x 10 rules (~1k).  Config 3: 1000 pods x 10 rules (~10k).
+Config 5: the config 3 shape with mixed address families --
+every other app (so half the pods) IPv6, pods at fd00:10::/64 hosts,
+IPv6 apps' destination networks from fd00:20::/32 (/48-/64) -- destination
+port ranges in the ACL form (some named ports widened to [p, p+w], the same
+for every rule naming p), 10% ICMP, packets in the 16-byte layout.
 Traffic pools (pod IPs, rule destination prefixes, rule ports) feed the
 splitmix64 generator (DESIGN.md "Traffic").
 """
@@ -32,7 +37,10 @@ SEEDS = {2: 0xC0175EED02, 3: 0xC0175EED03, 4: 0xC0175EED04, 5: 0xC0175EED05}
 CONFIGS = {
     2: dict(n_pods=100, rules_per_pod=10, n_apps=10, packets=16 << 20),
     3: dict(n_pods=1000, rules_per_pod=10, n_apps=100, packets=256 << 20),
+    5: dict(n_pods=1000, rules_per_pod=10, n_apps=100, packets=256 << 20, mixed=True),
 }
+V6_PODS = 0xFD000010 << 96          # fd00:10::/64
+V6_SVC = 0xFD000020 << 96           # fd00:20::/32
 
 
 def pod_ip(k: int) -> int:
@@ -55,6 +63,39 @@ def service_cidrs(rng: random.Random, n: int = 256):
     return out
 
 
+def _mix64(z: int) -> int:
+    z = (z + 0x9E3779B97F4A7C15) & 0xFFFFFFFFFFFFFFFF
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & 0xFFFFFFFFFFFFFFFF
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & 0xFFFFFFFFFFFFFFFF
+    return z ^ (z >> 31)
+
+
+def pod_ip6(k: int) -> int:
+    """Pod k's IPv6 address: a host of fd00:10::/64."""
+    return V6_PODS | _mix64(k)
+
+
+def _v6(a: int) -> str:
+    import ipaddress
+    return str(ipaddress.IPv6Address(a))
+
+
+def service_cidrs6(rng: random.Random, n: int = 256):
+    out = []
+    for _ in range(n):
+        ln = rng.choice([48, 56, 60, 64, 64, 64])
+        a = (V6_SVC | (rng.getrandbits(32) << 64)) & ~((1 << (128 - ln)) - 1)
+        out.append("%s/%d" % (_v6(a), ln))
+    return out
+
+
+def port_range_of(p: int) -> tuple:
+    """Config 5: the dst port range a named port stands for in the ACL form."""
+    h = _mix64(p * 0x10001)
+    w = (0, 0, 0, 1, 7, 63, 1023)[h % 7]
+    return p, min(65535, p + w)
+
+
 def app_rules(rng: random.Random, cidrs, rules_per_pod: int):
     rules = []
     for _ in range(max(0, rules_per_pod - 2)):
@@ -68,17 +109,22 @@ def app_rules(rng: random.Random, cidrs, rules_per_pod: int):
     return rules
 
 
-def render_global(n_pods: int, rules_per_pod: int, n_apps: int, seed: int):
-    """Returns (acl: vpp_amd.model.Acl, traffic pools dict)."""
+def render_global(n_pods: int, rules_per_pod: int, n_apps: int, seed: int, mixed: bool = False):
+    """Returns (acl: vpp_amd.model.Acl, traffic pools dict).  mixed: config 5
+    (odd apps IPv6, port ranges; pools as 16-byte addresses)."""
     rng = random.Random(seed)
     cidrs = service_cidrs(rng)
-    apps = [app_rules(rng, cidrs, rules_per_pod) for _ in range(n_apps)]
+    cidrs6 = service_cidrs6(rng) if mixed else None
+    apps = [app_rules(rng, cidrs6 if mixed and a % 2 else cidrs, rules_per_pod) for a in range(n_apps)]
     pods = []
     for k in range(n_pods):
-        ip = gonet.one_host_subnet(_v4(pod_ip(k)))
+        v6 = mixed and (k % n_apps) % 2 == 1
+        ip = gonet.one_host_subnet(_v6(pod_ip6(k)) if v6 else _v4(pod_ip(k)))
         pods.append((ip, apps[k % n_apps]))
     table = build_global_table(pods)
     acl = render_acl(table, None)
+    if mixed:
+        return acl, _widen_and_pools(acl, table, pods)
     dst = sorted({(int.from_bytes(r.dest_network.ip[-4:], "big"), gonet.mask_size(r.dest_network.mask)[0])
                   for r in table.rules if len(r.dest_network.ip)})
     ports = sorted({r.dest_port for r in table.rules if r.dest_port})
@@ -89,10 +135,36 @@ def render_global(n_pods: int, rules_per_pod: int, n_apps: int, seed: int):
     return acl, pools
 
 
+def _widen_and_pools(acl, table, pods):
+    """Config 5: dst port ranges in the ACL form, and the 16-byte pools."""
+    for r in acl.rules:
+        ipr = r.matches.ip_rule if r.matches is not None else None
+        for sec in (ipr.tcp, ipr.udp) if ipr is not None else ():
+            if sec is not None and sec.destination_port_range is not None:
+                pr = sec.destination_port_range
+                if pr.lower_port == pr.upper_port and pr.lower_port != 0:
+                    pr.lower_port, pr.upper_port = port_range_of(pr.lower_port)
+
+    def b16(net) -> bytes:
+        ip = bytes(net.ip)
+        return ip if len(ip) == 16 else bytes(10) + b"\xff\xff" + ip
+
+    dst = sorted({(b16(r.dest_network), gonet.mask_size(r.dest_network.mask)[0] +
+                   (96 if len(r.dest_network.ip) == 4 else 0))
+                  for r in table.rules if len(r.dest_network.ip)})
+    ports = sorted({r.dest_port for r in table.rules if r.dest_port})
+    return dict(pod_ips=np.frombuffer(b"".join(b16(ip) for ip, _ in pods), np.uint8).reshape(-1, 16).copy(),
+                dst_addrs=np.frombuffer(b"".join(a for a, _ in dst), np.uint8).reshape(-1, 16).copy(),
+                dst_lens=np.array([ln for _, ln in dst], np.uint8),
+                ports=np.array(ports, np.uint16))
+
+
 def config(cfg: int):
-    """(acl, traffic spec dict, default packet count) of BASELINE config 2 or 3."""
+    """(acl, traffic spec dict, default packet count) of BASELINE config 2, 3
+    or 5 (config 5: 16-byte pools, spec["layout"] == 16)."""
     c = CONFIGS[cfg]
-    acl, pools = render_global(c["n_pods"], c["rules_per_pod"], c["n_apps"], seed=cfg)
-    spec = dict(seed=SEEDS[cfg], pct_pod_src=60, pct_rule_dst=50, pct_table_port=50, pct_icmp=0,
-                **pools)
+    mixed = c.get("mixed", False)
+    acl, pools = render_global(c["n_pods"], c["rules_per_pod"], c["n_apps"], seed=cfg, mixed=mixed)
+    spec = dict(seed=SEEDS[cfg], pct_pod_src=60, pct_rule_dst=50, pct_table_port=50,
+                pct_icmp=10 if mixed else 0, layout=16 if mixed else 4, **pools)
     return acl, spec, c["packets"]
