@@ -308,6 +308,20 @@ int cls_compile_v4(const cls_rule* rules, uint32_t n_rules, void* blob, uint64_t
 typedef struct cls_image_v16_header {
     cls_image_v4_header core;
     uint32_t fe_key[2], fe_val[2], fe_top[2], fe_n[2];
+    /* src_mode 1 (every source prefix a host route): the source side is two
+     * cuckoo hashes straight to class rows -- IPv4-mapped: {key, row} 8-B
+     * entries at h4 (2 x cap4), key = address bytes 12-15 as a little-endian
+     * word, h = key x mul4; IPv6: 16-B keys at k6 and u32 rows at r6 (2 x
+     * cap6 slots), h = (w0 x fold0 ^ w1 x fold1 ^ w2 x fold2 ^ w3) x mul6;
+     * table 0 slot = h >> (32 - L), table 1 slot = (h >> (32 - 2L)) & (cap - 1).
+     * The source interval table (keys, reps at src_search_val) is then not
+     * in the image but at blob offset off_src_search (the protocol > 2 path). */
+    uint32_t src_mode, h4, cap4, mul4, k6, r6, cap6, mul6, fold[3], dflt_row[2];
+    uint32_t off_src_search, src_search_val;
+    /* fe_k8[s]: side s's keys are 8 B, key8(start) - 1 with key8(x) = hi64 == 0 ?
+     * min(lo64, 2^48) : 2^48 + min(hi64, 2^64 - 1 - 2^48) (exact when every
+     * start has hi64 = 0 and lo64 <= 2^48, or lo64 = 0) */
+    uint32_t fe_k8[2];
 } cls_image_v16_header;
 int cls_compile_v16(const cls_rule* rules, uint32_t n_rules, void* blob, uint64_t cap,
                     uint64_t* need);

@@ -206,8 +206,9 @@ class Image:
                 break
         return res, rule
 
-    def classify(self, src, dst, dport, proto):
-        """Returns (verdict u8[n], counters u64[R+1])."""
+    def classify(self, src, dst, dport, proto, cls=None):
+        """Returns (verdict u8[n], counters u64[R+1]).  cls: the packets'
+        source classes when found by a front end (core mode 3)."""
         src = np.asarray(src, np.uint32)
         dst = np.asarray(dst, np.uint32)
         dport = np.asarray(dport, np.uint16)
@@ -218,7 +219,8 @@ class Image:
             res, rule = self.linear(src, dst, dport, proto)
             np.add.at(counters, rule, 1)
             return res.astype(np.uint8), counters
-        cls = self.source_class(src)
+        if cls is None:
+            cls = self.source_class(src)
         if self.h.list_mode >= 3:
             return self._classify_bv3(cls, src, dst, dport, proto, counters)
         if self.h.list_mode >= 1:
@@ -253,9 +255,10 @@ class Image:
 
 
 class Image16:
-    """The 16-byte layout (cls_compile_v16): the front end's binary search
-    over 128-bit interval starts (kernels.hip fe_rep) maps each address to its
-    32-bit representative, then the core image classifies the reps."""
+    """The 16-byte layout (cls_compile_v16): the front end maps each address to
+    its 32-bit representative (kernels.hip fe_rep: binary search over 128-bit
+    interval starts) or, src_mode 1, the source straight to its class row
+    (src_hash16: host-route cuckoo hashes); the core image classifies."""
 
     def __init__(self, blob: bytes):
         h = _abi.Image16Header.from_buffer_copy(blob)
@@ -263,19 +266,33 @@ class Image16:
         self.h = h
         self.core = Image(blob)
         img = blob[h.core.off_image:h.core.off_image + h.core.img_bytes]
-        self.keys, self.vals = [], []
+        self._img = img
+        self.keys, self.vals = [None, None], [None, None]
         for sd in range(2):
-            k = np.frombuffer(img, np.uint32, count=4 * h.fe_top[sd], offset=h.fe_key[sd]).reshape(-1, 4)
-            hi = (k[:, 1].astype(object) << 32) | k[:, 0].astype(object)
-            lo = (k[:, 3].astype(object) << 32) | k[:, 2].astype(object)
-            self.keys.append([int(a) << 64 | int(b) for a, b in zip(hi, lo)])
-            self.vals.append(np.frombuffer(img, np.uint32, count=h.fe_n[sd], offset=h.fe_val[sd]))
+            src = img
+            koff, voff = h.fe_key[sd], h.fe_val[sd]
+            if sd == 0 and h.src_mode == 1:           # source interval table in the trailer
+                src, koff = blob, h.off_src_search
+                voff = koff + h.src_search_val
+            if h.fe_k8[sd]:                            # 8-B keys over key8(address)
+                k = np.frombuffer(src, np.uint32, count=2 * h.fe_top[sd], offset=koff).reshape(-1, 2)
+                self.keys[sd] = [int(b) << 32 | int(a) for a, b in k]
+            else:
+                k = np.frombuffer(src, np.uint32, count=4 * h.fe_top[sd], offset=koff).reshape(-1, 4)
+                hi = (k[:, 1].astype(object) << 32) | k[:, 0].astype(object)
+                lo = (k[:, 3].astype(object) << 32) | k[:, 2].astype(object)
+                self.keys[sd] = [int(a) << 64 | int(b) for a, b in zip(hi, lo)]
+            self.vals[sd] = np.frombuffer(src, np.uint32, count=h.fe_n[sd], offset=voff)
 
     def rep(self, sd: int, addrs) -> np.ndarray:
         keys, vals, top = self.keys[sd], self.vals[sd], self.h.fe_top[sd]
         out = np.empty(len(addrs), np.uint32)
+        k8 = self.h.fe_k8[sd]
         for i, a in enumerate(addrs):
             x = int.from_bytes(bytes(a), "big")
+            if k8:
+                hi, lo = x >> 64, x & ((1 << 64) - 1)
+                x = min(lo, 1 << 48) if hi == 0 else (1 << 48) + min(hi, (1 << 64) - 1 - (1 << 48))
             pos, s = 0, top >> 1
             while s:
                 if keys[pos + s] < x:
@@ -284,7 +301,40 @@ class Image16:
             out[i] = vals[pos]
         return out
 
+    def src_rows(self, addrs) -> np.ndarray:
+        """src_mode 1: kernels.hip src_hash16."""
+        h = self.h
+        w = np.frombuffer(np.ascontiguousarray(addrs).tobytes(), "<u4").reshape(-1, 4).astype(np.uint64)
+        M = np.uint64(0xFFFFFFFF)
+        L4, L6 = h.cap4.bit_length() - 1, h.cap6.bit_length() - 1
+        t4 = np.frombuffer(self._img, np.uint32, count=4 * h.cap4, offset=h.h4).reshape(-1, 2)
+        x = w[:, 3]
+        g = (x * np.uint64(h.mul4)) & M
+        e0 = t4[(g >> np.uint64(32 - L4)).astype(np.int64)]
+        e1 = t4[h.cap4 + ((g >> np.uint64(32 - 2 * L4)) & np.uint64(h.cap4 - 1)).astype(np.int64)]
+        r4 = np.where(e0[:, 0] == x, e0[:, 1], np.where(e1[:, 0] == x, e1[:, 1], h.dflt_row[0]))
+        k6 = np.frombuffer(self._img, np.uint32, count=8 * h.cap6, offset=h.k6).reshape(-1, 4)
+        r6t = np.frombuffer(self._img, np.uint32, count=2 * h.cap6, offset=h.r6)
+        f = ((w[:, 0] * np.uint64(h.fold[0])) & M) ^ ((w[:, 1] * np.uint64(h.fold[1])) & M) ^ \
+            ((w[:, 2] * np.uint64(h.fold[2])) & M) ^ w[:, 3]
+        g = (f * np.uint64(h.mul6)) & M
+        p0 = (g >> np.uint64(32 - L6)).astype(np.int64)
+        p1 = h.cap6 + ((g >> np.uint64(32 - 2 * L6)) & np.uint64(h.cap6 - 1)).astype(np.int64)
+        m0 = (k6[p0] == w).all(1)
+        m1 = (k6[p1] == w).all(1)
+        r6 = np.where(m0, r6t[p0], np.where(m1, r6t[p1], h.dflt_row[1]))
+        is4 = (w[:, 0] == 0) & (w[:, 1] == 0) & (w[:, 2] == 0xFFFF0000)
+        return np.where(is4, r4, r6).astype(np.int64)
+
     def classify(self, src16, dst16, dport, proto):
         src16 = np.asarray(src16, np.uint8).reshape(-1, 16)
         dst16 = np.asarray(dst16, np.uint8).reshape(-1, 16)
-        return self.core.classify(self.rep(0, src16), self.rep(1, dst16), dport, proto)
+        srep = self.rep(0, src16)
+        drep = self.rep(1, dst16)
+        if self.h.src_mode == 1:
+            rows = self.src_rows(src16)
+            # the hashed row must be the class row of the rep (what the core's
+            # own source lookup would give), protocol > 2 takes the rep
+            cls = (rows - self.core.h.off_cells) // self.core.h.row_bytes
+            return self.core.classify(srep, drep, dport, proto, cls=cls)
+        return self.core.classify(srep, drep, dport, proto)

@@ -108,3 +108,50 @@ def test_oracle_fast_matches_faithful_v16():
     ov, oc = oracle.classify_faithful(cr, tr["src"], tr["dst"], tr["dport"], tr["proto"], af=16)
     np.testing.assert_array_equal(fv, ov)
     np.testing.assert_array_equal(fc, oc)
+
+
+def _host_src_acl(seed, n_rules=200):
+    """Rules whose sources are all host routes (/32 and, as twins, /128): the
+    rendered global table's shape -> the source hashes (src_mode 1)."""
+    import random
+    import vpp_amd.model as M
+    from aclgen import PrefixPool, _v4
+    rng = random.Random(seed)
+    pool = PrefixPool(rng, 24)
+    hosts = [rng.getrandbits(32) for _ in range(40)] + [a for a, _ in pool.v4[:8]]
+    rules = []
+    for _ in range(n_rules):
+        src = "%s/32" % _v4(rng.choice(hosts)) if rng.random() < 0.85 else ""
+        da, dl = rng.choice(pool.v4)
+        dst = "%s/%d" % (_v4(da), dl) if rng.random() < 0.7 else ""
+        p = rng.choice([22, 53, 80, 443, 0])
+        rules.append(M.l4_rule(rng.choice([M.DENY, M.PERMIT, M.REFLECT]), src, dst,
+                               rng.choice(["tcp", "udp"]), 0, 65535, p, p if p else 65535))
+    pool.v4 = [(h, 32) for h in hosts] + pool.v4
+    return rules, pool
+
+
+@pytest.mark.parametrize("seed", range(6))
+@pytest.mark.parametrize("forced_search", [False, True])
+def test_v16_source_host_hashes(seed, forced_search, monkeypatch):
+    if forced_search:
+        monkeypatch.setenv("CONTIVCLS_V16_SRC_SEARCH", "1")
+    rules, pool = _host_src_acl(seed)
+    rules, tr = mix_families(rules, random_traffic(seed, 4000, pool), seed)
+    img = _check16(rules, tr)
+    assert img.h.src_mode == (0 if forced_search else 1)
+
+
+def test_config5_table_cpu():
+    """The config 5 render (vpp_amd/workload.py) on a prefix of its 16-byte
+    stream, against the oracle's fast port."""
+    from vpp_amd import workload
+    acl, spec, _ = workload.config(5)
+    tr = oracle.gen_traffic_v16(spec, 0, 20000)
+    img = _img16(acl.rules)
+    assert img.h.src_mode == 1
+    v, c = img.classify(tr["src"], tr["dst"], tr["dport"], tr["proto"])
+    ov, oc = oracle.classify_fast(oracle.rules_to_c(acl.rules), tr["src"], tr["dst"], tr["dport"],
+                                  tr["proto"], af=16)
+    np.testing.assert_array_equal(v, ov)
+    np.testing.assert_array_equal(c, oc)

@@ -102,7 +102,10 @@ class ImageHeader(C.Structure):
 class Image16Header(C.Structure):
     """cls_image_v16_header: the core (rep-space) header, then the front end."""
     _fields_ = [("core", ImageHeader), ("fe_key", C.c_uint32 * 2), ("fe_val", C.c_uint32 * 2),
-                ("fe_top", C.c_uint32 * 2), ("fe_n", C.c_uint32 * 2)]
+                ("fe_top", C.c_uint32 * 2), ("fe_n", C.c_uint32 * 2)] + [
+        (n, C.c_uint32) for n in ("src_mode", "h4", "cap4", "mul4", "k6", "r6", "cap6", "mul6")] + [
+        ("fold", C.c_uint32 * 3), ("dflt_row", C.c_uint32 * 2), ("off_src_search", C.c_uint32),
+        ("src_search_val", C.c_uint32), ("fe_k8", C.c_uint32 * 2)]
 
 
 _lib = None

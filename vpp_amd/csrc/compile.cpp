@@ -2,6 +2,8 @@
 #include "compile.hpp"
 
 #include <algorithm>
+#include <array>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -488,6 +490,11 @@ std::vector<Sublist> port_sublists(const std::vector<TmplKey>& ents, const std::
 
 }  // namespace
 
+uint32_t Cls4Image::row_of(uint32_t addr) const {
+    const size_t k = size_t(std::upper_bound(h_bounds.begin(), h_bounds.end(), addr) - h_bounds.begin()) - 1;
+    return off_cells + uint32_t(h_iclass[k]) * row_bytes;
+}
+
 bool build_cls4(const std::vector<SemRule>& sem, uint32_t n_rules, Cls4Image& img,
                 std::string& why, const Cls4Opts* opt) {
     img = Cls4Image();
@@ -554,6 +561,8 @@ bool build_cls4(const std::vector<SemRule>& sem, uint32_t n_rules, Cls4Image& im
     }
     const uint32_t n_classes = uint32_t(class_pfx.size());
     const uint32_t n_real_bounds = uint32_t(bounds.size());
+    img.h_bounds = bounds;
+    img.h_iclass = iclass;
 
     // Hash LPM (tuple space): when the classed prefixes use few distinct lengths
     // (a rendered global table has only pod /32s), the class of an address is
@@ -571,7 +580,9 @@ bool build_cls4(const std::vector<SemRule>& sem, uint32_t n_rules, Cls4Image& im
         uint32_t dflt = 0;
         if (len0_class >= 0) dflt = uint32_t(len0_class);
         else if (class_of_pfx[0] >= 0) dflt = uint32_t(class_of_pfx[0]);
-        if (keys.size() <= kMaxHashLens) {
+        if (opt && opt->ext_src) {
+            img.mode = 3;                            // the caller maps addresses to rows
+        } else if (keys.size() <= kMaxHashLens) {
             img.mode = 1;
             img.default_class = dflt;
             for (const auto& kv : keys) {
@@ -1054,8 +1065,10 @@ bool build_cls4(const std::vector<SemRule>& sem, uint32_t n_rules, Cls4Image& im
         img.off_hot = img.img_bytes + ((img.n_ctr * 4 + 15u) & ~15u);
         img.lds_bytes = img.off_hot + img.n_hot * 64u * 4u;
     };
+    const bool dbg = std::getenv("CONTIVCLS_DEBUG_MODES") != nullptr;   // diagnostics
     for (;;) {
         serialise(lmode);
+        if (dbg) std::fprintf(stderr, "list mode %u: lds %u img %u ctr %u\n", lmode, img.lds_bytes, img.img_bytes, img.n_ctr);
         if (lmode == 0) break;
         // block offset field: 16 bits in 8-B units (modes 1, 2); mode 3: the
         // pointer tables in the first 64 KiB, sublist slots below 2^16
@@ -1180,6 +1193,50 @@ void put_be32(uint8_t* a, uint32_t v) {
     a[0] = uint8_t(v >> 24); a[1] = uint8_t(v >> 16); a[2] = uint8_t(v >> 8); a[3] = uint8_t(v);
 }
 
+// 8-byte search keys (compile.hpp key8): exact for interval starts with hi64 0
+// and lo64 <= 2^48 (the v4-mapped block and below), or lo64 0 (IPv6 prefixes
+// up to /64)
+constexpr uint64_t kK8Lo = 1ull << 48, kK8HiMax = ~0ull - kK8Lo;
+bool has_key8(u128 b) {
+    const uint64_t h = uint64_t(b >> 64), l = uint64_t(b);
+    return h == 0 ? l <= kK8Lo : (l == 0 && h <= kK8HiMax);
+}
+uint64_t key8(u128 x) {
+    const uint64_t h = uint64_t(x >> 64), l = uint64_t(x);
+    return h == 0 ? std::min(l, kK8Lo) : kK8Lo + std::min(h, kK8HiMax);
+}
+
+// an address's 16 network-order bytes as the kernel loads them (4 little-endian words)
+std::array<uint32_t, 4> raw_words(u128 a) {
+    std::array<uint32_t, 4> w{};
+    for (int i = 0; i < 16; ++i) w[i / 4] |= uint32_t(uint8_t(a >> (120 - 8 * i))) << (8 * (i % 4));
+    return w;
+}
+
+// Two-table cuckoo hash of 16-byte keys (Cls16Image, IPv6 host routes):
+// slot_key[s] = key index in slot s, or -1; empty slots are then given keys
+// that never probe them (fill6).
+uint32_t h6_slot(const std::array<uint32_t, 4>& k, uint32_t cap, uint32_t mul, const uint32_t* f, int side) {
+    const uint32_t L = uint32_t(__builtin_ctz(cap));
+    const uint32_t h = fold6(k[0], k[1], k[2], k[3], f) * mul;
+    return side == 0 ? h >> (32u - L) : cap + ((h >> (32u - 2u * L)) & (cap - 1u));
+}
+
+bool cuckoo6(const std::vector<std::array<uint32_t, 4>>& keys, uint32_t cap, uint32_t mul, const uint32_t* f,
+             std::vector<int>& slot_key) {
+    slot_key.assign(size_t(cap) * 2, -1);
+    for (int i = 0; i < int(keys.size()); ++i) {
+        int cur = i, side = 0;
+        for (int kick = 0; kick < 256 && cur >= 0; ++kick) {
+            const uint32_t pos = h6_slot(keys[size_t(cur)], cap, mul, f, side);
+            std::swap(cur, slot_key[pos]);
+            side ^= 1;
+        }
+        if (cur >= 0) return false;
+    }
+    return true;
+}
+
 }  // namespace
 
 bool build_cls16(const std::vector<SemRule>& sem, uint32_t n_rules, Cls16Image& img, std::string& why) {
@@ -1209,35 +1266,142 @@ bool build_cls16(const std::vector<SemRule>& sem, uint32_t n_rules, Cls16Image& 
         }
         img.sem.push_back(r);
     }
-    // front-end tables (image tail): per side, keys then reps
-    Cls4Opts opt;
-    uint32_t rel_key[2], rel_val[2];
-    for (int sd = 0; sd < 2; ++sd) {
+    // Source front end: host-route hashes when every source prefix is a host
+    // route (CONTIVCLS_V16_SRC_SEARCH=1 forces the interval search: tests)
+    bool hosts = true;
+    for (int f = 0; f < 2; ++f)
+        for (const auto& r : side[0].pf[f]) hosts = hosts && r.lo == r.hi;
+    if (const char* e = std::getenv("CONTIVCLS_V16_SRC_SEARCH")) hosts = hosts && std::atoi(e) == 0;
+    img.src_mode = hosts ? 1u : 0u;
+
+    // interval tables: per side, keys (start - 1 as u64 hi, lo; padding all
+    // ones) then reps
+    auto search_table = [&](int sd, std::vector<uint32_t>& out, uint32_t& top, uint32_t& nval, uint32_t& rel_val,
+                            uint32_t& k8) {
         std::vector<u128> start;
         std::vector<uint32_t> rep;
         side[sd].intervals(start, rep);
         uint32_t K = 1;
         while (K < start.size()) K *= 2;
-        img.fe_top[sd] = K;
-        img.fe_n[sd] = uint32_t(rep.size());
-        rel_key[sd] = uint32_t(opt.tail.size()) * 4;
+        top = K;
+        nval = uint32_t(rep.size());
+        // 8-B keys (key8, compile.hpp) when every interval start has a key8
+        k8 = 1;
+        for (size_t k = 1; k < start.size(); ++k) k8 &= has_key8(start[k]) ? 1u : 0u;
         for (uint32_t k = 0; k < K; ++k) {
+            if (k8) {
+                const uint64_t key = (k >= 1 && k < start.size()) ? key8(start[k]) - 1 : ~0ull;
+                out.push_back(uint32_t(key));
+                out.push_back(uint32_t(key >> 32));
+                continue;
+            }
             const u128 key = (k >= 1 && k < start.size()) ? start[k] - 1 : kAll;
             const uint64_t h = uint64_t(key >> 64), l = uint64_t(key);
-            opt.tail.push_back(uint32_t(h));
-            opt.tail.push_back(uint32_t(h >> 32));
-            opt.tail.push_back(uint32_t(l));
-            opt.tail.push_back(uint32_t(l >> 32));
+            out.push_back(uint32_t(h));
+            out.push_back(uint32_t(h >> 32));
+            out.push_back(uint32_t(l));
+            out.push_back(uint32_t(l >> 32));
         }
-        rel_val[sd] = uint32_t(opt.tail.size()) * 4;
-        opt.tail.insert(opt.tail.end(), rep.begin(), rep.end());
+        out.resize(align4(uint32_t(out.size())));
+        rel_val = uint32_t(out.size()) * 4;
+        out.insert(out.end(), rep.begin(), rep.end());
+        out.resize(align4(uint32_t(out.size())));
+    };
+    Cls4Opts opt;
+    opt.ext_src = hosts;
+    uint32_t rel_key[2] = {}, rel_val[2] = {};
+    for (int sd = hosts ? 1 : 0; sd < 2; ++sd) {
+        rel_key[sd] = uint32_t(opt.tail.size()) * 4;
+        search_table(sd, opt.tail, img.fe_top[sd], img.fe_n[sd], rel_val[sd], img.fe_k8[sd]);
+    }
+    // host-route hashes; their values (rows) are patched in once the core is laid out
+    std::vector<uint32_t> pfx4, pfx6;                     // prefix index per hashed key
+    std::vector<uint64_t> tab4;
+    std::vector<int> slot6;
+    uint32_t rel_h4 = 0, rel_k6 = 0, rel_r6 = 0;
+    if (hosts) {
+        img.src_search.clear();
+        uint32_t top0, n0, rv0;
+        search_table(0, img.src_search, top0, n0, rv0, img.fe_k8[0]);
+        img.fe_top[0] = top0;
+        img.fe_n[0] = n0;
+        img.src_search_val = rv0;
+        // IPv4-mapped: key = last 4 address bytes as a little-endian word
+        std::vector<std::pair<uint32_t, uint32_t>> k4;
+        for (uint32_t i = 0; i < side[0].pf[0].size(); ++i)
+            k4.push_back({raw_words(side[0].pf[0][i].lo)[3], i});
+        uint32_t cap = 16;
+        while (cap < k4.size()) cap *= 2;
+        for (bool ok = false; !ok;) {
+            for (uint32_t m : kHashMuls)
+                if (cuckoo_build(k4, cap, m, tab4)) { ok = true; img.mul4 = m; break; }
+            if (!ok) cap *= 2;
+            if (cap > (1u << 16)) { why = "IPv4 host-route hash failed"; return false; }
+        }
+        img.cap4 = cap;
+        rel_h4 = uint32_t(opt.tail.size()) * 4;
+        for (uint64_t e : tab4) {
+            opt.tail.push_back(uint32_t(e));
+            opt.tail.push_back(0u);
+        }
+        opt.tail.resize(align4(uint32_t(opt.tail.size())));
+        // IPv6: full 16-byte keys
+        std::vector<std::array<uint32_t, 4>> k6;
+        for (const auto& r : side[0].pf[1]) k6.push_back(raw_words(r.lo));
+        cap = 16;
+        while (cap < k6.size()) cap *= 2;
+        uint64_t z = 0x3C6EF372FE94F82Bull;               // splitmix64 stream of odd fold multipliers
+        auto next = [&z]() {
+            z += 0x9E3779B97F4A7C15ull;
+            uint64_t m = z;
+            m = (m ^ (m >> 30)) * 0xBF58476D1CE4E5B9ull;
+            m = (m ^ (m >> 27)) * 0x94D049BB133111EBull;
+            return uint32_t(m ^ (m >> 31)) | 1u;
+        };
+        for (bool ok = false; !ok;) {
+            for (int tries = 0; tries < 16 && !ok; ++tries) {
+                for (auto& f : img.fold) f = next();
+                img.mul6 = next();
+                ok = cuckoo6(k6, cap, img.mul6, img.fold, slot6);
+            }
+            if (!ok) cap *= 2;
+            if (cap > (1u << 16)) { why = "IPv6 host-route hash failed"; return false; }
+        }
+        img.cap6 = cap;
+        rel_k6 = uint32_t(opt.tail.size()) * 4;
+        for (uint32_t pos = 0; pos < 2 * cap; ++pos) {
+            std::array<uint32_t, 4> w{};
+            if (slot6[pos] >= 0) {
+                w = k6[size_t(slot6[pos])];
+            } else {                                      // a key that never probes this slot
+                const int sdx = pos >= cap ? 1 : 0;
+                for (uint32_t c = 0; h6_slot(w = {0u, 0u, 0u, c}, cap, img.mul6, img.fold, sdx) == pos; ++c) {}
+            }
+            opt.tail.insert(opt.tail.end(), w.begin(), w.end());
+        }
+        rel_r6 = uint32_t(opt.tail.size()) * 4;
+        opt.tail.resize(opt.tail.size() + 2 * size_t(cap), 0u);
         opt.tail.resize(align4(uint32_t(opt.tail.size())));
     }
     opt.hot_addr = side[0].root[0];                       // IPv4 sources matching no prefix
     if (!build_cls4(img.sem, n_rules, img.core, why, &opt)) return false;
-    for (int sd = 0; sd < 2; ++sd) {
-        img.fe_key[sd] = img.core.off_tail + rel_key[sd];
-        img.fe_val[sd] = img.core.off_tail + rel_val[sd];
+    const uint32_t tail = img.core.off_tail;
+    for (int sd = hosts ? 1 : 0; sd < 2; ++sd) {
+        img.fe_key[sd] = tail + rel_key[sd];
+        img.fe_val[sd] = tail + rel_val[sd];
+    }
+    if (hosts) {
+        Cls4Image& c = img.core;
+        img.h4 = tail + rel_h4;
+        img.k6 = tail + rel_k6;
+        img.r6 = tail + rel_r6;
+        for (int f = 0; f < 2; ++f) img.dflt_row[f] = c.row_of(side[0].root[f]);
+        // (an empty slot's filler key never probes it: its row is never read)
+        if (!side[0].pf[0].empty())
+            for (size_t pos = 0; pos < tab4.size(); ++pos)
+                c.words[(img.h4 + 8 * pos) / 4 + 1] = c.row_of(side[0].base[0][uint32_t(tab4[pos] >> 32)]);
+        for (size_t pos = 0; pos < slot6.size(); ++pos)
+            if (slot6[pos] >= 0) c.words[img.r6 / 4 + pos] = c.row_of(side[0].base[1][size_t(slot6[pos])]);
     }
     return true;
 }

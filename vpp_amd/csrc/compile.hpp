@@ -141,11 +141,16 @@ struct Cls4Image {
     uint32_t n_hot = 1;
     uint32_t off_hot = 0;
     uint32_t off_tail = 0;         // Cls4Opts::tail words (read-only, after the sections above)
+    // host only: the elementary source intervals and their classes
+    std::vector<uint32_t> h_bounds;
+    std::vector<uint16_t> h_iclass;
+    uint32_t row_of(uint32_t addr) const;   // byte address of the class row of `addr`
 };
 
 struct Cls4Opts {
     std::vector<uint32_t> tail;    // extra read-only words appended to the image
     int64_t hot_addr = -1;         // the hot class is this address's (default: the widest)
+    bool ext_src = false;          // no source lookup sections (mode 3: the caller finds rows)
 };
 
 // Build the image; returns false (with reason) if the table does not fit the
@@ -173,12 +178,36 @@ bool build_cls4(const std::vector<SemRule>& sem, uint32_t n_rules, Cls4Image& im
 //     block iff the address lies in the prefix.
 // Front-end tables per side s (0 src, 1 dst), in the image's tail: fe_top[s]
 // keys of 16 B (interval start - 1 as u64 hi, u64 lo; padding all-ones),
-// then fe_n[s] u32 reps.
+// then fe_n[s] u32 reps.  When every interval start b has hi64(b) = 0 and
+// lo64(b) <= 2^48, or lo64(b) = 0 (IPv4 and IPv6 prefixes up to /64), the
+// keys are 8 B: key8(x) = hi64 == 0 ? min(lo64, 2^48) : 2^48 + min(hi64,
+// 2^64 - 1 - 2^48), monotone and exact against such starts.
+//
+// Source front end, src_mode 1 (every source prefix a host route -- rendered
+// global tables: pod /32s and /128s): exact cuckoo hashes straight to the
+// class row (core mode 3, no rep on the hot path).  IPv4-mapped addresses:
+// key = the address's last 4 bytes as loaded (little-endian word), entries
+// {key, row} 8 B, h = key x mul4 (lpm_h0 / lpm_h1).  IPv6: keys are the 16
+// bytes as loaded (k6: 16 B per slot), rows at r6 (u32 per slot); f = w0 x
+// fold[0] ^ w1 x fold[1] ^ w2 x fold[2] ^ w3, h = f x mul6.  Misses take the
+// family's default row.  The source interval table (src_mode 0's) stays in
+// global memory for the protocol > 2 fallback, which needs the rep.
 struct Cls16Image {
     Cls4Image core;                // classifier over the rules in rep space
     std::vector<SemRule> sem;      // the rules in rep space (linear fallback)
     uint32_t fe_key[2] = {}, fe_val[2] = {}, fe_top[2] = {}, fe_n[2] = {};
+    uint32_t fe_k8[2] = {};        // 8-B keys: key8(start) - 1 (see key8)
+    uint32_t src_mode = 0;         // 0: interval search -> rep; 1: host-route hashes -> row
+    uint32_t h4 = 0, cap4 = 0, mul4 = 0;
+    uint32_t k6 = 0, r6 = 0, cap6 = 0, mul6 = 0, fold[3] = {};
+    uint32_t dflt_row[2] = {};     // per family (0 IPv4, 1 IPv6)
+    std::vector<uint32_t> src_search;  // src_mode 1: the source interval table (keys, reps)
+    uint32_t src_search_val = 0;   // byte offset of its reps
 };
+__host__ __device__ inline uint32_t fold6(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3,
+                                          const uint32_t* f) {
+    return (w0 * f[0]) ^ (w1 * f[1]) ^ (w2 * f[2]) ^ w3;
+}
 // sem: semantic_rules(..., fam 0, ...) -- a packet's src and dst may be of
 // different families (Contains tests each address on its own).
 bool build_cls16(const std::vector<SemRule>& sem, uint32_t n_rules, Cls16Image& img, std::string& why);

@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <cstdarg>
+#include <cstddef>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -63,6 +64,7 @@ struct Table {
         Cls16Image img;
         std::vector<LinRule4> lin; // rules in rep space (protocol > 2, FORCE_LINEAR)
         DevBuf d_img, d_lin, d_slot, d_map, d_part;
+        DevBuf d_src_search;       // src_mode 1: the source interval table (global memory)
         uint32_t n_slots = 0;
         bool lds_resident = false;
     } p16;
@@ -222,6 +224,11 @@ static int table_put_locked(cls_engine* e, const char* name, const cls_rule* rul
             HIPC(e, q.d_slot.ensure(size_t(q.n_slots) * 8));
             HIPC(e, q.d_map.ensure(size_t(q.n_slots) * 4));
             HIPC(e, hipMemcpy(q.d_map.p, m16.data(), m16.size() * 4, hipMemcpyHostToDevice));
+            if (q.img.src_mode == 1) {
+                HIPC(e, q.d_src_search.ensure(q.img.src_search.size() * 4));
+                HIPC(e, hipMemcpy(q.d_src_search.p, q.img.src_search.data(), q.img.src_search.size() * 4,
+                                  hipMemcpyHostToDevice));
+            }
         }
     }
     const uint32_t id = e->next_table++;
@@ -373,6 +380,31 @@ static int finish_counts(cls_engine* e, Table& t, DevBuf& d_slot, DevBuf& d_map,
     return CLS_OK;
 }
 
+static Fe16 fe16(const Cls16Image& m, const DevBuf& d_src_search) {
+    Fe16 fe;
+    std::memset(&fe, 0, sizeof fe);
+    for (int sd = 0; sd < 2; ++sd) {
+        fe.key[sd] = m.fe_key[sd];
+        fe.val[sd] = m.fe_val[sd];
+        fe.top[sd] = m.fe_top[sd];
+        fe.k8[sd] = m.fe_k8[sd];
+    }
+    fe.src_mode = m.src_mode;
+    if (m.src_mode == 1) {
+        const uint32_t L4 = uint32_t(__builtin_ctz(m.cap4)), L6 = uint32_t(__builtin_ctz(m.cap6));
+        fe.h4 = m.h4; fe.cap4 = m.cap4; fe.mul4 = m.mul4;
+        fe.s4_0 = 32u - L4; fe.s4_1 = 32u - 2u * L4; fe.L4 = L4;
+        fe.k6 = m.k6; fe.r6 = m.r6; fe.cap6 = m.cap6; fe.mul6 = m.mul6;
+        fe.s6_0 = 32u - L6; fe.s6_1 = 32u - 2u * L6; fe.L6 = L6;
+        for (int i = 0; i < 3; ++i) fe.fold[i] = m.fold[i];
+        fe.dflt4 = m.dflt_row[0];
+        fe.dflt6 = m.dflt_row[1];
+        fe.gsrc = d_src_search.as<uint8_t>();
+        fe.gval = m.src_search_val;
+    }
+    return fe;
+}
+
 // cls_classify of a 16-byte batch (CLS_AF_V16): front end to reps, then the
 // classifier over the rep-space rules (compile.hpp Cls16Image).
 static int classify16_locked(cls_engine* e, std::shared_ptr<Table> t, const cls_pkt_soa* pk, uint64_t n,
@@ -427,12 +459,7 @@ static int classify16_locked(cls_engine* e, std::shared_ptr<Table> t, const cls_
             HIPC(e, q.d_part.ensure(size_t(cfg.grid) * c.n_ctr * 4));
             cd.part = q.d_part.as<uint32_t>();
         }
-        Fe16 fe;
-        for (int sd = 0; sd < 2; ++sd) {
-            fe.key[sd] = q.img.fe_key[sd];
-            fe.val[sd] = q.img.fe_val[sd];
-            fe.top[sd] = q.img.fe_top[sd];
-        }
+        Fe16 fe = fe16(q.img, q.d_src_search);
         for (uint64_t off = 0; off < n; off += kClsChunk) {
             const uint64_t m = std::min<uint64_t>(kClsChunk, n - off);
             Pkts16 pc{reinterpret_cast<const uint4*>(src + 16 * off), reinterpret_cast<const uint4*>(dst + 16 * off),
@@ -765,7 +792,8 @@ int cls_gen_traffic_v4(cls_engine* e, const cls_traffic_spec* sp, uint64_t first
 // Blob of cls_compile_v4 / cls_compile_v16: header (v4 header, then `extra`
 // bytes of a larger header), image, slot -> rule map, linear rules.
 static int write_blob(const Cls4Image* img, const std::vector<LinRule4>& lin, uint32_t n, uint32_t magic,
-                      const void* extra, size_t extra_bytes, void* blob, uint64_t cap, uint64_t* need) {
+                      const void* extra, size_t extra_bytes, void* blob, uint64_t cap, uint64_t* need,
+                      const std::vector<uint32_t>* trailer = nullptr, size_t trailer_field = 0) {
     cls_image_v4_header h;
     std::memset(&h, 0, sizeof h);
     h.magic = magic;
@@ -810,12 +838,18 @@ static int write_blob(const Cls4Image* img, const std::vector<LinRule4>& lin, ui
     h.off_ctr_rule = uint32_t(al(h.off_image + h.img_bytes));
     h.off_lin = uint32_t(al(h.off_ctr_rule + uint64_t(h.n_ctr) * 4));
     h.total_bytes = uint32_t(h.off_lin + lin.size() * sizeof(LinRule4));
+    const uint32_t off_trailer = uint32_t(al(h.total_bytes));
+    if (trailer) h.total_bytes = off_trailer + uint32_t(trailer->size() * 4);
     *need = h.total_bytes;
     if (!blob || cap < h.total_bytes) return CLS_OK;
     uint8_t* b = static_cast<uint8_t*>(blob);
     std::memset(b, 0, h.total_bytes);
     std::memcpy(b, &h, sizeof h);
     if (extra_bytes) std::memcpy(b + sizeof h, extra, extra_bytes);
+    if (trailer) {
+        std::memcpy(b + sizeof h + trailer_field, &off_trailer, 4);   // extra header field: trailer offset
+        std::memcpy(b + off_trailer, trailer->data(), trailer->size() * 4);
+    }
     if (img) {
         std::memcpy(b + h.off_image, img->words.data(), img->img_bytes);
         std::memcpy(b + h.off_ctr_rule, img->ctr_rule.data(), size_t(h.n_ctr) * 4);
@@ -890,10 +924,19 @@ int cls_compile_v16(const cls_rule* rules, uint32_t n, void* blob, uint64_t cap,
         h16.fe_val[sd] = img.fe_val[sd];
         h16.fe_top[sd] = img.fe_top[sd];
         h16.fe_n[sd] = img.fe_n[sd];
+        h16.fe_k8[sd] = img.fe_k8[sd];
     }
+    h16.src_mode = img.src_mode;
+    h16.h4 = img.h4; h16.cap4 = img.cap4; h16.mul4 = img.mul4;
+    h16.k6 = img.k6; h16.r6 = img.r6; h16.cap6 = img.cap6; h16.mul6 = img.mul6;
+    for (int i = 0; i < 3; ++i) h16.fold[i] = img.fold[i];
+    h16.dflt_row[0] = img.dflt_row[0];
+    h16.dflt_row[1] = img.dflt_row[1];
+    h16.src_search_val = img.src_search_val;
     const size_t extra = sizeof h16 - sizeof h16.core;
     return write_blob(&img.core, linear4(img.sem), n, 0x434C3136u, reinterpret_cast<const uint8_t*>(&h16) + sizeof h16.core,
-                      extra, blob, cap, need);
+                      extra, blob, cap, need, img.src_mode == 1 ? &img.src_search : nullptr,
+                      offsetof(cls_image_v16_header, off_src_search) - sizeof h16.core);
 }
 
 }  // extern "C"

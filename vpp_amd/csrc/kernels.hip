@@ -149,7 +149,11 @@ __device__ __forceinline__ void sub_step(const Img<kLds>& im, const uint32_t (&d
 template <int N, bool kLds, int kMode>
 __device__ __forceinline__ void src_row(const Img<kLds>& im, const Cls4Dev& t,
                                         const uint32_t (&src)[N], uint32_t (&row)[N]) {
-    if constexpr (kMode >= 1) {
+    if constexpr (kMode == 3) {
+        // the caller found the rows (16-byte path, host-route hashes)
+#pragma unroll
+        for (int q = 0; q < N; ++q) row[q] = src[q];
+    } else if constexpr (kMode >= 1) {
         // Hash LPM: one cuckoo probe pair per prefix length, lengths ascending
         // so the longest hit wins.  Entries {key, row}; empty slots hold keys
         // that never probe them, so a key compare is the whole hit test.  The
@@ -398,7 +402,7 @@ __device__ __forceinline__ void run_n(const Img<kLds>& im, const Cls4Dev& t, uin
                                       unsigned long long* gslot, uint32_t& hot0,
                                       const uint32_t (&s)[N], const uint32_t (&d)[N],
                                       const uint32_t (&dp)[N], const uint32_t (&pr)[N],
-                                      bool pr_any, uint32_t (&res)[N]) {
+                                      bool pr_any, uint32_t (&res)[N], const uint32_t (&sl)[N]) {
     uint32_t slot[N];
     classify_n<N, kLds, kMode, kList, kD>(im, t, s, d, dp, pr, res, slot);
     // One LDS atomic per packet, no branch.  Hot slots (< n_hot: default DENY
@@ -429,7 +433,7 @@ __device__ __forceinline__ void run_n(const Img<kLds>& im, const Cls4Dev& t, uin
                     __hip_atomic_fetch_add(lctr_t(addr[q]), ~0u, __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_WORKGROUP);
                 uint32_t rule;
-                linear_one(t.lin, t.n_lin, t.n_rules, s[q], d[q], dp[q], 3u, res[q], rule);
+                linear_one(t.lin, t.n_lin, t.n_rules, sl[q], d[q], dp[q], 3u, res[q], rule);
                 atomicAdd(&gslot[t.n_ctr + rule], 1ull);
             }
         }
@@ -529,7 +533,7 @@ __global__ __launch_bounds__(kClsBlock) void classify4_cls(Cls4Dev t, Pkts4 p, u
                 other |= ((pr | ((pr & 0x7F7F7F7Fu) + 0x7D7D7D7Du)) & 0x80808080u) != 0u;
             }
             uint32_t v[kN];
-            run_n<kN, kLds, kMode, kList, kD>(im, t, hot_lane, gslot, hot0, sa, da, pa, ra, other, v);
+            run_n<kN, kLds, kMode, kList, kD>(im, t, hot_lane, gslot, hot0, sa, da, pa, ra, other, v, sa);
             if (verdict) {
 #pragma unroll
                 for (int k = 0; k < kG; ++k)
@@ -576,7 +580,7 @@ __global__ __launch_bounds__(kClsBlock) void classify4_cls(Cls4Dev t, Pkts4 p, u
             const uint32_t ra[4] = {pr & 0xFFu, (pr >> 8) & 0xFFu, (pr >> 16) & 0xFFu, pr >> 24};
             uint32_t v[4];
             run_n<4, kLds, kMode, kList, -1>(im, t, hot_lane, gslot, hot0, sa, da, pa, ra,
-                                             ((pr | ((pr & 0x7F7F7F7Fu) + 0x7D7D7D7Du)) & 0x80808080u) != 0u, v);
+                                             ((pr | ((pr & 0x7F7F7F7Fu) + 0x7D7D7D7Du)) & 0x80808080u) != 0u, v, sa);
             if (verdict)
                 stnt(v[0] | (v[1] << 8) | (v[2] << 16) | (v[3] << 24),
                      const_cast<uint32_t*>(at(reinterpret_cast<const uint32_t*>(verdict), gi)));
@@ -586,7 +590,7 @@ __global__ __launch_bounds__(kClsBlock) void classify4_cls(Cls4Dev t, Pkts4 p, u
     for (uint32_t i = tail_from + tid; i < uint32_t(p.n); i += nthreads) {
         const uint32_t sa[1] = {p.src[i]}, da[1] = {p.dst[i]}, pa[1] = {p.dport[i]}, ra[1] = {p.proto[i]};
         uint32_t v[1];
-        run_n<1, kLds, kMode, kList, -1>(im, t, hot_lane, gslot, hot0, sa, da, pa, ra, ra[0] > 2u, v);
+        run_n<1, kLds, kMode, kList, -1>(im, t, hot_lane, gslot, hot0, sa, da, pa, ra, ra[0] > 2u, v, sa);
         if (verdict) verdict[i] = uint8_t(v[0]);
     }
 
@@ -611,13 +615,32 @@ __device__ __forceinline__ void addr128(const uint4& a, uint64_t& hi, uint64_t& 
 
 template <int N, bool kLds>
 __device__ __forceinline__ void fe_rep(const Img<kLds>& im, uint32_t off_key, uint32_t off_val,
-                                       uint32_t top, const uint4 (&a)[N], uint32_t (&rep)[N]) {
+                                       uint32_t top, uint32_t k8, const uint4 (&a)[N], uint32_t (&rep)[N]) {
     uint64_t kh[N], kl[N];
     uint32_t pos[N];
 #pragma unroll
     for (int q = 0; q < N; ++q) {
         addr128(a[q], kh[q], kl[q]);
         pos[q] = off_key;
+    }
+    if (k8) {
+        // 8-B keys (compile.hpp key8): half the LDS bytes and one 64-bit compare per step
+        constexpr uint64_t kLo = 1ull << 48, kHiMax = ~0ull - kLo;
+        uint64_t k[N];
+#pragma unroll
+        for (int q = 0; q < N; ++q) k[q] = kh[q] == 0 ? min(kl[q], kLo) : kLo + min(kh[q], kHiMax);
+#pragma unroll 1
+        for (uint32_t s = top >> 1; s; s >>= 1) {
+            const uint32_t step = 8u * s;
+            uint2 e[N];
+#pragma unroll
+            for (int q = 0; q < N; ++q) e[q] = im.u64(pos[q] + step);
+#pragma unroll
+            for (int q = 0; q < N; ++q) pos[q] = ((uint64_t(e[q].y) << 32) | e[q].x) < k[q] ? pos[q] + step : pos[q];
+        }
+#pragma unroll
+        for (int q = 0; q < N; ++q) rep[q] = im.u32(off_val + ((pos[q] - off_key) >> 1));
+        return;
     }
 #pragma unroll 1
     for (uint32_t s = top >> 1; s; s >>= 1) {
@@ -650,7 +673,42 @@ __device__ __forceinline__ void lin_n(const Cls4Dev& t, unsigned long long* gslo
     }
 }
 
-template <bool kLds, int kMode, int kList, int kD, bool kLin>
+// Source rows of N 16-byte addresses from the host-route hashes (src_mode 1):
+// both families' probes for every lane (a wave holds both), the family
+// picked per lane.  IPv4-mapped = bytes 0-9 zero, bytes 10-11 0xFF (Go To4).
+template <int N, bool kLds>
+__device__ __forceinline__ void src_hash16(const Img<kLds>& im, const Fe16& fe, const uint4 (&a)[N],
+                                           uint32_t (&row)[N]) {
+    uint2 e0[N], e1[N];
+    uint4 c0[N], c1[N];
+    uint32_t v0[N], v1[N];
+#pragma unroll
+    for (int q = 0; q < N; ++q) {
+        const uint32_t h = a[q].w * fe.mul4;
+        e0[q] = im.u64(fe.h4 + 8u * (h >> fe.s4_0));
+        e1[q] = im.u64(fe.h4 + 8u * fe.cap4 + 8u * __builtin_amdgcn_ubfe(h, fe.s4_1, fe.L4));
+        const uint32_t g = fold6(a[q].x, a[q].y, a[q].z, a[q].w, fe.fold) * fe.mul6;
+        const uint32_t p0 = g >> fe.s6_0, p1 = fe.cap6 + __builtin_amdgcn_ubfe(g, fe.s6_1, fe.L6);
+        c0[q] = im.u128(fe.k6 + 16u * p0);
+        c1[q] = im.u128(fe.k6 + 16u * p1);
+        v0[q] = im.u32(fe.r6 + 4u * p0);
+        v1[q] = im.u32(fe.r6 + 4u * p1);
+    }
+#pragma unroll
+    for (int q = 0; q < N; ++q) {
+        const uint4 x = a[q];
+        const bool is4 = (x.x | x.y) == 0u && x.z == 0xFFFF0000u;
+        uint32_t r4 = e1[q].x == x.w ? e1[q].y : fe.dflt4;
+        r4 = e0[q].x == x.w ? e0[q].y : r4;
+        const bool m1 = c1[q].x == x.x && c1[q].y == x.y && c1[q].z == x.z && c1[q].w == x.w;
+        const bool m0 = c0[q].x == x.x && c0[q].y == x.y && c0[q].z == x.z && c0[q].w == x.w;
+        uint32_t r6 = m1 ? v1[q] : fe.dflt6;
+        r6 = m0 ? v0[q] : r6;
+        row[q] = is4 ? r4 : r6;
+    }
+}
+
+template <bool kLds, int kMode, int kList, int kD, bool kLin, int kFe>
 __global__ __launch_bounds__(kClsBlock) void classify16_cls(Cls4Dev t, Fe16 fe, Pkts16 p, uint8_t* verdict,
                                                             unsigned long long* gslot) {
     extern __shared__ uint4 smem[];
@@ -660,9 +718,29 @@ __global__ __launch_bounds__(kClsBlock) void classify16_cls(Cls4Dev t, Fe16 fe, 
     const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t hot0 = 0;
     const uint32_t hot_lane = t.off_hot + 4u * (threadIdx.x & 63u);
-    auto run = [&](auto& sa, auto& da, auto& pa, auto& ra, bool other, auto& v) {
-        if constexpr (kLin) lin_n(t, gslot, sa, da, pa, ra, v);
-        else run_n<sizeof(v) / 4, kLds, kMode, kList, kD>(im, t, hot_lane, gslot, hot0, sa, da, pa, ra, other, v);
+    // src_mode 1 keeps the source interval table in global memory: reps for
+    // the linear paths (protocol > 2 fallback, CLS_F_FORCE_LINEAR)
+    const Img<false> gim{fe.gsrc};
+    auto src_rep = [&](const auto& a, auto& out) {
+        if constexpr (kFe == 1) fe_rep(gim, 0u, fe.gval, fe.top[0], fe.k8[0], a, out);
+        else fe_rep(im, fe.key[0], fe.val[0], fe.top[0], fe.k8[0], a, out);
+    };
+    auto classify = [&](const auto& s16, const auto& d16, auto& pa, auto& ra, bool other, auto& v) {
+        constexpr int N = sizeof(v) / 4;
+        uint32_t sa[N], da[N];
+        fe_rep(im, fe.key[1], fe.val[1], fe.top[1], fe.k8[1], d16, da);
+        if constexpr (kLin) {
+            src_rep(s16, sa);
+            lin_n(t, gslot, sa, da, pa, ra, v);
+        } else if constexpr (kFe == 1) {
+            src_hash16(im, fe, s16, sa);
+            uint32_t sl[N];
+            if (__any(other)) src_rep(s16, sl);                // rare: protocols > 2
+            run_n<N, kLds, kMode, kList, kD>(im, t, hot_lane, gslot, hot0, sa, da, pa, ra, other, v, sl);
+        } else {
+            src_rep(s16, sa);
+            run_n<N, kLds, kMode, kList, kD>(im, t, hot_lane, gslot, hot0, sa, da, pa, ra, other, v, sa);
+        }
     };
     // 4 packets per lane per step (vector dport / proto / verdict words),
     // the next step's loads in flight during this step's lookups
@@ -686,13 +764,11 @@ __global__ __launch_bounds__(kClsBlock) void classify16_cls(Cls4Dev t, Fe16 fe, 
         }
     };
     auto step = [&](const Buf& b, uint32_t g) {
-        uint32_t sa[4], da[4], v[4];
-        fe_rep<4, kLds>(im, fe.key[0], fe.val[0], fe.top[0], b.s, sa);
-        fe_rep<4, kLds>(im, fe.key[1], fe.val[1], fe.top[1], b.d, da);
+        uint32_t v[4];
         const uint32_t pr = b.pr;
         uint32_t pa[4] = {b.dp.x & 0xFFFFu, b.dp.x >> 16, b.dp.y & 0xFFFFu, b.dp.y >> 16};
         uint32_t ra[4] = {pr & 0xFFu, (pr >> 8) & 0xFFu, (pr >> 16) & 0xFFu, pr >> 24};
-        run(sa, da, pa, ra, ((pr | ((pr & 0x7F7F7F7Fu) + 0x7D7D7D7Du)) & 0x80808080u) != 0u, v);
+        classify(b.s, b.d, pa, ra, ((pr | ((pr & 0x7F7F7F7Fu) + 0x7D7D7D7Du)) & 0x80808080u) != 0u, v);
         if (verdict)
             stnt(v[0] | (v[1] << 8) | (v[2] << 16) | (v[3] << 24),
                  const_cast<uint32_t*>(at(reinterpret_cast<const uint32_t*>(verdict), g)));
@@ -713,12 +789,9 @@ __global__ __launch_bounds__(kClsBlock) void classify16_cls(Cls4Dev t, Fe16 fe, 
     }
     for (uint32_t i = nsteps * 4u + tid; i < uint32_t(p.n); i += nthreads) {
         const uint4 s1[1] = {ldnt(at(p.src, i))}, d1[1] = {ldnt(at(p.dst, i))};
-        uint32_t sa[1], da[1], v[1];
-        fe_rep<1, kLds>(im, fe.key[0], fe.val[0], fe.top[0], s1, sa);
-        fe_rep<1, kLds>(im, fe.key[1], fe.val[1], fe.top[1], d1, da);
+        uint32_t v[1];
         uint32_t pa[1] = {p.dport[i]}, ra[1] = {p.proto[i]};
-        if constexpr (kLin) lin_n(t, gslot, sa, da, pa, ra, v);
-        else run_n<1, kLds, kMode, kList, -1>(im, t, hot_lane, gslot, hot0, sa, da, pa, ra, ra[0] > 2u, v);
+        classify(s1, d1, pa, ra, ra[0] > 2u, v);
         if (verdict) verdict[i] = uint8_t(v[0]);
     }
     if constexpr (!kLds) {
@@ -1027,46 +1100,58 @@ hipError_t launch_classify4_cls(const Cls4Dev& t, const Pkts4& p, uint8_t* verdi
     return hipGetLastError();
 }
 
-template <bool kLds, int kMode, int kList, int kD, bool kLin>
+template <bool kLds, int kMode, int kList, int kD, bool kLin, int kFe>
 static void launch16_d(const Cls4Dev& t, const Fe16& fe, const Pkts16& p, uint8_t* verdict,
                        unsigned long long* gslot, const LaunchCfg& cfg) {
     const size_t lds = kLds ? t.lds_bytes : 0;
     if (kLds)
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(classify16_cls<kLds, kMode, kList, kD, kLin>),
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(classify16_cls<kLds, kMode, kList, kD, kLin, kFe>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
-    hipLaunchKernelGGL((classify16_cls<kLds, kMode, kList, kD, kLin>), dim3(cfg.grid), dim3(kClsBlock), lds,
+    hipLaunchKernelGGL((classify16_cls<kLds, kMode, kList, kD, kLin, kFe>), dim3(cfg.grid), dim3(kClsBlock), lds,
                        cfg.stream, t, fe, p, verdict, gslot);
 }
 
-template <bool kLds, int kMode, int kList>
+template <bool kLds, int kMode, int kList, int kFe>
 static void launch16_cls(const Cls4Dev& t, const Fe16& fe, const Pkts16& p, uint8_t* verdict,
                          unsigned long long* gslot, const LaunchCfg& cfg) {
     if constexpr (kLds && kList >= 3) {
         switch (t.bv_steps) {
-        case 0: launch16_d<kLds, kMode, kList, 0, false>(t, fe, p, verdict, gslot, cfg); return;
-        case 1: launch16_d<kLds, kMode, kList, 1, false>(t, fe, p, verdict, gslot, cfg); return;
-        case 2: launch16_d<kLds, kMode, kList, 2, false>(t, fe, p, verdict, gslot, cfg); return;
-        case 3: launch16_d<kLds, kMode, kList, 3, false>(t, fe, p, verdict, gslot, cfg); return;
-        case 4: launch16_d<kLds, kMode, kList, 4, false>(t, fe, p, verdict, gslot, cfg); return;
-        case 5: launch16_d<kLds, kMode, kList, 5, false>(t, fe, p, verdict, gslot, cfg); return;
+        case 0: launch16_d<kLds, kMode, kList, 0, false, kFe>(t, fe, p, verdict, gslot, cfg); return;
+        case 1: launch16_d<kLds, kMode, kList, 1, false, kFe>(t, fe, p, verdict, gslot, cfg); return;
+        case 2: launch16_d<kLds, kMode, kList, 2, false, kFe>(t, fe, p, verdict, gslot, cfg); return;
+        case 3: launch16_d<kLds, kMode, kList, 3, false, kFe>(t, fe, p, verdict, gslot, cfg); return;
+        case 4: launch16_d<kLds, kMode, kList, 4, false, kFe>(t, fe, p, verdict, gslot, cfg); return;
+        case 5: launch16_d<kLds, kMode, kList, 5, false, kFe>(t, fe, p, verdict, gslot, cfg); return;
         default: break;
         }
     }
-    launch16_d<kLds, kMode, kList, -1, false>(t, fe, p, verdict, gslot, cfg);
+    launch16_d<kLds, kMode, kList, -1, false, kFe>(t, fe, p, verdict, gslot, cfg);
 }
 
 template <bool kLds>
 static void dispatch16(const Cls4Dev& t, const Fe16& fe, const Pkts16& p, uint8_t* verdict,
                        unsigned long long* gslot, bool lin, const LaunchCfg& cfg) {
     if (lin) {
-        launch16_d<kLds, 0, 0, -1, true>(t, fe, p, verdict, gslot, cfg);
+        if (fe.src_mode == 1) launch16_d<kLds, 0, 0, -1, true, 1>(t, fe, p, verdict, gslot, cfg);
+        else launch16_d<kLds, 0, 0, -1, true, 0>(t, fe, p, verdict, gslot, cfg);
+        return;
+    }
+    if (fe.src_mode == 1) {                      // rows from the host-route hashes (core mode 3)
+        switch (t.list_mode) {
+        case 0: launch16_cls<kLds, 3, 0, 1>(t, fe, p, verdict, gslot, cfg); break;
+        case 1: launch16_cls<kLds, 3, 1, 1>(t, fe, p, verdict, gslot, cfg); break;
+        case 2: launch16_cls<kLds, 3, 2, 1>(t, fe, p, verdict, gslot, cfg); break;
+        case 3: launch16_cls<kLds, 3, 3, 1>(t, fe, p, verdict, gslot, cfg); break;
+        case 4: launch16_cls<kLds, 3, 4, 1>(t, fe, p, verdict, gslot, cfg); break;
+        default: break;
+        }
         return;
     }
     const int src = t.mode != 1 ? 0 : t.n_hash == 1 ? 2 : 1;
 #define CLS16_SRC_CASES(L)                                                                  \
-    case 3 * L + 0: launch16_cls<kLds, 0, L>(t, fe, p, verdict, gslot, cfg); break;         \
-    case 3 * L + 1: launch16_cls<kLds, 1, L>(t, fe, p, verdict, gslot, cfg); break;         \
-    case 3 * L + 2: launch16_cls<kLds, 2, L>(t, fe, p, verdict, gslot, cfg); break;
+    case 3 * L + 0: launch16_cls<kLds, 0, L, 0>(t, fe, p, verdict, gslot, cfg); break;      \
+    case 3 * L + 1: launch16_cls<kLds, 1, L, 0>(t, fe, p, verdict, gslot, cfg); break;      \
+    case 3 * L + 2: launch16_cls<kLds, 2, L, 0>(t, fe, p, verdict, gslot, cfg); break;
     switch (src + 3 * int(t.list_mode)) {
         CLS16_SRC_CASES(0)
         CLS16_SRC_CASES(1)

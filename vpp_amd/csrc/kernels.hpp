@@ -31,6 +31,13 @@ struct Pkts16 {
 // and the rep array's LDS byte offsets and the padded key count
 struct Fe16 {
     uint32_t key[2], val[2], top[2];
+    uint32_t k8[2];            // 8-B keys (compile.hpp key8)
+    uint32_t src_mode;         // 1: host-route hashes -> class row (Cls16Image)
+    uint32_t h4, cap4, mul4, s4_0, s4_1, L4;             // IPv4-mapped hash (s0 = 32 - L, s1 = 32 - 2 L)
+    uint32_t k6, r6, cap6, mul6, s6_0, s6_1, L6, fold[3]; // IPv6 hash
+    uint32_t dflt4, dflt6;     // rows of the families' sources no prefix covers
+    const uint8_t* gsrc;       // src_mode 1: the source interval table in global memory
+    uint32_t gval;             // (keys at 0, reps at gval; fe.top[0] keys)
 };
 
 struct Cls4Dev {
