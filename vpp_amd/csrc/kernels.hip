@@ -708,6 +708,17 @@ __device__ __forceinline__ void src_hash16(const Img<kLds>& im, const Fe16& fe, 
     }
 }
 
+// The source rep of one address from the global-memory interval table
+// (src_mode 1, protocol > 2 lanes only): out of line, so the rare path costs
+// the hot loop no registers.
+__device__ __noinline__ uint32_t src_rep_global(const uint8_t* g, uint32_t gval, uint32_t top, uint32_t k8,
+                                                uint4 a) {
+    const uint4 a1[1] = {a};
+    uint32_t r[1];
+    fe_rep(Img<false>{g}, 0u, gval, top, k8, a1, r);
+    return r[0];
+}
+
 template <bool kLds, int kMode, int kList, int kD, bool kLin, int kFe>
 __global__ __launch_bounds__(kClsBlock) void classify16_cls(Cls4Dev t, Fe16 fe, Pkts16 p, uint8_t* verdict,
                                                             unsigned long long* gslot) {
@@ -735,7 +746,11 @@ __global__ __launch_bounds__(kClsBlock) void classify16_cls(Cls4Dev t, Fe16 fe, 
         } else if constexpr (kFe == 1) {
             src_hash16(im, fe, s16, sa);
             uint32_t sl[N];
-            if (__any(other)) src_rep(s16, sl);                // rare: protocols > 2
+            if (__any(other)) {                                // rare: protocols > 2 need the rep
+#pragma unroll
+                for (int q = 0; q < N; ++q)
+                    sl[q] = ra[q] > 2u ? src_rep_global(fe.gsrc, fe.gval, fe.top[0], fe.k8[0], s16[q]) : 0u;
+            }
             run_n<N, kLds, kMode, kList, kD>(im, t, hot_lane, gslot, hot0, sa, da, pa, ra, other, v, sl);
         } else {
             src_rep(s16, sa);
@@ -743,49 +758,35 @@ __global__ __launch_bounds__(kClsBlock) void classify16_cls(Cls4Dev t, Fe16 fe, 
         }
     };
     // 4 packets per lane per step (vector dport / proto / verdict words),
-    // the next step's loads in flight during this step's lookups
+    // classified two at a time: a 16-byte packet's lookups hold about twice
+    // the registers of an IPv4 one, and the kernel must stay within 128
+    // VGPRs (1024-thread workgroups) without scratch.  The CU's 16 waves
+    // overlap one another's loads and lookups (no prefetch buffer).
     const uint32_t nsteps = p.vec ? uint32_t(p.n / 4u) : 0u;
     const uint2* DP = reinterpret_cast<const uint2*>(p.dport);
     const uint32_t* PR = reinterpret_cast<const uint32_t*>(p.proto);
-    struct Buf {
+    for (uint32_t g = tid; g < nsteps; g += nthreads) {
         uint4 s[4], d[4];
-        uint2 dp;
-        uint32_t pr;
-    };
-    auto load = [&](Buf& b, uint32_t g, bool ok) {
-        if (ok) {
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                b.s[k] = ldnt(at(p.src, 4u * g + k));
-                b.d[k] = ldnt(at(p.dst, 4u * g + k));
-            }
-            b.dp = ldnt(at(DP, g));
-            b.pr = ldnt(at(PR, g));
+        for (int k = 0; k < 4; ++k) {
+            s[k] = ldnt(at(p.src, 4u * g + k));
+            d[k] = ldnt(at(p.dst, 4u * g + k));
         }
-    };
-    auto step = [&](const Buf& b, uint32_t g) {
+        const uint2 dp = ldnt(at(DP, g));
+        const uint32_t pr = ldnt(at(PR, g));
         uint32_t v[4];
-        const uint32_t pr = b.pr;
-        uint32_t pa[4] = {b.dp.x & 0xFFFFu, b.dp.x >> 16, b.dp.y & 0xFFFFu, b.dp.y >> 16};
-        uint32_t ra[4] = {pr & 0xFFu, (pr >> 8) & 0xFFu, (pr >> 16) & 0xFFu, pr >> 24};
-        classify(b.s, b.d, pa, ra, ((pr | ((pr & 0x7F7F7F7Fu) + 0x7D7D7D7Du)) & 0x80808080u) != 0u, v);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const uint4 s2[2] = {s[2 * h], s[2 * h + 1]}, d2[2] = {d[2 * h], d[2 * h + 1]};
+            const uint32_t w = h ? dp.y : dp.x, r = pr >> (16 * h);
+            uint32_t pa[2] = {w & 0xFFFFu, w >> 16}, ra[2] = {r & 0xFFu, (r >> 8) & 0xFFu}, v2[2];
+            classify(s2, d2, pa, ra, (ra[0] | ra[1]) > 2u, v2);
+            v[2 * h] = v2[0];
+            v[2 * h + 1] = v2[1];
+        }
         if (verdict)
             stnt(v[0] | (v[1] << 8) | (v[2] << 16) | (v[3] << 24),
                  const_cast<uint32_t*>(at(reinterpret_cast<const uint32_t*>(verdict), g)));
-    };
-    {
-        Buf a, b;
-        uint32_t g = tid;
-        load(a, g, g < nsteps);
-        while (g < nsteps) {
-            load(b, g + nthreads, g + nthreads < nsteps);
-            step(a, g);
-            g += nthreads;
-            if (g >= nsteps) break;
-            load(a, g + nthreads, g + nthreads < nsteps);
-            step(b, g);
-            g += nthreads;
-        }
     }
     for (uint32_t i = nsteps * 4u + tid; i < uint32_t(p.n); i += nthreads) {
         const uint4 s1[1] = {ldnt(at(p.src, i))}, d1[1] = {ldnt(at(p.dst, i))};
