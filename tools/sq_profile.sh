@@ -16,7 +16,7 @@ out = sys.argv[1]
 agg = collections.defaultdict(list)
 for f in glob.glob(out + "/*/run_counter_collection.csv"):
     for r in csv.DictReader(open(f)):
-        if "classify4_cls" in r["Kernel_Name"]:
+        if "classify4_cls" in r["Kernel_Name"] or "classify16_cls" in r["Kernel_Name"]:
             agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
 with open(out + "/summary.txt", "w") as fo:
     for k in sorted(agg):
