@@ -102,3 +102,30 @@ def test_mock_renderer_single_packets(eng):
             assert r.test_traffic(p1, d, s_ip, d_ip, p, 5000, dp) == want
     finally:
         r.close()
+
+
+def test_vpptcp_committed_tables_on_gpu(eng):
+    """Session-rule renderer: the IngressOrientation tables it
+    commits are compiled onto the engine; packets against a pod's local table
+    and the global table match TestTraffic over the same rule lists."""
+    from test_vpptcp_cpu import EG1, EG2, IN1, IN2, IN3, POD1, POD1_IP, POD1_NS, POD2, POD2_IP, POD2_NS, contiv, host
+    from vpp_amd.renderer import vpptcp as V
+    sink = V.SessionRuleTables()
+    rend = V.Renderer(contiv((POD1, POD1_NS), (POD2, POD2_NS)), sink, engine=eng).init()
+    txn = rend.new_txn(False)
+    txn.render(POD1, host(POD1_IP), [IN1(), IN2()], [EG1(), EG2()], False)
+    txn.render(POD2, host(POD2_IP), [IN1(), IN3()], [], False)
+    txn.commit()
+    rng = random.Random(11)
+    try:
+        tables = [rend.local_rule_table(POD1), rend.local_rule_table(POD2), rend.global_rule_table()]
+        assert all(t is not None for t in tables)
+        for t in tables:
+            src, dst, proto, sport, dport = rand_packets(rng, t.rules, 3001)
+            want_v, want_c, want_u = otraffic.test_traffic_batch(t.rules, src, dst, proto, sport, dport)
+            v, c, u = t.test_traffic_batch(_rows(src), _rows(dst), np.array(proto, np.uint8),
+                                           np.array(dport, np.uint16))
+            assert list(v) == want_v
+            assert [int(x) for x in c] == want_c and u == want_u
+    finally:
+        rend.close()

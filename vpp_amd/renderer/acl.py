@@ -41,9 +41,26 @@ class ContivIfs:
         self.host_interconnect = host_interconnect
         self.other_physical = list(other_physical or [])
         self.pod_if = {}
+        self.pod_app_ns = {}
 
     def set_pod_if_name(self, pod: PodID, if_name: str):
         self.pod_if[pod] = if_name
+
+    def set_pod_app_ns_index(self, pod: PodID, ns_index: int):
+        """SetPodAppNsIndex (contiv_mock.go:50-52)."""
+        self.pod_app_ns[pod] = ns_index
+
+    def get_ns_index(self, namespace: str, name: str):
+        """GetNsIndex (contiv_mock.go:134-137)."""
+        idx = self.pod_app_ns.get(PodID(name, namespace))
+        return (0, False) if idx is None else (idx, True)
+
+    def get_pod_by_app_ns_index(self, ns_index: int):
+        """GetPodByAppNsIndex (contiv_mock.go:150-157)."""
+        for pod, idx in self.pod_app_ns.items():
+            if idx == ns_index:
+                return pod.namespace, pod.name, True
+        return "", "", False
 
     def get_if_name(self, namespace: str, name: str):
         name_if = self.pod_if.get(PodID(name, namespace))
