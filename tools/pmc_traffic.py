@@ -37,10 +37,10 @@ def stats(path, out):
     print(json.dumps(res, indent=1))
 
 
-def _per_dispatch(path, counter):
+def _per_dispatch(path, counter, kernel=KERNEL):
     vals = {}
     for r in _rows(path):
-        if KERNEL not in _kname(r):
+        if kernel not in _kname(r):
             continue
         if r.get("Counter_Name") != counter:
             continue
@@ -50,16 +50,18 @@ def _per_dispatch(path, counter):
 
 
 def pmc(fetch_csv, write_csv, config, packets, out):
-    f = _per_dispatch(fetch_csv, "FETCH_SIZE")
-    w = _per_dispatch(write_csv, "WRITE_SIZE")
+    # config 5 runs the 16-byte layout: classify16_cls, 35 B read per packet
+    kernel, read_pp = ("classify16_cls", 35) if int(config) == 5 else (KERNEL, 11)
+    f = _per_dispatch(fetch_csv, "FETCH_SIZE", kernel)
+    w = _per_dispatch(write_csv, "WRITE_SIZE", kernel)
     fk = sum(f) / len(f)
     wk = sum(w) / len(w)
     read_bytes = 2.0 * fk * 1024        # gfx950 FETCH_SIZE half-count correction
     write_bytes = wk * 1024
     packets = int(packets)
-    alg_read = packets * 11
+    alg_read = packets * read_pp
     alg_write = packets * 1
-    d = {"config": int(config), "packets": int(packets), "kernel": KERNEL,
+    d = {"config": int(config), "packets": int(packets), "kernel": kernel,
          "dispatches": [len(f), len(w)], "fetch_kib_raw": fk, "write_kib_raw": wk,
          "hbm_read_bytes_per_launch": read_bytes, "hbm_write_bytes_per_launch": write_bytes,
          "hbm_bytes_per_launch": read_bytes + write_bytes,
