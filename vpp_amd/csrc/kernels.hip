@@ -40,6 +40,10 @@ namespace cls {
 namespace {
 
 constexpr int kBlock = 1024;      // linear kernel
+// 16-byte kernel packet order: 1 wave-contiguous (default), 0 four consecutive per lane
+#ifndef CLS_COAL16
+#define CLS_COAL16 1
+#endif
 #ifndef CLS_BLOCK
 #define CLS_BLOCK 1024
 #endif
@@ -762,6 +766,42 @@ __global__ __launch_bounds__(kClsBlock) void classify16_cls(Cls4Dev t, Fe16 fe, 
     // the registers of an IPv4 one, and the kernel must stay within 128
     // VGPRs (1024-thread workgroups) without scratch.  The CU's 16 waves
     // overlap one another's loads and lookups (no prefetch buffer).
+#if CLS_COAL16
+    // Wave-contiguous packets: a wave's step covers 256 consecutive packets
+    // and lane l takes packets base + 64k + l (k = 0..3), so each 16-B
+    // address load instruction reads 1 KiB contiguous per wave (the
+    // lane-owns-4-consecutive order strides 64 B per lane and fetched 25 %
+    // more than the algorithmic bytes, profiles/r01_pmc_config5_lane4order.json);
+    // dport / proto / verdict move one element per packet, also contiguous
+    // per instruction.  Whole waves only (nsteps a multiple of 64 groups of 4,
+    // wave-uniform); the rest goes to the per-packet tail.
+    const uint32_t nsteps = uint32_t(p.n / 256u) * 64u;
+    for (uint32_t g = tid; g < nsteps; g += nthreads) {
+        const uint32_t base = 4u * (g & ~63u) + (g & 63u);
+        uint4 s[4], d[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            s[k] = ldnt(at(p.src, base + 64u * k));
+            d[k] = ldnt(at(p.dst, base + 64u * k));
+        }
+        uint32_t dp[4], pr[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            dp[k] = __builtin_nontemporal_load(p.dport + base + 64u * k);
+            pr[k] = __builtin_nontemporal_load(p.proto + base + 64u * k);
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const uint4 s2[2] = {s[2 * h], s[2 * h + 1]}, d2[2] = {d[2 * h], d[2 * h + 1]};
+            uint32_t pa[2] = {dp[2 * h], dp[2 * h + 1]}, ra[2] = {pr[2 * h], pr[2 * h + 1]}, v2[2];
+            classify(s2, d2, pa, ra, (ra[0] | ra[1]) > 2u, v2);
+            if (verdict) {
+                __builtin_nontemporal_store(uint8_t(v2[0]), verdict + base + 64u * (2 * h));
+                __builtin_nontemporal_store(uint8_t(v2[1]), verdict + base + 64u * (2 * h + 1));
+            }
+        }
+    }
+#else
     const uint32_t nsteps = p.vec ? uint32_t(p.n / 4u) : 0u;
     const uint2* DP = reinterpret_cast<const uint2*>(p.dport);
     const uint32_t* PR = reinterpret_cast<const uint32_t*>(p.proto);
@@ -788,6 +828,7 @@ __global__ __launch_bounds__(kClsBlock) void classify16_cls(Cls4Dev t, Fe16 fe, 
             stnt(v[0] | (v[1] << 8) | (v[2] << 16) | (v[3] << 24),
                  const_cast<uint32_t*>(at(reinterpret_cast<const uint32_t*>(verdict), g)));
     }
+#endif
     for (uint32_t i = nsteps * 4u + tid; i < uint32_t(p.n); i += nthreads) {
         const uint4 s1[1] = {ldnt(at(p.src, i))}, d1[1] = {ldnt(at(p.dst, i))};
         uint32_t v[1];
