@@ -6,12 +6,14 @@ list, pure Python loops, for small cases.  Addresses are Go net.IP byte
 strings (4 or 16 bytes); ``IPNet.contains`` is the Go 1.9 restatement in
 vpp_amd/gonet.py (the data model, not the evaluator under test).
 
-Pinning: the reference's TestTraffic expectations (configurator_test.go) need
-the configurator, which is out of scope, so this evaluator is pinned through
-the evalACL oracle instead: on rule lists both can express (SrcPort 0, TCP/UDP
-rules) renderACL + evalACL and TestTraffic must agree on every packet, with
-evalACL's default DENY standing for UNMATCHED.  tests/test_traffic_cpu.py
-checks that agreement on random lists.
+Pinning: the reference's own TestTraffic expectations (configurator_test.go,
+10 tests, 115 verdicts) are replayed through the configurator restatement
+(vpp_amd/configurator.py) into this evaluator from
+tests/golden/configurator_scenarios.json (tests/test_configurator_cpu.py).
+It is also cross-checked against the evalACL oracle: on rule lists both can
+express (SrcPort 0, TCP/UDP rules) renderACL + evalACL and TestTraffic must
+agree on every packet, with evalACL's default DENY standing for UNMATCHED
+(tests/test_traffic_cpu.py).
 """
 from __future__ import annotations
 
