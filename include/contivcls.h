@@ -125,7 +125,8 @@ enum {
     CLS_F_NO_VERDICT = 1u << 1,   /* verdict_out may be NULL (counters only) */
     CLS_F_ACCUMULATE = 1u << 2,   /* add to counters_out instead of overwriting */
     CLS_F_FORCE_LINEAR = 1u << 3, /* use the linear (ballot) kernel: GPU cross-check */
-    CLS_F_TIMING = 1u << 4        /* record HIP events around the classify kernel */
+    CLS_F_TIMING = 1u << 4,       /* record HIP events around the classify kernel */
+    CLS_F_CONN_CLS = 1u << 5      /* cls_connect_batch: use the classifier images at any batch size */
 };
 
 typedef struct cls_engine cls_engine;
@@ -212,6 +213,12 @@ int cls_if_acls(cls_engine* e, uint32_t if_id, int32_t* in_table, int32_t* out_t
  * with (src->dst, dport); SYN-ACK through dst_if inbound then src_if outbound
  * with (dst->src, sport); REFLECT marks sides reflected exactly as the
  * reference does.  Interface->ACL bindings are snapshotted at the call.
+ * In batches >= 65536, an ACL with a compiled classifier image whose linear
+ * work would be large (host batch: connections touching it x its rules >=
+ * 2048 x batch; device batch: >= 2048 rules) is evaluated by the classifier
+ * kernel for both tuples of every connection before the connection kernel
+ * runs; the others by a linear scan.  CLS_F_CONN_CLS: every imaged ACL
+ * (>= 64 rules) at any batch size; CLS_F_FORCE_LINEAR: none.
  */
 typedef struct cls_conn_soa {
     cls_pkt_soa pkt;           /* src/dst/sport/dport/proto of the SYN */

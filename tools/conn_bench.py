@@ -1,0 +1,76 @@
+#!/usr/bin/env python3
+"""Connection-path throughput (testConnection batches).
+
+Layout: the config-3 global ACL (9963 rules) bound to if0/if1 (in) and
+if0/if2 (out), 64 random local ACLs (1-300 rules) on 77 further interfaces,
+half of the connections entering through a global-table interface.  Times
+``Engine.connect_batch`` (host arrays in and out, so PCIe copies included)
+over N connections and the C oracle (one thread) on a sample.  Prints one
+JSON line.  usage: python tools/conn_bench.py [--n 4194304] [--iters 5]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "tests")]
+
+from aclgen import random_traffic  # noqa: E402
+from test_gpu_connect_scale import build, oracle_connections  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=1 << 22)
+    ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--cpu-sample", type=int, default=20000)
+    ap.add_argument("--other-proto", type=int, default=1, help="6%% of packets with protocol > 2")
+    a = ap.parse_args()
+    from vpp_amd.engine import Engine
+    eng = Engine()
+    ifs, bind, pool, spec = build(eng, 0, cfg=3)
+    n = a.n
+    tr = random_traffic(7, n, pool, other_proto=bool(a.other_proto))
+    rng = np.random.default_rng(7)
+    half = rng.random(n) < 0.5
+    tr["src"][half] = rng.choice(spec["pod_ips"].astype(np.uint32), half.sum())
+    dsts = spec["dst_addrs"].astype(np.uint32)
+    tr["dst"][half] = rng.choice(dsts, half.sum()) | rng.integers(0, 256, half.sum()).astype(np.uint32)
+    ids = np.array([eng.if_id(x) for x in ifs], np.uint32)
+    si = np.where(half, rng.integers(0, 2, n), rng.integers(0, len(ifs), n))
+    di = rng.integers(0, len(ifs), n)
+    args = (ids[si], ids[di], tr["src"], tr["dst"], tr["proto"], tr["sport"], tr["dport"])
+    res = {}
+    for mode in ("linear", "auto"):
+        out = eng.connect_batch(*args, mode=mode)        # warm-up (and table upload)
+        t0 = time.perf_counter()
+        for _ in range(a.iters):
+            out = eng.connect_batch(*args, mode=mode)
+        res[mode] = ((time.perf_counter() - t0) / a.iters, out)
+    assert np.array_equal(res["linear"][1], res["auto"][1]), "linear and classifier modes differ"
+    dt, out = res["auto"]
+    k = a.cpu_sample
+    t1 = time.perf_counter()
+    want = oracle_connections(bind, ifs, si[:k], di[:k], tr["src"][:k], tr["dst"][:k], tr["proto"][:k],
+                              tr["sport"][:k], tr["dport"][:k])
+    cpu_dt = time.perf_counter() - t1
+    assert np.array_equal(out[:k], want), "connection verdicts differ from the oracle"
+    print(json.dumps({
+        "metric": "connections classified per second (testConnection, up to 4 ACL evaluations each)",
+        "value": round(n / dt / 1e6, 3), "unit": "Mconn/s", "n": n, "ms_per_batch": round(dt * 1e3, 3),
+        "pcie_included": True, "global_rules": len(bind["if0"][0]), "other_proto": bool(a.other_proto),
+        "linear_scan": {"value": round(n / res["linear"][0] / 1e6, 3), "unit": "Mconn/s",
+                        "ms_per_batch": round(res["linear"][0] * 1e3, 3)},
+        "verdicts": np.bincount(out, minlength=4).tolist(),
+        "cpu_baseline": {"value": round(k / cpu_dt / 1e6, 5), "unit": "Mconn/s", "cores": 1,
+                         "kind": "port", "sample": "%d connections, orc_test_connection" % k},
+        "parity": "first %d connections bit-exact vs oracle" % k}))
+    eng.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -17,7 +17,7 @@ LIB_PATH = os.environ.get("CONTIVCLS_LIB") or os.path.join(_HERE, "libcontivcls.
 # status codes
 OK, E_INVAL, E_NOMEM, E_HIP, E_RCCL, E_NOTFOUND, E_NODEV = 0, -1, -2, -3, -4, -5, -6
 # flags
-F_DEVICE, F_NO_VERDICT, F_ACCUMULATE, F_FORCE_LINEAR, F_TIMING = 1, 2, 4, 8, 16
+F_DEVICE, F_NO_VERDICT, F_ACCUMULATE, F_FORCE_LINEAR, F_TIMING, F_CONN_CLS = 1, 2, 4, 8, 16, 32
 AF_V4, AF_V16 = 4, 16
 
 R_MATCHES, R_MACIP, R_IPRULE, R_IP, R_OTHER = 1, 2, 4, 8, 16

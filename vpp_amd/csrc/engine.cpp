@@ -93,6 +93,7 @@ struct cls_engine {
     uint32_t changes = 0;
     // scratch for host-pointer batches
     DevBuf s_src, s_dst, s_sport, s_dport, s_proto, s_verdict, s_if_a, s_if_b, s_desc, s_ifs;
+    DevBuf s_pre;                  // connection path: classifier verdicts per large ACL (2 bytes/connection)
     DevBuf s_pool;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool timed = false;
@@ -278,6 +279,10 @@ int cls_table_get_info(cls_engine* e, uint32_t table_id, cls_table_info* info) {
 
 // ---------------------------------------------------------------------------
 constexpr uint64_t kClsChunk = 1ull << 30;   // packets per classify launch (32-bit offsets)
+constexpr uint64_t kConnClsMinBatch = 1ull << 16;  // connection batches that use the classifier images
+constexpr uint32_t kConnClsMinRules = 64;          // ACLs evaluated by the classifier in connection batches
+constexpr uint32_t kConnClsWork = 2048;            // ... when touches x rules >= this x batch size (host batch)
+constexpr uint32_t kConnClsDevRules = 2048;        // ... when it has this many rules (device batch)
 
 static bool aligned(const void* p, size_t a) { return (reinterpret_cast<uintptr_t>(p) % a) == 0; }
 
@@ -701,6 +706,7 @@ int cls_connect_batch(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t*
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : e->stream;
     // snapshot the bindings: descriptor per table, (in, out) per interface
     std::vector<AclDesc> desc;
+    std::vector<std::shared_ptr<Table>> dtab;     // table of each descriptor
     std::unordered_map<int32_t, int32_t> slot;
     auto desc_of = [&](int32_t tid) -> int32_t {
         if (tid < 0) return -1;
@@ -708,23 +714,20 @@ int cls_connect_batch(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t*
         if (f != slot.end()) return f->second;
         auto t = e->tables.find(uint32_t(tid));
         if (t == e->tables.end()) return -1;
-        AclDesc d{t->second->d_lin4.as<LinRule4>(), uint32_t(t->second->lin4.size()), 1u};
+        AclDesc d{t->second->d_lin4.as<LinRule4>(), uint32_t(t->second->lin4.size()), 1u, nullptr};
         desc.push_back(d);
+        dtab.push_back(t->second);
         slot[tid] = int32_t(desc.size() - 1);
         return int32_t(desc.size() - 1);
     };
     std::vector<IfAcls> ifs(std::max<size_t>(1, e->if_acl.size()));
     for (size_t i = 0; i < e->if_acl.size(); ++i)
         ifs[i] = IfAcls{desc_of(e->if_acl[i].first), desc_of(e->if_acl[i].second)};
-    if (desc.empty()) desc.push_back(AclDesc{nullptr, 0, 0});
+    if (desc.empty()) desc.push_back(AclDesc{nullptr, 0, 0, nullptr});
     if (!(flags & CLS_F_DEVICE))
         for (uint64_t i = 0; i < n; ++i)
             if (c->src_if[i] >= e->if_acl.size() || c->dst_if[i] >= e->if_acl.size())
                 return fail(e, CLS_E_INVAL, "connection %llu: unknown interface id", (unsigned long long)i);
-    HIPC(e, e->s_desc.ensure(desc.size() * sizeof(AclDesc)));
-    HIPC(e, e->s_ifs.ensure(ifs.size() * sizeof(IfAcls)));
-    HIPC(e, hipMemcpyAsync(e->s_desc.p, desc.data(), desc.size() * sizeof(AclDesc), hipMemcpyHostToDevice, s));
-    HIPC(e, hipMemcpyAsync(e->s_ifs.p, ifs.data(), ifs.size() * sizeof(IfAcls), hipMemcpyHostToDevice, s));
     const uint32_t *src = pk.src4, *dst = pk.dst4, *sif = c->src_if, *dif = c->dst_if;
     const uint16_t *sp = pk.sport, *dp = pk.dport;
     const uint8_t* pr = pk.proto;
@@ -747,6 +750,68 @@ int cls_connect_batch(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t*
         sp = e->s_sport.as<uint16_t>(); dp = e->s_dport.as<uint16_t>();
         pr = e->s_proto.as<uint8_t>(); o = e->s_verdict.as<uint8_t>();
     }
+    // Large ACLs: the classifier evaluates the SYN tuple (src, dst, dport) and
+    // the SYN-ACK tuple (dst, src, sport) of every connection, one launch
+    // each; the connection kernel then reads those verdicts instead of
+    // scanning the ACL.  Whole-batch evaluation keeps the classify launches
+    // dense (no compaction); it costs 2 launches per large ACL.
+    // Which ACLs: with a host batch, those whose linear work would be large --
+    // connections touching the ACL x its rule count >= kConnClsWork x batch
+    // (touches counted per interface binding); with a device batch, the
+    // ACLs of >= kConnClsDevRules rules.  CLS_F_CONN_CLS: every imaged ACL.
+    std::vector<uint32_t> big;
+    if (n && !(flags & CLS_F_FORCE_LINEAR) && (n >= kConnClsMinBatch || (flags & CLS_F_CONN_CLS))) {
+        std::vector<uint64_t> touch(dtab.size(), 0);
+        if (!dev && !(flags & CLS_F_CONN_CLS)) {
+            std::vector<uint64_t> per_if(ifs.size(), 0);
+            for (uint64_t i = 0; i < n; ++i) {
+                ++per_if[c->src_if[i]];
+                if (c->dst_if[i] != c->src_if[i]) ++per_if[c->dst_if[i]];
+            }
+            for (size_t f = 0; f < e->if_acl.size(); ++f) {
+                if (ifs[f].in >= 0) touch[ifs[f].in] += per_if[f];
+                if (ifs[f].out >= 0 && ifs[f].out != ifs[f].in) touch[ifs[f].out] += per_if[f];
+            }
+        }
+        for (uint32_t j = 0; j < dtab.size(); ++j) {
+            const Table& t = *dtab[j];
+            if (!t.has_cls || t.n_rules < kConnClsMinRules) continue;
+            const bool want = (flags & CLS_F_CONN_CLS) ||
+                              (dev ? t.n_rules >= kConnClsDevRules
+                                   : double(touch[j]) * t.n_rules >= double(kConnClsWork) * double(n));
+            if (want) big.push_back(j);
+        }
+    }
+    if (!big.empty()) {
+        if (n > kClsChunk) return fail(e, CLS_E_INVAL, "connection batch above 2^30 with classifier ACLs");
+        HIPC(e, e->s_pre.ensure(big.size() * 2 * n));
+        for (size_t b = 0; b < big.size(); ++b) {
+            Table& t = *dtab[big[b]];
+            uint8_t* pre = e->s_pre.as<uint8_t>() + b * 2 * n;
+            desc[big[b]].pre = pre;
+            Cls4Dev cd = cls4_dev(t.img, t.d_img, t.d_lin4, uint32_t(t.lin4.size()), t.n_rules);
+            LaunchCfg cfg;
+            cfg.stream = s;
+            cfg.grid = cls_grid(e, true, t.lds_resident, t.img.lds_bytes, n);
+            if (t.lds_resident) {
+                HIPC(e, t.d_part.ensure(size_t(cfg.grid) * t.img.n_ctr * 4));
+                cd.part = t.d_part.as<uint32_t>();
+            }
+            const Pkts4 syn{src, dst, dp, pr, n}, ack{dst, src, sp, pr, n};
+            for (int k = 0; k < 2; ++k) {
+                const Pkts4& q = k ? ack : syn;
+                const bool vec = aligned(q.src, 16) && aligned(q.dst, 16) && aligned(q.dport, 8) &&
+                                 aligned(q.proto, 4) && aligned(pre + k * n, 4);
+                // hit counters land in the table's scratch slots (cleared by every classify call)
+                HIPC(e, launch_classify4_cls(cd, q, pre + k * n, t.d_slot.as<unsigned long long>(),
+                                             t.lds_resident, vec, cfg));
+            }
+        }
+    }
+    HIPC(e, e->s_desc.ensure(desc.size() * sizeof(AclDesc)));
+    HIPC(e, e->s_ifs.ensure(ifs.size() * sizeof(IfAcls)));
+    HIPC(e, hipMemcpyAsync(e->s_desc.p, desc.data(), desc.size() * sizeof(AclDesc), hipMemcpyHostToDevice, s));
+    HIPC(e, hipMemcpyAsync(e->s_ifs.p, ifs.data(), ifs.size() * sizeof(IfAcls), hipMemcpyHostToDevice, s));
     HIPC(e, launch_connect4(e->s_desc.as<AclDesc>(), e->s_ifs.as<IfAcls>(), sif, dif, src, dst, sp, dp, pr,
                             n, o, s));
     if (!dev) {

@@ -921,12 +921,14 @@ __global__ void remap_kernel(const unsigned long long* __restrict__ slot,
     }
 }
 
-// evalACL on one ACL from global memory; returns ACLAction (nil ACL: PERMIT)
+// evalACL on one ACL; returns ACLAction (nil ACL: PERMIT).  ACLs with a
+// classifier image were evaluated for both tuples before this kernel (pre).
 __device__ uint32_t eval_acl4(const AclDesc* __restrict__ acls, int32_t a, uint32_t src,
-                              uint32_t dst, uint32_t port, uint32_t p) {
+                              uint32_t dst, uint32_t port, uint32_t p, uint64_t pre_idx) {
     if (a < 0) return 1u;
     const AclDesc A = acls[a];
     if (!A.valid) return 1u;
+    if (A.pre) return A.pre[pre_idx];
     uint32_t res, rule;
     linear_one(A.rules, A.n, 0xFFFFFFFFu, src, dst, port, p, res, rule);
     return res;
@@ -948,23 +950,23 @@ __global__ void connect4_kernel(const AclDesc* __restrict__ acls, const IfAcls* 
     const uint32_t sa = src[i], da = dst[i], sp = sport[i], dp = dport[i];
     const uint32_t p = proto[i] <= 2 ? proto[i] : 3u;
     bool srefl = false, drefl = false;
-    uint32_t a = eval_acl4(acls, S.in, sa, da, dp, p);            // SYN: src inbound
+    uint32_t a = eval_acl4(acls, S.in, sa, da, dp, p, i);         // SYN: src inbound
     if (a == 3u) { out[i] = 3; return; }
     if (a == 0u) { out[i] = 0; return; }
     if (a == 2u) { srefl = true; if (same) drefl = true; }
     if (!drefl) {                                                 // SYN: dst outbound
-        a = eval_acl4(acls, D.out, sa, da, dp, p);
+        a = eval_acl4(acls, D.out, sa, da, dp, p, i);
         if (a == 3u) { out[i] = 3; return; }
         if (a == 0u) { out[i] = 0; return; }
         if (a == 2u) { drefl = true; if (same) srefl = true; }
     }
     if (!drefl) {                                                 // SYN-ACK: dst inbound
-        a = eval_acl4(acls, D.in, da, sa, sp, p);
+        a = eval_acl4(acls, D.in, da, sa, sp, p, n + i);
         if (a == 3u) { out[i] = 3; return; }
         if (a == 0u) { out[i] = 1; return; }
     }
     if (!srefl) {                                                 // SYN-ACK: src outbound
-        a = eval_acl4(acls, S.out, da, sa, sp, p);
+        a = eval_acl4(acls, S.out, da, sa, sp, p, n + i);
         if (a == 3u) { out[i] = 3; return; }
         if (a == 0u) { out[i] = 1; return; }
     }

@@ -95,6 +95,7 @@ struct AclDesc {                 // one installed ACL for the connection kernel
     const LinRule4* rules;
     uint32_t n;
     uint32_t valid;              // 0 = nil ACL (PERMIT)
+    const uint8_t* pre;          // classifier verdicts: [0, n) SYN tuple, [n, 2n) SYN-ACK tuple; or null
 };
 struct IfAcls {                  // interface -> (inbound, outbound) AclDesc index, -1 = nil
     int32_t in, out;

@@ -229,7 +229,11 @@ class Engine:
         self._check(_abi.lib().cls_if_acls(self.h, if_id, C.byref(a), C.byref(b)))
         return a.value, b.value
 
-    def connect_batch(self, src_if, dst_if, src, dst, proto, sport, dport) -> np.ndarray:
+    def connect_batch(self, src_if, dst_if, src, dst, proto, sport, dport, mode: str = "auto") -> np.ndarray:
+        """testConnection over a batch (cls_connect_batch).  mode: "auto" (ACLs
+        with a classifier image use it for batches >= 65536), "classifier"
+        (at any size) or "linear" (every ACL scanned)."""
+        flags = {"auto": 0, "classifier": _abi.F_CONN_CLS, "linear": _abi.F_FORCE_LINEAR}[mode]
         arrs = [np.ascontiguousarray(src_if, np.uint32), np.ascontiguousarray(dst_if, np.uint32),
                 np.ascontiguousarray(src, np.uint32), np.ascontiguousarray(dst, np.uint32),
                 np.ascontiguousarray(proto, np.uint8), np.ascontiguousarray(sport, np.uint16),
@@ -239,7 +243,7 @@ class Engine:
         out = np.zeros(n, np.uint8)
         pk = _abi.PktSoa(_abi.AF_V4, _ptr(s), _ptr(d), None, None, _ptr(sp), _ptr(dp), _ptr(p))
         cs = _abi.ConnSoa(pk, _ptr(si), _ptr(di))
-        self._check(_abi.lib().cls_connect_batch(self.h, C.byref(cs), n, _ptr(out), 0, None))
+        self._check(_abi.lib().cls_connect_batch(self.h, C.byref(cs), n, _ptr(out), flags, None))
         return out
 
 
