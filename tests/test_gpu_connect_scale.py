@@ -74,7 +74,7 @@ def oracle_connections(bind, ifs, si, di, src, dst, proto, sport, dport):
     return out
 
 
-@pytest.mark.parametrize("mode", ["classifier", "linear", "auto"])
+@pytest.mark.parametrize("mode", ["classifier", "linear", "auto", "device"])
 @pytest.mark.parametrize("seed", [0, 1])
 def test_connections_at_scale_match_oracle(seed, mode):
     from vpp_amd.engine import Engine
@@ -91,8 +91,15 @@ def test_connections_at_scale_match_oracle(seed, mode):
         ids = np.array([eng.if_id(x) for x in ifs], np.uint32)
         si = rng.integers(0, len(ifs), n)
         di = np.where(rng.random(n) < 0.1, si, rng.integers(0, len(ifs), n))
-        got = eng.connect_batch(ids[si], ids[di], tr["src"], tr["dst"], tr["proto"], tr["sport"], tr["dport"],
-                                mode=mode)
+        args = [ids[si], ids[di], tr["src"], tr["dst"], tr["proto"], tr["sport"], tr["dport"]]
+        if mode == "device":                      # CLS_F_DEVICE batch: every ACL >= 64 rules on the classifier
+            import torch
+            dv = [torch.from_numpy(np.ascontiguousarray(x).view({4: np.int32, 2: np.int16, 1: np.uint8}[x.dtype.itemsize]))
+                  .to("cuda") for x in args]
+            torch.cuda.synchronize()
+            got = eng.connect_batch(*dv, mode="classifier").cpu().numpy()
+        else:
+            got = eng.connect_batch(*args, mode=mode)
         want = oracle_connections(bind, ifs, si, di, tr["src"], tr["dst"], tr["proto"], tr["sport"],
                                   tr["dport"])
         bad = np.nonzero(got != want)[0]

@@ -4,8 +4,9 @@
 Layout: the config-3 global ACL (9963 rules) bound to if0/if1 (in) and
 if0/if2 (out), 64 random local ACLs (1-300 rules) on 77 further interfaces,
 half of the connections entering through a global-table interface.  Times
-``Engine.connect_batch`` (host arrays in and out, so PCIe copies included)
-over N connections and the C oracle (one thread) on a sample.  Prints one
+``Engine.connect_batch`` over N connections with host arrays in and out
+(PCIe copies included; auto and linear modes) and with device-resident
+tensors (CLS_F_DEVICE, ``hbm_resident``), and the C oracle (one thread) on a sample.  Prints one
 JSON line.  usage: python tools/conn_bench.py [--n 4194304] [--iters 5]
 """
 import argparse
@@ -53,6 +54,17 @@ def main():
         res[mode] = ((time.perf_counter() - t0) / a.iters, out)
     assert np.array_equal(res["linear"][1], res["auto"][1]), "linear and classifier modes differ"
     dt, out = res["auto"]
+    # HBM-resident batch (CLS_F_DEVICE): no PCIe in the timed region
+    import torch
+    dargs = [torch.from_numpy(np.ascontiguousarray(x).view({4: np.int32, 2: np.int16, 1: np.uint8}[x.dtype.itemsize]))
+             .to("cuda") for x in (args[0], args[1], args[2], args[3], args[4], args[5], args[6])]
+    torch.cuda.synchronize()
+    dev_out = eng.connect_batch(*dargs)
+    assert np.array_equal(dev_out.cpu().numpy(), out), "device batch differs"
+    t0 = time.perf_counter()
+    for _ in range(a.iters):
+        dev_out = eng.connect_batch(*dargs)
+    dev_dt = (time.perf_counter() - t0) / a.iters
     k = a.cpu_sample
     t1 = time.perf_counter()
     want = oracle_connections(bind, ifs, si[:k], di[:k], tr["src"][:k], tr["dst"][:k], tr["proto"][:k],
@@ -63,6 +75,8 @@ def main():
         "metric": "connections classified per second (testConnection, up to 4 ACL evaluations each)",
         "value": round(n / dt / 1e6, 3), "unit": "Mconn/s", "n": n, "ms_per_batch": round(dt * 1e3, 3),
         "pcie_included": True, "global_rules": len(bind["if0"][0]), "other_proto": bool(a.other_proto),
+        "hbm_resident": {"value": round(n / dev_dt / 1e6, 3), "unit": "Mconn/s",
+                         "ms_per_batch": round(dev_dt * 1e3, 3)},
         "linear_scan": {"value": round(n / res["linear"][0] / 1e6, 3), "unit": "Mconn/s",
                         "ms_per_batch": round(res["linear"][0] * 1e3, 3)},
         "verdicts": np.bincount(out, minlength=4).tolist(),

@@ -234,6 +234,8 @@ class Engine:
         with a classifier image use it for batches >= 65536), "classifier"
         (at any size) or "linear" (every ACL scanned)."""
         flags = {"auto": 0, "classifier": _abi.F_CONN_CLS, "linear": _abi.F_FORCE_LINEAR}[mode]
+        if _is_torch(src):
+            return self._connect_batch_device(src_if, dst_if, src, dst, proto, sport, dport, flags)
         arrs = [np.ascontiguousarray(src_if, np.uint32), np.ascontiguousarray(dst_if, np.uint32),
                 np.ascontiguousarray(src, np.uint32), np.ascontiguousarray(dst, np.uint32),
                 np.ascontiguousarray(proto, np.uint8), np.ascontiguousarray(sport, np.uint16),
@@ -244,6 +246,23 @@ class Engine:
         pk = _abi.PktSoa(_abi.AF_V4, _ptr(s), _ptr(d), None, None, _ptr(sp), _ptr(dp), _ptr(p))
         cs = _abi.ConnSoa(pk, _ptr(si), _ptr(di))
         self._check(_abi.lib().cls_connect_batch(self.h, C.byref(cs), n, _ptr(out), flags, None))
+        return out
+
+    def _connect_batch_device(self, src_if, dst_if, src, dst, proto, sport, dport, flags):
+        """Device-resident batch (CLS_F_DEVICE): contiguous GPU tensors of 4-byte
+        interface ids and addresses, 2-byte ports and 1-byte protocols, already
+        written (the call runs on the engine's stream).  Returns a uint8 tensor."""
+        import torch
+        arrs = [src_if, dst_if, src, dst, sport, dport, proto]
+        sizes = [4, 4, 4, 4, 2, 2, 1]
+        n = src.numel()
+        for x, sz in zip(arrs, sizes):
+            if not (_is_torch(x) and x.is_cuda and x.is_contiguous() and x.element_size() == sz and x.numel() == n):
+                raise ClsError("device connection batch: contiguous GPU tensors of element sizes %s" % sizes)
+        out = torch.empty(n, dtype=torch.uint8, device=src.device)
+        pk = _abi.PktSoa(_abi.AF_V4, _ptr(src), _ptr(dst), None, None, _ptr(sport), _ptr(dport), _ptr(proto))
+        cs = _abi.ConnSoa(pk, _ptr(src_if), _ptr(dst_if))
+        self._check(_abi.lib().cls_connect_batch(self.h, C.byref(cs), n, _ptr(out), flags | _abi.F_DEVICE, None))
         return out
 
 
