@@ -232,3 +232,48 @@ def test_random_policy_sets_translation_matches_literal(seed):
             assert list(v) == want and [int(x) for x in c] == want_c and u == want_u
             checked += 1
     assert checked >= 5
+
+
+def test_rule_key_agrees_with_compare():
+    from vpp_amd.renderer.api import ContivRule
+    rng = random.Random(11)
+
+    def net():
+        k = rng.randrange(6)
+        if k == 0:
+            return IPNet()
+        if k in (1, 2):                                     # IPv4, 4- or 16-byte address
+            ones = rng.choice([0, 8, 16, 24, 30, 32])
+            ip = bytes([10, rng.randrange(2), rng.randrange(2), rng.randrange(4)])
+            return IPNet(ip if k == 1 else gonet.V4_IN_V6_PREFIX + ip, gonet.cidr_mask(ones, 32))
+        if k == 3:                                          # IPv6
+            ones = rng.choice([0, 64, 120, 128])
+            ip = bytes([0xfd] + [0] * 14 + [rng.randrange(4)])
+            return IPNet(ip, gonet.cidr_mask(ones, 128))
+        if k == 4:                                          # non-contiguous mask
+            return IPNet(bytes([10, 0, 0, rng.randrange(4)]), bytes([255, 0, 255, 0]))
+        return IPNet(bytes([10, 0, rng.randrange(2), 0]), gonet.cidr_mask(rng.choice([16, 24]), 128))
+
+    rules = [ContivRule(rng.randrange(2), net(), net(), rng.randrange(2), 0, rng.choice([0, 80])) for _ in range(400)]
+    for a in rules:
+        for b in rules[:120]:
+            ka, kb = C._rule_key(a), C._rule_key(b)
+            if ka is not None and kb is not None:
+                assert (ka == kb) == (a.compare(b) == 0), (a, b)
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_generate_rules_keyed_equals_scan(seed):
+    from configurator_replay import random_policy_set
+    rng = random.Random(seed)
+    cache, assign = random_policy_set(rng, n_pods=200, n_policies=60)
+    txn = C.PolicyConfigurator(cache).new_txn(False)
+    pols = sorted({id(p): p for ps in assign.values() for p in ps}.values(), key=C._policy_key)
+    fast = txn.generate_rules(C.MATCH_INGRESS, pols) + txn.generate_rules(C.MATCH_EGRESS, pols)
+    orig = C._RuleList
+    try:
+        C._RuleList = list                                  # the reference's linear scan
+        slow = txn.generate_rules(C.MATCH_INGRESS, pols) + txn.generate_rules(C.MATCH_EGRESS, pols)
+    finally:
+        C._RuleList = orig
+    assert len(fast) == len(slow) and all(a.compare(b) == 0 for a, b in zip(fast, slow))

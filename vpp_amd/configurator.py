@@ -114,10 +114,62 @@ def subtract_subnet(net1: IPNet, net2: IPNet) -> List[IPNet]:
     return out
 
 
+def _net_key(net: IPNet):
+    """A key with key(a) == key(b) iff CompareIPNets(a, b) == 0, for the
+    networks where that is easy to state (empty, or a contiguous mask of the
+    address family's width); None otherwise."""
+    if len(net.ip) == 0:
+        return ()
+    ip4 = gonet.to4(net.ip)
+    if ip4 is not None and len(net.mask) == 4:
+        ip, bits = ip4, 32
+    elif ip4 is None and len(net.ip) == 16 and len(net.mask) == 16:
+        ip, bits = net.ip, 128
+    else:
+        return None
+    ones = gonet.simple_mask_length(net.mask)
+    if ones < 0:
+        return None
+    return (bits, ones, gonet.ip_mask(ip, gonet.cidr_mask(ones, bits)))
+
+
+def _rule_key(r: ContivRule):
+    s, d = _net_key(r.src_network), _net_key(r.dest_network)
+    if s is None or d is None:
+        return None
+    return (r.protocol, s, d, r.src_port, r.dest_port, r.action)
+
+
+class _RuleList(list):
+    """A rule list with appendRule's duplicate test (Compare == 0) answered
+    from a key set -- O(1) per append instead of a scan of the list -- while
+    every rule has a key; any keyless rule switches back to the scan."""
+
+    def __init__(self):
+        super().__init__()
+        self.keys = set()
+        self.keyless = False
+
+    def append_unique(self, n: ContivRule) -> None:
+        k = None if self.keyless else _rule_key(n)
+        if k is None:
+            self.keyless = True
+            if any(r.compare(n) == 0 for r in self):
+                return
+        elif k in self.keys:
+            return
+        else:
+            self.keys.add(k)
+        self.append(n)
+
+
 def _append_rules(rules: List[ContivRule], *new: ContivRule) -> List[ContivRule]:
     """appendRule(s) (configurator_impl.go:482-498): skip exact duplicates."""
+    keyed = getattr(rules, "append_unique", None)
     for n in new:
-        if not any(r.compare(n) == 0 for r in rules):
+        if keyed is not None:
+            keyed(n)
+        elif not any(r.compare(n) == 0 for r in rules):
             rules.append(n)
     return rules
 
@@ -219,7 +271,7 @@ class PolicyConfiguratorTxn:
 
     def generate_rules(self, direction: int, policies: List[ContivPolicy]) -> List[ContivRule]:
         """generateRules (configurator_impl.go:248-479)."""
-        rules: List[ContivRule] = []
+        rules: List[ContivRule] = _RuleList()
         has_policy = False
         all_allowed = False
         for policy in policies:
@@ -265,4 +317,4 @@ class PolicyConfiguratorTxn:
                             _append_rules(rules, _rule(ACTION_PERMIT, _port_proto(port), port.number, src, dst))
         if has_policy and not all_allowed:                # :457-476 deny the rest
             _append_rules(rules, _rule(ACTION_DENY, R_TCP), _rule(ACTION_DENY, R_UDP))
-        return rules
+        return list(rules)
