@@ -40,3 +40,11 @@ def test_engine_create_without_gpu_fails_loudly():
 def test_library_is_gfx950_code_object():
     data = open(_abi.LIB_PATH, "rb").read()
     assert b"gfx950" in data
+
+
+def test_flag_values_match_header():
+    text = open(os.path.join(ROOT, "include", "contivcls.h")).read()
+    flags = {m.group(1): 1 << int(m.group(2))
+             for m in re.finditer(r"CLS_F_(\w+)\s*=\s*1u\s*<<\s*(\d+)", text)}
+    assert flags == {"DEVICE": _abi.F_DEVICE, "NO_VERDICT": _abi.F_NO_VERDICT, "ACCUMULATE": _abi.F_ACCUMULATE,
+                     "FORCE_LINEAR": _abi.F_FORCE_LINEAR, "TIMING": _abi.F_TIMING, "CONN_CLS": _abi.F_CONN_CLS}
