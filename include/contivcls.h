@@ -215,9 +215,9 @@ int cls_if_acls(cls_engine* e, uint32_t if_id, int32_t* in_table, int32_t* out_t
  * reference does.  Interface->ACL bindings are snapshotted at the call.
  * In batches >= 65536, an ACL with a compiled classifier image whose linear
  * work would be large (host batch: connections touching it x its rules >=
- * 2048 x batch; device batch: >= 2048 rules) is evaluated by the classifier
- * kernel for both tuples of every connection before the connection kernel
- * runs; the others by a linear scan.  CLS_F_CONN_CLS: every imaged ACL
+ * 2048 x batch, touches estimated from a sample; device batch: >= 2048
+ * rules) is evaluated by the classifier kernel for both tuples of every
+ * connection before the connection kernel runs; the others by a linear scan.  CLS_F_CONN_CLS: every imaged ACL
  * (>= 64 rules) at any batch size; CLS_F_FORCE_LINEAR: none.
  */
 typedef struct cls_conn_soa {

@@ -757,16 +757,19 @@ int cls_connect_batch(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t*
     // dense (no compaction); it costs 2 launches per large ACL.
     // Which ACLs: with a host batch, those whose linear work would be large --
     // connections touching the ACL x its rule count >= kConnClsWork x batch
-    // (touches counted per interface binding); with a device batch, the
+    // (touches estimated per interface binding from <= 64 Ki sampled
+    // connections); with a device batch, the
     // ACLs of >= kConnClsDevRules rules.  CLS_F_CONN_CLS: every imaged ACL.
     std::vector<uint32_t> big;
     if (n && !(flags & CLS_F_FORCE_LINEAR) && (n >= kConnClsMinBatch || (flags & CLS_F_CONN_CLS))) {
         std::vector<uint64_t> touch(dtab.size(), 0);
         if (!dev && !(flags & CLS_F_CONN_CLS)) {
+            // an estimate is enough: every step-th connection, scaled back
+            const uint64_t step = std::max<uint64_t>(1, n / 65536);
             std::vector<uint64_t> per_if(ifs.size(), 0);
-            for (uint64_t i = 0; i < n; ++i) {
-                ++per_if[c->src_if[i]];
-                if (c->dst_if[i] != c->src_if[i]) ++per_if[c->dst_if[i]];
+            for (uint64_t i = 0; i < n; i += step) {
+                per_if[c->src_if[i]] += step;
+                if (c->dst_if[i] != c->src_if[i]) per_if[c->dst_if[i]] += step;
             }
             for (size_t f = 0; f < e->if_acl.size(); ++f) {
                 if (ifs[f].in >= 0) touch[ifs[f].in] += per_if[f];
