@@ -277,3 +277,25 @@ def test_generate_rules_keyed_equals_scan(seed):
     finally:
         C._RuleList = orig
     assert len(fast) == len(slow) and all(a.compare(b) == 0 for a, b in zip(fast, slow))
+
+
+def test_gen_policy_small_translation_matches_literal():
+    """gen-policy.py shape at 3 blocks: the GPU renderer's translation (on the
+    C evalACL oracle) equals the literal TestTraffic oracle packet by packet."""
+    from configurator_replay import gen_policy_packets
+    rng = random.Random(3)
+    pol = C.gen_policy(rng, num_cidrs=3, num_ports=4)
+    pod = PodID("db", "default")
+    conf = C.PolicyConfigurator({pod: "10.1.1.1"})
+    r = T.TrafficRenderer("gen", EvalAclEngine())
+    conf.register_renderer(r)
+    conf.new_txn(False).configure(pod, [pol]).commit()
+    src, dst, proto, dport, s16, d16 = gen_policy_packets(rng, 400, 3)
+    ports = [p.number for m in pol.matches for p in m.ports]
+    dport = [rng.choice(ports) if rng.random() < 0.5 else p for p in dport]
+    sport = [1000] * len(src)
+    for d in (T.INGRESS_TRAFFIC, T.EGRESS_TRAFFIC):
+        rules = r.config[pod].ingress if d == T.INGRESS_TRAFFIC else r.config[pod].egress
+        want, want_c, want_u = otraffic.test_traffic_batch(rules, src, dst, proto, sport, dport)
+        v, c, u = r.test_traffic_batch(pod, d, s16, d16, np.array(proto, np.uint8), np.array(dport, np.uint16))
+        assert list(v) == want and [int(x) for x in c] == want_c and u == want_u

@@ -78,3 +78,40 @@ def test_random_policy_sets_on_gpu(eng, seed):
     finally:
         r.close()
     assert checked >= 8
+
+
+@pytest.mark.parametrize("num_cidrs", [20, 60])
+def test_gen_policy_scale_on_gpu(eng, num_cidrs):
+    """gen-policy.py's NetworkPolicy (1 policy, num_cidrs blocks x 5 excepts,
+    20 ports per direction) through the configurator: ~10k-30k rules per
+    list, compiled onto the classifier.  The expectation comes from the C
+    evalACL oracle over the same translation, which test_traffic_cpu.py pins
+    to the literal TestTraffic oracle."""
+    import oracle
+    from configurator_replay import gen_policy_packets
+    from vpp_amd.renderer.api import PodID
+    rng = random.Random(num_cidrs)
+    pol = C.gen_policy(rng, num_cidrs=num_cidrs)
+    pod = PodID("db", "default")
+    conf = C.PolicyConfigurator({pod: "10.1.1.1"})
+    r = T.TrafficRenderer("gen", eng)
+    conf.register_renderer(r)
+    conf.new_txn(False).configure(pod, [pol]).commit()
+    try:
+        # give a share of packets the policy's ports so PERMITs are exercised
+        src, dst, proto, dport, s16, d16 = gen_policy_packets(rng, 8000, num_cidrs)
+        ports = [p.number for m in pol.matches for p in m.ports]
+        dport = [rng.choice(ports) if rng.random() < 0.5 else p for p in dport]
+        p8, dp16 = np.array(proto, np.uint8), np.array(dport, np.uint16)
+        for d in (T.INGRESS_TRAFFIC, T.EGRESS_TRAFFIC):
+            rules = r.config[pod].ingress if d == T.INGRESS_TRAFFIC else r.config[pod].egress
+            assert len(rules) > 400 * num_cidrs
+            cr = oracle.rules_to_c(T.compile_rules(rules))
+            want_v, want_c = oracle.classify_faithful(cr, s16, d16, dp16, p8, af=16)
+            v, c, u = r.test_traffic_batch(pod, d, s16, d16, p8, dp16)
+            assert np.array_equal(v, want_v), d
+            per_rule, unmatched = T.rule_counters(want_c, len(rules))
+            assert np.array_equal(np.asarray(c), np.asarray(per_rule)) and u == unmatched
+            assert len(set(want_v.tolist())) >= 2
+    finally:
+        r.close()

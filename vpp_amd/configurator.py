@@ -318,3 +318,39 @@ class PolicyConfiguratorTxn:
         if has_policy and not all_allowed:                # :457-476 deny the rest
             _append_rules(rules, _rule(ACTION_DENY, R_TCP), _rule(ACTION_DENY, R_UDP))
         return list(rules)
+
+
+def gen_policy(rng, num_cidrs: int = 1000, num_excepts: int = 5, num_ports: int = 20,
+               name: str = "test-network-policy", namespace: str = "default") -> ContivPolicy:
+    """The NetworkPolicy of tests/policy/perf/gen-policy.py (:8-65) as the
+    ContivPolicy the policy processor would hand the configurator: ingress
+    from and egress to ``num_cidrs`` IP blocks (block i inside (i + 256) << 16,
+    /16-/24) with ``num_excepts`` excepts each (/24-/32 inside the block), and
+    ``num_ports`` random TCP/UDP ports per direction.  ``rng``: random.Random."""
+
+    def mask(a, ln):
+        return a & (0xFFFFFFFF ^ ((1 << (32 - ln)) - 1))
+
+    def net(a, ln):
+        return IPNet(a.to_bytes(4, "big"), gonet.cidr_mask(ln, 32))
+
+    def blocks():
+        out = []
+        for i in range(num_cidrs):
+            prefix = (i + 0x100) << 16
+            ln = rng.randint(16, 24)
+            cidr = mask(rng.randint(prefix, prefix | 0xFFFF), ln)
+            excepts = []
+            for _ in range(num_excepts):
+                e = rng.randint(cidr, cidr | ((1 << (32 - ln)) - 1))
+                eln = rng.randint(24, 32)
+                excepts.append(net(mask(e, eln), eln))
+            out.append(IPBlock(net(cidr, ln), excepts))
+        return out
+
+    def ports():
+        return [Port(TCP if rng.randint(0, 1) == 0 else UDP, rng.randint(0, 65535)) for _ in range(num_ports)]
+
+    ingress = Match(MATCH_INGRESS, ip_blocks=blocks(), ports=ports())
+    egress = Match(MATCH_EGRESS, ip_blocks=blocks(), ports=ports())
+    return ContivPolicy(PolicyID(name, namespace), POLICY_ALL, [ingress, egress])
