@@ -421,9 +421,23 @@ __device__ __forceinline__ void run_n(const Img<kLds>& im, const Cls4Dev& t, uin
             addr[q] = slot[q] < t.n_hot ? hot_lane + slot[q] * 256u : t.img_bytes + slot[q] * 4u;
             if constexpr (CLS_ABLATE & 1) asm volatile("" :: "v"(addr[q]));
             else __hip_atomic_fetch_add(lctr_t(addr[q]), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        } else if (pr[q] <= 2u) {
-            if (slot[q] == 0u) ++hot0;
-            else atomicAdd(&gslot[slot[q]], 1ull);
+        } else {
+            // Global counters: lanes holding the same slot are summed across
+            // the wave first (ballot per distinct slot, one atomic by the
+            // lowest lane), so a hot slot costs one atomic per wave, not 64.
+            uint32_t key = pr[q] <= 2u ? slot[q] : 0xFFFFFFFFu;
+            if (key == 0u) {
+                ++hot0;
+                key = 0xFFFFFFFFu;
+            }
+            unsigned long long pending = __ballot(key != 0xFFFFFFFFu);
+            while (pending) {
+                const int leader = __builtin_ctzll(pending);
+                const uint32_t sk = __shfl(key, leader);
+                const unsigned long long same = __ballot(key == sk);
+                if (int(__lane_id()) == leader) atomicAdd(&gslot[sk], (unsigned long long)__popcll(same));
+                pending &= ~same;
+            }
         }
     }
     // Protocols outside TCP/UDP/ICMP fall through evalACL's switch
