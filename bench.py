@@ -9,8 +9,15 @@ classify pass over the batch (verdict per packet + per-rule hit counters),
 plus, at N>1 GPUs, the RCCL all-reduce of the hit counters (the only
 collective: packets shard across ranks, the table is replicated).
 
+Config 4 (--config 4): the config 3 table over a fixed 2 Gi-packet batch,
+sharded contiguously over the ranks (strong scaling, 2 Gi / N per GPU).  The
+default run is weak: 256 Mi packets per GPU, so N = 8 classifies config 4's
+2 Gi packets.
+
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
-N>1 is launched by torch.distributed.run, one rank per GPU.
+N>1: one rank per GPU.  Under torch.distributed.run (WORLD_SIZE set) the
+ranks run directly; otherwise bench.py starts torch.distributed.run itself as
+a child process, before anything touches the GPU, and exits with its status.
 """
 from __future__ import annotations
 
@@ -35,19 +42,51 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", type=int, default=3, choices=[2, 3, 5])
+    ap.add_argument("--config", type=int, default=3, choices=[2, 3, 4, 5])
     ap.add_argument("--packets", type=int, default=0, help="packets per GPU (default: config's)")
     ap.add_argument("--cpu-sample", type=int, default=1 << 21,
                     help="packets timed on the host for the CPU baseline (0: skip)")
     ap.add_argument("--faithful-sample", type=int, default=4096)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (default: all host cores)")
+    ap.add_argument("--no-stream-floor", action="store_true", help="skip the live stream-floor measurement")
     return ap.parse_args()
 
 
-def cpu_baseline(acl, spec, sample: int, faithful_sample: int):
-    """Oracle CPU port on the host cores (OpenMP), and the faithful Go-style
-    evaluator (string re-parse per rule, one thread) on a smaller prefix."""
+def launch_ranks(args) -> int:
+    """--gpus N > 1 without a launcher: run torch.distributed.run as a child
+    (this process has not touched the GPU) and return its exit status."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=%d" % args.gpus,
+           "--master-addr=127.0.0.1", "--master-port=%d" % port, os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd).returncode
+
+
+def host_cpu():
+    """(logical cores, model name) of the host (lscpu's 'Model name')."""
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return os.cpu_count() or 1, model
+
+
+def cpu_baseline(acl, spec, sample: int, faithful_sample: int, threads: int = 0):
+    """Oracle CPU port on the host cores (OpenMP, every logical core unless
+    --cpu-threads says otherwise), and the faithful Go-style evaluator (string
+    re-parse per rule, one thread) on a smaller prefix."""
     import oracle
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    nproc, model = host_cpu()
+    threads = threads or nproc
     af = spec.get("layout", 4)
     tr = (oracle.gen_traffic_v16 if af == 16 else oracle.gen_traffic_v4)(spec, 0, sample)
     cr = oracle.rules_to_c(acl.rules)
@@ -58,6 +97,7 @@ def cpu_baseline(acl, spec, sample: int, faithful_sample: int):
     ft.classify(tr["src"], tr["dst"], tr["dport"], tr["proto"], af=af, nthreads=threads)
     dt = time.perf_counter() - t0
     out = {"value": round(sample / dt / 1e6, 4), "unit": "Mpps", "cores": threads, "kind": "port",
+           "nproc": nproc, "cpu_model": model,
            "sample": "%d packets of the same config stream (oracle/aclengine_ref.c orc_classify_fast, "
                      "rules pre-parsed, OpenMP %d threads), %.1f s" % (sample, threads, dt)}
     if faithful_sample:
@@ -74,33 +114,55 @@ def cpu_baseline(acl, spec, sample: int, faithful_sample: int):
 
 def pmc_traffic(cfg: int, n: int):
     """Per-launch HBM bytes of the classify kernel from the committed rocprofv3
-    PMC summary (profiles/pmc_*.json, written by tools/pmc_traffic.py)."""
+    PMC summary (profiles/pmc_*.json, written by tools/pmc_traffic.py on the
+    GPU box).  Only a summary measured on the current kernel sources counts:
+    each records the hash of vpp_amd/csrc, and a stale one is dropped.
+    Returns (bytes or None, source note)."""
     import glob
-    best = None
+    from vpp_amd._abi import source_hash
+    h = source_hash()
+    best, stale = None, None
     for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json"))):
         try:
             d = json.load(open(p))
         except Exception:
             continue
         if d.get("config") == cfg and d.get("packets") == n:
-            best = d
-    return None if best is None else best.get("hbm_bytes_per_launch")
+            if d.get("source_hash") == h:
+                best = (d, os.path.relpath(p, ROOT))
+            else:
+                stale = os.path.relpath(p, ROOT)
+    if best is None:
+        return None, ("no PMC summary for these kernel sources (stale: %s)" % stale) if stale else "not measured"
+    d, p = best
+    return d.get("hbm_bytes_per_launch"), "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, %s" % p
 
 
 def main():
     args = parse()
+    rank, world, local = (int(os.environ.get(k, d)) for k, d in
+                          (("RANK", "0"), ("WORLD_SIZE", "1"), ("LOCAL_RANK", "0")))
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))          # nothing has touched the GPU in this process
+    if world != args.gpus:
+        sys.exit("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
     import torch
     import torch.distributed as dist
 
     from vpp_amd import dist as D
     from vpp_amd import workload
-    rank, world, local = D.world()
     D.init("nccl")
-    torch.cuda.set_device(local if world > 1 else 0)
+    torch.cuda.set_device(D.device_index(local))
     from vpp_amd.engine import Engine
 
     acl, spec, n_default = workload.config(args.config)
-    n = args.packets or n_default
+    strong = args.config == 4
+    if args.packets:
+        n = args.packets
+    elif strong:
+        n = -(-n_default // world)            # config 4: the fixed batch over the ranks
+    else:
+        n = n_default
     eng = Engine(torch.cuda.current_device())
     table = eng.put_table("contiv/vpp-policy-GLOBAL", acl.rules)
     info = table.info()
@@ -117,11 +179,19 @@ def main():
     verdict = torch.empty(n, dtype=torch.uint8, device=dev)
     counters = torch.zeros(R + 1, dtype=torch.int64, device=dev)
     torch.cuda.synchronize()
+    ev = []                                   # (before, after) the counter all-reduce, per timed step
 
     def step(timing):
         eng.classify(table, pk["src"], pk["dst"], pk["dport"], pk["proto"], verdict=verdict,
                      counters=counters, timing=timing)
-        D.merge_counters(counters)         # RCCL over xGMI: merge per-rule hit counters
+        if world > 1:
+            if timing:
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record()
+            D.merge_counters(counters)     # RCCL over xGMI: merge per-rule hit counters
+            if timing:
+                b.record()
+                ev.append((a, b))
 
     for _ in range(args.warmup):
         step(False)
@@ -138,18 +208,32 @@ def main():
         dist.barrier()
     wall = time.perf_counter() - t0
     kms = eng.kernel_times(reset=True)
-    wall = D.max_over_ranks(wall, dev)
+    avg_k = float(np.mean(kms)) if kms else float("nan")
+    ar_ms = float(np.mean([a.elapsed_time(b) for a, b in ev])) if ev else 0.0
+    floor_ms = None
+    if not args.no_stream_floor:
+        floor_ms = eng.stream_floor(pk["src"], pk["dst"], pk["dport"], pk["proto"], verdict)
+    wall, k_max, ar_max = D.max_over_ranks([wall, avg_k, ar_ms], dev)
+    if floor_ms is not None:
+        floor_ms = D.max_over_ranks(floor_ms, dev)
 
     if rank == 0:
         total = n * world * args.steps
         mpps = total / wall / 1e6
-        avg_k = float(np.mean(kms)) if kms else float("nan")
         alg_bytes = n * BYTES_PER_PKT[af] + (R + 1) * 8
         achieved = alg_bytes / (avg_k / 1e3) / 1e9
-        traffic = pmc_traffic(args.config, n)
+        traffic, traffic_src = pmc_traffic(args.config, n)
         cpu = None
         if world == 1 and args.cpu_sample:
-            cpu = cpu_baseline(acl, spec, args.cpu_sample, args.faithful_sample)
+            cpu = cpu_baseline(acl, spec, args.cpu_sample, args.faithful_sample, args.cpu_threads)
+        if af == 4:
+            wl = "config%d: %d-rule global ACL (%d pods), %d IPv4 TCP/UDP packets per GPU" % (
+                args.config, R, len(spec["pod_ips"]), n)
+            if strong:
+                wl += " (%d-packet batch sharded over %d GPU%s)" % (n * world, world, "s" if world > 1 else "")
+        else:
+            wl = ("config%d: %d-rule global ACL (%d pods, half IPv6, dst port ranges), %d mixed IPv4/IPv6 "
+                  "packets per GPU (10%% ICMP)" % (args.config, R, len(spec["pod_ips"]), n))
         line = {
             "metric": "Mpps classified at 10k ACL rules, 1/8 GPU; % of HBM roofline",
             "value": round(mpps, 2),
@@ -159,26 +243,28 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(wall / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
             "dtype": "u32",
             "data": "synthetic (splitmix64 stream generated in HBM, seed %#x; rules rendered from a "
                     "synthetic 1000-pod policy set)" % spec["seed"],
-            "config": {"workload": ("config%d: %d-rule global ACL (%d pods), %d IPv4 TCP/UDP packets per GPU"
-                                    % (args.config, R, len(spec["pod_ips"]), n)) if af == 4 else
-                                   ("config%d: %d-rule global ACL (%d pods, half IPv6, dst port ranges), %d "
-                                    "mixed IPv4/IPv6 packets per GPU (10%% ICMP)" % (args.config, R,
-                                                                                   len(spec["pod_ips"]), n)),
+            "config": {"workload": wl,
                        "rules": R, "packets_per_gpu": n,
                        "layout": "IPv4 SoA, 12 B/packet" if af == 4 else "16-byte address SoA, 36 B/packet",
                        "kernel": "classifier" if info["kernel"] == 1 else "linear",
                        "lds_bytes": info["lds_bytes"] if af == 4 else info["lds_bytes_v16"],
                        "lds_resident": info["lds_resident"] if af == 4 else info["lds_resident_v16"],
-                       "parallelism": "dp%d" % world},
+                       "parallelism": "dp%d" % world,
+                       "collective": ("counter all-reduce, %s, %d B" % (D.backend(), (R + 1) * 8))
+                       if world > 1 else None},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                         "traffic": traffic,
+                         "traffic": traffic, "traffic_source": traffic_src,
                          "kernel_ms_avg": round(avg_k, 4),
+                         "kernel_ms_avg_max_rank": round(k_max, 4),
+                         "allreduce_ms_avg_max_rank": round(ar_max, 4) if world > 1 else None,
+                         "stream_floor_ms": round(floor_ms, 4) if floor_ms is not None else None,
+                         "frac_of_stream_floor": round(floor_ms / avg_k, 4) if floor_ms else None,
                          "algorithmic_bytes_per_launch": alg_bytes},
             "cpu_baseline": cpu,
         }

@@ -164,7 +164,10 @@ typedef struct cls_table_info {
     uint32_t has_v16;          /* 1 if CLS_AF_V16 batches can be classified */
     uint32_t lds_bytes_v16;    /* LDS image of the 16-byte layout's classifier */
     uint32_t lds_resident_v16;
-    uint32_t reserved[5];
+    uint32_t n_lctr;           /* slots counted in LDS (v4; the rest in global memory) */
+    uint32_t ctr16;            /* the LDS slot counters are u16 (v4) */
+    uint32_t list_mode;        /* candidate-list mode of the v4 classifier (cls_image_v4_header) */
+    uint32_t reserved[2];
 } cls_table_info;
 int cls_table_get_info(cls_engine* e, uint32_t table_id, cls_table_info* info);
 
@@ -175,6 +178,11 @@ int cls_table_get_info(cls_engine* e, uint32_t table_id, cls_table_info* info);
  * `stream` is a hipStream_t (NULL: the engine's own stream).  The call is
  * synchronous with respect to the host unless CLS_F_DEVICE is set, in which
  * case work is only enqueued on `stream`.
+ * Threading: any thread may call; calls are serialised while they enqueue.
+ * Device work of concurrent calls on different streams may overlap, also on
+ * one table: every (table, stream) pair has its own counter scratch.  A
+ * table deleted (cls_table_del, cls_acl_put/del) while device work on it is
+ * pending is freed only after that work finishes.
  */
 int cls_classify(cls_engine* e, uint32_t table_id, const cls_pkt_soa* pkts,
                  uint64_t n, uint8_t* verdict_out, uint64_t* counters_out,
@@ -188,6 +196,14 @@ int cls_last_kernel_ms(cls_engine* e, float* ms);
  * only events (no host synchronisation); reading blocks on the last one. */
 int cls_kernel_times(cls_engine* e, float* ms, uint32_t cap, uint32_t* count);
 int cls_kernel_times_reset(cls_engine* e);
+
+/* Measurement only (bench.py): the classify kernel's HBM stream without the
+ * lookups -- the same loads and stores, order and grid -- over a device batch
+ * (CLS_AF_V4: 16-B aligned addresses, 8-B dport, 4-B proto and verdict;
+ * CLS_AF_V16: 16-B aligned addresses, whole 256-packet steps), `reps` timed
+ * launches after one warm-up; *ms = the average launch.  Writes verdict. */
+int cls_stream_floor(cls_engine* e, const cls_pkt_soa* pkts, uint64_t n, uint8_t* verdict,
+                     uint32_t reps, float* ms, void* stream);
 
 /* ---- ACL configuration (ACLConfig, aclengine_mock.go:110-121,671-728) --- */
 /* PutACL semantics (:699-728): requires >=1 interface; re-putting a name
@@ -299,6 +315,8 @@ typedef struct cls_image_v4_header {
     uint32_t port_mul, port_mask4, port_dflt;  /* list mode 4: e = u32 at byte mulhi(port, mul) &
                                   mask4, class x 4 = (e & 0xFFFF) == port ? e >> 16 : port_dflt */
     uint32_t n_hot, off_hot;   /* per-lane counter rows of the hot slots (LDS offsets) */
+    uint32_t n_lctr;           /* slots counted in LDS (the rest: global counters) */
+    uint32_t ctr16;            /* LDS slot counters are u16 (else u32) */
 } cls_image_v4_header;
 int cls_compile_v4(const cls_rule* rules, uint32_t n_rules, void* blob, uint64_t cap,
                    uint64_t* need);

@@ -147,7 +147,8 @@ def random_packets(rng, cache, n):
 def gen_policy_packets(rng, n, n_blocks=1000):
     """Packets around gen-policy.py's address space: sources and destinations
     inside the block prefixes (i + 256) << 16 (block-, except- and gap-heavy),
-    ports mostly from a small set so some hit the policy's ports."""
+    ports mostly from a small set so some hit the policy's ports; protocols
+    TCP, UDP, ICMP and 47."""
     import numpy as np
     src = []
     dst = []
@@ -155,7 +156,9 @@ def gen_policy_packets(rng, n, n_blocks=1000):
         for out in (src, dst):
             i = rng.randrange(n_blocks + n_blocks // 10 + 1)
             out.append((((i + 0x100) << 16) | rng.randrange(1 << 16)).to_bytes(4, "big"))
-    proto = [rng.randrange(2) for _ in range(n)]
+    # TCP and UDP mostly, some ICMP and a protocol outside ProtocolType (47):
+    # TestTraffic's exact protocol test, evalACL's switch fall-through
+    proto = [rng.choice((0, 0, 0, 1, 1, 1, 2, 47)) for _ in range(n)]
     dport = [rng.randrange(65536) for _ in range(n)]
     rows = lambda ips: np.frombuffer(b"".join(gonet.V4_IN_V6_PREFIX + x for x in ips), np.uint8).reshape(-1, 16)
     return src, dst, proto, dport, rows(src), rows(dst)

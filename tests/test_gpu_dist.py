@@ -1,0 +1,95 @@
+"""N>1 on the GPU: two ranks on the box's GPU, each running the HIP engine on
+its contiguous shard of the config-3 stream; the counters are
+merged with the same vpp_amd.dist code bench.py uses (gloo here: RCCL refuses
+two ranks on one device, and the driver's 8-GPU run uses RCCL).  The merged
+counters and the per-shard verdicts must equal the oracle's over the whole
+stream.  Also: bench.py --gpus 2 launches its own ranks and reports n_gpus 2.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+import textwrap
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+pytestmark = pytest.mark.gpu
+
+WORKER = textwrap.dedent("""
+    import os, sys
+    sys.path[:0] = [%(root)r]
+    import numpy as np, torch
+    import torch.distributed as dist
+    from vpp_amd import dist as D, workload
+    from vpp_amd.engine import Engine
+    D.init("gloo")
+    rank, size, local = D.world()
+    torch.cuda.set_device(D.device_index(local))
+    acl, spec, _ = workload.config(3)
+    eng = Engine(torch.cuda.current_device())
+    t = eng.put_table("g", acl.rules)
+    n = %(n)d
+    first, _ = D.shard(rank, n)
+    pk = {k: torch.empty(n, dtype=dt, device="cuda") for k, dt in
+          (("src", torch.int32), ("dst", torch.int32), ("dport", torch.int16), ("proto", torch.uint8))}
+    eng.gen_traffic_v4(spec, first, pk)
+    v = torch.empty(n, dtype=torch.uint8, device="cuda")
+    c = torch.zeros(t.n_rules + 1, dtype=torch.int64, device="cuda")
+    eng.classify(t, pk["src"], pk["dst"], pk["dport"], pk["proto"], verdict=v, counters=c)
+    D.merge_counters(c)
+    torch.cuda.synchronize()
+    parts = [torch.empty(n, dtype=torch.uint8) for _ in range(size)]
+    dist.all_gather(parts, v.cpu())
+    if rank == 0:
+        np.save(%(out)r + ".c.npy", c.cpu().numpy())
+        np.save(%(out)r + ".v.npy", torch.cat(parts).numpy())
+    eng.close()
+    dist.destroy_process_group()
+""")
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_two_ranks_hip_engine(tmp_path):
+    import oracle
+    from vpp_amd import workload
+    n = 1 << 20
+    out = str(tmp_path / "r")
+    script = tmp_path / "w.py"
+    script.write_text(WORKER % {"root": ROOT, "out": out, "n": n})
+    env = dict(os.environ, VPP_DIST_BACKEND="gloo")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", "--master-port=%d" % _free_port(), str(script)]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    merged, verdict = np.load(out + ".c.npy"), np.load(out + ".v.npy")
+    acl, spec, _ = workload.config(3)
+    tr = oracle.gen_traffic_v4(spec, 0, 2 * n)
+    ov, oc = oracle.classify_fast(oracle.rules_to_c(acl.rules), tr["src"], tr["dst"], tr["dport"], tr["proto"])
+    np.testing.assert_array_equal(verdict, ov)
+    np.testing.assert_array_equal(merged, oc.astype(np.int64))
+    assert merged.sum() == 2 * n
+
+
+def test_bench_launches_its_ranks():
+    env = dict(os.environ, VPP_DIST_BACKEND="gloo")
+    env.pop("WORLD_SIZE", None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+           "--packets", str(1 << 22), "--cpu-sample", "0", "--no-stream-floor"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    line = lines[0]
+    assert line["n_gpus"] == 2 and line["scaling"] == "weak"
+    assert line["config"]["packets_per_gpu"] == 1 << 22
+    assert line["roofline"]["allreduce_ms_avg_max_rank"] is not None

@@ -8,11 +8,25 @@ missing -- there is no CPU fallback in the product.
 from __future__ import annotations
 
 import ctypes as C
+import hashlib
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # CONTIVCLS_LIB: diagnostics only (A/B timing of kernel build variants)
 LIB_PATH = os.environ.get("CONTIVCLS_LIB") or os.path.join(_HERE, "libcontivcls.so")
+
+SOURCES = ("kernels.hip", "kernels.hpp", "compile.cpp", "compile.hpp", "engine.cpp", "goparse.hpp")
+
+
+def source_hash() -> str:
+    """Hash of the native sources (vpp_amd/csrc): ties a committed profile
+    (profiles/pmc_*.json) to the kernels it measured."""
+    h = hashlib.sha256()
+    for f in SOURCES:
+        with open(os.path.join(_HERE, "csrc", f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
 
 # status codes
 OK, E_INVAL, E_NOMEM, E_HIP, E_RCCL, E_NOTFOUND, E_NODEV = 0, -1, -2, -3, -4, -5, -6
@@ -31,7 +45,7 @@ SYMBOLS = ["cls_abi_version", "cls_engine_create", "cls_engine_destroy", "cls_la
            "cls_last_kernel_ms", "cls_kernel_times", "cls_kernel_times_reset", "cls_acl_put", "cls_acl_del", "cls_acl_table", "cls_acl_counts",
            "cls_if_id",
            "cls_if_acls", "cls_connect_batch", "cls_gen_traffic_v4", "cls_compile_v4",
-           "cls_compile_v16", "cls_gen_traffic_v16"]
+           "cls_compile_v16", "cls_gen_traffic_v16", "cls_stream_floor"]
 
 
 class ClsRule(C.Structure):
@@ -64,7 +78,8 @@ class TableInfo(C.Structure):
                 ("n_intervals", C.c_uint32), ("n_classes", C.c_uint32),
                 ("n_templates", C.c_uint32), ("n_slots", C.c_uint32),
                 ("lds_resident", C.c_uint32), ("has_v16", C.c_uint32), ("lds_bytes_v16", C.c_uint32),
-                ("lds_resident_v16", C.c_uint32), ("reserved", C.c_uint32 * 5)]
+                ("lds_resident_v16", C.c_uint32), ("n_lctr", C.c_uint32), ("ctr16", C.c_uint32),
+                ("list_mode", C.c_uint32), ("reserved", C.c_uint32 * 2)]
 
 
 class TrafficSpec(C.Structure):
@@ -96,7 +111,7 @@ class ImageHeader(C.Structure):
         ("bv_wide", C.c_uint32), ("row_bytes", C.c_uint32), ("default_row", C.c_uint32),
         ("hash_mul", C.c_uint32 * 3), ("port_mul", C.c_uint32), ("port_mask4", C.c_uint32),
         ("port_dflt", C.c_uint32),
-        ("n_hot", C.c_uint32), ("off_hot", C.c_uint32)]
+        ("n_hot", C.c_uint32), ("off_hot", C.c_uint32), ("n_lctr", C.c_uint32), ("ctr16", C.c_uint32)]
 
 
 class Image16Header(C.Structure):
@@ -143,6 +158,7 @@ def lib():
         "cls_last_kernel_ms": (C.c_int, [vp, C.POINTER(C.c_float)]),
         "cls_kernel_times": (C.c_int, [vp, C.POINTER(C.c_float), u32, C.POINTER(u32)]),
         "cls_kernel_times_reset": (C.c_int, [vp]),
+        "cls_stream_floor": (C.c_int, [vp, C.POINTER(PktSoa), u64, vp, u32, C.POINTER(C.c_float), vp]),
         "cls_acl_put": (C.c_int, [vp, C.c_char_p, C.POINTER(ClsRule), u32,
                                   C.POINTER(C.c_char_p), u32, C.POINTER(C.c_char_p), u32]),
         "cls_acl_del": (C.c_int, [vp, C.c_char_p]),

@@ -495,6 +495,45 @@ uint32_t Cls4Image::row_of(uint32_t addr) const {
     return off_cells + uint32_t(h_iclass[k]) * row_bytes;
 }
 
+// LDS of one classify workgroup available to the image and its counters
+// (CONTIVCLS_LDS_BUDGET: diagnostics and tests, to exercise the counter tiers
+// with small tables).
+uint32_t lds_budget() {
+    if (const char* b = std::getenv("CONTIVCLS_LDS_BUDGET"))
+        return std::min<uint32_t>(kLdsBudget, uint32_t(std::strtoul(b, nullptr, 0)));
+    return kLdsBudget;
+}
+
+// Counter tiers of a serialised image (compile.hpp Cls4Image): per-lane u32
+// rows for the hot slots, then u32 LDS counters for every slot when they fit,
+// else u16 LDS counters (overflow carried to the global slot counters), and
+// with `partial` only the first n_lctr slots in LDS, the rest counted in
+// global memory.  Returns whether the image is LDS-resident.
+bool place_counters(Cls4Image& img, uint32_t budget, bool partial) {
+    const uint32_t hot = img.n_hot * 64u * 4u;
+    const uint32_t c32 = (img.n_ctr * 4u + 15u) & ~15u, c16 = (img.n_ctr * 2u + 15u) & ~15u;
+    uint32_t region = c32;
+    bool ok = true;
+    img.ctr16 = 0;
+    img.n_lctr = img.n_ctr;
+    if (uint64_t(img.img_bytes) + c32 + hot <= budget) {
+    } else if (uint64_t(img.img_bytes) + c16 + hot <= budget) {
+        img.ctr16 = 1;
+        region = c16;
+    } else if (partial && uint64_t(img.img_bytes) + hot + ((img.n_hot * 2u + 15u) & ~15u) <= budget) {
+        // at least the hot slots: their totals go through these slots' rows
+        img.ctr16 = 1;
+        img.n_lctr = std::min(img.n_ctr, ((budget - img.img_bytes - hot) / 2u) & ~7u);
+        region = (img.n_lctr * 2u + 15u) & ~15u;
+    } else {
+        ok = false;
+    }
+    img.off_hot = img.img_bytes + region;
+    img.lds_bytes = img.off_hot + hot;
+    img.lds_ok = ok;
+    return ok;
+}
+
 bool build_cls4(const std::vector<SemRule>& sem, uint32_t n_rules, Cls4Image& img,
                 std::string& why, const Cls4Opts* opt) {
     img = Cls4Image();
@@ -1062,19 +1101,48 @@ bool build_cls4(const std::vector<SemRule>& sem, uint32_t n_rules, Cls4Image& im
         img.n_list_entries = uint32_t(lists.size());
         img.n_ctr = uint32_t(img.ctr_rule.size());
         img.search_top = top;
-        img.off_hot = img.img_bytes + ((img.n_ctr * 4 + 15u) & ~15u);
-        img.lds_bytes = img.off_hot + img.n_hot * 64u * 4u;
     };
+    // The fastest list mode whose image and counters fit the workgroup's LDS:
+    // first with every slot counted in LDS (u32, else u16), then with the
+    // image resident and the coldest slots counted in global memory (Cls4Image
+    // counter tiers).  With neither, the image stays in global memory (list
+    // mode 1 when possible: its cells need no list scan).
     const bool dbg = std::getenv("CONTIVCLS_DEBUG_MODES") != nullptr;   // diagnostics
-    for (;;) {
-        serialise(lmode);
-        if (dbg) std::fprintf(stderr, "list mode %u: lds %u img %u ctr %u\n", lmode, img.lds_bytes, img.img_bytes, img.n_ctr);
-        if (lmode == 0) break;
-        // block offset field: 16 bits in 8-B units (modes 1, 2); mode 3: the
-        // pointer tables in the first 64 KiB, sublist slots below 2^16
-        const bool cell_ok = lmode >= 3 ? img.sub_bytes <= 0x10000u : img.img_bytes / 8u <= 0xFFFFu;
-        if (cell_ok && (lmode == 1 || img.lds_bytes <= kLdsBudget)) break;
-        lmode = lmode >= 3 ? 2u : (lmode == 2 && std::max(Sd, Sp) <= kMaxBvSteps) ? 1u : 0u;
+    const uint32_t budget = lds_budget();
+    std::vector<uint32_t> seq;
+    for (uint32_t lm = lmode;;) {
+        seq.push_back(lm);
+        if (lm == 0) break;
+        lm = lm >= 3 ? 2u : (lm == 2 && std::max(Sd, Sp) <= kMaxBvSteps) ? 1u : 0u;
+    }
+    // diagnostics / tests: exactly this list mode when it is available
+    // (CONTIVCLS_LIST_MODE), so a test's LDS budget picks the counter tier
+    if (const char* f = std::getenv("CONTIVCLS_LIST_MODE")) {
+        const uint32_t lm = uint32_t(std::strtoul(f, nullptr, 0));
+        if (std::find(seq.begin(), seq.end(), lm) != seq.end()) seq.assign(1, lm);
+    }
+    // block offset field: 16 bits in 8-B units (modes 1, 2); mode 3: the
+    // pointer tables in the first 64 KiB, sublist slots below 2^16
+    auto cell_ok = [&](uint32_t lm) {
+        return lm == 0 || (lm >= 3 ? img.sub_bytes <= 0x10000u : img.img_bytes / 8u <= 0xFFFFu);
+    };
+    for (int partial = 0; partial < 2; ++partial)
+        for (uint32_t lm : seq) {
+            serialise(lm);
+            const bool ok = cell_ok(lm) && place_counters(img, budget, partial != 0);
+            if (dbg)
+                std::fprintf(stderr, "list mode %u%s: lds %u img %u ctr %u lctr %u ctr16 %u -> %s\n", lm,
+                             partial ? " (partial)" : "", img.lds_bytes, img.img_bytes, img.n_ctr, img.n_lctr,
+                             img.ctr16, ok ? "resident" : "no");
+            if (ok) return true;
+        }
+    for (uint32_t lm : seq) {
+        if (lm > 1 && lm != seq.back()) continue;
+        serialise(lm);
+        if (!cell_ok(lm)) continue;
+        place_counters(img, budget, false);
+        if (dbg) std::fprintf(stderr, "list mode %u: global image\n", lm);
+        return true;
     }
     return true;
 }

@@ -140,6 +140,13 @@ struct Cls4Image {
     // (n_hot x 64 u32 at off_hot, after the slot counters)
     uint32_t n_hot = 1;
     uint32_t off_hot = 0;
+    // Counter tiers: slots [n_hot, n_lctr) are LDS counters after the image,
+    // u32 (ctr16 = 0) or u16 (ctr16 = 1: a lane whose add takes a counter to
+    // 0x8000 moves 0x8000 to the slot's global counter); slots [n_lctr,
+    // n_ctr) are counted in global memory (wave-aggregated atomics).
+    uint32_t n_lctr = 0;
+    uint32_t ctr16 = 0;
+    bool lds_ok = false;           // image and LDS counters fit the LDS budget (place_counters)
     uint32_t off_tail = 0;         // Cls4Opts::tail words (read-only, after the sections above)
     // host only: the elementary source intervals and their classes
     std::vector<uint32_t> h_bounds;
@@ -152,6 +159,9 @@ struct Cls4Opts {
     int64_t hot_addr = -1;         // the hot class is this address's (default: the widest)
     bool ext_src = false;          // no source lookup sections (mode 3: the caller finds rows)
 };
+
+uint32_t lds_budget();
+bool place_counters(Cls4Image& img, uint32_t budget, bool partial);
 
 // Build the image; returns false (with reason) if the table does not fit the
 // 16-bit list / template indices.

@@ -41,6 +41,33 @@ struct DevBuf {
     template <typename T> T* as() const { return static_cast<T*>(p); }
 };
 
+// Counter scratch of one (table variant, stream): concurrent classifies of
+// one table on different streams never share a counter buffer
+// (include/contivcls.h, threading).  slot_val is all zero between calls: the
+// remap kernel reads and clears it.
+struct Scratch {
+    DevBuf part;                   // per-workgroup LDS counter rows [rows][n_lctr]
+    DevBuf slot_val;               // u64 per slot: global-tier counters, folded partials
+    DevBuf out;                    // u64 rule counters when the caller gives none on device
+    hipEvent_t done = nullptr;     // recorded after the call's last kernel
+};
+
+// Slot counters of one classifier image (or of the linear kernel alone):
+// slots [0, n_ctr) of the image, then R + 1 direct rule slots.
+struct Counters {
+    uint32_t n_slots = 0;
+    uint32_t n_lctr = 0;           // slots counted in LDS (their partial rows)
+    DevBuf d_csr;                  // uint2 {slot, rule}, grouped by rule
+    std::map<hipStream_t, std::unique_ptr<Scratch>> sc;
+    ~Counters() {
+        for (auto& kv : sc)
+            if (kv.second->done) {
+                (void)hipEventSynchronize(kv.second->done);   // device work may still read the buffers
+                (void)hipEventDestroy(kv.second->done);
+            }
+    }
+};
+
 struct Table {
     std::string name;
     uint32_t n_rules = 0;
@@ -51,10 +78,6 @@ struct Table {
     bool has_cls = false;
     Cls4Image img;
     DevBuf d_img;
-    // counters: slots [0, n_ctr) of the classifier + [n_ctr, n_ctr + R + 1) direct rule slots
-    uint32_t n_slots = 0;
-    DevBuf d_slot, d_map, d_out;
-    DevBuf d_part;                 // per-workgroup slot counters of the LDS-resident kernel
     int kernel = 0;            // 0 linear, 1 classifier
     bool lds_resident = false;
     // 16-byte layout (IPv6 / IPv4-mapped): classifier over 32-bit reps
@@ -63,11 +86,13 @@ struct Table {
         std::string why;           // why there is none
         Cls16Image img;
         std::vector<LinRule4> lin; // rules in rep space (protocol > 2, FORCE_LINEAR)
-        DevBuf d_img, d_lin, d_slot, d_map, d_part;
+        DevBuf d_img, d_lin;
         DevBuf d_src_search;       // src_mode 1: the source interval table (global memory)
-        uint32_t n_slots = 0;
         bool lds_resident = false;
     } p16;
+    // declared last: destroyed first, so pending device work is waited for
+    // before any of the buffers above are freed
+    Counters c4, c16;
 };
 
 struct AclEntry {
@@ -165,6 +190,30 @@ void cls_engine_destroy(cls_engine* e) {
 const char* cls_last_error(const cls_engine* e) { return e ? e->err.c_str() : "null engine"; }
 
 // ---------------------------------------------------------------------------
+// The slot -> rule map of a table variant as the remap kernel reads it: every
+// slot once, grouped by rule (slot order within a rule).
+static int counters_init(cls_engine* e, Counters& c, const Cls4Image* img, uint32_t n_rules) {
+    const uint32_t n_cls = img ? img->n_ctr : 0;
+    c.n_slots = n_cls + n_rules + 1;
+    c.n_lctr = img ? img->n_lctr : 0;
+    std::vector<uint32_t> cnt(size_t(n_rules) + 2, 0);
+    auto rule_of = [&](uint32_t i) { return i < n_cls ? img->ctr_rule[i] : i - n_cls; };
+    for (uint32_t i = 0; i < c.n_slots; ++i) cnt[rule_of(i) + 1]++;
+    for (size_t r = 1; r < cnt.size(); ++r) cnt[r] += cnt[r - 1];
+    std::vector<uint32_t> csr(size_t(c.n_slots) * 2);
+    for (uint32_t i = 0; i < c.n_slots; ++i) {
+        const uint32_t r = rule_of(i), k = cnt[r]++;
+        csr[2 * size_t(k)] = i;
+        csr[2 * size_t(k) + 1] = r;
+    }
+    HIPC(e, c.d_csr.ensure(csr.size() * 4));
+    HIPC(e, hipMemcpy(c.d_csr.p, csr.data(), csr.size() * 4, hipMemcpyHostToDevice));
+    return CLS_OK;
+}
+
+// The counter scratch of (table variant, stream), created on first use.
+static int scratch_of(cls_engine* e, Counters& c, uint32_t n_rules, hipStream_t s, Scratch** out);
+
 static int table_put_locked(cls_engine* e, const char* name, const cls_rule* rules, uint32_t n,
                             uint32_t* table_id) {
     if (n && !rules) return fail(e, CLS_E_INVAL, "rules is NULL");
@@ -186,20 +235,15 @@ static int table_put_locked(cls_engine* e, const char* name, const cls_rule* rul
         if (build_cls4(sem, n, t->img, why)) {
             t->has_cls = true;
             t->kernel = 1;
-            t->lds_resident = t->img.lds_bytes <= uint32_t(max_lds_bytes());
+            t->lds_resident = t->img.lds_ok && t->img.lds_bytes <= uint32_t(max_lds_bytes());
             HIPC(e, t->d_img.ensure(t->img.img_bytes));
             HIPC(e, hipMemcpy(t->d_img.p, t->img.words.data(), t->img.img_bytes, hipMemcpyHostToDevice));
         }
     }
-    const uint32_t n_cls_slots = t->has_cls ? t->img.n_ctr : 0;
-    t->n_slots = n_cls_slots + n + 1;
-    std::vector<uint32_t> map(t->n_slots);
-    for (uint32_t i = 0; i < n_cls_slots; ++i) map[i] = t->img.ctr_rule[i];
-    for (uint32_t i = 0; i <= n; ++i) map[n_cls_slots + i] = i;
-    HIPC(e, t->d_slot.ensure(size_t(t->n_slots) * 8));
-    HIPC(e, t->d_map.ensure(size_t(t->n_slots) * 4));
-    HIPC(e, t->d_out.ensure(size_t(n + 1) * 8));
-    HIPC(e, hipMemcpy(t->d_map.p, map.data(), map.size() * 4, hipMemcpyHostToDevice));
+    {
+        const int rc2 = counters_init(e, t->c4, t->has_cls ? &t->img : nullptr, n);
+        if (rc2 != CLS_OK) return rc2;
+    }
     // 16-byte layout: both families' reductions over one rep space
     {
         auto& q = t->p16;
@@ -212,19 +256,14 @@ static int table_put_locked(cls_engine* e, const char* name, const cls_rule* rul
         if (q.ok) {
             const Cls4Image& c = q.img.core;
             q.lin = linear4(q.img.sem);
-            q.lds_resident = c.lds_bytes <= uint32_t(max_lds_bytes());
+            q.lds_resident = c.lds_ok && c.lds_bytes <= uint32_t(max_lds_bytes());
             HIPC(e, q.d_img.ensure(c.img_bytes));
             HIPC(e, hipMemcpy(q.d_img.p, c.words.data(), c.img_bytes, hipMemcpyHostToDevice));
             HIPC(e, q.d_lin.ensure(std::max<size_t>(1, q.lin.size()) * sizeof(LinRule4)));
             if (!q.lin.empty())
                 HIPC(e, hipMemcpy(q.d_lin.p, q.lin.data(), q.lin.size() * sizeof(LinRule4), hipMemcpyHostToDevice));
-            q.n_slots = c.n_ctr + n + 1;
-            std::vector<uint32_t> m16(q.n_slots);
-            for (uint32_t i = 0; i < c.n_ctr; ++i) m16[i] = c.ctr_rule[i];
-            for (uint32_t i = 0; i <= n; ++i) m16[c.n_ctr + i] = i;
-            HIPC(e, q.d_slot.ensure(size_t(q.n_slots) * 8));
-            HIPC(e, q.d_map.ensure(size_t(q.n_slots) * 4));
-            HIPC(e, hipMemcpy(q.d_map.p, m16.data(), m16.size() * 4, hipMemcpyHostToDevice));
+            const int rc2 = counters_init(e, t->c16, &c, n);
+            if (rc2 != CLS_OK) return rc2;
             if (q.img.src_mode == 1) {
                 HIPC(e, q.d_src_search.ensure(q.img.src_search.size() * 4));
                 HIPC(e, hipMemcpy(q.d_src_search.p, q.img.src_search.data(), q.img.src_search.size() * 4,
@@ -248,6 +287,7 @@ int cls_table_put(cls_engine* e, const char* name, const cls_rule* rules, uint32
 int cls_table_del(cls_engine* e, uint32_t table_id) {
     if (!e) return CLS_E_INVAL;
     std::lock_guard<std::mutex> g(e->mu);
+    HIPC(e, hipSetDevice(e->device));
     if (!e->tables.erase(table_id)) return fail(e, CLS_E_NOTFOUND, "no table %u", table_id);
     return CLS_OK;
 }
@@ -268,6 +308,9 @@ int cls_table_get_info(cls_engine* e, uint32_t table_id, cls_table_info* info) {
         info->n_templates = t.img.n_tmpl;
         info->n_slots = t.img.n_ctr;
         info->lds_resident = t.lds_resident ? 1 : 0;
+        info->n_lctr = t.img.n_lctr;
+        info->ctr16 = t.img.ctr16;
+        info->list_mode = t.img.list_mode;
     }
     info->has_v16 = t.p16.ok ? 1u : 0u;
     if (t.p16.ok) {
@@ -329,6 +372,8 @@ static Cls4Dev cls4_dev(const Cls4Image& im, const DevBuf& d_img, const DevBuf& 
     cd.off_ptop = im.off_ptop;
     cd.bv_wide = im.bv_wide;
     cd.off_hot = im.off_hot;
+    cd.n_lctr = im.n_lctr;
+    cd.ctr16 = im.ctr16;
     cd.part = nullptr;
     for (uint32_t i = 0; i < kMaxHashLens; ++i) {
         cd.hash_mask[i] = im.hash_mask[i];
@@ -351,30 +396,54 @@ static int cls_grid(const cls_engine* e, bool use_cls, bool lds_resident, uint32
         if (lds_resident)
             per_cu = std::max(1, std::min(by_threads, int(max_lds_bytes() / std::max<uint32_t>(1, lds_bytes))));
         if (const char* w = std::getenv("CONTIVCLS_WG_PER_CU"))   // diagnostics
-            per_cu = std::max(1, std::atoi(w));
+            per_cu = std::max(1, std::min(by_threads, std::atoi(w)));
     }
     const uint64_t want = (n + 4ull * 1024 - 1) / (4ull * 1024);
     return int(std::max<uint64_t>(1, std::min<uint64_t>(uint64_t(e->n_cu) * per_cu, want)));
 }
 
-// slot counters -> rule counters; host batches: copy verdicts and counters back
-static int finish_counts(cls_engine* e, Table& t, DevBuf& d_slot, DevBuf& d_map, uint32_t n_slots, uint64_t n,
-                         uint8_t* verdict_out, const uint8_t* d_verdict, uint64_t* counters_out,
+static int scratch_of(cls_engine* e, Counters& c, uint32_t n_rules, hipStream_t s, Scratch** out) {
+    auto& p = c.sc[s];
+    if (!p) {
+        auto q = std::make_unique<Scratch>();
+        HIPC(e, q->slot_val.ensure(size_t(c.n_slots) * 8));
+        HIPC(e, hipMemsetAsync(q->slot_val.p, 0, size_t(c.n_slots) * 8, s));
+        HIPC(e, q->out.ensure(size_t(n_rules + 1) * 8));
+        // rows for the largest grid (cls_grid): never reallocated under pending work
+        HIPC(e, q->part.ensure(size_t(e->n_cu) * (2048 / cls_block()) * std::max<uint32_t>(1, c.n_lctr) * 4));
+        HIPC(e, hipEventCreateWithFlags(&q->done, hipEventDisableTiming));
+        p = std::move(q);
+    }
+    *out = p.get();
+    return CLS_OK;
+}
+
+// Where a call's rule counters go, and whether they start from zero.
+struct CountOut {
+    unsigned long long* out;       // device rule counters (the caller's or the scratch's)
+    bool zero;                     // cleared by the first fold launch
+};
+static CountOut count_out(Scratch* sc, uint64_t* counters_out, uint32_t flags) {
+    const bool dev = flags & CLS_F_DEVICE;
+    if (dev && counters_out)
+        return {reinterpret_cast<unsigned long long*>(counters_out), !(flags & CLS_F_ACCUMULATE)};
+    return {sc->out.as<unsigned long long>(), true};   // host batches accumulate on the host
+}
+
+// Slot counters -> rule counters (remap, which also clears the slots);
+// host batches: copy verdicts and counters back.
+static int finish_counts(cls_engine* e, const Table& t, const Counters& c, Scratch* sc, const CountOut& co,
+                         uint64_t n, uint8_t* verdict_out, const uint8_t* d_verdict, uint64_t* counters_out,
                          uint32_t flags, hipStream_t s) {
     const bool dev = flags & CLS_F_DEVICE;
-    unsigned long long* out = dev && counters_out ? reinterpret_cast<unsigned long long*>(counters_out)
-                                                  : t.d_out.as<unsigned long long>();
-    if (counters_out || !dev) {
-        if (!(dev && (flags & CLS_F_ACCUMULATE)))
-            HIPC(e, hipMemsetAsync(out, 0, size_t(t.n_rules + 1) * 8, s));
-        HIPC(e, launch_remap(d_slot.as<unsigned long long>(), d_map.as<uint32_t>(), n_slots, out, s));
-    }
+    HIPC(e, launch_remap(sc->slot_val.as<unsigned long long>(), c.d_csr.as<uint2>(), c.n_slots, co.out, s));
+    HIPC(e, hipEventRecord(sc->done, s));
     if (!dev) {
         if (verdict_out && n) HIPC(e, hipMemcpyAsync(verdict_out, d_verdict, n, hipMemcpyDeviceToHost, s));
         std::vector<uint64_t> tmp;
         if (counters_out) {
             tmp.resize(t.n_rules + 1);
-            HIPC(e, hipMemcpyAsync(tmp.data(), out, tmp.size() * 8, hipMemcpyDeviceToHost, s));
+            HIPC(e, hipMemcpyAsync(tmp.data(), co.out, tmp.size() * 8, hipMemcpyDeviceToHost, s));
         }
         HIPC(e, hipStreamSynchronize(s));
         if (counters_out) {
@@ -447,7 +516,13 @@ static int classify16_locked(cls_engine* e, std::shared_ptr<Table> t, const cls_
             d_verdict = e->s_verdict.as<uint8_t>();
         }
     }
-    HIPC(e, hipMemsetAsync(q.d_slot.p, 0, size_t(q.n_slots) * 8, s));
+    Scratch* sc = nullptr;
+    {
+        const int rc = scratch_of(e, t->c16, t->n_rules, s, &sc);
+        if (rc != CLS_OK) return rc;
+    }
+    const CountOut co = count_out(sc, counters_out, flags);
+    unsigned long long* slot_val = sc->slot_val.as<unsigned long long>();
     const Cls4Image& c = q.img.core;
     const bool lin = flags & CLS_F_FORCE_LINEAR;
     LaunchCfg cfg;
@@ -458,12 +533,10 @@ static int classify16_locked(cls_engine* e, std::shared_ptr<Table> t, const cls_
         const int rc = timing_begin(e, s);
         if (rc != CLS_OK) return rc;
     }
+    bool zeroed = false;
     if (n) {
         Cls4Dev cd = cls4_dev(c, q.d_img, q.d_lin, uint32_t(q.lin.size()), t->n_rules);
-        if (q.lds_resident) {
-            HIPC(e, q.d_part.ensure(size_t(cfg.grid) * c.n_ctr * 4));
-            cd.part = q.d_part.as<uint32_t>();
-        }
+        if (q.lds_resident) cd.part = sc->part.as<uint32_t>();
         Fe16 fe = fe16(q.img, q.d_src_search);
         for (uint64_t off = 0; off < n; off += kClsChunk) {
             const uint64_t m = std::min<uint64_t>(kClsChunk, n - off);
@@ -471,18 +544,21 @@ static int classify16_locked(cls_engine* e, std::shared_ptr<Table> t, const cls_
                       dp + off, pr + off, m, 0u};
             uint8_t* vo = d_verdict ? d_verdict + off : nullptr;
             pc.vec = aligned(pc.dport, 8) && aligned(pc.proto, 4) && (!vo || aligned(vo, 4)) ? 1u : 0u;
-            HIPC(e, launch_classify16_cls(cd, fe, pc, vo, q.d_slot.as<unsigned long long>(), q.lds_resident, lin,
-                                          cfg));
+            HIPC(e, launch_classify16_cls(cd, fe, pc, vo, slot_val, q.lds_resident, lin, cfg));
             if (timing && off + m >= n) HIPC(e, hipEventRecord(e->ev1, s));
-            if (q.lds_resident)
-                HIPC(e, launch_fold(cd.part, uint32_t(cfg.grid), c.n_ctr, q.d_slot.as<unsigned long long>(), s));
+            if (q.lds_resident) {
+                HIPC(e, launch_fold(cd.part, uint32_t(cfg.grid), c.n_lctr, slot_val, co.zero && !zeroed ? co.out : nullptr,
+                                    t->n_rules + 1, s));
+                zeroed = true;
+            }
         }
     }
     if (timing) {
         if (!n) HIPC(e, hipEventRecord(e->ev1, s));
         e->timed = true;
     }
-    return finish_counts(e, *t, q.d_slot, q.d_map, q.n_slots, n, verdict_out, d_verdict, counters_out, flags, s);
+    if (co.zero && !zeroed) HIPC(e, launch_fold(nullptr, 0, 0, slot_val, co.out, t->n_rules + 1, s));
+    return finish_counts(e, *t, t->c16, sc, co, n, verdict_out, d_verdict, counters_out, flags, s);
 }
 
 int cls_classify(cls_engine* e, uint32_t table_id, const cls_pkt_soa* pk, uint64_t n,
@@ -521,7 +597,13 @@ int cls_classify(cls_engine* e, uint32_t table_id, const cls_pkt_soa* pk, uint64
             d_verdict = e->s_verdict.as<uint8_t>();
         }
     }
-    HIPC(e, hipMemsetAsync(t->d_slot.p, 0, size_t(t->n_slots) * 8, s));
+    Scratch* sc = nullptr;
+    {
+        const int rc = scratch_of(e, t->c4, t->n_rules, s, &sc);
+        if (rc != CLS_OK) return rc;
+    }
+    const CountOut co = count_out(sc, counters_out, flags);
+    unsigned long long* slot_val = sc->slot_val.as<unsigned long long>();
 
     const bool vec = aligned(p.src, 16) && aligned(p.dst, 16) && aligned(p.dport, 8) &&
                      aligned(p.proto, 4) && (!d_verdict || aligned(d_verdict, 4));
@@ -535,40 +617,73 @@ int cls_classify(cls_engine* e, uint32_t table_id, const cls_pkt_soa* pk, uint64
         const int rc = timing_begin(e, s);
         if (rc != CLS_OK) return rc;
     }
+    bool zeroed = false;
     if (n) {
         if (use_cls) {
             Cls4Dev cd = cls4_dev(t->img, t->d_img, t->d_lin4, uint32_t(t->lin4.size()), t->n_rules);
-            cd.part = nullptr;
-            if (t->lds_resident) {
-                HIPC(e, t->d_part.ensure(size_t(cfg.grid) * t->img.n_ctr * 4));
-                cd.part = t->d_part.as<uint32_t>();
-            }
+            if (t->lds_resident) cd.part = sc->part.as<uint32_t>();
             // the kernel indexes packets with 32-bit offsets: chunks of 2^30
             for (uint64_t off = 0; off < n; off += kClsChunk) {
                 const uint64_t m = std::min<uint64_t>(kClsChunk, n - off);
                 const Pkts4 pc{p.src + off, p.dst + off, p.dport + off, p.proto + off, m};
-                HIPC(e, launch_classify4_cls(cd, pc, d_verdict ? d_verdict + off : nullptr,
-                                             t->d_slot.as<unsigned long long>(), t->lds_resident, vec,
-                                             cfg));
-                if (t->lds_resident && timing && off + m >= n) HIPC(e, hipEventRecord(e->ev1, s));
-                if (t->lds_resident)
-                    HIPC(e, launch_fold(cd.part, uint32_t(cfg.grid), t->img.n_ctr,
-                                        t->d_slot.as<unsigned long long>(), s));
+                HIPC(e, launch_classify4_cls(cd, pc, d_verdict ? d_verdict + off : nullptr, slot_val,
+                                             t->lds_resident, vec, cfg));
+                if (timing && off + m >= n) HIPC(e, hipEventRecord(e->ev1, s));
+                if (t->lds_resident) {
+                    HIPC(e, launch_fold(cd.part, uint32_t(cfg.grid), t->img.n_lctr, slot_val,
+                                        co.zero && !zeroed ? co.out : nullptr, t->n_rules + 1, s));
+                    zeroed = true;
+                }
             }
         } else {
             const uint32_t base = t->has_cls ? t->img.n_ctr : 0;
             HIPC(e, launch_classify4_linear(t->d_lin4.as<LinRule4>(), uint32_t(t->lin4.size()), t->n_rules, p,
-                                            d_verdict, t->d_slot.as<unsigned long long>() + base, cfg));
+                                            d_verdict, slot_val + base, cfg));
         }
     }
     if (timing) {
         // ev1 brackets the classify kernel itself (recorded above, before the
-        // fold of the workgroup partials, when the image is LDS-resident)
-        if (!(n && use_cls && t->lds_resident)) HIPC(e, hipEventRecord(e->ev1, s));
+        // fold of the workgroup partials)
+        if (!(n && use_cls)) HIPC(e, hipEventRecord(e->ev1, s));
         e->timed = true;
     }
-    return finish_counts(e, *t, t->d_slot, t->d_map, t->n_slots, n, verdict_out, d_verdict, counters_out,
-                         flags, s);
+    if (co.zero && !zeroed) HIPC(e, launch_fold(nullptr, 0, 0, slot_val, co.out, t->n_rules + 1, s));
+    return finish_counts(e, *t, t->c4, sc, co, n, verdict_out, d_verdict, counters_out, flags, s);
+}
+
+int cls_stream_floor(cls_engine* e, const cls_pkt_soa* pk, uint64_t n, uint8_t* verdict, uint32_t reps,
+                     float* ms, void* stream) {
+    if (!e || !pk || !ms || !verdict || n == 0 || n > kClsChunk) return CLS_E_INVAL;
+    std::lock_guard<std::mutex> g(e->mu);
+    HIPC(e, hipSetDevice(e->device));
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : e->stream;
+    Pkts4 p4{pk->src4, pk->dst4, pk->dport, pk->proto, n};
+    Pkts16 p16{reinterpret_cast<const uint4*>(pk->src16), reinterpret_cast<const uint4*>(pk->dst16), pk->dport,
+               pk->proto, n, 1u};
+    const bool v4 = pk->af == CLS_AF_V4;
+    if (v4 ? !(aligned(pk->src4, 16) && aligned(pk->dst4, 16) && aligned(pk->dport, 8) && aligned(pk->proto, 4) &&
+               aligned(verdict, 4))
+           : !(pk->af == CLS_AF_V16 && aligned(pk->src16, 16) && aligned(pk->dst16, 16)))
+        return fail(e, CLS_E_INVAL, "stream floor: device arrays of the classify kernel's alignment");
+    const int grid = e->n_cu;                  // one 1024-thread workgroup per CU, as the LDS-resident classify
+    hipEvent_t a, b;
+    HIPC(e, hipEventCreate(&a));
+    HIPC(e, hipEventCreate(&b));
+    int rc = CLS_OK;
+    const uint32_t k = std::max<uint32_t>(1, reps);
+    for (uint32_t i = 0; i <= k && rc == CLS_OK; ++i) {   // launch 0: warm-up
+        if (i == 1 && hipEventRecord(a, s) != hipSuccess) rc = CLS_E_HIP;
+        if (rc == CLS_OK && launch_stream(v4 ? &p4 : nullptr, v4 ? nullptr : &p16, verdict, grid, s) != hipSuccess)
+            rc = fail(e, CLS_E_HIP, "stream floor launch failed");
+    }
+    if (rc == CLS_OK && hipEventRecord(b, s) == hipSuccess && hipEventSynchronize(b) == hipSuccess &&
+        hipEventElapsedTime(ms, a, b) == hipSuccess)
+        *ms /= float(k);
+    else if (rc == CLS_OK)
+        rc = fail(e, CLS_E_HIP, "stream floor timing failed");
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    return rc;
 }
 
 int cls_last_kernel_ms(cls_engine* e, float* ms) {
@@ -614,6 +729,7 @@ static int acl_del_locked(cls_engine* e, const std::string& name) {
     auto it = e->acls.find(name);
     if (it == e->acls.end()) return fail(e, CLS_E_NOTFOUND, "cannot find ACL: %s", name.c_str());
     const int32_t tid = int32_t(it->second.table_id);
+    (void)hipSetDevice(e->device);
     for (auto& b : e->if_acl) {
         if (b.first == tid) b.first = -1;
         if (b.second == tid) b.second = -1;
@@ -796,19 +912,23 @@ int cls_connect_batch(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t*
             LaunchCfg cfg;
             cfg.stream = s;
             cfg.grid = cls_grid(e, true, t.lds_resident, t.img.lds_bytes, n);
-            if (t.lds_resident) {
-                HIPC(e, t.d_part.ensure(size_t(cfg.grid) * t.img.n_ctr * 4));
-                cd.part = t.d_part.as<uint32_t>();
+            Scratch* sc = nullptr;
+            {
+                const int rc = scratch_of(e, t.c4, t.n_rules, s, &sc);
+                if (rc != CLS_OK) return rc;
             }
+            if (t.lds_resident) cd.part = sc->part.as<uint32_t>();
+            unsigned long long* slot_val = sc->slot_val.as<unsigned long long>();
             const Pkts4 syn{src, dst, dp, pr, n}, ack{dst, src, sp, pr, n};
             for (int k = 0; k < 2; ++k) {
                 const Pkts4& q = k ? ack : syn;
                 const bool vec = aligned(q.src, 16) && aligned(q.dst, 16) && aligned(q.dport, 8) &&
                                  aligned(q.proto, 4) && aligned(pre + k * n, 4);
-                // hit counters land in the table's scratch slots (cleared by every classify call)
-                HIPC(e, launch_classify4_cls(cd, q, pre + k * n, t.d_slot.as<unsigned long long>(),
-                                             t.lds_resident, vec, cfg));
+                HIPC(e, launch_classify4_cls(cd, q, pre + k * n, slot_val, t.lds_resident, vec, cfg));
             }
+            // these launches' slot counts are not the connection's: cleared
+            HIPC(e, launch_remap(slot_val, t.c4.d_csr.as<uint2>(), t.c4.n_slots, nullptr, s));
+            HIPC(e, hipEventRecord(sc->done, s));
         }
     }
     HIPC(e, e->s_desc.ensure(desc.size() * sizeof(AclDesc)));
@@ -893,6 +1013,8 @@ static int write_blob(const Cls4Image* img, const std::vector<LinRule4>& lin, ui
         h.default_row = im.default_row;
         h.n_hot = im.n_hot;
         h.off_hot = im.off_hot;
+        h.n_lctr = im.n_lctr;
+        h.ctr16 = im.ctr16;
         for (uint32_t i = 0; i < kMaxHashLens; ++i) {
             h.hash_mask[i] = im.hash_mask[i];
             h.hash_shift[i] = im.hash_shift[i];

@@ -399,9 +399,25 @@ __device__ __forceinline__ void classify_n(const Img<kLds>& im, const Cls4Dev& t
     }
 }
 
+// Global slot counters from a wave: lanes holding the same slot are summed
+// across the wave first (ballot per distinct slot, one atomic by the lowest
+// lane), so a hot slot costs one atomic per wave, not 64.  key ~0u: nothing.
+__device__ __forceinline__ void wave_count(unsigned long long* gslot, uint32_t key) {
+    unsigned long long pending = __ballot(key != 0xFFFFFFFFu);
+    while (pending) {
+        const int leader = __builtin_ctzll(pending);
+        const uint32_t sk = __shfl(key, leader);
+        const unsigned long long same = __ballot(key == sk);
+        if (int(__lane_id()) == leader) atomicAdd(&gslot[sk], (unsigned long long)__popcll(same));
+        pending &= ~same;
+    }
+}
+
 // Classify N packets and count their slots.  pr_any: some packet of the
-// group has a protocol outside TCP/UDP/ICMP.
-template <int N, bool kLds, int kMode, int kList, int kD>
+// group has a protocol outside TCP/UDP/ICMP.  kCtr (LDS-resident image): 0 --
+// every slot has a u32 LDS counter; 1 -- u16 LDS counters for slots <
+// n_lctr (compile.hpp Cls4Image counter tiers), global counters above.
+template <int N, bool kLds, int kMode, int kList, int kD, int kCtr>
 __device__ __forceinline__ void run_n(const Img<kLds>& im, const Cls4Dev& t, uint32_t hot_lane,
                                       unsigned long long* gslot, uint32_t& hot0,
                                       const uint32_t (&s)[N], const uint32_t (&d)[N],
@@ -417,27 +433,43 @@ __device__ __forceinline__ void run_n(const Img<kLds>& im, const Cls4Dev& t, uin
     uint32_t addr[N];
 #pragma unroll
     for (int q = 0; q < N; ++q) {
-        if constexpr (kLds) {
+        if constexpr (kLds && kCtr == 0) {
             addr[q] = slot[q] < t.n_hot ? hot_lane + slot[q] * 256u : t.img_bytes + slot[q] * 4u;
             if constexpr (CLS_ABLATE & 1) asm volatile("" :: "v"(addr[q]));
             else __hip_atomic_fetch_add(lctr_t(addr[q]), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        } else if constexpr (kLds) {
+            // Tiered counters.  A u16 counter lives in half of an LDS word; the
+            // lane whose add takes it from 0x7FFF to 0x8000 moves 0x8000 to the
+            // slot's global counter at once, so a half never carries into its
+            // neighbour (that would need 0x8000 more adds to one slot in the
+            // few instructions before the move).
+            uint32_t key = 0xFFFFFFFFu;
+            if (pr[q] <= 2u) {
+                if (slot[q] < t.n_hot) {
+                    __hip_atomic_fetch_add(lctr_t(hot_lane + slot[q] * 256u), 1u, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_WORKGROUP);
+                } else if (slot[q] < t.n_lctr) {
+                    const uint32_t w = t.img_bytes + ((slot[q] * 2u) & ~3u), sh = (slot[q] & 1u) * 16u;
+                    const uint32_t old = __hip_atomic_fetch_add(lctr_t(w), 1u << sh, __ATOMIC_RELAXED,
+                                                                __HIP_MEMORY_SCOPE_WORKGROUP);
+                    if (((old >> sh) & 0xFFFFu) == 0x7FFFu) {
+                        __hip_atomic_fetch_add(lctr_t(w), 0u - (0x8000u << sh), __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP);
+                        atomicAdd(&gslot[slot[q]], 0x8000ull);
+                    }
+                } else {
+                    key = slot[q];
+                }
+            }
+            wave_count(gslot, key);
         } else {
-            // Global counters: lanes holding the same slot are summed across
-            // the wave first (ballot per distinct slot, one atomic by the
-            // lowest lane), so a hot slot costs one atomic per wave, not 64.
+            // Global counters (image not LDS-resident)
             uint32_t key = pr[q] <= 2u ? slot[q] : 0xFFFFFFFFu;
             if (key == 0u) {
                 ++hot0;
                 key = 0xFFFFFFFFu;
             }
-            unsigned long long pending = __ballot(key != 0xFFFFFFFFu);
-            while (pending) {
-                const int leader = __builtin_ctzll(pending);
-                const uint32_t sk = __shfl(key, leader);
-                const unsigned long long same = __ballot(key == sk);
-                if (int(__lane_id()) == leader) atomicAdd(&gslot[sk], (unsigned long long)__popcll(same));
-                pending &= ~same;
-            }
+            wave_count(gslot, key);
         }
     }
     // Protocols outside TCP/UDP/ICMP fall through evalACL's switch
@@ -447,7 +479,7 @@ __device__ __forceinline__ void run_n(const Img<kLds>& im, const Cls4Dev& t, uin
 #pragma unroll
         for (int q = 0; q < N; ++q) {
             if (pr[q] > 2u) {
-                if constexpr (kLds)                                   // undo the cell count
+                if constexpr (kLds && kCtr == 0)                      // undo the cell count
                     __hip_atomic_fetch_add(lctr_t(addr[q]), ~0u, __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_WORKGROUP);
                 uint32_t rule;
@@ -476,25 +508,32 @@ __device__ __forceinline__ void stage_lds(const Cls4Dev& t, uint4* smem) {
     __syncthreads();
 }
 
-// End of an LDS-resident launch: fold the per-lane hot rows into their slots,
-// then store this workgroup's slot counters plainly into its own row of the
-// partials (fold_kernel sums the rows): no global atomics from every
-// workgroup onto the same addresses at the end of the launch.
+// End of an LDS-resident launch: this workgroup's slot counters go plainly
+// into its own row of the partials (fold_kernel sums the rows): no global
+// atomics from every workgroup onto the same addresses at the end of the
+// launch.  Hot slots: wave h sums slot h's per-lane row.
+template <int kCtr>
 __device__ __forceinline__ void flush_lds(const Cls4Dev& t, uint4* smem) {
     __syncthreads();
-    uint32_t* lctr = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(smem) + t.img_bytes);
-    const uint32_t* hrow = reinterpret_cast<const uint32_t*>(reinterpret_cast<uint8_t*>(smem) + t.off_hot);
-    for (uint32_t i = threadIdx.x; i < t.n_hot * 64u; i += blockDim.x) {
-        const uint32_t v = hrow[i];
-        if (v) atomicAdd(&lctr[i >> 6], v);
+    const uint8_t* lds = reinterpret_cast<const uint8_t*>(smem);
+    const uint32_t* lctr = reinterpret_cast<const uint32_t*>(lds + t.img_bytes);
+    const uint32_t* hrow = reinterpret_cast<const uint32_t*>(lds + t.off_hot);
+    uint32_t* part = t.part + size_t(blockIdx.x) * t.n_lctr;
+    if constexpr (CLS_ABLATE & 16) return;
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    for (uint32_t h = wave; h < t.n_hot; h += blockDim.x >> 6) {
+        uint32_t v = hrow[h * 64u + lane];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+        if (lane == 0 && h < t.n_lctr) part[h] = v + (kCtr == 0 ? lctr[h] : 0u);
     }
-    __syncthreads();
-    uint32_t* part = t.part + size_t(blockIdx.x) * t.n_ctr;
-    if constexpr (!(CLS_ABLATE & 16))
-        for (uint32_t i = threadIdx.x; i < t.n_ctr; i += blockDim.x) part[i] = lctr[i];
+    for (uint32_t i = t.n_hot + threadIdx.x; i < t.n_lctr; i += blockDim.x) {
+        if constexpr (kCtr == 0) part[i] = lctr[i];
+        else part[i] = (lctr[i >> 1] >> ((i & 1u) * 16u)) & 0xFFFFu;
+    }
 }
 
-template <bool kLds, bool kVec, int kMode, int kList, int kD>
+template <bool kLds, bool kVec, int kMode, int kList, int kD, int kCtr>
 __global__ __launch_bounds__(kClsBlock) void classify4_cls(Cls4Dev t, Pkts4 p, uint8_t* verdict,
                                                            unsigned long long* gslot) {
     extern __shared__ uint4 smem[];
@@ -551,7 +590,7 @@ __global__ __launch_bounds__(kClsBlock) void classify4_cls(Cls4Dev t, Pkts4 p, u
                 other |= ((pr | ((pr & 0x7F7F7F7Fu) + 0x7D7D7D7Du)) & 0x80808080u) != 0u;
             }
             uint32_t v[kN];
-            run_n<kN, kLds, kMode, kList, kD>(im, t, hot_lane, gslot, hot0, sa, da, pa, ra, other, v, sa);
+            run_n<kN, kLds, kMode, kList, kD, kCtr>(im, t, hot_lane, gslot, hot0, sa, da, pa, ra, other, v, sa);
             if (verdict) {
 #pragma unroll
                 for (int k = 0; k < kG; ++k)
@@ -597,7 +636,7 @@ __global__ __launch_bounds__(kClsBlock) void classify4_cls(Cls4Dev t, Pkts4 p, u
             const uint32_t pa[4] = {p2.x & 0xFFFFu, p2.x >> 16, p2.y & 0xFFFFu, p2.y >> 16};
             const uint32_t ra[4] = {pr & 0xFFu, (pr >> 8) & 0xFFu, (pr >> 16) & 0xFFu, pr >> 24};
             uint32_t v[4];
-            run_n<4, kLds, kMode, kList, -1>(im, t, hot_lane, gslot, hot0, sa, da, pa, ra,
+            run_n<4, kLds, kMode, kList, -1, kCtr>(im, t, hot_lane, gslot, hot0, sa, da, pa, ra,
                                              ((pr | ((pr & 0x7F7F7F7Fu) + 0x7D7D7D7Du)) & 0x80808080u) != 0u, v, sa);
             if (verdict)
                 stnt(v[0] | (v[1] << 8) | (v[2] << 16) | (v[3] << 24),
@@ -608,14 +647,71 @@ __global__ __launch_bounds__(kClsBlock) void classify4_cls(Cls4Dev t, Pkts4 p, u
     for (uint32_t i = tail_from + tid; i < uint32_t(p.n); i += nthreads) {
         const uint32_t sa[1] = {p.src[i]}, da[1] = {p.dst[i]}, pa[1] = {p.dport[i]}, ra[1] = {p.proto[i]};
         uint32_t v[1];
-        run_n<1, kLds, kMode, kList, -1>(im, t, hot_lane, gslot, hot0, sa, da, pa, ra, ra[0] > 2u, v, sa);
+        run_n<1, kLds, kMode, kList, -1, kCtr>(im, t, hot_lane, gslot, hot0, sa, da, pa, ra, ra[0] > 2u, v, sa);
         if (verdict) verdict[i] = uint8_t(v[0]);
     }
 
     if constexpr (!kLds) {
         if (hot0) atomicAdd(&gslot[0], (unsigned long long)hot0);
     }
-    if constexpr (kLds) flush_lds(t, smem);
+    if constexpr (kLds) flush_lds<kCtr>(t, smem);
+}
+
+// The classify kernels' HBM stream without the lookups (bench.py's measured
+// floor): the same loads and stores, in the same order, on the same grid;
+// the verdict is a mix of the packet's fields.
+__global__ __launch_bounds__(kClsBlock) void stream4_kernel(Pkts4 p, uint8_t* verdict) {
+    const uint32_t nthreads = gridDim.x * blockDim.x;
+    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t nsteps = uint32_t(p.n / 4u);
+    const uint4* S = reinterpret_cast<const uint4*>(p.src);
+    const uint4* D = reinterpret_cast<const uint4*>(p.dst);
+    const uint2* DP = reinterpret_cast<const uint2*>(p.dport);
+    const uint32_t* PR = reinterpret_cast<const uint32_t*>(p.proto);
+    struct Buf {
+        uint4 s, d;
+        uint2 dp;
+        uint32_t pr;
+    };
+    auto load = [&](Buf& b, uint32_t g) {
+        if (g < nsteps) {
+            b.s = ldnt(at(S, g)); b.d = ldnt(at(D, g)); b.dp = ldnt(at(DP, g)); b.pr = ldnt(at(PR, g));
+        }
+    };
+    auto step = [&](const Buf& b, uint32_t g) {
+        const uint32_t v = (b.s.x ^ b.d.x ^ b.s.y ^ b.d.y ^ b.s.z ^ b.d.z ^ b.s.w ^ b.d.w ^ b.dp.x ^ b.dp.y ^ b.pr) &
+                           0x03030303u;
+        stnt(v, const_cast<uint32_t*>(at(reinterpret_cast<const uint32_t*>(verdict), g)));
+    };
+    Buf a, b;
+    uint32_t g = tid;
+    load(a, g);
+    while (g < nsteps) {
+        load(b, g + nthreads);
+        step(a, g);
+        g += nthreads;
+        if (g >= nsteps) break;
+        load(a, g + nthreads);
+        step(b, g);
+        g += nthreads;
+    }
+}
+
+__global__ __launch_bounds__(kClsBlock) void stream16_kernel(Pkts16 p, uint8_t* verdict) {
+    const uint32_t nthreads = gridDim.x * blockDim.x;
+    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t nsteps = uint32_t(p.n / 256u) * 64u;
+    for (uint32_t g = tid; g < nsteps; g += nthreads) {
+        const uint32_t base = 4u * (g & ~63u) + (g & 63u);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint4 s = ldnt(at(p.src, base + 64u * k)), d = ldnt(at(p.dst, base + 64u * k));
+            const uint32_t dp = __builtin_nontemporal_load(p.dport + base + 64u * k);
+            const uint32_t pr = __builtin_nontemporal_load(p.proto + base + 64u * k);
+            __builtin_nontemporal_store(uint8_t((s.x ^ s.y ^ s.z ^ s.w ^ d.x ^ d.y ^ d.z ^ d.w ^ dp ^ pr) & 3u),
+                                        verdict + base + 64u * k);
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -737,7 +833,7 @@ __device__ __noinline__ uint32_t src_rep_global(const uint8_t* g, uint32_t gval,
     return r[0];
 }
 
-template <bool kLds, int kMode, int kList, int kD, bool kLin, int kFe>
+template <bool kLds, int kMode, int kList, int kD, bool kLin, int kFe, int kCtr>
 __global__ __launch_bounds__(kClsBlock) void classify16_cls(Cls4Dev t, Fe16 fe, Pkts16 p, uint8_t* verdict,
                                                             unsigned long long* gslot) {
     extern __shared__ uint4 smem[];
@@ -769,10 +865,10 @@ __global__ __launch_bounds__(kClsBlock) void classify16_cls(Cls4Dev t, Fe16 fe, 
                 for (int q = 0; q < N; ++q)
                     sl[q] = ra[q] > 2u ? src_rep_global(fe.gsrc, fe.gval, fe.top[0], fe.k8[0], s16[q]) : 0u;
             }
-            run_n<N, kLds, kMode, kList, kD>(im, t, hot_lane, gslot, hot0, sa, da, pa, ra, other, v, sl);
+            run_n<N, kLds, kMode, kList, kD, kCtr>(im, t, hot_lane, gslot, hot0, sa, da, pa, ra, other, v, sl);
         } else {
             src_rep(s16, sa);
-            run_n<N, kLds, kMode, kList, kD>(im, t, hot_lane, gslot, hot0, sa, da, pa, ra, other, v, sa);
+            run_n<N, kLds, kMode, kList, kD, kCtr>(im, t, hot_lane, gslot, hot0, sa, da, pa, ra, other, v, sa);
         }
     };
     // 4 packets per lane per step (vector dport / proto / verdict words),
@@ -853,25 +949,46 @@ __global__ __launch_bounds__(kClsBlock) void classify16_cls(Cls4Dev t, Fe16 fe, 
     if constexpr (!kLds) {
         if (hot0) atomicAdd(&gslot[0], (unsigned long long)hot0);
     }
-    if constexpr (kLds) flush_lds(t, smem);
+    if constexpr (kLds) flush_lds<kCtr>(t, smem);
 }
 
-// gslot[i] += sum over the grid's rows of part[w][i].  Thread (slot i, row
-// group blockIdx.y) sums kFoldRows rows with independent coalesced loads and
-// adds once: rows / kFoldRows atomics per slot instead of one per workgroup.
-constexpr uint32_t kFoldRows = 16;
-__global__ void fold_kernel(const uint32_t* __restrict__ part, uint32_t rows, uint32_t n,
-                            unsigned long long* __restrict__ gslot) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const uint32_t w0 = blockIdx.y * kFoldRows;
-    unsigned long long s64 = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < kFoldRows; ++k) {
-        const uint32_t w = w0 + k;
-        if (w < rows) s64 += part[size_t(w) * n + i];
+// slot_val[i] += the sum over the grid's rows of part[w][i], i < n: block b
+// takes slots [64 b, 64 b + 64), wave w of its 16 the rows w, w + 16, ...
+// (256 contiguous bytes per load instruction), then one wave adds the 16
+// partial sums -- a plain read-modify-write, this launch being the only
+// writer.  Blocks past the slot range zero `zero` (the call's rule counters):
+// no separate memset launch.
+constexpr uint32_t kFoldWaves = 16;
+__global__ __launch_bounds__(1024) void fold_kernel(const uint32_t* __restrict__ part, uint32_t rows, uint32_t n,
+                                                    unsigned long long* __restrict__ slot_val,
+                                                    unsigned long long* __restrict__ zero, uint32_t n_zero) {
+    const uint32_t nb = (n + 63u) / 64u;
+    if (blockIdx.x >= nb) {
+        const uint32_t i = (blockIdx.x - nb) * blockDim.x + threadIdx.x;
+        if (i < n_zero) zero[i] = 0ull;
+        return;
     }
-    if (s64) atomicAdd(&gslot[i], s64);
+    __shared__ unsigned long long acc[kFoldWaves][64];
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint32_t i = blockIdx.x * 64u + lane;
+    unsigned long long s64 = 0;
+    if (i < n) {
+        uint32_t w = wave;
+        for (; w + 3u * kFoldWaves < rows; w += 4u * kFoldWaves) {
+            const uint32_t a = part[size_t(w) * n + i], b = part[size_t(w + kFoldWaves) * n + i];
+            const uint32_t c = part[size_t(w + 2u * kFoldWaves) * n + i];
+            const uint32_t d = part[size_t(w + 3u * kFoldWaves) * n + i];
+            s64 += (unsigned long long)a + b + c + d;
+        }
+        for (; w < rows; w += kFoldWaves) s64 += part[size_t(w) * n + i];
+    }
+    acc[wave][lane] = s64;
+    __syncthreads();
+    if (wave == 0 && i < n) {
+#pragma unroll
+        for (uint32_t k = 1; k < kFoldWaves; ++k) s64 += acc[k][lane];
+        if (s64) slot_val[i] += s64;
+    }
 }
 
 __global__ __launch_bounds__(kBlock) void classify4_linear(const LinRule4* __restrict__ rules,
@@ -925,14 +1042,32 @@ __global__ __launch_bounds__(kBlock) void classify4_linear(const LinRule4* __res
     }
 }
 
-__global__ void remap_kernel(const unsigned long long* __restrict__ slot,
-                             const uint32_t* __restrict__ map, uint32_t n,
-                             unsigned long long* __restrict__ out) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) {
-        const unsigned long long v = slot[i];
-        if (v) atomicAdd(&out[map[i]], v);
+// Slot counters -> rule counters, read and cleared (slot_val is all zero
+// between calls).  csr: every slot once, grouped by rule, entry {slot, rule}.
+// A wave sums the values of each run of equal rules among its 64 entries
+// (suffix sums over the lanes) and the run's first lane adds the total: one
+// atomic per (wave, rule).  out == nullptr: clear only.
+__global__ __launch_bounds__(256) void remap_kernel(unsigned long long* __restrict__ slot_val,
+                                                    const uint2* __restrict__ csr, uint32_t n,
+                                                    unsigned long long* __restrict__ out) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t rule = 0xFFFFFFFFu;
+    unsigned long long v = 0;
+    if (k < n) {
+        const uint2 e = csr[k];
+        rule = e.y;
+        v = slot_val[e.x];
+        if (v) slot_val[e.x] = 0ull;
     }
+    const uint32_t lane = __lane_id();
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const unsigned long long w = __shfl_down(v, d);
+        const uint32_t r2 = __shfl_down(rule, d);
+        if (lane + uint32_t(d) < 64u && r2 == rule) v += w;
+    }
+    const uint32_t prev = __shfl_up(rule, 1);
+    if (out && k < n && v && (lane == 0 || prev != rule)) atomicAdd(&out[rule], v);
 }
 
 // evalACL on one ACL; returns ACLAction (nil ACL: PERMIT).  ACLs with a
@@ -1095,22 +1230,29 @@ __global__ void gen16_kernel(TrafficDev16 t, uint64_t first, uint64_t n, uint4* 
 int max_lds_bytes() { return kLdsMax; }
 int cls_block() { return kClsBlock; }
 
-template <bool kLds, bool kVec, int kMode, int kList, int kD>
+template <bool kLds, bool kVec, int kMode, int kList, int kD, int kCtr = 0>
 static void launch_d(const Cls4Dev& t, const Pkts4& p, uint8_t* verdict, unsigned long long* gslot,
                      const LaunchCfg& cfg) {
     const size_t lds = kLds ? t.lds_bytes : 0;
     if (kLds)
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(classify4_cls<kLds, kVec, kMode, kList, kD>),
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(classify4_cls<kLds, kVec, kMode, kList, kD, kCtr>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
-    hipLaunchKernelGGL((classify4_cls<kLds, kVec, kMode, kList, kD>), dim3(cfg.grid), dim3(kClsBlock), lds,
+    hipLaunchKernelGGL((classify4_cls<kLds, kVec, kMode, kList, kD, kCtr>), dim3(cfg.grid), dim3(kClsBlock), lds,
                        cfg.stream, t, p, verdict, gslot);
 }
 
-// The hot variants (LDS-resident image, vector loads, sublist lists) are
-// specialised on the search depth; the others take it at run time.
+// The hot variants (LDS-resident image, vector loads, sublist lists, u32
+// LDS counters) are specialised on the search depth; the others take it at
+// run time.
 template <bool kLds, bool kVec, int kMode, int kList>
 static void launch_cls(const Cls4Dev& t, const Pkts4& p, uint8_t* verdict, unsigned long long* gslot,
                        const LaunchCfg& cfg) {
+    if constexpr (kLds) {
+        if (t.ctr16) {
+            launch_d<kLds, kVec, kMode, kList, -1, 1>(t, p, verdict, gslot, cfg);
+            return;
+        }
+    }
     if constexpr (kLds && kVec && kList >= 3) {
         switch (t.bv_steps) {
         case 0: launch_d<kLds, kVec, kMode, kList, 0>(t, p, verdict, gslot, cfg); return;
@@ -1158,20 +1300,27 @@ hipError_t launch_classify4_cls(const Cls4Dev& t, const Pkts4& p, uint8_t* verdi
     return hipGetLastError();
 }
 
-template <bool kLds, int kMode, int kList, int kD, bool kLin, int kFe>
+template <bool kLds, int kMode, int kList, int kD, bool kLin, int kFe, int kCtr = 0>
 static void launch16_d(const Cls4Dev& t, const Fe16& fe, const Pkts16& p, uint8_t* verdict,
                        unsigned long long* gslot, const LaunchCfg& cfg) {
     const size_t lds = kLds ? t.lds_bytes : 0;
     if (kLds)
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(classify16_cls<kLds, kMode, kList, kD, kLin, kFe>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
-    hipLaunchKernelGGL((classify16_cls<kLds, kMode, kList, kD, kLin, kFe>), dim3(cfg.grid), dim3(kClsBlock), lds,
-                       cfg.stream, t, fe, p, verdict, gslot);
+        (void)hipFuncSetAttribute(
+            reinterpret_cast<const void*>(classify16_cls<kLds, kMode, kList, kD, kLin, kFe, kCtr>),
+            hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
+    hipLaunchKernelGGL((classify16_cls<kLds, kMode, kList, kD, kLin, kFe, kCtr>), dim3(cfg.grid), dim3(kClsBlock),
+                       lds, cfg.stream, t, fe, p, verdict, gslot);
 }
 
 template <bool kLds, int kMode, int kList, int kFe>
 static void launch16_cls(const Cls4Dev& t, const Fe16& fe, const Pkts16& p, uint8_t* verdict,
                          unsigned long long* gslot, const LaunchCfg& cfg) {
+    if constexpr (kLds) {
+        if (t.ctr16) {
+            launch16_d<kLds, kMode, kList, -1, false, kFe, 1>(t, fe, p, verdict, gslot, cfg);
+            return;
+        }
+    }
     if constexpr (kLds && kList >= 3) {
         switch (t.bv_steps) {
         case 0: launch16_d<kLds, kMode, kList, 0, false, kFe>(t, fe, p, verdict, gslot, cfg); return;
@@ -1237,18 +1386,26 @@ hipError_t launch_classify4_linear(const LinRule4* rules, uint32_t n_lin, uint32
     return hipGetLastError();
 }
 
-hipError_t launch_fold(const uint32_t* part, uint32_t rows, uint32_t n, unsigned long long* gslot,
-                       hipStream_t s) {
-    if (n == 0 || rows == 0) return hipSuccess;
-    hipLaunchKernelGGL(fold_kernel, dim3((n + 255) / 256, (rows + kFoldRows - 1) / kFoldRows), dim3(256), 0, s,
-                       part, rows, n, gslot);
+hipError_t launch_fold(const uint32_t* part, uint32_t rows, uint32_t n, unsigned long long* slot_val,
+                       unsigned long long* zero, uint32_t n_zero, hipStream_t s) {
+    if (rows == 0) n = 0;
+    if (!zero) n_zero = 0;
+    const uint32_t blocks = (n + 63u) / 64u + (n_zero + 1023u) / 1024u;
+    if (blocks == 0) return hipSuccess;
+    hipLaunchKernelGGL(fold_kernel, dim3(blocks), dim3(1024), 0, s, part, rows, n, slot_val, zero, n_zero);
     return hipGetLastError();
 }
 
-hipError_t launch_remap(const unsigned long long* slot, const uint32_t* map, uint32_t n,
-                        unsigned long long* out, hipStream_t s) {
+hipError_t launch_remap(unsigned long long* slot_val, const uint2* csr, uint32_t n, unsigned long long* out,
+                        hipStream_t s) {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(remap_kernel, dim3((n + 255) / 256), dim3(256), 0, s, slot, map, n, out);
+    hipLaunchKernelGGL(remap_kernel, dim3((n + 255) / 256), dim3(256), 0, s, slot_val, csr, n, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_stream(const Pkts4* p4, const Pkts16* p16, uint8_t* verdict, int grid, hipStream_t s) {
+    if (p4) hipLaunchKernelGGL(stream4_kernel, dim3(grid), dim3(kClsBlock), 0, s, *p4, verdict);
+    else hipLaunchKernelGGL(stream16_kernel, dim3(grid), dim3(kClsBlock), 0, s, *p16, verdict);
     return hipGetLastError();
 }
 

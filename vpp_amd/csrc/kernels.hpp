@@ -65,7 +65,9 @@ struct Cls4Dev {
     uint32_t bv_wide;          // some list > 16 entries: result bits need the hi word
     uint32_t row_bytes;        // cells per class row x cell size (interval search scales by it)
     uint32_t port_mul, port_mask4, port_dflt;   // list mode 4: port perfect hash at LDS 0
-    uint32_t* part;            // LDS-resident image: per-workgroup slot counters [grid][n_ctr]
+    uint32_t n_lctr;           // LDS-resident image: slots [0, n_lctr) counted in LDS, the rest in gslot
+    uint32_t ctr16;            // LDS counters are u16 (compile.hpp counter tiers)
+    uint32_t* part;            // LDS-resident image: per-workgroup slot counters [grid][n_lctr]
 };
 
 struct LaunchCfg {
@@ -84,12 +86,19 @@ hipError_t launch_classify16_cls(const Cls4Dev& t, const Fe16& fe, const Pkts16&
 hipError_t launch_classify4_linear(const LinRule4* rules, uint32_t n_lin, uint32_t n_rules,
                                    const Pkts4& p, uint8_t* verdict, unsigned long long* gslot,
                                    const LaunchCfg& cfg);
-// gslot[i] += sum_w part[w * n + i], w < rows (the classify kernel's partials)
-hipError_t launch_fold(const uint32_t* part, uint32_t rows, uint32_t n, unsigned long long* gslot,
-                       hipStream_t s);
-// out[map[i]] += slot[i]
-hipError_t launch_remap(const unsigned long long* slot, const uint32_t* map, uint32_t n,
-                        unsigned long long* out, hipStream_t s);
+// slot_val[i] += sum_w part[w * n + i], w < rows (the classify kernel's
+// partials); zero[0, n_zero) = 0 in the same launch (zero may be null)
+hipError_t launch_fold(const uint32_t* part, uint32_t rows, uint32_t n, unsigned long long* slot_val,
+                       unsigned long long* zero, uint32_t n_zero, hipStream_t s);
+// out[csr[k].y] += slot_val[csr[k].x], then slot_val[csr[k].x] = 0, for k < n
+// (csr: every slot once, grouped by rule); out null: clear only
+hipError_t launch_remap(unsigned long long* slot_val, const uint2* csr, uint32_t n, unsigned long long* out,
+                        hipStream_t s);
+
+// the classify kernels' packet stream without the lookups (stream floor);
+// exactly one of p4 / p16; p4 needs 16-B aligned src/dst, 8-B dport, 4-B
+// proto and verdict; p16 covers whole 256-packet wave steps only
+hipError_t launch_stream(const Pkts4* p4, const Pkts16* p16, uint8_t* verdict, int grid, hipStream_t s);
 
 struct AclDesc {                 // one installed ACL for the connection kernel
     const LinRule4* rules;

@@ -19,9 +19,22 @@ def world() -> tuple:
             int(os.environ.get("LOCAL_RANK", "0")))
 
 
+def device_index(local: int) -> int:
+    """GPU of a local rank: one rank per GPU.  With fewer GPUs than ranks
+    (a gloo rehearsal of N ranks on a one-GPU box) ranks share devices
+    round-robin; RCCL itself refuses two ranks on one device."""
+    import torch
+    n = torch.cuda.device_count()
+    return local % n if n else 0
+
+
 def init(backend: str = "nccl"):
+    """Join the process group.  ``backend`` "nccl" is RCCL over xGMI; "gloo"
+    runs the same collectives on the host (CPU tests, and rehearsing N ranks
+    on fewer GPUs).  VPP_DIST_BACKEND overrides it."""
     import torch
     import torch.distributed as dist
+    backend = os.environ.get("VPP_DIST_BACKEND", backend)
     rank, size, local = world()
     if size <= 1 or dist.is_initialized():
         return
@@ -32,24 +45,41 @@ def init(backend: str = "nccl"):
         dist.init_process_group(backend)
 
 
+def backend() -> str:
+    import torch.distributed as dist
+    return dist.get_backend() if dist.is_initialized() else "none"
+
+
 def shard(rank: int, n_per_rank: int) -> tuple:
     """First stream index and count of this rank's packets."""
     return rank * n_per_rank, n_per_rank
 
 
 def merge_counters(counters):
-    """All-reduce (sum) an int64 counter tensor in place across ranks."""
+    """All-reduce (sum) an int64 counter tensor in place across ranks.  With
+    gloo the collective runs on the host: device counters go through a host
+    copy (the rehearsal path; RCCL reduces them in HBM)."""
     import torch.distributed as dist
     if dist.is_initialized() and dist.get_world_size() > 1:
-        dist.all_reduce(counters, op=dist.ReduceOp.SUM)
+        if counters.is_cuda and dist.get_backend() == "gloo":
+            h = counters.cpu()
+            dist.all_reduce(h, op=dist.ReduceOp.SUM)
+            counters.copy_(h)
+        else:
+            dist.all_reduce(counters, op=dist.ReduceOp.SUM)
     return counters
 
 
-def max_over_ranks(value: float, device=None) -> float:
+def max_over_ranks(value, device=None):
+    """Max of a float (or a list of floats, elementwise) over the ranks."""
     import torch
     import torch.distributed as dist
     if not (dist.is_initialized() and dist.get_world_size() > 1):
         return value
-    t = torch.tensor([value], dtype=torch.float64, device=device)
+    if dist.get_backend() == "gloo":
+        device = None
+    vals = list(value) if isinstance(value, (list, tuple)) else [value]
+    t = torch.tensor(vals, dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t.item())
+    out = [float(x) for x in t.cpu()]
+    return out if isinstance(value, (list, tuple)) else out[0]

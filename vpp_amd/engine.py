@@ -142,6 +142,26 @@ class Engine:
                                             flags, None))
         return v, c
 
+    def stream_floor(self, src, dst, dport, proto, verdict, reps: int = 10, stream=None) -> float:
+        """Average ms of the classify kernel's packet stream alone (same loads,
+        stores and grid, no lookups) over a device batch: the measured floor
+        the classify kernel is compared against (bench.py)."""
+        import torch
+        v16 = src.dim() == 2
+        n = int(dport.numel())
+        if v16:
+            pk = _abi.PktSoa(_abi.AF_V16, None, None, _ptr(src), _ptr(dst), None, _ptr(dport), _ptr(proto))
+            n -= n % 256
+        else:
+            pk = _abi.PktSoa(_abi.AF_V4, _ptr(src), _ptr(dst), None, None, None, _ptr(dport), _ptr(proto))
+            n -= n % 4
+        if stream is None:
+            stream = torch.cuda.current_stream()
+        s = stream.cuda_stream if hasattr(stream, "cuda_stream") else stream
+        ms = C.c_float(0)
+        self._check(_abi.lib().cls_stream_floor(self.h, C.byref(pk), n, _ptr(verdict), reps, C.byref(ms), s))
+        return ms.value * (int(dport.numel()) / n if n else 1.0)
+
     def last_kernel_ms(self) -> float:
         ms = C.c_float(0)
         self._check(_abi.lib().cls_last_kernel_ms(self.h, C.byref(ms)))

@@ -37,6 +37,8 @@ SEEDS = {2: 0xC0175EED02, 3: 0xC0175EED03, 4: 0xC0175EED04, 5: 0xC0175EED05}
 CONFIGS = {
     2: dict(n_pods=100, rules_per_pod=10, n_apps=10, packets=16 << 20),
     3: dict(n_pods=1000, rules_per_pod=10, n_apps=100, packets=256 << 20),
+    # config 4: the config 3 table, one 2 Gi-packet batch sharded over the GPUs
+    4: dict(n_pods=1000, rules_per_pod=10, n_apps=100, packets=2 << 30, table=3),
     5: dict(n_pods=1000, rules_per_pod=10, n_apps=100, packets=256 << 20, mixed=True),
 }
 V6_PODS = 0xFD000010 << 96          # fd00:10::/64
@@ -160,11 +162,14 @@ def _widen_and_pools(acl, table, pods):
 
 
 def config(cfg: int):
-    """(acl, traffic spec dict, default packet count) of BASELINE config 2, 3
-    or 5 (config 5: 16-byte pools, spec["layout"] == 16)."""
+    """(acl, traffic spec dict, default packet count) of BASELINE config 2, 3,
+    4 or 5 (config 4: the config 3 table, its own stream seed and the whole
+    2 Gi-packet batch -- bench.py shards it; config 5: 16-byte pools,
+    spec["layout"] == 16)."""
     c = CONFIGS[cfg]
     mixed = c.get("mixed", False)
-    acl, pools = render_global(c["n_pods"], c["rules_per_pod"], c["n_apps"], seed=cfg, mixed=mixed)
+    acl, pools = render_global(c["n_pods"], c["rules_per_pod"], c["n_apps"], seed=c.get("table", cfg),
+                               mixed=mixed)
     spec = dict(seed=SEEDS[cfg], pct_pod_src=60, pct_rule_dst=50, pct_table_port=50,
                 pct_icmp=10 if mixed else 0, layout=16 if mixed else 4, **pools)
     return acl, spec, c["packets"]
