@@ -47,7 +47,8 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=1 << 21,
                     help="packets timed on the host for the CPU baseline (0: skip)")
     ap.add_argument("--faithful-sample", type=int, default=4096)
-    ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (default: all host cores)")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU baseline threads (default: every core this process may use)")
     ap.add_argument("--no-stream-floor", action="store_true", help="skip the live stream-floor measurement")
     return ap.parse_args()
 
@@ -66,6 +67,20 @@ def launch_ranks(args) -> int:
     return subprocess.run(cmd).returncode
 
 
+def cpu_share() -> int:
+    """Cores this process may use: its affinity mask, capped by a cgroup CPU
+    quota (a GPU box shows every host core but grants a share of them)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, int(int(q) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
 def host_cpu():
     """(logical cores, model name) of the host (lscpu's 'Model name')."""
     model = ""
@@ -81,12 +96,13 @@ def host_cpu():
 
 
 def cpu_baseline(acl, spec, sample: int, faithful_sample: int, threads: int = 0):
-    """Oracle CPU port on the host cores (OpenMP, every logical core unless
-    --cpu-threads says otherwise), and the faithful Go-style evaluator (string
-    re-parse per rule, one thread) on a smaller prefix."""
+    """Oracle CPU port on the host cores (OpenMP over every core this process
+    may use -- affinity and cgroup quota -- unless --cpu-threads says
+    otherwise), and the faithful Go-style evaluator (string re-parse per rule,
+    one thread) on a smaller prefix."""
     import oracle
     nproc, model = host_cpu()
-    threads = threads or nproc
+    threads = threads or cpu_share()
     af = spec.get("layout", 4)
     tr = (oracle.gen_traffic_v16 if af == 16 else oracle.gen_traffic_v4)(spec, 0, sample)
     cr = oracle.rules_to_c(acl.rules)
@@ -97,7 +113,7 @@ def cpu_baseline(acl, spec, sample: int, faithful_sample: int, threads: int = 0)
     ft.classify(tr["src"], tr["dst"], tr["dport"], tr["proto"], af=af, nthreads=threads)
     dt = time.perf_counter() - t0
     out = {"value": round(sample / dt / 1e6, 4), "unit": "Mpps", "cores": threads, "kind": "port",
-           "nproc": nproc, "cpu_model": model,
+           "nproc": nproc, "cpu_share": cpu_share(), "cpu_model": model,
            "sample": "%d packets of the same config stream (oracle/aclengine_ref.c orc_classify_fast, "
                      "rules pre-parsed, OpenMP %d threads), %.1f s" % (sample, threads, dt)}
     if faithful_sample:

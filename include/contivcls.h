@@ -167,7 +167,8 @@ typedef struct cls_table_info {
     uint32_t n_lctr;           /* slots counted in LDS (v4; the rest in global memory) */
     uint32_t ctr16;            /* the LDS slot counters are u16 (v4) */
     uint32_t list_mode;        /* candidate-list mode of the v4 classifier (cls_image_v4_header) */
-    uint32_t reserved[2];
+    uint32_t swap;             /* the v4 classifier is keyed on destinations (cls_image_v4_header) */
+    uint32_t reserved[1];
 } cls_table_info;
 int cls_table_get_info(cls_engine* e, uint32_t table_id, cls_table_info* info);
 
@@ -309,7 +310,8 @@ typedef struct cls_image_v4_header {
                                   then u8 windows of class per port) */
     uint32_t n_pclass;         /* list modes 2, 3: global port classes */
     uint32_t bv_wide;          /* some bit-vector list has more than 16 entries */
-    uint32_t row_bytes;        /* a class's 3 cells at off_cells + class x row_bytes */
+    uint32_t row_bytes;        /* a class's 4 cells (TCP, UDP, ICMP, other protocols) at
+                                  off_cells + class x row_bytes */
     uint32_t default_row;      /* hash LPM: cell row of default_class (hash entries hold rows) */
     uint32_t hash_mul[3];      /* hash LPM: p = key x mul; h0 = p >> shift, h1 = next log2(cap) bits */
     uint32_t port_mul, port_mask4, port_dflt;  /* list mode 4: e = u32 at byte mulhi(port, mul) &
@@ -317,6 +319,11 @@ typedef struct cls_image_v4_header {
     uint32_t n_hot, off_hot;   /* per-lane counter rows of the hot slots (LDS offsets) */
     uint32_t n_lctr;           /* slots counted in LDS (the rest: global counters) */
     uint32_t ctr16;            /* LDS slot counters are u16 (else u32) */
+    uint32_t swap;             /* 1: classes keyed on the DESTINATION address -- the image sees
+                                  packets with src and dst exchanged */
+    uint32_t off_other;        /* blob offset of the OTHER image (protocols > 2: one cell per
+                                  class, interval search, template scan; magic 0x434C534F "CLSO",
+                                  its slots numbered after this image's), 0 if none */
 } cls_image_v4_header;
 int cls_compile_v4(const cls_rule* rules, uint32_t n_rules, void* blob, uint64_t cap,
                    uint64_t* need);

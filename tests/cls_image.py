@@ -2,9 +2,10 @@
 
 Reads the blob of ``cls_compile_v4`` (include/contivcls.h) and evaluates it
 exactly as the gfx950 kernels do (vpp_amd/csrc/kernels.hip: classify4_cls's
-branch-free interval search -> class -> cell -> template scan; linear_one
-for protocols > 2), so the rule compiler can be checked against the oracle
-without a GPU.  Never used by the product.
+branch-free interval search -> class -> cell -> candidate list; protocols >
+2 on the OTHER image; linear_one for tables without a classifier), so the
+rule compiler can be checked against the oracle without a GPU.  Never used
+by the product.
 """
 from __future__ import annotations
 
@@ -31,7 +32,7 @@ def compile_blob(crules, fn="cls_compile_v4") -> bytes:
 class Image:
     def __init__(self, blob: bytes):
         h = _abi.ImageHeader.from_buffer_copy(blob)
-        assert h.magic in (0x434C5334, 0x434C3136)
+        assert h.magic in (0x434C5334, 0x434C3136, 0x434C534F)
         self.h = h
         self.n_rules = h.n_rules
         lin = np.frombuffer(blob, np.uint32, count=h.n_lin * 12, offset=h.off_lin).reshape(-1, 12)
@@ -44,8 +45,10 @@ class Image:
             if h.mode == 0:
                 self.bounds = np.frombuffer(img, np.uint32, count=2 * top, offset=h.off_bounds)
                 self.iclass = np.frombuffer(img, np.uint16, count=2 * top, offset=h.off_iclass)
+            # cells per class: 3 (TCP, UDP, ICMP) or 1 (the OTHER image)
+            self.ncell = h.row_bytes // (8 if h.list_mode == 0 else 4)
             if h.list_mode == 0:                   # uint2 cells
-                self.cells = np.frombuffer(img, np.uint32, count=h.n_classes * 6,
+                self.cells = np.frombuffer(img, np.uint32, count=h.n_classes * 2 * self.ncell,
                                            offset=h.off_cells).reshape(-1, 2)
             if h.list_mode == 0:
                 self.lists = np.frombuffer(img, np.uint16, count=h.n_list_entries, offset=h.off_lists)
@@ -57,6 +60,8 @@ class Image:
                 cap = h.hash_cap[i]
                 tab = np.frombuffer(img, np.uint32, count=4 * cap, offset=h.off_hash[i]).reshape(-1, 2)
                 self.hash.append((h.hash_mask[i], h.hash_shift[i], cap, tab, h.hash_mul[i]))
+        # protocols > 2: the OTHER image (its own blob inside this one)
+        self.other = Image(blob[h.off_other:]) if h.off_other else None
 
     @staticmethod
     def _h0(k, mul, shift):
@@ -96,9 +101,9 @@ class Image:
         interval and the port interval; first match = lowest common bit."""
         img = np.frombuffer(self._img, np.uint32)
         pr = np.minimum(proto, 2).astype(np.int64)
-        cells1 = np.frombuffer(self._img, np.uint32, count=self.h.n_classes * 3,
+        cells1 = np.frombuffer(self._img, np.uint32, count=self.h.n_classes * self.ncell,
                                offset=self.h.off_cells)
-        cell = cells1[cls * 3 + pr]
+        cell = cells1[cls * self.ncell + pr]
         cb = (cell >> 16).astype(np.int64)
         d_off = ((cell & 0xFFFF).astype(np.int64) * 8) // 4
         S = int(self.h.bv_steps_d)
@@ -128,7 +133,7 @@ class Image:
         else:
             mp = search(p_off, sp, dport.astype(np.uint32))
         m = (md & mp).astype(np.uint64)
-        found = (m != 0) & (proto <= 2)
+        found = m != 0
         low = m & (~m + np.uint64(1))
         j = np.zeros(len(m), np.int64)
         nz = low != 0
@@ -136,12 +141,6 @@ class Image:
         res = np.where(found, (res_bits >> (2 * j).astype(np.uint64)) & np.uint64(3), 0).astype(np.uint32)
         slot = np.where(found, cb + j, 0)
         np.add.at(counters, self.ctr_rule[slot].astype(np.int64), 1)
-        other = proto > 2
-        if other.any():
-            r2, rule2 = self.linear(src[other], dst[other], dport[other], proto[other])
-            res[other] = r2
-            np.subtract.at(counters, self.ctr_rule[slot[other]].astype(np.int64), 1)
-            np.add.at(counters, rule2, 1)
         return res.astype(np.uint8), counters
 
     def _port_class(self, dport):
@@ -170,22 +169,16 @@ class Image:
         moves the state when start - 1 < dst; outcome = result | (j + 1) << 2."""
         img = np.frombuffer(self._img, np.uint32).astype(np.int64)
         pr = np.minimum(proto, 2).astype(np.int64)
-        cell = img[(self.h.off_cells + cls * 12 + pr * 4) // 4]
+        cell = img[(self.h.off_cells + cls * self.h.row_bytes + pr * 4) // 4]
         pc4 = self._port_class4(dport)                # class x 4
         st = img[((cell & 0xFFFF) + pc4) // 4]
         d = dst.astype(np.int64)
         for i in range(int(self.h.bv_steps_d) - 1, -1, -1):
             a = ((st >> 13) + (8 << i)) // 4
             st = np.where(img[a] < d, img[a + 1], st)
-        res = np.where(proto <= 2, st & 3, 0).astype(np.uint32)
+        res = (st & 3).astype(np.uint32)
         slot = (cell >> 16) + ((st >> 2) & 63)       # the cell's no-match slot when j + 1 == 0
         np.add.at(counters, self.ctr_rule[slot].astype(np.int64), 1)
-        other = proto > 2
-        if other.any():
-            r2, rule2 = self.linear(src[other], dst[other], dport[other], proto[other])
-            res[other] = r2
-            np.subtract.at(counters, self.ctr_rule[slot[other]].astype(np.int64), 1)
-            np.add.at(counters, rule2, 1)
         return res.astype(np.uint8), counters
 
     def linear(self, src, dst, dport, proto):
@@ -206,13 +199,27 @@ class Image:
                 break
         return res, rule
 
-    def classify(self, src, dst, dport, proto, cls=None):
+    def classify(self, src, dst, dport, proto, cls=None, framed=False):
         """Returns (verdict u8[n], counters u64[R+1]).  cls: the packets'
-        source classes when found by a front end (core mode 3)."""
+        source classes when found by a front end (core mode 3).  A
+        destination-keyed image (h.swap) sees src and dst exchanged, unless
+        the caller already did that (framed)."""
         src = np.asarray(src, np.uint32)
         dst = np.asarray(dst, np.uint32)
+        if self.h.swap and not framed:
+            src, dst = dst, src
         dport = np.asarray(dport, np.uint16)
         proto = np.asarray(proto, np.uint8)
+        oth = proto > 2
+        if self.other is not None and oth.any():
+            # the kernels classify protocols > 2 on the OTHER image (one cell per class)
+            keep = ~oth
+            v = np.zeros(len(src), np.uint8)
+            v[keep], c = self.classify(src[keep], dst[keep], dport[keep], proto[keep],
+                                       None if cls is None else cls[keep], framed=True)
+            v[oth], c2 = self.other.classify(src[oth], dst[oth], dport[oth], np.zeros(int(oth.sum()), np.uint8),
+                                             framed=True)
+            return v, c + c2
         n = len(src)
         counters = np.zeros(self.n_rules + 1, np.uint64)
         if not self.has_cls:
@@ -226,7 +233,7 @@ class Image:
         if self.h.list_mode >= 1:
             return self._classify_bv(cls, src, dst, dport, proto, counters)
         pr = np.minimum(proto, 2).astype(np.int64)
-        cell = self.cells[cls * 3 + pr]
+        cell = self.cells[cls * self.ncell + pr]
         start = (cell[:, 0] & 0xFFFF).astype(np.int64)
         ln = (cell[:, 0] >> 16).astype(np.int64)
         base = cell[:, 1].astype(np.int64)
@@ -244,13 +251,6 @@ class Image:
             slot[m] = base[m] + j
             done |= m
         np.add.at(counters, self.ctr_rule[slot].astype(np.int64), 1)
-        other = proto > 2
-        if other.any():
-            r2, rule2 = self.linear(src[other], dst[other], dport[other], proto[other])
-            res[other] = r2
-            # undo the slot count made above for these packets, use the rule path
-            np.subtract.at(counters, self.ctr_rule[slot[other]].astype(np.int64), 1)
-            np.add.at(counters, rule2, 1)
         return res.astype(np.uint8), counters
 
 
@@ -329,6 +329,8 @@ class Image16:
     def classify(self, src16, dst16, dport, proto):
         src16 = np.asarray(src16, np.uint8).reshape(-1, 16)
         dst16 = np.asarray(dst16, np.uint8).reshape(-1, 16)
+        if self.h.core.swap:                           # destination-keyed
+            src16, dst16 = dst16, src16
         srep = self.rep(0, src16)
         drep = self.rep(1, dst16)
         if self.h.src_mode == 1:
@@ -336,5 +338,5 @@ class Image16:
             # the hashed row must be the class row of the rep (what the core's
             # own source lookup would give), protocol > 2 takes the rep
             cls = (rows - self.core.h.off_cells) // self.core.h.row_bytes
-            return self.core.classify(srep, drep, dport, proto, cls=cls)
-        return self.core.classify(srep, drep, dport, proto)
+            return self.core.classify(srep, drep, dport, proto, cls=cls, framed=True)
+        return self.core.classify(srep, drep, dport, proto, framed=True)

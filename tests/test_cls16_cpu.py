@@ -19,6 +19,13 @@ from cls_image import Image, Image16, compile_blob
 from vpp_amd import _abi
 
 
+@pytest.fixture(autouse=True)
+def _source_keyed(monkeypatch):
+    """These tests pin list modes of the source-keyed layout; the compiler's
+    choice of orientation (compile.cpp build_cls4) is tested on its own."""
+    monkeypatch.setenv("CONTIVCLS_ORIENT", "src")
+
+
 def _img16(rules):
     return Image16(compile_blob(_abi.CRules(rules), "cls_compile_v16"))
 

@@ -14,6 +14,13 @@ from cls_image import Image, compile_blob
 from vpp_amd import _abi
 
 
+@pytest.fixture(autouse=True)
+def _source_keyed(monkeypatch):
+    """These tests pin list modes of the source-keyed layout; the compiler's
+    choice of orientation (compile.cpp build_cls4) is tested on its own."""
+    monkeypatch.setenv("CONTIVCLS_ORIENT", "src")
+
+
 def _check(rules, traffic):
     img = Image(compile_blob(_abi.CRules(rules)))
     v, c = img.classify(traffic["src"], traffic["dst"], traffic["dport"], traffic["proto"])

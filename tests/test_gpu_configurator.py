@@ -80,7 +80,7 @@ def test_random_policy_sets_on_gpu(eng, seed):
     assert checked >= 8
 
 
-@pytest.mark.parametrize("num_cidrs", [20, 60])
+@pytest.mark.parametrize("num_cidrs", [20, 60, 200])
 def test_gen_policy_scale_on_gpu(eng, num_cidrs):
     """gen-policy.py's NetworkPolicy (1 policy, num_cidrs blocks x 5 excepts,
     20 ports per direction) through the configurator: ~10k-95k rules per

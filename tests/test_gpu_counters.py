@@ -29,9 +29,10 @@ def eng():
     e.close()
 
 
-def _layout(rules):
+def _layout(rules, monkeypatch):
     from cls_image import Image, compile_blob
     from vpp_amd import _abi
+    monkeypatch.setenv("CONTIVCLS_ORIENT", "src")
     return Image(compile_blob(_abi.CRules(rules))).h
 
 
@@ -49,10 +50,11 @@ def _budget(h, tier):
 
 
 def _check(eng, rules, tr, monkeypatch, tier):
-    h = _layout(rules)
+    h = _layout(rules, monkeypatch)
     assert h.has_cls
     monkeypatch.setenv("CONTIVCLS_LDS_BUDGET", str(_budget(h, tier)))
     monkeypatch.setenv("CONTIVCLS_LIST_MODE", str(h.list_mode))   # the layout the budget was sized on
+    monkeypatch.setenv("CONTIVCLS_ORIENT", "src")
     t = eng.put_table("tier", rules)
     try:
         info = t.info()

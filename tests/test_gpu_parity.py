@@ -12,6 +12,14 @@ from scenario_replay import load_scenarios, replay
 
 pytestmark = pytest.mark.gpu
 
+
+@pytest.fixture(autouse=True)
+def _source_keyed(monkeypatch):
+    """These tests pin list modes of the source-keyed layout; the compiler's
+    choice of orientation (compile.cpp build_cls4) is tested on its own."""
+    monkeypatch.setenv("CONTIVCLS_ORIENT", "src")
+
+
 SCENARIOS = load_scenarios()
 
 

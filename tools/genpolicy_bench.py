@@ -2,11 +2,12 @@
 """Classification rate on rule lists from the gen-policy.py workload
 (tests/policy/perf/gen-policy.py restated as vpp_amd.configurator.gen_policy).
 
-For each block count: the configurator generates the pod's egress list
-(source = the policy's IP blocks minus excepts, x 20 ports), the list is
-compiled onto the classifier (TestTraffic semantics, renderer/traffic.py),
-and 64 Mi device-resident IPv4 packets around the blocks are classified,
-timed with the engine's HIP events.  Prints one JSON line per block count.
+For each block count and direction: the configurator generates the pod's
+list (ingress: the policy's IP blocks minus excepts as sources; egress: as
+destinations; x 20 ports), the list is compiled onto the classifier
+(TestTraffic semantics, renderer/traffic.py), and 64 Mi device-resident IPv4
+packets around the blocks (TCP/UDP, 10 % ICMP, 1 % protocol 47) are
+classified, timed with the engine's HIP events.  One JSON line per list.
 usage: python tools/genpolicy_bench.py [--blocks 20 60 200] [--packets 67108864]
 """
 import argparse
@@ -22,64 +23,73 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
+def bench_list(eng, pol, txn, nb, match, n, iters):
+    """Classify n device-resident packets against one of the pod's lists."""
+    import torch
+    from vpp_amd import configurator as C
+    from vpp_amd.renderer.traffic import compile_rules
+    t0 = time.perf_counter()
+    # MATCH_INGRESS: the list keyed on the blocks as sources; MATCH_EGRESS: as destinations
+    rules = txn.generate_rules(C.MATCH_INGRESS if match == "ingress" else C.MATCH_EGRESS, [pol])
+    t_gen = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    table = eng.put_table("gen%d" % nb, compile_rules(rules))
+    t_put = time.perf_counter() - t0
+    info = table.info()
+    g = np.random.default_rng(nb)
+    blk = g.integers(0, nb + nb // 10 + 1, n, dtype=np.uint64)
+    inblk = (((blk + 0x100) << 16) | g.integers(0, 1 << 16, n, dtype=np.uint64)).astype(np.uint32)
+    other = g.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
+    src, dst = (inblk, other) if match == "ingress" else (other, inblk)
+    ports = np.array([p.number for p in pol.matches[0].ports], np.uint16)
+    dport = np.where(g.random(n) < 0.5, g.choice(ports, n), g.integers(0, 65536, n)).astype(np.uint16)
+    # TCP/UDP, 10 % ICMP, 1 % protocol 47
+    proto = g.choice(np.array([0, 1, 2, 47], np.uint8), n, p=[0.445, 0.445, 0.1, 0.01])
+    d = {k: torch.from_numpy(v.view(np.int32) if v.dtype == np.uint32 else
+                             (v.view(np.int16) if v.dtype == np.uint16 else v)).to("cuda")
+         for k, v in dict(src=src, dst=dst, dport=dport, proto=proto).items()}
+    verdict = torch.empty(n, dtype=torch.uint8, device="cuda")
+    counters = torch.zeros(table.n_rules + 1, dtype=torch.int64, device="cuda")
+    eng.classify(table, d["src"], d["dst"], d["dport"], d["proto"], verdict, counters)
+    torch.cuda.synchronize()
+    eng.kernel_times(reset=True)
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        eng.classify(table, d["src"], d["dst"], d["dport"], d["proto"], verdict, counters, timing=True)
+    torch.cuda.synchronize()
+    wall = (time.perf_counter() - t0) / iters
+    kms = eng.kernel_times(reset=True)
+    k_avg = sum(kms) / max(1, len(kms))
+    vh = np.bincount(verdict.cpu().numpy(), minlength=3).tolist()
+    eng.del_table(table)
+    return {
+        "workload": "gen-policy.py, %d blocks x 5 excepts x 20 ports: the pod's %s list" % (nb, match),
+        "rules": len(rules), "gen_s": round(t_gen, 2), "compile_s": round(t_put, 2),
+        "kernel": info.get("kernel"), "lds_resident": info.get("lds_resident"),
+        "list_mode": info.get("list_mode"), "dst_keyed": info.get("swap"), "ctr16": info.get("ctr16"),
+        "lds_slots": info.get("n_lctr"), "slots": info.get("n_slots"),
+        "packets": n, "Gpps_wall": round(n / wall / 1e9, 2), "kernel_ms": round(k_avg, 4),
+        "Gpps_kernel": round(n / (k_avg * 1e-3) / 1e9, 2) if k_avg else None,
+        "hbm_frac_kernel": round(12 * n / (k_avg * 1e-3) / 8e12, 3) if k_avg else None,
+        "verdicts_deny_permit_unmatched": vh}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--blocks", type=int, nargs="+", default=[20, 60, 200])
     ap.add_argument("--packets", type=int, default=1 << 26)
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--match", nargs="+", default=["ingress", "egress"])
     a = ap.parse_args()
-    import torch
     from vpp_amd import configurator as C
     from vpp_amd.engine import Engine
     from vpp_amd.renderer.api import PodID
-    from vpp_amd.renderer.traffic import compile_rules
     eng = Engine()
-    n = a.packets
     for nb in a.blocks:
-        rng = random.Random(nb)
-        pol = C.gen_policy(rng, num_cidrs=nb)
-        pod = PodID("db", "default")
-        txn = C.PolicyConfigurator({pod: "10.1.1.1"}).new_txn(False)
-        t0 = time.perf_counter()
-        rules = txn.generate_rules(C.MATCH_INGRESS, [pol])       # the vswitch egress list
-        t_gen = time.perf_counter() - t0
-        t0 = time.perf_counter()
-        table = eng.put_table("gen%d" % nb, compile_rules(rules))
-        t_put = time.perf_counter() - t0
-        info = table.info()
-        g = np.random.default_rng(nb)
-        blk = g.integers(0, nb + nb // 10 + 1, n, dtype=np.uint64)
-        src = (((blk + 0x100) << 16) | g.integers(0, 1 << 16, n, dtype=np.uint64)).astype(np.uint32)
-        dst = g.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
-        ports = np.array([p.number for p in pol.matches[0].ports], np.uint16)
-        dport = np.where(g.random(n) < 0.5, g.choice(ports, n), g.integers(0, 65536, n)).astype(np.uint16)
-        proto = g.integers(0, 2, n).astype(np.uint8)
-        d = {k: torch.from_numpy(v.view(np.int32) if v.dtype == np.uint32 else
-                                 (v.view(np.int16) if v.dtype == np.uint16 else v)).to("cuda")
-             for k, v in dict(src=src, dst=dst, dport=dport, proto=proto).items()}
-        verdict = torch.empty(n, dtype=torch.uint8, device="cuda")
-        counters = torch.zeros(table.n_rules + 1, dtype=torch.int64, device="cuda")
-        eng.classify(table, d["src"], d["dst"], d["dport"], d["proto"], verdict, counters)
-        torch.cuda.synchronize()
-        eng.kernel_times(reset=True)
-        t0 = time.perf_counter()
-        for _ in range(a.iters):
-            eng.classify(table, d["src"], d["dst"], d["dport"], d["proto"], verdict, counters, timing=True)
-        torch.cuda.synchronize()
-        wall = (time.perf_counter() - t0) / a.iters
-        kms = eng.kernel_times(reset=True)
-        k_avg = sum(kms) / max(1, len(kms))
-        vh = np.bincount(verdict.cpu().numpy(), minlength=3).tolist()
-        print(json.dumps({
-            "workload": "gen-policy.py, %d blocks x 5 excepts x 20 ports: pod egress list" % nb,
-            "rules": len(rules), "gen_s": round(t_gen, 2), "compile_s": round(t_put, 2),
-            "kernel": info.get("kernel"), "lds_resident": info.get("lds_resident"),
-            "packets": n, "Gpps_wall": round(n / wall / 1e9, 2), "kernel_ms": round(k_avg, 4),
-            "Gpps_kernel": round(n / (k_avg * 1e-3) / 1e9, 2) if k_avg else None,
-            "hbm_frac_kernel": round(12 * n / (k_avg * 1e-3) / 8e12, 3) if k_avg else None,
-            "verdicts_deny_permit_unmatched": vh}), flush=True)
-        del d, verdict, counters
-        eng.del_table(table)
+        pol = C.gen_policy(random.Random(nb), num_cidrs=nb)
+        txn = C.PolicyConfigurator({PodID("db", "default"): "10.1.1.1"}).new_txn(False)
+        for match in a.match:
+            print(json.dumps(bench_list(eng, pol, txn, nb, match, a.packets, a.iters)), flush=True)
     eng.close()
 
 

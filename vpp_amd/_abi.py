@@ -79,7 +79,7 @@ class TableInfo(C.Structure):
                 ("n_templates", C.c_uint32), ("n_slots", C.c_uint32),
                 ("lds_resident", C.c_uint32), ("has_v16", C.c_uint32), ("lds_bytes_v16", C.c_uint32),
                 ("lds_resident_v16", C.c_uint32), ("n_lctr", C.c_uint32), ("ctr16", C.c_uint32),
-                ("list_mode", C.c_uint32), ("reserved", C.c_uint32 * 2)]
+                ("list_mode", C.c_uint32), ("swap", C.c_uint32), ("reserved", C.c_uint32 * 1)]
 
 
 class TrafficSpec(C.Structure):
@@ -111,7 +111,8 @@ class ImageHeader(C.Structure):
         ("bv_wide", C.c_uint32), ("row_bytes", C.c_uint32), ("default_row", C.c_uint32),
         ("hash_mul", C.c_uint32 * 3), ("port_mul", C.c_uint32), ("port_mask4", C.c_uint32),
         ("port_dflt", C.c_uint32),
-        ("n_hot", C.c_uint32), ("off_hot", C.c_uint32), ("n_lctr", C.c_uint32), ("ctr16", C.c_uint32)]
+        ("n_hot", C.c_uint32), ("off_hot", C.c_uint32), ("n_lctr", C.c_uint32), ("ctr16", C.c_uint32),
+        ("swap", C.c_uint32), ("off_other", C.c_uint32)]
 
 
 class Image16Header(C.Structure):

@@ -511,7 +511,8 @@ uint32_t lds_budget() {
 // global memory.  Returns whether the image is LDS-resident.
 bool place_counters(Cls4Image& img, uint32_t budget, bool partial) {
     const uint32_t hot = img.n_hot * 64u * 4u;
-    const uint32_t c32 = (img.n_ctr * 4u + 15u) & ~15u, c16 = (img.n_ctr * 2u + 15u) & ~15u;
+    auto a16 = [](uint32_t x) { return (x + 15u) & ~15u; };
+    const uint32_t c32 = a16(img.n_ctr * 4u), c16 = a16(img.n_ctr * 2u);
     uint32_t region = c32;
     bool ok = true;
     img.ctr16 = 0;
@@ -520,11 +521,11 @@ bool place_counters(Cls4Image& img, uint32_t budget, bool partial) {
     } else if (uint64_t(img.img_bytes) + c16 + hot <= budget) {
         img.ctr16 = 1;
         region = c16;
-    } else if (partial && uint64_t(img.img_bytes) + hot + ((img.n_hot * 2u + 15u) & ~15u) <= budget) {
+    } else if (partial && uint64_t(img.img_bytes) + hot + a16(img.n_hot * 2u) <= budget) {
         // at least the hot slots: their totals go through these slots' rows
         img.ctr16 = 1;
         img.n_lctr = std::min(img.n_ctr, ((budget - img.img_bytes - hot) / 2u) & ~7u);
-        region = (img.n_lctr * 2u + 15u) & ~15u;
+        region = a16(img.n_lctr * 2u);
     } else {
         ok = false;
     }
@@ -534,7 +535,7 @@ bool place_counters(Cls4Image& img, uint32_t budget, bool partial) {
     return ok;
 }
 
-bool build_cls4(const std::vector<SemRule>& sem, uint32_t n_rules, Cls4Image& img,
+static bool build_cls4_one(const std::vector<SemRule>& sem, uint32_t n_rules, Cls4Image& img,
                 std::string& why, const Cls4Opts* opt) {
     img = Cls4Image();
     // distinct source prefixes
@@ -619,7 +620,9 @@ bool build_cls4(const std::vector<SemRule>& sem, uint32_t n_rules, Cls4Image& im
         uint32_t dflt = 0;
         if (len0_class >= 0) dflt = uint32_t(len0_class);
         else if (class_of_pfx[0] >= 0) dflt = uint32_t(class_of_pfx[0]);
-        if (opt && opt->ext_src) {
+        if (opt && opt->other) {
+            img.mode = 0;                            // the OTHER image: interval search (Cls4Opts)
+        } else if (opt && opt->ext_src) {
             img.mode = 3;                            // the caller maps addresses to rows
         } else if (keys.size() <= kMaxHashLens) {
             img.mode = 1;
@@ -659,7 +662,10 @@ bool build_cls4(const std::vector<SemRule>& sem, uint32_t n_rules, Cls4Image& im
     std::vector<TmplKey> tmpls;
     std::unordered_map<std::vector<uint16_t>, uint32_t, VecHash> list_id;
     std::vector<uint16_t> lists;
-    std::vector<uint32_t> cells(size_t(n_classes) * 3 * 2);
+    // cells per class: TCP, UDP, ICMP (the main image), or OTHER alone
+    const uint32_t pr0 = opt && opt->other ? uint32_t(P_OTHER) : 0u, ncell = opt && opt->other ? 1u : 3u;
+    img.n_cells = ncell;
+    std::vector<uint32_t> cells(size_t(n_classes) * ncell * 2);
     img.ctr_rule.assign(1, n_rules);  // slot 0: default DENY
     // Hot class: the one covering most of the address space (random sources
     // land there).  Its cells take the slots right after slot 0, so the
@@ -688,7 +694,8 @@ bool build_cls4(const std::vector<SemRule>& sem, uint32_t n_rules, Cls4Image& im
             cand.insert(cand.end(), by_pfx[p].begin(), by_pfx[p].end());
         cand.insert(cand.end(), any_src.begin(), any_src.end());
         std::sort(cand.begin(), cand.end());
-        for (int pr = 0; pr < 3; ++pr) {
+        for (uint32_t k = 0; k < ncell; ++k) {
+            const int pr = int(pr0 + k);
             std::vector<uint16_t> seq;
             const uint32_t ctr_base = uint32_t(img.ctr_rule.size());
             for (uint32_t pos : cand) {
@@ -727,8 +734,8 @@ bool build_cls4(const std::vector<SemRule>& sem, uint32_t n_rules, Cls4Image& im
                 }
             }
             if (start > 0xFFFF) { why = "candidate list storage exceeds 65536 entries"; return false; }
-            cells[(size_t(c) * 3 + pr) * 2 + 0] = start | (uint32_t(seq.size()) << 16);
-            cells[(size_t(c) * 3 + pr) * 2 + 1] = ctr_base;
+            cells[(size_t(c) * ncell + k) * 2 + 0] = start | (uint32_t(seq.size()) << 16);
+            cells[(size_t(c) * ncell + k) * 2 + 1] = ctr_base;
         }
         if (ci == 0) img.n_hot = std::min<uint32_t>(uint32_t(img.ctr_rule.size()), kMaxHot);
     }
@@ -746,8 +753,8 @@ bool build_cls4(const std::vector<SemRule>& sem, uint32_t n_rules, Cls4Image& im
     bool all_bv = true;
     std::vector<uint32_t> bv_lists;                       // distinct cell list keys
     for (uint32_t c = 0; c < n_classes && all_bv; ++c)
-        for (int pr = 0; pr < 3; ++pr) {
-            const uint32_t x = cells[(size_t(c) * 3 + pr) * 2];
+        for (uint32_t k = 0; k < ncell; ++k) {
+            const uint32_t x = cells[(size_t(c) * ncell + k) * 2];
             if ((x >> 16) > 32) { all_bv = false; break; }
             bv_lists.push_back(x);
         }
@@ -893,12 +900,12 @@ bool build_cls4(const std::vector<SemRule>& sem, uint32_t n_rules, Cls4Image& im
     // (j + 1) with no select; same cell order, so the hot class stays first
     const std::vector<uint32_t> ctr_base_rule = img.ctr_rule;
     const uint32_t hot_base = img.n_hot;
-    std::vector<uint32_t> ctr3(1, n_rules), cb3(size_t(n_classes) * 3);
+    std::vector<uint32_t> ctr3(1, n_rules), cb3(size_t(n_classes) * ncell);
     uint32_t hot3 = 1;
     for (uint32_t ci = 0; ci < n_classes; ++ci) {
         const uint32_t c = ci == 0 ? hot_class : (ci <= hot_class ? ci - 1 : ci);
-        for (int pr = 0; pr < 3; ++pr) {
-            const size_t k = size_t(c) * 3 + pr;
+        for (uint32_t kk = 0; kk < ncell; ++kk) {
+            const size_t k = size_t(c) * ncell + kk;
             cb3[k] = uint32_t(ctr3.size());
             ctr3.push_back(n_rules);
             const uint32_t len = cells[2 * k] >> 16, b = cells[2 * k + 1];
@@ -972,7 +979,7 @@ bool build_cls4(const std::vector<SemRule>& sem, uint32_t n_rules, Cls4Image& im
             w.resize(align4(uint32_t(w.size())));
         }
         img.off_cells = uint32_t(w.size()) * 4;
-        img.row_bytes = lm == 0 ? 24u : 12u;          // 3 cells of uint2 (scan) / u32
+        img.row_bytes = lm == 0 ? 8u * ncell : 4u * ncell;   // cells of uint2 (scan) / u32
         img.default_row = img.off_cells + img.default_class * img.row_bytes;
         if (lm == 0) {
             // scan cells: uint2 {list start | len << 16, counter base}
@@ -994,12 +1001,12 @@ bool build_cls4(const std::vector<SemRule>& sem, uint32_t n_rules, Cls4Image& im
         } else if (lm >= 3) {
             // sublist cells: u32 {pointer table byte offset | counter base << 16},
             // the base being the cell's own no-match slot
-            const size_t n_cells = size_t(n_classes) * 3;
+            const size_t n_cells = size_t(n_classes) * ncell;
             for (size_t i = 0; i < n_cells; ++i) w.push_back(ptr_off.at(cells[2 * i]) | (cb3[i] << 16));
             w.resize(align4(uint32_t(w.size())));
         } else {
             // bit-vector cells: u32 {list block offset / 8 | counter base << 16}
-            const size_t n_cells = size_t(n_classes) * 3;
+            const size_t n_cells = size_t(n_classes) * ncell;
             const uint32_t off_bv = uint32_t(align4(uint32_t(w.size() + n_cells))) * 4;
             img.off_bv = off_bv;
             for (size_t i = 0; i < n_cells; ++i) {
@@ -1115,9 +1122,10 @@ bool build_cls4(const std::vector<SemRule>& sem, uint32_t n_rules, Cls4Image& im
         if (lm == 0) break;
         lm = lm >= 3 ? 2u : (lm == 2 && std::max(Sd, Sp) <= kMaxBvSteps) ? 1u : 0u;
     }
+    if (opt && opt->other) seq.assign(1, 0u);     // the OTHER image: template scan (Cls4Opts)
     // diagnostics / tests: exactly this list mode when it is available
     // (CONTIVCLS_LIST_MODE), so a test's LDS budget picks the counter tier
-    if (const char* f = std::getenv("CONTIVCLS_LIST_MODE")) {
+    else if (const char* f = std::getenv("CONTIVCLS_LIST_MODE")) {
         const uint32_t lm = uint32_t(std::strtoul(f, nullptr, 0));
         if (std::find(seq.begin(), seq.end(), lm) != seq.end()) seq.assign(1, lm);
     }
@@ -1307,7 +1315,7 @@ bool cuckoo6(const std::vector<std::array<uint32_t, 4>>& keys, uint32_t cap, uin
 
 }  // namespace
 
-bool build_cls16(const std::vector<SemRule>& sem, uint32_t n_rules, Cls16Image& img, std::string& why) {
+static bool build_cls16_one(const std::vector<SemRule>& sem, uint32_t n_rules, Cls16Image& img, std::string& why) {
     img = Cls16Image();
     Side side[2];                                         // 0 src, 1 dst
     for (const SemRule& s : sem) {
@@ -1452,7 +1460,7 @@ bool build_cls16(const std::vector<SemRule>& sem, uint32_t n_rules, Cls16Image& 
         opt.tail.resize(align4(uint32_t(opt.tail.size())));
     }
     opt.hot_addr = side[0].root[0];                       // IPv4 sources matching no prefix
-    if (!build_cls4(img.sem, n_rules, img.core, why, &opt)) return false;
+    if (!build_cls4_one(img.sem, n_rules, img.core, why, &opt)) return false;
     const uint32_t tail = img.core.off_tail;
     for (int sd = hosts ? 1 : 0; sd < 2; ++sd) {
         img.fe_key[sd] = tail + rel_key[sd];
@@ -1471,6 +1479,91 @@ bool build_cls16(const std::vector<SemRule>& sem, uint32_t n_rules, Cls16Image& 
         for (size_t pos = 0; pos < slot6.size(); ++pos)
             if (slot6[pos] >= 0) c.words[img.r6 / 4 + pos] = c.row_of(side[0].base[1][size_t(slot6[pos])]);
     }
+    return true;
+}
+
+}  // namespace cls
+
+// ---------------------------------------------------------------------------
+// Orientation: the classifier keys its classes on the packet's source
+// address.  evalACL tests the two networks symmetrically (a dst parse error
+// is a FAIL term once the src matched, aclengine_mock.go:513-524, which
+// SemRule already states as dst ANY + FAIL), so the same rules with src and
+// dst exchanged, run on packets with src and dst exchanged, give the same
+// first match.  Tables keyed on destinations (a pod's egress list from IP
+// blocks: one source class, every rule in one long list) compile far better
+// that way.
+// ---------------------------------------------------------------------------
+namespace cls {
+
+std::vector<SemRule> swap_sides(const std::vector<SemRule>& sem) {
+    std::vector<SemRule> out(sem);
+    for (SemRule& r : out) {
+        std::swap(r.src_any, r.dst_any);
+        std::swap(r.src, r.dst);
+    }
+    return out;
+}
+
+namespace {
+
+// (LDS-resident, every slot in LDS, not the template scan, list mode, -LDS bytes)
+std::array<int64_t, 5> image_rank(const Cls4Image& m) {
+    return {m.lds_ok ? 1 : 0, m.n_lctr == m.n_ctr ? 1 : 0, m.list_mode >= 1 ? 1 : 0, int64_t(m.list_mode),
+            -int64_t(m.lds_bytes)};
+}
+
+bool good_enough(const Cls4Image& m) { return m.lds_ok && m.n_lctr == m.n_ctr && m.list_mode >= 1; }
+
+// CONTIVCLS_ORIENT=src|dst (diagnostics, tests): one orientation only
+int forced_orient() {
+    const char* f = std::getenv("CONTIVCLS_ORIENT");
+    if (!f) return -1;
+    return std::strcmp(f, "dst") == 0 ? 1 : 0;
+}
+
+}  // namespace
+
+bool build_cls4(const std::vector<SemRule>& sem, uint32_t n_rules, Cls4Image& img, std::string& why,
+                const Cls4Opts* opt) {
+    const int f = opt ? 0 : forced_orient();
+    if (f == 1) {
+        if (!build_cls4_one(swap_sides(sem), n_rules, img, why, opt)) return false;
+        img.swap = 1;
+        return true;
+    }
+    const bool ok = build_cls4_one(sem, n_rules, img, why, opt);
+    if (f == 0 || opt || (ok && good_enough(img))) return ok;
+    Cls4Image alt;
+    std::string why2;
+    if (!build_cls4_one(swap_sides(sem), n_rules, alt, why2, nullptr)) return ok;
+    if (ok && !(image_rank(alt) > image_rank(img))) return true;
+    img = std::move(alt);
+    img.swap = 1;
+    return true;
+}
+
+bool build_other4(const std::vector<SemRule>& sem, uint32_t n_rules, Cls4Image& img, std::string& why) {
+    Cls4Opts opt;
+    opt.other = true;
+    return build_cls4_one(sem, n_rules, img, why, &opt);
+}
+
+bool build_cls16(const std::vector<SemRule>& sem, uint32_t n_rules, Cls16Image& img, std::string& why) {
+    const int f = forced_orient();
+    if (f == 1) {
+        if (!build_cls16_one(swap_sides(sem), n_rules, img, why)) return false;
+        img.core.swap = 1;
+        return true;
+    }
+    const bool ok = build_cls16_one(sem, n_rules, img, why);
+    if (f == 0 || (ok && good_enough(img.core))) return ok;
+    Cls16Image alt;
+    std::string why2;
+    if (!build_cls16_one(swap_sides(sem), n_rules, alt, why2)) return ok;
+    if (ok && !(image_rank(alt.core) > image_rank(img.core))) return true;
+    img = std::move(alt);
+    img.core.swap = 1;
     return true;
 }
 

@@ -58,6 +58,7 @@ __host__ __device__ inline uint32_t lpm_h1(uint32_t k, uint32_t mul, uint32_t L)
 enum : uint8_t { RES_DENY = 0, RES_PERMIT = 1, RES_REFLECT = 2, RES_FAIL = 3 };
 enum : int { P_TCP = 0, P_UDP = 1, P_ICMP = 2, P_OTHER = 3, NPROTO = 4 };
 
+
 struct Term {
     bool term = false;     // false = SKIP (rule never matches this protocol)
     uint16_t lo = 0, hi = 0xFFFF;
@@ -100,6 +101,8 @@ struct alignas(16) LinRule16 {
 static_assert(sizeof(LinRule16) == 64, "LinRule16 layout");
 
 std::vector<LinRule4> linear4(const std::vector<SemRule>& sem);
+// the rules with src and dst exchanged (Cls4Image::swap)
+std::vector<SemRule> swap_sides(const std::vector<SemRule>& sem);
 std::vector<LinRule16> linear16(const std::vector<SemRule>& sem);
 
 // ---- IPv4 classifier image -------------------------------------------------
@@ -118,7 +121,7 @@ struct Cls4Image {
     uint32_t hash_mask[kMaxHashLens] = {}, hash_shift[kMaxHashLens] = {};  // shift = 32 - L
     uint32_t hash_mul[kMaxHashLens] = {};
     uint32_t hash_cap[kMaxHashLens] = {}, off_hash[kMaxHashLens] = {};
-    // class rows: a class's 3 cells (TCP, UDP, ICMP) at off_cells + class x
+    // class rows: a class's n_cells cells at off_cells + class x
     // row_bytes; hash entries hold that byte address, not the class index
     uint32_t row_bytes = 12;
     uint32_t default_row = 0;      // hash mode: row of default_class
@@ -141,12 +144,21 @@ struct Cls4Image {
     uint32_t n_hot = 1;
     uint32_t off_hot = 0;
     // Counter tiers: slots [n_hot, n_lctr) are LDS counters after the image,
-    // u32 (ctr16 = 0) or u16 (ctr16 = 1: a lane whose add takes a counter to
-    // 0x8000 moves 0x8000 to the slot's global counter); slots [n_lctr,
-    // n_ctr) are counted in global memory (wave-aggregated atomics).
+    // u32 (ctr16 = 0, then n_lctr = n_ctr) or u16 (ctr16 = 1: a lane whose
+    // add takes a counter to 0x8000 moves 0x8000 to the slot's global
+    // counter); slots [n_lctr, n_ctr) are counted in global memory
+    // (wave-aggregated atomics).
     uint32_t n_lctr = 0;
     uint32_t ctr16 = 0;
+    // Cells per class: 3 -- TCP, UDP, ICMP (a packet's cell is min(proto,
+    // 2)); 1 -- OTHER alone (Cls4Opts::other)
+    uint32_t n_cells = 3;
     bool lds_ok = false;           // image and LDS counters fit the LDS budget (place_counters)
+    // 1: classes are keyed on the packet's DESTINATION address (built from the
+    // rules with src and dst exchanged, compile.cpp build_cls4): the caller
+    // passes the packet's dst as the kernel's src and vice versa; the linear
+    // fallback rules (lin) are in that exchanged frame too
+    uint32_t swap = 0;
     uint32_t off_tail = 0;         // Cls4Opts::tail words (read-only, after the sections above)
     // host only: the elementary source intervals and their classes
     std::vector<uint32_t> h_bounds;
@@ -158,13 +170,24 @@ struct Cls4Opts {
     std::vector<uint32_t> tail;    // extra read-only words appended to the image
     int64_t hot_addr = -1;         // the hot class is this address's (default: the widest)
     bool ext_src = false;          // no source lookup sections (mode 3: the caller finds rows)
+    // The OTHER image: one cell per class for protocol values outside
+    // ProtocolType (evalACL's switch has no case for them,
+    // aclengine_mock.go:527-643: the networks alone decide), interval search
+    // and template scan, read from global memory by the few lanes holding
+    // such a packet (kernels.hip run_n).  Its slots follow the main image's.
+    bool other = false;
 };
+
+// The OTHER image of a rule set (in the main image's orientation: pass the
+// swapped rules for a destination-keyed one).
+bool build_other4(const std::vector<SemRule>& sem, uint32_t n_rules, Cls4Image& img, std::string& why);
 
 uint32_t lds_budget();
 bool place_counters(Cls4Image& img, uint32_t budget, bool partial);
 
-// Build the image; returns false (with reason) if the table does not fit the
-// 16-bit list / template indices.
+// Build the image in the better orientation (Cls4Image::swap); returns false
+// (with reason) if the table does not fit the 16-bit list / template indices.
+// With opt (the 16-byte core): the given orientation only.
 bool build_cls4(const std::vector<SemRule>& sem, uint32_t n_rules, Cls4Image& img,
                 std::string& why, const Cls4Opts* opt = nullptr);
 

@@ -57,6 +57,7 @@ struct Scratch {
 struct Counters {
     uint32_t n_slots = 0;
     uint32_t n_lctr = 0;           // slots counted in LDS (their partial rows)
+    uint32_t n_image = 0;          // slots of the classifier images; the direct rule slots follow
     DevBuf d_csr;                  // uint2 {slot, rule}, grouped by rule
     std::map<hipStream_t, std::unique_ptr<Scratch>> sc;
     ~Counters() {
@@ -78,6 +79,8 @@ struct Table {
     bool has_cls = false;
     Cls4Image img;
     DevBuf d_img;
+    Cls4Image oimg;            // protocols > 2 (compile.hpp Cls4Opts::other), read from global memory
+    DevBuf d_oimg;
     int kernel = 0;            // 0 linear, 1 classifier
     bool lds_resident = false;
     // 16-byte layout (IPv6 / IPv4-mapped): classifier over 32-bit reps
@@ -85,8 +88,9 @@ struct Table {
         bool ok = false;
         std::string why;           // why there is none
         Cls16Image img;
-        std::vector<LinRule4> lin; // rules in rep space (protocol > 2, FORCE_LINEAR)
-        DevBuf d_img, d_lin;
+        std::vector<LinRule4> lin; // rules in rep space (FORCE_LINEAR)
+        Cls4Image oimg;            // protocols > 2, rep space
+        DevBuf d_img, d_lin, d_oimg;
         DevBuf d_src_search;       // src_mode 1: the source interval table (global memory)
         bool lds_resident = false;
     } p16;
@@ -192,12 +196,18 @@ const char* cls_last_error(const cls_engine* e) { return e ? e->err.c_str() : "n
 // ---------------------------------------------------------------------------
 // The slot -> rule map of a table variant as the remap kernel reads it: every
 // slot once, grouped by rule (slot order within a rule).
-static int counters_init(cls_engine* e, Counters& c, const Cls4Image* img, uint32_t n_rules) {
-    const uint32_t n_cls = img ? img->n_ctr : 0;
-    c.n_slots = n_cls + n_rules + 1;
+// Slots: the main image's, the OTHER image's, then one per rule plus the
+// default DENY (the linear kernel's).
+static int counters_init(cls_engine* e, Counters& c, const Cls4Image* img, const Cls4Image* oimg,
+                         uint32_t n_rules) {
+    const uint32_t n_cls = img ? img->n_ctr : 0, n_oth = oimg ? oimg->n_ctr : 0;
+    c.n_slots = n_cls + n_oth + n_rules + 1;
     c.n_lctr = img ? img->n_lctr : 0;
+    c.n_image = n_cls + n_oth;
     std::vector<uint32_t> cnt(size_t(n_rules) + 2, 0);
-    auto rule_of = [&](uint32_t i) { return i < n_cls ? img->ctr_rule[i] : i - n_cls; };
+    auto rule_of = [&](uint32_t i) {
+        return i < n_cls ? img->ctr_rule[i] : i < n_cls + n_oth ? oimg->ctr_rule[i - n_cls] : i - n_cls - n_oth;
+    };
     for (uint32_t i = 0; i < c.n_slots; ++i) cnt[rule_of(i) + 1]++;
     for (size_t r = 1; r < cnt.size(); ++r) cnt[r] += cnt[r - 1];
     std::vector<uint32_t> csr(size_t(c.n_slots) * 2);
@@ -208,6 +218,20 @@ static int counters_init(cls_engine* e, Counters& c, const Cls4Image* img, uint3
     }
     HIPC(e, c.d_csr.ensure(csr.size() * 4));
     HIPC(e, hipMemcpy(c.d_csr.p, csr.data(), csr.size() * 4, hipMemcpyHostToDevice));
+    return CLS_OK;
+}
+
+// The main classifier of a rule set and its OTHER image (protocols > 2), in
+// the main image's orientation.
+static bool build_pair(const std::vector<SemRule>& sem, uint32_t n, Cls4Image& img, Cls4Image& oimg,
+                       std::string& why) {
+    if (!build_cls4(sem, n, img, why)) return false;
+    return build_other4(img.swap ? swap_sides(sem) : sem, n, oimg, why);
+}
+
+static int upload(cls_engine* e, DevBuf& d, const Cls4Image& im) {
+    HIPC(e, d.ensure(im.img_bytes));
+    HIPC(e, hipMemcpy(d.p, im.words.data(), im.img_bytes, hipMemcpyHostToDevice));
     return CLS_OK;
 }
 
@@ -232,16 +256,17 @@ static int table_put_locked(cls_engine* e, const char* name, const cls_rule* rul
     // classifier for anything but tiny tables
     t->kernel = 0;
     if (sem.size() > 8) {
-        if (build_cls4(sem, n, t->img, why)) {
+        if (build_pair(sem, n, t->img, t->oimg, why)) {
             t->has_cls = true;
             t->kernel = 1;
             t->lds_resident = t->img.lds_ok && t->img.lds_bytes <= uint32_t(max_lds_bytes());
-            HIPC(e, t->d_img.ensure(t->img.img_bytes));
-            HIPC(e, hipMemcpy(t->d_img.p, t->img.words.data(), t->img.img_bytes, hipMemcpyHostToDevice));
+            rc = upload(e, t->d_img, t->img);
+            if (rc == CLS_OK) rc = upload(e, t->d_oimg, t->oimg);
+            if (rc != CLS_OK) return rc;
         }
     }
     {
-        const int rc2 = counters_init(e, t->c4, t->has_cls ? &t->img : nullptr, n);
+        const int rc2 = counters_init(e, t->c4, t->has_cls ? &t->img : nullptr, t->has_cls ? &t->oimg : nullptr, n);
         if (rc2 != CLS_OK) return rc2;
     }
     // 16-byte layout: both families' reductions over one rep space
@@ -251,18 +276,19 @@ static int table_put_locked(cls_engine* e, const char* name, const cls_rule* rul
         rc = semantic_rules(rules, n, 0, s16, why);
         if (rc != CLS_OK) return fail(e, rc, "%s", why.c_str());
         std::string why16;
-        q.ok = build_cls16(s16, n, q.img, why16);
+        q.ok = build_cls16(s16, n, q.img, why16) && build_other4(q.img.sem, n, q.oimg, why16);
         q.why = why16;
         if (q.ok) {
             const Cls4Image& c = q.img.core;
             q.lin = linear4(q.img.sem);
             q.lds_resident = c.lds_ok && c.lds_bytes <= uint32_t(max_lds_bytes());
-            HIPC(e, q.d_img.ensure(c.img_bytes));
-            HIPC(e, hipMemcpy(q.d_img.p, c.words.data(), c.img_bytes, hipMemcpyHostToDevice));
+            rc = upload(e, q.d_img, c);
+            if (rc == CLS_OK) rc = upload(e, q.d_oimg, q.oimg);
+            if (rc != CLS_OK) return rc;
             HIPC(e, q.d_lin.ensure(std::max<size_t>(1, q.lin.size()) * sizeof(LinRule4)));
             if (!q.lin.empty())
                 HIPC(e, hipMemcpy(q.d_lin.p, q.lin.data(), q.lin.size() * sizeof(LinRule4), hipMemcpyHostToDevice));
-            const int rc2 = counters_init(e, t->c16, &c, n);
+            const int rc2 = counters_init(e, t->c16, &c, &q.oimg, n);
             if (rc2 != CLS_OK) return rc2;
             if (q.img.src_mode == 1) {
                 HIPC(e, q.d_src_search.ensure(q.img.src_search.size() * 4));
@@ -311,6 +337,7 @@ int cls_table_get_info(cls_engine* e, uint32_t table_id, cls_table_info* info) {
         info->n_lctr = t.img.n_lctr;
         info->ctr16 = t.img.ctr16;
         info->list_mode = t.img.list_mode;
+        info->swap = t.img.swap;
     }
     info->has_v16 = t.p16.ok ? 1u : 0u;
     if (t.p16.ok) {
@@ -384,6 +411,15 @@ static Cls4Dev cls4_dev(const Cls4Image& im, const DevBuf& d_img, const DevBuf& 
         cd.off_hash[i] = im.off_hash[i];
     }
     return cd;
+}
+
+// The v4 classifier of a table (its kernel never reads the linear rules:
+// every protocol has a cell).
+static Cls4Dev table_dev(const Table& t) { return cls4_dev(t.img, t.d_img, DevBuf(), 0, t.n_rules); }
+
+// Packets in an image's frame: src and dst exchanged for a destination-keyed one.
+static Pkts4 framed(const Cls4Image& im, const Pkts4& p) {
+    return im.swap ? Pkts4{p.dst, p.src, p.dport, p.proto, p.n} : p;
 }
 
 // Workgroups of a classify launch: persistent grid, as many per CU as LDS
@@ -536,12 +572,14 @@ static int classify16_locked(cls_engine* e, std::shared_ptr<Table> t, const cls_
     bool zeroed = false;
     if (n) {
         Cls4Dev cd = cls4_dev(c, q.d_img, q.d_lin, uint32_t(q.lin.size()), t->n_rules);
+        cfg.other = cls4_dev(q.oimg, q.d_oimg, DevBuf(), 0, t->n_rules);
         if (q.lds_resident) cd.part = sc->part.as<uint32_t>();
         Fe16 fe = fe16(q.img, q.d_src_search);
         for (uint64_t off = 0; off < n; off += kClsChunk) {
             const uint64_t m = std::min<uint64_t>(kClsChunk, n - off);
             Pkts16 pc{reinterpret_cast<const uint4*>(src + 16 * off), reinterpret_cast<const uint4*>(dst + 16 * off),
                       dp + off, pr + off, m, 0u};
+            if (c.swap) std::swap(pc.src, pc.dst);          // destination-keyed image
             uint8_t* vo = d_verdict ? d_verdict + off : nullptr;
             pc.vec = aligned(pc.dport, 8) && aligned(pc.proto, 4) && (!vo || aligned(vo, 4)) ? 1u : 0u;
             HIPC(e, launch_classify16_cls(cd, fe, pc, vo, slot_val, q.lds_resident, lin, cfg));
@@ -620,12 +658,13 @@ int cls_classify(cls_engine* e, uint32_t table_id, const cls_pkt_soa* pk, uint64
     bool zeroed = false;
     if (n) {
         if (use_cls) {
-            Cls4Dev cd = cls4_dev(t->img, t->d_img, t->d_lin4, uint32_t(t->lin4.size()), t->n_rules);
+            Cls4Dev cd = table_dev(*t);
+            cfg.other = cls4_dev(t->oimg, t->d_oimg, DevBuf(), 0, t->n_rules);
             if (t->lds_resident) cd.part = sc->part.as<uint32_t>();
             // the kernel indexes packets with 32-bit offsets: chunks of 2^30
             for (uint64_t off = 0; off < n; off += kClsChunk) {
                 const uint64_t m = std::min<uint64_t>(kClsChunk, n - off);
-                const Pkts4 pc{p.src + off, p.dst + off, p.dport + off, p.proto + off, m};
+                const Pkts4 pc = framed(t->img, Pkts4{p.src + off, p.dst + off, p.dport + off, p.proto + off, m});
                 HIPC(e, launch_classify4_cls(cd, pc, d_verdict ? d_verdict + off : nullptr, slot_val,
                                              t->lds_resident, vec, cfg));
                 if (timing && off + m >= n) HIPC(e, hipEventRecord(e->ev1, s));
@@ -636,7 +675,7 @@ int cls_classify(cls_engine* e, uint32_t table_id, const cls_pkt_soa* pk, uint64
                 }
             }
         } else {
-            const uint32_t base = t->has_cls ? t->img.n_ctr : 0;
+            const uint32_t base = t->c4.n_image;
             HIPC(e, launch_classify4_linear(t->d_lin4.as<LinRule4>(), uint32_t(t->lin4.size()), t->n_rules, p,
                                             d_verdict, slot_val + base, cfg));
         }
@@ -665,22 +704,47 @@ int cls_stream_floor(cls_engine* e, const cls_pkt_soa* pk, uint64_t n, uint8_t* 
                aligned(verdict, 4))
            : !(pk->af == CLS_AF_V16 && aligned(pk->src16, 16) && aligned(pk->dst16, 16)))
         return fail(e, CLS_E_INVAL, "stream floor: device arrays of the classify kernel's alignment");
-    const int grid = e->n_cu;                  // one 1024-thread workgroup per CU, as the LDS-resident classify
+    // diagnostics: the same stream over buffers this library allocates
+    DevBuf own[5];
+    if (v4 && std::getenv("CONTIVCLS_FLOOR_OWN")) {
+        const size_t sz[5] = {n * 4, n * 4, n * 2, n, n};
+        const void* from[5] = {pk->src4, pk->dst4, pk->dport, pk->proto, verdict};
+        for (int i = 0; i < 5; ++i) {
+            HIPC(e, own[i].ensure(sz[i]));
+            HIPC(e, hipMemcpyAsync(own[i].p, from[i], sz[i], hipMemcpyDeviceToDevice, s));
+        }
+        p4 = Pkts4{own[0].as<uint32_t>(), own[1].as<uint32_t>(), own[2].as<uint16_t>(), own[3].as<uint8_t>(), n};
+        verdict = own[4].as<uint8_t>();
+    }
+    // the floor is the fastest of the stream shapes: one or two 1024-thread
+    // workgroups per CU (the classify kernel runs one when its LDS image
+    // takes more than half the CU's LDS), loads one step ahead or not, the
+    // protocol stream non-temporal or cached
     hipEvent_t a, b;
     HIPC(e, hipEventCreate(&a));
     HIPC(e, hipEventCreate(&b));
     int rc = CLS_OK;
     const uint32_t k = std::max<uint32_t>(1, reps);
-    for (uint32_t i = 0; i <= k && rc == CLS_OK; ++i) {   // launch 0: warm-up
-        if (i == 1 && hipEventRecord(a, s) != hipSuccess) rc = CLS_E_HIP;
-        if (rc == CLS_OK && launch_stream(v4 ? &p4 : nullptr, v4 ? nullptr : &p16, verdict, grid, s) != hipSuccess)
-            rc = fail(e, CLS_E_HIP, "stream floor launch failed");
+    const bool dbg = std::getenv("CONTIVCLS_DEBUG_FLOOR") != nullptr;
+    *ms = 0.0f;
+    for (int shape = 0; shape < (v4 ? 8 : 2) && rc == CLS_OK; ++shape) {
+        const int grid = e->n_cu * (1 + (shape & 1)), variant = shape >> 1;
+        for (uint32_t i = 0; i <= k && rc == CLS_OK; ++i) {   // launch 0: warm-up
+            if (i == 1 && hipEventRecord(a, s) != hipSuccess) rc = CLS_E_HIP;
+            if (rc == CLS_OK &&
+                launch_stream(v4 ? &p4 : nullptr, v4 ? nullptr : &p16, verdict, grid, variant, s) != hipSuccess)
+                rc = fail(e, CLS_E_HIP, "stream floor launch failed");
+        }
+        float t = 0.0f;
+        if (rc == CLS_OK && hipEventRecord(b, s) == hipSuccess && hipEventSynchronize(b) == hipSuccess &&
+            hipEventElapsedTime(&t, a, b) == hipSuccess) {
+            t /= float(k);
+            if (dbg) std::fprintf(stderr, "stream floor: grid %d variant %d: %.4f ms\n", grid, variant, t);
+            if (*ms == 0.0f || t < *ms) *ms = t;
+        } else if (rc == CLS_OK) {
+            rc = fail(e, CLS_E_HIP, "stream floor timing failed");
+        }
     }
-    if (rc == CLS_OK && hipEventRecord(b, s) == hipSuccess && hipEventSynchronize(b) == hipSuccess &&
-        hipEventElapsedTime(ms, a, b) == hipSuccess)
-        *ms /= float(k);
-    else if (rc == CLS_OK)
-        rc = fail(e, CLS_E_HIP, "stream floor timing failed");
     (void)hipEventDestroy(a);
     (void)hipEventDestroy(b);
     return rc;
@@ -908,9 +972,10 @@ int cls_connect_batch(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t*
             Table& t = *dtab[big[b]];
             uint8_t* pre = e->s_pre.as<uint8_t>() + b * 2 * n;
             desc[big[b]].pre = pre;
-            Cls4Dev cd = cls4_dev(t.img, t.d_img, t.d_lin4, uint32_t(t.lin4.size()), t.n_rules);
+            Cls4Dev cd = table_dev(t);
             LaunchCfg cfg;
             cfg.stream = s;
+            cfg.other = cls4_dev(t.oimg, t.d_oimg, DevBuf(), 0, t.n_rules);
             cfg.grid = cls_grid(e, true, t.lds_resident, t.img.lds_bytes, n);
             Scratch* sc = nullptr;
             {
@@ -919,7 +984,7 @@ int cls_connect_batch(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t*
             }
             if (t.lds_resident) cd.part = sc->part.as<uint32_t>();
             unsigned long long* slot_val = sc->slot_val.as<unsigned long long>();
-            const Pkts4 syn{src, dst, dp, pr, n}, ack{dst, src, sp, pr, n};
+            const Pkts4 syn = framed(t.img, Pkts4{src, dst, dp, pr, n}), ack = framed(t.img, Pkts4{dst, src, sp, pr, n});
             for (int k = 0; k < 2; ++k) {
                 const Pkts4& q = k ? ack : syn;
                 const bool vec = aligned(q.src, 16) && aligned(q.dst, 16) && aligned(q.dport, 8) &&
@@ -981,7 +1046,8 @@ int cls_gen_traffic_v4(cls_engine* e, const cls_traffic_spec* sp, uint64_t first
 // bytes of a larger header), image, slot -> rule map, linear rules.
 static int write_blob(const Cls4Image* img, const std::vector<LinRule4>& lin, uint32_t n, uint32_t magic,
                       const void* extra, size_t extra_bytes, void* blob, uint64_t cap, uint64_t* need,
-                      const std::vector<uint32_t>* trailer = nullptr, size_t trailer_field = 0) {
+                      const std::vector<uint32_t>* trailer = nullptr, size_t trailer_field = 0,
+                      const Cls4Image* other = nullptr) {
     cls_image_v4_header h;
     std::memset(&h, 0, sizeof h);
     h.magic = magic;
@@ -1015,6 +1081,7 @@ static int write_blob(const Cls4Image* img, const std::vector<LinRule4>& lin, ui
         h.off_hot = im.off_hot;
         h.n_lctr = im.n_lctr;
         h.ctr16 = im.ctr16;
+        h.swap = im.swap;
         for (uint32_t i = 0; i < kMaxHashLens; ++i) {
             h.hash_mask[i] = im.hash_mask[i];
             h.hash_shift[i] = im.hash_shift[i];
@@ -1030,6 +1097,12 @@ static int write_blob(const Cls4Image* img, const std::vector<LinRule4>& lin, ui
     h.total_bytes = uint32_t(h.off_lin + lin.size() * sizeof(LinRule4));
     const uint32_t off_trailer = uint32_t(al(h.total_bytes));
     if (trailer) h.total_bytes = off_trailer + uint32_t(trailer->size() * 4);
+    uint64_t need_o = 0;                      // the OTHER image: a nested blob (magic "CLSO")
+    if (other) {
+        write_blob(other, {}, n, 0x434C534Fu, nullptr, 0, nullptr, 0, &need_o);
+        h.off_other = uint32_t(al(h.total_bytes));
+        h.total_bytes = h.off_other + uint32_t(need_o);
+    }
     *need = h.total_bytes;
     if (!blob || cap < h.total_bytes) return CLS_OK;
     uint8_t* b = static_cast<uint8_t*>(blob);
@@ -1045,6 +1118,7 @@ static int write_blob(const Cls4Image* img, const std::vector<LinRule4>& lin, ui
         std::memcpy(b + h.off_ctr_rule, img->ctr_rule.data(), size_t(h.n_ctr) * 4);
     }
     if (!lin.empty()) std::memcpy(b + h.off_lin, lin.data(), lin.size() * sizeof(LinRule4));
+    if (other) write_blob(other, {}, n, 0x434C534Fu, nullptr, 0, b + h.off_other, need_o, &need_o);
     return CLS_OK;
 }
 
@@ -1094,9 +1168,10 @@ int cls_compile_v4(const cls_rule* rules, uint32_t n, void* blob, uint64_t cap, 
     int rc = semantic_rules(rules, n, 4, sem, why);
     if (rc != CLS_OK) return rc;
     std::vector<LinRule4> lin = linear4(sem);
-    Cls4Image img;
-    const bool has = sem.size() > 8 && build_cls4(sem, n, img, why);
-    return write_blob(has ? &img : nullptr, lin, n, 0x434C5334u, nullptr, 0, blob, cap, need);
+    Cls4Image img, oimg;
+    const bool has = sem.size() > 8 && build_pair(sem, n, img, oimg, why);
+    return write_blob(has ? &img : nullptr, lin, n, 0x434C5334u, nullptr, 0, blob, cap, need, nullptr, 0,
+                      has ? &oimg : nullptr);
 }
 
 int cls_compile_v16(const cls_rule* rules, uint32_t n, void* blob, uint64_t cap, uint64_t* need) {
@@ -1106,7 +1181,8 @@ int cls_compile_v16(const cls_rule* rules, uint32_t n, void* blob, uint64_t cap,
     int rc = semantic_rules(rules, n, 0, sem, why);
     if (rc != CLS_OK) return rc;
     Cls16Image img;
-    if (!build_cls16(sem, n, img, why)) return CLS_E_INVAL;
+    Cls4Image oimg;
+    if (!build_cls16(sem, n, img, why) || !build_other4(img.sem, n, oimg, why)) return CLS_E_INVAL;
     cls_image_v16_header h16;
     std::memset(&h16, 0, sizeof h16);
     for (int sd = 0; sd < 2; ++sd) {
@@ -1126,7 +1202,7 @@ int cls_compile_v16(const cls_rule* rules, uint32_t n, void* blob, uint64_t cap,
     const size_t extra = sizeof h16 - sizeof h16.core;
     return write_blob(&img.core, linear4(img.sem), n, 0x434C3136u, reinterpret_cast<const uint8_t*>(&h16) + sizeof h16.core,
                       extra, blob, cap, need, img.src_mode == 1 ? &img.src_search : nullptr,
-                      offsetof(cls_image_v16_header, off_src_search) - sizeof h16.core);
+                      offsetof(cls_image_v16_header, off_src_search) - sizeof h16.core, &oimg);
 }
 
 }  // extern "C"

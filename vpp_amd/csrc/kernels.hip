@@ -413,12 +413,14 @@ __device__ __forceinline__ void wave_count(unsigned long long* gslot, uint32_t k
     }
 }
 
-// Classify N packets and count their slots.  pr_any: some packet of the
-// group has a protocol outside TCP/UDP/ICMP.  kCtr (LDS-resident image): 0 --
+// Classify N packets and count their slots.  kCtr (LDS-resident image): 0 --
 // every slot has a u32 LDS counter; 1 -- u16 LDS counters for slots <
 // n_lctr (compile.hpp Cls4Image counter tiers), global counters above.
+// pr_any: some packet of the group has a protocol outside TCP/UDP/ICMP; those
+// packets are classified on the OTHER image `o` (global memory) from `sl`
+// (their source, or its rep on the 16-byte path).
 template <int N, bool kLds, int kMode, int kList, int kD, int kCtr>
-__device__ __forceinline__ void run_n(const Img<kLds>& im, const Cls4Dev& t, uint32_t hot_lane,
+__device__ __forceinline__ void run_n(const Img<kLds>& im, const Cls4Dev& t, const Cls4Dev& o, uint32_t hot_lane,
                                       unsigned long long* gslot, uint32_t& hot0,
                                       const uint32_t (&s)[N], const uint32_t (&d)[N],
                                       const uint32_t (&dp)[N], const uint32_t (&pr)[N],
@@ -463,7 +465,8 @@ __device__ __forceinline__ void run_n(const Img<kLds>& im, const Cls4Dev& t, uin
             }
             wave_count(gslot, key);
         } else {
-            // Global counters (image not LDS-resident)
+            // Global counters (image not LDS-resident); slot 0 (default DENY,
+            // the hottest) is counted per lane and added once at the end
             uint32_t key = pr[q] <= 2u ? slot[q] : 0xFFFFFFFFu;
             if (key == 0u) {
                 ++hot0;
@@ -474,24 +477,39 @@ __device__ __forceinline__ void run_n(const Img<kLds>& im, const Cls4Dev& t, uin
     }
     // Protocols outside TCP/UDP/ICMP fall through evalACL's switch
     // (aclengine_mock.go:508-664): networks alone decide.  Rare; taken per
-    // wave only when some lane holds such a packet.
+    // wave only when some lane holds such a packet: the OTHER image's
+    // interval search and candidate scan from global memory (L2), its slots
+    // after the main image's.
     if (__any(pr_any)) {
+        const uint32_t zero[N] = {};
+        uint32_t ores[N], oslot[N];
+        classify_n<N, false, 0, 0, -1>(Img<false>{reinterpret_cast<const uint8_t*>(o.img)}, o, sl, d, dp, zero,
+                                       ores, oslot);
 #pragma unroll
         for (int q = 0; q < N; ++q) {
-            if (pr[q] > 2u) {
-                if constexpr (kLds && kCtr == 0)                      // undo the cell count
-                    __hip_atomic_fetch_add(lctr_t(addr[q]), ~0u, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_WORKGROUP);
-                uint32_t rule;
-                linear_one(t.lin, t.n_lin, t.n_rules, sl[q], d[q], dp[q], 3u, res[q], rule);
-                atomicAdd(&gslot[t.n_ctr + rule], 1ull);
+            const bool other = pr[q] > 2u;
+            if constexpr (kLds && kCtr == 0) {                        // undo the main image's count
+                if (other)
+                    __hip_atomic_fetch_add(lctr_t(addr[q]), ~0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
+            res[q] = other ? ores[q] : res[q];
+            wave_count(gslot, other ? t.n_ctr + oslot[q] : 0xFFFFFFFFu);
         }
     }
 }
 
 #ifndef CLS_GROUPS
 #define CLS_GROUPS 1
+#endif
+// The protocol stream (4 B per lane) as a cached load, the others
+// non-temporal: tools/nt_sweep.hip measured this mix as the fastest stream
+// of the 32 combinations (0.523 vs 0.566 ms per 256 Mi packets all-nt).
+#ifndef CLS_NT_PROTO
+#define CLS_NT_PROTO 0
+#endif
+// 16-byte kernel: dport / proto (2 B / 1 B per lane) non-temporal
+#ifndef CLS_NT16_SMALL
+#define CLS_NT16_SMALL 1
 #endif
 #ifndef CLS_PREFETCH
 #define CLS_PREFETCH 1
@@ -534,7 +552,7 @@ __device__ __forceinline__ void flush_lds(const Cls4Dev& t, uint4* smem) {
 }
 
 template <bool kLds, bool kVec, int kMode, int kList, int kD, int kCtr>
-__global__ __launch_bounds__(kClsBlock) void classify4_cls(Cls4Dev t, Pkts4 p, uint8_t* verdict,
+__global__ __launch_bounds__(kClsBlock) void classify4_cls(Cls4Dev t, Cls4Dev o, Pkts4 p, uint8_t* verdict,
                                                            unsigned long long* gslot) {
     extern __shared__ uint4 smem[];
     Img<kLds> im{reinterpret_cast<const uint8_t*>(t.img)};
@@ -568,7 +586,8 @@ __global__ __launch_bounds__(kClsBlock) void classify4_cls(Cls4Dev t, Pkts4 p, u
                 for (int k = 0; k < kG; ++k) {
                     const uint32_t gi = g + uint32_t(k) * nthreads;
                     b.s[k] = ldnt(at(S, gi)); b.d[k] = ldnt(at(D, gi));
-                    b.dp[k] = ldnt(at(DP, gi)); b.pr[k] = ldnt(at(PR, gi));
+                    b.dp[k] = ldnt(at(DP, gi));
+                    b.pr[k] = CLS_NT_PROTO ? ldnt(at(PR, gi)) : *at(PR, gi);
                 }
             }
         };
@@ -590,7 +609,7 @@ __global__ __launch_bounds__(kClsBlock) void classify4_cls(Cls4Dev t, Pkts4 p, u
                 other |= ((pr | ((pr & 0x7F7F7F7Fu) + 0x7D7D7D7Du)) & 0x80808080u) != 0u;
             }
             uint32_t v[kN];
-            run_n<kN, kLds, kMode, kList, kD, kCtr>(im, t, hot_lane, gslot, hot0, sa, da, pa, ra, other, v, sa);
+            run_n<kN, kLds, kMode, kList, kD, kCtr>(im, t, o, hot_lane, gslot, hot0, sa, da, pa, ra, other, v, sa);
             if (verdict) {
 #pragma unroll
                 for (int k = 0; k < kG; ++k)
@@ -636,8 +655,9 @@ __global__ __launch_bounds__(kClsBlock) void classify4_cls(Cls4Dev t, Pkts4 p, u
             const uint32_t pa[4] = {p2.x & 0xFFFFu, p2.x >> 16, p2.y & 0xFFFFu, p2.y >> 16};
             const uint32_t ra[4] = {pr & 0xFFu, (pr >> 8) & 0xFFu, (pr >> 16) & 0xFFu, pr >> 24};
             uint32_t v[4];
-            run_n<4, kLds, kMode, kList, -1, kCtr>(im, t, hot_lane, gslot, hot0, sa, da, pa, ra,
-                                             ((pr | ((pr & 0x7F7F7F7Fu) + 0x7D7D7D7Du)) & 0x80808080u) != 0u, v, sa);
+            run_n<4, kLds, kMode, kList, -1, kCtr>(im, t, o, hot_lane, gslot, hot0, sa, da, pa, ra,
+                                                   ((pr | ((pr & 0x7F7F7F7Fu) + 0x7D7D7D7Du)) & 0x80808080u) != 0u,
+                                                   v, sa);
             if (verdict)
                 stnt(v[0] | (v[1] << 8) | (v[2] << 16) | (v[3] << 24),
                      const_cast<uint32_t*>(at(reinterpret_cast<const uint32_t*>(verdict), gi)));
@@ -647,7 +667,7 @@ __global__ __launch_bounds__(kClsBlock) void classify4_cls(Cls4Dev t, Pkts4 p, u
     for (uint32_t i = tail_from + tid; i < uint32_t(p.n); i += nthreads) {
         const uint32_t sa[1] = {p.src[i]}, da[1] = {p.dst[i]}, pa[1] = {p.dport[i]}, ra[1] = {p.proto[i]};
         uint32_t v[1];
-        run_n<1, kLds, kMode, kList, -1, kCtr>(im, t, hot_lane, gslot, hot0, sa, da, pa, ra, ra[0] > 2u, v, sa);
+        run_n<1, kLds, kMode, kList, -1, kCtr>(im, t, o, hot_lane, gslot, hot0, sa, da, pa, ra, ra[0] > 2u, v, sa);
         if (verdict) verdict[i] = uint8_t(v[0]);
     }
 
@@ -660,6 +680,7 @@ __global__ __launch_bounds__(kClsBlock) void classify4_cls(Cls4Dev t, Pkts4 p, u
 // The classify kernels' HBM stream without the lookups (bench.py's measured
 // floor): the same loads and stores, in the same order, on the same grid;
 // the verdict is a mix of the packet's fields.
+template <bool kPf, bool kNtPr>
 __global__ __launch_bounds__(kClsBlock) void stream4_kernel(Pkts4 p, uint8_t* verdict) {
     const uint32_t nthreads = gridDim.x * blockDim.x;
     const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
@@ -675,7 +696,8 @@ __global__ __launch_bounds__(kClsBlock) void stream4_kernel(Pkts4 p, uint8_t* ve
     };
     auto load = [&](Buf& b, uint32_t g) {
         if (g < nsteps) {
-            b.s = ldnt(at(S, g)); b.d = ldnt(at(D, g)); b.dp = ldnt(at(DP, g)); b.pr = ldnt(at(PR, g));
+            b.s = ldnt(at(S, g)); b.d = ldnt(at(D, g)); b.dp = ldnt(at(DP, g));
+            b.pr = kNtPr ? ldnt(at(PR, g)) : *at(PR, g);
         }
     };
     auto step = [&](const Buf& b, uint32_t g) {
@@ -683,17 +705,25 @@ __global__ __launch_bounds__(kClsBlock) void stream4_kernel(Pkts4 p, uint8_t* ve
                            0x03030303u;
         stnt(v, const_cast<uint32_t*>(at(reinterpret_cast<const uint32_t*>(verdict), g)));
     };
-    Buf a, b;
-    uint32_t g = tid;
-    load(a, g);
-    while (g < nsteps) {
-        load(b, g + nthreads);
-        step(a, g);
-        g += nthreads;
-        if (g >= nsteps) break;
-        load(a, g + nthreads);
-        step(b, g);
-        g += nthreads;
+    if constexpr (kPf) {
+        Buf a, b;
+        uint32_t g = tid;
+        load(a, g);
+        while (g < nsteps) {
+            load(b, g + nthreads);
+            step(a, g);
+            g += nthreads;
+            if (g >= nsteps) break;
+            load(a, g + nthreads);
+            step(b, g);
+            g += nthreads;
+        }
+    } else {
+        for (uint32_t g = tid; g < nsteps; g += nthreads) {
+            Buf a;
+            load(a, g);
+            step(a, g);
+        }
     }
 }
 
@@ -834,8 +864,8 @@ __device__ __noinline__ uint32_t src_rep_global(const uint8_t* g, uint32_t gval,
 }
 
 template <bool kLds, int kMode, int kList, int kD, bool kLin, int kFe, int kCtr>
-__global__ __launch_bounds__(kClsBlock) void classify16_cls(Cls4Dev t, Fe16 fe, Pkts16 p, uint8_t* verdict,
-                                                            unsigned long long* gslot) {
+__global__ __launch_bounds__(kClsBlock) void classify16_cls(Cls4Dev t, Cls4Dev o, Fe16 fe, Pkts16 p,
+                                                            uint8_t* verdict, unsigned long long* gslot) {
     extern __shared__ uint4 smem[];
     Img<kLds> im{reinterpret_cast<const uint8_t*>(t.img)};
     if constexpr (kLds) stage_lds(t, smem);
@@ -856,19 +886,19 @@ __global__ __launch_bounds__(kClsBlock) void classify16_cls(Cls4Dev t, Fe16 fe, 
         fe_rep(im, fe.key[1], fe.val[1], fe.top[1], fe.k8[1], d16, da);
         if constexpr (kLin) {
             src_rep(s16, sa);
-            lin_n(t, gslot, sa, da, pa, ra, v);
+            lin_n(t, gslot + o.n_ctr, sa, da, pa, ra, v);   // direct rule slots after both images
         } else if constexpr (kFe == 1) {
-            src_hash16(im, fe, s16, sa);
+            src_hash16(im, fe, s16, sa);                       // class rows, not reps
             uint32_t sl[N];
             if (__any(other)) {                                // rare: protocols > 2 need the rep
 #pragma unroll
                 for (int q = 0; q < N; ++q)
                     sl[q] = ra[q] > 2u ? src_rep_global(fe.gsrc, fe.gval, fe.top[0], fe.k8[0], s16[q]) : 0u;
             }
-            run_n<N, kLds, kMode, kList, kD, kCtr>(im, t, hot_lane, gslot, hot0, sa, da, pa, ra, other, v, sl);
+            run_n<N, kLds, kMode, kList, kD, kCtr>(im, t, o, hot_lane, gslot, hot0, sa, da, pa, ra, other, v, sl);
         } else {
             src_rep(s16, sa);
-            run_n<N, kLds, kMode, kList, kD, kCtr>(im, t, hot_lane, gslot, hot0, sa, da, pa, ra, other, v, sa);
+            run_n<N, kLds, kMode, kList, kD, kCtr>(im, t, o, hot_lane, gslot, hot0, sa, da, pa, ra, other, v, sa);
         }
     };
     // 4 packets per lane per step (vector dport / proto / verdict words),
@@ -897,8 +927,13 @@ __global__ __launch_bounds__(kClsBlock) void classify16_cls(Cls4Dev t, Fe16 fe, 
         uint32_t dp[4], pr[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            dp[k] = __builtin_nontemporal_load(p.dport + base + 64u * k);
-            pr[k] = __builtin_nontemporal_load(p.proto + base + 64u * k);
+            if constexpr (CLS_NT16_SMALL) {
+                dp[k] = __builtin_nontemporal_load(p.dport + base + 64u * k);
+                pr[k] = __builtin_nontemporal_load(p.proto + base + 64u * k);
+            } else {
+                dp[k] = p.dport[base + 64u * k];
+                pr[k] = p.proto[base + 64u * k];
+            }
         }
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
@@ -1238,7 +1273,7 @@ static void launch_d(const Cls4Dev& t, const Pkts4& p, uint8_t* verdict, unsigne
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(classify4_cls<kLds, kVec, kMode, kList, kD, kCtr>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
     hipLaunchKernelGGL((classify4_cls<kLds, kVec, kMode, kList, kD, kCtr>), dim3(cfg.grid), dim3(kClsBlock), lds,
-                       cfg.stream, t, p, verdict, gslot);
+                       cfg.stream, t, cfg.other, p, verdict, gslot);
 }
 
 // The hot variants (LDS-resident image, vector loads, sublist lists, u32
@@ -1309,7 +1344,7 @@ static void launch16_d(const Cls4Dev& t, const Fe16& fe, const Pkts16& p, uint8_
             reinterpret_cast<const void*>(classify16_cls<kLds, kMode, kList, kD, kLin, kFe, kCtr>),
             hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
     hipLaunchKernelGGL((classify16_cls<kLds, kMode, kList, kD, kLin, kFe, kCtr>), dim3(cfg.grid), dim3(kClsBlock),
-                       lds, cfg.stream, t, fe, p, verdict, gslot);
+                       lds, cfg.stream, t, cfg.other, fe, p, verdict, gslot);
 }
 
 template <bool kLds, int kMode, int kList, int kFe>
@@ -1403,9 +1438,18 @@ hipError_t launch_remap(unsigned long long* slot_val, const uint2* csr, uint32_t
     return hipGetLastError();
 }
 
-hipError_t launch_stream(const Pkts4* p4, const Pkts16* p16, uint8_t* verdict, int grid, hipStream_t s) {
-    if (p4) hipLaunchKernelGGL(stream4_kernel, dim3(grid), dim3(kClsBlock), 0, s, *p4, verdict);
-    else hipLaunchKernelGGL(stream16_kernel, dim3(grid), dim3(kClsBlock), 0, s, *p16, verdict);
+hipError_t launch_stream(const Pkts4* p4, const Pkts16* p16, uint8_t* verdict, int grid, int variant,
+                         hipStream_t s) {
+    if (p4) {
+        switch (variant) {
+        case 0: hipLaunchKernelGGL((stream4_kernel<true, true>), dim3(grid), dim3(kClsBlock), 0, s, *p4, verdict); break;
+        case 1: hipLaunchKernelGGL((stream4_kernel<false, true>), dim3(grid), dim3(kClsBlock), 0, s, *p4, verdict); break;
+        case 2: hipLaunchKernelGGL((stream4_kernel<true, false>), dim3(grid), dim3(kClsBlock), 0, s, *p4, verdict); break;
+        default: hipLaunchKernelGGL((stream4_kernel<false, false>), dim3(grid), dim3(kClsBlock), 0, s, *p4, verdict);
+        }
+    } else {
+        hipLaunchKernelGGL(stream16_kernel, dim3(grid), dim3(kClsBlock), 0, s, *p16, verdict);
+    }
     return hipGetLastError();
 }
 

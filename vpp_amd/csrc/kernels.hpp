@@ -47,9 +47,9 @@ struct Cls4Dev {
     uint32_t search_top;       // power of two; bounds padded to 2*search_top
     uint32_t n_ctr;            // slot counters in the image's LDS tail
     uint32_t lds_bytes;
-    const LinRule4* lin;       // linear rules: fallback for protocols outside TCP/UDP/ICMP
+    const LinRule4* lin;       // linear rules (the 16-byte kernel's FORCE_LINEAR cross-check)
     uint32_t n_lin;
-    uint32_t n_rules;          // R: direct rule slots start at n_ctr
+    uint32_t n_rules;          // R
     uint32_t mode;             // 0 interval search, 1 hash LPM
     uint32_t default_row;      // source lookup miss: byte address of the default class's cells
     uint32_t n_hash;
@@ -73,6 +73,7 @@ struct Cls4Dev {
 struct LaunchCfg {
     int grid;                  // workgroups (persistent, grid-stride)
     hipStream_t stream;
+    Cls4Dev other;             // classify kernels: the OTHER image (protocols > 2), global memory
 };
 
 // verdict may be null; gslot: u64 slot counters (added to)
@@ -97,8 +98,11 @@ hipError_t launch_remap(unsigned long long* slot_val, const uint2* csr, uint32_t
 
 // the classify kernels' packet stream without the lookups (stream floor);
 // exactly one of p4 / p16; p4 needs 16-B aligned src/dst, 8-B dport, 4-B
-// proto and verdict; p16 covers whole 256-packet wave steps only
-hipError_t launch_stream(const Pkts4* p4, const Pkts16* p16, uint8_t* verdict, int grid, hipStream_t s);
+// proto and verdict (variant bit 0: load and use instead of the next step's
+// loads in flight; bit 1: the protocol stream a cached load, not
+// non-temporal); p16 covers whole 256-packet wave steps only
+hipError_t launch_stream(const Pkts4* p4, const Pkts16* p16, uint8_t* verdict, int grid, int variant,
+                         hipStream_t s);
 
 struct AclDesc {                 // one installed ACL for the connection kernel
     const LinRule4* rules;
