@@ -162,3 +162,31 @@ def test_stream_floor(eng):
     d16 = torch.zeros((n, 16), dtype=torch.uint8, device="cuda")
     ms16 = eng.stream_floor(d16, d16, d["dport"], d["proto"], v, reps=3)
     assert 0.0 < ms16 < 100.0
+
+
+@pytest.mark.parametrize("cap", [None, "0", "1000"])
+@pytest.mark.parametrize("v16", [False, True])
+def test_other_protocols_queue(eng, monkeypatch, cap, v16):
+    """Protocols outside ProtocolType (30 % here): queued for the OTHER image
+    and classified after the launch, or in place once the queue is full
+    (CONTIVCLS_OTHER_CAP); every path equals the oracle."""
+    from aclgen import random_acl16, random_traffic16
+    if cap is not None:
+        monkeypatch.setenv("CONTIVCLS_OTHER_CAP", cap)
+    if v16:
+        rules, pool = random_acl16(23, 300, 0.0)
+        tr = random_traffic16(4, 70001, pool)
+    else:
+        rules, pool = random_acl(23, 300, 0.0)
+        tr = random_traffic(4, 70001, pool)
+    rng = np.random.default_rng(9)
+    tr["proto"][rng.random(len(tr["proto"])) < 0.3] = 47
+    t = eng.put_table("other", rules)
+    try:
+        v, c = eng.classify(t, tr["src"], tr["dst"], tr["dport"], tr["proto"])
+    finally:
+        eng.del_table(t)
+    ov, oc = oracle.classify_fast(oracle.rules_to_c(rules), tr["src"], tr["dst"], tr["dport"], tr["proto"],
+                                  af=16 if v16 else 4)
+    np.testing.assert_array_equal(v, ov)
+    np.testing.assert_array_equal(c, oc)

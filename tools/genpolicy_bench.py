@@ -23,7 +23,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def bench_list(eng, pol, txn, nb, match, n, iters):
+def bench_list(eng, pol, txn, nb, match, n, iters, mix=(0.445, 0.445, 0.1, 0.01)):
     """Classify n device-resident packets against one of the pod's lists."""
     import torch
     from vpp_amd import configurator as C
@@ -43,8 +43,8 @@ def bench_list(eng, pol, txn, nb, match, n, iters):
     src, dst = (inblk, other) if match == "ingress" else (other, inblk)
     ports = np.array([p.number for p in pol.matches[0].ports], np.uint16)
     dport = np.where(g.random(n) < 0.5, g.choice(ports, n), g.integers(0, 65536, n)).astype(np.uint16)
-    # TCP/UDP, 10 % ICMP, 1 % protocol 47
-    proto = g.choice(np.array([0, 1, 2, 47], np.uint8), n, p=[0.445, 0.445, 0.1, 0.01])
+    # default: TCP/UDP, 10 % ICMP, 1 % protocol 47
+    proto = g.choice(np.array([0, 1, 2, 47], np.uint8), n, p=mix)
     d = {k: torch.from_numpy(v.view(np.int32) if v.dtype == np.uint32 else
                              (v.view(np.int16) if v.dtype == np.uint16 else v)).to("cuda")
          for k, v in dict(src=src, dst=dst, dport=dport, proto=proto).items()}
@@ -64,6 +64,7 @@ def bench_list(eng, pol, txn, nb, match, n, iters):
     eng.del_table(table)
     return {
         "workload": "gen-policy.py, %d blocks x 5 excepts x 20 ports: the pod's %s list" % (nb, match),
+        "proto_mix_tcp_udp_icmp_47": list(mix),
         "rules": len(rules), "gen_s": round(t_gen, 2), "compile_s": round(t_put, 2),
         "kernel": info.get("kernel"), "lds_resident": info.get("lds_resident"),
         "list_mode": info.get("list_mode"), "dst_keyed": info.get("swap"), "ctr16": info.get("ctr16"),
@@ -80,6 +81,8 @@ def main():
     ap.add_argument("--packets", type=int, default=1 << 26)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--match", nargs="+", default=["ingress", "egress"])
+    ap.add_argument("--mix", type=float, nargs=4, default=[0.445, 0.445, 0.1, 0.01],
+                    help="shares of TCP, UDP, ICMP, protocol 47")
     a = ap.parse_args()
     from vpp_amd import configurator as C
     from vpp_amd.engine import Engine
@@ -89,7 +92,7 @@ def main():
         pol = C.gen_policy(random.Random(nb), num_cidrs=nb)
         txn = C.PolicyConfigurator({PodID("db", "default"): "10.1.1.1"}).new_txn(False)
         for match in a.match:
-            print(json.dumps(bench_list(eng, pol, txn, nb, match, a.packets, a.iters)), flush=True)
+            print(json.dumps(bench_list(eng, pol, txn, nb, match, a.packets, a.iters, tuple(a.mix))), flush=True)
     eng.close()
 
 

@@ -45,8 +45,17 @@ struct DevBuf {
 // one table on different streams never share a counter buffer
 // (include/contivcls.h, threading).  slot_val is all zero between calls: the
 // remap kernel reads and clears it.
+// OTHER queue (protocols > 2 deferred to other_kernel): per workgroup room
+// for 1/16 of its packets (CONTIVCLS_OTHER_CAP: tests, to reach the
+// in-place path of a full segment)
+static uint32_t other_cap(uint64_t n, int grid) {
+    if (const char* c = std::getenv("CONTIVCLS_OTHER_CAP")) return uint32_t(std::strtoul(c, nullptr, 0));
+    return uint32_t(std::max<uint64_t>(1024, (n / uint64_t(std::max(grid, 1)) + 15) / 16));
+}
+
 struct Scratch {
     DevBuf part;                   // per-workgroup LDS counter rows [rows][n_lctr]
+    DevBuf oq;                     // OTHER queue {fill per workgroup, segments of indices}
     DevBuf slot_val;               // u64 per slot: global-tier counters, folded partials
     DevBuf out;                    // u64 rule counters when the caller gives none on device
     hipEvent_t done = nullptr;     // recorded after the call's last kernel
@@ -402,6 +411,8 @@ static Cls4Dev cls4_dev(const Cls4Image& im, const DevBuf& d_img, const DevBuf& 
     cd.n_lctr = im.n_lctr;
     cd.ctr16 = im.ctr16;
     cd.part = nullptr;
+    cd.oq = nullptr;                 // protocols > 2 classified in place unless the caller sets a queue
+    cd.oq_cap = 0;
     for (uint32_t i = 0; i < kMaxHashLens; ++i) {
         cd.hash_mask[i] = im.hash_mask[i];
         cd.hash_shift[i] = im.hash_shift[i];
@@ -451,6 +462,17 @@ static int scratch_of(cls_engine* e, Counters& c, uint32_t n_rules, hipStream_t 
         p = std::move(q);
     }
     *out = p.get();
+    return CLS_OK;
+}
+
+// The OTHER queue of a launch of `grid` workgroups with segments of `cap`.
+static int other_queue(cls_engine* e, Scratch* sc, int grid, uint32_t cap, hipStream_t s, uint32_t** out) {
+    const size_t need = (size_t(grid) + size_t(grid) * cap) * 4;
+    if (need > sc->oq.bytes) {
+        HIPC(e, hipStreamSynchronize(s));       // earlier launches on this stream may still read it
+        HIPC(e, sc->oq.ensure(need));
+    }
+    *out = sc->oq.as<uint32_t>();
     return CLS_OK;
 }
 
@@ -573,6 +595,11 @@ static int classify16_locked(cls_engine* e, std::shared_ptr<Table> t, const cls_
     if (n) {
         Cls4Dev cd = cls4_dev(c, q.d_img, q.d_lin, uint32_t(q.lin.size()), t->n_rules);
         cfg.other = cls4_dev(q.oimg, q.d_oimg, DevBuf(), 0, t->n_rules);
+        cd.oq_cap = other_cap(std::min<uint64_t>(n, kClsChunk), cfg.grid);
+        {
+            const int rc = other_queue(e, sc, cfg.grid, cd.oq_cap, s, &cd.oq);
+            if (rc != CLS_OK) return rc;
+        }
         if (q.lds_resident) cd.part = sc->part.as<uint32_t>();
         Fe16 fe = fe16(q.img, q.d_src_search);
         for (uint64_t off = 0; off < n; off += kClsChunk) {
@@ -583,6 +610,7 @@ static int classify16_locked(cls_engine* e, std::shared_ptr<Table> t, const cls_
             uint8_t* vo = d_verdict ? d_verdict + off : nullptr;
             pc.vec = aligned(pc.dport, 8) && aligned(pc.proto, 4) && (!vo || aligned(vo, 4)) ? 1u : 0u;
             HIPC(e, launch_classify16_cls(cd, fe, pc, vo, slot_val, q.lds_resident, lin, cfg));
+            if (!lin) HIPC(e, launch_other16(cd, cfg.other, fe, cd.oq, uint32_t(cfg.grid), cd.oq_cap, pc, vo, slot_val, s));
             if (timing && off + m >= n) HIPC(e, hipEventRecord(e->ev1, s));
             if (q.lds_resident) {
                 HIPC(e, launch_fold(cd.part, uint32_t(cfg.grid), c.n_lctr, slot_val, co.zero && !zeroed ? co.out : nullptr,
@@ -660,6 +688,11 @@ int cls_classify(cls_engine* e, uint32_t table_id, const cls_pkt_soa* pk, uint64
         if (use_cls) {
             Cls4Dev cd = table_dev(*t);
             cfg.other = cls4_dev(t->oimg, t->d_oimg, DevBuf(), 0, t->n_rules);
+            cd.oq_cap = other_cap(std::min<uint64_t>(n, kClsChunk), cfg.grid);
+            {
+                const int rc = other_queue(e, sc, cfg.grid, cd.oq_cap, s, &cd.oq);
+                if (rc != CLS_OK) return rc;
+            }
             if (t->lds_resident) cd.part = sc->part.as<uint32_t>();
             // the kernel indexes packets with 32-bit offsets: chunks of 2^30
             for (uint64_t off = 0; off < n; off += kClsChunk) {
@@ -667,6 +700,8 @@ int cls_classify(cls_engine* e, uint32_t table_id, const cls_pkt_soa* pk, uint64
                 const Pkts4 pc = framed(t->img, Pkts4{p.src + off, p.dst + off, p.dport + off, p.proto + off, m});
                 HIPC(e, launch_classify4_cls(cd, pc, d_verdict ? d_verdict + off : nullptr, slot_val,
                                              t->lds_resident, vec, cfg));
+                HIPC(e, launch_other4(cfg.other, t->img.n_ctr, cd.oq, uint32_t(cfg.grid), cd.oq_cap, pc,
+                                      d_verdict ? d_verdict + off : nullptr, slot_val, s));
                 if (timing && off + m >= n) HIPC(e, hipEventRecord(e->ev1, s));
                 if (t->lds_resident) {
                     HIPC(e, launch_fold(cd.part, uint32_t(cfg.grid), t->img.n_lctr, slot_val,

@@ -424,7 +424,8 @@ __device__ __forceinline__ void run_n(const Img<kLds>& im, const Cls4Dev& t, con
                                       unsigned long long* gslot, uint32_t& hot0,
                                       const uint32_t (&s)[N], const uint32_t (&d)[N],
                                       const uint32_t (&dp)[N], const uint32_t (&pr)[N],
-                                      bool pr_any, uint32_t (&res)[N], const uint32_t (&sl)[N]) {
+                                      bool pr_any, uint32_t (&res)[N], const uint32_t (&sl)[N],
+                                      const uint32_t (&idx)[N], uint32_t oq_lds) {
     uint32_t slot[N];
     classify_n<N, kLds, kMode, kList, kD>(im, t, s, d, dp, pr, res, slot);
     // One LDS atomic per packet, no branch.  Hot slots (< n_hot: default DENY
@@ -477,23 +478,46 @@ __device__ __forceinline__ void run_n(const Img<kLds>& im, const Cls4Dev& t, con
     }
     // Protocols outside TCP/UDP/ICMP fall through evalACL's switch
     // (aclengine_mock.go:508-664): networks alone decide.  Rare; taken per
-    // wave only when some lane holds such a packet: the OTHER image's
-    // interval search and candidate scan from global memory (L2), its slots
-    // after the main image's.
+    // wave only when some lane holds such a packet.  Such a packet's index
+    // goes to the OTHER queue (t.oq: count, then indices), which other_kernel
+    // classifies on the OTHER image after this launch (verdict and count);
+    // when the queue is full, here and now (the OTHER image's interval
+    // search and candidate scan from global memory, its slots after the main
+    // image's).
     if (__any(pr_any)) {
-        const uint32_t zero[N] = {};
-        uint32_t ores[N], oslot[N];
-        classify_n<N, false, 0, 0, -1>(Img<false>{reinterpret_cast<const uint8_t*>(o.img)}, o, sl, d, dp, zero,
-                                       ores, oslot);
+        const Img<false> oim{reinterpret_cast<const uint8_t*>(o.img)};
 #pragma unroll
         for (int q = 0; q < N; ++q) {
-            const bool other = pr[q] > 2u;
+            const bool oth = pr[q] > 2u;
             if constexpr (kLds && kCtr == 0) {                        // undo the main image's count
-                if (other)
+                if (oth)
                     __hip_atomic_fetch_add(lctr_t(addr[q]), ~0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
-            res[q] = other ? ores[q] : res[q];
-            wave_count(gslot, other ? t.n_ctr + oslot[q] : 0xFFFFFFFFu);
+            bool now = oth;
+            const unsigned long long m = __ballot(oth);
+            if (m && t.oq) {
+                // this workgroup's queue segment, its fill counted in LDS
+                const int leader = __builtin_ctzll(m);
+                uint32_t base = 0;
+                if (int(__lane_id()) == leader)
+                    base = __hip_atomic_fetch_add(lctr_t(oq_lds), uint32_t(__popcll(m)), __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_WORKGROUP);
+                base = __shfl(base, leader);
+                const uint32_t pos = base + uint32_t(__popcll(m & ((1ull << __lane_id()) - 1ull)));
+                if (oth && pos < t.oq_cap) {
+                    t.oq[gridDim.x + blockIdx.x * t.oq_cap + pos] = idx[q];
+                    now = false;
+                }
+            }
+            uint32_t key = 0xFFFFFFFFu;
+            if (now) {                                                 // only these lanes load
+                const uint32_t s1[1] = {sl[q]}, d1[1] = {d[q]}, p1[1] = {dp[q]}, z1[1] = {0u};
+                uint32_t r1[1], k1[1];
+                classify_n<1, false, 0, 0, -1>(oim, o, s1, d1, p1, z1, r1, k1);
+                res[q] = r1[0];
+                key = t.n_ctr + k1[0];
+            }
+            wave_count(gslot, key);
         }
     }
 }
@@ -515,6 +539,25 @@ __device__ __forceinline__ void run_n(const Img<kLds>& im, const Cls4Dev& t, con
 #define CLS_PREFETCH 1
 #endif
 constexpr int kG = CLS_GROUPS;     // 16-B packet groups per lane per step
+
+// The OTHER queue's fill counter of this workgroup: one LDS word after the
+// image's LDS (the launch adds 16 bytes of dynamic LDS for it).  Zeroed
+// here, made visible by the barrier of stage_lds (or this one).
+template <bool kLds>
+__device__ __forceinline__ uint32_t queue_begin(const Cls4Dev& t, uint4* smem) {
+    const uint32_t a = kLds ? t.lds_bytes : 0u;
+    if (threadIdx.x == 0) *reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(smem) + a) = 0u;
+    if constexpr (!kLds) __syncthreads();
+    return a;
+}
+
+// End of a launch: the workgroup's queue fill -> oq[blockIdx.x] (other_kernel).
+__device__ __forceinline__ void queue_end(const Cls4Dev& t, uint32_t oq_lds) {
+    if (!t.oq) return;
+    __syncthreads();
+    if (threadIdx.x == 0)
+        t.oq[blockIdx.x] = min(*reinterpret_cast<const __attribute__((address_space(3))) uint32_t*>(oq_lds), t.oq_cap);
+}
 
 // Stage the read-only image into LDS (at address 0) and zero the counters.
 __device__ __forceinline__ void stage_lds(const Cls4Dev& t, uint4* smem) {
@@ -556,6 +599,7 @@ __global__ __launch_bounds__(kClsBlock) void classify4_cls(Cls4Dev t, Cls4Dev o,
                                                            unsigned long long* gslot) {
     extern __shared__ uint4 smem[];
     Img<kLds> im{reinterpret_cast<const uint8_t*>(t.img)};
+    const uint32_t oq_lds = queue_begin<kLds>(t, smem);
     if constexpr (kLds && !(CLS_ABLATE & 16)) stage_lds(t, smem);
 
     const uint32_t nthreads = gridDim.x * blockDim.x;
@@ -608,8 +652,11 @@ __global__ __launch_bounds__(kClsBlock) void classify4_cls(Cls4Dev t, Cls4Dev o,
                 // computed without inter-byte carries)
                 other |= ((pr | ((pr & 0x7F7F7F7Fu) + 0x7D7D7D7Du)) & 0x80808080u) != 0u;
             }
-            uint32_t v[kN];
-            run_n<kN, kLds, kMode, kList, kD, kCtr>(im, t, o, hot_lane, gslot, hot0, sa, da, pa, ra, other, v, sa);
+            uint32_t v[kN], ix[kN];
+#pragma unroll
+            for (int k = 0; k < kN; ++k) ix[k] = 4u * (g + uint32_t(k / 4) * nthreads) + uint32_t(k % 4);
+            run_n<kN, kLds, kMode, kList, kD, kCtr>(im, t, o, hot_lane, gslot, hot0, sa, da, pa, ra, other, v, sa, ix,
+                                                    oq_lds);
             if (verdict) {
 #pragma unroll
                 for (int k = 0; k < kG; ++k)
@@ -655,9 +702,10 @@ __global__ __launch_bounds__(kClsBlock) void classify4_cls(Cls4Dev t, Cls4Dev o,
             const uint32_t pa[4] = {p2.x & 0xFFFFu, p2.x >> 16, p2.y & 0xFFFFu, p2.y >> 16};
             const uint32_t ra[4] = {pr & 0xFFu, (pr >> 8) & 0xFFu, (pr >> 16) & 0xFFu, pr >> 24};
             uint32_t v[4];
+            const uint32_t ix[4] = {4u * gi, 4u * gi + 1u, 4u * gi + 2u, 4u * gi + 3u};
             run_n<4, kLds, kMode, kList, -1, kCtr>(im, t, o, hot_lane, gslot, hot0, sa, da, pa, ra,
                                                    ((pr | ((pr & 0x7F7F7F7Fu) + 0x7D7D7D7Du)) & 0x80808080u) != 0u,
-                                                   v, sa);
+                                                   v, sa, ix, oq_lds);
             if (verdict)
                 stnt(v[0] | (v[1] << 8) | (v[2] << 16) | (v[3] << 24),
                      const_cast<uint32_t*>(at(reinterpret_cast<const uint32_t*>(verdict), gi)));
@@ -667,7 +715,9 @@ __global__ __launch_bounds__(kClsBlock) void classify4_cls(Cls4Dev t, Cls4Dev o,
     for (uint32_t i = tail_from + tid; i < uint32_t(p.n); i += nthreads) {
         const uint32_t sa[1] = {p.src[i]}, da[1] = {p.dst[i]}, pa[1] = {p.dport[i]}, ra[1] = {p.proto[i]};
         uint32_t v[1];
-        run_n<1, kLds, kMode, kList, -1, kCtr>(im, t, o, hot_lane, gslot, hot0, sa, da, pa, ra, ra[0] > 2u, v, sa);
+        const uint32_t ix[1] = {i};
+        run_n<1, kLds, kMode, kList, -1, kCtr>(im, t, o, hot_lane, gslot, hot0, sa, da, pa, ra, ra[0] > 2u, v, sa,
+                                               ix, oq_lds);
         if (verdict) verdict[i] = uint8_t(v[0]);
     }
 
@@ -675,6 +725,7 @@ __global__ __launch_bounds__(kClsBlock) void classify4_cls(Cls4Dev t, Cls4Dev o,
         if (hot0) atomicAdd(&gslot[0], (unsigned long long)hot0);
     }
     if constexpr (kLds) flush_lds<kCtr>(t, smem);
+    queue_end(t, oq_lds);
 }
 
 // The classify kernels' HBM stream without the lookups (bench.py's measured
@@ -742,6 +793,55 @@ __global__ __launch_bounds__(kClsBlock) void stream16_kernel(Pkts16 p, uint8_t* 
                                         verdict + base + 64u * k);
         }
     }
+}
+
+// The packets a classify launch queued for the OTHER image (protocols > 2,
+// run_n): classified here with every lane on one such packet, so the rare
+// packets cost the streaming kernel nothing but the queue append.  oq =
+// {fill of each of the launch's `rows` workgroups, then their segments of
+// cap indices}; the packets a full segment could not take were classified in
+// place.  Counts: a block histogram in LDS for tables with few OTHER slots.
+constexpr uint32_t kOtherLds = 4096;
+template <typename Load>
+__device__ __forceinline__ void other_loop(const Cls4Dev& o, uint32_t slot0, const uint32_t* __restrict__ oq,
+                                           uint32_t rows, uint32_t cap, uint8_t* verdict,
+                                           unsigned long long* gslot, const Load& load) {
+    __shared__ uint32_t h[kOtherLds];
+    const bool lds = o.n_ctr <= kOtherLds;
+    if (lds) {
+        for (uint32_t i = threadIdx.x; i < o.n_ctr; i += blockDim.x) h[i] = 0u;
+        __syncthreads();
+    }
+    const Img<false> oim{reinterpret_cast<const uint8_t*>(o.img)};
+    for (uint32_t r = blockIdx.x; r < rows; r += gridDim.x) {
+        const uint32_t n = oq[r];
+        for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+            const uint32_t k = oq[rows + r * cap + i];
+            uint32_t s1[1], d1[1], p1[1];
+            load(k, s1[0], d1[0], p1[0]);
+            const uint32_t z1[1] = {0u};
+            uint32_t r1[1], k1[1];
+            classify_n<1, false, 0, 0, -1>(oim, o, s1, d1, p1, z1, r1, k1);
+            if (verdict) verdict[k] = uint8_t(r1[0]);
+            if (lds) atomicAdd(&h[k1[0]], 1u);
+            else wave_count(gslot, slot0 + k1[0]);
+        }
+    }
+    if (lds) {
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < o.n_ctr; i += blockDim.x)
+            if (h[i]) atomicAdd(&gslot[slot0 + i], (unsigned long long)h[i]);
+    }
+}
+
+__global__ __launch_bounds__(256) void other4_kernel(Cls4Dev o, uint32_t n_main, const uint32_t* __restrict__ oq,
+                                                     uint32_t rows, uint32_t cap, Pkts4 p, uint8_t* verdict,
+                                                     unsigned long long* gslot) {
+    other_loop(o, n_main, oq, rows, cap, verdict, gslot, [&](uint32_t k, uint32_t& s, uint32_t& d, uint32_t& dp) {
+        s = p.src[k];
+        d = p.dst[k];
+        dp = p.dport[k];
+    });
 }
 
 // ---------------------------------------------------------------------------
@@ -868,6 +968,7 @@ __global__ __launch_bounds__(kClsBlock) void classify16_cls(Cls4Dev t, Cls4Dev o
                                                             uint8_t* verdict, unsigned long long* gslot) {
     extern __shared__ uint4 smem[];
     Img<kLds> im{reinterpret_cast<const uint8_t*>(t.img)};
+    const uint32_t oq_lds = queue_begin<kLds>(t, smem);
     if constexpr (kLds) stage_lds(t, smem);
     const uint32_t nthreads = gridDim.x * blockDim.x;
     const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
@@ -880,7 +981,7 @@ __global__ __launch_bounds__(kClsBlock) void classify16_cls(Cls4Dev t, Cls4Dev o
         if constexpr (kFe == 1) fe_rep(gim, 0u, fe.gval, fe.top[0], fe.k8[0], a, out);
         else fe_rep(im, fe.key[0], fe.val[0], fe.top[0], fe.k8[0], a, out);
     };
-    auto classify = [&](const auto& s16, const auto& d16, auto& pa, auto& ra, bool other, auto& v) {
+    auto classify = [&](const auto& s16, const auto& d16, auto& pa, auto& ra, bool other, auto& v, const auto& ix) {
         constexpr int N = sizeof(v) / 4;
         uint32_t sa[N], da[N];
         fe_rep(im, fe.key[1], fe.val[1], fe.top[1], fe.k8[1], d16, da);
@@ -895,10 +996,12 @@ __global__ __launch_bounds__(kClsBlock) void classify16_cls(Cls4Dev t, Cls4Dev o
                 for (int q = 0; q < N; ++q)
                     sl[q] = ra[q] > 2u ? src_rep_global(fe.gsrc, fe.gval, fe.top[0], fe.k8[0], s16[q]) : 0u;
             }
-            run_n<N, kLds, kMode, kList, kD, kCtr>(im, t, o, hot_lane, gslot, hot0, sa, da, pa, ra, other, v, sl);
+            run_n<N, kLds, kMode, kList, kD, kCtr>(im, t, o, hot_lane, gslot, hot0, sa, da, pa, ra, other, v, sl, ix,
+                                                   oq_lds);
         } else {
             src_rep(s16, sa);
-            run_n<N, kLds, kMode, kList, kD, kCtr>(im, t, o, hot_lane, gslot, hot0, sa, da, pa, ra, other, v, sa);
+            run_n<N, kLds, kMode, kList, kD, kCtr>(im, t, o, hot_lane, gslot, hot0, sa, da, pa, ra, other, v, sa, ix,
+                                                   oq_lds);
         }
     };
     // 4 packets per lane per step (vector dport / proto / verdict words),
@@ -939,7 +1042,8 @@ __global__ __launch_bounds__(kClsBlock) void classify16_cls(Cls4Dev t, Cls4Dev o
         for (int h = 0; h < 2; ++h) {
             const uint4 s2[2] = {s[2 * h], s[2 * h + 1]}, d2[2] = {d[2 * h], d[2 * h + 1]};
             uint32_t pa[2] = {dp[2 * h], dp[2 * h + 1]}, ra[2] = {pr[2 * h], pr[2 * h + 1]}, v2[2];
-            classify(s2, d2, pa, ra, (ra[0] | ra[1]) > 2u, v2);
+            const uint32_t ix[2] = {base + 64u * (2 * h), base + 64u * (2 * h + 1)};
+            classify(s2, d2, pa, ra, (ra[0] | ra[1]) > 2u, v2, ix);
             if (verdict) {
                 __builtin_nontemporal_store(uint8_t(v2[0]), verdict + base + 64u * (2 * h));
                 __builtin_nontemporal_store(uint8_t(v2[1]), verdict + base + 64u * (2 * h + 1));
@@ -965,7 +1069,8 @@ __global__ __launch_bounds__(kClsBlock) void classify16_cls(Cls4Dev t, Cls4Dev o
             const uint4 s2[2] = {s[2 * h], s[2 * h + 1]}, d2[2] = {d[2 * h], d[2 * h + 1]};
             const uint32_t w = h ? dp.y : dp.x, r = pr >> (16 * h);
             uint32_t pa[2] = {w & 0xFFFFu, w >> 16}, ra[2] = {r & 0xFFu, (r >> 8) & 0xFFu}, v2[2];
-            classify(s2, d2, pa, ra, (ra[0] | ra[1]) > 2u, v2);
+            const uint32_t ix[2] = {4u * g + 2u * h, 4u * g + 2u * h + 1u};
+            classify(s2, d2, pa, ra, (ra[0] | ra[1]) > 2u, v2, ix);
             v[2 * h] = v2[0];
             v[2 * h + 1] = v2[1];
         }
@@ -978,13 +1083,33 @@ __global__ __launch_bounds__(kClsBlock) void classify16_cls(Cls4Dev t, Cls4Dev o
         const uint4 s1[1] = {ldnt(at(p.src, i))}, d1[1] = {ldnt(at(p.dst, i))};
         uint32_t v[1];
         uint32_t pa[1] = {p.dport[i]}, ra[1] = {p.proto[i]};
-        classify(s1, d1, pa, ra, ra[0] > 2u, v);
+        const uint32_t ix[1] = {i};
+        classify(s1, d1, pa, ra, ra[0] > 2u, v, ix);
         if (verdict) verdict[i] = uint8_t(v[0]);
     }
     if constexpr (!kLds) {
         if (hot0) atomicAdd(&gslot[0], (unsigned long long)hot0);
     }
     if constexpr (kLds) flush_lds<kCtr>(t, smem);
+    queue_end(t, oq_lds);
+}
+
+// other4_kernel for 16-byte batches: the reps from the front end in global
+// memory (the image's copy; src_mode 1: the source interval table).
+__global__ __launch_bounds__(256) void other16_kernel(Cls4Dev t, Cls4Dev o, Fe16 fe, const uint32_t* __restrict__ oq,
+                                                      uint32_t rows, uint32_t cap, Pkts16 p, uint8_t* verdict,
+                                                      unsigned long long* gslot) {
+    const Img<false> gim{reinterpret_cast<const uint8_t*>(t.img)};
+    other_loop(o, t.n_ctr, oq, rows, cap, verdict, gslot, [&](uint32_t k, uint32_t& s, uint32_t& d, uint32_t& dp) {
+        const uint4 s16[1] = {p.src[k]}, d16[1] = {p.dst[k]};
+        uint32_t s1[1], d1[1];
+        if (fe.src_mode == 1) s1[0] = src_rep_global(fe.gsrc, fe.gval, fe.top[0], fe.k8[0], s16[0]);
+        else fe_rep(gim, fe.key[0], fe.val[0], fe.top[0], fe.k8[0], s16, s1);
+        fe_rep(gim, fe.key[1], fe.val[1], fe.top[1], fe.k8[1], d16, d1);
+        s = s1[0];
+        d = d1[0];
+        dp = p.dport[k];
+    });
 }
 
 // slot_val[i] += the sum over the grid's rows of part[w][i], i < n: block b
@@ -1268,10 +1393,9 @@ int cls_block() { return kClsBlock; }
 template <bool kLds, bool kVec, int kMode, int kList, int kD, int kCtr = 0>
 static void launch_d(const Cls4Dev& t, const Pkts4& p, uint8_t* verdict, unsigned long long* gslot,
                      const LaunchCfg& cfg) {
-    const size_t lds = kLds ? t.lds_bytes : 0;
-    if (kLds)
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(classify4_cls<kLds, kVec, kMode, kList, kD, kCtr>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
+    const size_t lds = (kLds ? t.lds_bytes : 0) + 16;   // + the OTHER queue counter
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(classify4_cls<kLds, kVec, kMode, kList, kD, kCtr>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
     hipLaunchKernelGGL((classify4_cls<kLds, kVec, kMode, kList, kD, kCtr>), dim3(cfg.grid), dim3(kClsBlock), lds,
                        cfg.stream, t, cfg.other, p, verdict, gslot);
 }
@@ -1338,11 +1462,9 @@ hipError_t launch_classify4_cls(const Cls4Dev& t, const Pkts4& p, uint8_t* verdi
 template <bool kLds, int kMode, int kList, int kD, bool kLin, int kFe, int kCtr = 0>
 static void launch16_d(const Cls4Dev& t, const Fe16& fe, const Pkts16& p, uint8_t* verdict,
                        unsigned long long* gslot, const LaunchCfg& cfg) {
-    const size_t lds = kLds ? t.lds_bytes : 0;
-    if (kLds)
-        (void)hipFuncSetAttribute(
-            reinterpret_cast<const void*>(classify16_cls<kLds, kMode, kList, kD, kLin, kFe, kCtr>),
-            hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
+    const size_t lds = (kLds ? t.lds_bytes : 0) + 16;   // + the OTHER queue counter
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(classify16_cls<kLds, kMode, kList, kD, kLin, kFe, kCtr>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
     hipLaunchKernelGGL((classify16_cls<kLds, kMode, kList, kD, kLin, kFe, kCtr>), dim3(cfg.grid), dim3(kClsBlock),
                        lds, cfg.stream, t, cfg.other, fe, p, verdict, gslot);
 }
@@ -1435,6 +1557,18 @@ hipError_t launch_remap(unsigned long long* slot_val, const uint2* csr, uint32_t
                         hipStream_t s) {
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(remap_kernel, dim3((n + 255) / 256), dim3(256), 0, s, slot_val, csr, n, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_other4(const Cls4Dev& o, uint32_t n_main, const uint32_t* oq, uint32_t rows, uint32_t cap,
+                         const Pkts4& p, uint8_t* verdict, unsigned long long* gslot, hipStream_t s) {
+    hipLaunchKernelGGL(other4_kernel, dim3(rows), dim3(256), 0, s, o, n_main, oq, rows, cap, p, verdict, gslot);
+    return hipGetLastError();
+}
+
+hipError_t launch_other16(const Cls4Dev& t, const Cls4Dev& o, const Fe16& fe, const uint32_t* oq, uint32_t rows,
+                          uint32_t cap, const Pkts16& p, uint8_t* verdict, unsigned long long* gslot, hipStream_t s) {
+    hipLaunchKernelGGL(other16_kernel, dim3(rows), dim3(256), 0, s, t, o, fe, oq, rows, cap, p, verdict, gslot);
     return hipGetLastError();
 }
 

@@ -68,6 +68,9 @@ struct Cls4Dev {
     uint32_t n_lctr;           // LDS-resident image: slots [0, n_lctr) counted in LDS, the rest in gslot
     uint32_t ctr16;            // LDS counters are u16 (compile.hpp counter tiers)
     uint32_t* part;            // LDS-resident image: per-workgroup slot counters [grid][n_lctr]
+    uint32_t* oq;              // OTHER queue {fill per workgroup, segments of oq_cap indices}
+                               // (null: classify such packets in place)
+    uint32_t oq_cap;
 };
 
 struct LaunchCfg {
@@ -95,7 +98,13 @@ hipError_t launch_fold(const uint32_t* part, uint32_t rows, uint32_t n, unsigned
 // (csr: every slot once, grouped by rule); out null: clear only
 hipError_t launch_remap(unsigned long long* slot_val, const uint2* csr, uint32_t n, unsigned long long* out,
                         hipStream_t s);
-
+// the packets a classify launch of `rows` workgroups queued for the OTHER
+// image (oq = {fill per workgroup, then rows segments of cap indices}):
+// verdicts and counts (slots n_main + OTHER slot)
+hipError_t launch_other4(const Cls4Dev& o, uint32_t n_main, const uint32_t* oq, uint32_t rows, uint32_t cap,
+                         const Pkts4& p, uint8_t* verdict, unsigned long long* gslot, hipStream_t s);
+hipError_t launch_other16(const Cls4Dev& t, const Cls4Dev& o, const Fe16& fe, const uint32_t* oq, uint32_t rows,
+                          uint32_t cap, const Pkts16& p, uint8_t* verdict, unsigned long long* gslot, hipStream_t s);
 // the classify kernels' packet stream without the lookups (stream floor);
 // exactly one of p4 / p16; p4 needs 16-B aligned src/dst, 8-B dport, 4-B
 // proto and verdict (variant bit 0: load and use instead of the next step's
