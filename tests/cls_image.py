@@ -162,8 +162,8 @@ class Image:
         return np.where((e & 0xFFFF) == dp, e >> 16, self.h.port_dflt)
 
     def _classify_bv3(self, cls, src, dst, dport, proto, counters):
-        """List mode 3 (port-filtered sublists): cell u32 {pointer table byte
-        offset | counter base << 16}; table[port class] = initial state
+        """List mode 3 (port-filtered sublists): cell u32 {pointer table word
+        offset | counter base << 14}; table[port class] = initial state
         {outcome | entry slot << 16} (state >> 13 = entry byte address);
         entries {start - 1, state}, a probe of step i reads 8 << i bytes on and
         moves the state when start - 1 < dst; outcome = result | (j + 1) << 2."""
@@ -171,13 +171,13 @@ class Image:
         pr = np.minimum(proto, 2).astype(np.int64)
         cell = img[(self.h.off_cells + cls * self.h.row_bytes + pr * 4) // 4]
         pc4 = self._port_class4(dport)                # class x 4
-        st = img[((cell & 0xFFFF) + pc4) // 4]
+        st = img[((cell & 0x3FFF) * 4 + pc4) // 4]
         d = dst.astype(np.int64)
         for i in range(int(self.h.bv_steps_d) - 1, -1, -1):
             a = ((st >> 13) + (8 << i)) // 4
             st = np.where(img[a] < d, img[a + 1], st)
         res = (st & 3).astype(np.uint32)
-        slot = (cell >> 16) + ((st >> 2) & 63)       # the cell's no-match slot when j + 1 == 0
+        slot = (cell >> 14) + ((st >> 2) & 63)       # the cell's no-match slot when j + 1 == 0
         np.add.at(counters, self.ctr_rule[slot].astype(np.int64), 1)
         return res.astype(np.uint8), counters
 

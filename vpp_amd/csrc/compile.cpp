@@ -500,8 +500,8 @@ uint32_t Cls4Image::row_of(uint32_t addr) const {
 // with small tables).
 uint32_t lds_budget() {
     if (const char* b = std::getenv("CONTIVCLS_LDS_BUDGET"))
-        return std::min<uint32_t>(kLdsBudget, uint32_t(std::strtoul(b, nullptr, 0)));
-    return kLdsBudget;
+        return std::min<uint32_t>(kLdsBudget - kLdsReserved, uint32_t(std::strtoul(b, nullptr, 0)));
+    return kLdsBudget - kLdsReserved;
 }
 
 // Counter tiers of a serialised image (compile.hpp Cls4Image): per-lane u32
@@ -772,7 +772,7 @@ static bool build_cls4_one(const std::vector<SemRule>& sem, uint32_t n_rules, Cl
     uint32_t Sd = 0, Sp = 0;
     std::vector<uint32_t> G, toff;
     std::vector<uint8_t> psub;
-    if (img.ctr_rule.size() > 0xFFFFu) all_bv = false;    // counter base: 16-bit cell field
+    // (modes 1, 2 keep a 16-bit counter base in the cell: cell_ok below)
     if (all_bv) {
         for (uint32_t x : bv_lists) {
             bv_ents.push_back(ents_of(x));
@@ -913,7 +913,7 @@ static bool build_cls4_one(const std::vector<SemRule>& sem, uint32_t n_rules, Cl
         }
         if (ci == 0) hot3 = std::min<uint32_t>(uint32_t(ctr3.size()), kMaxHot);
     }
-    if (lmode >= 3 && ctr3.size() > 0xFFFFu) lmode = 2;   // 16-bit cell field
+    if (lmode >= 3 && ctr3.size() > 0x3FFFFu) lmode = 2;  // 18-bit counter base in the cell
 
     std::vector<uint32_t>& w = img.words;
     auto serialise = [&](uint32_t lm) {
@@ -999,10 +999,11 @@ static bool build_cls4_one(const std::vector<SemRule>& sem, uint32_t n_rules, Cl
             }
             w.resize(align4(uint32_t(w.size())));
         } else if (lm >= 3) {
-            // sublist cells: u32 {pointer table byte offset | counter base << 16},
-            // the base being the cell's own no-match slot
+            // sublist cells: u32 {pointer table word offset (14 bits: the
+            // tables lie in the first 64 KiB) | counter base << 14}, the base
+            // being the cell's own no-match slot
             const size_t n_cells = size_t(n_classes) * ncell;
-            for (size_t i = 0; i < n_cells; ++i) w.push_back(ptr_off.at(cells[2 * i]) | (cb3[i] << 16));
+            for (size_t i = 0; i < n_cells; ++i) w.push_back((ptr_off.at(cells[2 * i]) >> 2) | (cb3[i] << 14));
             w.resize(align4(uint32_t(w.size())));
         } else {
             // bit-vector cells: u32 {list block offset / 8 | counter base << 16}
@@ -1132,7 +1133,8 @@ static bool build_cls4_one(const std::vector<SemRule>& sem, uint32_t n_rules, Cl
     // block offset field: 16 bits in 8-B units (modes 1, 2); mode 3: the
     // pointer tables in the first 64 KiB, sublist slots below 2^16
     auto cell_ok = [&](uint32_t lm) {
-        return lm == 0 || (lm >= 3 ? img.sub_bytes <= 0x10000u : img.img_bytes / 8u <= 0xFFFFu);
+        return lm == 0 || (lm >= 3 ? img.sub_bytes <= 0x10000u
+                                   : img.img_bytes / 8u <= 0xFFFFu && img.ctr_rule.size() <= 0xFFFFu);
     };
     for (int partial = 0; partial < 2; ++partial)
         for (uint32_t lm : seq) {

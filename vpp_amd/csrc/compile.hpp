@@ -45,6 +45,7 @@ constexpr uint32_t kPortUniform = 1u << 19;  // port radix: chunk inside one cla
 constexpr uint32_t kMaxPortClasses3 = 64;   // list modes 3, 4: class x 4 fits a byte
 constexpr uint32_t kMaxPortHash = 64;       // list mode 4: ports outside the default class
 constexpr uint32_t kLdsBudget = 160 * 1024;  // LDS of one classify workgroup
+constexpr uint32_t kLdsReserved = 16;        // after the image's LDS: the OTHER-queue fill counter
 // One multiply per key: p = key x mul; table 0 takes the top L bits of p,
 // table 1 the next L bits (L = log2 cap <= 16).  The compiler picks mul from a
 // fixed list until the cuckoo build succeeds.

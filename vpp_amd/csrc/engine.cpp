@@ -268,7 +268,7 @@ static int table_put_locked(cls_engine* e, const char* name, const cls_rule* rul
         if (build_pair(sem, n, t->img, t->oimg, why)) {
             t->has_cls = true;
             t->kernel = 1;
-            t->lds_resident = t->img.lds_ok && t->img.lds_bytes <= uint32_t(max_lds_bytes());
+            t->lds_resident = t->img.lds_ok && t->img.lds_bytes + kLdsReserved <= uint32_t(max_lds_bytes());
             rc = upload(e, t->d_img, t->img);
             if (rc == CLS_OK) rc = upload(e, t->d_oimg, t->oimg);
             if (rc != CLS_OK) return rc;
@@ -290,7 +290,7 @@ static int table_put_locked(cls_engine* e, const char* name, const cls_rule* rul
         if (q.ok) {
             const Cls4Image& c = q.img.core;
             q.lin = linear4(q.img.sem);
-            q.lds_resident = c.lds_ok && c.lds_bytes <= uint32_t(max_lds_bytes());
+            q.lds_resident = c.lds_ok && c.lds_bytes + kLdsReserved <= uint32_t(max_lds_bytes());
             rc = upload(e, q.d_img, c);
             if (rc == CLS_OK) rc = upload(e, q.d_oimg, q.oimg);
             if (rc != CLS_OK) return rc;
@@ -441,7 +441,7 @@ static int cls_grid(const cls_engine* e, bool use_cls, bool lds_resident, uint32
         const int by_threads = 2048 / cls_block();
         per_cu = by_threads;
         if (lds_resident)
-            per_cu = std::max(1, std::min(by_threads, int(max_lds_bytes() / std::max<uint32_t>(1, lds_bytes))));
+            per_cu = std::max(1, std::min(by_threads, int(max_lds_bytes() / (lds_bytes + kLdsReserved))));
         if (const char* w = std::getenv("CONTIVCLS_WG_PER_CU"))   // diagnostics
             per_cu = std::max(1, std::min(by_threads, std::atoi(w)));
     }

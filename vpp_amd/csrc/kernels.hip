@@ -251,8 +251,8 @@ __device__ __forceinline__ void classify_n(const Img<kLds>& im, const Cls4Dev& t
     }
 
     if constexpr (kList >= 3) {
-        // Port-filtered sublists.  cell = {pointer table byte address | counter
-        // base << 16} (slot base + 0: the cell's own no-match slot, counted as
+        // Port-filtered sublists.  cell = {pointer table word address | counter
+        // base << 14} (slot base + 0: the cell's own no-match slot, counted as
         // default DENY); the pointer table holds, per global port
         // class, the initial search state of the sublist deciding first-match
         // for that class: state = outcome | 8-B slot of the current entry << 16,
@@ -271,7 +271,7 @@ __device__ __forceinline__ void classify_n(const Img<kLds>& im, const Cls4Dev& t
 #pragma unroll
             for (int q = 0; q < N; ++q) cell[q] = im.u32(row[q] + 4u * min(proto[q], 2u));
 #pragma unroll
-            for (int q = 0; q < N; ++q) st[q] = im.u32((cell[q] & 0xFFFFu) + pc[q]);
+            for (int q = 0; q < N; ++q) st[q] = im.u32(((cell[q] & 0x3FFFu) << 2) + pc[q]);
         }
         // kD >= 0: the table's depth is a template argument -- straight-line
         // probes.  kD < 0 (scalar tail, global-image variants): guarded steps
@@ -302,7 +302,7 @@ __device__ __forceinline__ void classify_n(const Img<kLds>& im, const Cls4Dev& t
 #pragma unroll
         for (int q = 0; q < N; ++q) {
             res[q] = st[q] & 3u;                                      // DENY when no entry
-            slot[q] = (cell[q] >> 16) + ((st[q] >> 2) & 63u);         // base + j + 1 (0: no entry)
+            slot[q] = (cell[q] >> 14) + ((st[q] >> 2) & 63u);         // base + j + 1 (0: no entry)
         }
     } else if constexpr (kList >= 1) {
         // Bit vectors: the entries of the cell's list covering the packet's dst
