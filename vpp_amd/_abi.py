@@ -138,6 +138,13 @@ def lib():
     if not os.path.exists(LIB_PATH):
         raise ClsError("libcontivcls.so not built (run __graft_entry__.build() or "
                        "make -C vpp_amd/csrc); the product has no CPU fallback")
+    _lib = bind(LIB_PATH)
+    return _lib
+
+
+def bind(path: str):
+    """Load a build of the library (RTLD_LOCAL: several builds may live in
+    one process -- tools/ab_inproc.py) and declare its signatures."""
     # One HIP runtime per process: PyTorch ships its own libamdhip64.so.7.
     # Load it first so that our NEEDED libamdhip64.so.7 resolves to the same
     # already-loaded runtime (two runtimes in one process cannot share the GPU).
@@ -145,7 +152,7 @@ def lib():
         import torch  # noqa: F401
     except ImportError:
         pass
-    L = C.CDLL(LIB_PATH)
+    L = C.CDLL(path, mode=os.RTLD_LOCAL | os.RTLD_NOW)
     vp, u32, u64, i32 = C.c_void_p, C.c_uint32, C.c_uint64, C.c_int32
     sig = {
         "cls_abi_version": (C.c_int, []),
@@ -179,7 +186,6 @@ def lib():
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args
-    _lib = L
     return L
 
 
