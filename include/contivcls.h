@@ -126,7 +126,9 @@ enum {
     CLS_F_ACCUMULATE = 1u << 2,   /* add to counters_out instead of overwriting */
     CLS_F_FORCE_LINEAR = 1u << 3, /* use the linear (ballot) kernel: GPU cross-check */
     CLS_F_TIMING = 1u << 4,       /* record HIP events around the classify kernel */
-    CLS_F_CONN_CLS = 1u << 5      /* cls_connect_batch: use the classifier images at any batch size */
+    CLS_F_CONN_CLS = 1u << 5,     /* cls_connect_batch: use the classifier images at any batch size */
+    CLS_F_COUNT = 1u << 6         /* cls_connect_batch: count every evalACL call's terminating rule
+                                     into the tables' connection counters (cls_conn_counters) */
 };
 
 typedef struct cls_engine cls_engine;
@@ -209,7 +211,10 @@ int cls_stream_floor(cls_engine* e, const cls_pkt_soa* pkts, uint64_t n, uint8_t
 /* ---- ACL configuration (ACLConfig, aclengine_mock.go:110-121,671-728) --- */
 /* PutACL semantics (:699-728): requires >=1 interface; re-putting a name
  * replaces it without counting an extra change; last writer wins per
- * interface direction. */
+ * interface direction.  A re-put whose rules equal the installed ACL's (the
+ * renderer re-puts a local table whose pods changed, acl_renderer.go:186-190)
+ * keeps the compiled table and its connection counters and only moves the
+ * interface bindings: no compilation, no upload. */
 int cls_acl_put(cls_engine* e, const char* acl_name, const cls_rule* rules,
                 uint32_t n_rules, const char* const* ingress_ifs, uint32_t n_ingress,
                 const char* const* egress_ifs, uint32_t n_egress);
@@ -219,6 +224,8 @@ int cls_acl_del(cls_engine* e, const char* acl_name);
 int cls_acl_table(cls_engine* e, const char* acl_name, uint32_t* table_id);
 /* GetNumOfACLs (:209), GetNumOfACLChanges (:237). */
 int cls_acl_counts(cls_engine* e, uint32_t* n_acls, uint32_t* n_changes);
+/* cls_acl_put calls that compiled a table / that kept the installed one. */
+int cls_acl_stats(cls_engine* e, uint32_t* n_compiles, uint32_t* n_rebinds);
 /* Interface id used by cls_conn_batch; ids are stable for the engine's life. */
 int cls_if_id(cls_engine* e, const char* if_name, uint32_t* id);
 /* Table id of the inbound/outbound ACL on an interface, -1 if none
@@ -230,12 +237,22 @@ int cls_if_acls(cls_engine* e, uint32_t if_id, int32_t* in_table, int32_t* out_t
  * with (src->dst, dport); SYN-ACK through dst_if inbound then src_if outbound
  * with (dst->src, sport); REFLECT marks sides reflected exactly as the
  * reference does.  Interface->ACL bindings are snapshotted at the call.
- * In batches >= 65536, an ACL with a compiled classifier image whose linear
- * work would be large (host batch: connections touching it x its rules >=
- * 2048 x batch, touches estimated from a sample; device batch: >= 2048
- * rules) is evaluated by the classifier kernel for both tuples of every
- * connection before the connection kernel runs; the others by a linear scan.  CLS_F_CONN_CLS: every imaged ACL
- * (>= 64 rules) at any batch size; CLS_F_FORCE_LINEAR: none.
+ * Addresses: CLS_AF_V4 (src4/dst4) or CLS_AF_V16 (src16/dst16, 16-byte
+ * aligned on the device; IPv4-mapped = IPv4, as Go's To4) -- Connection*
+ * takes any net.IP (:243-390).  A device batch's interface id outside the
+ * engine's ids gives CLS_CONN_FAILURE for that connection (a host batch is
+ * rejected with CLS_E_INVAL).
+ * Large ACLs: in batches >= 65536, an ACL with a compiled classifier image
+ * whose linear work would be large (host batch: connections touching it x
+ * its rules >= 2048 x batch, touches estimated from a hashed sample of <= 64
+ * Ki connections -- a heuristic, verdicts do not depend on it; device batch:
+ * >= 2048 rules) is evaluated by the classifier kernel for both tuples of
+ * every connection before the connection kernel runs; the others by a linear
+ * scan of compact rules, staged in LDS when they fit.  CLS_F_CONN_CLS: every
+ * imaged ACL (>= 64 rules) at any batch size; CLS_F_FORCE_LINEAR: none.
+ * CLS_F_COUNT: for every evalACL call the batch makes on a non-nil ACL (only
+ * the calls testConnection makes, in its order), the table's connection
+ * counter of the terminating rule (R: default DENY) is incremented.
  */
 typedef struct cls_conn_soa {
     cls_pkt_soa pkt;           /* src/dst/sport/dport/proto of the SYN */
@@ -244,6 +261,14 @@ typedef struct cls_conn_soa {
 } cls_conn_soa;
 int cls_connect_batch(cls_engine* e, const cls_conn_soa* conns, uint64_t n,
                       uint8_t* conn_verdict_out, uint32_t flags, void* stream);
+
+/* Per-(ACL, rule) hit counters of the connection path: counters_out[k]
+ * (k < R) = evalACL calls of cls_connect_batch (CLS_F_COUNT) on this table that
+ * terminated at rule k, counters_out[R] = calls that fell through to the
+ * default DENY (:667); summed over calls since the table was put or last
+ * reset (reset != 0 clears them after the read).  Waits for pending device
+ * work.  The reference has no counters. */
+int cls_conn_counters(cls_engine* e, uint32_t table_id, uint64_t* counters_out, uint32_t reset);
 
 /* ---- synthetic traffic (BASELINE.md / SURVEY 8(d) generator) -----------
  * Generates packets i in [first, first+n) of the counter-based splitmix64

@@ -73,6 +73,10 @@ def lib():
         L.orc_test_connection.restype = C.c_int
         L.orc_test_connection.argtypes = [C.POINTER(AclRef)] * 4 + [
             C.c_int, C.c_char_p, C.c_int, C.c_char_p, C.c_int, C.c_int, C.c_uint16, C.c_uint16]
+        L.orc_test_connection_hits.restype = C.c_int
+        L.orc_test_connection_hits.argtypes = [C.POINTER(AclRef)] * 4 + [
+            C.c_int, C.c_char_p, C.c_int, C.c_char_p, C.c_int, C.c_int, C.c_uint16, C.c_uint16,
+            C.POINTER(C.c_int32)]
         L.orc_classify_faithful.restype = C.c_int
         L.orc_classify_faithful.argtypes = [C.POINTER(ClsRule), C.c_uint32, C.c_int, C.c_void_p,
                                             C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64,

@@ -372,36 +372,53 @@ typedef struct orc_acl_ref {
     int nil;
 } orc_acl_ref;
 
+/* hits (may be NULL): the terminating rule of each evalACL call testConnection
+ * makes, in call order -- [0] src inbound (SYN), [1] dst outbound (SYN),
+ * [2] dst inbound (SYN-ACK), [3] src outbound (SYN-ACK); n of that ACL for the
+ * default DENY, -1 for a call not made or made on a nil ACL.  These define
+ * the connection path's per-(ACL, rule) hit counters (the reference has no
+ * counters: parity unpinned, as for cls_classify's). */
+int orc_test_connection_hits(const orc_acl_ref* src_in, const orc_acl_ref* src_out,
+                             const orc_acl_ref* dst_in, const orc_acl_ref* dst_out, int same_if,
+                             const uint8_t* src_ip, int src_len, const uint8_t* dst_ip, int dst_len,
+                             int proto, uint16_t sport, uint16_t dport, int32_t* hits) {
+    int src_refl = 0, dst_refl = 0, a;
+    int32_t h[4] = {-1, -1, -1, -1};
+#define ORC_RET(v) do { if (hits) memcpy(hits, h, sizeof h); return (v); } while (0)
+    a = orc_eval_acl(src_in->rules, src_in->n, src_in->nil, src_ip, src_len, dst_ip, dst_len, proto, dport, &h[0]);
+    if (a < 0) ORC_RET(a);
+    if (a == CLS_ACL_FAILURE) ORC_RET(CLS_CONN_FAILURE);
+    if (a == CLS_ACL_DENY) ORC_RET(CLS_CONN_DENY_SYN);
+    if (a == CLS_ACL_REFLECT) { src_refl = 1; if (same_if) dst_refl = 1; }
+    if (!dst_refl) {
+        a = orc_eval_acl(dst_out->rules, dst_out->n, dst_out->nil, src_ip, src_len, dst_ip, dst_len, proto, dport, &h[1]);
+        if (a < 0) ORC_RET(a);
+        if (a == CLS_ACL_FAILURE) ORC_RET(CLS_CONN_FAILURE);
+        if (a == CLS_ACL_DENY) ORC_RET(CLS_CONN_DENY_SYN);
+        if (a == CLS_ACL_REFLECT) { dst_refl = 1; if (same_if) src_refl = 1; }
+    }
+    if (!dst_refl) {
+        a = orc_eval_acl(dst_in->rules, dst_in->n, dst_in->nil, dst_ip, dst_len, src_ip, src_len, proto, sport, &h[2]);
+        if (a < 0) ORC_RET(a);
+        if (a == CLS_ACL_FAILURE) ORC_RET(CLS_CONN_FAILURE);
+        if (a == CLS_ACL_DENY) ORC_RET(CLS_CONN_DENY_SYN_ACK);
+    }
+    if (!src_refl) {
+        a = orc_eval_acl(src_out->rules, src_out->n, src_out->nil, dst_ip, dst_len, src_ip, src_len, proto, sport, &h[3]);
+        if (a < 0) ORC_RET(a);
+        if (a == CLS_ACL_FAILURE) ORC_RET(CLS_CONN_FAILURE);
+        if (a == CLS_ACL_DENY) ORC_RET(CLS_CONN_DENY_SYN_ACK);
+    }
+    ORC_RET(CLS_CONN_ALLOW);
+#undef ORC_RET
+}
+
 int orc_test_connection(const orc_acl_ref* src_in, const orc_acl_ref* src_out,
                         const orc_acl_ref* dst_in, const orc_acl_ref* dst_out, int same_if,
                         const uint8_t* src_ip, int src_len, const uint8_t* dst_ip, int dst_len,
                         int proto, uint16_t sport, uint16_t dport) {
-    int src_refl = 0, dst_refl = 0, a;
-    a = orc_eval_acl(src_in->rules, src_in->n, src_in->nil, src_ip, src_len, dst_ip, dst_len, proto, dport, NULL);
-    if (a < 0) return a;
-    if (a == CLS_ACL_FAILURE) return CLS_CONN_FAILURE;
-    if (a == CLS_ACL_DENY) return CLS_CONN_DENY_SYN;
-    if (a == CLS_ACL_REFLECT) { src_refl = 1; if (same_if) dst_refl = 1; }
-    if (!dst_refl) {
-        a = orc_eval_acl(dst_out->rules, dst_out->n, dst_out->nil, src_ip, src_len, dst_ip, dst_len, proto, dport, NULL);
-        if (a < 0) return a;
-        if (a == CLS_ACL_FAILURE) return CLS_CONN_FAILURE;
-        if (a == CLS_ACL_DENY) return CLS_CONN_DENY_SYN;
-        if (a == CLS_ACL_REFLECT) { dst_refl = 1; if (same_if) src_refl = 1; }
-    }
-    if (!dst_refl) {
-        a = orc_eval_acl(dst_in->rules, dst_in->n, dst_in->nil, dst_ip, dst_len, src_ip, src_len, proto, sport, NULL);
-        if (a < 0) return a;
-        if (a == CLS_ACL_FAILURE) return CLS_CONN_FAILURE;
-        if (a == CLS_ACL_DENY) return CLS_CONN_DENY_SYN_ACK;
-    }
-    if (!src_refl) {
-        a = orc_eval_acl(src_out->rules, src_out->n, src_out->nil, dst_ip, dst_len, src_ip, src_len, proto, sport, NULL);
-        if (a < 0) return a;
-        if (a == CLS_ACL_FAILURE) return CLS_CONN_FAILURE;
-        if (a == CLS_ACL_DENY) return CLS_CONN_DENY_SYN_ACK;
-    }
-    return CLS_CONN_ALLOW;
+    return orc_test_connection_hits(src_in, src_out, dst_in, dst_out, same_if, src_ip, src_len, dst_ip, dst_len,
+                                    proto, sport, dport, NULL);
 }
 
 /* ---------------------------------------------------------------------------

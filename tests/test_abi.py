@@ -47,4 +47,5 @@ def test_flag_values_match_header():
     flags = {m.group(1): 1 << int(m.group(2))
              for m in re.finditer(r"CLS_F_(\w+)\s*=\s*1u\s*<<\s*(\d+)", text)}
     assert flags == {"DEVICE": _abi.F_DEVICE, "NO_VERDICT": _abi.F_NO_VERDICT, "ACCUMULATE": _abi.F_ACCUMULATE,
-                     "FORCE_LINEAR": _abi.F_FORCE_LINEAR, "TIMING": _abi.F_TIMING, "CONN_CLS": _abi.F_CONN_CLS}
+                     "FORCE_LINEAR": _abi.F_FORCE_LINEAR, "TIMING": _abi.F_TIMING, "CONN_CLS": _abi.F_CONN_CLS,
+                     "COUNT": _abi.F_COUNT}

@@ -1,14 +1,22 @@
 """Connection path at scale on the GPU (testConnection, aclengine_mock.go:394-471;
 SURVEY 8(a5) / 8(f) rank 1).
 
-Many ACLs bound to many interfaces -- a 1003-rule rendered global table
-(config 2), 64 random local ACLs of 1-300 rules with REFLECT, DENY and
-PERMIT actions and odd protocols, interfaces with no ACL -- and 20k random
+Many ACLs bound to many interfaces -- a rendered global table (config 2,
+1003 rules), random local ACLs of 1-300 rules with REFLECT, DENY and PERMIT
+actions and odd protocols, interfaces with no ACL -- and 20k random
 connections between them, including same-interface pairs (the REFLECT
 short-cuts of :412-421).  Every ConnectionAction must equal the C oracle's
 orc_test_connection (aclengine_ref.c), bit for bit -- with the large ACLs
-evaluated by the classifier kernel (cls_connect_batch's precomputed SYN /
-SYN-ACK verdicts), by the linear scan, and in the automatic mode.
+evaluated by the classifier kernel (cls_connect_batch's slot-mode SYN /
+SYN-ACK passes), by the linear scan, and in the automatic mode; for IPv4
+(CLS_AF_V4) and mixed-family (CLS_AF_V16: IPv4-mapped and IPv6 endpoints,
+IPv6 and IPv4 networks in the ACLs) batches.
+
+Counters (CLS_F_COUNT): the per-(ACL, rule) connection counters must equal
+the oracle's -- the terminating rule of every evalACL call testConnection
+makes (orc_test_connection_hits), summed per ACL -- with the rule pool in LDS
+or global memory and the counters in LDS or global memory.  The reference
+has no counters (parity unpinned; the definition is the oracle's).
 """
 import ctypes as C
 import random
@@ -17,61 +25,132 @@ import numpy as np
 import pytest
 
 import oracle
-from aclgen import random_acl, random_traffic
+from aclgen import mix_families, random_acl, random_acl16, random_traffic, random_traffic16
 from vpp_amd import workload
 
 pytestmark = pytest.mark.gpu
 
-
-def _b4(a: int) -> bytes:
-    return int(a).to_bytes(4, "big")
+V6_TWIN = 0xFD000030 << 96
 
 
-def build(eng, seed=0, n_local=64, n_if=80, cfg=2):
+def build(eng, seed=0, n_local=64, n_if=80, cfg=2, fam=4):
+    """ACLs installed on `eng`; returns (interface names, binding: if -> [in
+    ACL name, out ACL name], rules by ACL name, prefix pool, traffic spec)."""
     rng = random.Random(seed)
     glob, spec, _ = workload.config(cfg)
+    grules = glob.rules
+    if fam == 16:
+        tr0 = random_traffic(1, 4, random_acl(1, 1)[1])
+        grules, _ = mix_families(grules, tr0, seed)
     ifs = ["if%d" % i for i in range(n_if)]
-    bind = {name: [None, None] for name in ifs}          # name -> [in rules, out rules]
-    acls = [("global", glob.rules, ["if0", "if1"], ["if0", "if2"])]
+    bind = {name: [None, None] for name in ifs}
+    acls = [("global", grules, ["if0", "if1"], ["if0", "if2"])]
     pool = None
     for k in range(n_local):
-        rules, pool = random_acl(1000 + k, rng.choice([1, 3, 12, 40, 150, 300]),
-                                 weird=rng.choice([0.0, 0.003, 0.15]))
+        size = rng.choice([1, 3, 12, 40, 150, 300])
+        weird = rng.choice([0.0, 0.003, 0.15])
+        rules, pool = (random_acl16 if fam == 16 else random_acl)(1000 + k, size, weird=weird)
         ing = rng.sample(ifs[3:], rng.randrange(1, 3))
         eg = rng.sample(ifs[3:], rng.randrange(0, 3))
         acls.append(("local%d" % k, rules, ing, eg))
+    by_name = {}
     for name, rules, ing, eg in acls:
         assert eng.acl_put(name, rules, ing, eg) == 0
+        by_name[name] = rules
         for i in ing:
-            bind[i][0] = rules
+            bind[i][0] = name
         for e in eg:
-            bind[e][1] = rules
-    return ifs, bind, pool, spec
+            bind[e][1] = name
+    return ifs, bind, by_name, pool, spec
 
 
-def oracle_connections(bind, ifs, si, di, src, dst, proto, sport, dport):
-    crs = {}
+def traffic(seed, n, pool, spec, fam):
+    rng = np.random.default_rng(seed)
+    pods = spec["pod_ips"].astype(np.uint32)
+    mix = rng.random(n) < 0.33                       # a third of the sources are the global table's pods
+    if fam == 4:
+        tr = random_traffic(50 + seed, n, pool)
+        tr["src"][mix] = rng.choice(pods, mix.sum())
+        return tr
+    tr = random_traffic16(50 + seed, n, pool)
+    p = rng.choice(pods, mix.sum()).astype(np.uint64)
+    twin = rng.random(mix.sum()) < 0.5
+    hi = np.where(twin, np.uint64(V6_TWIN >> 64), np.uint64(0))
+    lo = np.where(twin, np.uint64(0), np.uint64(0xFFFF << 32)) | p
+    b = np.empty((mix.sum(), 16), np.uint8)
+    b[:, :8] = hi.astype(">u8").view(np.uint8).reshape(-1, 8)
+    b[:, 8:] = lo.astype(">u8").view(np.uint8).reshape(-1, 8)
+    tr["src"][mix] = b
+    return tr
 
-    def ref(rules):
-        if rules is None:
+
+def _addr(a, fam) -> bytes:
+    return int(a).to_bytes(4, "big") if fam == 4 else bytes(a)
+
+
+def oracle_connections(bind, by_name, ifs, si, di, tr, fam):
+    """Verdicts and per-ACL hit counters (name -> R + 1 counts)."""
+    crs = {name: oracle.rules_to_c(rules) for name, rules in by_name.items()}
+    counts = {name: np.zeros(len(rules) + 1, np.uint64) for name, rules in by_name.items()}
+
+    def ref(name):
+        if name is None:
             return oracle.AclRef(None, 0, 1)
-        key = id(rules)
-        if key not in crs:
-            crs[key] = oracle.rules_to_c(rules)
-        cr = crs[key]
-        return oracle.AclRef(cr.ptr(), cr.n, 0)
+        return oracle.AclRef(crs[name].ptr(), crs[name].n, 0)
 
     L = oracle.lib()
-    out = np.zeros(len(src), np.uint8)
-    for i in range(len(src)):
+    n = len(tr["proto"])
+    out = np.zeros(n, np.uint8)
+    hits = (C.c_int32 * 4)()
+    alen = 4 if fam == 4 else 16
+    for i in range(n):
         a, b = ifs[si[i]], ifs[di[i]]
-        refs = [ref(bind[a][0]), ref(bind[a][1]), ref(bind[b][0]), ref(bind[b][1])]
-        s, d = _b4(src[i]), _b4(dst[i])
-        rc = L.orc_test_connection(*[C.byref(r) for r in refs], 1 if a == b else 0, s, 4, d, 4,
-                                   int(proto[i]), int(sport[i]), int(dport[i]))
+        names = [bind[a][0], bind[a][1], bind[b][0], bind[b][1]]
+        s, d = _addr(tr["src"][i], fam), _addr(tr["dst"][i], fam)
+        rc = L.orc_test_connection_hits(*[C.byref(ref(x)) for x in names], 1 if a == b else 0, s, alen, d, alen,
+                                        int(tr["proto"][i]), int(tr["sport"][i]), int(tr["dport"][i]), hits)
         assert rc >= 0
         out[i] = rc
-    return out
+        # call order: src inbound, dst outbound, dst inbound, src outbound
+        for k, name in zip(range(4), (names[0], names[3], names[2], names[1])):
+            if hits[k] >= 0:
+                counts[name][hits[k]] += 1
+    return out, counts
+
+
+def _run(eng, seed, mode, fam, count, n=20000, n_local=64):
+    ifs, bind, by_name, pool, spec = build(eng, seed, fam=fam, n_local=n_local)
+    tr = traffic(seed, n, pool, spec, fam)
+    rng = np.random.default_rng(seed)
+    ids = np.array([eng.if_id(x) for x in ifs], np.uint32)
+    si = rng.integers(0, len(ifs), n)
+    di = np.where(rng.random(n) < 0.1, si, rng.integers(0, len(ifs), n))
+    args = [ids[si], ids[di], tr["src"], tr["dst"], tr["proto"], tr["sport"], tr["dport"]]
+    if mode == "device":                      # CLS_F_DEVICE batch: every ACL >= 64 rules on the classifier
+        import torch
+
+        def dev(x):
+            x = np.ascontiguousarray(x)
+            if x.ndim == 2:
+                return torch.from_numpy(x).to("cuda")
+            return torch.from_numpy(x.view({4: np.int32, 2: np.int16, 1: np.uint8}[x.dtype.itemsize])).to("cuda")
+        dv = [dev(x) for x in args]
+        torch.cuda.synchronize()
+        got = eng.connect_batch(*dv, mode="classifier", count=count).cpu().numpy()
+    else:
+        got = eng.connect_batch(*args, mode=mode, count=count)
+    want, wcounts = oracle_connections(bind, by_name, ifs, si, di, tr, fam)
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, (bad[:10], got[bad[:10]], want[bad[:10]])
+    assert len(set(want.tolist())) >= 3              # allowed, denied, reflected/failure all seen
+    if count:
+        for name in by_name:
+            c = eng.conn_counters(name, reset=True)
+            d = np.nonzero(c != wcounts[name])[0]
+            assert d.size == 0, (name, d[:10], c[d[:10]], wcounts[name][d[:10]])
+        assert sum(int(v.sum()) for v in wcounts.values()) > n // 4   # counted calls seen
+        assert not eng.conn_counters("global").any()    # reset
+    return want
 
 
 @pytest.mark.parametrize("mode", ["classifier", "linear", "auto", "device"])
@@ -80,30 +159,83 @@ def test_connections_at_scale_match_oracle(seed, mode):
     from vpp_amd.engine import Engine
     eng = Engine()
     try:
-        ifs, bind, pool, spec = build(eng, seed)
-        n = 20000
-        tr = random_traffic(50 + seed, n, pool)
-        rng = np.random.default_rng(seed)
-        # a third of the endpoints from the global table's pod addresses
-        pods = spec["pod_ips"].astype(np.uint32)
-        mix = rng.random(n) < 0.33
-        tr["src"][mix] = rng.choice(pods, mix.sum())
+        _run(eng, seed, mode, 4, count=False)
+    finally:
+        eng.close()
+
+
+@pytest.mark.parametrize("mode", ["classifier", "linear", "device"])
+def test_connections16_mixed_families_match_oracle(mode):
+    """CLS_AF_V16 batches: IPv4-mapped and IPv6 endpoints, both families of
+    networks, counters included."""
+    from vpp_amd.engine import Engine
+    eng = Engine()
+    try:
+        _run(eng, 3, mode, 16, count=True, n=12000)
+    finally:
+        eng.close()
+
+
+@pytest.mark.parametrize("fam", [4, 16])
+@pytest.mark.parametrize("no_lds", [0, 1, 2, 3])
+def test_connection_counters_match_oracle(fam, no_lds, monkeypatch):
+    """Per-(ACL, rule) counters with the rule pool in LDS (few locals: the
+    pool fits) or in global memory, the counters in LDS or global memory."""
+    from vpp_amd.engine import Engine
+    monkeypatch.setenv("CONTIVCLS_CONN_NO_LDS", str(no_lds))
+    eng = Engine()
+    try:
+        _run(eng, 7 + no_lds, "classifier", fam, count=True, n=8000, n_local=12)
+    finally:
+        eng.close()
+
+
+def test_connection_counters_accumulate_over_calls():
+    """Counters add up over batches until read with reset; nil ACLs are not counted."""
+    from vpp_amd.engine import Engine
+    eng = Engine()
+    try:
+        ifs, bind, by_name, pool, spec = build(eng, 5, n_local=8, n_if=20)
+        tr = traffic(5, 3000, pool, spec, 4)
+        rng = np.random.default_rng(5)
         ids = np.array([eng.if_id(x) for x in ifs], np.uint32)
-        si = rng.integers(0, len(ifs), n)
-        di = np.where(rng.random(n) < 0.1, si, rng.integers(0, len(ifs), n))
+        si, di = rng.integers(0, len(ifs), 3000), rng.integers(0, len(ifs), 3000)
         args = [ids[si], ids[di], tr["src"], tr["dst"], tr["proto"], tr["sport"], tr["dport"]]
-        if mode == "device":                      # CLS_F_DEVICE batch: every ACL >= 64 rules on the classifier
-            import torch
-            dv = [torch.from_numpy(np.ascontiguousarray(x).view({4: np.int32, 2: np.int16, 1: np.uint8}[x.dtype.itemsize]))
-                  .to("cuda") for x in args]
-            torch.cuda.synchronize()
-            got = eng.connect_batch(*dv, mode="classifier").cpu().numpy()
-        else:
-            got = eng.connect_batch(*args, mode=mode)
-        want = oracle_connections(bind, ifs, si, di, tr["src"], tr["dst"], tr["proto"], tr["sport"],
-                                  tr["dport"])
-        bad = np.nonzero(got != want)[0]
-        assert bad.size == 0, (bad[:10], got[bad[:10]], want[bad[:10]])
-        assert len(set(want.tolist())) >= 3              # allowed, denied, reflected/failure all seen
+        eng.connect_batch(*args, count=True)
+        eng.connect_batch(*args, count=True)
+        eng.connect_batch(*args)                     # not counted
+        _, want = oracle_connections(bind, by_name, ifs, si, di, tr, 4)
+        for name in by_name:
+            assert np.array_equal(eng.conn_counters(name), 2 * want[name]), name
+    finally:
+        eng.close()
+
+
+def test_device_batch_unknown_interface_is_failure():
+    """A device batch cannot be checked on the host: an interface id outside
+    the engine's ids is a Failure verdict for that connection (never a read
+    out of bounds)."""
+    import torch
+    from vpp_amd.engine import Engine
+    eng = Engine()
+    try:
+        ifs, bind, by_name, pool, spec = build(eng, 2, n_local=4, n_if=10)
+        n = 4096
+        tr = traffic(2, n, pool, spec, 4)
+        rng = np.random.default_rng(2)
+        si = rng.integers(0, 10, n).astype(np.uint32)
+        di = rng.integers(0, 10, n).astype(np.uint32)
+        bad = rng.random(n) < 0.1
+        si[bad] = 1 << 20
+        ids = np.array([eng.if_id(x) for x in ifs], np.uint32)
+        si_ok = np.where(bad, 0, si)
+        dv = [torch.from_numpy(np.ascontiguousarray(x).view({4: np.int32, 2: np.int16, 1: np.uint8}[x.dtype.itemsize]))
+              .to("cuda") for x in [np.where(bad, si, ids[si_ok]).astype(np.uint32), ids[di], tr["src"], tr["dst"],
+                                    tr["proto"], tr["sport"], tr["dport"]]]
+        got = eng.connect_batch(*dv).cpu().numpy()
+        assert (got[bad] == 3).all()
+        want, _ = oracle_connections(bind, by_name, ifs, si_ok[~bad], di[~bad],
+                                     {k: v[~bad] for k, v in tr.items()}, 4)
+        assert np.array_equal(got[~bad], want)
     finally:
         eng.close()

@@ -7,7 +7,9 @@
 
 The same chain with the oracle MockACLEngine restatement (OracleACLEngine)
 gives the expected ConnectionAction for every connection: pod to pod, pod to
-internet and internet to pod, between 150 pods with random policies.
+internet and internet to pod, between 150 pods with random policies.  With
+IPv6 pods among them the batch goes through the 16-byte connection path
+(CLS_AF_V16: IPv4 endpoints IPv4-mapped, as Go's To4/To16 see them).
 """
 import random
 
@@ -36,12 +38,16 @@ def chain(engine_factory, cache, assign, contiv):
     return engine
 
 
+@pytest.mark.parametrize("families", ["v4", "mixed"])
 @pytest.mark.parametrize("seed", range(2))
-def test_policy_chain_connections_on_gpu(seed):
+def test_policy_chain_connections_on_gpu(seed, families):
     from vpp_amd.engine import ACLEngine, Engine
     rng = random.Random(seed)
     cache, assign = random_policy_set(rng, n_pods=150, n_policies=50)
-    cache = {p: ip for p, ip in cache.items() if ":" not in ip}      # the connection path is IPv4
+    if families == "v4":
+        cache = {p: ip for p, ip in cache.items() if ":" not in ip}
+    else:
+        assert any(":" in ip for ip in cache.values())
     contiv = ContivIfs(main_if="GbE", vxlan_bvi="VXLAN-BVI", host_interconnect="VPP-Host")
     for k, pod in enumerate(cache):
         contiv.set_pod_if_name(pod, "tap%d" % k)
@@ -56,6 +62,8 @@ def test_policy_chain_connections_on_gpu(seed):
             proto, sport = rng.randrange(2), rng.randrange(1024, 65536)
             dport = rng.choice([22, 53, 80, 443, 8080, rng.randrange(65536)])
             ext = "10.%d.%d.%d" % (rng.randrange(4), rng.randrange(256), rng.randrange(256))
+            if families == "mixed" and rng.random() < 0.3:
+                ext = "fd00:10::%x" % rng.randrange(1 << 16)
             if k < 0.6:
                 calls.append(("ConnectionPodToPod", (rng.choice(pods), rng.choice(pods), proto, sport, dport)))
             elif k < 0.8:

@@ -7,7 +7,10 @@ half of the connections entering through a global-table interface.  Times
 ``Engine.connect_batch`` over N connections with host arrays in and out
 (PCIe copies included; auto and linear modes) and with device-resident
 tensors (CLS_F_DEVICE, ``hbm_resident``), and the C oracle (one thread) on a sample.  Prints one
-JSON line.  usage: python tools/conn_bench.py [--n 4194304] [--iters 5]
+JSON line.  --count 1 times CLS_F_COUNT batches (per-(ACL, rule) counters)
+beside the plain ones; --locals sets the number of local ACLs (12: a rule
+pool that fits LDS).
+usage: python tools/conn_bench.py [--n 4194304] [--iters 5] [--locals 64]
 """
 import argparse
 import json
@@ -30,10 +33,12 @@ def main():
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--cpu-sample", type=int, default=20000)
     ap.add_argument("--other-proto", type=int, default=1, help="6%% of packets with protocol > 2")
+    ap.add_argument("--locals", type=int, default=64)
+    ap.add_argument("--count", type=int, default=1)
     a = ap.parse_args()
     from vpp_amd.engine import Engine
     eng = Engine()
-    ifs, bind, pool, spec = build(eng, 0, cfg=3)
+    ifs, bind, by_name, pool, spec = build(eng, 0, cfg=3, n_local=a.locals)
     n = a.n
     tr = random_traffic(7, n, pool, other_proto=bool(a.other_proto))
     rng = np.random.default_rng(7)
@@ -65,16 +70,24 @@ def main():
     for _ in range(a.iters):
         dev_out = eng.connect_batch(*dargs)
     dev_dt = (time.perf_counter() - t0) / a.iters
+    counted = None
+    if a.count:
+        eng.connect_batch(*dargs, count=True)
+        t0 = time.perf_counter()
+        for _ in range(a.iters):
+            eng.connect_batch(*dargs, count=True)
+        dt_c = (time.perf_counter() - t0) / a.iters
+        counted = {"value": round(n / dt_c / 1e6, 3), "unit": "Mconn/s", "ms_per_batch": round(dt_c * 1e3, 3)}
     k = a.cpu_sample
     t1 = time.perf_counter()
-    want = oracle_connections(bind, ifs, si[:k], di[:k], tr["src"][:k], tr["dst"][:k], tr["proto"][:k],
-                              tr["sport"][:k], tr["dport"][:k])
+    want, _ = oracle_connections(bind, by_name, ifs, si[:k], di[:k], {f: v[:k] for f, v in tr.items()}, 4)
     cpu_dt = time.perf_counter() - t1
     assert np.array_equal(out[:k], want), "connection verdicts differ from the oracle"
     print(json.dumps({
         "metric": "connections classified per second (testConnection, up to 4 ACL evaluations each)",
         "value": round(n / dt / 1e6, 3), "unit": "Mconn/s", "n": n, "ms_per_batch": round(dt * 1e3, 3),
-        "pcie_included": True, "global_rules": len(bind["if0"][0]), "other_proto": bool(a.other_proto),
+        "pcie_included": True, "global_rules": len(by_name["global"]), "local_acls": a.locals,
+        "other_proto": bool(a.other_proto), "hbm_resident_counted": counted,
         "hbm_resident": {"value": round(n / dev_dt / 1e6, 3), "unit": "Mconn/s",
                          "ms_per_batch": round(dev_dt * 1e3, 3)},
         "linear_scan": {"value": round(n / res["linear"][0] / 1e6, 3), "unit": "Mconn/s",

@@ -31,7 +31,7 @@ def source_hash() -> str:
 # status codes
 OK, E_INVAL, E_NOMEM, E_HIP, E_RCCL, E_NOTFOUND, E_NODEV = 0, -1, -2, -3, -4, -5, -6
 # flags
-F_DEVICE, F_NO_VERDICT, F_ACCUMULATE, F_FORCE_LINEAR, F_TIMING, F_CONN_CLS = 1, 2, 4, 8, 16, 32
+F_DEVICE, F_NO_VERDICT, F_ACCUMULATE, F_FORCE_LINEAR, F_TIMING, F_CONN_CLS, F_COUNT = 1, 2, 4, 8, 16, 32, 64
 AF_V4, AF_V16 = 4, 16
 
 R_MATCHES, R_MACIP, R_IPRULE, R_IP, R_OTHER = 1, 2, 4, 8, 16
@@ -45,7 +45,8 @@ SYMBOLS = ["cls_abi_version", "cls_engine_create", "cls_engine_destroy", "cls_la
            "cls_last_kernel_ms", "cls_kernel_times", "cls_kernel_times_reset", "cls_acl_put", "cls_acl_del", "cls_acl_table", "cls_acl_counts",
            "cls_if_id",
            "cls_if_acls", "cls_connect_batch", "cls_gen_traffic_v4", "cls_compile_v4",
-           "cls_compile_v16", "cls_gen_traffic_v16", "cls_stream_floor"]
+           "cls_compile_v16", "cls_gen_traffic_v16", "cls_stream_floor", "cls_conn_counters",
+           "cls_acl_stats"]
 
 
 class ClsRule(C.Structure):
@@ -175,6 +176,8 @@ def bind(path: str):
         "cls_if_id": (C.c_int, [vp, C.c_char_p, C.POINTER(u32)]),
         "cls_if_acls": (C.c_int, [vp, u32, C.POINTER(i32), C.POINTER(i32)]),
         "cls_connect_batch": (C.c_int, [vp, C.POINTER(ConnSoa), u64, vp, u32, vp]),
+        "cls_conn_counters": (C.c_int, [vp, u32, vp, u32]),
+        "cls_acl_stats": (C.c_int, [vp, C.POINTER(u32), C.POINTER(u32)]),
         "cls_gen_traffic_v4": (C.c_int, [vp, C.POINTER(TrafficSpec), u64, u64, vp, vp, vp, vp,
                                          vp, vp]),
         "cls_compile_v4": (C.c_int, [C.POINTER(ClsRule), u32, vp, u64, C.POINTER(u64)]),

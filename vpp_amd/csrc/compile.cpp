@@ -169,18 +169,72 @@ std::vector<LinRule4> linear4(const std::vector<SemRule>& sem) {
     return v;
 }
 
-std::vector<LinRule16> linear16(const std::vector<SemRule>& sem) {
-    std::vector<LinRule16> v(sem.size());
+// An ICMP / OTHER term spans every port (the compact forms rely on it).
+static void check_port_free(const SemRule& s) {
+    for (int p = P_ICMP; p < NPROTO; ++p)
+        if (s.t[p].term && (s.t[p].lo != 0 || s.t[p].hi != 0xFFFF)) std::abort();
+}
+
+std::vector<ConnRule4> conn_rules4(const std::vector<SemRule>& sem) {
+    std::vector<ConnRule4> v(sem.size());
     for (size_t i = 0; i < sem.size(); ++i) {
         const SemRule& s = sem[i];
-        LinRule16& l = v[i];
-        std::memset(&l, 0, sizeof l);
-        l.src_any = s.src_any; l.dst_any = s.dst_any;
-        if (!s.src_any) { std::memcpy(l.src_addr, s.src.addr, 16); l.src_len = uint8_t(s.src.len); }
-        if (!s.dst_any) { std::memcpy(l.dst_addr, s.dst.addr, 16); l.dst_len = uint8_t(s.dst.len); }
-        for (int p = 0; p < NPROTO; ++p) l.port[p] = pack_port(s.t[p]);
-        l.meta = pack_meta(s);
-        l.index = s.index;
+        check_port_free(s);
+        ConnRule4& c = v[i];
+        std::memset(&c, 0, sizeof c);
+        if (!s.src_any) { c.src_mask = v4_mask(s.src.len); c.src_addr = v4_word(s.src.addr) & c.src_mask; }
+        if (!s.dst_any) { c.dst_mask = v4_mask(s.dst.len); c.dst_addr = v4_word(s.dst.addr) & c.dst_mask; }
+        c.port[0] = pack_port(s.t[P_TCP]);
+        c.port[1] = pack_port(s.t[P_UDP]);
+        c.meta = pack_meta(s);
+        c.index = s.index;
+    }
+    return v;
+}
+
+// A prefix as 4 little-endian words of its 16 network-order bytes and masks
+// (ConnRule16); returns the fam bit (1: IPv6 prefix).
+static uint32_t conn_prefix16(const Prefix& p, uint32_t* a, uint32_t* m) {
+    uint8_t ab[16] = {}, mb[16] = {};
+    int off = 0, len = p.len;
+    if (p.fam == 4) {                        // ::ffff:a.b.c.d/(96 + len)
+        ab[10] = ab[11] = 0xFF;
+        std::memcpy(ab + 12, p.addr, 4);
+        off = 12;
+        std::memset(mb, 0xFF, 12);
+    } else {
+        std::memcpy(ab, p.addr, 16);
+    }
+    for (int b = off; b < 16; ++b) {
+        const int ones = len - 8 * (b - off);
+        mb[b] = ones >= 8 ? 0xFF : ones <= 0 ? 0 : uint8_t(0xFF << (8 - ones));
+    }
+    for (int w = 0; w < 4; ++w) {
+        uint32_t x = 0, y = 0;
+        for (int j = 3; j >= 0; --j) {
+            x = (x << 8) | ab[4 * w + j];
+            y = (y << 8) | mb[4 * w + j];
+        }
+        m[w] = y;
+        a[w] = x & y;
+    }
+    return p.fam == 16 ? 1u : 0u;
+}
+
+std::vector<ConnRule16> conn_rules16(const std::vector<SemRule>& sem) {
+    std::vector<ConnRule16> v(sem.size());
+    for (size_t i = 0; i < sem.size(); ++i) {
+        const SemRule& s = sem[i];
+        check_port_free(s);
+        ConnRule16& c = v[i];
+        std::memset(&c, 0, sizeof c);
+        uint32_t fam = 0;
+        if (!s.src_any) fam |= conn_prefix16(s.src, c.src, c.smask);
+        if (!s.dst_any) fam |= conn_prefix16(s.dst, c.dst, c.dmask) << 1;
+        c.port[0] = pack_port(s.t[P_TCP]);
+        c.port[1] = pack_port(s.t[P_UDP]);
+        c.meta = pack_meta(s);
+        c.index_fam = (s.index << 2) | fam;
     }
     return v;
 }

@@ -91,20 +91,37 @@ struct alignas(16) LinRule4 {
 };
 static_assert(sizeof(LinRule4) == 48, "LinRule4 layout");
 
-struct alignas(16) LinRule16 {
-    uint8_t src_addr[16], dst_addr[16];
-    uint8_t src_len, dst_len, src_any, dst_any;
-    uint32_t port[NPROTO];
-    uint32_t meta;
-    uint32_t index;
-    uint32_t pad[1];
-};
-static_assert(sizeof(LinRule16) == 64, "LinRule16 layout");
-
 std::vector<LinRule4> linear4(const std::vector<SemRule>& sem);
 // the rules with src and dst exchanged (Cls4Image::swap)
 std::vector<SemRule> swap_sides(const std::vector<SemRule>& sem);
-std::vector<LinRule16> linear16(const std::vector<SemRule>& sem);
+
+// ---- connection-path rules (cls_connect_batch; staged in LDS) -------------
+// Only the TCP and UDP terms carry a port range: an ICMP or OTHER term always
+// spans every port (icmp_term, and evalACL's fall-through), so the compact
+// forms drop those two port words.  meta byte p: bit7 = TERM, bits0-1 = result.
+struct alignas(16) ConnRule4 {
+    uint32_t src_addr, src_mask, dst_addr, dst_mask;
+    uint32_t port[2];        // TCP, UDP: lo | (hi - lo) << 16
+    uint32_t meta;
+    uint32_t index;          // rule index in the ACL
+};
+static_assert(sizeof(ConnRule4) == 32, "ConnRule4 layout");
+// 16-byte packets: addresses compared as loaded (network-order bytes in
+// little-endian words).  An IPv4 prefix is stored in its IPv4-mapped form
+// with full masks on words 0-2, so only IPv4-mapped packets can match it; an
+// IPv6 prefix sets fam bit 0 (src) / 1 (dst), and an IPv4-mapped packet never
+// matches it (Go 1.9 IPNet.Contains compares lengths after To4,
+// aclengine_mock.go:506,520).  ANY: masks zero, fam bit clear.
+struct alignas(16) ConnRule16 {
+    uint32_t src[4], smask[4], dst[4], dmask[4];
+    uint32_t port[2];
+    uint32_t meta;
+    uint32_t index_fam;      // rule index << 2 | fam bits
+};
+static_assert(sizeof(ConnRule16) == 80, "ConnRule16 layout");
+// sem from semantic_rules(..., fam 4) / (..., fam 0) respectively
+std::vector<ConnRule4> conn_rules4(const std::vector<SemRule>& sem);
+std::vector<ConnRule16> conn_rules16(const std::vector<SemRule>& sem);
 
 // ---- IPv4 classifier image -------------------------------------------------
 struct Cls4Image {

@@ -81,6 +81,7 @@ struct Counters {
 struct Table {
     std::string name;
     uint32_t n_rules = 0;
+    std::string sig;           // the rules as given (rule_sig): a re-put of equal rules keeps this table
     // linear (ballot) table, also the protocol>2 fallback
     std::vector<LinRule4> lin4;
     DevBuf d_lin4;
@@ -102,7 +103,15 @@ struct Table {
         DevBuf d_img, d_lin, d_oimg;
         DevBuf d_src_search;       // src_mode 1: the source interval table (global memory)
         bool lds_resident = false;
+        DevBuf d_slot_rule;        // slot mode (connection batches): slot -> rule, core then OTHER image
     } p16;
+    // connection path: compact linear rules (cls_connect_batch's rule pool),
+    // slot -> rule of the v4 images (slot mode), and the per-rule connection
+    // counters (CLS_F_COUNT; allocated on first use, R + 1 u64)
+    std::vector<ConnRule4> conn4;
+    std::vector<ConnRule16> conn16;
+    DevBuf d_slot_rule;
+    DevBuf d_conn_ctr;
     // declared last: destroyed first, so pending device work is waited for
     // before any of the buffers above are freed
     Counters c4, c16;
@@ -129,9 +138,11 @@ struct cls_engine {
     std::vector<std::string> if_names;
     std::vector<std::pair<int32_t, int32_t>> if_acl;   // per if id: (inbound, outbound) table id
     uint32_t changes = 0;
+    uint32_t compiles = 0, rebinds = 0;   // cls_acl_put: tables compiled / puts that kept the table
     // scratch for host-pointer batches
     DevBuf s_src, s_dst, s_sport, s_dport, s_proto, s_verdict, s_if_a, s_if_b, s_desc, s_ifs;
-    DevBuf s_pre;                  // connection path: classifier verdicts per large ACL (2 bytes/connection)
+    DevBuf s_pre;                  // connection path: classifier slot words per large ACL (8 bytes/connection)
+    DevBuf s_rules, s_tctr, s_cctr;  // connection path: rule pool, table counter pointers, call counters
     DevBuf s_pool;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool timed = false;
@@ -230,6 +241,35 @@ static int counters_init(cls_engine* e, Counters& c, const Cls4Image* img, const
     return CLS_OK;
 }
 
+// slot -> rule of an image and its OTHER image (slot mode of the classify
+// kernels: OTHER slots follow the main image's)
+static int upload_slot_rule(cls_engine* e, DevBuf& d, const Cls4Image& img, const Cls4Image& oimg) {
+    std::vector<uint32_t> m(img.ctr_rule.begin(), img.ctr_rule.end());
+    m.insert(m.end(), oimg.ctr_rule.begin(), oimg.ctr_rule.end());
+    HIPC(e, d.ensure(std::max<size_t>(1, m.size()) * 4));
+    if (!m.empty()) HIPC(e, hipMemcpy(d.p, m.data(), m.size() * 4, hipMemcpyHostToDevice));
+    return CLS_OK;
+}
+
+// The rules as the caller gave them, serialised (NULL network = ""): two
+// puts with equal signatures compile to the same table.
+static std::string rule_sig(const cls_rule* rules, uint32_t n) {
+    std::string sg;
+    sg.reserve(size_t(n) * 80);
+    for (uint32_t k = 0; k < n; ++k) {
+        const cls_rule& r = rules[k];
+        const uint32_t w[14] = {r.flags, uint32_t(r.acl_action), r.tcp_src_lo, r.tcp_src_hi, r.tcp_dst_lo,
+                                r.tcp_dst_hi, r.udp_src_lo, r.udp_src_hi, r.udp_dst_lo, r.udp_dst_hi,
+                                r.icmp_code_first, r.icmp_code_last, r.icmp_type_first, r.icmp_type_last};
+        sg.append(reinterpret_cast<const char*>(w), sizeof w);
+        sg.append(r.src_network ? r.src_network : "");
+        sg.push_back('\0');
+        sg.append(r.dst_network ? r.dst_network : "");
+        sg.push_back('\0');
+    }
+    return sg;
+}
+
 // The main classifier of a rule set and its OTHER image (protocols > 2), in
 // the main image's orientation.
 static bool build_pair(const std::vector<SemRule>& sem, uint32_t n, Cls4Image& img, Cls4Image& oimg,
@@ -253,11 +293,13 @@ static int table_put_locked(cls_engine* e, const char* name, const cls_rule* rul
     auto t = std::make_shared<Table>();
     t->name = name ? name : "";
     t->n_rules = n;
+    t->sig = rule_sig(rules, n);
     std::vector<SemRule> sem;
     std::string why;
     int rc = semantic_rules(rules, n, 4, sem, why);
     if (rc != CLS_OK) return fail(e, rc, "%s", why.c_str());
     t->lin4 = linear4(sem);
+    t->conn4 = conn_rules4(sem);
     HIPC(e, hipSetDevice(e->device));
     HIPC(e, t->d_lin4.ensure(std::max<size_t>(1, t->lin4.size()) * sizeof(LinRule4)));
     if (!t->lin4.empty())
@@ -271,6 +313,7 @@ static int table_put_locked(cls_engine* e, const char* name, const cls_rule* rul
             t->lds_resident = t->img.lds_ok && t->img.lds_bytes + kLdsReserved <= uint32_t(max_lds_bytes());
             rc = upload(e, t->d_img, t->img);
             if (rc == CLS_OK) rc = upload(e, t->d_oimg, t->oimg);
+            if (rc == CLS_OK) rc = upload_slot_rule(e, t->d_slot_rule, t->img, t->oimg);
             if (rc != CLS_OK) return rc;
         }
     }
@@ -284,6 +327,7 @@ static int table_put_locked(cls_engine* e, const char* name, const cls_rule* rul
         std::vector<SemRule> s16;
         rc = semantic_rules(rules, n, 0, s16, why);
         if (rc != CLS_OK) return fail(e, rc, "%s", why.c_str());
+        t->conn16 = conn_rules16(s16);
         std::string why16;
         q.ok = build_cls16(s16, n, q.img, why16) && build_other4(q.img.sem, n, q.oimg, why16);
         q.why = why16;
@@ -293,6 +337,7 @@ static int table_put_locked(cls_engine* e, const char* name, const cls_rule* rul
             q.lds_resident = c.lds_ok && c.lds_bytes + kLdsReserved <= uint32_t(max_lds_bytes());
             rc = upload(e, q.d_img, c);
             if (rc == CLS_OK) rc = upload(e, q.d_oimg, q.oimg);
+            if (rc == CLS_OK) rc = upload_slot_rule(e, q.d_slot_rule, c, q.oimg);
             if (rc != CLS_OK) return rc;
             HIPC(e, q.d_lin.ensure(std::max<size_t>(1, q.lin.size()) * sizeof(LinRule4)));
             if (!q.lin.empty())
@@ -845,13 +890,29 @@ int cls_acl_put(cls_engine* e, const char* acl_name, const cls_rule* rules, uint
     if (!e || !acl_name) return CLS_E_INVAL;
     std::lock_guard<std::mutex> g(e->mu);
     if (n_ingress + n_egress == 0) return fail(e, CLS_E_INVAL, "ACL with empty interfaces");
-    uint32_t tid;
-    int rc = table_put_locked(e, acl_name, rules, n_rules, &tid);
-    if (rc != CLS_OK) return rc;
+    if (n_rules && !rules) return fail(e, CLS_E_INVAL, "rules is NULL");
     const std::string name(acl_name);
-    if (e->acls.count(name)) {          // PutACL: delete the original first, not a change
-        acl_del_locked(e, name);
-        e->changes--;
+    uint32_t tid;
+    auto old = e->acls.find(name);
+    auto same = old == e->acls.end() ? e->tables.end() : e->tables.find(old->second.table_id);
+    if (same != e->tables.end() && same->second->sig == rule_sig(rules, n_rules)) {
+        // Equal rules (the renderer re-puts a table whose pods changed,
+        // acl_renderer.go:186-190): keep the compiled table, move the bindings.
+        tid = old->second.table_id;
+        for (auto& b : e->if_acl) {
+            if (b.first == int32_t(tid)) b.first = -1;
+            if (b.second == int32_t(tid)) b.second = -1;
+        }
+        e->acls.erase(old);
+        e->rebinds++;
+    } else {
+        int rc = table_put_locked(e, acl_name, rules, n_rules, &tid);
+        if (rc != CLS_OK) return rc;
+        if (old != e->acls.end()) {         // PutACL: delete the original first, not a change
+            acl_del_locked(e, name);
+            e->changes--;
+        }
+        e->compiles++;
     }
     AclEntry a;
     a.table_id = tid;
@@ -867,6 +928,14 @@ int cls_acl_put(cls_engine* e, const char* acl_name, const cls_rule* rules, uint
     }
     e->acls[name] = a;
     e->changes++;
+    return CLS_OK;
+}
+
+int cls_acl_stats(cls_engine* e, uint32_t* n_compiles, uint32_t* n_rebinds) {
+    if (!e) return CLS_E_INVAL;
+    std::lock_guard<std::mutex> g(e->mu);
+    if (n_compiles) *n_compiles = e->compiles;
+    if (n_rebinds) *n_rebinds = e->rebinds;
     return CLS_OK;
 }
 
@@ -914,22 +983,36 @@ int cls_connect_batch(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t*
     if (!e || !c || (n && !out)) return CLS_E_INVAL;
     std::lock_guard<std::mutex> g(e->mu);
     const cls_pkt_soa& pk = c->pkt;
-    if (pk.af != CLS_AF_V4) return fail(e, CLS_E_INVAL, "only CLS_AF_V4 connections are supported");
-    if (n && (!pk.src4 || !pk.dst4 || !pk.sport || !pk.dport || !pk.proto || !c->src_if || !c->dst_if))
+    const bool k16 = pk.af == CLS_AF_V16;
+    if (!k16 && pk.af != CLS_AF_V4) return fail(e, CLS_E_INVAL, "af must be CLS_AF_V4 or CLS_AF_V16");
+    const void *src = k16 ? static_cast<const void*>(pk.src16) : pk.src4,
+               *dst = k16 ? static_cast<const void*>(pk.dst16) : pk.dst4;
+    if (n && (!src || !dst || !pk.sport || !pk.dport || !pk.proto || !c->src_if || !c->dst_if))
         return fail(e, CLS_E_INVAL, "missing connection arrays");
+    const bool dev = flags & CLS_F_DEVICE, count = flags & CLS_F_COUNT;
+    const size_t ab = k16 ? 16 : 4;                       // address bytes
+    if (dev && k16 && n && (!aligned(src, 16) || !aligned(dst, 16)))
+        return fail(e, CLS_E_INVAL, "device src16/dst16 must be 16-byte aligned");
     HIPC(e, hipSetDevice(e->device));
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : e->stream;
-    // snapshot the bindings: descriptor per table, (in, out) per interface
-    std::vector<AclDesc> desc;
-    std::vector<std::shared_ptr<Table>> dtab;     // table of each descriptor
+    // Snapshot the bindings: one descriptor per bound table, (in, out) per
+    // interface.  Linear ACLs' compact rules go to the call's rule pool.
+    std::vector<ConnDesc> desc;
+    std::vector<std::shared_ptr<Table>> dtab;             // table of each descriptor
     std::unordered_map<int32_t, int32_t> slot;
+    uint32_t n_ctr = 0;
     auto desc_of = [&](int32_t tid) -> int32_t {
         if (tid < 0) return -1;
         auto f = slot.find(tid);
         if (f != slot.end()) return f->second;
         auto t = e->tables.find(uint32_t(tid));
         if (t == e->tables.end()) return -1;
-        AclDesc d{t->second->d_lin4.as<LinRule4>(), uint32_t(t->second->lin4.size()), 1u, nullptr};
+        const Table& T = *t->second;
+        ConnDesc d{};
+        d.n = uint32_t(k16 ? T.conn16.size() : T.conn4.size());
+        d.n_rules = T.n_rules;
+        d.ctr_off = n_ctr;
+        n_ctr += T.n_rules + 1;
         desc.push_back(d);
         dtab.push_back(t->second);
         slot[tid] = int32_t(desc.size() - 1);
@@ -938,62 +1021,70 @@ int cls_connect_batch(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t*
     std::vector<IfAcls> ifs(std::max<size_t>(1, e->if_acl.size()));
     for (size_t i = 0; i < e->if_acl.size(); ++i)
         ifs[i] = IfAcls{desc_of(e->if_acl[i].first), desc_of(e->if_acl[i].second)};
-    if (desc.empty()) desc.push_back(AclDesc{nullptr, 0, 0, nullptr});
-    if (!(flags & CLS_F_DEVICE))
+    const uint32_t n_ifs = uint32_t(e->if_acl.size());
+    if (!dev)
         for (uint64_t i = 0; i < n; ++i)
-            if (c->src_if[i] >= e->if_acl.size() || c->dst_if[i] >= e->if_acl.size())
+            if (c->src_if[i] >= n_ifs || c->dst_if[i] >= n_ifs)
                 return fail(e, CLS_E_INVAL, "connection %llu: unknown interface id", (unsigned long long)i);
-    const uint32_t *src = pk.src4, *dst = pk.dst4, *sif = c->src_if, *dif = c->dst_if;
+    const uint32_t *sif = c->src_if, *dif = c->dst_if;
     const uint16_t *sp = pk.sport, *dp = pk.dport;
     const uint8_t* pr = pk.proto;
     uint8_t* o = out;
-    const bool dev = flags & CLS_F_DEVICE;
     if (!dev && n) {
-        HIPC(e, e->s_src.ensure(n * 4)); HIPC(e, e->s_dst.ensure(n * 4));
+        HIPC(e, e->s_src.ensure(n * ab)); HIPC(e, e->s_dst.ensure(n * ab));
         HIPC(e, e->s_if_a.ensure(n * 4)); HIPC(e, e->s_if_b.ensure(n * 4));
         HIPC(e, e->s_sport.ensure(n * 2)); HIPC(e, e->s_dport.ensure(n * 2));
         HIPC(e, e->s_proto.ensure(n)); HIPC(e, e->s_verdict.ensure(n));
-        HIPC(e, hipMemcpyAsync(e->s_src.p, src, n * 4, hipMemcpyHostToDevice, s));
-        HIPC(e, hipMemcpyAsync(e->s_dst.p, dst, n * 4, hipMemcpyHostToDevice, s));
+        HIPC(e, hipMemcpyAsync(e->s_src.p, src, n * ab, hipMemcpyHostToDevice, s));
+        HIPC(e, hipMemcpyAsync(e->s_dst.p, dst, n * ab, hipMemcpyHostToDevice, s));
         HIPC(e, hipMemcpyAsync(e->s_if_a.p, sif, n * 4, hipMemcpyHostToDevice, s));
         HIPC(e, hipMemcpyAsync(e->s_if_b.p, dif, n * 4, hipMemcpyHostToDevice, s));
         HIPC(e, hipMemcpyAsync(e->s_sport.p, sp, n * 2, hipMemcpyHostToDevice, s));
         HIPC(e, hipMemcpyAsync(e->s_dport.p, dp, n * 2, hipMemcpyHostToDevice, s));
         HIPC(e, hipMemcpyAsync(e->s_proto.p, pr, n, hipMemcpyHostToDevice, s));
-        src = e->s_src.as<uint32_t>(); dst = e->s_dst.as<uint32_t>();
+        src = e->s_src.p; dst = e->s_dst.p;
         sif = e->s_if_a.as<uint32_t>(); dif = e->s_if_b.as<uint32_t>();
         sp = e->s_sport.as<uint16_t>(); dp = e->s_dport.as<uint16_t>();
         pr = e->s_proto.as<uint8_t>(); o = e->s_verdict.as<uint8_t>();
     }
     // Large ACLs: the classifier evaluates the SYN tuple (src, dst, dport) and
-    // the SYN-ACK tuple (dst, src, sport) of every connection, one launch
-    // each; the connection kernel then reads those verdicts instead of
-    // scanning the ACL.  Whole-batch evaluation keeps the classify launches
-    // dense (no compaction); it costs 2 launches per large ACL.
+    // the SYN-ACK tuple (dst, src, sport) of every connection, one slot-mode
+    // launch each (res | slot << 2 per connection); the connection kernel
+    // then reads those words instead of scanning the ACL, and maps the slot
+    // to its rule only for the calls testConnection makes.  Whole-batch
+    // evaluation keeps the classify launches dense (no compaction).
     // Which ACLs: with a host batch, those whose linear work would be large --
     // connections touching the ACL x its rule count >= kConnClsWork x batch
     // (touches estimated per interface binding from <= 64 Ki sampled
-    // connections); with a device batch, the
-    // ACLs of >= kConnClsDevRules rules.  CLS_F_CONN_CLS: every imaged ACL.
+    // connections, at hashed positions); with a device batch, the ACLs of >=
+    // kConnClsDevRules rules.  CLS_F_CONN_CLS: every imaged ACL.
     std::vector<uint32_t> big;
     if (n && !(flags & CLS_F_FORCE_LINEAR) && (n >= kConnClsMinBatch || (flags & CLS_F_CONN_CLS))) {
         std::vector<uint64_t> touch(dtab.size(), 0);
         if (!dev && !(flags & CLS_F_CONN_CLS)) {
-            // an estimate is enough: every step-th connection, scaled back
-            const uint64_t step = std::max<uint64_t>(1, n / 65536);
+            const uint64_t m = std::min<uint64_t>(n, 65536);
             std::vector<uint64_t> per_if(ifs.size(), 0);
-            for (uint64_t i = 0; i < n; i += step) {
-                per_if[c->src_if[i]] += step;
-                if (c->dst_if[i] != c->src_if[i]) per_if[c->dst_if[i]] += step;
+            for (uint64_t k = 0; k < m; ++k) {
+                // sample k: a splitmix-scrambled position in stratum k (no stride aliasing)
+                uint64_t z = (k + 1) * 0x9E3779B97F4A7C15ull;
+                z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+                z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+                z ^= z >> 31;
+                const uint64_t lo = k * n / m, hi = (k + 1) * n / m;
+                const uint64_t i = lo + z % (hi - lo);
+                per_if[c->src_if[i]] += 1;
+                if (c->dst_if[i] != c->src_if[i]) per_if[c->dst_if[i]] += 1;
             }
-            for (size_t f = 0; f < e->if_acl.size(); ++f) {
-                if (ifs[f].in >= 0) touch[ifs[f].in] += per_if[f];
-                if (ifs[f].out >= 0 && ifs[f].out != ifs[f].in) touch[ifs[f].out] += per_if[f];
+            for (size_t f = 0; f < n_ifs; ++f) {
+                const uint64_t t = per_if[f] * n / m;
+                if (ifs[f].in >= 0) touch[ifs[f].in] += t;
+                if (ifs[f].out >= 0 && ifs[f].out != ifs[f].in) touch[ifs[f].out] += t;
             }
         }
         for (uint32_t j = 0; j < dtab.size(); ++j) {
             const Table& t = *dtab[j];
-            if (!t.has_cls || t.n_rules < kConnClsMinRules) continue;
+            const bool imaged = k16 ? t.p16.ok : t.has_cls;
+            if (!imaged || t.n_rules < kConnClsMinRules) continue;
             const bool want = (flags & CLS_F_CONN_CLS) ||
                               (dev ? t.n_rules >= kConnClsDevRules
                                    : double(touch[j]) * t.n_rules >= double(kConnClsWork) * double(n));
@@ -1002,48 +1093,128 @@ int cls_connect_batch(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t*
     }
     if (!big.empty()) {
         if (n > kClsChunk) return fail(e, CLS_E_INVAL, "connection batch above 2^30 with classifier ACLs");
-        HIPC(e, e->s_pre.ensure(big.size() * 2 * n));
+        HIPC(e, e->s_pre.ensure(big.size() * 2 * n * 4));
         for (size_t b = 0; b < big.size(); ++b) {
             Table& t = *dtab[big[b]];
-            uint8_t* pre = e->s_pre.as<uint8_t>() + b * 2 * n;
+            uint32_t* pre = e->s_pre.as<uint32_t>() + b * 2 * n;
             desc[big[b]].pre = pre;
-            Cls4Dev cd = table_dev(t);
             LaunchCfg cfg;
             cfg.stream = s;
-            cfg.other = cls4_dev(t.oimg, t.d_oimg, DevBuf(), 0, t.n_rules);
-            cfg.grid = cls_grid(e, true, t.lds_resident, t.img.lds_bytes, n);
-            Scratch* sc = nullptr;
-            {
-                const int rc = scratch_of(e, t.c4, t.n_rules, s, &sc);
-                if (rc != CLS_OK) return rc;
+            if (!k16) {
+                desc[big[b]].slot_rule = t.d_slot_rule.as<uint32_t>();
+                Cls4Dev cd = table_dev(t);
+                cfg.other = cls4_dev(t.oimg, t.d_oimg, DevBuf(), 0, t.n_rules);
+                cfg.grid = cls_grid(e, true, t.lds_resident, t.img.lds_bytes, n);
+                const uint32_t *s4 = static_cast<const uint32_t*>(src), *d4 = static_cast<const uint32_t*>(dst);
+                const Pkts4 syn = framed(t.img, Pkts4{s4, d4, dp, pr, n}), ack = framed(t.img, Pkts4{d4, s4, sp, pr, n});
+                HIPC(e, launch_classify4_slots(cd, syn, pre, t.lds_resident, cfg));
+                HIPC(e, launch_classify4_slots(cd, ack, pre + n, t.lds_resident, cfg));
+            } else {
+                auto& q = t.p16;
+                desc[big[b]].slot_rule = q.d_slot_rule.as<uint32_t>();
+                const Cls4Image& ci = q.img.core;
+                Cls4Dev cd = cls4_dev(ci, q.d_img, q.d_lin, uint32_t(q.lin.size()), t.n_rules);
+                cfg.other = cls4_dev(q.oimg, q.d_oimg, DevBuf(), 0, t.n_rules);
+                cfg.grid = cls_grid(e, true, q.lds_resident, ci.lds_bytes, n);
+                const Fe16 fe = fe16(q.img, q.d_src_search);
+                const uint4 *s16 = static_cast<const uint4*>(src), *d16 = static_cast<const uint4*>(dst);
+                Pkts16 syn{s16, d16, dp, pr, n, 0u}, ack{d16, s16, sp, pr, n, 0u};
+                if (ci.swap) {                               // destination-keyed image
+                    std::swap(syn.src, syn.dst);
+                    std::swap(ack.src, ack.dst);
+                }
+                HIPC(e, launch_classify16_slots(cd, fe, syn, pre, q.lds_resident, cfg));
+                HIPC(e, launch_classify16_slots(cd, fe, ack, pre + n, q.lds_resident, cfg));
             }
-            if (t.lds_resident) cd.part = sc->part.as<uint32_t>();
-            unsigned long long* slot_val = sc->slot_val.as<unsigned long long>();
-            const Pkts4 syn = framed(t.img, Pkts4{src, dst, dp, pr, n}), ack = framed(t.img, Pkts4{dst, src, sp, pr, n});
-            for (int k = 0; k < 2; ++k) {
-                const Pkts4& q = k ? ack : syn;
-                const bool vec = aligned(q.src, 16) && aligned(q.dst, 16) && aligned(q.dport, 8) &&
-                                 aligned(q.proto, 4) && aligned(pre + k * n, 4);
-                HIPC(e, launch_classify4_cls(cd, q, pre + k * n, slot_val, t.lds_resident, vec, cfg));
-            }
-            // these launches' slot counts are not the connection's: cleared
-            HIPC(e, launch_remap(slot_val, t.c4.d_csr.as<uint2>(), t.c4.n_slots, nullptr, s));
-            HIPC(e, hipEventRecord(sc->done, s));
         }
     }
-    HIPC(e, e->s_desc.ensure(desc.size() * sizeof(AclDesc)));
-    HIPC(e, e->s_ifs.ensure(ifs.size() * sizeof(IfAcls)));
-    HIPC(e, hipMemcpyAsync(e->s_desc.p, desc.data(), desc.size() * sizeof(AclDesc), hipMemcpyHostToDevice, s));
-    HIPC(e, hipMemcpyAsync(e->s_ifs.p, ifs.data(), ifs.size() * sizeof(IfAcls), hipMemcpyHostToDevice, s));
-    HIPC(e, launch_connect4(e->s_desc.as<AclDesc>(), e->s_ifs.as<IfAcls>(), sif, dif, src, dst, sp, dp, pr,
-                            n, o, s));
-    if (!dev) {
-        if (n) HIPC(e, hipMemcpyAsync(out, o, n, hipMemcpyDeviceToHost, s));
-        HIPC(e, hipStreamSynchronize(s));
-    } else {
-        // descriptor buffers are engine scratch: finish before they can be reused
-        HIPC(e, hipStreamSynchronize(s));
+    // the rule pool of the linear ACLs
+    std::vector<uint8_t> pool;
+    const size_t rb = k16 ? sizeof(ConnRule16) : sizeof(ConnRule4);
+    for (size_t j = 0; j < desc.size(); ++j) {
+        if (desc[j].pre) {
+            desc[j].n = 0;
+            continue;
+        }
+        desc[j].rule_off = uint32_t(pool.size() / rb);
+        const uint8_t* r = k16 ? reinterpret_cast<const uint8_t*>(dtab[j]->conn16.data())
+                               : reinterpret_cast<const uint8_t*>(dtab[j]->conn4.data());
+        pool.insert(pool.end(), r, r + size_t(desc[j].n) * rb);
     }
+    ConnArgs a{};
+    a.n_ifs = n_ifs;
+    a.rules_bytes = uint32_t(pool.size());
+    a.n_ctr = count ? n_ctr : 0;
+    a.src_if = sif; a.dst_if = dif; a.src = src; a.dst = dst;
+    a.sport = sp; a.dport = dp; a.proto = pr; a.n = n; a.out = o;
+    // LDS: the rule pool first (every evaluation step reads it), then the u32
+    // counters if they fit beside it; otherwise global-memory variants
+    // (CONTIVCLS_CONN_NO_LDS, tests: bit 0 rules from global memory, bit 1
+    // global counters)
+    const char* nl = std::getenv("CONTIVCLS_CONN_NO_LDS");
+    const int no_lds = nl ? std::atoi(nl) : 0;
+    const size_t lds_max = size_t(max_lds_bytes());
+    const bool lds_rules = n && !pool.empty() && pool.size() <= lds_max && !(no_lds & 1);
+    const size_t lds_used = lds_rules ? pool.size() : 0;
+    int cmode = 0;
+    if (count && n_ctr) cmode = lds_used + size_t(n_ctr) * 4 <= lds_max && !(no_lds & 2) ? 1 : 2;
+    a.ctr_lds = uint32_t(lds_used);
+    HIPC(e, e->s_desc.ensure(std::max<size_t>(1, desc.size()) * sizeof(ConnDesc)));
+    HIPC(e, e->s_ifs.ensure(ifs.size() * sizeof(IfAcls)));
+    HIPC(e, e->s_rules.ensure(std::max<size_t>(16, pool.size())));
+    if (!desc.empty())
+        HIPC(e, hipMemcpyAsync(e->s_desc.p, desc.data(), desc.size() * sizeof(ConnDesc), hipMemcpyHostToDevice, s));
+    HIPC(e, hipMemcpyAsync(e->s_ifs.p, ifs.data(), ifs.size() * sizeof(IfAcls), hipMemcpyHostToDevice, s));
+    if (!pool.empty()) HIPC(e, hipMemcpyAsync(e->s_rules.p, pool.data(), pool.size(), hipMemcpyHostToDevice, s));
+    a.desc = e->s_desc.as<ConnDesc>();
+    a.ifs = e->s_ifs.as<IfAcls>();
+    a.rules = e->s_rules.p;
+    std::vector<unsigned long long*> tctr;
+    if (cmode) {
+        HIPC(e, e->s_cctr.ensure(size_t(n_ctr) * 8));
+        HIPC(e, hipMemsetAsync(e->s_cctr.p, 0, size_t(n_ctr) * 8, s));
+        a.ctr = e->s_cctr.as<unsigned long long>();
+        for (size_t j = 0; j < dtab.size(); ++j) {
+            Table& t = *dtab[j];
+            if (!t.d_conn_ctr.p) {
+                HIPC(e, t.d_conn_ctr.ensure(size_t(t.n_rules + 1) * 8));
+                HIPC(e, hipMemsetAsync(t.d_conn_ctr.p, 0, size_t(t.n_rules + 1) * 8, s));
+            }
+            tctr.push_back(t.d_conn_ctr.as<unsigned long long>());
+        }
+        HIPC(e, e->s_tctr.ensure(tctr.size() * sizeof(void*)));
+        HIPC(e, hipMemcpyAsync(e->s_tctr.p, tctr.data(), tctr.size() * sizeof(void*), hipMemcpyHostToDevice, s));
+    }
+    // persistent grid: as many 1024-thread workgroups per CU as the LDS allows
+    const size_t lds = lds_used + (cmode == 1 ? size_t(n_ctr) * 4 : 0);
+    const int per_cu = lds ? std::max(1, std::min(2, int(lds_max / lds))) : 2;
+    const int grid = int(std::max<uint64_t>(1, std::min<uint64_t>(uint64_t(e->n_cu) * per_cu, (n + 1023) / 1024)));
+    HIPC(e, launch_connect(a, k16, lds_rules, cmode, grid, s));
+    if (cmode && n)
+        HIPC(e, launch_conn_scatter(a.desc, e->s_tctr.as<unsigned long long* const>(), uint32_t(desc.size()),
+                                    e->s_cctr.as<unsigned long long>(), s));
+    if (!dev && n) HIPC(e, hipMemcpyAsync(out, o, n, hipMemcpyDeviceToHost, s));
+    // descriptor, pool and counter buffers are engine scratch: finish before
+    // they can be reused (and before the host vectors above go away)
+    HIPC(e, hipStreamSynchronize(s));
+    return CLS_OK;
+}
+
+int cls_conn_counters(cls_engine* e, uint32_t table_id, uint64_t* counters_out, uint32_t reset) {
+    if (!e || !counters_out) return CLS_E_INVAL;
+    std::lock_guard<std::mutex> g(e->mu);
+    auto it = e->tables.find(table_id);
+    if (it == e->tables.end()) return fail(e, CLS_E_NOTFOUND, "no table %u", table_id);
+    Table& t = *it->second;
+    HIPC(e, hipSetDevice(e->device));
+    const size_t bytes = size_t(t.n_rules + 1) * 8;
+    if (!t.d_conn_ctr.p) {
+        std::memset(counters_out, 0, bytes);
+        return CLS_OK;
+    }
+    HIPC(e, hipDeviceSynchronize());          // every stream's connection batches on this table
+    HIPC(e, hipMemcpy(counters_out, t.d_conn_ctr.p, bytes, hipMemcpyDeviceToHost));
+    if (reset) HIPC(e, hipMemset(t.d_conn_ctr.p, 0, bytes));
     return CLS_OK;
 }
 

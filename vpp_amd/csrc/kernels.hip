@@ -434,6 +434,27 @@ __device__ __forceinline__ void run_n(const Img<kLds>& im, const Cls4Dev& t, con
     // (hot_lane + slot * 256 bytes: one bank per lane) and folded at the end.
     typedef __attribute__((address_space(3))) uint32_t* lctr_t;
     uint32_t addr[N];
+    if constexpr (kCtr == 2) {
+        // Slot mode (connection batches, cls_connect_batch): no counting; the
+        // result word is res | slot << 2, OTHER packets classified in place
+        // with their slots after the main image's (the caller maps slots to
+        // rules for the evaluations testConnection actually makes).
+#pragma unroll
+        for (int q = 0; q < N; ++q) res[q] |= slot[q] << 2;
+        if (__any(pr_any)) {
+            const Img<false> oim{reinterpret_cast<const uint8_t*>(o.img)};
+#pragma unroll
+            for (int q = 0; q < N; ++q) {
+                if (pr[q] > 2u) {
+                    const uint32_t s1[1] = {sl[q]}, d1[1] = {d[q]}, p1[1] = {dp[q]}, z1[1] = {0u};
+                    uint32_t r1[1], k1[1];
+                    classify_n<1, false, 0, 0, -1>(oim, o, s1, d1, p1, z1, r1, k1);
+                    res[q] = r1[0] | ((t.n_ctr + k1[0]) << 2);
+                }
+            }
+        }
+        return;
+    }
 #pragma unroll
     for (int q = 0; q < N; ++q) {
         if constexpr (kLds && kCtr == 0) {
@@ -718,9 +739,11 @@ __global__ __launch_bounds__(kClsBlock) void classify4_cls(Cls4Dev t, Cls4Dev o,
         const uint32_t ix[1] = {i};
         run_n<1, kLds, kMode, kList, -1, kCtr>(im, t, o, hot_lane, gslot, hot0, sa, da, pa, ra, ra[0] > 2u, v, sa,
                                                ix, oq_lds);
-        if (verdict) verdict[i] = uint8_t(v[0]);
+        if constexpr (kCtr == 2) reinterpret_cast<uint32_t*>(verdict)[i] = v[0];   // slot mode: res | slot << 2
+        else if (verdict) verdict[i] = uint8_t(v[0]);
     }
 
+    if constexpr (kCtr == 2) return;
     if constexpr (!kLds) {
         if (hot0) atomicAdd(&gslot[0], (unsigned long long)hot0);
     }
@@ -1044,13 +1067,17 @@ __global__ __launch_bounds__(kClsBlock) void classify16_cls(Cls4Dev t, Cls4Dev o
             uint32_t pa[2] = {dp[2 * h], dp[2 * h + 1]}, ra[2] = {pr[2 * h], pr[2 * h + 1]}, v2[2];
             const uint32_t ix[2] = {base + 64u * (2 * h), base + 64u * (2 * h + 1)};
             classify(s2, d2, pa, ra, (ra[0] | ra[1]) > 2u, v2, ix);
-            if (verdict) {
+            if constexpr (kCtr == 2) {                                 // slot mode: res | slot << 2
+                reinterpret_cast<uint32_t*>(verdict)[base + 64u * (2 * h)] = v2[0];
+                reinterpret_cast<uint32_t*>(verdict)[base + 64u * (2 * h + 1)] = v2[1];
+            } else if (verdict) {
                 __builtin_nontemporal_store(uint8_t(v2[0]), verdict + base + 64u * (2 * h));
                 __builtin_nontemporal_store(uint8_t(v2[1]), verdict + base + 64u * (2 * h + 1));
             }
         }
     }
 #else
+    static_assert(kCtr != 2, "slot mode (connection batches) needs the wave-contiguous order");
     const uint32_t nsteps = p.vec ? uint32_t(p.n / 4u) : 0u;
     const uint2* DP = reinterpret_cast<const uint2*>(p.dport);
     const uint32_t* PR = reinterpret_cast<const uint32_t*>(p.proto);
@@ -1085,8 +1112,10 @@ __global__ __launch_bounds__(kClsBlock) void classify16_cls(Cls4Dev t, Cls4Dev o
         uint32_t pa[1] = {p.dport[i]}, ra[1] = {p.proto[i]};
         const uint32_t ix[1] = {i};
         classify(s1, d1, pa, ra, ra[0] > 2u, v, ix);
-        if (verdict) verdict[i] = uint8_t(v[0]);
+        if constexpr (kCtr == 2) reinterpret_cast<uint32_t*>(verdict)[i] = v[0];
+        else if (verdict) verdict[i] = uint8_t(v[0]);
     }
+    if constexpr (kCtr == 2) return;
     if constexpr (!kLds) {
         if (hot0) atomicAdd(&gslot[0], (unsigned long long)hot0);
     }
@@ -1230,56 +1259,202 @@ __global__ __launch_bounds__(256) void remap_kernel(unsigned long long* __restri
     if (out && k < n && v && (lane == 0 || prev != rule)) atomicAdd(&out[rule], v);
 }
 
-// evalACL on one ACL; returns ACLAction (nil ACL: PERMIT).  ACLs with a
-// classifier image were evaluated for both tuples before this kernel (pre).
-__device__ uint32_t eval_acl4(const AclDesc* __restrict__ acls, int32_t a, uint32_t src,
-                              uint32_t dst, uint32_t port, uint32_t p, uint64_t pre_idx) {
-    if (a < 0) return 1u;
-    const AclDesc A = acls[a];
-    if (!A.valid) return 1u;
-    if (A.pre) return A.pre[pre_idx];
-    uint32_t res, rule;
-    linear_one(A.rules, A.n, 0xFFFFFFFFu, src, dst, port, p, res, rule);
+// ---------------------------------------------------------------------------
+// Connection batches: testConnection (aclengine_mock.go:394-471), one lane per
+// connection, persistent grid.  Up to four evalACL calls per connection, in
+// the reference's order and with its REFLECT short-cuts: SYN through the
+// source interface's inbound then the destination's outbound ACL with
+// (src, dst, dport); SYN-ACK through the destination's inbound then the
+// source's outbound ACL with (dst, src, sport).  An ACL the host evaluated
+// with the classifier (slot mode, both tuples of every connection) is read
+// from its slot words; the others are scanned from the call's rule pool of
+// compact rules (compile.hpp ConnRule4 / ConnRule16), staged in LDS when it
+// fits -- every lane may scan a different ACL, so the scans are divergent,
+// but LDS serves them without the global-memory latency of each step.
+// Counting (CLS_F_COUNT): the terminating rule of every call made on a
+// non-nil ACL -> the call's counter space (descriptor ctr_off + rule), in LDS
+// (u32, folded into the u64 counters at the end) or with wave-aggregated
+// global atomics.
+
+template <bool k16> struct ConnT;
+template <> struct ConnT<false> {
+    typedef uint32_t A;
+    typedef ConnRule4 R;
+};
+template <> struct ConnT<true> {
+    typedef uint4 A;
+    typedef ConnRule16 R;
+};
+
+template <bool kLds>
+__device__ __forceinline__ ConnRule4 conn_rule(const ConnRule4* g, uint32_t i) {
+    if constexpr (kLds) {                      // the pool at LDS address 0: two ds_read_b128
+        const uint32_t a = i * uint32_t(sizeof(ConnRule4));
+        const v4u x = *lds128_t(a), y = *lds128_t(a + 16u);
+        ConnRule4 r;
+        r.src_addr = x.x; r.src_mask = x.y; r.dst_addr = x.z; r.dst_mask = x.w;
+        r.port[0] = y.x; r.port[1] = y.y; r.meta = y.z; r.index = y.w;
+        return r;
+    } else {
+        return g[i];
+    }
+}
+template <bool kLds>
+__device__ __forceinline__ ConnRule16 conn_rule(const ConnRule16* g, uint32_t i) {
+    if constexpr (kLds) {
+        const uint32_t a = i * uint32_t(sizeof(ConnRule16));
+        v4u w[5];
+#pragma unroll
+        for (int k = 0; k < 5; ++k) w[k] = *lds128_t(a + 16u * k);
+        ConnRule16 r;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            r.src[k] = w[0][k]; r.smask[k] = w[1][k]; r.dst[k] = w[2][k]; r.dmask[k] = w[3][k];
+        }
+        r.port[0] = w[4].x; r.port[1] = w[4].y; r.meta = w[4].z; r.index_fam = w[4].w;
+        return r;
+    } else {
+        return g[i];
+    }
+}
+__device__ __forceinline__ bool conn_match(const ConnRule4& r, uint32_t s, uint32_t d, bool, bool) {
+    return (((s ^ r.src_addr) & r.src_mask) | ((d ^ r.dst_addr) & r.dst_mask)) == 0u;
+}
+// s4 / d4: the address is IPv4-mapped (Go's To4 succeeds)
+__device__ __forceinline__ bool conn_match(const ConnRule16& r, const uint4& s, const uint4& d, bool s4, bool d4) {
+    const uint32_t x = ((s.x ^ r.src[0]) & r.smask[0]) | ((s.y ^ r.src[1]) & r.smask[1]) |
+                       ((s.z ^ r.src[2]) & r.smask[2]) | ((s.w ^ r.src[3]) & r.smask[3]) |
+                       ((d.x ^ r.dst[0]) & r.dmask[0]) | ((d.y ^ r.dst[1]) & r.dmask[1]) |
+                       ((d.z ^ r.dst[2]) & r.dmask[2]) | ((d.w ^ r.dst[3]) & r.dmask[3]);
+    const uint32_t fam = r.index_fam & 3u;
+    return x == 0u && !((fam & 1u) && s4) && !((fam & 2u) && d4);
+}
+__device__ __forceinline__ uint32_t conn_index(const ConnRule4& r) { return r.index; }
+__device__ __forceinline__ uint32_t conn_index(const ConnRule16& r) { return r.index_fam >> 2; }
+__device__ __forceinline__ bool mapped4(uint32_t) { return true; }
+__device__ __forceinline__ bool mapped4(const uint4& a) { return (a.x | a.y) == 0u && a.z == 0xFFFF0000u; }
+
+// One evalACL call: ACLAction, and the counter key of its terminating rule
+// (~0u for a nil ACL: PERMIT, not counted -- aclengine_mock.go:476-478).
+template <bool k16, bool kLds>
+__device__ __forceinline__ uint32_t conn_eval(const ConnArgs& a, int32_t di, uint32_t tuple, uint64_t i,
+                                              const typename ConnT<k16>::A& s, const typename ConnT<k16>::A& d,
+                                              bool s4, bool d4, uint32_t port, uint32_t p, uint32_t& key) {
+    typedef typename ConnT<k16>::R R;
+    key = 0xFFFFFFFFu;
+    if (di < 0) return 1u;
+    const ConnDesc D = a.desc[di];
+    uint32_t res = 0u, rule = D.n_rules;                  // default DENY (:667)
+    if (D.pre) {
+        const uint32_t w = D.pre[uint64_t(tuple) * a.n + i];
+        res = w & 3u;
+        rule = D.slot_rule[w >> 2];
+    } else {
+        const R* g = static_cast<const R*>(a.rules);
+        for (uint32_t r = 0; r < D.n; ++r) {
+            const R x = conn_rule<kLds>(g, D.rule_off + r);
+            const uint32_t meta = (x.meta >> (8u * p)) & 0xFFu;
+            const uint32_t pw = p == 0u ? x.port[0] : p == 1u ? x.port[1] : 0xFFFF0000u;   // ICMP / OTHER: any port
+            if ((meta & 0x80u) && conn_match(x, s, d, s4, d4) && port_in(port, pw)) {
+                res = meta & 3u;
+                rule = conn_index(x);
+                break;
+            }
+        }
+    }
+    key = D.ctr_off + rule;
     return res;
 }
 
-__global__ void connect4_kernel(const AclDesc* __restrict__ acls, const IfAcls* __restrict__ ifs,
-                                const uint32_t* __restrict__ src_if,
-                                const uint32_t* __restrict__ dst_if,
-                                const uint32_t* __restrict__ src, const uint32_t* __restrict__ dst,
-                                const uint16_t* __restrict__ sport,
-                                const uint16_t* __restrict__ dport,
-                                const uint8_t* __restrict__ proto, uint64_t n,
-                                uint8_t* __restrict__ out) {
-    const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const uint32_t si = src_if[i], di = dst_if[i];
-    const IfAcls S = ifs[si], D = ifs[di];
-    const bool same = si == di;
-    const uint32_t sa = src[i], da = dst[i], sp = sport[i], dp = dport[i];
-    const uint32_t p = proto[i] <= 2 ? proto[i] : 3u;
-    bool srefl = false, drefl = false;
-    uint32_t a = eval_acl4(acls, S.in, sa, da, dp, p, i);         // SYN: src inbound
-    if (a == 3u) { out[i] = 3; return; }
-    if (a == 0u) { out[i] = 0; return; }
-    if (a == 2u) { srefl = true; if (same) drefl = true; }
-    if (!drefl) {                                                 // SYN: dst outbound
-        a = eval_acl4(acls, D.out, sa, da, dp, p, i);
-        if (a == 3u) { out[i] = 3; return; }
-        if (a == 0u) { out[i] = 0; return; }
-        if (a == 2u) { drefl = true; if (same) srefl = true; }
+template <bool k16, bool kLdsRules, int kCount>
+__global__ __launch_bounds__(1024) void connect_kernel(ConnArgs a) {
+    typedef typename ConnT<k16>::A A;
+    extern __shared__ uint4 smem[];
+    typedef __attribute__((address_space(3))) uint32_t* lctr_t;
+    if constexpr (kLdsRules) {
+        const uint4* g = static_cast<const uint4*>(a.rules);
+        for (uint32_t j = threadIdx.x; j < a.rules_bytes / 16u; j += blockDim.x) smem[j] = g[j];
     }
-    if (!drefl) {                                                 // SYN-ACK: dst inbound
-        a = eval_acl4(acls, D.in, da, sa, sp, p, n + i);
-        if (a == 3u) { out[i] = 3; return; }
-        if (a == 0u) { out[i] = 1; return; }
+    if constexpr (kCount == 1) {
+        for (uint32_t j = threadIdx.x; j < a.n_ctr; j += blockDim.x) *lctr_t(a.ctr_lds + 4u * j) = 0u;
     }
-    if (!srefl) {                                                 // SYN-ACK: src outbound
-        a = eval_acl4(acls, S.out, da, sa, sp, p, n + i);
-        if (a == 3u) { out[i] = 3; return; }
-        if (a == 0u) { out[i] = 1; return; }
+    if constexpr (kLdsRules || kCount == 1) __syncthreads();
+    const A* src = static_cast<const A*>(a.src);
+    const A* dst = static_cast<const A*>(a.dst);
+    const uint64_t nthreads = uint64_t(gridDim.x) * blockDim.x;
+    const uint64_t n_iter = (a.n + nthreads - 1) / nthreads;    // uniform trip count (ballots below)
+    for (uint64_t it = 0; it < n_iter; ++it) {
+        const uint64_t i = it * nthreads + uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+        uint32_t key[4] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+        if (i < a.n) {
+            const uint32_t si = a.src_if[i], dj = a.dst_if[i];
+            uint32_t v = 3u;                                    // unknown interface id: Failure
+            if (si < a.n_ifs && dj < a.n_ifs) {
+                const IfAcls S = a.ifs[si], D = a.ifs[dj];
+                const bool same = si == dj;
+                const A sa = src[i], da = dst[i];
+                const bool s4 = mapped4(sa), d4 = mapped4(da);
+                const uint32_t sp = a.sport[i], dp = a.dport[i], pr = a.proto[i];
+                const uint32_t p = pr <= 2u ? pr : 3u;
+                bool srefl = false, drefl = false, done = false;
+                uint32_t r = conn_eval<k16, kLdsRules>(a, S.in, 0u, i, sa, da, s4, d4, dp, p, key[0]);   // SYN: src inbound
+                if (r == 3u) { v = 3u; done = true; }
+                else if (r == 0u) { v = 0u; done = true; }
+                else if (r == 2u) { srefl = true; drefl = same; }
+                if (!done && !drefl) {                                                               // SYN: dst outbound
+                    r = conn_eval<k16, kLdsRules>(a, D.out, 0u, i, sa, da, s4, d4, dp, p, key[1]);
+                    if (r == 3u) { v = 3u; done = true; }
+                    else if (r == 0u) { v = 0u; done = true; }
+                    else if (r == 2u) { drefl = true; srefl = srefl || same; }
+                }
+                if (!done && !drefl) {                                                               // SYN-ACK: dst inbound
+                    r = conn_eval<k16, kLdsRules>(a, D.in, 1u, i, da, sa, d4, s4, sp, p, key[2]);
+                    if (r == 3u) { v = 3u; done = true; }
+                    else if (r == 0u) { v = 1u; done = true; }
+                }
+                if (!done && !srefl) {                                                               // SYN-ACK: src outbound
+                    r = conn_eval<k16, kLdsRules>(a, S.out, 1u, i, da, sa, d4, s4, sp, p, key[3]);
+                    if (r == 3u) { v = 3u; done = true; }
+                    else if (r == 0u) { v = 1u; done = true; }
+                }
+                if (!done) v = 2u;
+            }
+            a.out[i] = uint8_t(v);
+        }
+        if constexpr (kCount == 1) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (key[k] != 0xFFFFFFFFu)
+                    __hip_atomic_fetch_add(lctr_t(a.ctr_lds + 4u * key[k]), 1u, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_WORKGROUP);
+        } else if constexpr (kCount == 2) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) wave_count(a.ctr, key[k]);
+        }
     }
-    out[i] = 2;
+    if constexpr (kCount == 1) {
+        __syncthreads();
+        for (uint32_t j = threadIdx.x; j < a.n_ctr; j += blockDim.x) {
+            const uint32_t c = *lctr_t(a.ctr_lds + 4u * j);
+            if (c) atomicAdd(&a.ctr[j], (unsigned long long)c);
+        }
+    }
+}
+
+// The call's counters -> the tables' connection counters (one workgroup per
+// descriptor; a table has one descriptor per call), cleared for the next call.
+__global__ __launch_bounds__(256) void conn_scatter_kernel(const ConnDesc* __restrict__ desc,
+                                                           unsigned long long* const* __restrict__ table_ctr,
+                                                           unsigned long long* __restrict__ call_ctr) {
+    const ConnDesc D = desc[blockIdx.x];
+    unsigned long long* out = table_ctr[blockIdx.x];
+    for (uint32_t r = threadIdx.x; r <= D.n_rules; r += blockDim.x) {
+        const unsigned long long v = call_ctr[D.ctr_off + r];
+        if (v) {
+            atomicAdd(&out[r], v);
+            call_ctr[D.ctr_off + r] = 0ull;
+        }
+    }
 }
 
 constexpr uint64_t kGolden = 0x9E3779B97F4A7C15ull;
@@ -1535,6 +1710,71 @@ hipError_t launch_classify16_cls(const Cls4Dev& t, const Fe16& fe, const Pkts16&
     return hipGetLastError();
 }
 
+// Slot mode: one packet per lane (kVec false), run-time search depth.
+template <bool kLds>
+static void dispatch_slots4(const Cls4Dev& t, const Pkts4& p, uint32_t* out, const LaunchCfg& cfg) {
+    uint8_t* o = reinterpret_cast<uint8_t*>(out);
+    const int src = t.mode != 1 ? 0 : t.n_hash == 1 ? 2 : 1;
+#define CLS_SLOT_CASES(L)                                                                          \
+    case 3 * L + 0: launch_d<kLds, false, 0, L, -1, 2>(t, p, o, nullptr, cfg); break;              \
+    case 3 * L + 1: launch_d<kLds, false, 1, L, -1, 2>(t, p, o, nullptr, cfg); break;              \
+    case 3 * L + 2: launch_d<kLds, false, 2, L, -1, 2>(t, p, o, nullptr, cfg); break;
+    switch (src + 3 * int(t.list_mode)) {
+        CLS_SLOT_CASES(0)
+        CLS_SLOT_CASES(1)
+        CLS_SLOT_CASES(2)
+        CLS_SLOT_CASES(3)
+        CLS_SLOT_CASES(4)
+    default: break;
+    }
+#undef CLS_SLOT_CASES
+}
+
+hipError_t launch_classify4_slots(const Cls4Dev& t, const Pkts4& p, uint32_t* out, bool lds_resident,
+                                  const LaunchCfg& cfg) {
+    if (lds_resident) dispatch_slots4<true>(t, p, out, cfg);
+    else dispatch_slots4<false>(t, p, out, cfg);
+    return hipGetLastError();
+}
+
+template <bool kLds>
+static void dispatch_slots16(const Cls4Dev& t, const Fe16& fe, const Pkts16& p, uint32_t* out,
+                             const LaunchCfg& cfg) {
+    uint8_t* o = reinterpret_cast<uint8_t*>(out);
+    if (fe.src_mode == 1) {
+        switch (t.list_mode) {
+        case 0: launch16_d<kLds, 3, 0, -1, false, 1, 2>(t, fe, p, o, nullptr, cfg); break;
+        case 1: launch16_d<kLds, 3, 1, -1, false, 1, 2>(t, fe, p, o, nullptr, cfg); break;
+        case 2: launch16_d<kLds, 3, 2, -1, false, 1, 2>(t, fe, p, o, nullptr, cfg); break;
+        case 3: launch16_d<kLds, 3, 3, -1, false, 1, 2>(t, fe, p, o, nullptr, cfg); break;
+        case 4: launch16_d<kLds, 3, 4, -1, false, 1, 2>(t, fe, p, o, nullptr, cfg); break;
+        default: break;
+        }
+        return;
+    }
+    const int src = t.mode != 1 ? 0 : t.n_hash == 1 ? 2 : 1;
+#define CLS16_SLOT_CASES(L)                                                                        \
+    case 3 * L + 0: launch16_d<kLds, 0, L, -1, false, 0, 2>(t, fe, p, o, nullptr, cfg); break;     \
+    case 3 * L + 1: launch16_d<kLds, 1, L, -1, false, 0, 2>(t, fe, p, o, nullptr, cfg); break;     \
+    case 3 * L + 2: launch16_d<kLds, 2, L, -1, false, 0, 2>(t, fe, p, o, nullptr, cfg); break;
+    switch (src + 3 * int(t.list_mode)) {
+        CLS16_SLOT_CASES(0)
+        CLS16_SLOT_CASES(1)
+        CLS16_SLOT_CASES(2)
+        CLS16_SLOT_CASES(3)
+        CLS16_SLOT_CASES(4)
+    default: break;
+    }
+#undef CLS16_SLOT_CASES
+}
+
+hipError_t launch_classify16_slots(const Cls4Dev& t, const Fe16& fe, const Pkts16& p, uint32_t* out,
+                                   bool lds_resident, const LaunchCfg& cfg) {
+    if (lds_resident) dispatch_slots16<true>(t, fe, p, out, cfg);
+    else dispatch_slots16<false>(t, fe, p, out, cfg);
+    return hipGetLastError();
+}
+
 hipError_t launch_classify4_linear(const LinRule4* rules, uint32_t n_lin, uint32_t n_rules,
                                    const Pkts4& p, uint8_t* verdict, unsigned long long* gslot,
                                    const LaunchCfg& cfg) {
@@ -1587,13 +1827,28 @@ hipError_t launch_stream(const Pkts4* p4, const Pkts16* p16, uint8_t* verdict, i
     return hipGetLastError();
 }
 
-hipError_t launch_connect4(const AclDesc* acls, const IfAcls* ifs, const uint32_t* src_if,
-                           const uint32_t* dst_if, const uint32_t* src, const uint32_t* dst,
-                           const uint16_t* sport, const uint16_t* dport, const uint8_t* proto,
-                           uint64_t n, uint8_t* out, hipStream_t s) {
-    if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(connect4_kernel, dim3(uint32_t((n + 255) / 256)), dim3(256), 0, s, acls, ifs,
-                       src_if, dst_if, src, dst, sport, dport, proto, n, out);
+hipError_t launch_connect(const ConnArgs& a, bool k16, bool lds_rules, int count, int grid, hipStream_t s) {
+    if (a.n == 0) return hipSuccess;
+    const size_t lds = (lds_rules ? a.rules_bytes : 0) + (count == 1 ? size_t(a.n_ctr) * 4 : 0);
+#define CONN_CASE(K16, L, C)                                                                               \
+    if (k16 == K16 && lds_rules == L && count == C) {                                                      \
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(connect_kernel<K16, L, C>),                \
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));                   \
+        hipLaunchKernelGGL((connect_kernel<K16, L, C>), dim3(grid), dim3(1024), lds, s, a);                \
+        return hipGetLastError();                                                                          \
+    }
+    CONN_CASE(false, false, 0) CONN_CASE(false, false, 1) CONN_CASE(false, false, 2)
+    CONN_CASE(false, true, 0) CONN_CASE(false, true, 1) CONN_CASE(false, true, 2)
+    CONN_CASE(true, false, 0) CONN_CASE(true, false, 1) CONN_CASE(true, false, 2)
+    CONN_CASE(true, true, 0) CONN_CASE(true, true, 1) CONN_CASE(true, true, 2)
+#undef CONN_CASE
+    return hipErrorInvalidValue;
+}
+
+hipError_t launch_conn_scatter(const ConnDesc* desc, unsigned long long* const* table_ctr, uint32_t n_desc,
+                               unsigned long long* call_ctr, hipStream_t s) {
+    if (n_desc == 0) return hipSuccess;
+    hipLaunchKernelGGL(conn_scatter_kernel, dim3(n_desc), dim3(256), 0, s, desc, table_ctr, call_ctr);
     return hipGetLastError();
 }
 

@@ -113,19 +113,51 @@ hipError_t launch_other16(const Cls4Dev& t, const Cls4Dev& o, const Fe16& fe, co
 hipError_t launch_stream(const Pkts4* p4, const Pkts16* p16, uint8_t* verdict, int grid, int variant,
                          hipStream_t s);
 
-struct AclDesc {                 // one installed ACL for the connection kernel
-    const LinRule4* rules;
-    uint32_t n;
-    uint32_t valid;              // 0 = nil ACL (PERMIT)
-    const uint8_t* pre;          // classifier verdicts: [0, n) SYN tuple, [n, 2n) SYN-ACK tuple; or null
+// Slot mode of the classify kernels (connection batches): out[i] = result |
+// slot << 2 (u32), no counting; protocols > 2 in place, their slots after
+// the main image's.  p4: one packet per lane (no vector requirements).
+hipError_t launch_classify4_slots(const Cls4Dev& t, const Pkts4& p, uint32_t* out, bool lds_resident,
+                                  const LaunchCfg& cfg);
+hipError_t launch_classify16_slots(const Cls4Dev& t, const Fe16& fe, const Pkts16& p, uint32_t* out,
+                                   bool lds_resident, const LaunchCfg& cfg);
+
+struct ConnDesc {                // one bound ACL for the connection kernel
+    uint32_t rule_off;           // linear ACLs: first rule in the call's rule pool
+    uint32_t n;                  // linear rules
+    uint32_t n_rules;            // R (default DENY: rule R)
+    uint32_t ctr_off;            // counting: counter of rule 0 in the call's counter space
+    const uint32_t* pre;         // classifier slot words (res | slot << 2): [0, N) SYN, [N, 2N) SYN-ACK; or null
+    const uint32_t* slot_rule;   // pre: slot -> rule index
 };
-struct IfAcls {                  // interface -> (inbound, outbound) AclDesc index, -1 = nil
+struct IfAcls {                  // interface -> (inbound, outbound) ConnDesc index, -1 = nil
     int32_t in, out;
 };
-hipError_t launch_connect4(const AclDesc* acls, const IfAcls* ifs, const uint32_t* src_if,
-                           const uint32_t* dst_if, const uint32_t* src, const uint32_t* dst,
-                           const uint16_t* sport, const uint16_t* dport, const uint8_t* proto,
-                           uint64_t n, uint8_t* out, hipStream_t s);
+struct ConnArgs {
+    const ConnDesc* desc;
+    const IfAcls* ifs;
+    uint32_t n_ifs;
+    const void* rules;           // ConnRule4 / ConnRule16 pool (global memory)
+    uint32_t rules_bytes;        // staged into LDS at address 0 when the launch says so
+    uint32_t n_ctr;              // counting: counter space (sum of R + 1 over the descriptors)
+    uint32_t ctr_lds;            // counting: LDS byte offset of the u32 counters (LDS variant)
+    unsigned long long* ctr;     // counting: the call's u64 counters (n_ctr)
+    const uint32_t* src_if;
+    const uint32_t* dst_if;
+    const void* src;             // u32 host order, or 16-B network-order addresses
+    const void* dst;
+    const uint16_t* sport;
+    const uint16_t* dport;
+    const uint8_t* proto;
+    uint64_t n;
+    uint8_t* out;
+};
+// k16: 16-byte addresses; lds_rules: stage the pool; count: 0 none, 1 LDS
+// counters, 2 global (wave-aggregated) counters; grid: persistent workgroups
+hipError_t launch_connect(const ConnArgs& a, bool k16, bool lds_rules, int count, int grid, hipStream_t s);
+// tables' connection counters += the call's counters (ConnDesc ctr_off ..
+// + n_rules), which are cleared: one workgroup per descriptor
+hipError_t launch_conn_scatter(const ConnDesc* desc, unsigned long long* const* table_ctr, uint32_t n_desc,
+                               unsigned long long* call_ctr, hipStream_t s);
 
 struct TrafficDev {
     uint64_t seed;

@@ -239,6 +239,12 @@ class Engine:
         self._check(_abi.lib().cls_acl_counts(self.h, C.byref(a), C.byref(c)))
         return a.value, c.value
 
+    def acl_stats(self):
+        """(tables compiled, puts that kept the installed table) by cls_acl_put."""
+        a, c = C.c_uint32(0), C.c_uint32(0)
+        self._check(_abi.lib().cls_acl_stats(self.h, C.byref(a), C.byref(c)))
+        return a.value, c.value
+
     def if_id(self, name: str) -> int:
         i = C.c_uint32(0)
         self._check(_abi.lib().cls_if_id(self.h, name.encode(), C.byref(i)))
@@ -249,41 +255,78 @@ class Engine:
         self._check(_abi.lib().cls_if_acls(self.h, if_id, C.byref(a), C.byref(b)))
         return a.value, b.value
 
-    def connect_batch(self, src_if, dst_if, src, dst, proto, sport, dport, mode: str = "auto") -> np.ndarray:
-        """testConnection over a batch (cls_connect_batch).  mode: "auto" (ACLs
-        with a classifier image use it for batches >= 65536), "classifier"
-        (at any size) or "linear" (every ACL scanned)."""
+    def connect_batch(self, src_if, dst_if, src, dst, proto, sport, dport, mode: str = "auto",
+                      count: bool = False) -> np.ndarray:
+        """testConnection over a batch (cls_connect_batch).  Addresses: host-order
+        u32 (IPv4) or n x 16 network-order bytes (IPv6, IPv4-mapped = IPv4).
+        mode: "auto" (ACLs with a classifier image use it for batches >=
+        65536), "classifier" (at any size) or "linear" (every ACL scanned).
+        count: add every evalACL call's terminating rule to the tables'
+        connection counters (conn_counters)."""
         flags = {"auto": 0, "classifier": _abi.F_CONN_CLS, "linear": _abi.F_FORCE_LINEAR}[mode]
+        if count:
+            flags |= _abi.F_COUNT
         if _is_torch(src):
             return self._connect_batch_device(src_if, dst_if, src, dst, proto, sport, dport, flags)
-        arrs = [np.ascontiguousarray(src_if, np.uint32), np.ascontiguousarray(dst_if, np.uint32),
-                np.ascontiguousarray(src, np.uint32), np.ascontiguousarray(dst, np.uint32),
-                np.ascontiguousarray(proto, np.uint8), np.ascontiguousarray(sport, np.uint16),
-                np.ascontiguousarray(dport, np.uint16)]
-        si, di, s, d, p, sp, dp = arrs
+        v16 = np.asarray(src).ndim == 2
+        if v16:
+            s = np.ascontiguousarray(src, np.uint8).reshape(-1, 16)
+            d = np.ascontiguousarray(dst, np.uint8).reshape(-1, 16)
+        else:
+            s, d = np.ascontiguousarray(src, np.uint32), np.ascontiguousarray(dst, np.uint32)
+        si, di = np.ascontiguousarray(src_if, np.uint32), np.ascontiguousarray(dst_if, np.uint32)
+        p, sp = np.ascontiguousarray(proto, np.uint8), np.ascontiguousarray(sport, np.uint16)
+        dp = np.ascontiguousarray(dport, np.uint16)
         n = len(s)
         out = np.zeros(n, np.uint8)
-        pk = _abi.PktSoa(_abi.AF_V4, _ptr(s), _ptr(d), None, None, _ptr(sp), _ptr(dp), _ptr(p))
+        if v16:
+            pk = _abi.PktSoa(_abi.AF_V16, None, None, _ptr(s), _ptr(d), _ptr(sp), _ptr(dp), _ptr(p))
+        else:
+            pk = _abi.PktSoa(_abi.AF_V4, _ptr(s), _ptr(d), None, None, _ptr(sp), _ptr(dp), _ptr(p))
         cs = _abi.ConnSoa(pk, _ptr(si), _ptr(di))
         self._check(_abi.lib().cls_connect_batch(self.h, C.byref(cs), n, _ptr(out), flags, None))
         return out
 
     def _connect_batch_device(self, src_if, dst_if, src, dst, proto, sport, dport, flags):
         """Device-resident batch (CLS_F_DEVICE): contiguous GPU tensors of 4-byte
-        interface ids and addresses, 2-byte ports and 1-byte protocols, already
-        written (the call runs on the engine's stream).  Returns a uint8 tensor."""
+        interface ids, 4-byte (or n x 16 uint8) addresses, 2-byte ports and
+        1-byte protocols, already written (the call runs on the engine's
+        stream).  Returns a uint8 tensor."""
         import torch
+        v16 = src.dim() == 2
         arrs = [src_if, dst_if, src, dst, sport, dport, proto]
-        sizes = [4, 4, 4, 4, 2, 2, 1]
-        n = src.numel()
+        sizes = [4, 4, 1 if v16 else 4, 1 if v16 else 4, 2, 2, 1]
+        n = src.shape[0]
         for x, sz in zip(arrs, sizes):
-            if not (_is_torch(x) and x.is_cuda and x.is_contiguous() and x.element_size() == sz and x.numel() == n):
+            if not (_is_torch(x) and x.is_cuda and x.is_contiguous() and x.element_size() == sz and x.shape[0] == n):
                 raise ClsError("device connection batch: contiguous GPU tensors of element sizes %s" % sizes)
         out = torch.empty(n, dtype=torch.uint8, device=src.device)
-        pk = _abi.PktSoa(_abi.AF_V4, _ptr(src), _ptr(dst), None, None, _ptr(sport), _ptr(dport), _ptr(proto))
+        if v16:
+            pk = _abi.PktSoa(_abi.AF_V16, None, None, _ptr(src), _ptr(dst), _ptr(sport), _ptr(dport), _ptr(proto))
+        else:
+            pk = _abi.PktSoa(_abi.AF_V4, _ptr(src), _ptr(dst), None, None, _ptr(sport), _ptr(dport), _ptr(proto))
         cs = _abi.ConnSoa(pk, _ptr(src_if), _ptr(dst_if))
         self._check(_abi.lib().cls_connect_batch(self.h, C.byref(cs), n, _ptr(out), flags | _abi.F_DEVICE, None))
         return out
+
+    def conn_counters(self, table, reset: bool = False) -> np.ndarray:
+        """Per-rule connection counters of a table (a Table, a table id or an
+        installed ACL's name): R + 1 u64, [R] = default DENY."""
+        if isinstance(table, str):
+            table = self.acl_table(table)
+        tid = table.id if isinstance(table, Table) else int(table)
+        info = _abi.TableInfo()
+        self._check(_abi.lib().cls_table_get_info(self.h, tid, C.byref(info)))
+        out = np.zeros(info.n_rules + 1, np.uint64)
+        self._check(_abi.lib().cls_conn_counters(self.h, tid, _ptr(out), 1 if reset else 0))
+        return out
+
+
+def _ip16(ip: Optional[bytes]) -> Optional[bytes]:
+    """net.IP as the 16-byte form (IPv4 as IPv4-mapped, like Go's To16)."""
+    if ip is None or len(ip) not in (4, 16):
+        return None
+    return bytes(10) + b"\xff\xff" + bytes(ip) if len(ip) == 4 else bytes(ip)
 
 
 def _ip4(ip: Optional[bytes]) -> Optional[int]:
@@ -404,8 +447,9 @@ class ACLEngine:
             return CONN_FAILURE
         return sif, ip, dif, d[0], proto, sport, dport
 
-    def connection_batch(self, calls):
-        """calls: list of (fn name, args).  One GPU launch for all of them."""
+    def connection_batch(self, calls, count: bool = False):
+        """calls: list of (fn name, args).  One GPU launch for all of them: the
+        IPv4 layout when every endpoint is IPv4, else the 16-byte layout."""
         out = [None] * len(calls)
         rows = []
         for i, (fn, args) in enumerate(calls):
@@ -414,15 +458,24 @@ class ACLEngine:
                 out[i] = CONN_FAILURE
                 continue
             sif, sip, dif, dip, proto, sport, dport = r
-            s4, d4 = _ip4(sip), _ip4(dip)
-            if s4 is None or d4 is None:
-                raise ClsError("connection path supports IPv4 endpoints only")
-            rows.append((i, self.engine.if_id(sif), self.engine.if_id(dif), s4, d4, proto, sport, dport))
-        if rows:
-            a = np.array([r[1:] for r in rows], np.int64)
-            res = self.engine.connect_batch(a[:, 0], a[:, 1], a[:, 2], a[:, 3], a[:, 4], a[:, 5], a[:, 6])
-            for (i, *_), v in zip(rows, res):
-                out[i] = int(v)
+            rows.append((i, self.engine.if_id(sif), self.engine.if_id(dif), sip, dip, proto, sport, dport))
+        if not rows:
+            return out
+        four = [(_ip4(r[3]), _ip4(r[4])) for r in rows]
+        meta = np.array([(r[1], r[2], r[5], r[6], r[7]) for r in rows], np.int64)
+        if all(a is not None and b is not None for a, b in four):
+            src = np.array([a for a, _ in four], np.uint32)
+            dst = np.array([b for _, b in four], np.uint32)
+        else:
+            a16 = [(_ip16(r[3]), _ip16(r[4])) for r in rows]
+            if any(a is None or b is None for a, b in a16):
+                raise ClsError("connection endpoint is not an IPv4 or IPv6 address")
+            src = np.frombuffer(b"".join(a for a, _ in a16), np.uint8).reshape(-1, 16)
+            dst = np.frombuffer(b"".join(b for _, b in a16), np.uint8).reshape(-1, 16)
+        res = self.engine.connect_batch(meta[:, 0], meta[:, 1], src, dst, meta[:, 2], meta[:, 3], meta[:, 4],
+                                        count=count)
+        for (i, *_), v in zip(rows, res):
+            out[i] = int(v)
         return out
 
     def connection_pod_to_pod(self, src_pod, dst_pod, proto, sport, dport):
