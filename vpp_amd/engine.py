@@ -15,7 +15,6 @@ would: the protobuf ACLs by name, pods and interface names.
 """
 from __future__ import annotations
 
-import copy
 import ctypes as C
 from typing import Optional
 
@@ -358,7 +357,7 @@ class ACLEngine:
                 return "non-ACL changed in txn"
             name = key[len(ACL_KEY_PREFIX):]
             if value is not None:
-                acl = copy.deepcopy(value)
+                acl = value.clone()          # the engine keeps its own message (rules shared, never modified)
                 ifs = acl.interfaces
                 rc = self.engine.acl_put(acl.acl_name, acl.rules,
                                          ifs.ingress if ifs else [], ifs.egress if ifs else [])

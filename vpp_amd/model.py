@@ -117,8 +117,11 @@ class Acl:
     interfaces: Optional[Interfaces] = None
 
     def clone(self) -> "Acl":
-        """proto.Clone equivalent (acl_renderer.go:189)."""
-        return copy.deepcopy(self)
+        """proto.Clone equivalent (acl_renderer.go:189).  Rule messages are
+        never modified once rendered, so the clone shares them; the rule list
+        and the interfaces (which the renderer rewrites) are copies."""
+        return Acl(rules=list(self.rules), acl_name=self.acl_name,
+                   interfaces=copy.deepcopy(self.interfaces))
 
 
 MAX_PORT = 0xFFFF

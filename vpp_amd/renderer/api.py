@@ -141,6 +141,57 @@ def compare_ports(a: int, b: int) -> int:
     return -1 if a < b else 1
 
 
+def net_key(n: IPNet):
+    """A sort key of ``n`` consistent with compare_ipnets (equal keys <=>
+    compare_ipnets == 0), or None where the key form does not apply (a
+    non-canonical mask, a mask whose width differs from the address's):
+    IPv4 before IPv6, longer prefix first, then the masked address; the
+    empty network last.  For disjoint prefixes of one length the masked and
+    the unmasked address order agree (they differ inside the prefix)."""
+    if n is None:
+        return None
+    ck = (n.ip, n.mask)
+    k = _NET_KEYS.get(ck, _MISSING)
+    if k is _MISSING:
+        if len(_NET_KEYS) > 1 << 20:
+            _NET_KEYS.clear()
+        k = _NET_KEYS[ck] = _net_key(n)
+    return k
+
+
+_NET_KEYS = {}
+_MISSING = object()
+
+
+def _net_key(n: IPNet):
+    if len(n.ip) == 0:
+        return (2, 0, 0)
+    a4 = gonet.to4(n.ip)
+    if a4 is not None:
+        if len(n.mask) != 4:
+            return None
+        ip = a4
+        fam = 0
+    else:
+        if len(n.ip) != 16 or len(n.mask) != 16:
+            return None
+        ip = n.ip
+        fam = 1
+    ones, bits = gonet.mask_size(n.mask)
+    if bits == 0:
+        return None
+    x = int.from_bytes(ip, "big") & int.from_bytes(n.mask, "big")
+    return (fam, -ones, x)
+
+
+def rule_key(r: ContivRule):
+    """Sort key of a rule consistent with ContivRule.compare, or None."""
+    s, d = net_key(r.src_network), net_key(r.dest_network)
+    if s is None or d is None:
+        return None
+    return (r.protocol, s, d, r.src_port or 0x10000, r.dest_port or 0x10000, r.action)
+
+
 def compare_rule_lists(a, b) -> int:
     """compareRuleLists (renderer/cache/local_tables.go:242-263)."""
     if a is None and b is None:

@@ -20,7 +20,7 @@ from typing import Dict, Iterable, List, Optional
 
 from ..gonet import IPNet
 from .api import (ACTION_DENY, ACTION_PERMIT, ANY_PORT, TCP, UDP, ContivRule, PodID,
-                  allow_all_tcp, allow_all_udp, compare_rule_lists)
+                  allow_all_tcp, allow_all_udp, compare_rule_lists, rule_key)
 from .. import gonet
 
 # Orientation (cache_api.go)
@@ -170,6 +170,34 @@ def get_allowed_ingress_ports(dst_ip: IPNet, ingress) -> tuple:
     return tcp, udp
 
 
+class _KeyedRules(list):
+    """A rule list built in keyed form, carrying its keys (valid while its
+    length is unchanged)."""
+    __slots__ = ("keys",)
+
+
+def _list_keys(rules):
+    """The rules' keys as one tuple (None if some rule has no key)."""
+    if isinstance(rules, _KeyedRules) and len(rules.keys) == len(rules):
+        return rules.keys
+    keys = []
+    for r in rules:
+        k = rule_key(r)
+        if k is None:
+            return None
+        keys.append(k)
+    return tuple(keys)
+
+
+def _table_keys(t: "ContivRuleTable"):
+    c = getattr(t, "_rkeys", None)
+    if c is not None and c[0] is t.rules and c[1] == len(t.rules):
+        return c[2]
+    k = _list_keys(t.rules)
+    t._rkeys = (t.rules, len(t.rules), k)
+    return k
+
+
 class LocalTables:
     """LocalTables (local_tables.go:43-263): tables ordered by rule lists."""
 
@@ -179,10 +207,18 @@ class LocalTables:
         self.by_pod: Dict[PodID, ContivRuleTable] = {}
 
     def _lookup_idx_by_rules(self, rules) -> int:
+        # compareRuleLists by length, then rule by rule: with every rule keyed
+        # (api.rule_key) the same order is one tuple comparison
+        qk = _list_keys(rules) if KEYED else None
         lo, hi = 0, len(self.tables)
         while lo < hi:
             mid = (lo + hi) // 2
-            if compare_rule_lists(rules, self.tables[mid].rules) <= 0:
+            tk = _table_keys(self.tables[mid]) if qk is not None else None
+            if tk is not None:
+                c = (len(rules) > len(tk)) - (len(rules) < len(tk)) or (qk > tk) - (qk < tk)
+            else:
+                c = compare_rule_lists(rules, self.tables[mid].rules)
+            if c <= 0:
                 hi = mid
             else:
                 lo = mid + 1
@@ -231,8 +267,12 @@ class LocalTables:
 
     def lookup_by_rules(self, rules) -> Optional[ContivRuleTable]:
         idx = self._lookup_idx_by_rules(rules)
-        if idx < len(self.tables) and compare_rule_lists(rules, self.tables[idx].rules) == 0:
-            return self.tables[idx]
+        if idx < len(self.tables):
+            t = self.tables[idx]
+            qk = _list_keys(rules) if KEYED else None
+            tk = _table_keys(t) if qk is not None else None
+            if (qk == tk) if tk is not None else compare_rule_lists(rules, t.rules) == 0:
+                return t
         return None
 
     def lookup_by_pod(self, pod: PodID) -> Optional[ContivRuleTable]:
@@ -249,6 +289,10 @@ class TxnChange:
 
 
 _ids = itertools.count(1)
+
+# Keyed table construction (_LocalCtx, _rebuild_global_table); False: the
+# literal InsertRule path only (tests compare the two).
+KEYED = True
 
 
 class RendererCache:
@@ -425,6 +469,7 @@ class RendererCacheTxn:
 
     # -- table construction (cache_impl.go:418-673) ---------------------------
     def _refresh_tables(self):
+        self._ctx = _LocalCtx(self)
         for pod in sorted(self.get_all_pods().join(self.get_removed_pods()), key=tuple):
             cfg = self.get_pod_config(pod)
             new_table = self._build_local_table(pod, cfg)
@@ -445,6 +490,7 @@ class RendererCacheTxn:
                 continue
             self.local_tables.insert(new_table)
         self._rebuild_global_table()
+        self._ctx = None
         self.up_to_date = True
 
     def _build_local_table(self, dst_pod: PodID, dst_cfg: PodConfig) -> ContivRuleTable:
@@ -452,6 +498,13 @@ class RendererCacheTxn:
         table.pods.add(dst_pod)
         if dst_cfg.removed:
             return table
+        ctx = getattr(self, "_ctx", None)
+        if KEYED and ctx is not None and ctx.ok:
+            try:
+                table.rules = ctx.local_rules(dst_cfg)
+                return table
+            except ValueError:
+                pass                        # outside the keyed form: the literal path
         rules = dst_cfg.egress if self.cache.orientation == EGRESS_ORIENTATION else dst_cfg.ingress
         for rule in rules:
             table.insert_rule(rule.copy())
@@ -514,7 +567,33 @@ class RendererCacheTxn:
 
     def _rebuild_global_table(self):
         self.global_table = ContivRuleTable(GLOBAL_TABLE_ID)
-        for pod in sorted(self.get_all_pods(), key=tuple):
+        pods = sorted(self.get_all_pods(), key=tuple)
+        # keyed form (one sort, first of equal rules kept -- InsertRule's
+        # outcome) when every rule has a key; else sorted insertions
+        egress = self.cache.orientation == EGRESS_ORIENTATION
+        rules = []
+        for pod in pods:
+            cfg = self.get_pod_config(pod)
+            for rule in (cfg.ingress if egress else cfg.egress):
+                c = rule.copy()
+                if egress:
+                    c.src_network = cfg.pod_ip
+                else:
+                    c.dest_network = cfg.pod_ip
+                rules.append(c)
+        keys = [rule_key(r) for r in rules]
+        if KEYED and all(k is not None for k in keys):
+            if rules:
+                rules += [allow_all_tcp(), allow_all_udp()]
+                keys += [rule_key(rules[-2]), rule_key(rules[-1])]
+            out, last = [], None
+            for k, i in sorted((k, i) for i, k in enumerate(keys)):
+                if k != last:
+                    out.append(rules[i])
+                    last = k
+            self.global_table.rules = out
+            return
+        for pod in pods:
             self._install_global_rules(self.get_pod_config(pod))
         if self.global_table.num_of_rules > 0:
             self.global_table.insert_rule(allow_all_tcp())
@@ -537,6 +616,149 @@ class RendererCacheTxn:
             if tid not in self.cache.allocated_ids:
                 self.cache.allocated_ids.add(tid)
                 return tid
+
+
+class _LocalCtx:
+    """One refresh's shared state for building local tables in sorted-key form.
+
+    buildLocalTable (cache_impl.go:488-535) inserts the pod's own rules, then
+    for every pod on the node (installLocalRules :543-571) removes the rules
+    whose source (egress orientation; destination for ingress) is that pod's
+    host route, and inserts its allowed-port permits and a deny
+    (installAllowedPorts :576-634) -- every InsertRule a sorted insertion,
+    O(R) each.  Here the same rule multiset is collected and sorted once by a
+    key consistent with Compare (api.rule_key), keeping the first of equal
+    rules as InsertRule does.  The allowed-port sets depend only on a rule
+    list and one address, so they are computed once per (list content,
+    address).  Exactness needs: every pod address a host route and distinct
+    (the removals of one pod then touch only that pod's rules) and every rule
+    keyable; otherwise ``ok`` is False and the literal path runs.
+    Equivalence: tests/test_cache_fast_cpu.py."""
+
+    def __init__(self, txn: "RendererCacheTxn"):
+        self.egress = txn.cache.orientation == EGRESS_ORIENTATION
+        pods = sorted(txn.get_all_pods(), key=tuple)
+        self.src = []                  # (ip16, pod_ip, id of its opposite-side rule list)
+        self.ok = True
+        self._lists = {}
+        self._pcache = {}
+        self._pint = {}
+        self._built = {}
+        seen = set()
+        for pod in pods:
+            cfg = txn.get_pod_config(pod)
+            ip16 = self._host16(cfg.pod_ip)
+            if ip16 is None or ip16 in seen:
+                self.ok = False
+                return
+            seen.add(ip16)
+            lid = self._intern(cfg.ingress if self.egress else cfg.egress)
+            if lid is None:
+                self.ok = False
+                return
+            self.src.append((ip16, cfg.pod_ip, lid, cfg.ingress if self.egress else cfg.egress))
+
+    @staticmethod
+    def _host16(net):
+        if net is None or len(net.ip) == 0:
+            return None
+        ones, bits = gonet.mask_size(net.mask)
+        if bits == 0 or ones != bits:
+            return None
+        return gonet.to16(net.ip)
+
+    def _intern(self, rules):
+        keys = []
+        for r in rules:
+            k = rule_key(r)
+            if k is None:
+                return None
+            keys.append(k)
+        return self._lists.setdefault(tuple(keys), len(self._lists))
+
+    def _ports(self, fn, lid, rules, net, ip16):
+        k = (fn is get_allowed_ingress_ports, lid, ip16)
+        v = self._pcache.get(k)
+        if v is None:
+            v = fn(net, rules)
+            v = self._pcache[k] = self._pint.setdefault((frozenset(v[0]), frozenset(v[1])), v)   # one object per content
+        return v
+
+    def local_rules(self, dst_cfg: PodConfig):
+        """The sorted rules of the destination pod's local table, or raises
+        if a rule is not keyable (the caller checked ok)."""
+        egress = self.egress
+        own = dst_cfg.egress if egress else dst_cfg.ingress
+        dst16 = self._host16(dst_cfg.pod_ip)
+        own_lid = self._intern(own)
+        if dst16 is None or own_lid is None:
+            raise ValueError("local table outside the keyed form")
+        # The table depends on the destination pod only through its own rule
+        # list and the source pods' allowed ports towards it: equal
+        # signatures, equal tables (built once per refresh).
+        sfn = get_allowed_ingress_ports if egress else get_allowed_egress_ports
+        sp_all = [self._ports(sfn, lid, rules, dst_cfg.pod_ip, dst16) for _, _, lid, rules in self.src]
+        sig = (own_lid, tuple(map(id, sp_all)))
+        hit = self._built.get(sig)
+        if hit is not None:
+            return self._keyed(*hit)
+        base = [r.copy() for r in own]
+        # base rules a pod's installAllowedPorts would remove: (protocol, host ip16)
+        removable = {}
+        for i, r in enumerate(base):
+            h = self._host16(r.src_network if egress else r.dest_network)
+            if h is not None:
+                removable.setdefault((r.protocol, h), []).append(i)
+        dropped = set()
+        installed = []
+        dfn = get_allowed_egress_ports if egress else get_allowed_ingress_ports
+        for (ip16, pod_ip, lid, rules), (src_tcp, src_udp) in zip(self.src, sp_all):
+            dst_tcp, dst_udp = self._ports(dfn, own_lid, own, pod_ip, ip16)
+            for proto, d, sp in ((TCP, dst_tcp, src_tcp), (UDP, dst_udp, src_udp)):
+                if d.is_subset_of(sp):
+                    continue
+                dropped.update(removable.get((proto, ip16), ()))
+                for port in sorted(d.intersection(sp)):
+                    r = ContivRule(ACTION_PERMIT, IPNet(), IPNet(), proto, ANY_PORT, port)
+                    if egress:
+                        r.src_network = pod_ip
+                    else:
+                        r.dest_network = pod_ip
+                    installed.append(r)
+                r = ContivRule(ACTION_DENY, IPNet(), IPNet(), proto, ANY_PORT, ANY_PORT)
+                if egress:
+                    r.src_network = pod_ip
+                else:
+                    r.dest_network = pod_ip
+                installed.append(r)
+        rules = [r for i, r in enumerate(base) if i not in dropped] + installed
+        if rules:
+            all_tcp = all_udp = False
+            for r in rules:
+                if r.dest_port == 0 and len(r.src_network.ip) == 0 and len(r.dest_network.ip) == 0:
+                    if r.protocol == TCP:
+                        all_tcp = True
+                    else:
+                        all_udp = True
+            if not all_tcp:
+                rules.append(allow_all_tcp())
+            if not all_udp:
+                rules.append(allow_all_udp())
+        keyed = sorted(((rule_key(r), i) for i, r in enumerate(rules)))   # stable: equal keys by position
+        out, keys, last = [], [], None
+        for k, i in keyed:
+            if k != last:
+                out.append(rules[i])
+                keys.append(k)
+                last = k
+        self._built[sig] = (out, tuple(keys))
+        return self._keyed(out, self._built[sig][1])
+
+    @staticmethod
+    def _keyed(rules, keys):
+        r = _KeyedRules(rules)
+        r.keys = keys
+        return r
 
 
 def build_global_table(pods) -> ContivRuleTable:
