@@ -13,6 +13,7 @@ side is doubled.  FETCH_SIZE and WRITE_SIZE are collected in separate passes.
 """
 import csv
 import json
+import os
 import sys
 
 KERNEL = "classify4_cls"
@@ -49,6 +50,13 @@ def _per_dispatch(path, counter, kernel=KERNEL):
     return list(vals.values())
 
 
+def _source_hash():
+    """The native sources measured (bench.py drops a summary of other sources)."""
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from vpp_amd._abi import source_hash
+    return source_hash()
+
+
 def pmc(fetch_csv, write_csv, config, packets, out):
     # config 5 runs the 16-byte layout: classify16_cls, 35 B read per packet
     kernel, read_pp = ("classify16_cls", 35) if int(config) == 5 else (KERNEL, 11)
@@ -69,7 +77,8 @@ def pmc(fetch_csv, write_csv, config, packets, out):
          "read_ratio_vs_algorithmic": read_bytes / alg_read,
          "write_ratio_vs_algorithmic": write_bytes / alg_write,
          "correction": "read = 2 x FETCH_SIZE KiB (gfx950 half-count, MI355X_MICROARCH.md HBM); "
-                       "write = WRITE_SIZE KiB"}
+                       "write = WRITE_SIZE KiB",
+         "source_hash": _source_hash()}
     json.dump(d, open(out, "w"), indent=1)
     print(json.dumps(d, indent=1))
 
