@@ -904,10 +904,21 @@ static bool build_cls4_one(const std::vector<SemRule>& sem, uint32_t n_rules, Cl
         for (uint32_t x = 0; x < 65536 && special.size() <= kMaxPortHash; ++x)
             if (mcls(x) != d) special.push_back(x);
         if (special.size() <= kMaxPortHash) {
+            // A table of <= 32 words is bank-conflict free: ds_read_b32 serves
+            // each 32-lane half in one cycle when every bank holds at most one
+            // word of it (MI355X LDS: bank = (a/4) mod 32), so distinct ports
+            // never collide.  Dense tables (load > 1/2) take a longer search
+            // for a collision-free multiplier: 18 ports in 32 slots succeed
+            // with p ~ 0.3 % per multiplier.  CONTIVCLS_PHASH_DENSE=0: at
+            // least 2 slots per port (diagnostics / A/B).
+            const char* dn = std::getenv("CONTIVCLS_PHASH_DENSE");
+            const bool dense = !(dn && std::atoi(dn) == 0);
             uint64_t z = 0x243F6A8885A308D3ull;           // splitmix64 stream of odd multipliers
             for (uint32_t L = 4; L <= 11 && !phash_mul; ++L) {
-                if ((1u << L) < 2 * special.size()) continue;
-                for (int tries = 0; tries < 256 && !phash_mul; ++tries) {
+                const bool half = (1u << L) >= 2 * special.size();
+                if (!half && !(dense && L <= 5 && (1u << L) >= special.size())) continue;
+                const int max_tries = half ? 256 : 16384;
+                for (int tries = 0; tries < max_tries && !phash_mul; ++tries) {
                     z += 0x9E3779B97F4A7C15ull;
                     uint64_t m = z;
                     m = (m ^ (m >> 30)) * 0xBF58476D1CE4E5B9ull;

@@ -68,6 +68,8 @@ struct Counters {
     uint32_t n_lctr = 0;           // slots counted in LDS (their partial rows)
     uint32_t n_image = 0;          // slots of the classifier images; the direct rule slots follow
     DevBuf d_csr;                  // uint2 {slot, rule}, grouped by rule
+    DevBuf d_slot_rule;            // finish launch: u32 per slot (rule, or kHotRule | h), then the hot rules
+    uint32_t n_hot = 0;
     std::map<hipStream_t, std::unique_ptr<Scratch>> sc;
     ~Counters() {
         for (auto& kv : sc)
@@ -238,6 +240,30 @@ static int counters_init(cls_engine* e, Counters& c, const Cls4Image* img, const
     }
     HIPC(e, c.d_csr.ensure(csr.size() * 4));
     HIPC(e, hipMemcpy(c.d_csr.p, csr.data(), csr.size() * 4, hipMemcpyHostToDevice));
+    // slot -> rule for the finish launch.  Rules owning many slots (default
+    // DENY: one no-match slot per cell; allow-all rules: one per class) are
+    // "hot": a tile sums them in LDS, so such a rule takes one atomic per
+    // tile instead of one per slot.
+    std::vector<std::pair<uint32_t, uint32_t>> mult;            // (slots, rule)
+    for (uint32_t r = 0; r <= n_rules; ++r) {
+        const uint32_t m = cnt[r] - (r ? cnt[r - 1] : 0u);      // cnt[r] is now the end of rule r's run
+        if (m >= 8) mult.push_back({m, r});
+    }
+    std::sort(mult.begin(), mult.end(), [](const auto& a, const auto& b) {
+        return a.first != b.first ? a.first > b.first : a.second < b.second;
+    });
+    if (mult.size() > kMaxHotRules) mult.resize(kMaxHotRules);
+    std::vector<uint32_t> hot_of(size_t(n_rules) + 1, 0xFFFFFFFFu);
+    for (uint32_t h = 0; h < mult.size(); ++h) hot_of[mult[h].second] = h;
+    std::vector<uint32_t> sr(size_t(c.n_slots) + mult.size());
+    for (uint32_t i = 0; i < c.n_slots; ++i) {
+        const uint32_t r = rule_of(i);
+        sr[i] = hot_of[r] != 0xFFFFFFFFu ? (kHotRule | hot_of[r]) : r;
+    }
+    for (uint32_t h = 0; h < mult.size(); ++h) sr[c.n_slots + h] = mult[h].second;
+    c.n_hot = uint32_t(mult.size());
+    HIPC(e, c.d_slot_rule.ensure(sr.size() * 4));
+    HIPC(e, hipMemcpy(c.d_slot_rule.p, sr.data(), sr.size() * 4, hipMemcpyHostToDevice));
     return CLS_OK;
 }
 
@@ -533,13 +559,36 @@ static CountOut count_out(Scratch* sc, uint64_t* counters_out, uint32_t flags) {
     return {sc->out.as<unsigned long long>(), true};   // host batches accumulate on the host
 }
 
+// The finish launch of a classify chunk (kernels.hpp FinishArgs): fold the
+// workgroups' partials, and on the last chunk move every slot to its rule;
+// the OTHER queue's packets classified and counted.
+static FinishArgs finish_args(const Counters& c, Scratch* sc, const Cls4Dev& cd, const CountOut& co, bool lds_resident,
+                              uint32_t rows, uint32_t n_main, bool last) {
+    FinishArgs f;
+    f.part = lds_resident ? sc->part.as<uint32_t>() : nullptr;
+    f.rows = rows;
+    f.n_lctr = c.n_lctr;
+    f.slot_val = sc->slot_val.as<unsigned long long>();
+    f.n_slots = c.n_slots;
+    f.slot_rule = c.d_slot_rule.as<uint32_t>();
+    f.n_hot = c.n_hot;
+    f.out = co.out;
+    f.remap = last;
+    f.oq = cd.oq;
+    f.oq_rows = rows;
+    f.oq_cap = cd.oq_cap;
+    f.n_main = n_main;
+    return f;
+}
+
 // Slot counters -> rule counters (remap, which also clears the slots);
 // host batches: copy verdicts and counters back.
 static int finish_counts(cls_engine* e, const Table& t, const Counters& c, Scratch* sc, const CountOut& co,
                          uint64_t n, uint8_t* verdict_out, const uint8_t* d_verdict, uint64_t* counters_out,
-                         uint32_t flags, hipStream_t s) {
+                         uint32_t flags, hipStream_t s, bool remapped = false) {
     const bool dev = flags & CLS_F_DEVICE;
-    HIPC(e, launch_remap(sc->slot_val.as<unsigned long long>(), c.d_csr.as<uint2>(), c.n_slots, co.out, s));
+    if (!remapped)
+        HIPC(e, launch_remap(sc->slot_val.as<unsigned long long>(), c.d_csr.as<uint2>(), c.n_slots, co.out, s));
     HIPC(e, hipEventRecord(sc->done, s));
     if (!dev) {
         if (verdict_out && n) HIPC(e, hipMemcpyAsync(verdict_out, d_verdict, n, hipMemcpyDeviceToHost, s));
@@ -636,7 +685,7 @@ static int classify16_locked(cls_engine* e, std::shared_ptr<Table> t, const cls_
         const int rc = timing_begin(e, s);
         if (rc != CLS_OK) return rc;
     }
-    bool zeroed = false;
+    bool zeroed = false, remapped = false;
     if (n) {
         Cls4Dev cd = cls4_dev(c, q.d_img, q.d_lin, uint32_t(q.lin.size()), t->n_rules);
         cfg.other = cls4_dev(q.oimg, q.d_oimg, DevBuf(), 0, t->n_rules);
@@ -654,14 +703,16 @@ static int classify16_locked(cls_engine* e, std::shared_ptr<Table> t, const cls_
             if (c.swap) std::swap(pc.src, pc.dst);          // destination-keyed image
             uint8_t* vo = d_verdict ? d_verdict + off : nullptr;
             pc.vec = aligned(pc.dport, 8) && aligned(pc.proto, 4) && (!vo || aligned(vo, 4)) ? 1u : 0u;
+            cd.zero = co.zero && !zeroed ? co.out : nullptr;    // the first launch clears the call's counters
+            cd.n_zero = t->n_rules + 1;
             HIPC(e, launch_classify16_cls(cd, fe, pc, vo, slot_val, q.lds_resident, lin, cfg));
-            if (!lin) HIPC(e, launch_other16(cd, cfg.other, fe, cd.oq, uint32_t(cfg.grid), cd.oq_cap, pc, vo, slot_val, s));
+            zeroed = true;
+            cd.zero = nullptr;
             if (timing && off + m >= n) HIPC(e, hipEventRecord(e->ev1, s));
-            if (q.lds_resident) {
-                HIPC(e, launch_fold(cd.part, uint32_t(cfg.grid), c.n_lctr, slot_val, co.zero && !zeroed ? co.out : nullptr,
-                                    t->n_rules + 1, s));
-                zeroed = true;
-            }
+            const FinishArgs f = finish_args(t->c16, sc, cd, co, q.lds_resident, uint32_t(cfg.grid), c.n_ctr,
+                                             off + m >= n);
+            HIPC(e, launch_finish16(f, cd, cfg.other, fe, pc, vo, s));
+            remapped = true;
         }
     }
     if (timing) {
@@ -669,7 +720,7 @@ static int classify16_locked(cls_engine* e, std::shared_ptr<Table> t, const cls_
         e->timed = true;
     }
     if (co.zero && !zeroed) HIPC(e, launch_fold(nullptr, 0, 0, slot_val, co.out, t->n_rules + 1, s));
-    return finish_counts(e, *t, t->c16, sc, co, n, verdict_out, d_verdict, counters_out, flags, s);
+    return finish_counts(e, *t, t->c16, sc, co, n, verdict_out, d_verdict, counters_out, flags, s, remapped);
 }
 
 int cls_classify(cls_engine* e, uint32_t table_id, const cls_pkt_soa* pk, uint64_t n,
@@ -728,7 +779,7 @@ int cls_classify(cls_engine* e, uint32_t table_id, const cls_pkt_soa* pk, uint64
         const int rc = timing_begin(e, s);
         if (rc != CLS_OK) return rc;
     }
-    bool zeroed = false;
+    bool zeroed = false, remapped = false;
     if (n) {
         if (use_cls) {
             Cls4Dev cd = table_dev(*t);
@@ -743,16 +794,17 @@ int cls_classify(cls_engine* e, uint32_t table_id, const cls_pkt_soa* pk, uint64
             for (uint64_t off = 0; off < n; off += kClsChunk) {
                 const uint64_t m = std::min<uint64_t>(kClsChunk, n - off);
                 const Pkts4 pc = framed(t->img, Pkts4{p.src + off, p.dst + off, p.dport + off, p.proto + off, m});
-                HIPC(e, launch_classify4_cls(cd, pc, d_verdict ? d_verdict + off : nullptr, slot_val,
-                                             t->lds_resident, vec, cfg));
-                HIPC(e, launch_other4(cfg.other, t->img.n_ctr, cd.oq, uint32_t(cfg.grid), cd.oq_cap, pc,
-                                      d_verdict ? d_verdict + off : nullptr, slot_val, s));
+                uint8_t* vo = d_verdict ? d_verdict + off : nullptr;
+                cd.zero = co.zero && !zeroed ? co.out : nullptr;   // the first launch clears the call's counters
+                cd.n_zero = t->n_rules + 1;
+                HIPC(e, launch_classify4_cls(cd, pc, vo, slot_val, t->lds_resident, vec, cfg));
+                zeroed = true;
+                cd.zero = nullptr;
                 if (timing && off + m >= n) HIPC(e, hipEventRecord(e->ev1, s));
-                if (t->lds_resident) {
-                    HIPC(e, launch_fold(cd.part, uint32_t(cfg.grid), t->img.n_lctr, slot_val,
-                                        co.zero && !zeroed ? co.out : nullptr, t->n_rules + 1, s));
-                    zeroed = true;
-                }
+                const FinishArgs f = finish_args(t->c4, sc, cd, co, t->lds_resident, uint32_t(cfg.grid),
+                                                 t->img.n_ctr, off + m >= n);
+                HIPC(e, launch_finish4(f, cfg.other, pc, vo, s));
+                remapped = true;
             }
         } else {
             const uint32_t base = t->c4.n_image;
@@ -767,7 +819,7 @@ int cls_classify(cls_engine* e, uint32_t table_id, const cls_pkt_soa* pk, uint64
         e->timed = true;
     }
     if (co.zero && !zeroed) HIPC(e, launch_fold(nullptr, 0, 0, slot_val, co.out, t->n_rules + 1, s));
-    return finish_counts(e, *t, t->c4, sc, co, n, verdict_out, d_verdict, counters_out, flags, s);
+    return finish_counts(e, *t, t->c4, sc, co, n, verdict_out, d_verdict, counters_out, flags, s, remapped);
 }
 
 int cls_stream_floor(cls_engine* e, const cls_pkt_soa* pk, uint64_t n, uint8_t* verdict, uint32_t reps,

@@ -619,6 +619,9 @@ template <bool kLds, bool kVec, int kMode, int kList, int kD, int kCtr>
 __global__ __launch_bounds__(kClsBlock) void classify4_cls(Cls4Dev t, Cls4Dev o, Pkts4 p, uint8_t* verdict,
                                                            unsigned long long* gslot) {
     extern __shared__ uint4 smem[];
+    if (t.zero)   // the call's rule counters, added to by the finish launch
+        for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < t.n_zero; i += gridDim.x * blockDim.x)
+            t.zero[i] = 0ull;
     Img<kLds> im{reinterpret_cast<const uint8_t*>(t.img)};
     const uint32_t oq_lds = queue_begin<kLds>(t, smem);
     if constexpr (kLds && !(CLS_ABLATE & 16)) stage_lds(t, smem);
@@ -645,15 +648,21 @@ __global__ __launch_bounds__(kClsBlock) void classify4_cls(Cls4Dev t, Cls4Dev o,
             uint2 dp[kG];
             uint32_t pr[kG];
         };
+        // The loads are unconditional: a lane past the end re-reads the last
+        // group (its data unused).  Loads under a divergent branch make the
+        // compiler wait for *every* outstanding load (vmcnt(0)) where the
+        // branches join -- the next step's prefetch included, which then
+        // overlaps nothing.
+        const uint32_t span = nthreads * uint32_t(kG);
+        const uint32_t nfull = nsteps / span * span;   // whole grid steps: uniform trip count
         auto load = [&](Buf& b, uint32_t g, bool ok) {
-            if (ok) {
+            (void)ok;
 #pragma unroll
-                for (int k = 0; k < kG; ++k) {
-                    const uint32_t gi = g + uint32_t(k) * nthreads;
-                    b.s[k] = ldnt(at(S, gi)); b.d[k] = ldnt(at(D, gi));
-                    b.dp[k] = ldnt(at(DP, gi));
-                    b.pr[k] = CLS_NT_PROTO ? ldnt(at(PR, gi)) : *at(PR, gi);
-                }
+            for (int k = 0; k < kG; ++k) {
+                const uint32_t gi = min(g + uint32_t(k) * nthreads, nfull - 1u);
+                b.s[k] = ldnt(at(S, gi)); b.d[k] = ldnt(at(D, gi));
+                b.dp[k] = ldnt(at(DP, gi));
+                b.pr[k] = CLS_NT_PROTO ? ldnt(at(PR, gi)) : *at(PR, gi);
             }
         };
         auto step = [&](const Buf& b, uint32_t g) {
@@ -692,20 +701,20 @@ __global__ __launch_bounds__(kClsBlock) void classify4_cls(Cls4Dev t, Cls4Dev o,
         // lookups -- the pure stream is faster that way (tools/stream_bench.hip:
         // 0.527 vs 0.558 ms per 256 Mi packets) but with the lookups the two
         // measure the same within noise on config 3 (0.605-0.626 ms).
-        const uint32_t span = nthreads * uint32_t(kG);
-        const uint32_t nfull = nsteps / span * span;
 #if CLS_PREFETCH
-        Buf a, b;
-        uint32_t g = tid;
-        load(a, g, g < nfull);
-        while (g < nfull) {
-            load(b, g + span, g + span < nfull);
-            step(a, g);
-            g += span;
-            if (g >= nfull) break;
-            load(a, g + span, g + span < nfull);
-            step(b, g);
-            g += span;
+        if (nfull) {
+            Buf a, b;
+            uint32_t g = tid;
+            load(a, g, true);
+            while (g < nfull) {
+                load(b, g + span, g + span < nfull);
+                step(a, g);
+                g += span;
+                if (g >= nfull) break;
+                load(a, g + span, g + span < nfull);
+                step(b, g);
+                g += span;
+            }
         }
 #else
         for (uint32_t g = tid; g < nfull; g += span) {
@@ -780,17 +789,32 @@ __global__ __launch_bounds__(kClsBlock) void stream4_kernel(Pkts4 p, uint8_t* ve
         stnt(v, const_cast<uint32_t*>(at(reinterpret_cast<const uint32_t*>(verdict), g)));
     };
     if constexpr (kPf) {
-        Buf a, b;
-        uint32_t g = tid;
-        load(a, g);
-        while (g < nsteps) {
-            load(b, g + nthreads);
+        // as classify4_cls: whole grid steps with unconditional (clamped)
+        // loads, so the next step's loads stay in flight; the rest after
+        const uint32_t nfull = nsteps / nthreads * nthreads;
+        auto loadc = [&](Buf& b, uint32_t g) {
+            const uint32_t gi = min(g, nfull - 1u);
+            b.s = ldnt(at(S, gi)); b.d = ldnt(at(D, gi)); b.dp = ldnt(at(DP, gi));
+            b.pr = kNtPr ? ldnt(at(PR, gi)) : *at(PR, gi);
+        };
+        if (nfull) {
+            Buf a, b;
+            uint32_t g = tid;
+            loadc(a, g);
+            while (g < nfull) {
+                loadc(b, g + nthreads);
+                step(a, g);
+                g += nthreads;
+                if (g >= nfull) break;
+                loadc(a, g + nthreads);
+                step(b, g);
+                g += nthreads;
+            }
+        }
+        for (uint32_t g = nfull + tid; g < nsteps; g += nthreads) {
+            Buf a;
+            load(a, g);
             step(a, g);
-            g += nthreads;
-            if (g >= nsteps) break;
-            load(a, g + nthreads);
-            step(b, g);
-            g += nthreads;
         }
     } else {
         for (uint32_t g = tid; g < nsteps; g += nthreads) {
@@ -861,6 +885,106 @@ __global__ __launch_bounds__(256) void other4_kernel(Cls4Dev o, uint32_t n_main,
                                                      uint32_t rows, uint32_t cap, Pkts4 p, uint8_t* verdict,
                                                      unsigned long long* gslot) {
     other_loop(o, n_main, oq, rows, cap, verdict, gslot, [&](uint32_t k, uint32_t& s, uint32_t& d, uint32_t& dp) {
+        s = p.src[k];
+        d = p.dst[k];
+        dp = p.dport[k];
+    });
+}
+
+// The rule of a slot (FinishArgs.slot_rule: hot rules through their table).
+__device__ __forceinline__ uint32_t slot_rule_of(const FinishArgs& f, uint32_t slot) {
+    const uint32_t e = f.slot_rule[slot];
+    return (e & kHotRule) ? f.slot_rule[f.n_slots + (e & ~kHotRule)] : e;
+}
+
+// One launch at the end of a classify call (kernels.hpp FinishArgs).  Blocks
+// [0, ntile): 64 slots each -- the 16 waves sum the workgroups' partial rows
+// (rows w, w + 16, ...: 256 contiguous bytes per load instruction), wave 0
+// adds the slot's global counter and moves the total to its rule (hot rules:
+// summed in LDS over the tile first, one atomic per tile).  Blocks after:
+// one OTHER queue row each (the packets one classify workgroup queued),
+// every lane on one packet, counted in an LDS histogram over the OTHER
+// slots.  No block waits for another: the OTHER slots are counted straight
+// into their rules, and the tiles read only what the classify launch wrote.
+constexpr uint32_t kFoldWaves = 16;
+template <typename Load>
+__device__ __forceinline__ void finish_body(const FinishArgs& f, const Cls4Dev& o, uint8_t* verdict,
+                                            const Load& load) {
+    __shared__ unsigned long long acc[kFoldWaves][64];
+    __shared__ unsigned long long hot[kMaxHotRules];
+    __shared__ uint32_t h[kOtherLds];
+    const uint32_t span = f.remap ? f.n_slots : (f.part ? f.n_lctr : 0u);
+    const uint32_t ntile = (span + 63u) / 64u;
+    if (blockIdx.x < ntile) {
+        const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+        const uint32_t i = blockIdx.x * 64u + lane;
+        if (threadIdx.x < f.n_hot) hot[threadIdx.x] = 0ull;
+        unsigned long long s64 = 0;
+        if (f.part && i < f.n_lctr) {
+            const uint32_t n = f.n_lctr, rows = f.rows;
+            const uint32_t* part = f.part;
+            uint32_t w = wave;
+            for (; w + 3u * kFoldWaves < rows; w += 4u * kFoldWaves) {
+                const uint32_t a = part[size_t(w) * n + i], b = part[size_t(w + kFoldWaves) * n + i];
+                const uint32_t c = part[size_t(w + 2u * kFoldWaves) * n + i];
+                const uint32_t d = part[size_t(w + 3u * kFoldWaves) * n + i];
+                s64 += (unsigned long long)a + b + c + d;
+            }
+            for (; w < rows; w += kFoldWaves) s64 += part[size_t(w) * n + i];
+        }
+        acc[wave][lane] = s64;
+        __syncthreads();
+        if (wave == 0 && i < span) {
+#pragma unroll
+            for (uint32_t k = 1; k < kFoldWaves; ++k) s64 += acc[k][lane];
+            if (f.remap) {
+                const unsigned long long sv = f.slot_val[i];
+                if (sv) f.slot_val[i] = 0ull;
+                s64 += sv;
+                if (s64) {
+                    const uint32_t e = f.slot_rule[i];
+                    if (e & kHotRule) atomicAdd(&hot[e & ~kHotRule], s64);
+                    else atomicAdd(&f.out[e], s64);
+                }
+            } else if (s64) {
+                f.slot_val[i] += s64;            // an earlier chunk: this launch is the only writer
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x < f.n_hot && hot[threadIdx.x])
+            atomicAdd(&f.out[f.slot_rule[f.n_slots + threadIdx.x]], hot[threadIdx.x]);
+        return;
+    }
+    const uint32_t r = blockIdx.x - ntile;
+    if (r >= f.oq_rows) return;
+    const uint32_t n = f.oq[r];
+    if (n == 0) return;
+    const bool lds = o.n_ctr <= kOtherLds;
+    if (lds) {
+        for (uint32_t i = threadIdx.x; i < o.n_ctr; i += blockDim.x) h[i] = 0u;
+        __syncthreads();
+    }
+    const Img<false> oim{reinterpret_cast<const uint8_t*>(o.img)};
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+        const uint32_t k = f.oq[f.oq_rows + r * f.oq_cap + i];
+        uint32_t s1[1], d1[1], p1[1];
+        load(k, s1[0], d1[0], p1[0]);
+        const uint32_t z1[1] = {0u};
+        uint32_t r1[1], k1[1];
+        classify_n<1, false, 0, 0, -1>(oim, o, s1, d1, p1, z1, r1, k1);
+        if (verdict) verdict[k] = uint8_t(r1[0]);
+        if (lds) atomicAdd(&h[k1[0]], 1u);
+        else wave_count(f.out, slot_rule_of(f, f.n_main + k1[0]));
+    }
+    if (lds) {
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < o.n_ctr; i += blockDim.x)
+            if (h[i]) atomicAdd(&f.out[slot_rule_of(f, f.n_main + i)], (unsigned long long)h[i]);
+    }
+}
+
+__global__ __launch_bounds__(1024) void finish4_kernel(FinishArgs f, Cls4Dev o, Pkts4 p, uint8_t* verdict) {
+    finish_body(f, o, verdict, [&](uint32_t k, uint32_t& s, uint32_t& d, uint32_t& dp) {
         s = p.src[k];
         d = p.dst[k];
         dp = p.dport[k];
@@ -990,6 +1114,9 @@ template <bool kLds, int kMode, int kList, int kD, bool kLin, int kFe, int kCtr>
 __global__ __launch_bounds__(kClsBlock) void classify16_cls(Cls4Dev t, Cls4Dev o, Fe16 fe, Pkts16 p,
                                                             uint8_t* verdict, unsigned long long* gslot) {
     extern __shared__ uint4 smem[];
+    if (t.zero)   // the call's rule counters, added to by the finish launch
+        for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < t.n_zero; i += gridDim.x * blockDim.x)
+            t.zero[i] = 0ull;
     Img<kLds> im{reinterpret_cast<const uint8_t*>(t.img)};
     const uint32_t oq_lds = queue_begin<kLds>(t, smem);
     if constexpr (kLds) stage_lds(t, smem);
@@ -1141,13 +1268,27 @@ __global__ __launch_bounds__(256) void other16_kernel(Cls4Dev t, Cls4Dev o, Fe16
     });
 }
 
+__global__ __launch_bounds__(1024) void finish16_kernel(FinishArgs f, Cls4Dev t, Cls4Dev o, Fe16 fe, Pkts16 p,
+                                                       uint8_t* verdict) {
+    const Img<false> gim{reinterpret_cast<const uint8_t*>(t.img)};
+    finish_body(f, o, verdict, [&](uint32_t k, uint32_t& s, uint32_t& d, uint32_t& dp) {
+        const uint4 s16[1] = {p.src[k]}, d16[1] = {p.dst[k]};
+        uint32_t s1[1], d1[1];
+        if (fe.src_mode == 1) s1[0] = src_rep_global(fe.gsrc, fe.gval, fe.top[0], fe.k8[0], s16[0]);
+        else fe_rep(gim, fe.key[0], fe.val[0], fe.top[0], fe.k8[0], s16, s1);
+        fe_rep(gim, fe.key[1], fe.val[1], fe.top[1], fe.k8[1], d16, d1);
+        s = s1[0];
+        d = d1[0];
+        dp = p.dport[k];
+    });
+}
+
 // slot_val[i] += the sum over the grid's rows of part[w][i], i < n: block b
 // takes slots [64 b, 64 b + 64), wave w of its 16 the rows w, w + 16, ...
 // (256 contiguous bytes per load instruction), then one wave adds the 16
 // partial sums -- a plain read-modify-write, this launch being the only
 // writer.  Blocks past the slot range zero `zero` (the call's rule counters):
 // no separate memset launch.
-constexpr uint32_t kFoldWaves = 16;
 __global__ __launch_bounds__(1024) void fold_kernel(const uint32_t* __restrict__ part, uint32_t rows, uint32_t n,
                                                     unsigned long long* __restrict__ slot_val,
                                                     unsigned long long* __restrict__ zero, uint32_t n_zero) {
@@ -1797,6 +1938,26 @@ hipError_t launch_remap(unsigned long long* slot_val, const uint2* csr, uint32_t
                         hipStream_t s) {
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(remap_kernel, dim3((n + 255) / 256), dim3(256), 0, s, slot_val, csr, n, out);
+    return hipGetLastError();
+}
+
+static uint32_t finish_grid(const FinishArgs& f) {
+    const uint32_t span = f.remap ? f.n_slots : (f.part ? f.n_lctr : 0u);
+    return (span + 63u) / 64u + (f.oq ? f.oq_rows : 0u);
+}
+
+hipError_t launch_finish4(const FinishArgs& f, const Cls4Dev& o, const Pkts4& p, uint8_t* verdict, hipStream_t s) {
+    const uint32_t g = finish_grid(f);
+    if (g == 0) return hipSuccess;
+    hipLaunchKernelGGL(finish4_kernel, dim3(g), dim3(1024), 0, s, f, o, p, verdict);
+    return hipGetLastError();
+}
+
+hipError_t launch_finish16(const FinishArgs& f, const Cls4Dev& t, const Cls4Dev& o, const Fe16& fe, const Pkts16& p,
+                           uint8_t* verdict, hipStream_t s) {
+    const uint32_t g = finish_grid(f);
+    if (g == 0) return hipSuccess;
+    hipLaunchKernelGGL(finish16_kernel, dim3(g), dim3(1024), 0, s, f, t, o, fe, p, verdict);
     return hipGetLastError();
 }
 
