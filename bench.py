@@ -40,8 +40,9 @@ BYTES_PER_PKT = {4: 12,         # src 4 + dst 4 + dport 2 + proto 1 + verdict 1 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=25,
+                    help="untimed steps first: the GPU clocks settle over the first ~10 ms of work")
     ap.add_argument("--config", type=int, default=3, choices=[2, 3, 4, 5])
     ap.add_argument("--packets", type=int, default=0, help="packets per GPU (default: config's)")
     ap.add_argument("--cpu-sample", type=int, default=1 << 21,

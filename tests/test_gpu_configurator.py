@@ -119,3 +119,33 @@ def test_gen_policy_scale_on_gpu(eng, num_cidrs):
             assert len(set(want_v.tolist())) >= 2
     finally:
         r.close()
+
+
+def test_gen_policy_default_scale_on_gpu(eng):
+    """gen-policy.py at its defaults (tests/policy/perf/gen-policy.py:8-11:
+    1000 blocks x 5 excepts x 20 ports): the pod's ingress list has ~477k
+    rules and compiles to the global-memory image (template scan).  2000
+    packets against the pre-parsed C evalACL oracle, verdicts and per-rule
+    counts."""
+    import oracle
+    from configurator_replay import gen_policy_packets
+    from vpp_amd.renderer.api import PodID
+    rng = random.Random(1000)
+    pol = C.gen_policy(rng, num_cidrs=1000)
+    pod = PodID("db", "default")
+    rules = C.PolicyConfigurator({pod: "10.1.1.1"}).new_txn(False).generate_rules(C.MATCH_INGRESS, [pol])
+    assert len(rules) > 400_000
+    src, dst, proto, dport, s16, d16 = gen_policy_packets(rng, 2000, 1000)
+    ports = [p.number for m in pol.matches for p in m.ports]
+    dport = [rng.choice(ports) if rng.random() < 0.5 else p for p in dport]
+    p8, dp16 = np.array(proto, np.uint8), np.array(dport, np.uint16)
+    acl_rules = T.compile_rules(rules)
+    want_v, want_c = oracle.classify_fast(oracle.rules_to_c(acl_rules), s16, d16, dp16, p8, af=16)
+    t = eng.put_table("gen1000", acl_rules)
+    try:
+        v, c = eng.classify(t, s16, d16, dp16, p8)
+        assert np.array_equal(v, want_v)
+        assert np.array_equal(c, want_c)
+        assert len(set(want_v.tolist())) >= 2
+    finally:
+        eng.del_table(t)

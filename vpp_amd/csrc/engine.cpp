@@ -560,10 +560,9 @@ static CountOut count_out(Scratch* sc, uint64_t* counters_out, uint32_t flags) {
 }
 
 // The finish launch of a classify chunk (kernels.hpp FinishArgs): fold the
-// workgroups' partials, and on the last chunk move every slot to its rule;
-// the OTHER queue's packets classified and counted.
-static FinishArgs finish_args(const Counters& c, Scratch* sc, const Cls4Dev& cd, const CountOut& co, bool lds_resident,
-                              uint32_t rows, uint32_t n_main, bool last) {
+// workgroups' partials, and on the last chunk move every slot to its rule.
+static FinishArgs finish_args(const Counters& c, Scratch* sc, const CountOut& co, bool lds_resident, uint32_t rows,
+                              bool last) {
     FinishArgs f;
     f.part = lds_resident ? sc->part.as<uint32_t>() : nullptr;
     f.rows = rows;
@@ -574,10 +573,6 @@ static FinishArgs finish_args(const Counters& c, Scratch* sc, const Cls4Dev& cd,
     f.n_hot = c.n_hot;
     f.out = co.out;
     f.remap = last;
-    f.oq = cd.oq;
-    f.oq_rows = rows;
-    f.oq_cap = cd.oq_cap;
-    f.n_main = n_main;
     return f;
 }
 
@@ -709,9 +704,8 @@ static int classify16_locked(cls_engine* e, std::shared_ptr<Table> t, const cls_
             zeroed = true;
             cd.zero = nullptr;
             if (timing && off + m >= n) HIPC(e, hipEventRecord(e->ev1, s));
-            const FinishArgs f = finish_args(t->c16, sc, cd, co, q.lds_resident, uint32_t(cfg.grid), c.n_ctr,
-                                             off + m >= n);
-            HIPC(e, launch_finish16(f, cd, cfg.other, fe, pc, vo, s));
+            if (!lin) HIPC(e, launch_other16(cd, cfg.other, fe, cd.oq, uint32_t(cfg.grid), cd.oq_cap, pc, vo, slot_val, s));
+            HIPC(e, launch_finish(finish_args(t->c16, sc, co, q.lds_resident, uint32_t(cfg.grid), off + m >= n), s));
             remapped = true;
         }
     }
@@ -801,9 +795,10 @@ int cls_classify(cls_engine* e, uint32_t table_id, const cls_pkt_soa* pk, uint64
                 zeroed = true;
                 cd.zero = nullptr;
                 if (timing && off + m >= n) HIPC(e, hipEventRecord(e->ev1, s));
-                const FinishArgs f = finish_args(t->c4, sc, cd, co, t->lds_resident, uint32_t(cfg.grid),
-                                                 t->img.n_ctr, off + m >= n);
-                HIPC(e, launch_finish4(f, cfg.other, pc, vo, s));
+                HIPC(e, launch_other4(cfg.other, t->img.n_ctr, cd.oq, uint32_t(cfg.grid), cd.oq_cap, pc, vo, slot_val,
+                                      s));
+                HIPC(e, launch_finish(finish_args(t->c4, sc, co, t->lds_resident, uint32_t(cfg.grid), off + m >= n),
+                                      s));
                 remapped = true;
             }
         } else {

@@ -556,8 +556,14 @@ __device__ __forceinline__ void run_n(const Img<kLds>& im, const Cls4Dev& t, con
 #ifndef CLS_NT16_SMALL
 #define CLS_NT16_SMALL 1
 #endif
+// 0 (default): load and use, the CU's 16 waves overlapping one another's
+// loads and lookups; 1: the next step's loads in flight during this step's
+// lookups (two buffers); 2: two steps ahead (three buffers).  Config 3,
+// in-process A/B on MI355X (profiles/r02s4_prefetch_depth_ab_config3.txt):
+// 0.559 / 0.566 / 0.583 ms -- the buffers' registers cost more than the
+// overlap they buy at 16 waves per CU.
 #ifndef CLS_PREFETCH
-#define CLS_PREFETCH 1
+#define CLS_PREFETCH 0
 #endif
 constexpr int kG = CLS_GROUPS;     // 16-B packet groups per lane per step
 
@@ -579,6 +585,7 @@ __device__ __forceinline__ void queue_end(const Cls4Dev& t, uint32_t oq_lds) {
     if (threadIdx.x == 0)
         t.oq[blockIdx.x] = min(*reinterpret_cast<const __attribute__((address_space(3))) uint32_t*>(oq_lds), t.oq_cap);
 }
+
 
 // Stage the read-only image into LDS (at address 0) and zero the counters.
 __device__ __forceinline__ void stage_lds(const Cls4Dev& t, uint4* smem) {
@@ -695,13 +702,29 @@ __global__ __launch_bounds__(kClsBlock) void classify4_cls(Cls4Dev t, Cls4Dev o,
                                                   g + uint32_t(k) * nthreads)));
             }
         };
-        // Full steps over groups [0, nfull).  CLS_PREFETCH (default): two
-        // buffers in turn, the next step's loads in flight during this step's
-        // lookups.  Off: load and use, the CU's 16 waves overlapping stream and
-        // lookups -- the pure stream is faster that way (tools/stream_bench.hip:
-        // 0.527 vs 0.558 ms per 256 Mi packets) but with the lookups the two
-        // measure the same within noise on config 3 (0.605-0.626 ms).
-#if CLS_PREFETCH
+        // Full steps over groups [0, nfull) (CLS_PREFETCH above).
+#if CLS_PREFETCH == 2
+        // two steps of loads in flight: three buffers in turn
+        if (nfull) {
+            Buf a, b, c;
+            uint32_t g = tid;
+            load(a, g, true);
+            load(b, g + span, true);
+            while (g < nfull) {
+                load(c, g + 2u * span, true);
+                step(a, g);
+                g += span;
+                if (g >= nfull) break;
+                load(a, g + 2u * span, true);
+                step(b, g);
+                g += span;
+                if (g >= nfull) break;
+                load(b, g + 2u * span, true);
+                step(c, g);
+                g += span;
+            }
+        }
+#elif CLS_PREFETCH
         if (nfull) {
             Buf a, b;
             uint32_t g = tid;
@@ -891,104 +914,54 @@ __global__ __launch_bounds__(256) void other4_kernel(Cls4Dev o, uint32_t n_main,
     });
 }
 
-// The rule of a slot (FinishArgs.slot_rule: hot rules through their table).
-__device__ __forceinline__ uint32_t slot_rule_of(const FinishArgs& f, uint32_t slot) {
-    const uint32_t e = f.slot_rule[slot];
-    return (e & kHotRule) ? f.slot_rule[f.n_slots + (e & ~kHotRule)] : e;
-}
-
-// One launch at the end of a classify call (kernels.hpp FinishArgs).  Blocks
-// [0, ntile): 64 slots each -- the 16 waves sum the workgroups' partial rows
-// (rows w, w + 16, ...: 256 contiguous bytes per load instruction), wave 0
-// adds the slot's global counter and moves the total to its rule (hot rules:
-// summed in LDS over the tile first, one atomic per tile).  Blocks after:
-// one OTHER queue row each (the packets one classify workgroup queued),
-// every lane on one packet, counted in an LDS histogram over the OTHER
-// slots.  No block waits for another: the OTHER slots are counted straight
-// into their rules, and the tiles read only what the classify launch wrote.
+// One launch at the end of a classify call (kernels.hpp FinishArgs): tiles
+// of 64 slots -- the 16 waves sum the workgroups' partial rows (rows w,
+// w + 16, ...: 256 contiguous bytes per load instruction), wave 0 adds the
+// slot's global counter and moves the total to its rule (hot rules: summed
+// in LDS over the tile first, one atomic per tile).  The tiles read only what
+// the classify launch wrote, so no tile waits for another.
 constexpr uint32_t kFoldWaves = 16;
-template <typename Load>
-__device__ __forceinline__ void finish_body(const FinishArgs& f, const Cls4Dev& o, uint8_t* verdict,
-                                            const Load& load) {
+__global__ __launch_bounds__(1024) void finish_kernel(FinishArgs f) {
     __shared__ unsigned long long acc[kFoldWaves][64];
     __shared__ unsigned long long hot[kMaxHotRules];
-    __shared__ uint32_t h[kOtherLds];
     const uint32_t span = f.remap ? f.n_slots : (f.part ? f.n_lctr : 0u);
-    const uint32_t ntile = (span + 63u) / 64u;
-    if (blockIdx.x < ntile) {
-        const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-        const uint32_t i = blockIdx.x * 64u + lane;
-        if (threadIdx.x < f.n_hot) hot[threadIdx.x] = 0ull;
-        unsigned long long s64 = 0;
-        if (f.part && i < f.n_lctr) {
-            const uint32_t n = f.n_lctr, rows = f.rows;
-            const uint32_t* part = f.part;
-            uint32_t w = wave;
-            for (; w + 3u * kFoldWaves < rows; w += 4u * kFoldWaves) {
-                const uint32_t a = part[size_t(w) * n + i], b = part[size_t(w + kFoldWaves) * n + i];
-                const uint32_t c = part[size_t(w + 2u * kFoldWaves) * n + i];
-                const uint32_t d = part[size_t(w + 3u * kFoldWaves) * n + i];
-                s64 += (unsigned long long)a + b + c + d;
-            }
-            for (; w < rows; w += kFoldWaves) s64 += part[size_t(w) * n + i];
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint32_t i = blockIdx.x * 64u + lane;
+    if (threadIdx.x < f.n_hot) hot[threadIdx.x] = 0ull;
+    unsigned long long s64 = 0;
+    if (f.part && i < f.n_lctr) {
+        const uint32_t n = f.n_lctr, rows = f.rows;
+        const uint32_t* part = f.part;
+        uint32_t w = wave;
+        for (; w + 3u * kFoldWaves < rows; w += 4u * kFoldWaves) {
+            const uint32_t a = part[size_t(w) * n + i], b = part[size_t(w + kFoldWaves) * n + i];
+            const uint32_t c = part[size_t(w + 2u * kFoldWaves) * n + i];
+            const uint32_t d = part[size_t(w + 3u * kFoldWaves) * n + i];
+            s64 += (unsigned long long)a + b + c + d;
         }
-        acc[wave][lane] = s64;
-        __syncthreads();
-        if (wave == 0 && i < span) {
+        for (; w < rows; w += kFoldWaves) s64 += part[size_t(w) * n + i];
+    }
+    acc[wave][lane] = s64;
+    __syncthreads();
+    if (wave == 0 && i < span) {
 #pragma unroll
-            for (uint32_t k = 1; k < kFoldWaves; ++k) s64 += acc[k][lane];
-            if (f.remap) {
-                const unsigned long long sv = f.slot_val[i];
-                if (sv) f.slot_val[i] = 0ull;
-                s64 += sv;
-                if (s64) {
-                    const uint32_t e = f.slot_rule[i];
-                    if (e & kHotRule) atomicAdd(&hot[e & ~kHotRule], s64);
-                    else atomicAdd(&f.out[e], s64);
-                }
-            } else if (s64) {
-                f.slot_val[i] += s64;            // an earlier chunk: this launch is the only writer
+        for (uint32_t k = 1; k < kFoldWaves; ++k) s64 += acc[k][lane];
+        if (f.remap) {
+            const unsigned long long sv = f.slot_val[i];
+            if (sv) f.slot_val[i] = 0ull;
+            s64 += sv;
+            if (s64) {
+                const uint32_t e = f.slot_rule[i];
+                if (e & kHotRule) atomicAdd(&hot[e & ~kHotRule], s64);
+                else atomicAdd(&f.out[e], s64);
             }
+        } else if (s64) {
+            f.slot_val[i] += s64;            // an earlier chunk: this launch is the only writer
         }
-        __syncthreads();
-        if (threadIdx.x < f.n_hot && hot[threadIdx.x])
-            atomicAdd(&f.out[f.slot_rule[f.n_slots + threadIdx.x]], hot[threadIdx.x]);
-        return;
     }
-    const uint32_t r = blockIdx.x - ntile;
-    if (r >= f.oq_rows) return;
-    const uint32_t n = f.oq[r];
-    if (n == 0) return;
-    const bool lds = o.n_ctr <= kOtherLds;
-    if (lds) {
-        for (uint32_t i = threadIdx.x; i < o.n_ctr; i += blockDim.x) h[i] = 0u;
-        __syncthreads();
-    }
-    const Img<false> oim{reinterpret_cast<const uint8_t*>(o.img)};
-    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
-        const uint32_t k = f.oq[f.oq_rows + r * f.oq_cap + i];
-        uint32_t s1[1], d1[1], p1[1];
-        load(k, s1[0], d1[0], p1[0]);
-        const uint32_t z1[1] = {0u};
-        uint32_t r1[1], k1[1];
-        classify_n<1, false, 0, 0, -1>(oim, o, s1, d1, p1, z1, r1, k1);
-        if (verdict) verdict[k] = uint8_t(r1[0]);
-        if (lds) atomicAdd(&h[k1[0]], 1u);
-        else wave_count(f.out, slot_rule_of(f, f.n_main + k1[0]));
-    }
-    if (lds) {
-        __syncthreads();
-        for (uint32_t i = threadIdx.x; i < o.n_ctr; i += blockDim.x)
-            if (h[i]) atomicAdd(&f.out[slot_rule_of(f, f.n_main + i)], (unsigned long long)h[i]);
-    }
-}
-
-__global__ __launch_bounds__(1024) void finish4_kernel(FinishArgs f, Cls4Dev o, Pkts4 p, uint8_t* verdict) {
-    finish_body(f, o, verdict, [&](uint32_t k, uint32_t& s, uint32_t& d, uint32_t& dp) {
-        s = p.src[k];
-        d = p.dst[k];
-        dp = p.dport[k];
-    });
+    __syncthreads();
+    if (threadIdx.x < f.n_hot && hot[threadIdx.x])
+        atomicAdd(&f.out[f.slot_rule[f.n_slots + threadIdx.x]], hot[threadIdx.x]);
 }
 
 // ---------------------------------------------------------------------------
@@ -1257,21 +1230,6 @@ __global__ __launch_bounds__(256) void other16_kernel(Cls4Dev t, Cls4Dev o, Fe16
                                                       unsigned long long* gslot) {
     const Img<false> gim{reinterpret_cast<const uint8_t*>(t.img)};
     other_loop(o, t.n_ctr, oq, rows, cap, verdict, gslot, [&](uint32_t k, uint32_t& s, uint32_t& d, uint32_t& dp) {
-        const uint4 s16[1] = {p.src[k]}, d16[1] = {p.dst[k]};
-        uint32_t s1[1], d1[1];
-        if (fe.src_mode == 1) s1[0] = src_rep_global(fe.gsrc, fe.gval, fe.top[0], fe.k8[0], s16[0]);
-        else fe_rep(gim, fe.key[0], fe.val[0], fe.top[0], fe.k8[0], s16, s1);
-        fe_rep(gim, fe.key[1], fe.val[1], fe.top[1], fe.k8[1], d16, d1);
-        s = s1[0];
-        d = d1[0];
-        dp = p.dport[k];
-    });
-}
-
-__global__ __launch_bounds__(1024) void finish16_kernel(FinishArgs f, Cls4Dev t, Cls4Dev o, Fe16 fe, Pkts16 p,
-                                                       uint8_t* verdict) {
-    const Img<false> gim{reinterpret_cast<const uint8_t*>(t.img)};
-    finish_body(f, o, verdict, [&](uint32_t k, uint32_t& s, uint32_t& d, uint32_t& dp) {
         const uint4 s16[1] = {p.src[k]}, d16[1] = {p.dst[k]};
         uint32_t s1[1], d1[1];
         if (fe.src_mode == 1) s1[0] = src_rep_global(fe.gsrc, fe.gval, fe.top[0], fe.k8[0], s16[0]);
@@ -1941,23 +1899,11 @@ hipError_t launch_remap(unsigned long long* slot_val, const uint2* csr, uint32_t
     return hipGetLastError();
 }
 
-static uint32_t finish_grid(const FinishArgs& f) {
+hipError_t launch_finish(const FinishArgs& f, hipStream_t s) {
     const uint32_t span = f.remap ? f.n_slots : (f.part ? f.n_lctr : 0u);
-    return (span + 63u) / 64u + (f.oq ? f.oq_rows : 0u);
-}
-
-hipError_t launch_finish4(const FinishArgs& f, const Cls4Dev& o, const Pkts4& p, uint8_t* verdict, hipStream_t s) {
-    const uint32_t g = finish_grid(f);
+    const uint32_t g = (span + 63u) / 64u;
     if (g == 0) return hipSuccess;
-    hipLaunchKernelGGL(finish4_kernel, dim3(g), dim3(1024), 0, s, f, o, p, verdict);
-    return hipGetLastError();
-}
-
-hipError_t launch_finish16(const FinishArgs& f, const Cls4Dev& t, const Cls4Dev& o, const Fe16& fe, const Pkts16& p,
-                           uint8_t* verdict, hipStream_t s) {
-    const uint32_t g = finish_grid(f);
-    if (g == 0) return hipSuccess;
-    hipLaunchKernelGGL(finish16_kernel, dim3(g), dim3(1024), 0, s, f, t, o, fe, p, verdict);
+    hipLaunchKernelGGL(finish_kernel, dim3(g), dim3(1024), 0, s, f);
     return hipGetLastError();
 }
 

@@ -107,16 +107,13 @@ hipError_t launch_other4(const Cls4Dev& o, uint32_t n_main, const uint32_t* oq, 
                          const Pkts4& p, uint8_t* verdict, unsigned long long* gslot, hipStream_t s);
 hipError_t launch_other16(const Cls4Dev& t, const Cls4Dev& o, const Fe16& fe, const uint32_t* oq, uint32_t rows,
                           uint32_t cap, const Pkts16& p, uint8_t* verdict, unsigned long long* gslot, hipStream_t s);
-// The end of a classify call, one launch (finish4 / finish16): tiles of 64
-// slots fold the workgroups' LDS partials (part, rows x n_lctr; null: none)
-// and, with remap, move slot_val + partials to the rule counters out (slot
-// -> rule: slot_rule, entries kHotRule | h for the hot rules -- rules with
-// many slots, summed per tile in LDS -- then their n_hot rule ids) and clear
-// slot_val; without remap (an earlier chunk of a long batch) slot_val +=
-// partials.  Blocks after the tiles classify the OTHER queue's packets
-// (oq: {fill per workgroup, rows segments of cap indices}) on the OTHER
-// image o and count them into out (their slots n_main + k).  out must be
-// cleared before (the classify launch's zero).
+// The end of a classify call, one launch: tiles of 64 slots fold the
+// workgroups' LDS partials (part, rows x n_lctr; null: none) and, with
+// remap, move slot_val + partials to the rule counters out (slot -> rule:
+// slot_rule, entries kHotRule | h for the hot rules -- rules with many slots,
+// summed per tile in LDS -- then their n_hot rule ids) and clear slot_val;
+// without remap (an earlier chunk of a long batch) slot_val += partials.
+// out must be cleared before (the classify launch's zero).
 constexpr uint32_t kHotRule = 0x80000000u;
 constexpr uint32_t kMaxHotRules = 64;
 struct FinishArgs {
@@ -128,12 +125,8 @@ struct FinishArgs {
     uint32_t n_hot;
     unsigned long long* out;
     bool remap;
-    const uint32_t* oq;
-    uint32_t oq_rows, oq_cap, n_main;
 };
-hipError_t launch_finish4(const FinishArgs& f, const Cls4Dev& o, const Pkts4& p, uint8_t* verdict, hipStream_t s);
-hipError_t launch_finish16(const FinishArgs& f, const Cls4Dev& t, const Cls4Dev& o, const Fe16& fe, const Pkts16& p,
-                           uint8_t* verdict, hipStream_t s);
+hipError_t launch_finish(const FinishArgs& f, hipStream_t s);
 // the classify kernels' packet stream without the lookups (stream floor);
 // exactly one of p4 / p16; p4 needs 16-B aligned src/dst, 8-B dport, 4-B
 // proto and verdict (variant bit 0: load and use instead of the next step's
