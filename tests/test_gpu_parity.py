@@ -212,6 +212,50 @@ def test_config3_full_size_properties(eng):
     eng.del_table(t)
 
 
+def test_batch_beyond_one_launch(eng):
+    """A batch of 2^30 + 4099 packets (12.9 GB in HBM) takes two classify
+    launches (32-bit packet offsets inside the kernel): the first launch's
+    partials are folded without the remap, the last one's with it.  The
+    whole batch in one call must equal the two pieces classified by separate
+    calls (verdicts and counters), every packet counted once, and the pieces
+    around the launch boundary equal the oracle."""
+    import torch
+    from vpp_amd import workload
+    acl, spec, _ = workload.config(3)
+    t = eng.put_table("chunks", acl.rules)
+    n = (1 << 30) + 4099
+    out = {k: torch.empty(n, dtype=dt, device="cuda") for k, dt in
+           (("src", torch.int32), ("dst", torch.int32), ("dport", torch.int16),
+            ("proto", torch.uint8))}
+    eng.gen_traffic_v4(spec, 0, out)
+    verdict = torch.empty(n, dtype=torch.uint8, device="cuda")
+    counters = torch.zeros(t.n_rules + 1, dtype=torch.int64, device="cuda")
+    eng.classify(t, out["src"], out["dst"], out["dport"], out["proto"], verdict=verdict, counters=counters)
+    torch.cuda.synchronize()
+    assert int(counters.sum()) == n
+    cut = 1 << 30
+    parts = torch.zeros_like(counters)
+    for a, b in ((0, cut), (cut, n)):
+        v = torch.empty(b - a, dtype=torch.uint8, device="cuda")
+        c = torch.zeros_like(counters)
+        eng.classify(t, out["src"][a:b], out["dst"][a:b], out["dport"][a:b], out["proto"][a:b],
+                     verdict=v, counters=c)
+        torch.cuda.synchronize()
+        assert torch.equal(v, verdict[a:b])
+        parts += c
+        del v
+    assert torch.equal(parts, counters)
+    cr = oracle.rules_to_c(acl.rules)
+    for a in (0, cut - 4096, n - 4096):
+        sl = {k: v[a:a + 4096].cpu().numpy() for k, v in out.items()}
+        ov, _ = oracle.classify_fast(cr, sl["src"].view(np.uint32), sl["dst"].view(np.uint32),
+                                     sl["dport"].view(np.uint16), sl["proto"])
+        assert np.array_equal(verdict[a:a + 4096].cpu().numpy(), ov)
+    del out, verdict
+    torch.cuda.empty_cache()
+    eng.del_table(t)
+
+
 def test_kernel_timing(eng):
     import torch
     from vpp_amd import workload

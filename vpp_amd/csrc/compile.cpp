@@ -726,6 +726,7 @@ static bool build_cls4_one(const std::vector<SemRule>& sem, uint32_t n_rules, Cl
     // kernel can tell the heavily hit slots by `slot < n_hot` and count them
     // in per-lane LDS rows instead of one contended word.
     uint32_t hot_class = 0;
+    std::vector<uint32_t> class_order;
     {
         std::vector<double> span(n_classes, 0.0);
         for (uint32_t k = 0; k < n_real_bounds; ++k) {
@@ -738,10 +739,20 @@ static bool build_cls4_one(const std::vector<SemRule>& sem, uint32_t n_rules, Cl
             hot_class = iclass[uint32_t(std::upper_bound(bounds.begin(), bounds.begin() + n_real_bounds, x) -
                                         bounds.begin()) - 1u];
         }
+        // Slot order: the hot class, then the classes by address space
+        // covered, widest first (ties: class order).  When the counters only
+        // partly fit LDS (slots < n_lctr), the classes most packets land in
+        // are the ones counted there.
+        class_order.resize(n_classes);
+        for (uint32_t c = 0; c < n_classes; ++c) class_order[c] = c;
+        std::stable_sort(class_order.begin(), class_order.end(), [&](uint32_t a, uint32_t b) {
+            if ((a == hot_class) != (b == hot_class)) return a == hot_class;
+            return span[a] > span[b];
+        });
     }
     std::vector<uint32_t> cand;
     for (uint32_t ci = 0; ci < n_classes; ++ci) {
-        const uint32_t c = ci == 0 ? hot_class : (ci <= hot_class ? ci - 1 : ci);
+        const uint32_t c = class_order[ci];
         // merge candidate rule positions: chain of covering prefixes + ANY
         cand.clear();
         for (int p = class_pfx[c]; p >= 0; p = parent[p])
@@ -968,7 +979,7 @@ static bool build_cls4_one(const std::vector<SemRule>& sem, uint32_t n_rules, Cl
     std::vector<uint32_t> ctr3(1, n_rules), cb3(size_t(n_classes) * ncell);
     uint32_t hot3 = 1;
     for (uint32_t ci = 0; ci < n_classes; ++ci) {
-        const uint32_t c = ci == 0 ? hot_class : (ci <= hot_class ? ci - 1 : ci);
+        const uint32_t c = class_order[ci];
         for (uint32_t kk = 0; kk < ncell; ++kk) {
             const size_t k = size_t(c) * ncell + kk;
             cb3[k] = uint32_t(ctr3.size());
