@@ -190,3 +190,32 @@ def test_other_protocols_queue(eng, monkeypatch, cap, v16):
                                   af=16 if v16 else 4)
     np.testing.assert_array_equal(v, ov)
     np.testing.assert_array_equal(c, oc)
+
+
+def test_other_protocols_many_rules(eng):
+    """Protocol-47 packets whose terminating rules are more distinct rules
+    than the finish launch's LDS rule histogram holds (6000 > 4096): counted
+    with wave-aggregated atomics per rule instead; verdicts and counters
+    equal the oracle's."""
+    from vpp_amd import model as M
+    rng = np.random.default_rng(11)
+    hosts = rng.choice(1 << 24, 6000, replace=False) + (10 << 24)
+    rules = [M.l4_rule(M.PERMIT if i % 3 else M.DENY, "%d.%d.%d.%d/32" % (h >> 24, (h >> 16) & 255, (h >> 8) & 255,
+                                                                          h & 255), "", "tcp", 0, 65535, 80, 80)
+             for i, h in enumerate(hosts.tolist())]
+    n = 50000
+    src = rng.choice(hosts, n).astype(np.uint32)
+    miss = rng.random(n) < 0.2                   # some sources match no rule: default DENY
+    src[miss] = rng.integers(0, 1 << 32, int(miss.sum()), dtype=np.uint64).astype(np.uint32)
+    dst = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
+    dport = rng.choice(np.array([80, 443], np.uint16), n)
+    proto = rng.choice(np.array([0, 47, 47, 47], np.uint8), n)
+    t = eng.put_table("other_many", rules)
+    try:
+        v, c = eng.classify(t, src, dst, dport, proto)
+    finally:
+        eng.del_table(t)
+    ov, oc = oracle.classify_fast(oracle.rules_to_c(rules), src, dst, dport, proto)
+    np.testing.assert_array_equal(v, ov)
+    np.testing.assert_array_equal(c, oc)
+    assert (oc[:6000] > 0).sum() > 4096

@@ -70,6 +70,8 @@ struct Counters {
     DevBuf d_csr;                  // uint2 {slot, rule}, grouped by rule
     DevBuf d_slot_rule;            // finish launch: u32 per slot (rule, or kHotRule | h), then the hot rules
     uint32_t n_hot = 0;
+    DevBuf d_other_map;            // finish launch: compact rule index per OTHER slot, then those rules
+    uint32_t n_other = 0, n_orules = 0;
     std::map<hipStream_t, std::unique_ptr<Scratch>> sc;
     ~Counters() {
         for (auto& kv : sc)
@@ -264,6 +266,27 @@ static int counters_init(cls_engine* e, Counters& c, const Cls4Image* img, const
     c.n_hot = uint32_t(mult.size());
     HIPC(e, c.d_slot_rule.ensure(sr.size() * 4));
     HIPC(e, hipMemcpy(c.d_slot_rule.p, sr.data(), sr.size() * 4, hipMemcpyHostToDevice));
+    // The OTHER slots' rules, numbered compactly: the finish launch counts
+    // the queued OTHER packets per rule in LDS and adds one total per
+    // (workgroup, rule).  (Per slot would put many slots of one rule -- a
+    // TestTraffic list's sentinel -- on one counter word from every
+    // workgroup.)
+    c.n_other = n_oth;
+    std::vector<uint32_t> om(n_oth), orules;
+    std::map<uint32_t, uint32_t> cidx;
+    for (uint32_t k = 0; k < n_oth; ++k) {
+        const uint32_t r = rule_of(n_cls + k);
+        auto it = cidx.find(r);
+        if (it == cidx.end()) {
+            it = cidx.emplace(r, uint32_t(orules.size())).first;
+            orules.push_back(r);
+        }
+        om[k] = it->second;
+    }
+    c.n_orules = uint32_t(orules.size());
+    om.insert(om.end(), orules.begin(), orules.end());
+    HIPC(e, c.d_other_map.ensure(std::max<size_t>(1, om.size()) * 4));
+    if (!om.empty()) HIPC(e, hipMemcpy(c.d_other_map.p, om.data(), om.size() * 4, hipMemcpyHostToDevice));
     return CLS_OK;
 }
 
@@ -561,8 +584,8 @@ static CountOut count_out(Scratch* sc, uint64_t* counters_out, uint32_t flags) {
 
 // The finish launch of a classify chunk (kernels.hpp FinishArgs): fold the
 // workgroups' partials, and on the last chunk move every slot to its rule.
-static FinishArgs finish_args(const Counters& c, Scratch* sc, const CountOut& co, bool lds_resident, uint32_t rows,
-                              bool last) {
+static FinishArgs finish_args(const Counters& c, Scratch* sc, const Cls4Dev& cd, const CountOut& co,
+                              bool lds_resident, uint32_t rows, bool last) {
     FinishArgs f;
     f.part = lds_resident ? sc->part.as<uint32_t>() : nullptr;
     f.rows = rows;
@@ -573,6 +596,12 @@ static FinishArgs finish_args(const Counters& c, Scratch* sc, const CountOut& co
     f.n_hot = c.n_hot;
     f.out = co.out;
     f.remap = last;
+    f.oq = cd.oq;
+    f.oq_rows = rows;
+    f.oq_cap = cd.oq_cap;
+    f.other_map = c.d_other_map.as<uint32_t>();
+    f.n_other = c.n_other;
+    f.n_orules = c.n_orules;
     return f;
 }
 
@@ -704,8 +733,8 @@ static int classify16_locked(cls_engine* e, std::shared_ptr<Table> t, const cls_
             zeroed = true;
             cd.zero = nullptr;
             if (timing && off + m >= n) HIPC(e, hipEventRecord(e->ev1, s));
-            if (!lin) HIPC(e, launch_other16(cd, cfg.other, fe, cd.oq, uint32_t(cfg.grid), cd.oq_cap, pc, vo, slot_val, s));
-            HIPC(e, launch_finish(finish_args(t->c16, sc, co, q.lds_resident, uint32_t(cfg.grid), off + m >= n), s));
+            HIPC(e, launch_finish16(finish_args(t->c16, sc, cd, co, q.lds_resident, uint32_t(cfg.grid), off + m >= n),
+                                    cd, cfg.other, fe, pc, vo, s));
             remapped = true;
         }
     }
@@ -795,10 +824,8 @@ int cls_classify(cls_engine* e, uint32_t table_id, const cls_pkt_soa* pk, uint64
                 zeroed = true;
                 cd.zero = nullptr;
                 if (timing && off + m >= n) HIPC(e, hipEventRecord(e->ev1, s));
-                HIPC(e, launch_other4(cfg.other, t->img.n_ctr, cd.oq, uint32_t(cfg.grid), cd.oq_cap, pc, vo, slot_val,
-                                      s));
-                HIPC(e, launch_finish(finish_args(t->c4, sc, co, t->lds_resident, uint32_t(cfg.grid), off + m >= n),
-                                      s));
+                HIPC(e, launch_finish4(finish_args(t->c4, sc, cd, co, t->lds_resident, uint32_t(cfg.grid), off + m >= n),
+                                       cfg.other, pc, vo, s));
                 remapped = true;
             }
         } else {

@@ -865,103 +865,103 @@ __global__ __launch_bounds__(kClsBlock) void stream16_kernel(Pkts16 p, uint8_t* 
     }
 }
 
-// The packets a classify launch queued for the OTHER image (protocols > 2,
-// run_n): classified here with every lane on one such packet, so the rare
-// packets cost the streaming kernel nothing but the queue append.  oq =
-// {fill of each of the launch's `rows` workgroups, then their segments of
-// cap indices}; the packets a full segment could not take were classified in
-// place.  Counts: a block histogram in LDS for tables with few OTHER slots.
-constexpr uint32_t kOtherLds = 4096;
+constexpr uint32_t kOtherLds = 4096;   // finish launch: LDS histogram of the OTHER packets' rules
+
+// One launch at the end of a classify call (kernels.hpp FinishArgs).  Blocks
+// [0, ntile): 64 slots each -- the 16 waves sum the workgroups' partial rows
+// (rows w, w + 16, ...: 256 contiguous bytes per load instruction), wave 0
+// adds the slot's global counter and moves the total to its rule (hot rules:
+// summed in LDS over the tile first, one atomic per tile).  Blocks after:
+// one OTHER queue row each (the packets one classify workgroup queued),
+// every lane on one packet, counted per rule in LDS (compact rule indices)
+// and added once per (block, rule).  No block waits for another: the OTHER
+// packets are counted straight into their rules, the tiles read only what
+// the classify launch wrote.
+constexpr uint32_t kFoldWaves = 16;
 template <typename Load>
-__device__ __forceinline__ void other_loop(const Cls4Dev& o, uint32_t slot0, const uint32_t* __restrict__ oq,
-                                           uint32_t rows, uint32_t cap, uint8_t* verdict,
-                                           unsigned long long* gslot, const Load& load) {
+__device__ __forceinline__ void finish_body(const FinishArgs& f, const Cls4Dev& o, uint8_t* verdict,
+                                            const Load& load) {
+    __shared__ unsigned long long acc[kFoldWaves][64];
+    __shared__ unsigned long long hot[kMaxHotRules];
     __shared__ uint32_t h[kOtherLds];
-    const bool lds = o.n_ctr <= kOtherLds;
+    const uint32_t span = f.remap ? f.n_slots : (f.part ? f.n_lctr : 0u);
+    const uint32_t ntile = (span + 63u) / 64u;
+    if (blockIdx.x < ntile) {
+        const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+        const uint32_t i = blockIdx.x * 64u + lane;
+        if (threadIdx.x < f.n_hot) hot[threadIdx.x] = 0ull;
+        unsigned long long s64 = 0;
+        if (f.part && i < f.n_lctr) {
+            const uint32_t n = f.n_lctr, rows = f.rows;
+            const uint32_t* part = f.part;
+            uint32_t w = wave;
+            for (; w + 3u * kFoldWaves < rows; w += 4u * kFoldWaves) {
+                const uint32_t a = part[size_t(w) * n + i], b = part[size_t(w + kFoldWaves) * n + i];
+                const uint32_t c = part[size_t(w + 2u * kFoldWaves) * n + i];
+                const uint32_t d = part[size_t(w + 3u * kFoldWaves) * n + i];
+                s64 += (unsigned long long)a + b + c + d;
+            }
+            for (; w < rows; w += kFoldWaves) s64 += part[size_t(w) * n + i];
+        }
+        acc[wave][lane] = s64;
+        __syncthreads();
+        if (wave == 0 && i < span) {
+#pragma unroll
+            for (uint32_t k = 1; k < kFoldWaves; ++k) s64 += acc[k][lane];
+            if (f.remap) {
+                const unsigned long long sv = f.slot_val[i];
+                if (sv) f.slot_val[i] = 0ull;
+                s64 += sv;
+                if (s64) {
+                    const uint32_t e = f.slot_rule[i];
+                    if (e & kHotRule) atomicAdd(&hot[e & ~kHotRule], s64);
+                    else atomicAdd(&f.out[e], s64);
+                }
+            } else if (s64) {
+                f.slot_val[i] += s64;            // an earlier chunk: this launch is the only writer
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x < f.n_hot && hot[threadIdx.x])
+            atomicAdd(&f.out[f.slot_rule[f.n_slots + threadIdx.x]], hot[threadIdx.x]);
+        return;
+    }
+    const uint32_t r = blockIdx.x - ntile;
+    if (!f.oq || r >= f.oq_rows) return;
+    const uint32_t n = f.oq[r];
+    if (n == 0) return;                          // the usual case: no OTHER packet in this row
+    const bool lds = f.n_orules <= kOtherLds;
     if (lds) {
-        for (uint32_t i = threadIdx.x; i < o.n_ctr; i += blockDim.x) h[i] = 0u;
+        for (uint32_t i = threadIdx.x; i < f.n_orules; i += blockDim.x) h[i] = 0u;
         __syncthreads();
     }
     const Img<false> oim{reinterpret_cast<const uint8_t*>(o.img)};
-    for (uint32_t r = blockIdx.x; r < rows; r += gridDim.x) {
-        const uint32_t n = oq[r];
-        for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
-            const uint32_t k = oq[rows + r * cap + i];
-            uint32_t s1[1], d1[1], p1[1];
-            load(k, s1[0], d1[0], p1[0]);
-            const uint32_t z1[1] = {0u};
-            uint32_t r1[1], k1[1];
-            classify_n<1, false, 0, 0, -1>(oim, o, s1, d1, p1, z1, r1, k1);
-            if (verdict) verdict[k] = uint8_t(r1[0]);
-            if (lds) atomicAdd(&h[k1[0]], 1u);
-            else wave_count(gslot, slot0 + k1[0]);
-        }
+    const uint32_t* orule = f.other_map + f.n_other;
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+        const uint32_t k = f.oq[f.oq_rows + r * f.oq_cap + i];
+        uint32_t s1[1], d1[1], p1[1];
+        load(k, s1[0], d1[0], p1[0]);
+        const uint32_t z1[1] = {0u};
+        uint32_t r1[1], k1[1];
+        classify_n<1, false, 0, 0, -1>(oim, o, s1, d1, p1, z1, r1, k1);
+        if (verdict) verdict[k] = uint8_t(r1[0]);
+        const uint32_t c = f.other_map[k1[0]];
+        if (lds) atomicAdd(&h[c], 1u);
+        else wave_count(f.out, orule[c]);
     }
     if (lds) {
         __syncthreads();
-        for (uint32_t i = threadIdx.x; i < o.n_ctr; i += blockDim.x)
-            if (h[i]) atomicAdd(&gslot[slot0 + i], (unsigned long long)h[i]);
+        for (uint32_t i = threadIdx.x; i < f.n_orules; i += blockDim.x)
+            if (h[i]) atomicAdd(&f.out[orule[i]], (unsigned long long)h[i]);
     }
 }
 
-__global__ __launch_bounds__(256) void other4_kernel(Cls4Dev o, uint32_t n_main, const uint32_t* __restrict__ oq,
-                                                     uint32_t rows, uint32_t cap, Pkts4 p, uint8_t* verdict,
-                                                     unsigned long long* gslot) {
-    other_loop(o, n_main, oq, rows, cap, verdict, gslot, [&](uint32_t k, uint32_t& s, uint32_t& d, uint32_t& dp) {
+__global__ __launch_bounds__(1024) void finish4_kernel(FinishArgs f, Cls4Dev o, Pkts4 p, uint8_t* verdict) {
+    finish_body(f, o, verdict, [&](uint32_t k, uint32_t& s, uint32_t& d, uint32_t& dp) {
         s = p.src[k];
         d = p.dst[k];
         dp = p.dport[k];
     });
-}
-
-// One launch at the end of a classify call (kernels.hpp FinishArgs): tiles
-// of 64 slots -- the 16 waves sum the workgroups' partial rows (rows w,
-// w + 16, ...: 256 contiguous bytes per load instruction), wave 0 adds the
-// slot's global counter and moves the total to its rule (hot rules: summed
-// in LDS over the tile first, one atomic per tile).  The tiles read only what
-// the classify launch wrote, so no tile waits for another.
-constexpr uint32_t kFoldWaves = 16;
-__global__ __launch_bounds__(1024) void finish_kernel(FinishArgs f) {
-    __shared__ unsigned long long acc[kFoldWaves][64];
-    __shared__ unsigned long long hot[kMaxHotRules];
-    const uint32_t span = f.remap ? f.n_slots : (f.part ? f.n_lctr : 0u);
-    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-    const uint32_t i = blockIdx.x * 64u + lane;
-    if (threadIdx.x < f.n_hot) hot[threadIdx.x] = 0ull;
-    unsigned long long s64 = 0;
-    if (f.part && i < f.n_lctr) {
-        const uint32_t n = f.n_lctr, rows = f.rows;
-        const uint32_t* part = f.part;
-        uint32_t w = wave;
-        for (; w + 3u * kFoldWaves < rows; w += 4u * kFoldWaves) {
-            const uint32_t a = part[size_t(w) * n + i], b = part[size_t(w + kFoldWaves) * n + i];
-            const uint32_t c = part[size_t(w + 2u * kFoldWaves) * n + i];
-            const uint32_t d = part[size_t(w + 3u * kFoldWaves) * n + i];
-            s64 += (unsigned long long)a + b + c + d;
-        }
-        for (; w < rows; w += kFoldWaves) s64 += part[size_t(w) * n + i];
-    }
-    acc[wave][lane] = s64;
-    __syncthreads();
-    if (wave == 0 && i < span) {
-#pragma unroll
-        for (uint32_t k = 1; k < kFoldWaves; ++k) s64 += acc[k][lane];
-        if (f.remap) {
-            const unsigned long long sv = f.slot_val[i];
-            if (sv) f.slot_val[i] = 0ull;
-            s64 += sv;
-            if (s64) {
-                const uint32_t e = f.slot_rule[i];
-                if (e & kHotRule) atomicAdd(&hot[e & ~kHotRule], s64);
-                else atomicAdd(&f.out[e], s64);
-            }
-        } else if (s64) {
-            f.slot_val[i] += s64;            // an earlier chunk: this launch is the only writer
-        }
-    }
-    __syncthreads();
-    if (threadIdx.x < f.n_hot && hot[threadIdx.x])
-        atomicAdd(&f.out[f.slot_rule[f.n_slots + threadIdx.x]], hot[threadIdx.x]);
 }
 
 // ---------------------------------------------------------------------------
@@ -1223,13 +1223,12 @@ __global__ __launch_bounds__(kClsBlock) void classify16_cls(Cls4Dev t, Cls4Dev o
     queue_end(t, oq_lds);
 }
 
-// other4_kernel for 16-byte batches: the reps from the front end in global
-// memory (the image's copy; src_mode 1: the source interval table).
-__global__ __launch_bounds__(256) void other16_kernel(Cls4Dev t, Cls4Dev o, Fe16 fe, const uint32_t* __restrict__ oq,
-                                                      uint32_t rows, uint32_t cap, Pkts16 p, uint8_t* verdict,
-                                                      unsigned long long* gslot) {
+// finish for 16-byte batches: the OTHER packets' reps from the front end in
+// global memory (the image's copy; src_mode 1: the source interval table).
+__global__ __launch_bounds__(1024) void finish16_kernel(FinishArgs f, Cls4Dev t, Cls4Dev o, Fe16 fe, Pkts16 p,
+                                                       uint8_t* verdict) {
     const Img<false> gim{reinterpret_cast<const uint8_t*>(t.img)};
-    other_loop(o, t.n_ctr, oq, rows, cap, verdict, gslot, [&](uint32_t k, uint32_t& s, uint32_t& d, uint32_t& dp) {
+    finish_body(f, o, verdict, [&](uint32_t k, uint32_t& s, uint32_t& d, uint32_t& dp) {
         const uint4 s16[1] = {p.src[k]}, d16[1] = {p.dst[k]};
         uint32_t s1[1], d1[1];
         if (fe.src_mode == 1) s1[0] = src_rep_global(fe.gsrc, fe.gval, fe.top[0], fe.k8[0], s16[0]);
@@ -1899,23 +1898,23 @@ hipError_t launch_remap(unsigned long long* slot_val, const uint2* csr, uint32_t
     return hipGetLastError();
 }
 
-hipError_t launch_finish(const FinishArgs& f, hipStream_t s) {
+static uint32_t finish_grid(const FinishArgs& f) {
     const uint32_t span = f.remap ? f.n_slots : (f.part ? f.n_lctr : 0u);
-    const uint32_t g = (span + 63u) / 64u;
+    return (span + 63u) / 64u + (f.oq ? f.oq_rows : 0u);
+}
+
+hipError_t launch_finish4(const FinishArgs& f, const Cls4Dev& o, const Pkts4& p, uint8_t* verdict, hipStream_t s) {
+    const uint32_t g = finish_grid(f);
     if (g == 0) return hipSuccess;
-    hipLaunchKernelGGL(finish_kernel, dim3(g), dim3(1024), 0, s, f);
+    hipLaunchKernelGGL(finish4_kernel, dim3(g), dim3(1024), 0, s, f, o, p, verdict);
     return hipGetLastError();
 }
 
-hipError_t launch_other4(const Cls4Dev& o, uint32_t n_main, const uint32_t* oq, uint32_t rows, uint32_t cap,
-                         const Pkts4& p, uint8_t* verdict, unsigned long long* gslot, hipStream_t s) {
-    hipLaunchKernelGGL(other4_kernel, dim3(rows), dim3(256), 0, s, o, n_main, oq, rows, cap, p, verdict, gslot);
-    return hipGetLastError();
-}
-
-hipError_t launch_other16(const Cls4Dev& t, const Cls4Dev& o, const Fe16& fe, const uint32_t* oq, uint32_t rows,
-                          uint32_t cap, const Pkts16& p, uint8_t* verdict, unsigned long long* gslot, hipStream_t s) {
-    hipLaunchKernelGGL(other16_kernel, dim3(rows), dim3(256), 0, s, t, o, fe, oq, rows, cap, p, verdict, gslot);
+hipError_t launch_finish16(const FinishArgs& f, const Cls4Dev& t, const Cls4Dev& o, const Fe16& fe, const Pkts16& p,
+                           uint8_t* verdict, hipStream_t s) {
+    const uint32_t g = finish_grid(f);
+    if (g == 0) return hipSuccess;
+    hipLaunchKernelGGL(finish16_kernel, dim3(g), dim3(1024), 0, s, f, t, o, fe, p, verdict);
     return hipGetLastError();
 }
 

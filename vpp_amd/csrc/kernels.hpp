@@ -100,13 +100,6 @@ hipError_t launch_fold(const uint32_t* part, uint32_t rows, uint32_t n, unsigned
 // (csr: every slot once, grouped by rule); out null: clear only
 hipError_t launch_remap(unsigned long long* slot_val, const uint2* csr, uint32_t n, unsigned long long* out,
                         hipStream_t s);
-// the packets a classify launch of `rows` workgroups queued for the OTHER
-// image (oq = {fill per workgroup, then rows segments of cap indices}):
-// verdicts and counts (slots n_main + OTHER slot)
-hipError_t launch_other4(const Cls4Dev& o, uint32_t n_main, const uint32_t* oq, uint32_t rows, uint32_t cap,
-                         const Pkts4& p, uint8_t* verdict, unsigned long long* gslot, hipStream_t s);
-hipError_t launch_other16(const Cls4Dev& t, const Cls4Dev& o, const Fe16& fe, const uint32_t* oq, uint32_t rows,
-                          uint32_t cap, const Pkts16& p, uint8_t* verdict, unsigned long long* gslot, hipStream_t s);
 // The end of a classify call, one launch: tiles of 64 slots fold the
 // workgroups' LDS partials (part, rows x n_lctr; null: none) and, with
 // remap, move slot_val + partials to the rule counters out (slot -> rule:
@@ -125,8 +118,19 @@ struct FinishArgs {
     uint32_t n_hot;
     unsigned long long* out;
     bool remap;
+    // the OTHER queue of the classify launch (rows = its workgroups; null:
+    // none): blocks after the tiles classify the queued packets (protocols
+    // > 2) on the OTHER image and count them per rule -- other_map: compact
+    // rule index of each of the n_other OTHER slots, then the n_orules rules
+    const uint32_t* oq;
+    uint32_t oq_rows, oq_cap;
+    const uint32_t* other_map;
+    uint32_t n_other, n_orules;
 };
-hipError_t launch_finish(const FinishArgs& f, hipStream_t s);
+// finish4 / finish16: the OTHER packets' loads from the 4- / 16-byte batch
+hipError_t launch_finish4(const FinishArgs& f, const Cls4Dev& o, const Pkts4& p, uint8_t* verdict, hipStream_t s);
+hipError_t launch_finish16(const FinishArgs& f, const Cls4Dev& t, const Cls4Dev& o, const Fe16& fe, const Pkts16& p,
+                           uint8_t* verdict, hipStream_t s);
 // the classify kernels' packet stream without the lookups (stream floor);
 // exactly one of p4 / p16; p4 needs 16-B aligned src/dst, 8-B dport, 4-B
 // proto and verdict (variant bit 0: load and use instead of the next step's
