@@ -8,5 +8,6 @@ for f in sys.argv[1:]:
     print("==", f)
     for r in csv.DictReader(open(f)):
         n = r["Name"]
-        short = n.split("(")[0].split("::")[-1]
-        print("  %-40s calls %4s avg %9.1f us" % (short[:40], r["Calls"], float(r["AverageNs"]) / 1e3))
+        short = n[:n.index("(cls::")] if "(cls::" in n else n
+        short = short.replace("void ", "").replace("cls::(anonymous namespace)::", "")
+        print("  %-60s calls %4s avg %9.1f us" % (short[:60], r["Calls"], float(r["AverageNs"]) / 1e3))

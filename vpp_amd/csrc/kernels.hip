@@ -694,7 +694,12 @@ __global__ __launch_bounds__(kClsBlock) void classify4_cls(Cls4Dev t, Cls4Dev o,
             for (int k = 0; k < kN; ++k) ix[k] = 4u * (g + uint32_t(k / 4) * nthreads) + uint32_t(k % 4);
             run_n<kN, kLds, kMode, kList, kD, kCtr>(im, t, o, hot_lane, gslot, hot0, sa, da, pa, ra, other, v, sa, ix,
                                                     oq_lds);
-            if (verdict) {
+            if constexpr (kCtr == 2) {                           // slot mode: 4 result words per lane
+#pragma unroll
+                for (int k = 0; k < kG; ++k)
+                    reinterpret_cast<uint4*>(verdict)[g + uint32_t(k) * nthreads] =
+                        make_uint4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
+            } else if (verdict) {
 #pragma unroll
                 for (int k = 0; k < kG; ++k)
                     stnt(v[4 * k] | (v[4 * k + 1] << 8) | (v[4 * k + 2] << 16) | (v[4 * k + 3] << 24),
@@ -759,7 +764,9 @@ __global__ __launch_bounds__(kClsBlock) void classify4_cls(Cls4Dev t, Cls4Dev o,
             run_n<4, kLds, kMode, kList, -1, kCtr>(im, t, o, hot_lane, gslot, hot0, sa, da, pa, ra,
                                                    ((pr | ((pr & 0x7F7F7F7Fu) + 0x7D7D7D7Du)) & 0x80808080u) != 0u,
                                                    v, sa, ix, oq_lds);
-            if (verdict)
+            if constexpr (kCtr == 2)
+                reinterpret_cast<uint4*>(verdict)[gi] = make_uint4(v[0], v[1], v[2], v[3]);
+            else if (verdict)
                 stnt(v[0] | (v[1] << 8) | (v[2] << 16) | (v[3] << 24),
                      const_cast<uint32_t*>(at(reinterpret_cast<const uint32_t*>(verdict), gi)));
         }
@@ -1808,11 +1815,31 @@ hipError_t launch_classify16_cls(const Cls4Dev& t, const Fe16& fe, const Pkts16&
     return hipGetLastError();
 }
 
-// Slot mode: one packet per lane (kVec false), run-time search depth.
+// Slot mode, run-time search depth: 4 packets per lane (vector loads, one
+// 16-B result store) for an LDS-resident image on aligned arrays, else one
+// packet per lane.
 template <bool kLds>
 static void dispatch_slots4(const Cls4Dev& t, const Pkts4& p, uint32_t* out, const LaunchCfg& cfg) {
     uint8_t* o = reinterpret_cast<uint8_t*>(out);
     const int src = t.mode != 1 ? 0 : t.n_hash == 1 ? 2 : 1;
+    if constexpr (kLds) {
+        auto al = [](const void* q, uintptr_t a) { return (reinterpret_cast<uintptr_t>(q) & (a - 1)) == 0; };
+        if (al(p.src, 16) && al(p.dst, 16) && al(p.dport, 8) && al(p.proto, 4) && al(out, 16)) {
+#define CLS_SLOTV_CASES(L)                                                                         \
+    case 3 * L + 0: launch_d<true, true, 0, L, -1, 2>(t, p, o, nullptr, cfg); return;              \
+    case 3 * L + 1: launch_d<true, true, 1, L, -1, 2>(t, p, o, nullptr, cfg); return;              \
+    case 3 * L + 2: launch_d<true, true, 2, L, -1, 2>(t, p, o, nullptr, cfg); return;
+            switch (src + 3 * int(t.list_mode)) {
+                CLS_SLOTV_CASES(0)
+                CLS_SLOTV_CASES(1)
+                CLS_SLOTV_CASES(2)
+                CLS_SLOTV_CASES(3)
+                CLS_SLOTV_CASES(4)
+            default: break;
+            }
+#undef CLS_SLOTV_CASES
+        }
+    }
 #define CLS_SLOT_CASES(L)                                                                          \
     case 3 * L + 0: launch_d<kLds, false, 0, L, -1, 2>(t, p, o, nullptr, cfg); break;              \
     case 3 * L + 1: launch_d<kLds, false, 1, L, -1, 2>(t, p, o, nullptr, cfg); break;              \
