@@ -640,10 +640,19 @@ class _LocalCtx:
         pods = sorted(txn.get_all_pods(), key=tuple)
         self.src = []                  # (ip16, pod_ip, id of its opposite-side rule list)
         self.ok = True
-        self._lists = {}
-        self._pcache = {}
-        self._pint = {}
-        self._built = {}
+        # Content caches, kept by the renderer cache across refreshes (a txn
+        # rebuilds every local table, cache_impl.go:420-474, but the rule
+        # lists, addresses and allowed-port sets mostly repeat): list content
+        # -> id, (fn, list id, address) -> port sets, one object per
+        # port-set content, table signature -> table.
+        memo = getattr(txn.cache, "_local_memo", None)
+        if memo is None or len(memo["pcache"]) > 4_000_000 or memo["egress"] != self.egress:
+            memo = txn.cache._local_memo = {"egress": self.egress, "lists": {}, "pcache": {}, "pint": {},
+                                            "built": {}}
+        self._lists = memo["lists"]
+        self._pcache = memo["pcache"]
+        self._pint = memo["pint"]
+        self._built = memo["built"]
         seen = set()
         for pod in pods:
             cfg = txn.get_pod_config(pod)
@@ -657,6 +666,15 @@ class _LocalCtx:
                 self.ok = False
                 return
             self.src.append((ip16, cfg.pod_ip, lid, cfg.ingress if self.egress else cfg.egress))
+        # sources grouped by rule list: a destination's allowed-port sets are
+        # computed once per distinct list, not once per source pod
+        firsts = {}
+        for k, (_, _, lid, rules) in enumerate(self.src):
+            firsts.setdefault(lid, (len(firsts), rules))
+        self.lids = [(lid, rules) for lid, (_, rules) in sorted(firsts.items(), key=lambda kv: kv[1][0])]
+        self.src_slot = [firsts[lid][0] for _, _, lid, _ in self.src]
+        sets = memo.setdefault("srcsets", {})
+        self.srcset = sets.setdefault(tuple((ip16, lid) for ip16, _, lid, _ in self.src), len(sets))
 
     @staticmethod
     def _host16(net):
@@ -697,11 +715,15 @@ class _LocalCtx:
         # list and the source pods' allowed ports towards it: equal
         # signatures, equal tables (built once per refresh).
         sfn = get_allowed_ingress_ports if egress else get_allowed_egress_ports
-        sp_all = [self._ports(sfn, lid, rules, dst_cfg.pod_ip, dst16) for _, _, lid, rules in self.src]
-        sig = (own_lid, tuple(map(id, sp_all)))
+        sp_lid = [self._ports(sfn, lid, rules, dst_cfg.pod_ip, dst16) for lid, rules in self.lids]
+        # The table depends on the destination only through its own list and
+        # the allowed-port sets; the source pods (addresses and lists) are
+        # named by the refresh's interned source set.
+        sig = (own_lid, self.srcset, tuple(map(id, sp_lid)))
         hit = self._built.get(sig)
         if hit is not None:
             return self._keyed(*hit)
+        sp_all = [sp_lid[k] for k in self.src_slot]
         base = [r.copy() for r in own]
         # base rules a pod's installAllowedPorts would remove: (protocol, host ip16)
         removable = {}
