@@ -82,7 +82,7 @@ def _run(seed, orientation, keyed, monkeypatch):
     cache.init(orientation)
     out = []
     live = set()
-    for step in range(5):
+    for step in range(10):   # refreshes share the renderer cache's content caches
         txn = cache.new_txn()
         for p in rng.sample(pods, rng.randrange(1, 12) if step else len(pods)):
             if p in live and rng.random() < 0.15:
