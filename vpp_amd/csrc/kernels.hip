@@ -413,6 +413,20 @@ __device__ __forceinline__ void wave_count(unsigned long long* gslot, uint32_t k
     }
 }
 
+// Global slot counters of the cold tier (slots past the LDS counters):
+// spread keys, so one aggregation round for the leader's key (a popular slot
+// costs one atomic) and direct atomics for the rest, instead of one ballot
+// round per distinct key.
+__device__ __forceinline__ void wave_count_cold(unsigned long long* gslot, uint32_t key) {
+    const unsigned long long pending = __ballot(key != 0xFFFFFFFFu);
+    if (!pending) return;
+    const int leader = __builtin_ctzll(pending);
+    const uint32_t sk = __shfl(key, leader);
+    const unsigned long long same = __ballot(key == sk);
+    if (int(__lane_id()) == leader) atomicAdd(&gslot[sk], (unsigned long long)__popcll(same));
+    else if (key != 0xFFFFFFFFu && key != sk) atomicAdd(&gslot[key], 1ull);
+}
+
 // Classify N packets and count their slots.  kCtr (LDS-resident image): 0 --
 // every slot has a u32 LDS counter; 1 -- u16 LDS counters for slots <
 // n_lctr (compile.hpp Cls4Image counter tiers), global counters above.
@@ -485,7 +499,7 @@ __device__ __forceinline__ void run_n(const Img<kLds>& im, const Cls4Dev& t, con
                     key = slot[q];
                 }
             }
-            wave_count(gslot, key);
+            wave_count_cold(gslot, key);
         } else {
             // Global counters (image not LDS-resident); slot 0 (default DENY,
             // the hottest) is counted per lane and added once at the end
