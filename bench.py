@@ -229,7 +229,11 @@ def main():
     ar_ms = float(np.mean([a.elapsed_time(b) for a, b in ev])) if ev else 0.0
     floor_ms = None
     if not args.no_stream_floor:
-        floor_ms = eng.stream_floor(pk["src"], pk["dst"], pk["dport"], pk["proto"], verdict)
+        # one launch covers at most 2^30 packets (the kernels' 32-bit offsets):
+        # time the floor on that prefix and scale to the batch
+        m = min(n, 1 << 30)
+        floor_ms = eng.stream_floor(pk["src"][:m], pk["dst"][:m], pk["dport"][:m], pk["proto"][:m],
+                                    verdict[:m]) * (n / m)
     wall, k_max, ar_max = D.max_over_ranks([wall, avg_k, ar_ms], dev)
     if floor_ms is not None:
         floor_ms = D.max_over_ranks(floor_ms, dev)
