@@ -324,32 +324,51 @@ def _dump_rule(ar: model.Rule) -> Optional[ContivRule]:
     return rule
 
 
+# Rendered rules by their exact rendering inputs: a txn re-renders whole
+# tables (the global one has ~10k rules at 1000 pods) of which few rules
+# changed.  The engines treat ACL rule messages as immutable, so equal rules
+# share one message.
+_rendered = {}
+
+
 def render_acl(table: ContivRuleTable, interfaces: model.Interfaces) -> model.Acl:
     """renderACL (acl_renderer.go:312-402)."""
     acl = model.Acl(acl_name=ACL_NAME_PREFIX + table.id, interfaces=interfaces)
     reflective = table.id == REFLECTIVE_ACL_NAME
+    if len(_rendered) > 1_000_000:
+        _rendered.clear()
     for rule in table.rules:
-        if rule.action == ACTION_DENY:
-            action = model.DENY
-        elif reflective:
-            action = model.REFLECT
-        else:
-            action = model.PERMIT
-        ip = model.Ip()
-        if len(rule.src_network.ip) > 0:
-            ip.source_network = rule.src_network.string()
-        if len(rule.dest_network.ip) > 0:
-            ip.destination_network = rule.dest_network.string()
-        srange = model.PortRange(rule.src_port, MAX_PORT if rule.src_port == 0 else rule.src_port)
-        drange = model.PortRange(rule.dest_port, MAX_PORT if rule.dest_port == 0 else rule.dest_port)
-        iprule = model.IpRule(ip=ip)
-        if rule.protocol == TCP:
-            iprule.tcp = model.Tcp(destination_port_range=drange, source_port_range=srange)
-        else:
-            iprule.udp = model.Udp(destination_port_range=drange, source_port_range=srange)
-        acl.rules.append(model.Rule(actions=model.Actions(action),
-                                    matches=model.Matches(ip_rule=iprule)))
+        k = (rule.action, reflective, bytes(rule.src_network.ip), bytes(rule.src_network.mask),
+             bytes(rule.dest_network.ip), bytes(rule.dest_network.mask), rule.protocol, rule.src_port,
+             rule.dest_port)
+        r = _rendered.get(k)
+        if r is None:
+            r = _rendered[k] = _render_rule(rule, reflective)
+        acl.rules.append(r)
     if table.num_of_rules > 0:
         acl.rules.append(model.icmp_rule(model.REFLECT if reflective else model.PERMIT))
     table.private = acl
     return acl
+
+
+def _render_rule(rule, reflective: bool) -> model.Rule:
+    """One ContivRule as an ACL rule (acl_renderer.go:324-375)."""
+    if rule.action == ACTION_DENY:
+        action = model.DENY
+    elif reflective:
+        action = model.REFLECT
+    else:
+        action = model.PERMIT
+    ip = model.Ip()
+    if len(rule.src_network.ip) > 0:
+        ip.source_network = rule.src_network.string()
+    if len(rule.dest_network.ip) > 0:
+        ip.destination_network = rule.dest_network.string()
+    srange = model.PortRange(rule.src_port, MAX_PORT if rule.src_port == 0 else rule.src_port)
+    drange = model.PortRange(rule.dest_port, MAX_PORT if rule.dest_port == 0 else rule.dest_port)
+    iprule = model.IpRule(ip=ip)
+    if rule.protocol == TCP:
+        iprule.tcp = model.Tcp(destination_port_range=drange, source_port_range=srange)
+    else:
+        iprule.udp = model.Udp(destination_port_range=drange, source_port_range=srange)
+    return model.Rule(actions=model.Actions(action), matches=model.Matches(ip_rule=iprule))
