@@ -9,7 +9,7 @@ sub-message: evalACL's semantics depend on nil-ness
 from __future__ import annotations
 
 import copy
-from dataclasses import dataclass, field
+from dataclasses import dataclass, field, fields
 from typing import List, Optional
 
 # vpp_acl.AclAction (acl.proto:4-8)
@@ -122,6 +122,51 @@ class Acl:
         and the interfaces (which the renderer rewrites) are copies."""
         return Acl(rules=list(self.rules), acl_name=self.acl_name,
                    interfaces=copy.deepcopy(self.interfaces))
+
+
+class FrozenMessageError(AttributeError):
+    """An attempt to edit a read-only (shared) rule message."""
+
+
+def _sealed_class(base):
+    """A read-only variant of a message class: same fields, isinstance of
+    ``base``, equal to a ``base`` message with equal fields; setting a field
+    raises FrozenMessageError; ``copy.deepcopy`` returns a mutable ``base``
+    copy (like proto.Clone)."""
+    names = [f.name for f in fields(base)]
+
+    def __setattr__(self, k, v):
+        raise FrozenMessageError("%s is a shared rendered message; deepcopy it to edit" % base.__name__)
+
+    def __delattr__(self, k):
+        raise FrozenMessageError("%s is a shared rendered message" % base.__name__)
+
+    def __eq__(self, other):
+        if not isinstance(other, base):
+            return NotImplemented
+        return all(getattr(self, n) == getattr(other, n) for n in names)
+
+    def __deepcopy__(self, memo):
+        return base(**{n: copy.deepcopy(getattr(self, n), memo) for n in names})
+
+    return type("Frozen" + base.__name__, (base,),
+                dict(__setattr__=__setattr__, __delattr__=__delattr__, __eq__=__eq__, __hash__=None,
+                     __deepcopy__=__deepcopy__))
+
+
+_FROZEN = {c: _sealed_class(c) for c in (PortRange, Tcp, Udp, IcmpRange, Icmp, Ip, IpRule, Matches, Actions,
+                                         Rule)}
+
+
+def frozen(cls, **values):
+    """A read-only ``cls`` message (cls one of the rule message classes).
+    Rendered rules are shared between ACLs (renderer/acl.py memo), so they
+    are built read-only: nobody can edit one ACL's rule and thereby another's."""
+    o = object.__new__(_FROZEN[cls])
+    d = o.__dict__
+    for f in fields(cls):
+        d[f.name] = values.get(f.name, f.default)
+    return o
 
 
 MAX_PORT = 0xFFFF

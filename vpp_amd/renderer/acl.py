@@ -326,8 +326,12 @@ def _dump_rule(ar: model.Rule) -> Optional[ContivRule]:
 
 # Rendered rules by their exact rendering inputs: a txn re-renders whole
 # tables (the global one has ~10k rules at 1000 pods) of which few rules
-# changed.  The engines treat ACL rule messages as immutable, so equal rules
-# share one message.
+# changed, so equal rules share one message.  Shared messages are read-only
+# (model.frozen): a caller that edits a rendered or dumped ACL's rule gets
+# FrozenMessageError instead of silently rewriting every ACL that shares it,
+# and copy.deepcopy gives an editable copy.  (Go's renderACL allocates fresh
+# messages per call, acl_renderer.go:324; building 10k fresh messages per
+# render costs ~20x the memoised render here.)
 _rendered = {}
 
 
@@ -337,38 +341,46 @@ def render_acl(table: ContivRuleTable, interfaces: model.Interfaces) -> model.Ac
     reflective = table.id == REFLECTIVE_ACL_NAME
     if len(_rendered) > 1_000_000:
         _rendered.clear()
+    out = acl.rules
     for rule in table.rules:
         k = (rule.action, reflective, bytes(rule.src_network.ip), bytes(rule.src_network.mask),
              bytes(rule.dest_network.ip), bytes(rule.dest_network.mask), rule.protocol, rule.src_port,
              rule.dest_port)
         r = _rendered.get(k)
         if r is None:
-            r = _rendered[k] = _render_rule(rule, reflective)
-        acl.rules.append(r)
+            r = _rendered[k] = _build_rule(_recipe(rule, reflective))
+        out.append(r)
     if table.num_of_rules > 0:
-        acl.rules.append(model.icmp_rule(model.REFLECT if reflective else model.PERMIT))
+        out.append(model.icmp_rule(model.REFLECT if reflective else model.PERMIT))
     table.private = acl
     return acl
 
 
-def _render_rule(rule, reflective: bool) -> model.Rule:
-    """One ContivRule as an ACL rule (acl_renderer.go:324-375)."""
+def _recipe(rule, reflective: bool) -> tuple:
+    """What one ContivRule renders to (acl_renderer.go:324-375), as a tuple:
+    (action, src network string, dst network string, is TCP, src lo, src hi,
+    dst lo, dst hi)."""
     if rule.action == ACTION_DENY:
         action = model.DENY
     elif reflective:
         action = model.REFLECT
     else:
         action = model.PERMIT
-    ip = model.Ip()
-    if len(rule.src_network.ip) > 0:
-        ip.source_network = rule.src_network.string()
-    if len(rule.dest_network.ip) > 0:
-        ip.destination_network = rule.dest_network.string()
-    srange = model.PortRange(rule.src_port, MAX_PORT if rule.src_port == 0 else rule.src_port)
-    drange = model.PortRange(rule.dest_port, MAX_PORT if rule.dest_port == 0 else rule.dest_port)
-    iprule = model.IpRule(ip=ip)
-    if rule.protocol == TCP:
-        iprule.tcp = model.Tcp(destination_port_range=drange, source_port_range=srange)
-    else:
-        iprule.udp = model.Udp(destination_port_range=drange, source_port_range=srange)
-    return model.Rule(actions=model.Actions(action), matches=model.Matches(ip_rule=iprule))
+    src = rule.src_network.string() if len(rule.src_network.ip) > 0 else ""
+    dst = rule.dest_network.string() if len(rule.dest_network.ip) > 0 else ""
+    return (action, src, dst, rule.protocol == TCP,
+            rule.src_port, MAX_PORT if rule.src_port == 0 else rule.src_port,
+            rule.dest_port, MAX_PORT if rule.dest_port == 0 else rule.dest_port)
+
+
+def _build_rule(rec: tuple) -> model.Rule:
+    """A read-only rule message from a recipe: TCP rules get a Tcp section,
+    every other protocol a Udp section (acl_renderer.go:342-374)."""
+    action, src, dst, tcp, slo, shi, dlo, dhi = rec
+    F = model.frozen
+    sec = F(model.Tcp if tcp else model.Udp,
+            destination_port_range=F(model.PortRange, lower_port=dlo, upper_port=dhi),
+            source_port_range=F(model.PortRange, lower_port=slo, upper_port=shi))
+    ip = F(model.Ip, destination_network=dst, source_network=src)
+    iprule = F(model.IpRule, ip=ip, tcp=sec) if tcp else F(model.IpRule, ip=ip, udp=sec)
+    return F(model.Rule, actions=F(model.Actions, acl_action=action), matches=F(model.Matches, ip_rule=iprule))

@@ -22,6 +22,7 @@ splitmix64 generator (DESIGN.md "Traffic").
 """
 from __future__ import annotations
 
+import copy
 import random
 
 import numpy as np
@@ -139,13 +140,18 @@ def render_global(n_pods: int, rules_per_pod: int, n_apps: int, seed: int, mixed
 
 def _widen_and_pools(acl, table, pods):
     """Config 5: dst port ranges in the ACL form, and the 16-byte pools."""
-    for r in acl.rules:
+    # rendered rules are shared read-only messages: widen editable copies
+    for i, r in enumerate(acl.rules):
         ipr = r.matches.ip_rule if r.matches is not None else None
         for sec in (ipr.tcp, ipr.udp) if ipr is not None else ():
             if sec is not None and sec.destination_port_range is not None:
                 pr = sec.destination_port_range
                 if pr.lower_port == pr.upper_port and pr.lower_port != 0:
+                    r = acl.rules[i] = copy.deepcopy(r)
+                    ipr = r.matches.ip_rule
+                    pr = (ipr.tcp or ipr.udp).destination_port_range
                     pr.lower_port, pr.upper_port = port_range_of(pr.lower_port)
+                    break
 
     def b16(net) -> bytes:
         ip = bytes(net.ip)
