@@ -13,7 +13,9 @@
 //
 // Ownership (cgo rule): every pointer handed to the C ABI is valid only for
 // the duration of the call; the engine deep-copies rules and keeps no caller
-// pointer.
+// pointer.  The packet / connection SoA structs are Go values that hold Go
+// slice addresses, so those slices are pinned (runtime.Pinner, Go >= 1.21)
+// for the call; rule records hold only C strings (C.CString).
 package contivcls
 
 /*
@@ -27,6 +29,7 @@ import "C"
 import (
 	"errors"
 	"net"
+	"runtime"
 	"strings"
 	"sync"
 	"unsafe"
@@ -466,6 +469,11 @@ func (en *Engine) ConnectionBatch(calls []Conn, count bool) ([]aclengine.Connect
 	if n == 0 {
 		return out, nil
 	}
+	// cs is Go memory holding pointers to Go memory: cgo allows that only
+	// for pinned memory, for the length of the call (runtime.Pinner).
+	var pin runtime.Pinner
+	defer pin.Unpin()
+	pinAll(&pin, &sif[0], &dif[0], &sport[0], &dport[0], &proto[0])
 	var cs C.cls_conn_soa
 	cs.src_if, cs.dst_if = (*C.uint32_t)(&sif[0]), (*C.uint32_t)(&dif[0])
 	cs.pkt.sport, cs.pkt.dport = (*C.uint16_t)(&sport[0]), (*C.uint16_t)(&dport[0])
@@ -477,6 +485,7 @@ func (en *Engine) ConnectionBatch(calls []Conn, count bool) ([]aclengine.Connect
 			s4[k] = uint32(a[0])<<24 | uint32(a[1])<<16 | uint32(a[2])<<8 | uint32(a[3])
 			d4[k] = uint32(b[0])<<24 | uint32(b[1])<<16 | uint32(b[2])<<8 | uint32(b[3])
 		}
+		pinAll(&pin, &s4[0], &d4[0])
 		cs.pkt.af = C.CLS_AF_V4
 		cs.pkt.src4, cs.pkt.dst4 = (*C.uint32_t)(&s4[0]), (*C.uint32_t)(&d4[0])
 		return en.connect(&cs, n, idx, out, count)
@@ -490,6 +499,7 @@ func (en *Engine) ConnectionBatch(calls []Conn, count bool) ([]aclengine.Connect
 		copy(s16[16*k:], a)
 		copy(d16[16*k:], b)
 	}
+	pinAll(&pin, &s16[0], &d16[0])
 	cs.pkt.af = C.CLS_AF_V16
 	cs.pkt.src16, cs.pkt.dst16 = (*C.uint8_t)(&s16[0]), (*C.uint8_t)(&d16[0])
 	return en.connect(&cs, n, idx, out, count)
@@ -594,6 +604,9 @@ func (en *Engine) ClassifyBatch(t *Table, src, dst []uint32, dport []uint16,
 	for i, p := range proto {
 		pr[i] = uint8(p)
 	}
+	var pin runtime.Pinner // pk holds Go pointers: pinned for the call
+	defer pin.Unpin()
+	pinAll(&pin, &src[0], &dst[0], &dport[0], &pr[0])
 	var pk C.cls_pkt_soa
 	pk.af = C.CLS_AF_V4
 	pk.src4, pk.dst4 = (*C.uint32_t)(&src[0]), (*C.uint32_t)(&dst[0])
@@ -630,6 +643,9 @@ func (en *Engine) ClassifyBatchIP(t *Table, src, dst []net.IP, dport []uint16,
 		copy(d16[16*i:], b)
 		pr[i] = uint8(proto[i])
 	}
+	var pin runtime.Pinner // pk holds Go pointers: pinned for the call
+	defer pin.Unpin()
+	pinAll(&pin, &s16[0], &d16[0], &dport[0], &pr[0])
 	var pk C.cls_pkt_soa
 	pk.af = C.CLS_AF_V16
 	pk.src16, pk.dst16 = (*C.uint8_t)(&s16[0]), (*C.uint8_t)(&d16[0])
@@ -667,4 +683,13 @@ func (en *Engine) ConnCounters(aclName string, reset bool) ([]uint64, error) {
 		return nil, en.lastErr()
 	}
 	return out, nil
+}
+
+// pinAll pins the base of every Go slice whose address goes into a C struct
+// that lives in Go memory (cls_pkt_soa, cls_conn_soa): cgo forbids passing Go
+// memory that holds unpinned Go pointers (cgocheck=1 panics).  Needs Go 1.21+.
+func pinAll(p *runtime.Pinner, ptrs ...interface{}) {
+	for _, x := range ptrs {
+		p.Pin(x)
+	}
 }

@@ -31,7 +31,12 @@
 extern "C" {
 #endif
 
-#define CLS_ABI_VERSION 1
+/* 2: cls_image_v4_header gained n_lctr, ctr16, swap (a destination-keyed
+ *    image: the packets' src and dst must be exchanged) and off_other (a
+ *    nested OTHER image); blob version 3; cls_table_info's n_lctr, ctr16,
+ *    list_mode and swap; CLS_F_COUNT; CLS_AF_V16 connections;
+ *    cls_acl_stats.  A v1 consumer that ignores `swap` would misread blobs. */
+#define CLS_ABI_VERSION 2
 
 /* ---- status codes ------------------------------------------------------ */
 enum {
@@ -213,8 +218,9 @@ int cls_stream_floor(cls_engine* e, const cls_pkt_soa* pkts, uint64_t n, uint8_t
  * replaces it without counting an extra change; last writer wins per
  * interface direction.  A re-put whose rules equal the installed ACL's (the
  * renderer re-puts a local table whose pods changed, acl_renderer.go:186-190)
- * keeps the compiled table and its connection counters and only moves the
- * interface bindings: no compilation, no upload. */
+ * keeps the compiled table and only moves the interface bindings: no
+ * compilation, no upload.  Either way the put installs a new ACL, so its
+ * connection counters (cls_conn_counters) start from zero. */
 int cls_acl_put(cls_engine* e, const char* acl_name, const cls_rule* rules,
                 uint32_t n_rules, const char* const* ingress_ifs, uint32_t n_ingress,
                 const char* const* egress_ifs, uint32_t n_egress);
@@ -316,7 +322,7 @@ int cls_gen_traffic_v16(cls_engine* e, const cls_traffic_spec16* spec, uint64_t 
  */
 typedef struct cls_image_v4_header {
     uint32_t magic;            /* 0x434C5334 "CLS4" */
-    uint32_t version;
+    uint32_t version;          /* 3 (CLS_ABI_VERSION 2) */
     uint32_t n_rules, n_lin, has_cls;
     uint32_t img_bytes, off_bounds, off_iclass, off_cells, off_lists, off_tmpl;
     uint32_t n_bounds, search_top, n_classes, n_tmpl, n_list_entries, n_ctr, lds_bytes;

@@ -40,7 +40,10 @@ def test_reput_equal_rules_rebinds_without_compiling():
         eng.close()
 
 
-def test_rebound_table_keeps_connection_counters_and_verdicts():
+def test_rebound_table_restarts_connection_counters_keeps_verdicts():
+    """Every put installs a new ACL (PutACL replaces the message,
+    aclengine_mock.go:707-713): a rebind keeps the compiled table but its
+    connection counters restart from zero, as after a compiling put."""
     from vpp_amd.engine import Engine
     eng = Engine()
     try:
@@ -61,6 +64,8 @@ def test_rebound_table_keeps_connection_counters_and_verdicts():
         i1 = eng.if_id("in1")
         v2 = eng.connect_batch(np.full(n, i1), np.full(n, i9), src, dst, proto, sport, dport, count=True)
         assert np.array_equal(v1, v2)
-        assert np.array_equal(eng.conn_counters("a"), 2 * c1)
+        assert np.array_equal(eng.conn_counters("a"), c1)      # only the batch after the put
+        assert eng.acl_put("a", rules, ["in1"], []) == 0        # rebind with no batch after it
+        assert not eng.conn_counters("a").any()
     finally:
         eng.close()

@@ -45,12 +45,15 @@ struct DevBuf {
 // one table on different streams never share a counter buffer
 // (include/contivcls.h, threading).  slot_val is all zero between calls: the
 // remap kernel reads and clears it.
-// OTHER queue (protocols > 2 deferred to other_kernel): per workgroup room
-// for 1/16 of its packets (CONTIVCLS_OTHER_CAP: tests, to reach the
-// in-place path of a full segment)
+// OTHER queue (protocols > 2 deferred to the finish launch): per workgroup
+// room for 1/16 of its packets, at most 16 Ki entries (64 KiB per workgroup:
+// the queue exists per (table, stream), and a full segment classifies in
+// place, so a cap costs only speed on batches with > 6 % protocol > 2).
+// CONTIVCLS_OTHER_CAP: tests, to reach the in-place path.
 static uint32_t other_cap(uint64_t n, int grid) {
     if (const char* c = std::getenv("CONTIVCLS_OTHER_CAP")) return uint32_t(std::strtoul(c, nullptr, 0));
-    return uint32_t(std::max<uint64_t>(1024, (n / uint64_t(std::max(grid, 1)) + 15) / 16));
+    const uint64_t want = (n / uint64_t(std::max(grid, 1)) + 15) / 16;
+    return uint32_t(std::min<uint64_t>(16384, std::max<uint64_t>(1024, want)));
 }
 
 struct Scratch {
@@ -972,7 +975,16 @@ int cls_acl_put(cls_engine* e, const char* acl_name, const cls_rule* rules, uint
     if (same != e->tables.end() && same->second->sig == rule_sig(rules, n_rules)) {
         // Equal rules (the renderer re-puts a table whose pods changed,
         // acl_renderer.go:186-190): keep the compiled table, move the bindings.
+        // A put installs a new ACL (PutACL replaces the message,
+        // aclengine_mock.go:707-713), so its connection counters start from
+        // zero either way: clear the kept table's once its pending work is done.
         tid = old->second.table_id;
+        Table& kt = *same->second;
+        if (kt.d_conn_ctr.p) {
+            (void)hipSetDevice(e->device);
+            HIPC(e, hipDeviceSynchronize());
+            HIPC(e, hipMemset(kt.d_conn_ctr.p, 0, size_t(kt.n_rules + 1) * 8));
+        }
         for (auto& b : e->if_acl) {
             if (b.first == int32_t(tid)) b.first = -1;
             if (b.second == int32_t(tid)) b.second = -1;
@@ -1331,7 +1343,7 @@ static int write_blob(const Cls4Image* img, const std::vector<LinRule4>& lin, ui
     cls_image_v4_header h;
     std::memset(&h, 0, sizeof h);
     h.magic = magic;
-    h.version = 2;
+    h.version = 3;
     h.n_rules = n;
     h.n_lin = uint32_t(lin.size());
     h.has_cls = img ? 1u : 0u;
