@@ -41,8 +41,10 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=25,
-                    help="untimed steps first: the GPU clocks settle over the first ~10 ms of work")
+    ap.add_argument("--warmup", type=int, default=25, help="untimed steps after the settle phase")
+    ap.add_argument("--settle-ms", type=float, default=300.0,
+                    help="untimed steps first, for at least this much wall time: the GPU clocks settle "
+                         "over the first ~10 ms of work, whatever --warmup is")
     ap.add_argument("--config", type=int, default=3, choices=[2, 3, 4, 5])
     ap.add_argument("--packets", type=int, default=0, help="packets per GPU (default: config's)")
     ap.add_argument("--cpu-sample", type=int, default=1 << 21,
@@ -163,6 +165,8 @@ def main():
         sys.exit(launch_ranks(args))          # nothing has touched the GPU in this process
     if world != args.gpus:
         sys.exit("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
+    # under torch.distributed.run (also with one rank) the counters are merged
+    # by a real collective; a plain N=1 run has no process group
     import torch
     import torch.distributed as dist
 
@@ -194,24 +198,63 @@ def main():
     first, _ = D.shard(rank, n)
     (eng.gen_traffic_v16 if af == 16 else eng.gen_traffic_v4)(spec, first, pk)
     verdict = torch.empty(n, dtype=torch.uint8, device=dev)
-    counters = torch.zeros(R + 1, dtype=torch.int64, device=dev)
-    torch.cuda.synchronize()
+    # The counter all-reduce (the only collective, whenever a process group
+    # exists -- also a 1-rank RCCL group under torch.distributed.run) runs on
+    # a side stream behind an event, so step i's all-reduce overlaps step
+    # i+1's classify; the counter buffers alternate, and a buffer is written
+    # again only after its previous all-reduce (event) has finished.
+    coll = dist.is_initialized()
+    nbuf = 2 if coll else 1
+    counters = [torch.zeros(R + 1, dtype=torch.int64, device=dev) for _ in range(nbuf)]
+    side = torch.cuda.Stream(device=dev) if coll else None
+    reduced = [None] * nbuf                   # event after the last all-reduce of each buffer
     ev = []                                   # (before, after) the counter all-reduce, per timed step
+    sev = []                                  # (before, after) each timed step on the launch stream
+    torch.cuda.synchronize()
 
-    def step(timing):
+    def step(i, timing):
+        b = i % nbuf
+        main = torch.cuda.current_stream()
+        if timing:
+            s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s0.record(main)
+        if reduced[b] is not None:
+            main.wait_event(reduced[b])
         eng.classify(table, pk["src"], pk["dst"], pk["dport"], pk["proto"], verdict=verdict,
-                     counters=counters, timing=timing)
-        if world > 1:
-            if timing:
-                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                a.record()
-            D.merge_counters(counters)     # RCCL over xGMI: merge per-rule hit counters
-            if timing:
-                b.record()
-                ev.append((a, b))
+                     counters=counters[b], timing=timing)
+        if timing:
+            s1.record(main)
+            sev.append((s0, s1))
+        if coll:
+            done = torch.cuda.Event()
+            done.record(main)
+            with torch.cuda.stream(side):
+                side.wait_event(done)
+                if timing:
+                    a, z = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    a.record(side)
+                D.merge_counters(counters[b])     # RCCL over xGMI: merge per-rule hit counters
+                if timing:
+                    z.record(side)
+                    ev.append((a, z))
+                r = torch.cuda.Event()
+                r.record(side)
+                reduced[b] = r
 
+    # Settle the clocks independently of --warmup: untimed steps until at
+    # least --settle-ms of wall time has passed with the GPU busy (the first
+    # ~10 ms of work run at lower clocks), then the counted warm-up steps.
+    i = 0
+    t_settle = time.perf_counter()
+    while (time.perf_counter() - t_settle) * 1e3 < args.settle_ms:
+        for _ in range(8):
+            step(i, False)
+            i += 1
+        torch.cuda.synchronize()
+    settle_ms = (time.perf_counter() - t_settle) * 1e3
     for _ in range(args.warmup):
-        step(False)
+        step(i, False)
+        i += 1
     torch.cuda.synchronize()
     eng.kernel_times(reset=True)
     if world > 1:
@@ -219,14 +262,19 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step(True)
+        step(i, True)
+        i += 1
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     wall = time.perf_counter() - t0
     kms = eng.kernel_times(reset=True)
     avg_k = float(np.mean(kms)) if kms else float("nan")
-    ar_ms = float(np.mean([a.elapsed_time(b) for a, b in ev])) if ev else 0.0
+    med_k = float(np.median(kms)) if kms else float("nan")
+    med_step = float(np.median([a.elapsed_time(b) for a, b in sev])) if sev else float("nan")
+    ar = [a.elapsed_time(b) for a, b in ev]
+    ar_ms = float(np.mean(ar)) if ar else 0.0
+    ar_med = float(np.median(ar)) if ar else 0.0
     floor_ms = None
     if not args.no_stream_floor:
         # one launch covers at most 2^30 packets (the kernels' 32-bit offsets):
@@ -234,7 +282,7 @@ def main():
         m = min(n, 1 << 30)
         floor_ms = eng.stream_floor(pk["src"][:m], pk["dst"][:m], pk["dport"][:m], pk["proto"][:m],
                                     verdict[:m]) * (n / m)
-    wall, k_max, ar_max = D.max_over_ranks([wall, avg_k, ar_ms], dev)
+    wall, k_max, kmed_max, ar_max, armed_max = D.max_over_ranks([wall, avg_k, med_k, ar_ms, ar_med], dev)
     if floor_ms is not None:
         floor_ms = D.max_over_ranks(floor_ms, dev)
 
@@ -276,16 +324,22 @@ def main():
                        "lds_bytes": info["lds_bytes"] if af == 4 else info["lds_bytes_v16"],
                        "lds_resident": info["lds_resident"] if af == 4 else info["lds_resident_v16"],
                        "parallelism": "dp%d" % world,
-                       "collective": ("counter all-reduce, %s, %d B" % (D.backend(), (R + 1) * 8))
-                       if world > 1 else None},
+                       "collective": ("counter all-reduce, %s, %d B, side stream overlapping the next "
+                                      "step's classify" % (D.backend(), (R + 1) * 8)) if coll else None},
+            "settle_ms": round(settle_ms, 1),
+            "step_ms_median": round(med_step, 4),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
                          "traffic": traffic, "traffic_source": traffic_src,
                          "kernel_ms_avg": round(avg_k, 4),
+                         "kernel_ms_median": round(med_k, 4),
                          "kernel_ms_avg_max_rank": round(k_max, 4),
-                         "allreduce_ms_avg_max_rank": round(ar_max, 4) if world > 1 else None,
+                         "kernel_ms_median_max_rank": round(kmed_max, 4),
+                         "allreduce_ms_avg_max_rank": round(ar_max, 4) if coll else None,
+                         "allreduce_ms_median_max_rank": round(armed_max, 4) if coll else None,
                          "stream_floor_ms": round(floor_ms, 4) if floor_ms is not None else None,
                          "frac_of_stream_floor": round(floor_ms / avg_k, 4) if floor_ms else None,
+                         "frac_of_stream_floor_median": round(floor_ms / med_k, 4) if floor_ms else None,
                          "algorithmic_bytes_per_launch": alg_bytes},
             "cpu_baseline": cpu,
         }

@@ -93,3 +93,85 @@ def test_bench_launches_its_ranks():
     assert line["n_gpus"] == 2 and line["scaling"] == "weak"
     assert line["config"]["packets_per_gpu"] == 1 << 22
     assert line["roofline"]["allreduce_ms_avg_max_rank"] is not None
+
+
+RCCL_WORKER = textwrap.dedent("""
+    import os, sys
+    sys.path[:0] = [%(root)r]
+    import numpy as np, torch
+    import torch.distributed as dist
+    from vpp_amd import dist as D, workload
+    from vpp_amd.engine import Engine
+    D.init("nccl")                      # RCCL; a 1-rank group under torch.distributed.run
+    assert D.backend() == "nccl", D.backend()
+    rank, size, local = D.world()
+    torch.cuda.set_device(D.device_index(local))
+    acl, spec, _ = workload.config(3)
+    eng = Engine(torch.cuda.current_device())
+    t = eng.put_table("g", acl.rules)
+    n = %(n)d
+    first, _ = D.shard(rank, n)
+    pk = {k: torch.empty(n, dtype=dt, device="cuda") for k, dt in
+          (("src", torch.int32), ("dst", torch.int32), ("dport", torch.int16), ("proto", torch.uint8))}
+    eng.gen_traffic_v4(spec, first, pk)
+    v = torch.empty(n, dtype=torch.uint8, device="cuda")
+    c = torch.zeros(t.n_rules + 1, dtype=torch.int64, device="cuda")
+    eng.classify(t, pk["src"], pk["dst"], pk["dport"], pk["proto"], verdict=v, counters=c)
+    side = torch.cuda.Stream()
+    done = torch.cuda.Event()
+    done.record()
+    with torch.cuda.stream(side):       # the overlapped form bench.py uses
+        side.wait_event(done)
+        D.merge_counters(c)             # int64 SUM in HBM over RCCL
+    torch.cuda.synchronize()
+    mx = D.max_over_ranks([1.5 + rank, -2.0], torch.device("cuda", torch.cuda.current_device()))
+    assert mx == [1.5 + size - 1, -2.0], mx
+    np.save(%(out)r + ".c.npy", c.cpu().numpy())
+    np.save(%(out)r + ".v.npy", v.cpu().numpy())
+    eng.close()
+    dist.destroy_process_group()
+""")
+
+
+def test_rccl_counter_allreduce_one_rank(tmp_path):
+    """The RCCL branch itself: a 1-rank nccl group (torch.distributed.run
+    --nproc-per-node 1), counters merged on device (int64 SUM) from a side
+    stream, max_over_ranks on device float64; counters equal the oracle's."""
+    import oracle
+    from vpp_amd import workload
+    n = 1 << 20
+    out = str(tmp_path / "r")
+    script = tmp_path / "w.py"
+    script.write_text(RCCL_WORKER % {"root": ROOT, "out": out, "n": n})
+    env = dict(os.environ)
+    env.pop("VPP_DIST_BACKEND", None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+           "--master-addr=127.0.0.1", "--master-port=%d" % _free_port(), str(script)]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    merged, verdict = np.load(out + ".c.npy"), np.load(out + ".v.npy")
+    acl, spec, _ = workload.config(3)
+    tr = oracle.gen_traffic_v4(spec, 0, n)
+    ov, oc = oracle.classify_fast(oracle.rules_to_c(acl.rules), tr["src"], tr["dst"], tr["dport"], tr["proto"])
+    np.testing.assert_array_equal(verdict, ov)
+    np.testing.assert_array_equal(merged, oc.astype(np.int64))
+
+
+def test_bench_rccl_overlapped_allreduce_one_rank():
+    """bench.py under torch.distributed.run with one rank: the counter
+    all-reduce runs over RCCL on the side stream and is timed."""
+    env = dict(os.environ)
+    env.pop("VPP_DIST_BACKEND", None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+           "--master-addr=127.0.0.1", "--master-port=%d" % _free_port(), os.path.join(ROOT, "bench.py"),
+           "--gpus", "1", "--steps", "8", "--warmup", "2", "--settle-ms", "20", "--packets", str(1 << 24),
+           "--cpu-sample", "0", "--no-stream-floor"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    line = lines[0]
+    assert "nccl" in line["config"]["collective"]
+    assert line["roofline"]["allreduce_ms_avg_max_rank"] > 0
+    assert line["roofline"]["allreduce_ms_median_max_rank"] > 0
+    assert line["settle_ms"] >= 20

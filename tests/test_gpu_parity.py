@@ -208,6 +208,21 @@ def test_config3_full_size_properties(eng):
     torch.cuda.synchronize()
     assert torch.equal(v2, verdict[:m])
     assert torch.equal(c1, c2)
+    # 64 windows of 4 Ki packets strided across the whole 256 Mi stream: the
+    # full-batch verdicts, and each window classified on its own (counters),
+    # equal the oracle's on the same stream positions
+    cr = oracle.rules_to_c(acl.rules)
+    w, stride = 4096, n // 64
+    wc = torch.zeros_like(counters)
+    for k in range(64):
+        a = k * stride + (k * 7919 % (stride - w)) // 16 * 16
+        tr = oracle.gen_traffic_v4(spec, a, w)
+        ov, oc = oracle.classify_fast(cr, tr["src"], tr["dst"], tr["dport"], tr["proto"])
+        assert np.array_equal(verdict[a:a + w].cpu().numpy(), ov), "window %d at %d" % (k, a)
+        eng.classify(t, out["src"][a:a + w], out["dst"][a:a + w], out["dport"][a:a + w],
+                     out["proto"][a:a + w], counters=wc)
+        torch.cuda.synchronize()
+        assert np.array_equal(wc.cpu().numpy().astype(np.uint64), oc), "window %d counters" % k
     del out, verdict
     eng.del_table(t)
 

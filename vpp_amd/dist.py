@@ -36,7 +36,10 @@ def init(backend: str = "nccl"):
     import torch.distributed as dist
     backend = os.environ.get("VPP_DIST_BACKEND", backend)
     rank, size, local = world()
-    if size <= 1 or dist.is_initialized():
+    # A process started by torch.distributed.run (WORLD_SIZE in the env)
+    # joins a group even at world size 1, so the RCCL path runs there too;
+    # a plain single process has no group and no collective.
+    if "WORLD_SIZE" not in os.environ or dist.is_initialized():
         return
     if backend == "nccl":
         torch.cuda.set_device(local)
@@ -56,11 +59,12 @@ def shard(rank: int, n_per_rank: int) -> tuple:
 
 
 def merge_counters(counters):
-    """All-reduce (sum) an int64 counter tensor in place across ranks.  With
-    gloo the collective runs on the host: device counters go through a host
-    copy (the rehearsal path; RCCL reduces them in HBM)."""
+    """All-reduce (sum) an int64 counter tensor in place across the ranks of
+    the group (any size, 1 included).  With gloo the collective runs on the
+    host: device counters go through a host copy (the rehearsal path; RCCL
+    reduces them in HBM, on the caller's current stream's order)."""
     import torch.distributed as dist
-    if dist.is_initialized() and dist.get_world_size() > 1:
+    if dist.is_initialized():
         if counters.is_cuda and dist.get_backend() == "gloo":
             h = counters.cpu()
             dist.all_reduce(h, op=dist.ReduceOp.SUM)
@@ -74,7 +78,7 @@ def max_over_ranks(value, device=None):
     """Max of a float (or a list of floats, elementwise) over the ranks."""
     import torch
     import torch.distributed as dist
-    if not (dist.is_initialized() and dist.get_world_size() > 1):
+    if not dist.is_initialized():
         return value
     if dist.get_backend() == "gloo":
         device = None
