@@ -328,14 +328,15 @@ typedef struct cls_image_v4_header {
     uint32_t n_bounds, search_top, n_classes, n_tmpl, n_list_entries, n_ctr, lds_bytes;
     uint32_t off_image, off_ctr_rule, off_lin;   /* byte offsets inside the blob */
     uint32_t total_bytes;
-    uint32_t mode;             /* source lookup: 0 interval search, 1 hash LPM */
+    uint32_t mode;             /* source lookup: 0 interval search, 1 hash LPM, 4 trie */
     uint32_t default_class;    /* hash LPM: class when no hashed prefix matches */
     uint32_t n_hash;           /* hashed prefix lengths (ascending) */
     uint32_t hash_mask[3], hash_shift[3], hash_cap[3], off_hash[3];
     uint32_t list_mode;        /* candidate lists: 0 template scan, 1 bit vectors,
                                   2 bit vectors with global port classes,
                                   3 port-filtered sublists (radix port classes),
-                                  4 port-filtered sublists (hashed port classes) */
+                                  4 port-filtered sublists (hashed port classes),
+                                  5, 6: 4, 3 with wide cells in global memory (off_gcells) */
     uint32_t off_bv, bv_steps_d, bv_steps_p;
     uint32_t off_ptop;         /* list modes 2, 3: port radix at 0 (256 x u32 window address,
                                   then u8 windows of class per port) */
@@ -355,6 +356,14 @@ typedef struct cls_image_v4_header {
     uint32_t off_other;        /* blob offset of the OTHER image (protocols > 2: one cell per
                                   class, interval search, template scan; magic 0x434C534F "CLSO",
                                   its slots numbered after this image's), 0 if none */
+    uint32_t off_trie;         /* mode 4 (source trie): level 1 (256 u32 by src >> 24: node byte
+                                  address), nodes (256 u32 by bits 16..23: leaf byte address << 4
+                                  | depth), leaves (2^depth u32 {key | class << 16}) */
+    uint32_t trie_depth;       /* deepest leaf of the trie */
+    uint32_t off_gcells;       /* list modes 5, 6 (4, 3 with wide cells): blob offset of the
+                                  cells, uint2 {pointer table byte address, counter base} per
+                                  (class, protocol); n_gcells u32 words */
+    uint32_t n_gcells;
 } cls_image_v4_header;
 int cls_compile_v4(const cls_rule* rules, uint32_t n_rules, void* blob, uint64_t cap,
                    uint64_t* need);

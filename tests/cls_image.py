@@ -46,7 +46,7 @@ class Image:
                 self.bounds = np.frombuffer(img, np.uint32, count=2 * top, offset=h.off_bounds)
                 self.iclass = np.frombuffer(img, np.uint16, count=2 * top, offset=h.off_iclass)
             # cells per class: 3 (TCP, UDP, ICMP) or 1 (the OTHER image)
-            self.ncell = h.row_bytes // (8 if h.list_mode == 0 else 4)
+            self.ncell = h.row_bytes // (8 if h.list_mode in (0, 5, 6) else 4)
             if h.list_mode == 0:                   # uint2 cells
                 self.cells = np.frombuffer(img, np.uint32, count=h.n_classes * 2 * self.ncell,
                                            offset=h.off_cells).reshape(-1, 2)
@@ -60,6 +60,9 @@ class Image:
                 cap = h.hash_cap[i]
                 tab = np.frombuffer(img, np.uint32, count=4 * cap, offset=h.off_hash[i]).reshape(-1, 2)
                 self.hash.append((h.hash_mask[i], h.hash_shift[i], cap, tab, h.hash_mul[i]))
+        # list modes 5, 6: wide cells (uint2 {pointer table address, counter base}) in global memory
+        self.gcells = (np.frombuffer(blob, np.uint32, count=h.n_gcells, offset=h.off_gcells).reshape(-1, 2)
+                       if h.n_gcells else None)
         # protocols > 2: the OTHER image (its own blob inside this one)
         self.other = Image(blob[h.off_other:]) if h.off_other else None
 
@@ -74,6 +77,22 @@ class Image:
 
     def source_class(self, src):
         h = self.h
+        if h.mode == 4:
+            # source trie (compile.cpp build_trie): level 1 -> node -> leaf
+            # {address << 8 | m - 1}; branch-free lower bound for trie_depth steps
+            img = np.frombuffer(self._img, np.uint32).astype(np.int64)
+            s = src.astype(np.int64)
+            a = img[(h.off_trie + ((s >> 22) & 0x3FC)) // 4]
+            a = img[(a + ((s >> 14) & 0x3FC)) // 4]
+            ln = (a & 0xFF) + 1
+            a = a >> 8
+            x = s & 0xFFFF
+            for _ in range(h.trie_depth):
+                half = ln >> 1
+                c = a + 4 * half
+                a = np.where((img[c // 4] & 0xFFFF) < x, c, a)
+                ln = ln - half
+            return img[a // 4] >> 16
         if h.mode == 1:
             # entries hold the byte address of the class's cell row
             row = np.full(len(src), h.default_row, np.int64)
@@ -153,8 +172,9 @@ class Image:
         return b8[tp + (dp & 0xFF)].astype(np.int64)
 
     def _port_class4(self, dport):
-        """List modes 3, 4: merged port class x 4 (mode 4: perfect hash at 0)."""
-        if self.h.list_mode == 3:
+        """List modes 3, 4: merged port class x 4 (mode 4: perfect hash at 0;
+        5, 6 as 4, 3)."""
+        if self.h.list_mode in (3, 6):
             return self._port_class(dport)
         img = np.frombuffer(self._img, np.uint32).astype(np.int64)
         dp = dport.astype(np.int64)
@@ -169,15 +189,22 @@ class Image:
         moves the state when start - 1 < dst; outcome = result | (j + 1) << 2."""
         img = np.frombuffer(self._img, np.uint32).astype(np.int64)
         pr = np.minimum(proto, 2).astype(np.int64)
-        cell = img[(self.h.off_cells + cls * self.h.row_bytes + pr * 4) // 4]
         pc4 = self._port_class4(dport)                # class x 4
-        st = img[((cell & 0x3FFF) * 4 + pc4) // 4]
+        if self.h.list_mode >= 5:
+            # wide cells (list modes 5, 6) in global memory: {pointer table byte address, counter base}
+            wc = self.gcells[cls * self.ncell + pr].astype(np.int64)
+            st = img[(wc[:, 0] + pc4) // 4]
+            base = wc[:, 1]
+        else:
+            cell = img[(self.h.off_cells + cls * self.h.row_bytes + pr * 4) // 4]
+            st = img[((cell & 0x3FFF) * 4 + pc4) // 4]
+            base = cell >> 14
         d = dst.astype(np.int64)
         for i in range(int(self.h.bv_steps_d) - 1, -1, -1):
             a = ((st >> 13) + (8 << i)) // 4
             st = np.where(img[a] < d, img[a + 1], st)
         res = (st & 3).astype(np.uint32)
-        slot = (cell >> 14) + ((st >> 2) & 63)       # the cell's no-match slot when j + 1 == 0
+        slot = base + ((st >> 2) & 63)               # the cell's no-match slot when j + 1 == 0
         np.add.at(counters, self.ctr_rule[slot].astype(np.int64), 1)
         return res.astype(np.uint8), counters
 

@@ -542,6 +542,94 @@ std::vector<Sublist> port_sublists(const std::vector<TmplKey>& ents, const std::
     return res;
 }
 
+// Source trie (src mode 4): the class of a source address from a 256-entry
+// level over src >> 24, a 256-entry node over bits 16..23 and a short search
+// in the /16 chunk's leaf, instead of a binary search over every elementary
+// interval (compile.hpp Cls4Image::off_trie).  `bounds` (n sorted interval
+// starts, bounds[0] = 0) and `iclass` as build_cls4_one computes them;
+// `base`: the section's LDS byte address.  Entries:
+//   level 1 [src >> 24]: byte address of a node;
+//   node [(src >> 16) & 255]: leaf byte address << 8 | (m - 1), m <= 256;
+//   leaf: m u32 {key | class << 16}: entry 0 = the interval holding the
+//   chunk's first address (key 0xFFFF: never taken), entries 1..m-1 the
+//   intervals starting inside the chunk (key = start - 1, low 16 bits).
+//   Search (branch-free lower bound, no padding): a = leaf, len = m; per
+//   step: h = len >> 1, a' = a + 4 h, a = key(a') < (src & 0xFFFF) ? a' : a,
+//   len -= h; ceil(log2 m) steps (more are no-ops); class = word(a) >> 16.
+// Chunks inside one interval share a one-entry leaf per class, /8s inside
+// one interval a node per class, equal leaves one copy.
+struct Trie {
+    std::vector<uint32_t> words;
+    uint32_t depth = 0;            // steps of the largest leaf
+};
+
+bool build_trie(const std::vector<uint32_t>& bounds, uint32_t n, const std::vector<uint16_t>& iclass, uint32_t base,
+                uint32_t max_bytes, Trie& out) {
+    out = Trie();
+    auto interval = [&](uint64_t x) {                 // index of the interval holding x
+        return uint32_t(std::upper_bound(bounds.begin(), bounds.begin() + n, uint32_t(x)) - bounds.begin()) - 1u;
+    };
+    auto next_bound = [&](uint64_t x) {               // first bound above x (n if none)
+        return uint32_t(std::upper_bound(bounds.begin(), bounds.begin() + n, uint32_t(x)) - bounds.begin());
+    };
+    std::vector<uint32_t>& w = out.words;
+    w.assign(256, 0u);                                 // level 1, filled below
+    std::map<uint32_t, uint32_t> uniform_leaf, uniform_node;   // class -> word index
+    std::map<std::vector<uint32_t>, uint32_t> leaf_of;         // leaf content -> word index
+    auto addr = [&](uint32_t word) { return base + 4u * word; };
+    auto leaf_uniform = [&](uint32_t cls) {
+        auto it = uniform_leaf.find(cls);
+        if (it != uniform_leaf.end()) return it->second;
+        const uint32_t at = uint32_t(w.size());
+        w.push_back(0xFFFFu | (cls << 16));
+        uniform_leaf.emplace(cls, at);
+        return at;
+    };
+    std::vector<uint32_t> node(256), leaf;
+    for (uint32_t a = 0; a < 256; ++a) {
+        const uint64_t lo8 = uint64_t(a) << 24, hi8 = lo8 + (1u << 24) - 1u;
+        const uint32_t k8 = interval(lo8), nb8 = next_bound(lo8);
+        if (nb8 >= n || bounds[nb8] > hi8) {           // the /8 inside one interval
+            const uint32_t cls = iclass[k8];
+            auto it = uniform_node.find(cls);
+            if (it == uniform_node.end()) {
+                const uint32_t lw = leaf_uniform(cls);
+                const uint32_t at = uint32_t(w.size());
+                w.insert(w.end(), 256, addr(lw) << 8);
+                it = uniform_node.emplace(cls, at).first;
+            }
+            w[a] = addr(it->second);
+            continue;
+        }
+        for (uint32_t b = 0; b < 256; ++b) {
+            const uint64_t lo = lo8 | (uint64_t(b) << 16), hi = lo + 0xFFFFu;
+            const uint32_t k0 = interval(lo);
+            uint32_t j = next_bound(lo);
+            if (j >= n || bounds[j] > hi) {
+                node[b] = addr(leaf_uniform(iclass[k0])) << 8;
+                continue;
+            }
+            leaf.assign(1, 0xFFFFu | (uint32_t(iclass[k0]) << 16));
+            for (; j < n && bounds[j] <= hi; ++j)
+                leaf.push_back(((bounds[j] - uint32_t(lo) - 1u) & 0xFFFFu) | (uint32_t(iclass[j]) << 16));
+            if (leaf.size() > 256) return false;
+            uint32_t d = 0;
+            while ((size_t(1) << d) < leaf.size()) ++d;
+            out.depth = std::max(out.depth, d);
+            auto it = leaf_of.find(leaf);
+            if (it == leaf_of.end()) {
+                it = leaf_of.emplace(leaf, uint32_t(w.size())).first;
+                w.insert(w.end(), leaf.begin(), leaf.end());
+            }
+            node[b] = (addr(it->second) << 8) | uint32_t(leaf.size() - 1);
+        }
+        w[a] = addr(uint32_t(w.size()));
+        w.insert(w.end(), node.begin(), node.end());
+        if (w.size() * 4 > max_bytes) return false;
+    }
+    return w.size() * 4 <= max_bytes && uint64_t(base) + w.size() * 4 < (1ull << 24);
+}
+
 }  // namespace
 
 uint32_t Cls4Image::row_of(uint32_t addr) const {
@@ -989,10 +1077,19 @@ static bool build_cls4_one(const std::vector<SemRule>& sem, uint32_t n_rules, Cl
         }
         if (ci == 0) hot3 = std::min<uint32_t>(uint32_t(ctr3.size()), kMaxHot);
     }
+    // wide cells (list modes 5, 6: in global memory, 32-bit counter base)
+    // keep the sublist form when the LDS cells cannot
+    const uint32_t lmode_w = lmode >= 3 ? lmode : 0u;
     if (lmode >= 3 && ctr3.size() > 0x3FFFFu) lmode = 2;  // 18-bit counter base in the cell
+    const uint32_t mode0 = img.mode;                      // the source lookup without the trie
 
     std::vector<uint32_t>& w = img.words;
-    auto serialise = [&](uint32_t lm) {
+    // trie: the source trie replaces the interval search (mode 0 only);
+    // wide: list modes 3, 4 with the cells in global memory (gcells)
+    auto serialise = [&](uint32_t lm, bool trie, bool wide) -> bool {
+        img.mode = trie ? 4u : mode0;
+        img.off_trie = img.trie_depth = 0;
+        img.gcells.clear();
         img.ctr_rule = lm >= 3 ? ctr3 : ctr_base_rule;
         img.n_hot = lm >= 3 ? hot3 : hot_base;
         // lists
@@ -1045,7 +1142,18 @@ static bool build_cls4_one(const std::vector<SemRule>& sem, uint32_t n_rules, Cl
             w.resize(align4(uint32_t(w.size())));
             img.sub_bytes = uint32_t(w.size()) * 4;
         }
-        if (img.mode == 0) {
+        if (trie) {
+            Trie tr;
+            if (!build_trie(bounds, n_real_bounds, iclass, uint32_t(w.size()) * 4, lds_budget(), tr)) {
+                if (std::getenv("CONTIVCLS_DEBUG_MODES"))
+                    std::fprintf(stderr, "trie: does not fit (%zu words at depth %u)\n", tr.words.size(), tr.depth);
+                return false;
+            }
+            img.off_trie = uint32_t(w.size()) * 4;
+            img.trie_depth = tr.depth;
+            w.insert(w.end(), tr.words.begin(), tr.words.end());
+            w.resize(align4(uint32_t(w.size())));
+        } else if (img.mode == 0) {
             img.off_bounds = uint32_t(w.size()) * 4;
             w.insert(w.end(), bounds.begin(), bounds.end());
             w.resize(align4(uint32_t(w.size())));
@@ -1054,8 +1162,8 @@ static bool build_cls4_one(const std::vector<SemRule>& sem, uint32_t n_rules, Cl
             std::memcpy(reinterpret_cast<uint8_t*>(w.data()) + img.off_iclass, iclass.data(), iclass.size() * 2);
             w.resize(align4(uint32_t(w.size())));
         }
-        img.off_cells = uint32_t(w.size()) * 4;
-        img.row_bytes = lm == 0 ? 8u * ncell : 4u * ncell;   // cells of uint2 (scan) / u32
+        img.off_cells = wide ? 0u : uint32_t(w.size()) * 4;
+        img.row_bytes = lm == 0 || wide ? 8u * ncell : 4u * ncell;   // cells of uint2 (scan, wide) / u32
         img.default_row = img.off_cells + img.default_class * img.row_bytes;
         if (lm == 0) {
             // scan cells: uint2 {list start | len << 16, counter base}
@@ -1074,6 +1182,15 @@ static bool build_cls4_one(const std::vector<SemRule>& sem, uint32_t n_rules, Cl
                 w.push_back(t.res);
             }
             w.resize(align4(uint32_t(w.size())));
+        } else if (wide) {
+            // wide cells, in global memory: uint2 {pointer table byte
+            // address, counter base (the cell's own no-match slot)}
+            const size_t n_cells = size_t(n_classes) * ncell;
+            img.gcells.resize(2 * n_cells);
+            for (size_t i = 0; i < n_cells; ++i) {
+                img.gcells[2 * i] = ptr_off.at(cells[2 * i]);
+                img.gcells[2 * i + 1] = cb3[i];
+            }
         } else if (lm >= 3) {
             // sublist cells: u32 {pointer table word offset (14 bits: the
             // tables lie in the first 64 KiB) | counter base << 14}, the base
@@ -1185,6 +1302,8 @@ static bool build_cls4_one(const std::vector<SemRule>& sem, uint32_t n_rules, Cl
         img.n_list_entries = uint32_t(lists.size());
         img.n_ctr = uint32_t(img.ctr_rule.size());
         img.search_top = top;
+        if (wide) img.list_mode = lm == 4 ? 5u : 6u;
+        return true;
     };
     // The fastest list mode whose image and counters fit the workgroup's LDS:
     // first with every slot counted in LDS (u32, else u16), then with the
@@ -1209,22 +1328,40 @@ static bool build_cls4_one(const std::vector<SemRule>& sem, uint32_t n_rules, Cl
     // block offset field: 16 bits in 8-B units (modes 1, 2); mode 3: the
     // pointer tables in the first 64 KiB, sublist slots below 2^16
     auto cell_ok = [&](uint32_t lm) {
+        if (img.list_mode >= 5) return img.sub_bytes != 0xFFFFFFFFu;   // wide cells: the state's slot field
         return lm == 0 || (lm >= 3 ? img.sub_bytes <= 0x10000u
                                    : img.img_bytes / 8u <= 0xFFFFu && img.ctr_rule.size() <= 0xFFFFu);
     };
-    for (int partial = 0; partial < 2; ++partial)
-        for (uint32_t lm : seq) {
-            serialise(lm);
-            const bool ok = cell_ok(lm) && place_counters(img, budget, partial != 0);
+    // The source trie where the interval search would run (sublist modes;
+    // CONTIVCLS_TRIE=0 / 1: never / only -- diagnostics and tests), preferred
+    // when it fits; wide cells only once no LDS-cell image fits
+    // (CONTIVCLS_WIDE=1: first -- tests).
+    const char* tenv = std::getenv("CONTIVCLS_TRIE");
+    const char* wenv = std::getenv("CONTIVCLS_WIDE");
+    const int tmode = tenv ? std::atoi(tenv) : -1;
+    const bool wide_first = wenv && std::atoi(wenv) == 1, wide_never = wenv && std::atoi(wenv) == 0;
+    const bool trie_ok = mode0 == 0 && !opt && tmode != 0;
+    auto try_fit = [&](uint32_t lm, bool wide, bool partial) {
+        for (int tr = trie_ok && lm >= 3 ? 1 : 0; tr >= (tmode == 1 && trie_ok && lm >= 3 ? 1 : 0); --tr) {
+            if (!serialise(lm, tr != 0, wide)) continue;
+            const bool ok = cell_ok(lm) && place_counters(img, budget, partial);
             if (dbg)
-                std::fprintf(stderr, "list mode %u%s: lds %u img %u ctr %u lctr %u ctr16 %u -> %s\n", lm,
-                             partial ? " (partial)" : "", img.lds_bytes, img.img_bytes, img.n_ctr, img.n_lctr,
-                             img.ctr16, ok ? "resident" : "no");
+                std::fprintf(stderr, "list mode %u%s%s%s: lds %u img %u ctr %u lctr %u ctr16 %u -> %s\n", img.list_mode,
+                             tr ? " trie" : "", wide ? " wide" : "", partial ? " (partial)" : "", img.lds_bytes,
+                             img.img_bytes, img.n_ctr, img.n_lctr, img.ctr16, ok ? "resident" : "no");
             if (ok) return true;
         }
+        return false;
+    };
+    const bool wide_ok = lmode_w >= 3 && !opt && !wide_never;
+    if (wide_ok && wide_first && try_fit(lmode_w, true, true)) return true;
+    for (int partial = 0; partial < 2; ++partial)
+        for (uint32_t lm : seq)
+            if (try_fit(lm, false, partial != 0)) return true;
+    if (wide_ok && try_fit(lmode_w, true, true)) return true;
     for (uint32_t lm : seq) {
         if (lm > 1 && lm != seq.back()) continue;
-        serialise(lm);
+        serialise(lm, false, false);
         if (!cell_ok(lm)) continue;
         place_counters(img, budget, false);
         if (dbg) std::fprintf(stderr, "list mode %u: global image\n", lm);
@@ -1585,13 +1722,18 @@ std::vector<SemRule> swap_sides(const std::vector<SemRule>& sem) {
 
 namespace {
 
-// (LDS-resident, every slot in LDS, not the template scan, list mode, -LDS bytes)
-std::array<int64_t, 5> image_rank(const Cls4Image& m) {
-    return {m.lds_ok ? 1 : 0, m.n_lctr == m.n_ctr ? 1 : 0, m.list_mode >= 1 ? 1 : 0, int64_t(m.list_mode),
+// (LDS-resident, every slot in LDS, cells in LDS, not the template scan,
+// list mode, -LDS bytes); wide list modes 5, 6 rank as 4, 3
+std::array<int64_t, 6> image_rank(const Cls4Image& m) {
+    const bool wide = m.list_mode >= 5;
+    const uint32_t lm = m.list_mode == 5 ? 4u : m.list_mode == 6 ? 3u : m.list_mode;
+    return {m.lds_ok ? 1 : 0, m.n_lctr == m.n_ctr ? 1 : 0, wide ? 0 : 1, lm >= 1 ? 1 : 0, int64_t(lm),
             -int64_t(m.lds_bytes)};
 }
 
-bool good_enough(const Cls4Image& m) { return m.lds_ok && m.n_lctr == m.n_ctr && m.list_mode >= 1; }
+bool good_enough(const Cls4Image& m) {
+    return m.lds_ok && m.n_lctr == m.n_ctr && m.list_mode >= 1 && m.list_mode <= 4;
+}
 
 // CONTIVCLS_ORIENT=src|dst (diagnostics, tests): one orientation only
 int forced_orient() {

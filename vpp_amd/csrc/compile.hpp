@@ -40,6 +40,7 @@ namespace cls {
 constexpr uint32_t kMaxHashLens = 3;
 constexpr uint32_t kMaxHot = 16;       // hot slots counted in per-lane LDS rows
 constexpr uint32_t kMaxBvSteps = 7;    // bit-vector search depth (lists <= 32 entries)
+constexpr uint32_t kMaxTrieDepth = 8;  // source trie: deepest leaf search (src mode 4)
 constexpr uint32_t kMaxPortClasses = 256;  // list modes 2, 3: global port classes
 constexpr uint32_t kPortUniform = 1u << 19;  // port radix: chunk inside one class
 constexpr uint32_t kMaxPortClasses3 = 64;   // list modes 3, 4: class x 4 fits a byte
@@ -132,8 +133,12 @@ struct Cls4Image {
     uint32_t search_top = 0;       // largest power of two <= n_bounds
     uint32_t lds_bytes = 0;        // image + counters (u32 per slot), 16 B aligned
     std::vector<uint32_t> ctr_rule;  // slot -> rule index (R = default DENY)
-    // source lookup: mode 0 = interval binary search, 1 = hash LPM
+    // source lookup: mode 0 = interval binary search, 1 = hash LPM, 3 = rows
+    // given by the caller (16-byte core), 4 = source trie (off_trie)
     uint32_t mode = 0;
+    // mode 4: level 1 (256 u32, indexed by src >> 24) at off_trie, then the
+    // nodes and leaves (compile.cpp build_trie); trie_depth = deepest leaf
+    uint32_t off_trie = 0, trie_depth = 0;
     uint32_t default_class = 0;    // hash mode: class of addresses no hashed prefix covers
     uint32_t n_hash = 0;           // hashed prefix lengths, ascending
     uint32_t hash_mask[kMaxHashLens] = {}, hash_shift[kMaxHashLens] = {};  // shift = 32 - L
@@ -146,8 +151,16 @@ struct Cls4Image {
     // candidate lists: mode 0 = scan of template ids, 1 = bit vectors (all lists
     // <= 32) with per-list port search, 2 = bit vectors with global port
     // classes, 3 = port-filtered sublists (per list and port class, the dst
-    // intervals with their first-match outcome; searched with one state word)
+    // intervals with their first-match outcome; searched with one state word),
+    // 4 = 3 with hashed port classes; 5, 6 = 4, 3 with wide cells in global
+    // memory (gcells)
     uint32_t list_mode = 0;
+    // list modes 5, 6: the cells are not in the LDS image but in gcells
+    // (global memory, after the image in the device buffer): uint2 {pointer
+    // table LDS byte address, counter base} per (class, protocol), so the
+    // counter base has 32 bits and the classes any number; a class row is a
+    // byte offset into gcells (off_cells 0, row_bytes 8 x n_cells)
+    std::vector<uint32_t> gcells;
     uint32_t sub_bytes = 0;        // modes 3, 4: end of the pointer tables (< 64 KiB)
     // mode 4: port perfect hash at LDS 0: e = u32 at byte mulhi(port, mul) &
     // mask4, class x 4 = (e & 0xFFFF) == port ? e >> 16 : port_dflt

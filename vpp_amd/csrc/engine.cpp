@@ -330,9 +330,13 @@ static bool build_pair(const std::vector<SemRule>& sem, uint32_t n, Cls4Image& i
     return build_other4(img.swap ? swap_sides(sem) : sem, n, oimg, why);
 }
 
+// The image, then (list modes 5, 6) its wide cells right after it: the
+// kernel stages [0, img_bytes) into LDS and reads the cells from global memory.
 static int upload(cls_engine* e, DevBuf& d, const Cls4Image& im) {
-    HIPC(e, d.ensure(im.img_bytes));
+    const size_t gb = im.gcells.size() * 4;
+    HIPC(e, d.ensure(im.img_bytes + gb));
     HIPC(e, hipMemcpy(d.p, im.words.data(), im.img_bytes, hipMemcpyHostToDevice));
+    if (gb) HIPC(e, hipMemcpy(static_cast<uint8_t*>(d.p) + im.img_bytes, im.gcells.data(), gb, hipMemcpyHostToDevice));
     return CLS_OK;
 }
 
@@ -507,6 +511,10 @@ static Cls4Dev cls4_dev(const Cls4Image& im, const DevBuf& d_img, const DevBuf& 
     cd.off_hot = im.off_hot;
     cd.n_lctr = im.n_lctr;
     cd.ctr16 = im.ctr16;
+    cd.off_trie = im.off_trie;
+    cd.trie_depth = im.trie_depth;
+    cd.gcells = im.gcells.empty() ? nullptr
+                                  : reinterpret_cast<const uint8_t*>(d_img.p) + im.img_bytes;   // upload()
     cd.part = nullptr;
     cd.oq = nullptr;                 // protocols > 2 classified in place unless the caller sets a queue
     cd.oq_cap = 0;
@@ -1374,6 +1382,9 @@ static int write_blob(const Cls4Image* img, const std::vector<LinRule4>& lin, ui
         h.n_lctr = im.n_lctr;
         h.ctr16 = im.ctr16;
         h.swap = im.swap;
+        h.off_trie = im.off_trie;
+        h.trie_depth = im.trie_depth;
+        h.n_gcells = uint32_t(im.gcells.size());
         for (uint32_t i = 0; i < kMaxHashLens; ++i) {
             h.hash_mask[i] = im.hash_mask[i];
             h.hash_shift[i] = im.hash_shift[i];
@@ -1387,6 +1398,10 @@ static int write_blob(const Cls4Image* img, const std::vector<LinRule4>& lin, ui
     h.off_ctr_rule = uint32_t(al(h.off_image + h.img_bytes));
     h.off_lin = uint32_t(al(h.off_ctr_rule + uint64_t(h.n_ctr) * 4));
     h.total_bytes = uint32_t(h.off_lin + lin.size() * sizeof(LinRule4));
+    if (h.n_gcells) {
+        h.off_gcells = uint32_t(al(h.total_bytes));
+        h.total_bytes = h.off_gcells + h.n_gcells * 4u;
+    }
     const uint32_t off_trailer = uint32_t(al(h.total_bytes));
     if (trailer) h.total_bytes = off_trailer + uint32_t(trailer->size() * 4);
     uint64_t need_o = 0;                      // the OTHER image: a nested blob (magic "CLSO")
@@ -1408,6 +1423,7 @@ static int write_blob(const Cls4Image* img, const std::vector<LinRule4>& lin, ui
     if (img) {
         std::memcpy(b + h.off_image, img->words.data(), img->img_bytes);
         std::memcpy(b + h.off_ctr_rule, img->ctr_rule.data(), size_t(h.n_ctr) * 4);
+        if (h.n_gcells) std::memcpy(b + h.off_gcells, img->gcells.data(), size_t(h.n_gcells) * 4);
     }
     if (!lin.empty()) std::memcpy(b + h.off_lin, lin.data(), lin.size() * sizeof(LinRule4));
     if (other) write_blob(other, {}, n, 0x434C534Fu, nullptr, 0, b + h.off_other, need_o, &need_o);

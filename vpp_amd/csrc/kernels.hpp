@@ -50,7 +50,9 @@ struct Cls4Dev {
     const LinRule4* lin;       // linear rules (the 16-byte kernel's FORCE_LINEAR cross-check)
     uint32_t n_lin;
     uint32_t n_rules;          // R
-    uint32_t mode;             // 0 interval search, 1 hash LPM
+    uint32_t mode;             // 0 interval search, 1 hash LPM, 4 source trie
+    uint32_t off_trie, trie_depth;   // mode 4: level 1 at off_trie (compile.cpp build_trie)
+    const uint8_t* gcells;     // list modes 5, 6: wide cells (uint2 {pointer table, counter base})
     uint32_t default_row;      // source lookup miss: byte address of the default class's cells
     uint32_t n_hash;
     uint32_t hash_mask[kMaxHashLens], hash_shift[kMaxHashLens], hash_cap[kMaxHashLens];

@@ -155,11 +155,40 @@ __device__ __forceinline__ void sub_step(const Img<kLds>& im, const uint32_t (&d
 // Source lookup of N packets, interleaved (N independent LDS chains per lane).
 // Result: the byte address of the packet's class row of cells.  kMode: 0
 // interval search, 1 hash LPM over t.n_hash prefix lengths, 2 hash LPM over
-// exactly one length (pod /32s: the common rendered table; fewer live SGPRs).
+// exactly one length (pod /32s: the common rendered table; fewer live SGPRs),
+// 4 source trie (compile.cpp build_trie).
 template <int N, bool kLds, int kMode>
 __device__ __forceinline__ void src_row(const Img<kLds>& im, const Cls4Dev& t,
                                         const uint32_t (&src)[N], uint32_t (&row)[N]) {
-    if constexpr (kMode == 3) {
+    if constexpr (kMode == 4) {
+        // level 1 -> node -> leaf {byte address << 8 | m - 1}; then the leaf's
+        // branch-free lower bound for t.trie_depth steps (uniform): steps
+        // past a lane's own ceil(log2 m) have h = 0 and re-test the current
+        // entry (already taken, or entry 0: key 0xFFFF), so no per-lane branch
+        uint32_t a[N], len[N], x[N];
+#pragma unroll
+        for (int q = 0; q < N; ++q) a[q] = im.u32(t.off_trie + ((src[q] >> 22) & 0x3FCu));
+#pragma unroll
+        for (int q = 0; q < N; ++q) a[q] = im.u32(a[q] + ((src[q] >> 14) & 0x3FCu));
+#pragma unroll
+        for (int q = 0; q < N; ++q) {
+            len[q] = (a[q] & 0xFFu) + 1u;
+            a[q] >>= 8;
+            x[q] = src[q] & 0xFFFFu;
+        }
+#pragma unroll
+        for (int i = 0; i < int(kMaxTrieDepth); ++i) {
+            if (uint32_t(i) >= t.trie_depth) break;              // uniform
+#pragma unroll
+            for (int q = 0; q < N; ++q) {
+                const uint32_t h = len[q] >> 1, c = a[q] + 4u * h;
+                a[q] = (im.u32(c) & 0xFFFFu) < x[q] ? c : a[q];
+                len[q] -= h;
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < N; ++q) row[q] = t.off_cells + (im.u32(a[q]) >> 16) * t.row_bytes;
+    } else if constexpr (kMode == 3) {
         // the caller found the rows (16-byte path, host-route hashes)
 #pragma unroll
         for (int q = 0; q < N; ++q) row[q] = src[q];
@@ -220,8 +249,11 @@ __device__ __forceinline__ void classify_n(const Img<kLds>& im, const Cls4Dev& t
                                            const uint32_t (&src)[N], const uint32_t (&dst)[N],
                                            const uint32_t (&dport)[N], const uint32_t (&proto)[N],
                                            uint32_t (&res)[N], uint32_t (&slot)[N]) {
+    // list modes 5, 6: 4, 3 with the wide cells in global memory (t.gcells)
+    constexpr bool kWide = kList >= 5;
+    constexpr int kPort = kList == 5 ? 4 : kList == 6 ? 3 : kList;
     uint32_t pc[N];
-    if constexpr (kList == 4) {
+    if constexpr (kPort == 4) {
         // Port class from the perfect hash at image address 0: one probe at
         // byte address mulhi(port, mul) & mask4, e = {port | class x 4 << 16};
         // ports absent from it are in the default class (rendered tables:
@@ -235,7 +267,7 @@ __device__ __forceinline__ void classify_n(const Img<kLds>& im, const Cls4Dev& t
                 pc[q] = (e & 0xFFFFu) == dport[q] ? e >> 16 : t.port_dflt;
             }
         }
-    } else if constexpr (kList >= 2) {
+    } else if constexpr (kPort >= 2) {
         // Global port class from the radix at image address 0: top[port >> 8]
         // = byte address of a 256-byte window, class = window[port & 255]
         // (class x 4 in mode 3).  Independent of the source lookup: these
@@ -273,6 +305,18 @@ __device__ __forceinline__ void classify_n(const Img<kLds>& im, const Cls4Dev& t
                 cell[q] = row[q] + proto[q] + pc[q];
                 st[q] = cell[q] & 0x3Fu;
             }
+        } else if constexpr (kWide) {
+            // cell = {pointer table byte address, counter base}; cell[q] keeps
+            // the base (the slot below)
+            uint2 wc[N];
+#pragma unroll
+            for (int q = 0; q < N; ++q)
+                wc[q] = *reinterpret_cast<const uint2*>(t.gcells + row[q] + 8u * min(proto[q], 2u));
+#pragma unroll
+            for (int q = 0; q < N; ++q) {
+                cell[q] = wc[q].y;
+                st[q] = im.u32(wc[q].x + pc[q]);
+            }
         } else {
 #pragma unroll
             for (int q = 0; q < N; ++q) cell[q] = im.u32(row[q] + 4u * min(proto[q], 2u));
@@ -308,7 +352,7 @@ __device__ __forceinline__ void classify_n(const Img<kLds>& im, const Cls4Dev& t
 #pragma unroll
         for (int q = 0; q < N; ++q) {
             res[q] = st[q] & 3u;                                      // DENY when no entry
-            slot[q] = (cell[q] >> 14) + ((st[q] >> 2) & 63u);         // base + j + 1 (0: no entry)
+            slot[q] = (kWide ? cell[q] : cell[q] >> 14) + ((st[q] >> 2) & 63u);   // base + j + 1 (0: no entry)
         }
     } else if constexpr (kList >= 1) {
         // Bit vectors: the entries of the cell's list covering the packet's dst
@@ -1093,7 +1137,7 @@ static void launch_cls(const Cls4Dev& t, const Pkts4& p, uint8_t* verdict, unsig
             return;
         }
     }
-    if constexpr (kLds && kVec && kList >= 3) {
+    if constexpr (kLds && kVec && (kList == 3 || kList == 4)) {
         switch (t.bv_steps) {
         case 0: launch_d<kLds, kVec, kMode, kList, 0>(t, p, verdict, gslot, cfg); return;
         case 1: launch_d<kLds, kVec, kMode, kList, 1>(t, p, verdict, gslot, cfg); return;
@@ -1107,11 +1151,32 @@ static void launch_cls(const Cls4Dev& t, const Pkts4& p, uint8_t* verdict, unsig
     launch_d<kLds, kVec, kMode, kList, -1>(t, p, verdict, gslot, cfg);
 }
 
+// source lookup variant: 0 interval search, 1 hash LPM, 2 hash LPM with one
+// length, 3 source trie (kMode 4)
+static inline int src_variant(const Cls4Dev& t) { return t.mode == 4 ? 3 : t.mode != 1 ? 0 : t.n_hash == 1 ? 2 : 1; }
+
 template <bool kLds, bool kVec>
 static void dispatch_cls(const Cls4Dev& t, const Pkts4& p, uint8_t* verdict, unsigned long long* gslot,
                          const LaunchCfg& cfg) {
-    // source lookup: 0 interval search, 1 hash LPM, 2 hash LPM with one length
-    const int src = t.mode != 1 ? 0 : t.n_hash == 1 ? 2 : 1;
+    const int src = src_variant(t);
+    if constexpr (kLds) {
+        // the source trie (sublist modes) and the wide cells (LDS-resident images only)
+        if (src == 3 || t.list_mode >= 5) {
+#define CLS_TW_CASES(L)                                                                       \
+    case 4 * L + 0: launch_cls<kLds, kVec, 0, L>(t, p, verdict, gslot, cfg); return;          \
+    case 4 * L + 1: launch_cls<kLds, kVec, 1, L>(t, p, verdict, gslot, cfg); return;          \
+    case 4 * L + 2: launch_cls<kLds, kVec, 2, L>(t, p, verdict, gslot, cfg); return;          \
+    case 4 * L + 3: launch_cls<kLds, kVec, 4, L>(t, p, verdict, gslot, cfg); return;
+            switch (src + 4 * int(t.list_mode)) {
+                case 4 * 3 + 3: launch_cls<kLds, kVec, 4, 3>(t, p, verdict, gslot, cfg); return;
+                case 4 * 4 + 3: launch_cls<kLds, kVec, 4, 4>(t, p, verdict, gslot, cfg); return;
+                CLS_TW_CASES(5)
+                CLS_TW_CASES(6)
+            default: return;
+            }
+#undef CLS_TW_CASES
+        }
+    }
 #define CLS_SRC_CASES(L)                                                                   \
     case 3 * L + 0: launch_cls<kLds, kVec, 0, L>(t, p, verdict, gslot, cfg); break;        \
     case 3 * L + 1: launch_cls<kLds, kVec, 1, L>(t, p, verdict, gslot, cfg); break;        \
@@ -1201,9 +1266,24 @@ static void dispatch16(const Cls4Dev& t, const Fe16& fe, const Pkts16& p, uint8_
 template <bool kLds>
 static void dispatch_slots4(const Cls4Dev& t, const Pkts4& p, uint32_t* out, const LaunchCfg& cfg) {
     uint8_t* o = reinterpret_cast<uint8_t*>(out);
-    const int src = t.mode != 1 ? 0 : t.n_hash == 1 ? 2 : 1;
+    const int src = src_variant(t);
     if constexpr (kLds) {
         auto al = [](const void* q, uintptr_t a) { return (reinterpret_cast<uintptr_t>(q) & (a - 1)) == 0; };
+        if (src == 3 || t.list_mode >= 5) {           // source trie / wide cells
+#define CLS_SLOTTW_CASES(L)                                                                        \
+    case 4 * L + 0: launch_d<true, false, 0, L, -1, 2>(t, p, o, nullptr, cfg); return;             \
+    case 4 * L + 1: launch_d<true, false, 1, L, -1, 2>(t, p, o, nullptr, cfg); return;             \
+    case 4 * L + 2: launch_d<true, false, 2, L, -1, 2>(t, p, o, nullptr, cfg); return;             \
+    case 4 * L + 3: launch_d<true, false, 4, L, -1, 2>(t, p, o, nullptr, cfg); return;
+            switch (src + 4 * int(t.list_mode)) {
+                case 4 * 3 + 3: launch_d<true, false, 4, 3, -1, 2>(t, p, o, nullptr, cfg); return;
+                case 4 * 4 + 3: launch_d<true, false, 4, 4, -1, 2>(t, p, o, nullptr, cfg); return;
+                CLS_SLOTTW_CASES(5)
+                CLS_SLOTTW_CASES(6)
+            default: return;
+            }
+#undef CLS_SLOTTW_CASES
+        }
         if (al(p.src, 16) && al(p.dst, 16) && al(p.dport, 8) && al(p.proto, 4) && al(out, 16)) {
 #define CLS_SLOTV_CASES(L)                                                                         \
     case 3 * L + 0: launch_d<true, true, 0, L, -1, 2>(t, p, o, nullptr, cfg); return;              \
