@@ -55,21 +55,26 @@ def test_forced_trie_wide_match_oracle(eng, monkeypatch, seed, trie, wide):
     np.testing.assert_array_equal(c, oc)
 
 
-@pytest.mark.parametrize("budget", [None, 24 * 1024])
-def test_wide_cells_counter_tiers(eng, monkeypatch, budget):
-    """Wide cells with every slot in LDS, and with a budget that leaves most
-    slots to the global counters."""
+@pytest.mark.parametrize("partial", [False, True])
+def test_wide_cells_counter_tiers(eng, monkeypatch, partial):
+    """Wide cells with every slot in LDS, and with a budget that leaves two
+    thirds of the slots to the global counters."""
+    from cls_image import Image, compile_blob
+    from vpp_amd import _abi
     monkeypatch.setenv("CONTIVCLS_ORIENT", "src")
     monkeypatch.setenv("CONTIVCLS_WIDE", "1")
-    if budget:
-        monkeypatch.setenv("CONTIVCLS_LDS_BUDGET", str(budget))
     rules, pool = single_port_acl(77, 400, n_prefixes=120)
+    if partial:
+        h = Image(compile_blob(_abi.CRules(rules))).h
+        a16 = lambda x: (x + 15) & ~15
+        budget = h.img_bytes + h.n_hot * 256 + a16(2 * max(h.n_hot, h.n_ctr // 3))
+        monkeypatch.setenv("CONTIVCLS_LDS_BUDGET", str(budget))
     tr = random_traffic(5, 200000, pool)
     t = eng.put_table("tiers", rules)
     try:
         info = t.info()
         assert info["list_mode"] in (5, 6) and info["lds_resident"] == 1
-        if budget:
+        if partial:
             assert info["n_lctr"] < info["n_slots"]
         v, c = eng.classify(t, tr["src"], tr["dst"], tr["dport"], tr["proto"])
     finally:

@@ -183,7 +183,8 @@ def test_export_import_round_trip():
 
 def test_committed_tables_follow_the_cache(sink):
     """With an engine the renderer keeps one compiled table per committed
-    IngressOrientation table (pod-group locals + global), replaced on change."""
+    IngressOrientation table (pod-group locals + global), replaced on change,
+    and one per installed session-rule table (global + per app namespace)."""
     from test_traffic_cpu import _StubEngine
     eng = _StubEngine()
     c = contiv((POD1, POD1_NS), (POD2, POD2_NS))
@@ -192,8 +193,11 @@ def test_committed_tables_follow_the_cache(sink):
     assert rend.local_rule_table(POD1) is not None and rend.local_rule_table(POD2) is not None
     g = rend.global_rule_table()
     assert [repr(r) for r in g.rules] == [repr(r) for r in rend.cache.get_global_table().rules]
-    assert len(eng.live) == 3
+    n_sess = len(rend.sessions.tables)
+    assert n_sess == 1 + sum(1 for t in sink.local_table.values() if t)
+    assert len(eng.live) == 3 + n_sess
     _two_pods_second_txn(rend, False)
-    assert rend.global_rule_table() is not g and len(eng.live) == 3
+    assert rend.global_rule_table() is not g
+    assert len(eng.live) == 3 + len(rend.sessions.tables)
     rend.close()
     assert not eng.live

@@ -13,12 +13,15 @@ dump :241-251, request / error counters).
 
 Session rules are the control-plane encoding only: the reference never
 evaluates a packet against them (the mock stores rules and answers HasRule;
-VPP's session-table lookup is external).  Packet evaluation for this renderer
-is defined by the build as TestTraffic semantics (renderer_mock.go:105-145)
-over the IngressOrientation tables the renderer commits -- each pod's local
-table and the global table -- and runs on the GPU through
-vpp_amd.renderer.traffic.RuleTable when the renderer is given an engine
-(parity unpinned by reference fixtures).
+VPP's session-table lookup is external).  With an engine the renderer
+evaluates packets two ways on the GPU (parity unpinned by reference
+fixtures):
+  * TestTraffic semantics (renderer_mock.go:105-145) over the
+    IngressOrientation tables it commits -- each pod's local table and the
+    global table (vpp_amd.renderer.traffic.RuleTable, ``rule_tables``);
+  * the session rules the sink holds, as exported (deny-all split covering
+    IPv4 only, allow-all and self rules not installed):
+    vpp_amd.renderer.sessions.SessionEvaluator, ``sessions``.
 """
 from __future__ import annotations
 
@@ -315,6 +318,7 @@ class Renderer:
         self.engine = engine
         self.cache: Optional[RendererCache] = None
         self.rule_tables: Dict[str, object] = {}     # table id -> traffic.RuleTable
+        self.sessions = None                         # sessions.SessionEvaluator of the sink's rules
 
     def init(self) -> "Renderer":
         self.cache = RendererCache()
@@ -341,7 +345,11 @@ class Renderer:
     def _sync_rule_tables(self):
         if self.engine is None:
             return
+        from .sessions import SessionEvaluator
         from .traffic import RuleTable
+        if self.sessions is None:
+            self.sessions = SessionEvaluator(self.engine, self.sink)
+        self.sessions.sync()
         want = {}
         g = self.cache.get_global_table()
         want[GLOBAL_TABLE_ID] = g
@@ -366,6 +374,8 @@ class Renderer:
         for t in self.rule_tables.values():
             t.close()
         self.rule_tables.clear()
+        if self.sessions is not None:
+            self.sessions.close()
 
 
 class RendererTxn:
