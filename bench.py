@@ -241,16 +241,24 @@ def main():
                 r.record(side)
                 reduced[b] = r
 
-    # Settle the clocks independently of --warmup: untimed steps until at
-    # least --settle-ms of wall time has passed with the GPU busy (the first
-    # ~10 ms of work run at lower clocks), then the counted warm-up steps.
+    # Settle the clocks independently of --warmup: untimed steps for at least
+    # --settle-ms of wall time with the GPU busy (the first ~10 ms of work run
+    # at lower clocks), then the counted warm-up steps.  Every rank runs the
+    # same number of steps (each step may hold a collective): 8 steps are
+    # timed, the count for the rest is the max over the ranks.
     i = 0
     t_settle = time.perf_counter()
-    while (time.perf_counter() - t_settle) * 1e3 < args.settle_ms:
-        for _ in range(8):
-            step(i, False)
-            i += 1
-        torch.cuda.synchronize()
+    for _ in range(8):
+        step(i, False)
+        i += 1
+    torch.cuda.synchronize()
+    per = (time.perf_counter() - t_settle) / 8
+    more = max(0, int(np.ceil((args.settle_ms / 1e3 - 8 * per) / max(per, 1e-6))))
+    more = int(D.max_over_ranks(float(more), dev))
+    for _ in range(more):
+        step(i, False)
+        i += 1
+    torch.cuda.synchronize()
     settle_ms = (time.perf_counter() - t_settle) * 1e3
     for _ in range(args.warmup):
         step(i, False)

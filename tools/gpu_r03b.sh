@@ -6,7 +6,7 @@ OUT=$ROOT/gpurun_out/${1:-r03b}
 mkdir -p $OUT
 cd $ROOT
 echo "pytest (changed GPU tests)"
-timeout -k 10 900 python -u -m pytest tests/test_gpu_trie_wide.py tests/test_gpu_sessions.py tests/test_gpu_dist.py tests/test_gpu_acl_config.py tests/test_gpu_parity.py -m gpu -x -v --timeout 300 --timeout-method thread > $OUT/pytest.log 2>&1 || { tail -60 $OUT/pytest.log; exit 1; }
+timeout -k 10 900 python -u -m pytest tests/test_gpu_trie_wide.py tests/test_gpu_sessions.py tests/test_gpu_dist.py tests/test_gpu_acl_config.py tests/test_gpu_parity.py -m gpu -x -v --timeout 170 --timeout-method thread > $OUT/pytest.log 2>&1 || { tail -60 $OUT/pytest.log; exit 1; }
 tail -3 $OUT/pytest.log
 for i in 1 2; do
   timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 --cpu-sample 0 > $OUT/bench_w5_$i.json 2> $OUT/bench_w5_$i.err
