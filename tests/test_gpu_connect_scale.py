@@ -239,3 +239,17 @@ def test_device_batch_unknown_interface_is_failure():
         assert np.array_equal(got[~bad], want)
     finally:
         eng.close()
+
+
+@pytest.mark.parametrize("fam", [4, 16])
+@pytest.mark.parametrize("count", [False, True])
+def test_per_lane_kernel_matches_oracle(fam, count, monkeypatch):
+    """The per-lane connection kernel (CONTIVCLS_CONN_SORTED=0; the default
+    sorts the linear scans by ACL): the same verdicts and counters."""
+    from vpp_amd.engine import Engine
+    monkeypatch.setenv("CONTIVCLS_CONN_SORTED", "0")
+    eng = Engine()
+    try:
+        _run(eng, 11, "linear", fam, count=count, n=8000, n_local=12)
+    finally:
+        eng.close()
