@@ -243,22 +243,19 @@ def main():
 
     # Settle the clocks independently of --warmup: untimed steps for at least
     # --settle-ms of wall time with the GPU busy (the first ~10 ms of work run
-    # at lower clocks), then the counted warm-up steps.  Every rank runs the
-    # same number of steps (each step may hold a collective): 8 steps are
-    # timed, the count for the rest is the max over the ranks.
+    # at lower clocks), then the counted warm-up steps.  Steps go in rounds
+    # of 8, and every rank runs the same rounds (each step may hold a
+    # collective): another round while any rank is short of the time.
     i = 0
     t_settle = time.perf_counter()
-    for _ in range(8):
-        step(i, False)
-        i += 1
-    torch.cuda.synchronize()
-    per = (time.perf_counter() - t_settle) / 8
-    more = max(0, int(np.ceil((args.settle_ms / 1e3 - 8 * per) / max(per, 1e-6))))
-    more = int(D.max_over_ranks(float(more), dev))
-    for _ in range(more):
-        step(i, False)
-        i += 1
-    torch.cuda.synchronize()
+    while True:
+        for _ in range(8):
+            step(i, False)
+            i += 1
+        torch.cuda.synchronize()
+        short = (time.perf_counter() - t_settle) * 1e3 < args.settle_ms
+        if not D.max_over_ranks(1.0 if short else 0.0, dev):
+            break
     settle_ms = (time.perf_counter() - t_settle) * 1e3
     for _ in range(args.warmup):
         step(i, False)

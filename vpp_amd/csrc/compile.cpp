@@ -1086,8 +1086,10 @@ static bool build_cls4_one(const std::vector<SemRule>& sem, uint32_t n_rules, Cl
     std::vector<uint32_t>& w = img.words;
     // trie: the source trie replaces the interval search (mode 0 only);
     // wide: list modes 3, 4 with the cells in global memory (gcells)
+    const uint32_t n_hash0 = img.n_hash;
     auto serialise = [&](uint32_t lm, bool trie, bool wide) -> bool {
         img.mode = trie ? 4u : mode0;
+        img.n_hash = trie ? 0u : n_hash0;                 // the trie replaces the hash LPM
         img.off_trie = img.trie_depth = 0;
         img.gcells.clear();
         img.ctr_rule = lm >= 3 ? ctr3 : ctr_base_rule;
@@ -1340,9 +1342,20 @@ static bool build_cls4_one(const std::vector<SemRule>& sem, uint32_t n_rules, Cl
     const char* wenv = std::getenv("CONTIVCLS_WIDE");
     const int tmode = tenv ? std::atoi(tenv) : -1;
     const bool wide_first = wenv && std::atoi(wenv) == 1, wide_never = wenv && std::atoi(wenv) == 0;
-    const bool trie_ok = mode0 == 0 && !opt && tmode != 0;
+    // (the 16-byte core searching reps takes them too; not the OTHER image).
+    // Behind a hash LPM the trie is the second choice (two probes beat it
+    // when the hash tables fit; large ones -- many prefixes of few lengths,
+    // e.g. reps -- do not).
+    const bool trie_ok = (mode0 == 0 || mode0 == 1) && !(opt && (opt->other || opt->ext_src)) && tmode != 0;
     auto try_fit = [&](uint32_t lm, bool wide, bool partial) {
-        for (int tr = trie_ok && lm >= 3 ? 1 : 0; tr >= (tmode == 1 && trie_ok && lm >= 3 ? 1 : 0); --tr) {
+        int cand[2] = {0, -1};
+        if (trie_ok && lm >= 3) {
+            if (tmode == 1) cand[0] = 1;
+            else if (mode0 == 0) cand[0] = 1, cand[1] = 0;
+            else cand[1] = 1;
+        }
+        for (int tr : cand) {
+            if (tr < 0) continue;
             if (!serialise(lm, tr != 0, wide)) continue;
             const bool ok = cell_ok(lm) && place_counters(img, budget, partial);
             if (dbg)
@@ -1353,7 +1366,7 @@ static bool build_cls4_one(const std::vector<SemRule>& sem, uint32_t n_rules, Cl
         }
         return false;
     };
-    const bool wide_ok = lmode_w >= 3 && !opt && !wide_never;
+    const bool wide_ok = lmode_w >= 3 && !(opt && opt->other) && !wide_never;
     if (wide_ok && wide_first && try_fit(lmode_w, true, true)) return true;
     for (int partial = 0; partial < 2; ++partial)
         for (uint32_t lm : seq)

@@ -1211,7 +1211,7 @@ static void launch16_cls(const Cls4Dev& t, const Fe16& fe, const Pkts16& p, uint
             return;
         }
     }
-    if constexpr (kLds && kList >= 3) {
+    if constexpr (kLds && (kList == 3 || kList == 4)) {
         switch (t.bv_steps) {
         case 0: launch16_d<kLds, kMode, kList, 0, false, kFe>(t, fe, p, verdict, gslot, cfg); return;
         case 1: launch16_d<kLds, kMode, kList, 1, false, kFe>(t, fe, p, verdict, gslot, cfg); return;
@@ -1240,11 +1240,31 @@ static void dispatch16(const Cls4Dev& t, const Fe16& fe, const Pkts16& p, uint8_
         case 2: launch16_cls<kLds, 3, 2, 1>(t, fe, p, verdict, gslot, cfg); break;
         case 3: launch16_cls<kLds, 3, 3, 1>(t, fe, p, verdict, gslot, cfg); break;
         case 4: launch16_cls<kLds, 3, 4, 1>(t, fe, p, verdict, gslot, cfg); break;
+        case 5: if constexpr (kLds) launch16_cls<kLds, 3, 5, 1>(t, fe, p, verdict, gslot, cfg); break;
+        case 6: if constexpr (kLds) launch16_cls<kLds, 3, 6, 1>(t, fe, p, verdict, gslot, cfg); break;
         default: break;
         }
         return;
     }
-    const int src = t.mode != 1 ? 0 : t.n_hash == 1 ? 2 : 1;
+    const int src = src_variant(t);
+    if constexpr (kLds) {
+        // the source trie over reps (sublist modes) and the wide cells (LDS-resident images only)
+        if (src == 3 || t.list_mode >= 5) {
+#define CLS16_TW_CASES(L)                                                                     \
+    case 4 * L + 0: launch16_cls<kLds, 0, L, 0>(t, fe, p, verdict, gslot, cfg); return;       \
+    case 4 * L + 1: launch16_cls<kLds, 1, L, 0>(t, fe, p, verdict, gslot, cfg); return;       \
+    case 4 * L + 2: launch16_cls<kLds, 2, L, 0>(t, fe, p, verdict, gslot, cfg); return;       \
+    case 4 * L + 3: launch16_cls<kLds, 4, L, 0>(t, fe, p, verdict, gslot, cfg); return;
+            switch (src + 4 * int(t.list_mode)) {
+                case 4 * 3 + 3: launch16_cls<kLds, 4, 3, 0>(t, fe, p, verdict, gslot, cfg); return;
+                case 4 * 4 + 3: launch16_cls<kLds, 4, 4, 0>(t, fe, p, verdict, gslot, cfg); return;
+                CLS16_TW_CASES(5)
+                CLS16_TW_CASES(6)
+            default: return;
+            }
+#undef CLS16_TW_CASES
+        }
+    }
 #define CLS16_SRC_CASES(L)                                                                  \
     case 3 * L + 0: launch16_cls<kLds, 0, L, 0>(t, fe, p, verdict, gslot, cfg); break;      \
     case 3 * L + 1: launch16_cls<kLds, 1, L, 0>(t, fe, p, verdict, gslot, cfg); break;      \
@@ -1326,11 +1346,30 @@ static void dispatch_slots16(const Cls4Dev& t, const Fe16& fe, const Pkts16& p, 
         case 2: launch16_d<kLds, 3, 2, -1, false, 1, 2>(t, fe, p, o, nullptr, cfg); break;
         case 3: launch16_d<kLds, 3, 3, -1, false, 1, 2>(t, fe, p, o, nullptr, cfg); break;
         case 4: launch16_d<kLds, 3, 4, -1, false, 1, 2>(t, fe, p, o, nullptr, cfg); break;
+        case 5: if constexpr (kLds) launch16_d<kLds, 3, 5, -1, false, 1, 2>(t, fe, p, o, nullptr, cfg); break;
+        case 6: if constexpr (kLds) launch16_d<kLds, 3, 6, -1, false, 1, 2>(t, fe, p, o, nullptr, cfg); break;
         default: break;
         }
         return;
     }
-    const int src = t.mode != 1 ? 0 : t.n_hash == 1 ? 2 : 1;
+    const int src = src_variant(t);
+    if constexpr (kLds) {
+        if (src == 3 || t.list_mode >= 5) {
+#define CLS16_SLOTTW_CASES(L)                                                                      \
+    case 4 * L + 0: launch16_d<kLds, 0, L, -1, false, 0, 2>(t, fe, p, o, nullptr, cfg); return;    \
+    case 4 * L + 1: launch16_d<kLds, 1, L, -1, false, 0, 2>(t, fe, p, o, nullptr, cfg); return;    \
+    case 4 * L + 2: launch16_d<kLds, 2, L, -1, false, 0, 2>(t, fe, p, o, nullptr, cfg); return;    \
+    case 4 * L + 3: launch16_d<kLds, 4, L, -1, false, 0, 2>(t, fe, p, o, nullptr, cfg); return;
+            switch (src + 4 * int(t.list_mode)) {
+                case 4 * 3 + 3: launch16_d<kLds, 4, 3, -1, false, 0, 2>(t, fe, p, o, nullptr, cfg); return;
+                case 4 * 4 + 3: launch16_d<kLds, 4, 4, -1, false, 0, 2>(t, fe, p, o, nullptr, cfg); return;
+                CLS16_SLOTTW_CASES(5)
+                CLS16_SLOTTW_CASES(6)
+            default: return;
+            }
+#undef CLS16_SLOTTW_CASES
+        }
+    }
 #define CLS16_SLOT_CASES(L)                                                                        \
     case 3 * L + 0: launch16_d<kLds, 0, L, -1, false, 0, 2>(t, fe, p, o, nullptr, cfg); break;     \
     case 3 * L + 1: launch16_d<kLds, 1, L, -1, false, 0, 2>(t, fe, p, o, nullptr, cfg); break;     \
