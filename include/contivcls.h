@@ -364,6 +364,10 @@ typedef struct cls_image_v4_header {
                                   cells, uint2 {pointer table byte address, counter base} per
                                   (class, protocol); n_gcells u32 words */
     uint32_t n_gcells;
+    uint32_t sub4;             /* list modes 3-6: sublists as 4-ary node trees of bv_steps_d levels
+                                  (16-B nodes {k1, k2, k3, first child | leaf outcomes}; the
+                                  pointer tables hold root node byte addresses, or the outcome
+                                  when there are 0 levels); else the binary slot form */
 } cls_image_v4_header;
 int cls_compile_v4(const cls_rule* rules, uint32_t n_rules, void* blob, uint64_t cap,
                    uint64_t* need);

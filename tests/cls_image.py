@@ -200,7 +200,14 @@ class Image:
             st = img[((cell & 0x3FFF) * 4 + pc4) // 4]
             base = cell >> 14
         d = dst.astype(np.int64)
-        for i in range(int(self.h.bv_steps_d) - 1, -1, -1):
+        if self.h.sub4:
+            # 4-ary node trees: interior {k1, k2, k3, first child}, leaf {k1, k2, k3, outcomes}
+            L = int(self.h.bv_steps_d)
+            for lvl in range(L):
+                a = st // 4
+                c = (img[a] < d).astype(np.int64) + (img[a + 1] < d) + (img[a + 2] < d)
+                st = img[a + 3] + 16 * c if lvl + 1 < L else (img[a + 3] >> (8 * c)) & 0xFF
+        for i in range(int(self.h.bv_steps_d) - 1 if not self.h.sub4 else -1, -1, -1):
             a = ((st >> 13) + (8 << i)) // 4
             st = np.where(img[a] < d, img[a + 1], st)
         res = (st & 3).astype(np.uint32)

@@ -11,8 +11,9 @@ tail -3 $OUT/pytest.log
 for i in 1 2; do
   timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 --cpu-sample 0 > $OUT/bench_w5_$i.json 2> $OUT/bench_w5_$i.err
   timeout -k 10 300 python bench.py --cpu-sample 0 > $OUT/bench_w25_$i.json 2> $OUT/bench_w25_$i.err
+  CONTIVCLS_SUB4=0 timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 --cpu-sample 0 > $OUT/bench_bin_w5_$i.json 2> $OUT/bench_bin_w5_$i.err
 done
-python tools/bsum.py $OUT/bench_w*.json
+python tools/bsum.py $OUT/bench_w*.json $OUT/bench_bin*.json
 echo "gen-policy lists"
 timeout -k 10 600 python tools/genpolicy_bench.py --blocks 20 200 1000 > $OUT/genpolicy.jsonl 2> $OUT/genpolicy.err
 python tools/jl.py $OUT/genpolicy.jsonl workload rules list_mode lds_slots slots kernel_ms Gpps_kernel Gpps_wall

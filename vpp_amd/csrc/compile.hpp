@@ -162,6 +162,9 @@ struct Cls4Image {
     // byte offset into gcells (off_cells 0, row_bytes 8 x n_cells)
     std::vector<uint32_t> gcells;
     uint32_t sub_bytes = 0;        // modes 3, 4: end of the pointer tables (< 64 KiB)
+    // modes 3-6: the sublists as 4-ary node trees of bv_steps_d levels
+    // (pointer tables hold root node addresses), else the binary slot form
+    uint32_t sub4 = 0;
     // mode 4: port perfect hash at LDS 0: e = u32 at byte mulhi(port, mul) &
     // mask4, class x 4 = (e & 0xFFFF) == port ? e >> 16 : port_dflt
     uint32_t port_mul = 0, port_mask4 = 0, port_dflt = 0;

@@ -60,7 +60,8 @@ struct Cls4Dev {
     uint32_t hash_mul[kMaxHashLens], hash_shift1[kMaxHashLens];   // shift1 = 32 - 2 L
     uint32_t list_mode;        // 0 template scan, 1 bit vectors, 2 + global port classes,
                                // 3 port-filtered sublists, 4 + hashed port classes
-    uint32_t bv_steps;         // bit-vector search depth (max over lists, both dims)
+    uint32_t bv_steps;         // bit-vector search depth (max over lists, both dims); sub4: levels
+    uint32_t sub4;             // list modes 3-6: 4-ary sublist node trees (compile.hpp Cls4Image::sub4)
     uint32_t n_hot;            // slots [0, n_hot) are counted in per-lane LDS rows
     uint32_t off_hot;          // byte offset of the rows (n_hot x 64 u32) in LDS
     uint32_t off_ptop;         // list mode 2: port radix

@@ -331,6 +331,34 @@ __device__ __forceinline__ void classify_n(const Img<kLds>& im, const Cls4Dev& t
         if constexpr (CLS_ABLATE & 2) {
 #pragma unroll
             for (int q = 0; q < N; ++q) st[q] ^= dst[q] & 0x10000000u;   // keep dst live
+        } else if (t.sub4) {
+            // 4-ary node trees (compile.cpp sub4): L - 1 interior levels
+            // {k1, k2, k3, first child}, then the leaf {k1, k2, k3, outcomes};
+            // c = #(k_i < dst) picks the child / interval.  One ds_read_b128
+            // per level: half the binary form's dependent reads.  L = 0: the
+            // pointer table held the outcome.
+            const uint32_t L = kD >= 0 ? uint32_t(kD) : t.bv_steps;
+#pragma unroll
+            for (uint32_t l = 0; l + 1 < (kD >= 0 ? uint32_t(kD) : 4u); ++l) {
+                if (kD < 0 && l + 1 >= L) break;
+                uint4 e[N];
+#pragma unroll
+                for (int q = 0; q < N; ++q) e[q] = im.u128(st[q]);
+#pragma unroll
+                for (int q = 0; q < N; ++q)
+                    st[q] = e[q].w + 16u * (uint32_t(e[q].x < dst[q]) + uint32_t(e[q].y < dst[q]) +
+                                            uint32_t(e[q].z < dst[q]));
+            }
+            if (L > 0) {
+                uint4 e[N];
+#pragma unroll
+                for (int q = 0; q < N; ++q) e[q] = im.u128(st[q]);
+#pragma unroll
+                for (int q = 0; q < N; ++q) {
+                    const uint32_t c = uint32_t(e[q].x < dst[q]) + uint32_t(e[q].y < dst[q]) + uint32_t(e[q].z < dst[q]);
+                    st[q] = (e[q].w >> (8u * c)) & 0xFFu;
+                }
+            }
         } else {
         if constexpr (kD > 6) sub_step<6>(im, dst, st);
         if constexpr (kD > 5) sub_step<5>(im, dst, st);
