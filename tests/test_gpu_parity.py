@@ -81,12 +81,13 @@ VARIANTS = {  # kind -> (source lookup mode, list mode)
     "hash_sph": (1, 4), "search_sph": (0, 4),
     "hash_cbv": (1, 3), "search_cbv": (0, 3),
     "hash_pc": (1, 2), "search_pc": (0, 2), "hash_bv": (1, 1), "search_bv": (0, 1),
-    "hash_scan": (1, 0), "search_scan": (0, 0)}
+    "hash_scan": (1, 0), "search_scan": (0, 0),
+    "trie_sph": (4, 4), "trie_cbv": (4, 3)}
 
 
 def variant_acl(kind, seed):
     from aclgen import long_list_acl, many_ports_acl, single_port_acl
-    hashed = kind.startswith("hash")
+    hashed = kind.startswith("hash")                 # trie_*: the search_* tables over the source trie
     if kind.endswith("_sph"):
         return single_port_acl(seed * 13 + 1, 90, n_prefixes=3 if hashed else 24)
     if kind.endswith("scan"):
@@ -100,18 +101,36 @@ def variant_acl(kind, seed):
 @pytest.mark.parametrize("seed", range(3))
 @pytest.mark.parametrize("kind", sorted(VARIANTS))
 def test_all_kernel_variants(eng, seed, kind, monkeypatch):
-    """The ten classifier variants (hash-LPM / interval-search source lookup
-    x port-filtered sublists with hashed / radix port classes / bit vectors
+    """The classifier variants (hash-LPM / interval-search source lookup x
+    port-filtered sublists with hashed / radix port classes / bit vectors
     with global port classes / bit vectors with per-list port search /
-    template scan) against the oracle."""
+    template scan; the source trie x both sublist forms) against the oracle."""
     if kind.endswith("_pc"):
         monkeypatch.setenv("CONTIVCLS_LIST_MODE_MAX", "2")
+    # the interval search and the source trie each on the same tables
+    monkeypatch.setenv("CONTIVCLS_TRIE", "1" if kind.startswith("trie") else "0")
     from cls_image import Image, compile_blob
     from vpp_amd import _abi
     rules, pool = variant_acl(kind, seed)
     h = Image(compile_blob(_abi.CRules(rules))).h
     assert (h.mode, h.list_mode) == VARIANTS[kind], kind
     tr = random_traffic(seed + 11, 30000, pool)
+    _assert_same(_gpu(eng, rules, tr), _oracle(rules, tr))
+
+
+@pytest.mark.parametrize("seed", range(2))
+@pytest.mark.parametrize("kind", ["hash_sph", "search_cbv", "trie_sph"])
+def test_binary_sublist_form(eng, seed, kind, monkeypatch):
+    """The binary sublist form (CONTIVCLS_SUB4=0; the default is 4-ary node
+    trees) on the sublist variants."""
+    monkeypatch.setenv("CONTIVCLS_SUB4", "0")
+    monkeypatch.setenv("CONTIVCLS_TRIE", "1" if kind.startswith("trie") else "0")
+    from cls_image import Image, compile_blob
+    from vpp_amd import _abi
+    rules, pool = variant_acl(kind, seed)
+    h = Image(compile_blob(_abi.CRules(rules))).h
+    assert (h.mode, h.list_mode) == VARIANTS[kind] and h.sub4 == 0, kind
+    tr = random_traffic(seed + 21, 30000, pool)
     _assert_same(_gpu(eng, rules, tr), _oracle(rules, tr))
 
 
