@@ -328,7 +328,8 @@ typedef struct cls_image_v4_header {
     uint32_t n_bounds, search_top, n_classes, n_tmpl, n_list_entries, n_ctr, lds_bytes;
     uint32_t off_image, off_ctr_rule, off_lin;   /* byte offsets inside the blob */
     uint32_t total_bytes;
-    uint32_t mode;             /* source lookup: 0 interval search, 1 hash LPM, 4 trie */
+    uint32_t mode;             /* source lookup: 0 interval search, 1 hash LPM, 4 trie,
+                                  6 hash LPM with the cells inline in the entries */
     uint32_t default_class;    /* hash LPM: class when no hashed prefix matches */
     uint32_t n_hash;           /* hashed prefix lengths (ascending) */
     uint32_t hash_mask[3], hash_shift[3], hash_cap[3], off_hash[3];
@@ -368,6 +369,8 @@ typedef struct cls_image_v4_header {
                                   (16-B nodes {k1, k2, k3, first child | leaf outcomes}; the
                                   pointer tables hold root node byte addresses, or the outcome
                                   when there are 0 levels); else the binary slot form */
+    uint32_t dflt_cell[3];     /* mode 6 (hash LPM of one length, 16-B entries {key, cell TCP,
+                                  cell UDP, cell ICMP}): the cells of addresses no entry holds */
 } cls_image_v4_header;
 int cls_compile_v4(const cls_rule* rules, uint32_t n_rules, void* blob, uint64_t cap,
                    uint64_t* need);

@@ -78,8 +78,9 @@ def test_random_acls_both_kernels(eng, seed, n_rules, weird):
 
 
 VARIANTS = {  # kind -> (source lookup mode, list mode)
-    "hash_sph": (1, 4), "search_sph": (0, 4),
-    "hash_cbv": (1, 3), "search_cbv": (0, 3),
+    "hash_sph": (6, 4), "search_sph": (0, 4),       # hash_* sublists: cells inline in the entries (mode 6)
+    "hash_cbv": (6, 3), "search_cbv": (0, 3),
+    "hrow_sph": (1, 4), "hrow_cbv": (1, 3),         # CONTIVCLS_INLINE=0: entries hold class rows
     "hash_pc": (1, 2), "search_pc": (0, 2), "hash_bv": (1, 1), "search_bv": (0, 1),
     "hash_scan": (1, 0), "search_scan": (0, 0),
     "trie_sph": (4, 4), "trie_cbv": (4, 3)}
@@ -87,7 +88,7 @@ VARIANTS = {  # kind -> (source lookup mode, list mode)
 
 def variant_acl(kind, seed):
     from aclgen import long_list_acl, many_ports_acl, single_port_acl
-    hashed = kind.startswith("hash")                 # trie_*: the search_* tables over the source trie
+    hashed = kind.startswith(("hash", "hrow"))       # trie_*: the search_* tables over the source trie
     if kind.endswith("_sph"):
         return single_port_acl(seed * 13 + 1, 90, n_prefixes=3 if hashed else 24)
     if kind.endswith("scan"):
@@ -107,8 +108,10 @@ def test_all_kernel_variants(eng, seed, kind, monkeypatch):
     template scan; the source trie x both sublist forms) against the oracle."""
     if kind.endswith("_pc"):
         monkeypatch.setenv("CONTIVCLS_LIST_MODE_MAX", "2")
-    # the interval search and the source trie each on the same tables
+    # the interval search and the source trie each on the same tables; hash
+    # entries with inline cells and with rows
     monkeypatch.setenv("CONTIVCLS_TRIE", "1" if kind.startswith("trie") else "0")
+    monkeypatch.setenv("CONTIVCLS_INLINE", "0" if kind.startswith("hrow") else "1")
     from cls_image import Image, compile_blob
     from vpp_amd import _abi
     rules, pool = variant_acl(kind, seed)

@@ -9,10 +9,11 @@ export TMPDIR=/tmp
 echo "bench config 3"
 for i in 1 2; do
   timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 --cpu-sample 0 > $OUT/bench_w5_$i.json 2> $OUT/bench_w5_$i.err
-  CONTIVCLS_SUB4=0 timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 --cpu-sample 0 > $OUT/bench_bin_w5_$i.json 2> $OUT/bench_bin_w5_$i.err
+  CONTIVCLS_SUB4=0 CONTIVCLS_INLINE=0 timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 --cpu-sample 0 > $OUT/bench_r2_w5_$i.json 2> $OUT/bench_r2_w5_$i.err
+  CONTIVCLS_INLINE=0 timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 --cpu-sample 0 > $OUT/bench_sub4_w5_$i.json 2> $OUT/bench_sub4_w5_$i.err
 done
 timeout -k 10 300 python bench.py --cpu-sample 0 > $OUT/bench_w25.json 2> $OUT/bench_w25.err
-python tools/bsum.py $OUT/bench_w*.json $OUT/bench_bin*.json
+python tools/bsum.py $OUT/bench_w*.json $OUT/bench_r2*.json $OUT/bench_sub4*.json
 echo "connection batches"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/conn_prof -o run --output-format csv -- python3 tools/conn_bench.py --locals 12 > $OUT/conn12.json 2> $OUT/conn12.err
 CONTIVCLS_CONN_SORTED=0 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/conn_prof_perlane -o run --output-format csv -- python3 tools/conn_bench.py --locals 12 > $OUT/conn12_perlane.json 2> $OUT/conn12_perlane.err

@@ -114,7 +114,8 @@ class ImageHeader(C.Structure):
         ("port_dflt", C.c_uint32),
         ("n_hot", C.c_uint32), ("off_hot", C.c_uint32), ("n_lctr", C.c_uint32), ("ctr16", C.c_uint32),
         ("swap", C.c_uint32), ("off_other", C.c_uint32), ("off_trie", C.c_uint32), ("trie_depth", C.c_uint32),
-        ("off_gcells", C.c_uint32), ("n_gcells", C.c_uint32), ("sub4", C.c_uint32)]
+        ("off_gcells", C.c_uint32), ("n_gcells", C.c_uint32), ("sub4", C.c_uint32),
+        ("dflt_cell", C.c_uint32 * 3)]
 
 
 class Image16Header(C.Structure):

@@ -1098,6 +1098,8 @@ static bool build_cls4_one(const std::vector<SemRule>& sem, uint32_t n_rules, Cl
         L4 = std::max(L4, l);
     }
     const uint32_t n_hash0 = img.n_hash;
+    const char* ienv = std::getenv("CONTIVCLS_INLINE");         // 0: rows in the hash entries (A/B, tests)
+    const bool inline_ok = !(ienv && std::atoi(ienv) == 0) && ncell == 3;
     auto serialise = [&](uint32_t lm, bool trie, bool wide) -> bool {
         img.mode = trie ? 4u : mode0;
         img.n_hash = trie ? 0u : n_hash0;                 // the trie replaces the hash LPM
@@ -1226,14 +1228,27 @@ static bool build_cls4_one(const std::vector<SemRule>& sem, uint32_t n_rules, Cl
             w.insert(w.end(), bv.begin(), bv.end());
             w.resize(align4(uint32_t(w.size())));
         }
+        // Inline cells (one hashed prefix length, sublist cells in LDS): an
+        // entry carries its class's three cells, so the probe that finds the
+        // class also delivers the cell (src mode 6; no cell read after it)
+        img.hash_inline = inline_ok && img.mode == 1 && img.n_hash == 1 && lm >= 3 && !wide ? 1u : 0u;
         for (uint32_t i = 0; i < img.n_hash; ++i) {
+            w.resize(align4(uint32_t(w.size())));
             img.off_hash[i] = uint32_t(w.size()) * 4;
-            // entry {key, byte address of the class's cell row}
             for (uint64_t e : hash_tabs[i]) {
+                const uint32_t row = img.off_cells + uint32_t(e >> 32) * img.row_bytes;
                 w.push_back(uint32_t(e));
-                w.push_back(img.off_cells + uint32_t(e >> 32) * img.row_bytes);
+                if (img.hash_inline) {               // entry {key, cell TCP, cell UDP, cell ICMP}
+                    for (uint32_t k = 0; k < 3; ++k) w.push_back(w[row / 4 + k]);
+                } else {                             // entry {key, byte address of the class's cell row}
+                    w.push_back(row);
+                }
             }
             w.resize(align4(uint32_t(w.size())));
+        }
+        if (img.hash_inline) {
+            img.mode = 6;
+            for (uint32_t k = 0; k < 3; ++k) img.dflt_cell[k] = w[img.default_row / 4 + k];
         }
         if (lm >= 3 && sub4) {
             // 4-ary sublist nodes (16 B, LDS-aligned): a sublist of n

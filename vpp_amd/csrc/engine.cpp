@@ -512,6 +512,7 @@ static Cls4Dev cls4_dev(const Cls4Image& im, const DevBuf& d_img, const DevBuf& 
     cd.n_lctr = im.n_lctr;
     cd.ctr16 = im.ctr16;
     cd.sub4 = im.sub4;
+    for (int k = 0; k < 3; ++k) cd.dflt_cell[k] = im.dflt_cell[k];
     cd.off_trie = im.off_trie;
     cd.trie_depth = im.trie_depth;
     cd.gcells = im.gcells.empty() ? nullptr
@@ -1403,6 +1404,7 @@ static int write_blob(const Cls4Image* img, const std::vector<LinRule4>& lin, ui
         h.ctr16 = im.ctr16;
         h.swap = im.swap;
         h.sub4 = im.sub4;
+        for (int k = 0; k < 3; ++k) h.dflt_cell[k] = im.dflt_cell[k];
         h.off_trie = im.off_trie;
         h.trie_depth = im.trie_depth;
         h.n_gcells = uint32_t(im.gcells.size());

@@ -52,6 +52,7 @@ struct Cls4Dev {
     uint32_t n_rules;          // R
     uint32_t mode;             // 0 interval search, 1 hash LPM, 4 source trie
     uint32_t off_trie, trie_depth;   // mode 4: level 1 at off_trie (compile.cpp build_trie)
+    uint32_t dflt_cell[3];     // mode 6 (hash entries with inline cells): the default class's cells
     const uint8_t* gcells;     // list modes 5, 6: wide cells (uint2 {pointer table, counter base})
     uint32_t default_row;      // source lookup miss: byte address of the default class's cells
     uint32_t n_hash;

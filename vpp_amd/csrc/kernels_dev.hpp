@@ -279,7 +279,11 @@ __device__ __forceinline__ void classify_n(const Img<kLds>& im, const Cls4Dev& t
         for (int q = 0; q < N; ++q) pc[q] = im.u8(tp[q] + (dport[q] & 0xFFu));
     }
     uint32_t row[N];
-    if constexpr (CLS_ABLATE & 4) {
+    if constexpr (kMode == 6) {
+        // inline cells: the hash probe below gives the cell itself
+#pragma unroll
+        for (int q = 0; q < N; ++q) row[q] = 0u;
+    } else if constexpr (CLS_ABLATE & 4) {
 #pragma unroll
         for (int q = 0; q < N; ++q) row[q] = t.default_row + ((src[q] & 1u) ? 0u : 0u) + (src[q] & 0u);
 #pragma unroll
@@ -305,6 +309,32 @@ __device__ __forceinline__ void classify_n(const Img<kLds>& im, const Cls4Dev& t
                 cell[q] = row[q] + proto[q] + pc[q];
                 st[q] = cell[q] & 0x3Fu;
             }
+        } else if constexpr (kMode == 6) {
+            // src mode 6: one hashed prefix length, entries {key, cell TCP,
+            // cell UDP, cell ICMP} -- the two cuckoo probes deliver the cell
+            // (a miss: the default class's cells), no cell read after them
+            const uint32_t tab = t.off_hash[0], mask = t.hash_mask[0], mul = t.hash_mul[0];
+            const uint32_t s0 = t.hash_shift[0], s1 = t.hash_shift1[0], L = 32u - s0;
+            const uint32_t tab1 = __builtin_amdgcn_readfirstlane(tab + 16u * t.hash_cap[0]);
+            uint4 e0[N], e1[N];
+            uint32_t key[N];
+#pragma unroll
+            for (int q = 0; q < N; ++q) {
+                key[q] = src[q] & mask;
+                const uint32_t h = key[q] * mul;
+                e0[q] = im.u128(tab + 16u * (h >> s0));
+                e1[q] = im.u128(tab1 + 16u * __builtin_amdgcn_ubfe(h, s1, L));
+            }
+#pragma unroll
+            for (int q = 0; q < N; ++q) {
+                const uint32_t p = proto[q];
+                const uint32_t c0 = p == 0u ? e0[q].y : p == 1u ? e0[q].z : e0[q].w;
+                const uint32_t c1 = p == 0u ? e1[q].y : p == 1u ? e1[q].z : e1[q].w;
+                const uint32_t cd = p == 0u ? t.dflt_cell[0] : p == 1u ? t.dflt_cell[1] : t.dflt_cell[2];
+                cell[q] = e0[q].x == key[q] ? c0 : (e1[q].x == key[q] ? c1 : cd);
+            }
+#pragma unroll
+            for (int q = 0; q < N; ++q) st[q] = im.u32(((cell[q] & 0x3FFFu) << 2) + pc[q]);
         } else if constexpr (kWide) {
             // cell = {pointer table byte address, counter base}; cell[q] keeps
             // the base (the slot below)
@@ -1181,20 +1211,28 @@ static void launch_cls(const Cls4Dev& t, const Pkts4& p, uint8_t* verdict, unsig
 
 // source lookup variant: 0 interval search, 1 hash LPM, 2 hash LPM with one
 // length, 3 source trie (kMode 4)
-static inline int src_variant(const Cls4Dev& t) { return t.mode == 4 ? 3 : t.mode != 1 ? 0 : t.n_hash == 1 ? 2 : 1; }
+static inline int src_variant(const Cls4Dev& t) {
+    return t.mode == 6 ? 4 : t.mode == 4 ? 3 : t.mode != 1 ? 0 : t.n_hash == 1 ? 2 : 1;
+}
 
 template <bool kLds, bool kVec>
 static void dispatch_cls(const Cls4Dev& t, const Pkts4& p, uint8_t* verdict, unsigned long long* gslot,
                          const LaunchCfg& cfg) {
     const int src = src_variant(t);
     if constexpr (kLds) {
-        // the source trie (sublist modes) and the wide cells (LDS-resident images only)
-        if (src == 3 || t.list_mode >= 5) {
+        // the source trie (sublist modes), inline hash cells (sublist modes,
+        // LDS cells) and the wide cells (LDS-resident images only)
+        if (src >= 3 || t.list_mode >= 5) {
 #define CLS_TW_CASES(L)                                                                       \
     case 4 * L + 0: launch_cls<kLds, kVec, 0, L>(t, p, verdict, gslot, cfg); return;          \
     case 4 * L + 1: launch_cls<kLds, kVec, 1, L>(t, p, verdict, gslot, cfg); return;          \
     case 4 * L + 2: launch_cls<kLds, kVec, 2, L>(t, p, verdict, gslot, cfg); return;          \
     case 4 * L + 3: launch_cls<kLds, kVec, 4, L>(t, p, verdict, gslot, cfg); return;
+            if (src == 4) {
+                if (t.list_mode == 3) launch_cls<kLds, kVec, 6, 3>(t, p, verdict, gslot, cfg);
+                else if (t.list_mode == 4) launch_cls<kLds, kVec, 6, 4>(t, p, verdict, gslot, cfg);
+                return;
+            }
             switch (src + 4 * int(t.list_mode)) {
                 case 4 * 3 + 3: launch_cls<kLds, kVec, 4, 3>(t, p, verdict, gslot, cfg); return;
                 case 4 * 4 + 3: launch_cls<kLds, kVec, 4, 4>(t, p, verdict, gslot, cfg); return;
@@ -1317,6 +1355,11 @@ static void dispatch_slots4(const Cls4Dev& t, const Pkts4& p, uint32_t* out, con
     const int src = src_variant(t);
     if constexpr (kLds) {
         auto al = [](const void* q, uintptr_t a) { return (reinterpret_cast<uintptr_t>(q) & (a - 1)) == 0; };
+        if (src == 4) {                               // inline hash cells
+            if (t.list_mode == 3) launch_d<true, false, 6, 3, -1, 2>(t, p, o, nullptr, cfg);
+            else if (t.list_mode == 4) launch_d<true, false, 6, 4, -1, 2>(t, p, o, nullptr, cfg);
+            return;
+        }
         if (src == 3 || t.list_mode >= 5) {           // source trie / wide cells
 #define CLS_SLOTTW_CASES(L)                                                                        \
     case 4 * L + 0: launch_d<true, false, 0, L, -1, 2>(t, p, o, nullptr, cfg); return;             \
