@@ -15,7 +15,8 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # CONTIVCLS_LIB: diagnostics only (A/B timing of kernel build variants)
 LIB_PATH = os.environ.get("CONTIVCLS_LIB") or os.path.join(_HERE, "libcontivcls.so")
 
-SOURCES = ("kernels.hip", "kernels.hpp", "compile.cpp", "compile.hpp", "engine.cpp", "goparse.hpp")
+SOURCES = ("kernels.hip", "kernels_dev.hpp", "k4_ldsv.hip", "k4_rest.hip", "k16.hip", "kernels.hpp", "compile.cpp",
+           "compile.hpp", "engine.cpp", "goparse.hpp")
 
 
 def source_hash() -> str:

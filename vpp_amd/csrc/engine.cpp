@@ -367,6 +367,9 @@ static int table_put_locked(cls_engine* e, const char* name, const cls_rule* rul
             t->has_cls = true;
             t->kernel = 1;
             t->lds_resident = t->img.lds_ok && t->img.lds_bytes + kLdsReserved <= uint32_t(max_lds_bytes());
+            // the trie, inline hash cells and wide cells exist only in LDS-resident images
+            if (!t->lds_resident && (t->img.mode == 4 || t->img.mode == 6 || t->img.list_mode >= 5))
+                return fail(e, CLS_E_INVAL, "compiler produced an LDS-only image that does not fit LDS");
             rc = upload(e, t->d_img, t->img);
             if (rc == CLS_OK) rc = upload(e, t->d_oimg, t->oimg);
             if (rc == CLS_OK) rc = upload_slot_rule(e, t->d_slot_rule, t->img, t->oimg);
@@ -391,6 +394,8 @@ static int table_put_locked(cls_engine* e, const char* name, const cls_rule* rul
             const Cls4Image& c = q.img.core;
             q.lin = linear4(q.img.sem);
             q.lds_resident = c.lds_ok && c.lds_bytes + kLdsReserved <= uint32_t(max_lds_bytes());
+            if (!q.lds_resident && (c.mode == 4 || c.mode == 6 || c.list_mode >= 5))
+                return fail(e, CLS_E_INVAL, "compiler produced an LDS-only 16-byte image that does not fit LDS");
             rc = upload(e, q.d_img, c);
             if (rc == CLS_OK) rc = upload(e, q.d_oimg, q.oimg);
             if (rc == CLS_OK) rc = upload_slot_rule(e, q.d_slot_rule, c, q.oimg);
