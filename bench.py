@@ -212,16 +212,20 @@ def main():
     sev = []                                  # (before, after) each timed step on the launch stream
     torch.cuda.synchronize()
 
+    # Every step runs on one explicit stream (`main`): the engine launches on
+    # torch's current stream, so the step events and the all-reduce's wait
+    # event bracket the classify itself.
+    main = torch.cuda.Stream(device=dev)
+
     def step(i, timing):
         b = i % nbuf
-        main = torch.cuda.current_stream()
         if timing:
             s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s0.record(main)
         if reduced[b] is not None:
             main.wait_event(reduced[b])
         eng.classify(table, pk["src"], pk["dst"], pk["dport"], pk["proto"], verdict=verdict,
-                     counters=counters[b], timing=timing)
+                     counters=counters[b], timing=timing, stream=main)
         if timing:
             s1.record(main)
             sev.append((s0, s1))

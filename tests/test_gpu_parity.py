@@ -78,16 +78,39 @@ def test_random_acls_both_kernels(eng, seed, n_rules, weird):
 
 
 VARIANTS = {  # kind -> (source lookup mode, list mode)
-    "hash_sph": (6, 4), "search_sph": (0, 4),       # hash_* sublists: cells inline in the entries (mode 6)
-    "hash_cbv": (6, 3), "search_cbv": (0, 3),
-    "hrow_sph": (1, 4), "hrow_cbv": (1, 3),         # CONTIVCLS_INLINE=0: entries hold class rows
+    "hash_sph": (1, 4), "search_sph": (0, 4),       # hash_*: several hashed prefix lengths
+    "hash_cbv": (1, 3), "search_cbv": (0, 3),
+    "inl_sph": (6, 4), "inl_cbv": (6, 3),           # /32 sources: one length, cells inline (mode 6)
+    "hrow_sph": (1, 4), "hrow_cbv": (1, 3),         # the same with CONTIVCLS_INLINE=0: entries hold rows
     "hash_pc": (1, 2), "search_pc": (0, 2), "hash_bv": (1, 1), "search_bv": (0, 1),
     "hash_scan": (1, 0), "search_scan": (0, 0),
     "trie_sph": (4, 4), "trie_cbv": (4, 3)}
 
 
+def _host_sources(rules, pool, seed):
+    """Every source prefix of the rules (and the traffic pool) as a /32 host
+    inside it: one hashed prefix length, so the compiler can put the cells
+    inline in the hash entries (src mode 6)."""
+    import random
+    from aclgen import _v4
+    rng = random.Random(seed)
+    host = {}
+    for a, ln in pool.v4:
+        host[(a, ln)] = (a | (rng.getrandbits(32) & ((1 << (32 - ln)) - 1) if ln < 32 else a), 32)
+    pool.v4 = [host[x] for x in pool.v4]
+    by_cidr = {"%s/%d" % (_v4(a), ln): "%s/32" % _v4(h[0]) for (a, ln), h in host.items()}
+    for r in rules:
+        ip = r.matches.ip_rule.ip if r.matches and r.matches.ip_rule else None
+        if ip is not None and ip.source_network:
+            ip.source_network = by_cidr.get(ip.source_network, ip.source_network.split("/")[0] + "/32")
+    return rules, pool
+
+
 def variant_acl(kind, seed):
     from aclgen import long_list_acl, many_ports_acl, single_port_acl
+    if kind.startswith("inl"):
+        rules, pool = variant_acl("hrow" + kind[3:], seed)
+        return _host_sources(rules, pool, seed)
     hashed = kind.startswith(("hash", "hrow"))       # trie_*: the search_* tables over the source trie
     if kind.endswith("_sph"):
         return single_port_acl(seed * 13 + 1, 90, n_prefixes=3 if hashed else 24)
@@ -112,6 +135,7 @@ def test_all_kernel_variants(eng, seed, kind, monkeypatch):
     # entries with inline cells and with rows
     monkeypatch.setenv("CONTIVCLS_TRIE", "1" if kind.startswith("trie") else "0")
     monkeypatch.setenv("CONTIVCLS_INLINE", "0" if kind.startswith("hrow") else "1")
+    monkeypatch.setenv("CONTIVCLS_SRC_SEARCH", "1" if kind.startswith(("search", "trie")) else "0")
     from cls_image import Image, compile_blob
     from vpp_amd import _abi
     rules, pool = variant_acl(kind, seed)
@@ -122,12 +146,13 @@ def test_all_kernel_variants(eng, seed, kind, monkeypatch):
 
 
 @pytest.mark.parametrize("seed", range(2))
-@pytest.mark.parametrize("kind", ["hash_sph", "search_cbv", "trie_sph"])
+@pytest.mark.parametrize("kind", ["hash_sph", "inl_sph", "search_cbv", "trie_sph"])
 def test_binary_sublist_form(eng, seed, kind, monkeypatch):
     """The binary sublist form (CONTIVCLS_SUB4=0; the default is 4-ary node
     trees) on the sublist variants."""
     monkeypatch.setenv("CONTIVCLS_SUB4", "0")
     monkeypatch.setenv("CONTIVCLS_TRIE", "1" if kind.startswith("trie") else "0")
+    monkeypatch.setenv("CONTIVCLS_SRC_SEARCH", "1" if kind.startswith(("search", "trie")) else "0")
     from cls_image import Image, compile_blob
     from vpp_amd import _abi
     rules, pool = variant_acl(kind, seed)

@@ -24,6 +24,8 @@ python tools/jl.py $OUT/genpolicy.jsonl workload rules list_mode lds_slots slots
 echo "LDS-DMA stream experiment"
 timeout -k 10 120 ./tools/stream_glds.bin > $OUT/stream_glds.txt 2>&1
 cat $OUT/stream_glds.txt
+timeout -k 10 180 ./tools/stream16_glds.bin > $OUT/stream16_glds.txt 2>&1
+cat $OUT/stream16_glds.txt
 echo "pytest (changed GPU tests)"
 timeout -k 10 1000 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_dist.py tests/test_gpu_connect_scale.py tests/test_gpu_trie_wide.py tests/test_gpu_sessions.py tests/test_gpu_acl_config.py -m gpu -x -v --timeout 170 --timeout-method thread > $OUT/pytest.log 2>&1 || { tail -60 $OUT/pytest.log; exit 1; }
 tail -3 $OUT/pytest.log

@@ -1,0 +1,182 @@
+// The 16-byte layout's HBM stream (config 5: 16-B src and dst, u16 dport, u8
+// proto read, u8 verdict written -- 36 B per packet), lookups left out, over
+// 256 Mi packets: does a different load path or in-flight depth get it from
+// ~5.5 TB/s to >= 6.0 TB/s?
+//   0  register loads as classify16_cls: lane l of a 256-packet wave step
+//      owns packets base + 64q + l (q < 4), every load and the verdict store nt
+//   1  0 without the verdict store (read ceiling)
+//   2  LDS-DMA (global_load_lds_dwordx4, nt), 64-packet wave steps, double
+//      buffered: src 1 KiB, dst 1 KiB, dport 128 B, proto 64 B per step;
+//      ds_read into registers, verdict byte stored nt
+//   3  2 with 128-packet steps
+//   4  3 triple buffered (two steps in flight while one is read)
+//   5  src / dst by LDS-DMA as 3, dport / proto register loads
+//   6  0 with 8 packets per lane per step (512-packet wave steps)
+//   7  0 with 512-thread workgroups, two per CU
+// build: hipcc -O3 --offload-arch=gfx950 -o tools/stream16_glds.bin tools/stream16_glds.hip
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s line %d\n", hipGetErrorString(e_), __LINE__); return 1; } } while (0)
+
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void* lds_t;
+
+__device__ __forceinline__ uint4 ldnt(const uint4* p) {
+    const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ uint32_t mix(const uint4& s, const uint4& d, uint32_t dp, uint32_t pr) {
+    return (s.x ^ s.y ^ s.z ^ s.w ^ d.x ^ d.y ^ d.z ^ d.w ^ dp ^ pr) & 3u;
+}
+// s_waitcnt vmcnt(v) with expcnt / lgkmcnt left open (gfx9 encoding)
+template <uint32_t v> __device__ __forceinline__ void wait_vm() {
+    __builtin_amdgcn_s_waitcnt((v & 15u) | ((v >> 4) << 14) | (7u << 4) | (15u << 8));
+}
+
+template <int M, int P>   // P packets per wave step
+__global__ __launch_bounds__(1024) void k(const uint4* S, const uint4* D, const uint16_t* DP, const uint8_t* PR,
+                                          uint8_t* V, uint32_t n, uint32_t* sink) {
+    extern __shared__ uint4 smem[];
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint32_t wpb = blockDim.x / 64u;
+    const uint32_t nwaves = gridDim.x * wpb, gw = blockIdx.x * wpb + wave;
+    const uint32_t nsteps = n / P;
+    uint32_t acc = 0;
+    if constexpr (M == 0 || M == 1 || M == 6 || M == 7) {
+        constexpr int Q = P / 64;
+        for (uint32_t t = gw; t < nsteps; t += nwaves) {
+            const uint32_t base = t * P + lane;
+            uint4 s[Q], d[Q];
+            uint32_t dp[Q], pr[Q];
+#pragma unroll
+            for (int q = 0; q < Q; ++q) { s[q] = ldnt(S + base + 64u * q); d[q] = ldnt(D + base + 64u * q); }
+#pragma unroll
+            for (int q = 0; q < Q; ++q) {
+                dp[q] = __builtin_nontemporal_load(DP + base + 64u * q);
+                pr[q] = __builtin_nontemporal_load(PR + base + 64u * q);
+            }
+#pragma unroll
+            for (int q = 0; q < Q; ++q) {
+                const uint32_t v = mix(s[q], d[q], dp[q], pr[q]);
+                if constexpr (M == 1) acc ^= v;
+                else __builtin_nontemporal_store(uint8_t(v), V + base + 64u * q);
+            }
+        }
+    } else {
+        constexpr uint32_t kBuf = (M == 4) ? 3u : 2u;
+        constexpr bool kRegSide = M == 5;
+        // slot: src P*16, dst P*16, dport P*2, proto P (rounded to 16)
+        constexpr uint32_t kSrc = 0, kDst = P * 16u, kDp = P * 32u, kPr = P * 34u;
+        constexpr uint32_t kSlot = (P * 35u + 15u) & ~15u;
+        constexpr uint32_t kPer = 2u * (P / 64u) + (kRegSide ? 0u : 2u);   // DMA instructions per step
+        uint8_t* base = reinterpret_cast<uint8_t*>(smem) + wave * kBuf * kSlot;
+        auto issue = [&](uint32_t t, uint32_t b) {
+            uint8_t* sl = base + b * kSlot;
+            const uint32_t p0 = t * P;
+#pragma unroll
+            for (uint32_t q = 0; q < P / 64u; ++q) {
+                __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(S + p0 + 64u * q + lane),
+                                                 (lds_t)(sl + kSrc + 1024u * q), 16, 0, 2);
+                __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(D + p0 + 64u * q + lane),
+                                                 (lds_t)(sl + kDst + 1024u * q), 16, 0, 2);
+            }
+            if constexpr (!kRegSide) {
+                // dport P*2 B = P/8 lanes of 16 B; proto P B = P/16 lanes
+                if (lane < P / 8u)
+                    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(reinterpret_cast<const uint4*>(DP + p0) + lane),
+                                                     (lds_t)(sl + kDp), 16, 0, 2);
+                if (lane < P / 16u)
+                    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(reinterpret_cast<const uint4*>(PR + p0) + lane),
+                                                     (lds_t)(sl + kPr), 16, 0, 2);
+            }
+        };
+        auto use = [&](uint32_t t, uint32_t b) {
+            const uint8_t* sl = base + b * kSlot;
+            const uint32_t p0 = t * P;
+#pragma unroll
+            for (uint32_t q = 0; q < P / 64u; ++q) {
+                const uint32_t j = 64u * q + lane;
+                const uint4 s = *reinterpret_cast<const uint4*>(sl + kSrc + 16u * j);
+                const uint4 d = *reinterpret_cast<const uint4*>(sl + kDst + 16u * j);
+                uint32_t dp, pr;
+                if constexpr (kRegSide) {
+                    dp = __builtin_nontemporal_load(DP + p0 + j);
+                    pr = __builtin_nontemporal_load(PR + p0 + j);
+                } else {
+                    dp = *reinterpret_cast<const uint16_t*>(sl + kDp + 2u * j);
+                    pr = sl[kPr + j];
+                }
+                __builtin_nontemporal_store(uint8_t(mix(s, d, dp, pr)), V + p0 + j);
+            }
+        };
+        uint32_t t = gw, b = 0;
+        // prologue: kBuf - 1 steps in flight
+        if (t < nsteps) issue(t, 0);
+        if constexpr (kBuf == 3) { if (t + nwaves < nsteps) issue(t + nwaves, 1); }
+        while (t < nsteps) {
+            const uint32_t ahead = t + (kBuf - 1u) * nwaves;
+            const uint32_t tb = (b + kBuf - 1u) % kBuf;
+            if (ahead < nsteps) {
+                issue(ahead, tb);
+                // wait for step t: everything but the kBuf-1 newer steps' DMAs (stores of the
+                // previous use() count too on gfx9, so this also waits for them: conservative)
+                wait_vm<kPer * (kBuf - 1u)>();
+            } else {
+                wait_vm<0>();
+            }
+            use(t, b);
+            t += nwaves;
+            b = (b + 1u) % kBuf;
+        }
+    }
+    if (acc == 0x12345678u) sink[0] = acc;
+}
+
+int main() {
+    const uint64_t N = 1ull << 28;
+    uint4 *src, *dst;
+    uint16_t* dp;
+    uint8_t *pr, *v;
+    uint32_t* sink;
+    CK(hipMalloc(&src, N * 16)); CK(hipMalloc(&dst, N * 16)); CK(hipMalloc(&dp, N * 2));
+    CK(hipMalloc(&pr, N)); CK(hipMalloc(&v, N)); CK(hipMalloc(&sink, 64));
+    CK(hipMemset(src, 1, N * 16)); CK(hipMemset(dst, 2, N * 16)); CK(hipMemset(dp, 3, N * 2));
+    CK(hipMemset(pr, 1, N)); CK(hipMemset(v, 0, N));
+    int ncu = 0;
+    CK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+    auto run = [&](auto kern, const char* name, int grid, int block, size_t lds, double bpp) -> int {
+        if (lds > 0)
+            CK(hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));
+        for (int rep = 0; rep < 3; ++rep) {
+            for (int i = 0; i < 3; ++i) kern<<<grid, block, lds>>>(src, dst, dp, pr, v, uint32_t(N), sink);
+            CK(hipGetLastError());
+            CK(hipDeviceSynchronize());
+            CK(hipEventRecord(e0));
+            for (int i = 0; i < 10; ++i) kern<<<grid, block, lds>>>(src, dst, dp, pr, v, uint32_t(N), sink);
+            CK(hipEventRecord(e1));
+            CK(hipEventSynchronize(e1));
+            float ms;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            ms /= 10;
+            printf("%-28s %.4f ms %.1f GB/s\n", name, ms, bpp * N / ms / 1e6);
+        }
+        return 0;
+    };
+    for (int i = 0; i < 100; ++i) k<0, 256><<<ncu, 1024>>>(src, dst, dp, pr, v, uint32_t(N), sink);
+    CK(hipDeviceSynchronize());
+    auto slot = [](int P) { return size_t((P * 35 + 15) & ~15); };
+    if (run(k<0, 256>, "0 reg 256", ncu, 1024, 0, 36.0)) return 1;
+    if (run(k<1, 256>, "1 reg 256 read-only", ncu, 1024, 0, 35.0)) return 1;
+    if (run(k<2, 64>, "2 dma 64 x2", ncu, 1024, 16 * 2 * slot(64), 36.0)) return 1;
+    if (run(k<3, 128>, "3 dma 128 x2", ncu, 1024, 16 * 2 * slot(128), 36.0)) return 1;
+    if (run(k<4, 64>, "4 dma 64 x3", ncu, 1024, 16 * 3 * slot(64), 36.0)) return 1;
+    if (run(k<5, 128>, "5 dma 128 x2 src/dst only", ncu, 1024, 16 * 2 * slot(128), 36.0)) return 1;
+    if (run(k<6, 512>, "6 reg 512", ncu, 1024, 0, 36.0)) return 1;
+    if (run(k<7, 256>, "7 reg 256 2x512", 2 * ncu, 512, 0, 36.0)) return 1;
+    if (run(k<0, 256>, "0 reg 256", ncu, 1024, 0, 36.0)) return 1;
+    return 0;
+}

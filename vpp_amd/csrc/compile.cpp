@@ -274,6 +274,12 @@ struct TmplHash {
 
 uint32_t align4(uint32_t w) { return (w + 3u) & ~3u; }
 
+// an environment switch set to a non-zero number (diagnostics and tests)
+bool env_flag(const char* name) {
+    const char* v = std::getenv(name);
+    return v && std::atoi(v) != 0;
+}
+
 // Two-table cuckoo hash of (key, class): table 0 at [0, cap), table 1 at
 // [cap, 2 cap); entry = key | class << 32.
 bool cuckoo_build(const std::vector<std::pair<uint32_t, uint32_t>>& keys, uint32_t cap, uint32_t mul,
@@ -766,7 +772,8 @@ static bool build_cls4_one(const std::vector<SemRule>& sem, uint32_t n_rules, Cl
             img.mode = 0;                            // the OTHER image: interval search (Cls4Opts)
         } else if (opt && opt->ext_src) {
             img.mode = 3;                            // the caller maps addresses to rows
-        } else if (keys.size() <= kMaxHashLens) {
+        } else if (keys.size() <= kMaxHashLens && !env_flag("CONTIVCLS_SRC_SEARCH")) {
+            // (CONTIVCLS_SRC_SEARCH=1: the interval search always -- tests)
             img.mode = 1;
             img.default_class = dflt;
             for (const auto& kv : keys) {

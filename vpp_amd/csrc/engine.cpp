@@ -197,7 +197,10 @@ int cls_engine_create(const cls_config* cfg, cls_engine** out) {
     if (!e) return CLS_E_NOMEM;
     e->device = dev;
     e->n_cu = prop.multiProcessorCount;
-    if (hipSetDevice(dev) != hipSuccess || hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
+    // The engine's stream (a call's stream == NULL) is a blocking stream: work
+    // on the legacy default stream (torch's current stream unless the caller
+    // set another) and the engine's calls stay ordered both ways.
+    if (hipSetDevice(dev) != hipSuccess || hipStreamCreateWithFlags(&e->stream, hipStreamDefault) != hipSuccess) {
         delete e;
         return CLS_E_HIP;
     }

@@ -316,6 +316,12 @@ __device__ __forceinline__ void classify_n(const Img<kLds>& im, const Cls4Dev& t
             const uint32_t tab = t.off_hash[0], mask = t.hash_mask[0], mul = t.hash_mul[0];
             const uint32_t s0 = t.hash_shift[0], s1 = t.hash_shift1[0], L = 32u - s0;
             const uint32_t tab1 = __builtin_amdgcn_readfirstlane(tab + 16u * t.hash_cap[0]);
+            // The default class's three cells as opaque SGPR values: a select
+            // among t.dflt_cell[0..2] by the lane's protocol would otherwise
+            // become a per-lane load from the kernel arguments, and its
+            // vmcnt(0) wait would drain the packet stream's loads in flight.
+            uint32_t cd0 = t.dflt_cell[0], cd1 = t.dflt_cell[1], cd2 = t.dflt_cell[2];
+            asm volatile("" : "+s"(cd0), "+s"(cd1), "+s"(cd2));
             uint4 e0[N], e1[N];
             uint32_t key[N];
 #pragma unroll
@@ -330,7 +336,7 @@ __device__ __forceinline__ void classify_n(const Img<kLds>& im, const Cls4Dev& t
                 const uint32_t p = proto[q];
                 const uint32_t c0 = p == 0u ? e0[q].y : p == 1u ? e0[q].z : e0[q].w;
                 const uint32_t c1 = p == 0u ? e1[q].y : p == 1u ? e1[q].z : e1[q].w;
-                const uint32_t cd = p == 0u ? t.dflt_cell[0] : p == 1u ? t.dflt_cell[1] : t.dflt_cell[2];
+                const uint32_t cd = p == 0u ? cd0 : p == 1u ? cd1 : cd2;
                 cell[q] = e0[q].x == key[q] ? c0 : (e1[q].x == key[q] ? c1 : cd);
             }
 #pragma unroll
