@@ -14,11 +14,16 @@ from cls_image import Image, compile_blob
 from vpp_amd import _abi
 
 
-@pytest.fixture(autouse=True)
-def _source_keyed(monkeypatch):
+@pytest.fixture(autouse=True, params=["binary", "sub4_inline"])
+def _source_keyed(monkeypatch, request):
     """These tests pin list modes of the source-keyed layout; the compiler's
-    choice of orientation (compile.cpp build_cls4) is tested on its own."""
+    choice of orientation (compile.cpp build_cls4) is tested on its own.
+    Every test runs on both sublist forms: binary sublists and row entries
+    (the default), 4-ary node sublists and inline hash cells."""
     monkeypatch.setenv("CONTIVCLS_ORIENT", "src")
+    on = "1" if request.param == "sub4_inline" else "0"
+    monkeypatch.setenv("CONTIVCLS_SUB4", on)
+    monkeypatch.setenv("CONTIVCLS_INLINE", on)
 
 
 def _check(rules, traffic):

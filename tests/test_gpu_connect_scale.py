@@ -177,10 +177,25 @@ def test_connections16_mixed_families_match_oracle(mode):
 
 
 @pytest.mark.parametrize("fam", [4, 16])
-@pytest.mark.parametrize("no_lds", [0, 1, 2, 3])
+def test_connections_inline_cells_sub4(fam, monkeypatch):
+    """Slot-mode classify launches over images with inline hash cells and
+    4-ary sublists (CONTIVCLS_INLINE=1, CONTIVCLS_SUB4=1), counters included."""
+    from vpp_amd.engine import Engine
+    monkeypatch.setenv("CONTIVCLS_INLINE", "1")
+    monkeypatch.setenv("CONTIVCLS_SUB4", "1")
+    eng = Engine()
+    try:
+        _run(eng, 3, "classifier", fam, count=True, n=12000)
+    finally:
+        eng.close()
+
+
+@pytest.mark.parametrize("fam", [4, 16])
+@pytest.mark.parametrize("no_lds", [0, 1, 2, 3, 7])
 def test_connection_counters_match_oracle(fam, no_lds, monkeypatch):
     """Per-(ACL, rule) counters with the rule pool in LDS (few locals: the
-    pool fits) or in global memory, the counters in LDS or global memory."""
+    pool fits) or in global memory, the counters in LDS or global memory,
+    the descriptor and interface tables in LDS or (bit 2) global memory."""
     from vpp_amd.engine import Engine
     monkeypatch.setenv("CONTIVCLS_CONN_NO_LDS", str(no_lds))
     eng = Engine()
@@ -243,11 +258,12 @@ def test_device_batch_unknown_interface_is_failure():
 
 @pytest.mark.parametrize("fam", [4, 16])
 @pytest.mark.parametrize("count", [False, True])
-def test_per_lane_kernel_matches_oracle(fam, count, monkeypatch):
-    """The per-lane connection kernel (CONTIVCLS_CONN_SORTED=0; the default
-    sorts the linear scans by ACL): the same verdicts and counters."""
+def test_global_tables_match_oracle(fam, count, monkeypatch):
+    """The connection kernel with its descriptor and interface tables read
+    from global memory (CONTIVCLS_CONN_NO_LDS bit 2; the default stages them
+    in LDS): the same verdicts and counters."""
     from vpp_amd.engine import Engine
-    monkeypatch.setenv("CONTIVCLS_CONN_SORTED", "0")
+    monkeypatch.setenv("CONTIVCLS_CONN_NO_LDS", "4")
     eng = Engine()
     try:
         _run(eng, 11, "linear", fam, count=count, n=8000, n_local=12)

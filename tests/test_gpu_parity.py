@@ -147,17 +147,18 @@ def test_all_kernel_variants(eng, seed, kind, monkeypatch):
 
 @pytest.mark.parametrize("seed", range(2))
 @pytest.mark.parametrize("kind", ["hash_sph", "inl_sph", "search_cbv", "trie_sph"])
-def test_binary_sublist_form(eng, seed, kind, monkeypatch):
-    """The binary sublist form (CONTIVCLS_SUB4=0; the default is 4-ary node
-    trees) on the sublist variants."""
-    monkeypatch.setenv("CONTIVCLS_SUB4", "0")
+def test_sub4_sublist_form(eng, seed, kind, monkeypatch):
+    """The 4-ary node sublists (CONTIVCLS_SUB4=1; the default is the binary
+    form) on the sublist variants."""
+    monkeypatch.setenv("CONTIVCLS_SUB4", "1")
+    monkeypatch.setenv("CONTIVCLS_INLINE", "1" if kind.startswith("inl") else "0")
     monkeypatch.setenv("CONTIVCLS_TRIE", "1" if kind.startswith("trie") else "0")
     monkeypatch.setenv("CONTIVCLS_SRC_SEARCH", "1" if kind.startswith(("search", "trie")) else "0")
     from cls_image import Image, compile_blob
     from vpp_amd import _abi
     rules, pool = variant_acl(kind, seed)
     h = Image(compile_blob(_abi.CRules(rules))).h
-    assert (h.mode, h.list_mode) == VARIANTS[kind] and h.sub4 == 0, kind
+    assert (h.mode, h.list_mode) == VARIANTS[kind] and h.sub4 == 1, kind
     tr = random_traffic(seed + 21, 30000, pool)
     _assert_same(_gpu(eng, rules, tr), _oracle(rules, tr))
 

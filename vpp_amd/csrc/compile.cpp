@@ -1093,10 +1093,12 @@ static bool build_cls4_one(const std::vector<SemRule>& sem, uint32_t n_rules, Cl
     std::vector<uint32_t>& w = img.words;
     // trie: the source trie replaces the interval search (mode 0 only);
     // wide: list modes 3, 4 with the cells in global memory (gcells)
-    // sublist search: 4-ary nodes (16-B reads, half the dependent steps) or
-    // the binary form (CONTIVCLS_SUB4=0)
-    const char* s4env = std::getenv("CONTIVCLS_SUB4");
-    const bool sub4 = !(s4env && std::atoi(s4env) == 0);
+    // sublist search: the binary form (8-B probes), or 4-ary nodes with
+    // CONTIVCLS_SUB4=1 (16-B reads, half the dependent steps -- but a random
+    // ds_read_b128 costs about two random ds_read_b64 in bank cycles, and the
+    // kernel is bound by those: config 3 0.613 ms against 0.600 binary,
+    // DESIGN.md section 4, item 5)
+    const bool sub4 = env_flag("CONTIVCLS_SUB4");
     uint32_t L4 = 0;
     for (const auto& sl : subs) {
         uint32_t l = 0, cap = 1;
@@ -1105,8 +1107,10 @@ static bool build_cls4_one(const std::vector<SemRule>& sem, uint32_t n_rules, Cl
         L4 = std::max(L4, l);
     }
     const uint32_t n_hash0 = img.n_hash;
-    const char* ienv = std::getenv("CONTIVCLS_INLINE");         // 0: rows in the hash entries (A/B, tests)
-    const bool inline_ok = !(ienv && std::atoi(ienv) == 0) && ncell == 3;
+    // inline cells in 16-B hash entries (src mode 6) with CONTIVCLS_INLINE=1;
+    // by default the entries hold class rows (config 3: 0.639 ms inline
+    // against 0.613, the 16-B probes' bank cycles again)
+    const bool inline_ok = env_flag("CONTIVCLS_INLINE") && ncell == 3;
     auto serialise = [&](uint32_t lm, bool trie, bool wide) -> bool {
         img.mode = trie ? 4u : mode0;
         img.n_hash = trie ? 0u : n_hash0;                 // the trie replaces the hash LPM

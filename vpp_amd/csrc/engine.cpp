@@ -1254,7 +1254,7 @@ int cls_connect_batch(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t*
     // LDS: the rule pool first (every evaluation step reads it), then the u32
     // counters if they fit beside it; otherwise global-memory variants
     // (CONTIVCLS_CONN_NO_LDS, tests: bit 0 rules from global memory, bit 1
-    // global counters)
+    // global counters, bit 2 descriptor / interface tables from global memory)
     const char* nl = std::getenv("CONTIVCLS_CONN_NO_LDS");
     const int no_lds = nl ? std::atoi(nl) : 0;
     const size_t lds_max = size_t(max_lds_bytes());
@@ -1289,30 +1289,22 @@ int cls_connect_batch(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t*
         HIPC(e, e->s_tctr.ensure(tctr.size() * sizeof(void*)));
         HIPC(e, hipMemcpyAsync(e->s_tctr.p, tctr.data(), tctr.size() * sizeof(void*), hipMemcpyHostToDevice, s));
     }
-    // persistent grid: as many workgroups per CU as the LDS allows.  When an
-    // ACL is scanned linearly, the sorted kernel (connect_sorted_kernel: the
-    // scans grouped by ACL, so a wave's lanes share one) runs if its chunk
-    // fits beside the pool and counters (CONTIVCLS_CONN_SORTED=0: the
-    // per-lane kernel, for A/B and tests).
-    const size_t lds = lds_used + (cmode == 1 ? size_t(n_ctr) * 4 : 0);
-    bool any_scan = false;
-    for (const auto& d : desc) any_scan = any_scan || (!d.pre && d.n);
-    const char* sv = std::getenv("CONTIVCLS_CONN_SORTED");
-    const bool want_sorted = any_scan && !(sv && std::atoi(sv) == 0);
-    const size_t chunk_at = (lds + 15) & ~size_t(15);
-    const size_t lds_sorted = chunk_at + conn_sorted_lds(k16, uint32_t(desc.size()));
-    if (want_sorted && lds_sorted <= lds_max) {
-        a.chunk_lds = uint32_t(chunk_at);
-        a.n_desc = uint32_t(desc.size());
-        const int per_cu = std::max(1, std::min(int(2048 / kConnSortBlock), int(lds_max / lds_sorted)));
-        const int grid = int(std::max<uint64_t>(
-            1, std::min<uint64_t>(uint64_t(e->n_cu) * per_cu, (n + kConnSortBlock - 1) / kConnSortBlock)));
-        HIPC(e, launch_connect_sorted(a, k16, lds_rules, cmode, grid, lds_sorted, s));
-    } else {
-        const int per_cu = lds ? std::max(1, std::min(2, int(lds_max / lds))) : 2;
-        const int grid = int(std::max<uint64_t>(1, std::min<uint64_t>(uint64_t(e->n_cu) * per_cu, (n + 1023) / 1024)));
-        HIPC(e, launch_connect(a, k16, lds_rules, cmode, grid, s));
+    // The descriptor and interface tables go to LDS after the pool and the
+    // counters when they fit (else the kernel reads them from global memory).
+    // Persistent grid: as many 1024-thread workgroups per CU as the LDS
+    // allows, at most two.
+    a.n_desc = uint32_t(desc.size());
+    size_t lds = lds_used + (cmode == 1 ? size_t(n_ctr) * 4 : 0);
+    const size_t meta_at = (lds + 15) & ~size_t(15);
+    const size_t meta = desc.size() * sizeof(ConnDesc) + ifs.size() * sizeof(IfAcls);
+    a.meta_lds = 0xFFFFFFFFu;
+    if (meta_at + meta <= lds_max && !(no_lds & 4)) {
+        a.meta_lds = uint32_t(meta_at);
+        lds = meta_at + meta;
     }
+    const int per_cu = lds ? std::max(1, std::min(2, int(lds_max / lds))) : 2;
+    const int grid = int(std::max<uint64_t>(1, std::min<uint64_t>(uint64_t(e->n_cu) * per_cu, (n + 1023) / 1024)));
+    HIPC(e, launch_connect(a, k16, lds_rules, cmode, grid, lds, s));
     if (cmode && n)
         HIPC(e, launch_conn_scatter(a.desc, e->s_tctr.as<unsigned long long* const>(), uint32_t(desc.size()),
                                     e->s_cctr.as<unsigned long long>(), s));

@@ -7,6 +7,7 @@ namespace cls {
 hipError_t launch_classify4_cls(const Cls4Dev& t, const Pkts4& p, uint8_t* verdict,
                                 unsigned long long* gslot, bool lds_resident, bool vec,
                                 const LaunchCfg& cfg) {
+    if (!cls_dispatchable(t, lds_resident, false)) return hipErrorInvalidValue;
     if (lds_resident) {
         if (vec) return launch_cls4_lds_vec(t, p, verdict, gslot, cfg);
         dispatch_cls<true, false>(t, p, verdict, gslot, cfg);
@@ -19,6 +20,7 @@ hipError_t launch_classify4_cls(const Cls4Dev& t, const Pkts4& p, uint8_t* verdi
 
 hipError_t launch_classify4_slots(const Cls4Dev& t, const Pkts4& p, uint32_t* out, bool lds_resident,
                                   const LaunchCfg& cfg) {
+    if (!cls_dispatchable(t, lds_resident, false)) return hipErrorInvalidValue;
     if (lds_resident) dispatch_slots4<true>(t, p, out, cfg);
     else dispatch_slots4<false>(t, p, out, cfg);
     return hipGetLastError();

@@ -398,38 +398,61 @@ __device__ __forceinline__ uint32_t conn_index(const ConnRule16& r) { return r.i
 __device__ __forceinline__ bool mapped4(uint32_t) { return true; }
 __device__ __forceinline__ bool mapped4(const uint4& a) { return (a.x | a.y) == 0u && a.z == 0xFFFF0000u; }
 
-// One evalACL call: ACLAction, and the counter key of its terminating rule
-// (~0u for a nil ACL: PERMIT, not counted -- aclengine_mock.go:476-478).
+// The call's descriptor and interface tables: staged in LDS at a.meta_lds
+// (descriptors, then the interfaces) when they fit, else read from global
+// memory (a.meta_lds == ~0u; uniform branch).  Staged, a connection's
+// interface and descriptor reads are LDS reads instead of dependent global
+// loads in front of every evaluation.
+__device__ __forceinline__ IfAcls conn_if(const ConnArgs& a, uint32_t j) {
+    if (a.meta_lds != 0xFFFFFFFFu) {
+        const v2u v = *lds64_t(a.meta_lds + a.n_desc * uint32_t(sizeof(ConnDesc)) + 8u * j);
+        return IfAcls{int32_t(v.x), int32_t(v.y)};
+    }
+    return a.ifs[j];
+}
+__device__ __forceinline__ ConnDesc conn_desc(const ConnArgs& a, uint32_t j) {
+    if (a.meta_lds != 0xFFFFFFFFu) {
+        const uint32_t b = a.meta_lds + j * uint32_t(sizeof(ConnDesc));
+        const v4u x = *lds128_t(b), y = *lds128_t(b + 16u);
+        ConnDesc d;
+        d.rule_off = x.x; d.n = x.y; d.n_rules = x.z; d.ctr_off = x.w;
+        d.pre = reinterpret_cast<const uint32_t*>(uint64_t(y.x) | (uint64_t(y.y) << 32));
+        d.slot_rule = reinterpret_cast<const uint32_t*>(uint64_t(y.z) | (uint64_t(y.w) << 32));
+        return d;
+    }
+    return a.desc[j];
+}
+
+// The linear scan of one evalACL call over an ACL of the rule pool: ACLAction
+// and the terminating rule (R: default DENY, aclengine_mock.go:667).
 template <bool k16, bool kLds>
-__device__ __forceinline__ uint32_t conn_eval(const ConnArgs& a, int32_t di, uint32_t tuple, uint64_t i,
+__device__ __forceinline__ uint32_t conn_scan(const ConnArgs& a, const ConnDesc& D,
                                               const typename ConnT<k16>::A& s, const typename ConnT<k16>::A& d,
-                                              bool s4, bool d4, uint32_t port, uint32_t p, uint32_t& key) {
+                                              bool s4, bool d4, uint32_t port, uint32_t p, uint32_t& rule) {
     typedef typename ConnT<k16>::R R;
-    key = 0xFFFFFFFFu;
-    if (di < 0) return 1u;
-    const ConnDesc D = a.desc[di];
-    uint32_t res = 0u, rule = D.n_rules;                  // default DENY (:667)
-    if (D.pre) {
-        const uint32_t w = D.pre[uint64_t(tuple) * a.n + i];
-        res = w & 3u;
-        rule = D.slot_rule[w >> 2];
-    } else {
-        const R* g = static_cast<const R*>(a.rules);
-        for (uint32_t r = 0; r < D.n; ++r) {
-            const R x = conn_rule<kLds>(g, D.rule_off + r);
-            const uint32_t meta = (x.meta >> (8u * p)) & 0xFFu;
-            const uint32_t pw = p == 0u ? x.port[0] : p == 1u ? x.port[1] : 0xFFFF0000u;   // ICMP / OTHER: any port
-            if ((meta & 0x80u) && conn_match(x, s, d, s4, d4) && port_in(port, pw)) {
-                res = meta & 3u;
-                rule = conn_index(x);
-                break;
-            }
+    const R* g = static_cast<const R*>(a.rules);
+    uint32_t res = 0u;
+    rule = D.n_rules;
+    for (uint32_t r = 0; r < D.n; ++r) {
+        const R x = conn_rule<kLds>(g, D.rule_off + r);
+        const uint32_t meta = (x.meta >> (8u * p)) & 0xFFu;
+        const uint32_t pw = p == 0u ? x.port[0] : p == 1u ? x.port[1] : 0xFFFF0000u;   // ICMP / OTHER: any port
+        if ((meta & 0x80u) && conn_match(x, s, d, s4, d4) && port_in(port, pw)) {
+            res = meta & 3u;
+            rule = conn_index(x);
+            break;
         }
     }
-    key = D.ctr_off + rule;
     return res;
 }
 
+// testConnection, one lane per connection: the evaluations in the
+// reference's order, each reading its descriptor (LDS) and then either the
+// classifier's slot word for this connection (and, counting, its slot's
+// rule) or scanning the ACL's rules.  (Loading the slot words of all four
+// possible evaluations up front, before the state machine knows which it
+// makes, measured slower: 185 vs 165 us per 4 Mi connections, 256 vs 176
+// counting -- the loads for skipped evaluations are not free.)
 template <bool k16, bool kLdsRules, int kCount>
 __global__ __launch_bounds__(1024) void connect_kernel(ConnArgs a) {
     typedef typename ConnT<k16>::A A;
@@ -442,7 +465,14 @@ __global__ __launch_bounds__(1024) void connect_kernel(ConnArgs a) {
     if constexpr (kCount == 1) {
         for (uint32_t j = threadIdx.x; j < a.n_ctr; j += blockDim.x) *lctr_t(a.ctr_lds + 4u * j) = 0u;
     }
-    if constexpr (kLdsRules || kCount == 1) __syncthreads();
+    if (a.meta_lds != 0xFFFFFFFFu) {
+        const uint32_t nd = a.n_desc * uint32_t(sizeof(ConnDesc)) / 4u;
+        const uint32_t* gd = reinterpret_cast<const uint32_t*>(a.desc);
+        const uint32_t* gi = reinterpret_cast<const uint32_t*>(a.ifs);
+        for (uint32_t j = threadIdx.x; j < nd; j += blockDim.x) *lctr_t(a.meta_lds + 4u * j) = gd[j];
+        for (uint32_t j = threadIdx.x; j < 2u * a.n_ifs; j += blockDim.x) *lctr_t(a.meta_lds + 4u * (nd + j)) = gi[j];
+    }
+    __syncthreads();
     const A* src = static_cast<const A*>(a.src);
     const A* dst = static_cast<const A*>(a.dst);
     const uint64_t nthreads = uint64_t(gridDim.x) * blockDim.x;
@@ -454,30 +484,51 @@ __global__ __launch_bounds__(1024) void connect_kernel(ConnArgs a) {
             const uint32_t si = a.src_if[i], dj = a.dst_if[i];
             uint32_t v = 3u;                                    // unknown interface id: Failure
             if (si < a.n_ifs && dj < a.n_ifs) {
-                const IfAcls S = a.ifs[si], D = a.ifs[dj];
+                const IfAcls S = conn_if(a, si), Dif = conn_if(a, dj);
                 const bool same = si == dj;
                 const A sa = src[i], da = dst[i];
                 const bool s4 = mapped4(sa), d4 = mapped4(da);
                 const uint32_t sp = a.sport[i], dp = a.dport[i], pr = a.proto[i];
                 const uint32_t p = pr <= 2u ? pr : 3u;
+                // the four calls in testConnection's order: SYN through the
+                // source's inbound and the destination's outbound ACL, SYN-ACK
+                // through the destination's inbound and the source's outbound
+                const int32_t di[4] = {S.in, Dif.out, Dif.in, S.out};
+                // one evalACL call: ACLAction; counting key of its terminating rule
+                auto eval = [&](int k) -> uint32_t {
+                    if (di[k] < 0) return 1u;                   // nil ACL: PERMIT, not counted (:476-478)
+                    const ConnDesc D = conn_desc(a, uint32_t(di[k]));
+                    uint32_t res, rule;
+                    if (D.pre) {
+                        const uint32_t w = D.pre[uint64_t(k >> 1) * a.n + i];
+                        res = w & 3u;
+                        rule = kCount != 0 ? D.slot_rule[w >> 2] : 0u;
+                    } else if (k < 2) {
+                        res = conn_scan<k16, kLdsRules>(a, D, sa, da, s4, d4, dp, p, rule);
+                    } else {
+                        res = conn_scan<k16, kLdsRules>(a, D, da, sa, d4, s4, sp, p, rule);
+                    }
+                    key[k] = D.ctr_off + rule;
+                    return res;
+                };
                 bool srefl = false, drefl = false, done = false;
-                uint32_t r = conn_eval<k16, kLdsRules>(a, S.in, 0u, i, sa, da, s4, d4, dp, p, key[0]);   // SYN: src inbound
+                uint32_t r = eval(0);                                                   // SYN: src inbound
                 if (r == 3u) { v = 3u; done = true; }
                 else if (r == 0u) { v = 0u; done = true; }
                 else if (r == 2u) { srefl = true; drefl = same; }
-                if (!done && !drefl) {                                                               // SYN: dst outbound
-                    r = conn_eval<k16, kLdsRules>(a, D.out, 0u, i, sa, da, s4, d4, dp, p, key[1]);
+                if (!done && !drefl) {                                                  // SYN: dst outbound
+                    r = eval(1);
                     if (r == 3u) { v = 3u; done = true; }
                     else if (r == 0u) { v = 0u; done = true; }
                     else if (r == 2u) { drefl = true; srefl = srefl || same; }
                 }
-                if (!done && !drefl) {                                                               // SYN-ACK: dst inbound
-                    r = conn_eval<k16, kLdsRules>(a, D.in, 1u, i, da, sa, d4, s4, sp, p, key[2]);
+                if (!done && !drefl) {                                                  // SYN-ACK: dst inbound
+                    r = eval(2);
                     if (r == 3u) { v = 3u; done = true; }
                     else if (r == 0u) { v = 1u; done = true; }
                 }
-                if (!done && !srefl) {                                                               // SYN-ACK: src outbound
-                    r = conn_eval<k16, kLdsRules>(a, S.out, 1u, i, da, sa, d4, s4, sp, p, key[3]);
+                if (!done && !srefl) {                                                  // SYN-ACK: src outbound
+                    r = eval(3);
                     if (r == 3u) { v = 3u; done = true; }
                     else if (r == 0u) { v = 1u; done = true; }
                 }
@@ -495,180 +546,6 @@ __global__ __launch_bounds__(1024) void connect_kernel(ConnArgs a) {
 #pragma unroll
             for (int k = 0; k < 4; ++k) wave_count(a.ctr, key[k]);
         }
-    }
-    if constexpr (kCount == 1) {
-        __syncthreads();
-        for (uint32_t j = threadIdx.x; j < a.n_ctr; j += blockDim.x) {
-            const uint32_t c = *lctr_t(a.ctr_lds + 4u * j);
-            if (c) atomicAdd(&a.ctr[j], (unsigned long long)c);
-        }
-    }
-}
-
-// testConnection with the linear ACL scans sorted by ACL (launch_connect_sorted).
-// A workgroup takes kConnSortBlock connections at a time, one per thread (the
-// owner), staged in LDS.  Each of testConnection's four evaluation steps:
-// the owner resolves a nil ACL (PERMIT) or a classifier-evaluated one (slot
-// words) itself; the connections whose ACL is scanned linearly are counting-
-// sorted by ACL descriptor, thread j scans the ACL of the j-th of them --
-// so a wave's lanes mostly share one ACL, read its rules by broadcast and
-// leave together -- and writes the result back to the owner, which applies
-// testConnection's state machine (aclengine_mock.go:394-471) as connect_kernel
-// does.  Verdicts and counters equal connect_kernel's.
-template <bool k16, bool kLdsRules, int kCount>
-__global__ __launch_bounds__(kConnSortBlock) void connect_sorted_kernel(ConnArgs a) {
-    typedef typename ConnT<k16>::A A;
-    typedef typename ConnT<k16>::R R;
-    constexpr uint32_t C = kConnSortBlock;
-    extern __shared__ uint4 smem[];
-    typedef __attribute__((address_space(3))) uint32_t* lctr_t;
-    uint8_t* L = reinterpret_cast<uint8_t*>(smem);
-    if constexpr (kLdsRules) {
-        const uint4* g = static_cast<const uint4*>(a.rules);
-        for (uint32_t j = threadIdx.x; j < a.rules_bytes / 16u; j += blockDim.x) smem[j] = g[j];
-    }
-    if constexpr (kCount == 1) {
-        for (uint32_t j = threadIdx.x; j < a.n_ctr; j += blockDim.x) *lctr_t(a.ctr_lds + 4u * j) = 0u;
-    }
-    A* cs = reinterpret_cast<A*>(L + a.chunk_lds);
-    A* cd = cs + C;
-    uint32_t* cport = reinterpret_cast<uint32_t*>(cd + C);      // sport | dport << 16
-    uint32_t* cmeta = cport + C;                                // proto class | s4 << 8 | d4 << 9 | desc << 16
-    uint32_t* cres = cmeta + C;                                 // scan result
-    uint32_t* hist = cres + C;                                  // counts [n_desc], cursors [n_desc], total
-    uint16_t* perm = reinterpret_cast<uint16_t*>(hist + 2u * a.n_desc + 4u);
-    const uint32_t t = threadIdx.x, lane = t & 63u;
-    const R* g = static_cast<const R*>(a.rules);
-    const A* src = static_cast<const A*>(a.src);
-    const A* dst = static_cast<const A*>(a.dst);
-    __syncthreads();
-    for (uint64_t base = uint64_t(blockIdx.x) * C; base < a.n; base += uint64_t(gridDim.x) * C) {
-        const uint64_t i = base + t;
-        bool live = false, same = false, srefl = false, drefl = false, s4 = false, d4 = false;
-        uint32_t v = 3u, sp = 0u, dp = 0u, p = 0u;
-        IfAcls S{-1, -1}, D{-1, -1};
-        A sa{}, da{};
-        if (i < a.n) {
-            const uint32_t si = a.src_if[i], dj = a.dst_if[i];
-            if (si < a.n_ifs && dj < a.n_ifs) {                 // unknown interface id: Failure
-                live = true;
-                S = a.ifs[si];
-                D = a.ifs[dj];
-                same = si == dj;
-                sa = src[i];
-                da = dst[i];
-                s4 = mapped4(sa);
-                d4 = mapped4(da);
-                sp = a.sport[i];
-                dp = a.dport[i];
-                const uint32_t pr = a.proto[i];
-                p = pr <= 2u ? pr : 3u;
-            }
-        }
-        cs[t] = sa;
-        cd[t] = da;
-        cport[t] = sp | (dp << 16);
-#pragma unroll 1
-        for (uint32_t k = 0; k < 4u; ++k) {
-            const bool syn = k < 2u;                            // SYN: (src, dst, dport); SYN-ACK: (dst, src, sport)
-            const bool need = live && (k == 0u || (k == 3u ? !srefl : !drefl));
-            const int32_t di = !need ? -1 : k == 0u ? S.in : k == 1u ? D.out : k == 2u ? D.in : S.out;
-            uint32_t r = 1u, key = 0xFFFFFFFFu;                 // nil ACL: PERMIT, not counted (:476-478)
-            bool scan = false;
-            if (di >= 0) {
-                const ConnDesc Dd = a.desc[di];
-                if (Dd.pre) {
-                    const uint32_t w = Dd.pre[uint64_t(syn ? 0u : 1u) * a.n + i];
-                    r = w & 3u;
-                    key = Dd.ctr_off + Dd.slot_rule[w >> 2];
-                } else if (Dd.n == 0u) {
-                    r = 0u;                                     // default DENY (:667)
-                    key = Dd.ctr_off + Dd.n_rules;
-                } else {
-                    scan = true;
-                }
-            }
-            cmeta[t] = p | (s4 ? 0x100u : 0u) | (d4 ? 0x200u : 0u) | (scan ? uint32_t(di) << 16 : 0u);
-            for (uint32_t j = t; j <= a.n_desc; j += C) hist[j == a.n_desc ? 2u * a.n_desc : j] = 0u;
-            __syncthreads();
-            if (scan) __hip_atomic_fetch_add(&hist[di], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            __syncthreads();
-            if (t < 64u) {                                      // exclusive scan of the counts: the cursors
-                uint32_t run = 0u;
-                for (uint32_t b = 0; b < a.n_desc; b += 64u) {
-                    const uint32_t d = b + lane;
-                    const uint32_t x = d < a.n_desc ? hist[d] : 0u;
-                    uint32_t inc = x;
-#pragma unroll
-                    for (int o = 1; o < 64; o <<= 1) {
-                        const uint32_t y = __shfl_up(inc, o);
-                        inc += lane >= uint32_t(o) ? y : 0u;
-                    }
-                    if (d < a.n_desc) hist[a.n_desc + d] = run + inc - x;
-                    run += __shfl(inc, 63);
-                }
-                if (t == 0u) hist[2u * a.n_desc] = run;
-            }
-            __syncthreads();
-            if (scan) {
-                const uint32_t pos = __hip_atomic_fetch_add(&hist[a.n_desc + uint32_t(di)], 1u, __ATOMIC_RELAXED,
-                                                            __HIP_MEMORY_SCOPE_WORKGROUP);
-                perm[pos] = uint16_t(t);
-            }
-            __syncthreads();
-            uint32_t ekey = 0xFFFFFFFFu;
-            if (t < hist[2u * a.n_desc]) {
-                const uint32_t o = perm[t];
-                const uint32_t meta = cmeta[o];
-                const ConnDesc Dd = a.desc[meta >> 16];
-                const A x = syn ? cs[o] : cd[o], y = syn ? cd[o] : cs[o];
-                const bool x4 = (meta >> (syn ? 8 : 9)) & 1u, y4 = (meta >> (syn ? 9 : 8)) & 1u;
-                const uint32_t port = syn ? cport[o] >> 16 : cport[o] & 0xFFFFu, pp = meta & 0xFFu;
-                uint32_t res = 0u, rule = Dd.n_rules;           // default DENY (:667)
-                for (uint32_t q = 0; q < Dd.n; ++q) {
-                    const R rr = conn_rule<kLdsRules>(g, Dd.rule_off + q);
-                    const uint32_t m8 = (rr.meta >> (8u * pp)) & 0xFFu;
-                    const uint32_t pw = pp == 0u ? rr.port[0] : pp == 1u ? rr.port[1] : 0xFFFF0000u;
-                    if ((m8 & 0x80u) && conn_match(rr, x, y, x4, y4) && port_in(port, pw)) {
-                        res = m8 & 3u;
-                        rule = conn_index(rr);
-                        break;
-                    }
-                }
-                cres[o] = res;
-                ekey = Dd.ctr_off + rule;
-            }
-            __syncthreads();
-            if (scan) r = cres[t];
-            if constexpr (kCount == 1) {
-                if (key != 0xFFFFFFFFu)
-                    __hip_atomic_fetch_add(lctr_t(a.ctr_lds + 4u * key), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                if (ekey != 0xFFFFFFFFu)
-                    __hip_atomic_fetch_add(lctr_t(a.ctr_lds + 4u * ekey), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            } else if constexpr (kCount == 2) {
-                wave_count(a.ctr, key);
-                wave_count(a.ctr, ekey);
-            }
-            if (need) {
-                if (r == 3u) {
-                    v = 3u;
-                    live = false;
-                } else if (r == 0u) {
-                    v = syn ? 0u : 1u;                          // DenySyn / DenySynAck
-                    live = false;
-                } else if (r == 2u && syn) {                    // REFLECT marks the side (and the other if same)
-                    if (k == 0u) {
-                        srefl = true;
-                        drefl = same;
-                    } else {
-                        drefl = true;
-                        srefl = srefl || same;
-                    }
-                }
-            }
-        }
-        if (i < a.n) a.out[i] = uint8_t(live ? 2u : v);
-        __syncthreads();                                        // the chunk arrays are reused
     }
     if constexpr (kCount == 1) {
         __syncthreads();
@@ -863,9 +740,9 @@ hipError_t launch_stream(const Pkts4* p4, const Pkts16* p16, uint8_t* verdict, i
     return hipGetLastError();
 }
 
-hipError_t launch_connect(const ConnArgs& a, bool k16, bool lds_rules, int count, int grid, hipStream_t s) {
+hipError_t launch_connect(const ConnArgs& a, bool k16, bool lds_rules, int count, int grid, size_t lds,
+                          hipStream_t s) {
     if (a.n == 0) return hipSuccess;
-    const size_t lds = (lds_rules ? a.rules_bytes : 0) + (count == 1 ? size_t(a.n_ctr) * 4 : 0);
 #define CONN_CASE(K16, L, C)                                                                               \
     if (k16 == K16 && lds_rules == L && count == C) {                                                      \
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(connect_kernel<K16, L, C>),                \
@@ -878,29 +755,6 @@ hipError_t launch_connect(const ConnArgs& a, bool k16, bool lds_rules, int count
     CONN_CASE(true, false, 0) CONN_CASE(true, false, 1) CONN_CASE(true, false, 2)
     CONN_CASE(true, true, 0) CONN_CASE(true, true, 1) CONN_CASE(true, true, 2)
 #undef CONN_CASE
-    return hipErrorInvalidValue;
-}
-
-uint32_t conn_sorted_lds(bool k16, uint32_t n_desc) {
-    const uint32_t C = kConnSortBlock, ab = k16 ? 16u : 4u;
-    return C * (2u * ab + 12u) + (2u * n_desc + 4u) * 4u + C * 2u;
-}
-
-hipError_t launch_connect_sorted(const ConnArgs& a, bool k16, bool lds_rules, int count, int grid,
-                                 size_t lds, hipStream_t s) {
-    if (a.n == 0) return hipSuccess;
-#define CONNS_CASE(K16, L, C)                                                                              \
-    if (k16 == K16 && lds_rules == L && count == C) {                                                      \
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(connect_sorted_kernel<K16, L, C>),         \
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));                   \
-        hipLaunchKernelGGL((connect_sorted_kernel<K16, L, C>), dim3(grid), dim3(kConnSortBlock), lds, s, a); \
-        return hipGetLastError();                                                                          \
-    }
-    CONNS_CASE(false, false, 0) CONNS_CASE(false, false, 1) CONNS_CASE(false, false, 2)
-    CONNS_CASE(false, true, 0) CONNS_CASE(false, true, 1) CONNS_CASE(false, true, 2)
-    CONNS_CASE(true, false, 0) CONNS_CASE(true, false, 1) CONNS_CASE(true, false, 2)
-    CONNS_CASE(true, true, 0) CONNS_CASE(true, true, 1) CONNS_CASE(true, true, 2)
-#undef CONNS_CASE
     return hipErrorInvalidValue;
 }
 

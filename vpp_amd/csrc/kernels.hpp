@@ -162,6 +162,7 @@ struct ConnDesc {                // one bound ACL for the connection kernel
 struct IfAcls {                  // interface -> (inbound, outbound) ConnDesc index, -1 = nil
     int32_t in, out;
 };
+static_assert(sizeof(ConnDesc) == 32 && sizeof(IfAcls) == 8, "connect_kernel reads the staged tables as 16-B / 8-B words");
 struct ConnArgs {
     const ConnDesc* desc;
     const IfAcls* ifs;
@@ -180,21 +181,14 @@ struct ConnArgs {
     const uint8_t* proto;
     uint64_t n;
     uint8_t* out;
-    uint32_t chunk_lds;          // sorted variant: LDS byte offset of the chunk arrays
-    uint32_t n_desc;             // sorted variant: descriptors (the per-ACL histogram)
+    uint32_t n_desc;             // descriptors in desc
+    uint32_t meta_lds;           // LDS byte offset of the staged desc + ifs tables; ~0u: global reads
 };
 // k16: 16-byte addresses; lds_rules: stage the pool; count: 0 none, 1 LDS
-// counters, 2 global (wave-aggregated) counters; grid: persistent workgroups
-hipError_t launch_connect(const ConnArgs& a, bool k16, bool lds_rules, int count, int grid, hipStream_t s);
-// The sorted variant: workgroups of kConnSortBlock threads take chunks of as
-// many connections; per evaluation step the connections whose ACL is scanned
-// linearly are counting-sorted by ACL in LDS, so each wave scans (mostly) one
-// ACL with broadcast rule reads.  LDS: the pool / counters as above, then
-// the chunk at a.chunk_lds (conn_sorted_lds bytes).
-constexpr uint32_t kConnSortBlock = 256;
-uint32_t conn_sorted_lds(bool k16, uint32_t n_desc);
-hipError_t launch_connect_sorted(const ConnArgs& a, bool k16, bool lds_rules, int count, int grid,
-                                 size_t lds_bytes, hipStream_t s);
+// counters, 2 global (wave-aggregated) counters; grid: persistent workgroups;
+// lds: dynamic LDS bytes (pool, LDS counters, a.meta_lds tables)
+hipError_t launch_connect(const ConnArgs& a, bool k16, bool lds_rules, int count, int grid, size_t lds,
+                          hipStream_t s);
 // tables' connection counters += the call's counters (ConnDesc ctr_off ..
 // + n_rules), which are cleared: one workgroup per descriptor
 hipError_t launch_conn_scatter(const ConnDesc* desc, unsigned long long* const* table_ctr, uint32_t n_desc,

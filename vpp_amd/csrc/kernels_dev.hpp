@@ -1216,9 +1216,26 @@ static void launch_cls(const Cls4Dev& t, const Pkts4& p, uint8_t* verdict, unsig
 }
 
 // source lookup variant: 0 interval search, 1 hash LPM, 2 hash LPM with one
-// length, 3 source trie (kMode 4)
+// length, 3 source trie (kMode 4), 4 inline hash cells (kMode 6)
 static inline int src_variant(const Cls4Dev& t) {
     return t.mode == 6 ? 4 : t.mode == 4 ? 3 : t.mode != 1 ? 0 : t.n_hash == 1 ? 2 : 1;
+}
+
+// Whether the dispatchers below have a kernel for this image (the engine
+// refuses the others before they get here; the launchers check again, so a
+// combination without a case is an error, never another variant's kernel
+// reading the image wrongly).  rep16: the 16-byte core (modes 0-4, 6; mode 3
+// = rows from the host hashes).
+static inline bool cls_dispatchable(const Cls4Dev& t, bool lds, bool rep16) {
+    const uint32_t lm = t.list_mode;
+    if (lm > 6 || (lm >= 5 && !lds)) return false;
+    switch (t.mode) {
+    case 0: case 1: return true;
+    case 3: return rep16;
+    case 4: return lds && lm >= 3;
+    case 6: return lds && (lm == 3 || lm == 4);
+    default: return false;
+    }
 }
 
 template <bool kLds, bool kVec>
@@ -1320,6 +1337,11 @@ static void dispatch16(const Cls4Dev& t, const Fe16& fe, const Pkts16& p, uint8_
     }
     const int src = src_variant(t);
     if constexpr (kLds) {
+        if (src == 4) {                               // inline hash cells over reps
+            if (t.list_mode == 3) launch16_cls<kLds, 6, 3, 0>(t, fe, p, verdict, gslot, cfg);
+            else if (t.list_mode == 4) launch16_cls<kLds, 6, 4, 0>(t, fe, p, verdict, gslot, cfg);
+            return;
+        }
         // the source trie over reps (sublist modes) and the wide cells (LDS-resident images only)
         if (src == 3 || t.list_mode >= 5) {
 #define CLS16_TW_CASES(L)                                                                     \
@@ -1431,6 +1453,11 @@ static void dispatch_slots16(const Cls4Dev& t, const Fe16& fe, const Pkts16& p, 
     }
     const int src = src_variant(t);
     if constexpr (kLds) {
+        if (src == 4) {                               // inline hash cells over reps
+            if (t.list_mode == 3) launch16_d<kLds, 6, 3, -1, false, 0, 2>(t, fe, p, o, nullptr, cfg);
+            else if (t.list_mode == 4) launch16_d<kLds, 6, 4, -1, false, 0, 2>(t, fe, p, o, nullptr, cfg);
+            return;
+        }
         if (src == 3 || t.list_mode >= 5) {
 #define CLS16_SLOTTW_CASES(L)                                                                      \
     case 4 * L + 0: launch16_d<kLds, 0, L, -1, false, 0, 2>(t, fe, p, o, nullptr, cfg); return;    \
