@@ -1437,9 +1437,17 @@ static bool build_cls4_one(const std::vector<SemRule>& sem, uint32_t n_rules, Cl
             else if (mode0 == 0) cand[0] = 1, cand[1] = 0;
             else cand[1] = 1;
         }
+        // dependent LDS reads per packet: interval search log2(top) + 1 steps
+        // and the class read; trie level 1, node, its leaf steps, final read
+        uint32_t isearch = 2;
+        for (uint32_t s = top; s > 1; s >>= 1) ++isearch;
         for (int tr : cand) {
             if (tr < 0) continue;
             if (!serialise(lm, tr != 0, wide)) continue;
+            // a small interval table searches in no more dependent reads than
+            // the trie walks, in a fraction of its LDS (the trie's first level
+            // alone is 1 KiB): take the interval search
+            if (tr && tmode != 1 && cand[1] == 0 && 3u + img.trie_depth >= isearch) continue;
             const bool ok = cell_ok(lm) && place_counters(img, budget, partial);
             if (dbg)
                 std::fprintf(stderr, "list mode %u%s%s%s: lds %u img %u ctr %u lctr %u ctr16 %u -> %s\n", img.list_mode,
