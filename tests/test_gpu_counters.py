@@ -46,7 +46,7 @@ def _budget(h, tier):
         return h.img_bytes + a16(2 * h.n_ctr) + hot
     if tier == "partial":
         return h.img_bytes + hot + a16(2 * max(h.n_hot, h.n_ctr // 3))
-    return h.img_bytes - 16                      # "global": the image does not fit
+    return 256                                   # "global": no image of this table fits
 
 
 def _check(eng, rules, tr, monkeypatch, tier):
@@ -54,6 +54,10 @@ def _check(eng, rules, tr, monkeypatch, tier):
     assert h.has_cls
     monkeypatch.setenv("CONTIVCLS_LDS_BUDGET", str(_budget(h, tier)))
     monkeypatch.setenv("CONTIVCLS_LIST_MODE", str(h.list_mode))   # the layout the budget was sized on
+    # and its source lookup: under a smaller budget the compiler would take
+    # the smaller interval table instead of the trie, and its counters would
+    # fit another tier
+    monkeypatch.setenv("CONTIVCLS_TRIE", "1" if h.mode == 4 else "0")
     monkeypatch.setenv("CONTIVCLS_ORIENT", "src")
     t = eng.put_table("tier", rules)
     try:

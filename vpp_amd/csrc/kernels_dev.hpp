@@ -40,6 +40,11 @@
 #ifndef CLS_ABLATE
 #define CLS_ABLATE 0
 #endif
+// 0: the 4-ary sublist search compiled out (A/B builds only: such a build
+// must not classify an image compiled with CONTIVCLS_SUB4=1)
+#ifndef CLS_SUB4_KERNEL
+#define CLS_SUB4_KERNEL 1
+#endif
 
 namespace cls {
 
@@ -367,7 +372,7 @@ __device__ __forceinline__ void classify_n(const Img<kLds>& im, const Cls4Dev& t
         if constexpr (CLS_ABLATE & 2) {
 #pragma unroll
             for (int q = 0; q < N; ++q) st[q] ^= dst[q] & 0x10000000u;   // keep dst live
-        } else if (t.sub4) {
+        } else if (CLS_SUB4_KERNEL && t.sub4) {
             // 4-ary node trees (compile.cpp sub4): L - 1 interior levels
             // {k1, k2, k3, first child}, then the leaf {k1, k2, k3, outcomes};
             // c = #(k_i < dst) picks the child / interval.  One ds_read_b128
@@ -800,6 +805,40 @@ __global__ __launch_bounds__(kClsBlock) void classify4_cls(Cls4Dev t, Cls4Dev o,
                 b.pr[k] = CLS_NT_PROTO ? ldnt(at(PR, gi)) : *at(PR, gi);
             }
         };
+        // the step's lookups; its verdict words (4 packets each) into vw
+        auto compute = [&](const Buf& b, uint32_t g, uint32_t (&vw)[kG]) {
+            constexpr int kN = 4 * kG;
+            uint32_t sa[kN], da[kN], pa[kN], ra[kN];
+            bool other = false;
+#pragma unroll
+            for (int k = 0; k < kG; ++k) {
+                sa[4 * k + 0] = b.s[k].x; sa[4 * k + 1] = b.s[k].y; sa[4 * k + 2] = b.s[k].z; sa[4 * k + 3] = b.s[k].w;
+                da[4 * k + 0] = b.d[k].x; da[4 * k + 1] = b.d[k].y; da[4 * k + 2] = b.d[k].z; da[4 * k + 3] = b.d[k].w;
+                pa[4 * k + 0] = b.dp[k].x & 0xFFFFu; pa[4 * k + 1] = b.dp[k].x >> 16;
+                pa[4 * k + 2] = b.dp[k].y & 0xFFFFu; pa[4 * k + 3] = b.dp[k].y >> 16;
+                const uint32_t pr = b.pr[k];
+                ra[4 * k + 0] = pr & 0xFFu; ra[4 * k + 1] = (pr >> 8) & 0xFFu;
+                ra[4 * k + 2] = (pr >> 16) & 0xFFu; ra[4 * k + 3] = pr >> 24;
+                other |= ((pr | ((pr & 0x7F7F7F7Fu) + 0x7D7D7D7Du)) & 0x80808080u) != 0u;
+            }
+            uint32_t v[kN], ix[kN];
+#pragma unroll
+            for (int k = 0; k < kN; ++k) ix[k] = 4u * (g + uint32_t(k / 4) * nthreads) + uint32_t(k % 4);
+            run_n<kN, kLds, kMode, kList, kD, kCtr>(im, t, o, hot_lane, gslot, hot0, sa, da, pa, ra, other, v, sa, ix,
+                                                    oq_lds);
+#pragma unroll
+            for (int k = 0; k < kG; ++k) vw[k] = v[4 * k] | (v[4 * k + 1] << 8) | (v[4 * k + 2] << 16) | (v[4 * k + 3] << 24);
+        };
+        auto store = [&](const uint32_t (&vw)[kG], uint32_t g) {
+            if (verdict) {
+#pragma unroll
+                for (int k = 0; k < kG; ++k)
+                    stnt(vw[k], const_cast<uint32_t*>(at(reinterpret_cast<const uint32_t*>(verdict),
+                                                         g + uint32_t(k) * nthreads)));
+            }
+        };
+        (void)compute;
+        (void)store;
         auto step = [&](const Buf& b, uint32_t g) {
             constexpr int kN = 4 * kG;
             uint32_t sa[kN], da[kN], pa[kN], ra[kN];
@@ -836,7 +875,55 @@ __global__ __launch_bounds__(kClsBlock) void classify4_cls(Cls4Dev t, Cls4Dev o,
             }
         };
         // Full steps over groups [0, nfull) (CLS_PREFETCH above).
-#if CLS_PREFETCH == 2
+#if CLS_PREFETCH == 3
+        if constexpr (kCtr != 2) {
+            // The next step's loads in flight during this step's lookups, in
+            // an order the vmcnt counter can serve: with a store and loads
+            // both pending the compiler can only wait for vmcnt(0), so a step
+            // first waits for its own loads (issued one step earlier, with
+            // the store before them), then stores the previous step's
+            // verdicts, then issues the next step's loads, then looks up --
+            // the scheduling barriers keep the loads from being hoisted above
+            // that wait.
+            if (nfull) {
+                Buf a, b;
+                uint32_t vw[kG];
+                auto pin = [&](const Buf& c) {
+#pragma unroll
+                    for (int k = 0; k < kG; ++k)
+                        asm volatile("" :: "v"(c.s[k].x), "v"(c.s[k].y), "v"(c.s[k].z), "v"(c.s[k].w),
+                                     "v"(c.d[k].x), "v"(c.d[k].y), "v"(c.d[k].z), "v"(c.d[k].w),
+                                     "v"(c.dp[k].x), "v"(c.dp[k].y), "v"(c.pr[k]));
+                };
+                auto turn = [&](Buf& cur, Buf& nxt, uint32_t g, bool st) {
+                    pin(cur);
+                    __builtin_amdgcn_sched_barrier(0);
+                    if (st) store(vw, g - span);
+                    load(nxt, g + span, true);
+                    __builtin_amdgcn_sched_barrier(0);
+                    compute(cur, g, vw);
+                };
+                uint32_t g = tid;
+                load(a, g, true);
+                turn(a, b, g, false);
+                g += span;
+                while (g < nfull) {
+                    turn(b, a, g, true);
+                    g += span;
+                    if (g >= nfull) break;
+                    turn(a, b, g, true);
+                    g += span;
+                }
+                store(vw, g - span);
+            }
+        } else {
+            for (uint32_t g = tid; g < nfull; g += span) {
+                Buf a;
+                load(a, g, true);
+                step(a, g);
+            }
+        }
+#elif CLS_PREFETCH == 2
         // two steps of loads in flight: three buffers in turn
         if (nfull) {
             Buf a, b, c;
