@@ -10,7 +10,12 @@ OUT=$ROOT/gpurun_out/$TAG
 mkdir -p $OUT
 cd $ROOT
 export TMPDIR=/tmp
-timeout -k 10 400 python tools/ab_inproc.py --config 3 --rounds 8 vpp_amd/libcontivcls.so vpp_amd/variants/lib_nos4.so vpp_amd/variants/lib_pf3.so vpp_amd/variants/lib_pf3nos4.so > $OUT/ab3.txt 2>&1
+for a in memset rand; do
+  timeout -k 10 60 tools/stream_glds.bin $a > $OUT/stream_glds_$a.txt 2>&1
+  timeout -k 10 60 tools/stream16_glds.bin $a > $OUT/stream16_glds_$a.txt 2>&1
+done
+head -30 $OUT/stream_glds_*.txt $OUT/stream16_glds_*.txt
+timeout -k 10 400 python tools/ab_inproc.py --config 3 --rounds 8 vpp_amd/libcontivcls.so vpp_amd/variants/lib_nos4.so vpp_amd/variants/lib_pf3.so > $OUT/ab3.txt 2>&1
 cat $OUT/ab3.txt
 timeout -k 10 200 python bench.py --steps 20 --warmup 5 --cpu-sample 0 > $OUT/b_s20w5.json 2> $OUT/b.err
 timeout -k 10 200 python bench.py --steps 50 --warmup 25 --cpu-sample 0 > $OUT/b_s50w25.json 2>> $OUT/b.err

@@ -134,7 +134,19 @@ __global__ __launch_bounds__(1024) void k(const uint4* S, const uint4* D, const 
     if (acc == 0x12345678u) sink[0] = acc;
 }
 
-int main() {
+// splitmix64 bytes: the stream over data like the benchmark's (a memset
+// pattern toggles no bits and streams faster)
+__global__ void fill_rand(uint64_t* p, uint64_t n, uint64_t seed) {
+    for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < n; i += uint64_t(gridDim.x) * blockDim.x) {
+        uint64_t z = (i + seed) * 0x9E3779B97F4A7C15ull;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        p[i] = z ^ (z >> 31);
+    }
+}
+
+int main(int argc, char** argv) {
+    const bool rnd = argc > 1 && argv[1][0] == 'r';
     const uint64_t N = 1ull << 28;
     uint4 *src, *dst;
     uint16_t* dp;
@@ -144,6 +156,14 @@ int main() {
     CK(hipMalloc(&pr, N)); CK(hipMalloc(&v, N)); CK(hipMalloc(&sink, 64));
     CK(hipMemset(src, 1, N * 16)); CK(hipMemset(dst, 2, N * 16)); CK(hipMemset(dp, 3, N * 2));
     CK(hipMemset(pr, 1, N)); CK(hipMemset(v, 0, N));
+    if (rnd) {
+        fill_rand<<<1024, 256>>>(reinterpret_cast<uint64_t*>(src), N * 16 / 8, 1);
+        fill_rand<<<1024, 256>>>(reinterpret_cast<uint64_t*>(dst), N * 16 / 8, 2);
+        fill_rand<<<1024, 256>>>(reinterpret_cast<uint64_t*>(dp), N * 2 / 8, 3);
+        fill_rand<<<1024, 256>>>(reinterpret_cast<uint64_t*>(pr), N / 8, 4);
+        CK(hipDeviceSynchronize());
+        printf("random data\n");
+    }
     int ncu = 0;
     CK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0));
     hipEvent_t e0, e1;

@@ -1298,7 +1298,10 @@ int cls_connect_batch(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t*
     const size_t meta_at = (lds + 15) & ~size_t(15);
     const size_t meta = desc.size() * sizeof(ConnDesc) + ifs.size() * sizeof(IfAcls);
     a.meta_lds = 0xFFFFFFFFu;
-    if (meta_at + meta <= lds_max && !(no_lds & 4)) {
+    // ... unless they would cost a workgroup per CU (the pool and counters
+    // alone leave room for two)
+    auto per_cu_of = [&](size_t b) { return b ? std::max(1, std::min(2, int(lds_max / b))) : 2; };
+    if (meta_at + meta <= lds_max && per_cu_of(meta_at + meta) == per_cu_of(lds) && !(no_lds & 4)) {
         a.meta_lds = uint32_t(meta_at);
         lds = meta_at + meta;
     }

@@ -40,11 +40,6 @@
 #ifndef CLS_ABLATE
 #define CLS_ABLATE 0
 #endif
-// 0: the 4-ary sublist search compiled out (A/B builds only: such a build
-// must not classify an image compiled with CONTIVCLS_SUB4=1)
-#ifndef CLS_SUB4_KERNEL
-#define CLS_SUB4_KERNEL 1
-#endif
 
 namespace cls {
 
@@ -372,16 +367,19 @@ __device__ __forceinline__ void classify_n(const Img<kLds>& im, const Cls4Dev& t
         if constexpr (CLS_ABLATE & 2) {
 #pragma unroll
             for (int q = 0; q < N; ++q) st[q] ^= dst[q] & 0x10000000u;   // keep dst live
-        } else if (CLS_SUB4_KERNEL && t.sub4) {
+        } else if (kD < 0 && t.sub4) {
+            // (depth-specialised variants are binary-only: a run-time branch
+            // there cost the hot config-3 kernel 6 %, 0.561 -> 0.598 ms,
+            // profiles/r03j_ab_config3.txt; sub4 images take the kD < 0 kernels)
             // 4-ary node trees (compile.cpp sub4): L - 1 interior levels
             // {k1, k2, k3, first child}, then the leaf {k1, k2, k3, outcomes};
             // c = #(k_i < dst) picks the child / interval.  One ds_read_b128
             // per level: half the binary form's dependent reads.  L = 0: the
             // pointer table held the outcome.
-            const uint32_t L = kD >= 0 ? uint32_t(kD) : t.bv_steps;
+            const uint32_t L = t.bv_steps;
 #pragma unroll
-            for (uint32_t l = 0; l + 1 < (kD >= 0 ? uint32_t(kD) : 4u); ++l) {
-                if (kD < 0 && l + 1 >= L) break;
+            for (uint32_t l = 0; l + 1 < 4u; ++l) {
+                if (l + 1 >= L) break;
                 uint4 e[N];
 #pragma unroll
                 for (int q = 0; q < N; ++q) e[q] = im.u128(st[q]);
@@ -1289,7 +1287,7 @@ static void launch_cls(const Cls4Dev& t, const Pkts4& p, uint8_t* verdict, unsig
         }
     }
     if constexpr (kLds && kVec && (kList == 3 || kList == 4)) {
-        switch (t.bv_steps) {
+        switch (t.sub4 ? -1 : int(t.bv_steps)) {
         case 0: launch_d<kLds, kVec, kMode, kList, 0>(t, p, verdict, gslot, cfg); return;
         case 1: launch_d<kLds, kVec, kMode, kList, 1>(t, p, verdict, gslot, cfg); return;
         case 2: launch_d<kLds, kVec, kMode, kList, 2>(t, p, verdict, gslot, cfg); return;
@@ -1388,7 +1386,7 @@ static void launch16_cls(const Cls4Dev& t, const Fe16& fe, const Pkts16& p, uint
         }
     }
     if constexpr (kLds && (kList == 3 || kList == 4)) {
-        switch (t.bv_steps) {
+        switch (t.sub4 ? -1 : int(t.bv_steps)) {
         case 0: launch16_d<kLds, kMode, kList, 0, false, kFe>(t, fe, p, verdict, gslot, cfg); return;
         case 1: launch16_d<kLds, kMode, kList, 1, false, kFe>(t, fe, p, verdict, gslot, cfg); return;
         case 2: launch16_d<kLds, kMode, kList, 2, false, kFe>(t, fe, p, verdict, gslot, cfg); return;
