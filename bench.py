@@ -284,16 +284,23 @@ def main():
     ar = [a.elapsed_time(b) for a, b in ev]
     ar_ms = float(np.mean(ar)) if ar else 0.0
     ar_med = float(np.median(ar)) if ar else 0.0
-    floor_ms = None
+    floor_ms = shape_ms = None
+    lds = info["lds_bytes"] if af == 4 else info["lds_bytes_v16"]
+    resident = info["lds_resident"] if af == 4 else info["lds_resident_v16"]
+    two_per_cu = not resident or 2 * (lds + 16) <= 160 * 1024     # the classify launch's workgroups per CU
     if not args.no_stream_floor:
         # one launch covers at most 2^30 packets (the kernels' 32-bit offsets):
         # time the floor on that prefix and scale to the batch
         m = min(n, 1 << 30)
-        floor_ms = eng.stream_floor(pk["src"][:m], pk["dst"][:m], pk["dport"][:m], pk["proto"][:m],
-                                    verdict[:m]) * (n / m)
+        shapes = [t * (n / m) for t in eng.stream_floor_shapes(pk["src"][:m], pk["dst"][:m], pk["dport"][:m],
+                                                              pk["proto"][:m], verdict[:m])]
+        floor_ms = min(shapes)
+        # the fastest shape with the classify launch's workgroups per CU (the
+        # kernel cannot take the other: its LDS image allows one per CU)
+        shape_ms = min(t for i, t in enumerate(shapes) if (i & 1) == int(two_per_cu) or len(shapes) < 2)
     wall, k_max, kmed_max, ar_max, armed_max = D.max_over_ranks([wall, avg_k, med_k, ar_ms, ar_med], dev)
     if floor_ms is not None:
-        floor_ms = D.max_over_ranks(floor_ms, dev)
+        floor_ms, shape_ms = D.max_over_ranks([floor_ms, shape_ms], dev)
 
     if rank == 0:
         total = n * world * args.steps
@@ -349,6 +356,9 @@ def main():
                          "stream_floor_ms": round(floor_ms, 4) if floor_ms is not None else None,
                          "frac_of_stream_floor": round(floor_ms / avg_k, 4) if floor_ms else None,
                          "frac_of_stream_floor_median": round(floor_ms / med_k, 4) if floor_ms else None,
+                         "stream_floor_launch_shape_ms": round(shape_ms, 4) if shape_ms else None,
+                         "launch_shape": "%d x 1024-thread workgroups per CU" % (2 if two_per_cu else 1),
+                         "frac_of_launch_shape_floor": round(shape_ms / avg_k, 4) if shape_ms else None,
                          "algorithmic_bytes_per_launch": alg_bytes},
             "cpu_baseline": cpu,
         }

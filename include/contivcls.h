@@ -212,6 +212,14 @@ int cls_kernel_times_reset(cls_engine* e);
  * launches after one warm-up; *ms = the average launch.  Writes verdict. */
 int cls_stream_floor(cls_engine* e, const cls_pkt_soa* pkts, uint64_t n, uint8_t* verdict,
                      uint32_t reps, float* ms, void* stream);
+/* The same, one average per stream shape (cls_stream_floor returns their
+ * minimum): shape = variant << 1 | (two 1024-thread workgroups per CU, else
+ * one -- the classify kernel's own shape when its LDS image takes more than
+ * half of the CU's LDS); variant 0 / 1 / 2 / 3 = loads as classify4_cls / one
+ * step ahead / protocol non-temporal / both (CLS_AF_V16: variant 0 only).  Up
+ * to `cap` times into ms; *count = the number of shapes. */
+int cls_stream_floor_shapes(cls_engine* e, const cls_pkt_soa* pkts, uint64_t n, uint8_t* verdict,
+                            uint32_t reps, float* ms, uint32_t cap, uint32_t* count, void* stream);
 
 /* ---- ACL configuration (ACLConfig, aclengine_mock.go:110-121,671-728) --- */
 /* PutACL semantics (:699-728): requires >=1 interface; re-putting a name

@@ -865,10 +865,11 @@ int cls_classify(cls_engine* e, uint32_t table_id, const cls_pkt_soa* pk, uint64
     return finish_counts(e, *t, t->c4, sc, co, n, verdict_out, d_verdict, counters_out, flags, s, remapped);
 }
 
-int cls_stream_floor(cls_engine* e, const cls_pkt_soa* pk, uint64_t n, uint8_t* verdict, uint32_t reps,
-                     float* ms, void* stream) {
-    if (!e || !pk || !ms || !verdict || n == 0 || n > kClsChunk) return CLS_E_INVAL;
-    std::lock_guard<std::mutex> g(e->mu);
+// Each stream shape's time (cls_stream_floor_shapes): shape = variant << 1 |
+// (two workgroups per CU), 8 shapes for the IPv4 layout, 2 for the 16-byte one.
+static int stream_shapes(cls_engine* e, const cls_pkt_soa* pk, uint64_t n, uint8_t* verdict, uint32_t reps,
+                         std::vector<float>& out, void* stream) {
+    if (!e || !pk || !verdict || n == 0 || n > kClsChunk) return CLS_E_INVAL;
     HIPC(e, hipSetDevice(e->device));
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : e->stream;
     Pkts4 p4{pk->src4, pk->dst4, pk->dport, pk->proto, n};
@@ -901,7 +902,7 @@ int cls_stream_floor(cls_engine* e, const cls_pkt_soa* pk, uint64_t n, uint8_t* 
     int rc = CLS_OK;
     const uint32_t k = std::max<uint32_t>(1, reps);
     const bool dbg = std::getenv("CONTIVCLS_DEBUG_FLOOR") != nullptr;
-    *ms = 0.0f;
+    out.clear();
     for (int shape = 0; shape < (v4 ? 8 : 2) && rc == CLS_OK; ++shape) {
         const int grid = e->n_cu * (1 + (shape & 1)), variant = shape >> 1;
         for (uint32_t i = 0; i <= k && rc == CLS_OK; ++i) {   // launch 0: warm-up
@@ -915,7 +916,7 @@ int cls_stream_floor(cls_engine* e, const cls_pkt_soa* pk, uint64_t n, uint8_t* 
             hipEventElapsedTime(&t, a, b) == hipSuccess) {
             t /= float(k);
             if (dbg) std::fprintf(stderr, "stream floor: grid %d variant %d: %.4f ms\n", grid, variant, t);
-            if (*ms == 0.0f || t < *ms) *ms = t;
+            out.push_back(t);
         } else if (rc == CLS_OK) {
             rc = fail(e, CLS_E_HIP, "stream floor timing failed");
         }
@@ -923,6 +924,29 @@ int cls_stream_floor(cls_engine* e, const cls_pkt_soa* pk, uint64_t n, uint8_t* 
     (void)hipEventDestroy(a);
     (void)hipEventDestroy(b);
     return rc;
+}
+
+int cls_stream_floor(cls_engine* e, const cls_pkt_soa* pk, uint64_t n, uint8_t* verdict, uint32_t reps,
+                     float* ms, void* stream) {
+    if (!e || !ms) return CLS_E_INVAL;
+    std::lock_guard<std::mutex> g(e->mu);
+    std::vector<float> t;
+    const int rc = stream_shapes(e, pk, n, verdict, reps, t, stream);
+    if (rc != CLS_OK) return rc;
+    *ms = *std::min_element(t.begin(), t.end());
+    return CLS_OK;
+}
+
+int cls_stream_floor_shapes(cls_engine* e, const cls_pkt_soa* pk, uint64_t n, uint8_t* verdict, uint32_t reps,
+                            float* ms, uint32_t cap, uint32_t* count, void* stream) {
+    if (!e || !count || (cap && !ms)) return CLS_E_INVAL;
+    std::lock_guard<std::mutex> g(e->mu);
+    std::vector<float> t;
+    const int rc = stream_shapes(e, pk, n, verdict, reps, t, stream);
+    if (rc != CLS_OK) return rc;
+    *count = uint32_t(t.size());
+    std::copy(t.begin(), t.begin() + std::min<size_t>(cap, t.size()), ms);
+    return CLS_OK;
 }
 
 int cls_last_kernel_ms(cls_engine* e, float* ms) {

@@ -366,7 +366,7 @@ __device__ __forceinline__ void classify_n(const Img<kLds>& im, const Cls4Dev& t
         static_assert(kMaxBvSteps == 7, "step chain below");
         if constexpr (CLS_ABLATE & 2) {
 #pragma unroll
-            for (int q = 0; q < N; ++q) st[q] ^= dst[q] & 0x10000000u;   // keep dst live
+            for (int q = 0; q < N; ++q) asm volatile("" :: "v"(dst[q]));   // keep the dst loads
         } else if (kD < 0 && t.sub4) {
             // (depth-specialised variants are binary-only: a run-time branch
             // there cost the hot config-3 kernel 6 %, 0.561 -> 0.598 ms,

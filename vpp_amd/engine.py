@@ -144,7 +144,13 @@ class Engine:
     def stream_floor(self, src, dst, dport, proto, verdict, reps: int = 10, stream=None) -> float:
         """Average ms of the classify kernel's packet stream alone (same loads,
         stores and grid, no lookups) over a device batch: the measured floor
-        the classify kernel is compared against (bench.py)."""
+        the classify kernel is compared against (bench.py) -- the fastest
+        stream shape."""
+        return min(self.stream_floor_shapes(src, dst, dport, proto, verdict, reps, stream))
+
+    def stream_floor_shapes(self, src, dst, dport, proto, verdict, reps: int = 10, stream=None):
+        """Each stream shape's average ms (cls_stream_floor_shapes): index =
+        variant << 1 | two workgroups per CU; IPv4 8 shapes, 16-byte 2."""
         import torch
         v16 = src.dim() == 2
         n = int(dport.numel())
@@ -157,9 +163,12 @@ class Engine:
         if stream is None:
             stream = torch.cuda.current_stream()
         s = stream.cuda_stream if hasattr(stream, "cuda_stream") else stream
-        ms = C.c_float(0)
-        self._check(_abi.lib().cls_stream_floor(self.h, C.byref(pk), n, _ptr(verdict), reps, C.byref(ms), s))
-        return ms.value * (int(dport.numel()) / n if n else 1.0)
+        ms = (C.c_float * 8)()
+        cnt = C.c_uint32(0)
+        self._check(_abi.lib().cls_stream_floor_shapes(self.h, C.byref(pk), n, _ptr(verdict), reps, ms, 8,
+                                                       C.byref(cnt), s))
+        scale = int(dport.numel()) / n if n else 1.0
+        return [ms[i] * scale for i in range(cnt.value)]
 
     def last_kernel_ms(self) -> float:
         ms = C.c_float(0)
