@@ -126,7 +126,7 @@ def _run(eng, seed, mode, fam, count, n=20000, n_local=64):
     si = rng.integers(0, len(ifs), n)
     di = np.where(rng.random(n) < 0.1, si, rng.integers(0, len(ifs), n))
     args = [ids[si], ids[di], tr["src"], tr["dst"], tr["proto"], tr["sport"], tr["dport"]]
-    if mode == "device":                      # CLS_F_DEVICE batch: every ACL >= 64 rules on the classifier
+    if mode in ("device", "device_auto"):     # CLS_F_DEVICE batch: every ACL >= 64 rules on the classifier
         import torch
 
         def dev(x):
@@ -136,7 +136,10 @@ def _run(eng, seed, mode, fam, count, n=20000, n_local=64):
             return torch.from_numpy(x.view({4: np.int32, 2: np.int16, 1: np.uint8}[x.dtype.itemsize])).to("cuda")
         dv = [dev(x) for x in args]
         torch.cuda.synchronize()
-        got = eng.connect_batch(*dv, mode="classifier", count=count).cpu().numpy()
+        # device_auto: the default selection (ACLs of >= 2048 rules on the
+        # classifier, the others in the bitmap form or scanned)
+        got = eng.connect_batch(*dv, mode="classifier" if mode == "device" else "auto",
+                                count=count).cpu().numpy()
     else:
         got = eng.connect_batch(*args, mode=mode, count=count)
     want, wcounts = oracle_connections(bind, by_name, ifs, si, di, tr, fam)
@@ -153,13 +156,30 @@ def _run(eng, seed, mode, fam, count, n=20000, n_local=64):
     return want
 
 
-@pytest.mark.parametrize("mode", ["classifier", "linear", "auto", "device"])
+@pytest.mark.parametrize("mode", ["classifier", "linear", "auto", "device", "device_auto"])
 @pytest.mark.parametrize("seed", [0, 1])
 def test_connections_at_scale_match_oracle(seed, mode):
     from vpp_amd.engine import Engine
     eng = Engine()
     try:
         _run(eng, seed, mode, 4, count=False)
+    finally:
+        eng.close()
+
+
+@pytest.mark.parametrize("no_lds", [0, 1, 6])
+@pytest.mark.parametrize("bitmap", ["1", "0"])
+def test_connections_bitmap_form_match_oracle(bitmap, no_lds, monkeypatch):
+    """Device batches with the default selection: the linear IPv4 ACLs (1-300
+    random rules) in the bitmap form (engine.cpp conn_bitmap4) or scanned
+    (CONTIVCLS_CONN_BITMAP=0), the pool in LDS or (no_lds 1) global memory,
+    the counters and tables in global memory (no_lds 6); verdicts and per-(ACL, rule) counters against orc_test_connection."""
+    from vpp_amd.engine import Engine
+    monkeypatch.setenv("CONTIVCLS_CONN_BITMAP", bitmap)
+    monkeypatch.setenv("CONTIVCLS_CONN_NO_LDS", str(no_lds))
+    eng = Engine()
+    try:
+        _run(eng, 11 + no_lds, "device_auto", 4, count=True, n=16000, n_local=24)
     finally:
         eng.close()
 

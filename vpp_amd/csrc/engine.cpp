@@ -117,6 +117,10 @@ struct Table {
     // counters (CLS_F_COUNT; allocated on first use, R + 1 u64)
     std::vector<ConnRule4> conn4;
     std::vector<ConnRule16> conn16;
+    // the bitmap form of conn4 (conn_bitmap4), built on the first connection
+    // batch that wants it; empty when its tables exceed kConnBmMaxWords
+    std::vector<uint32_t> conn_bm;
+    bool conn_bm_built = false;
     DevBuf d_slot_rule;
     DevBuf d_conn_ctr;
     // declared last: destroyed first, so pending device work is waited for
@@ -471,6 +475,8 @@ constexpr uint64_t kConnClsMinBatch = 1ull << 16;  // connection batches that us
 constexpr uint32_t kConnClsMinRules = 64;          // ACLs evaluated by the classifier in connection batches
 constexpr uint32_t kConnClsWork = 2048;            // ... when touches x rules >= this x batch size (host batch)
 constexpr uint32_t kConnClsDevRules = 2048;        // ... when it has this many rules (device batch)
+constexpr uint32_t kConnBmMinRules = 8;            // linear IPv4 ACLs given the bitmap form (conn_bitmap4) ...
+constexpr size_t kConnBmMaxWords = 12288;          // ... when their tables take at most 48 KiB
 
 static bool aligned(const void* p, size_t a) { return (reinterpret_cast<uintptr_t>(p) % a) == 0; }
 
@@ -1106,6 +1112,94 @@ int cls_if_acls(cls_engine* e, uint32_t if_id, int32_t* in_table, int32_t* out_t
     return CLS_OK;
 }
 
+// The bitmap form of a linear IPv4 ACL (kernels.hpp kConnBmHeader): for the
+// source, the destination and each protocol's destination port, the
+// elementary intervals of the rules' prefixes (port ranges) and, per
+// interval, the bit row of the rules whose term holds there -- each
+// predicate evaluated exactly as the scan does (conn_match, the meta TERM bit,
+// port_in) at the interval's first value, which is exact because prefixes
+// and ranges only change membership at the interval starts.  Appends the
+// words (16-B multiple) to `out`; false (nothing appended) when the tables
+// would exceed `cap_words`.
+static bool conn_bitmap4(const std::vector<ConnRule4>& r, uint32_t n_rules, size_t cap_words,
+                         std::vector<uint32_t>& out) {
+    const uint32_t R = uint32_t(r.size()), W = std::max<uint32_t>(1, (R + 31) / 32);
+    (void)n_rules;
+    auto port_in = [](uint32_t port, uint32_t pw) { return ((port - (pw & 0xFFFFu)) & 0xFFFFu) <= (pw >> 16); };
+    struct Tab {
+        std::vector<uint32_t> keys, rows;
+    };
+    auto addr_tab = [&](bool dst) {
+        std::vector<uint64_t> b{0};
+        for (const ConnRule4& x : r) {
+            const uint32_t a = dst ? x.dst_addr : x.src_addr, m = dst ? x.dst_mask : x.src_mask;
+            if (!m) continue;
+            b.push_back(a);
+            b.push_back(uint64_t(a) + uint64_t(~m) + 1);        // one past the prefix
+        }
+        std::sort(b.begin(), b.end());
+        b.erase(std::unique(b.begin(), b.end()), b.end());
+        while (!b.empty() && b.back() > 0xFFFFFFFFull) b.pop_back();
+        Tab t;
+        for (uint64_t k : b) {
+            const uint32_t x = uint32_t(k);
+            t.keys.push_back(x);
+            const size_t at = t.rows.size();
+            t.rows.resize(at + W, 0u);
+            for (uint32_t i = 0; i < R; ++i) {
+                const uint32_t a = dst ? r[i].dst_addr : r[i].src_addr, m = dst ? r[i].dst_mask : r[i].src_mask;
+                if (((x ^ a) & m) == 0) t.rows[at + i / 32] |= 1u << (i % 32);
+            }
+        }
+        return t;
+    };
+    auto proto_tab = [&](uint32_t p) {
+        std::vector<uint32_t> b{0};
+        if (p < 2)
+            for (const ConnRule4& x : r) {
+                if (!((x.meta >> (8 * p)) & 0x80u)) continue;
+                const uint32_t lo = x.port[p] & 0xFFFFu, end = lo + (x.port[p] >> 16) + 1;   // one past hi
+                b.push_back(lo);
+                b.push_back(end & 0xFFFFu);                      // wraps to 0 past 65535
+            }
+        std::sort(b.begin(), b.end());
+        b.erase(std::unique(b.begin(), b.end()), b.end());
+        Tab t;
+        for (uint32_t x : b) {
+            t.keys.push_back(x);
+            const size_t at = t.rows.size();
+            t.rows.resize(at + W, 0u);
+            for (uint32_t i = 0; i < R; ++i) {
+                const uint32_t pw = p == 0 ? r[i].port[0] : p == 1 ? r[i].port[1] : 0xFFFF0000u;
+                if (((r[i].meta >> (8 * p)) & 0x80u) && port_in(x, pw)) t.rows[at + i / 32] |= 1u << (i % 32);
+            }
+        }
+        return t;
+    };
+    // size first (the rows are R x intervals bits)
+    size_t words = kConnBmHeader / 4 + 2 * size_t(R);
+    std::vector<Tab> tabs;
+    for (int k = 0; k < 6; ++k) {
+        tabs.push_back(k < 2 ? addr_tab(k == 1) : proto_tab(uint32_t(k - 2)));
+        words += tabs.back().keys.size() + tabs.back().rows.size();
+        if (words > cap_words) return false;
+    }
+    const size_t at = out.size();
+    out.insert(out.end(), {W, uint32_t(tabs[0].keys.size()), uint32_t(tabs[1].keys.size()), R,
+                           uint32_t(tabs[2].keys.size()), uint32_t(tabs[3].keys.size()),
+                           uint32_t(tabs[4].keys.size()), uint32_t(tabs[5].keys.size())});
+    for (const Tab& t : tabs) {
+        out.insert(out.end(), t.keys.begin(), t.keys.end());
+        out.insert(out.end(), t.rows.begin(), t.rows.end());
+    }
+    for (const ConnRule4& x : r) {
+        out.push_back(x.meta);
+        out.push_back(x.index);
+    }
+    out.resize(at + ((out.size() - at + 3) & ~size_t(3)), 0u);
+    return true;
+}
+
 int cls_connect_batch(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t* out,
                       uint32_t flags, void* stream) {
     if (!e || !c || (n && !out)) return CLS_E_INVAL;
@@ -1259,7 +1353,9 @@ int cls_connect_batch(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t*
     // the rule pool of the linear ACLs
     std::vector<uint8_t> pool;
     const size_t rb = k16 ? sizeof(ConnRule16) : sizeof(ConnRule4);
+    const size_t lds_max0 = size_t(max_lds_bytes());
     for (size_t j = 0; j < desc.size(); ++j) {
+        desc[j].bm_off = 0xFFFFFFFFu;
         if (desc[j].pre) {
             desc[j].n = 0;
             continue;
@@ -1268,6 +1364,32 @@ int cls_connect_batch(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t*
         const uint8_t* r = k16 ? reinterpret_cast<const uint8_t*>(dtab[j]->conn16.data())
                                : reinterpret_cast<const uint8_t*>(dtab[j]->conn4.data());
         pool.insert(pool.end(), r, r + size_t(desc[j].n) * rb);
+    }
+    // IPv4: the bitmap form of the longer linear ACLs, longest first, while
+    // the pool (and the LDS counters when counting) still fit LDS -- a wave
+    // then pays a fixed number of reads per evaluation instead of its
+    // longest lane's scan (CONTIVCLS_CONN_BITMAP=0: scans only).
+    const char* bme = std::getenv("CONTIVCLS_CONN_BITMAP");
+    if (!k16 && n && !(flags & CLS_F_FORCE_LINEAR) && !(bme && std::atoi(bme) == 0)) {
+        const size_t cap = lds_max0 - (count ? size_t(n_ctr) * 4 : 0) - std::min<size_t>(lds_max0 / 8, 8192);
+        std::vector<size_t> order;
+        for (size_t j = 0; j < desc.size(); ++j)
+            if (!desc[j].pre && desc[j].n >= kConnBmMinRules) order.push_back(j);
+        std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) { return desc[a].n > desc[b].n; });
+        std::vector<uint32_t> words;
+        for (size_t j : order) {
+            Table& t = *dtab[j];
+            if (!t.conn_bm_built) {                         // once per table: rules are immutable
+                if (!conn_bitmap4(t.conn4, t.n_rules, kConnBmMaxWords, t.conn_bm)) t.conn_bm.clear();
+                t.conn_bm_built = true;
+            }
+            const size_t used = pool.size() + words.size() * 4;
+            if (t.conn_bm.empty() || used + t.conn_bm.size() * 4 > cap) continue;
+            desc[j].bm_off = uint32_t(used);                // the pool is a multiple of 32 B, blobs of 16 B
+            words.insert(words.end(), t.conn_bm.begin(), t.conn_bm.end());
+        }
+        const uint8_t* wb = reinterpret_cast<const uint8_t*>(words.data());
+        pool.insert(pool.end(), wb, wb + words.size() * 4);
     }
     ConnArgs a{};
     a.n_ifs = n_ifs;

@@ -418,6 +418,7 @@ __device__ __forceinline__ ConnDesc conn_desc(const ConnArgs& a, uint32_t j) {
         d.rule_off = x.x; d.n = x.y; d.n_rules = x.z; d.ctr_off = x.w;
         d.pre = reinterpret_cast<const uint32_t*>(uint64_t(y.x) | (uint64_t(y.y) << 32));
         d.slot_rule = reinterpret_cast<const uint32_t*>(uint64_t(y.z) | (uint64_t(y.w) << 32));
+        d.bm_off = *lds32_t(b + 32u);
         return d;
     }
     return a.desc[j];
@@ -444,6 +445,69 @@ __device__ __forceinline__ uint32_t conn_scan(const ConnArgs& a, const ConnDesc&
         }
     }
     return res;
+}
+
+// One evalACL call on the bitmap form of an IPv4 ACL (kernels.hpp
+// kConnBmHeader; engine.cpp conn_bitmap4): three interval searches (source,
+// destination, the protocol's destination port; ICMP and OTHER have one
+// interval) give three bit rows, and the lowest bit set in all three is the
+// first rule that matches -- the scan's answer in a fixed number of reads,
+// so the lanes of a wave no longer wait for the longest scan among them.
+template <bool kLds>
+__device__ __forceinline__ uint32_t bm_u32(const uint8_t* g, uint32_t a) {
+    if constexpr (kLds) return *lds32_t(a);
+    else return *reinterpret_cast<const uint32_t*>(g + a);
+}
+// the row address of the interval holding x: branch-free lower bound over
+// the n keys at byte address o (key 0 first), rows after the keys
+template <bool kLds>
+__device__ __forceinline__ uint32_t bm_row(const uint8_t* g, uint32_t o, uint32_t n, uint32_t W, uint32_t x) {
+    uint32_t pos = 0, len = n;
+    while (len > 1u) {
+        const uint32_t h = len >> 1;
+        pos = bm_u32<kLds>(g, o + 4u * (pos + h)) <= x ? pos + h : pos;
+        len -= h;
+    }
+    return o + 4u * n + 4u * W * pos;
+}
+template <bool kLds>
+__device__ __forceinline__ uint32_t conn_bm(const ConnArgs& a, const ConnDesc& D, uint32_t s, uint32_t d,
+                                            uint32_t port, uint32_t p, uint32_t& rule) {
+    const uint8_t* g = static_cast<const uint8_t*>(a.rules);
+    const uint32_t B = D.bm_off;
+    uint32_t W, ns, nd, nr, np[4];
+    if constexpr (kLds) {
+        const v4u h0 = *lds128_t(B), h1 = *lds128_t(B + 16u);
+        W = h0.x; ns = h0.y; nd = h0.z; nr = h0.w;
+        np[0] = h1.x; np[1] = h1.y; np[2] = h1.z; np[3] = h1.w;
+    } else {
+        const uint4 h0 = *reinterpret_cast<const uint4*>(g + B), h1 = *reinterpret_cast<const uint4*>(g + B + 16u);
+        W = h0.x; ns = h0.y; nd = h0.z; nr = h0.w;
+        np[0] = h1.x; np[1] = h1.y; np[2] = h1.z; np[3] = h1.w;
+    }
+    uint32_t o = B + kConnBmHeader;
+    const uint32_t sr = bm_row<kLds>(g, o, ns, W, s);
+    o += 4u * ns * (1u + W);
+    const uint32_t dr = bm_row<kLds>(g, o, nd, W, d);
+    o += 4u * nd * (1u + W);
+    // the four protocol tables in turn, then the {meta, index} pairs
+    const uint32_t t1 = o + 4u * np[0] * (1u + W), t2 = t1 + 4u * np[1] * (1u + W);
+    const uint32_t t3 = t2 + 4u * np[2] * (1u + W);
+    const uint32_t op = p == 0u ? o : p == 1u ? t1 : p == 2u ? t2 : t3;
+    const uint32_t n = p == 0u ? np[0] : p == 1u ? np[1] : p == 2u ? np[2] : np[3];
+    o = t3 + 4u * np[3] * (1u + W);
+    const uint32_t pr = bm_row<kLds>(g, op, n, W, port);
+    for (uint32_t w = 0; w < W; ++w) {
+        const uint32_t m = bm_u32<kLds>(g, sr + 4u * w) & bm_u32<kLds>(g, dr + 4u * w) & bm_u32<kLds>(g, pr + 4u * w);
+        if (m) {
+            const uint32_t i = 32u * w + uint32_t(__builtin_ctz(m));
+            rule = bm_u32<kLds>(g, o + 8u * i + 4u);
+            return (bm_u32<kLds>(g, o + 8u * i) >> (8u * p)) & 3u;
+        }
+    }
+    (void)nr;
+    rule = D.n_rules;
+    return 0u;
 }
 
 // testConnection, one lane per connection: the evaluations in the
@@ -503,6 +567,10 @@ __global__ __launch_bounds__(1024) void connect_kernel(ConnArgs a) {
                         const uint32_t w = D.pre[uint64_t(k >> 1) * a.n + i];
                         res = w & 3u;
                         rule = kCount != 0 ? D.slot_rule[w >> 2] : 0u;
+                    } else if (!k16 && D.bm_off != 0xFFFFFFFFu) {
+                        if constexpr (!k16)
+                            res = k < 2 ? conn_bm<kLdsRules>(a, D, sa, da, dp, p, rule)
+                                        : conn_bm<kLdsRules>(a, D, da, sa, sp, p, rule);
                     } else if (k < 2) {
                         res = conn_scan<k16, kLdsRules>(a, D, sa, da, s4, d4, dp, p, rule);
                     } else {
