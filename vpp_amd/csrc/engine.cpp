@@ -1176,13 +1176,14 @@ static bool conn_bitmap4(const std::vector<ConnRule4>& r, uint32_t n_rules, size
         }
         return t;
     };
-    // size first (the rows are R x intervals bits)
+    // size first (the rows are R x intervals bits); interval counts fit the
+    // descriptor's 16-bit fields
     size_t words = kConnBmHeader / 4 + 2 * size_t(R);
     std::vector<Tab> tabs;
     for (int k = 0; k < 6; ++k) {
         tabs.push_back(k < 2 ? addr_tab(k == 1) : proto_tab(uint32_t(k - 2)));
         words += tabs.back().keys.size() + tabs.back().rows.size();
-        if (words > cap_words) return false;
+        if (words > cap_words || tabs.back().keys.size() > 0xFFFFu) return false;
     }
     const size_t at = out.size();
     out.insert(out.end(), {W, uint32_t(tabs[0].keys.size()), uint32_t(tabs[1].keys.size()), R,
@@ -1386,6 +1387,10 @@ int cls_connect_batch(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t*
             const size_t used = pool.size() + words.size() * 4;
             if (t.conn_bm.empty() || used + t.conn_bm.size() * 4 > cap) continue;
             desc[j].bm_off = uint32_t(used);                // the pool is a multiple of 32 B, blobs of 16 B
+            const std::vector<uint32_t>& h = t.conn_bm;     // header {W, ns, nd, nr, n0, n1, n2, n3}
+            desc[j].bm_sd = h[1] | (h[2] << 16);
+            desc[j].bm_tu = h[4] | (h[5] << 16);
+            desc[j].bm_w = h[0];
             words.insert(words.end(), t.conn_bm.begin(), t.conn_bm.end());
         }
         const uint8_t* wb = reinterpret_cast<const uint8_t*>(words.data());

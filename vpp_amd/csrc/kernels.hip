@@ -418,7 +418,8 @@ __device__ __forceinline__ ConnDesc conn_desc(const ConnArgs& a, uint32_t j) {
         d.rule_off = x.x; d.n = x.y; d.n_rules = x.z; d.ctr_off = x.w;
         d.pre = reinterpret_cast<const uint32_t*>(uint64_t(y.x) | (uint64_t(y.y) << 32));
         d.slot_rule = reinterpret_cast<const uint32_t*>(uint64_t(y.z) | (uint64_t(y.w) << 32));
-        d.bm_off = *lds32_t(b + 32u);
+        const v4u z = *lds128_t(b + 32u);
+        d.bm_off = z.x; d.bm_sd = z.y; d.bm_tu = z.z; d.bm_w = z.w;
         return d;
     }
     return a.desc[j];
@@ -458,54 +459,40 @@ __device__ __forceinline__ uint32_t bm_u32(const uint8_t* g, uint32_t a) {
     if constexpr (kLds) return *lds32_t(a);
     else return *reinterpret_cast<const uint32_t*>(g + a);
 }
-// the row address of the interval holding x: branch-free lower bound over
-// the n keys at byte address o (key 0 first), rows after the keys
-template <bool kLds>
-__device__ __forceinline__ uint32_t bm_row(const uint8_t* g, uint32_t o, uint32_t n, uint32_t W, uint32_t x) {
-    uint32_t pos = 0, len = n;
-    while (len > 1u) {
-        const uint32_t h = len >> 1;
-        pos = bm_u32<kLds>(g, o + 4u * (pos + h)) <= x ? pos + h : pos;
-        len -= h;
-    }
-    return o + 4u * n + 4u * W * pos;
-}
 template <bool kLds>
 __device__ __forceinline__ uint32_t conn_bm(const ConnArgs& a, const ConnDesc& D, uint32_t s, uint32_t d,
                                             uint32_t port, uint32_t p, uint32_t& rule) {
     const uint8_t* g = static_cast<const uint8_t*>(a.rules);
-    const uint32_t B = D.bm_off;
-    uint32_t W, ns, nd, nr, np[4];
-    if constexpr (kLds) {
-        const v4u h0 = *lds128_t(B), h1 = *lds128_t(B + 16u);
-        W = h0.x; ns = h0.y; nd = h0.z; nr = h0.w;
-        np[0] = h1.x; np[1] = h1.y; np[2] = h1.z; np[3] = h1.w;
-    } else {
-        const uint4 h0 = *reinterpret_cast<const uint4*>(g + B), h1 = *reinterpret_cast<const uint4*>(g + B + 16u);
-        W = h0.x; ns = h0.y; nd = h0.z; nr = h0.w;
-        np[0] = h1.x; np[1] = h1.y; np[2] = h1.z; np[3] = h1.w;
+    const uint32_t W = D.bm_w, ns = D.bm_sd & 0xFFFFu, nd = D.bm_sd >> 16;
+    const uint32_t n0 = D.bm_tu & 0xFFFFu, n1 = D.bm_tu >> 16;
+    // the tables: src, dst, then the protocol tables (n2 = n3 = 1), then the rules
+    const uint32_t os = D.bm_off + kConnBmHeader, od = os + 4u * ns * (1u + W), t0 = od + 4u * nd * (1u + W);
+    const uint32_t t1 = t0 + 4u * n0 * (1u + W), t2 = t1 + 4u * n1 * (1u + W), t3 = t2 + 4u * (1u + W);
+    const uint32_t orl = t3 + 4u * (1u + W);
+    const uint32_t op = p == 0u ? t0 : p == 1u ? t1 : p == 2u ? t2 : t3;
+    const uint32_t np = p == 0u ? n0 : p == 1u ? n1 : 1u;
+    // the three branch-free lower bounds (last key <= x; key 0 first) in
+    // lock-step, their reads in flight together: a finished search re-reads
+    // its current key (h = 0), which still holds
+    uint32_t ps = 0, ls = ns, pd = 0, ld = nd, pp = 0, lp = np;
+    while ((ls | ld | lp) > 1u) {
+        const uint32_t hs = ls >> 1, hd = ld >> 1, hp = lp >> 1;
+        const uint32_t ks = bm_u32<kLds>(g, os + 4u * (ps + hs)), kd = bm_u32<kLds>(g, od + 4u * (pd + hd));
+        const uint32_t kp = bm_u32<kLds>(g, op + 4u * (pp + hp));
+        ps = ks <= s ? ps + hs : ps;
+        pd = kd <= d ? pd + hd : pd;
+        pp = kp <= port ? pp + hp : pp;
+        ls -= hs; ld -= hd; lp -= hp;
     }
-    uint32_t o = B + kConnBmHeader;
-    const uint32_t sr = bm_row<kLds>(g, o, ns, W, s);
-    o += 4u * ns * (1u + W);
-    const uint32_t dr = bm_row<kLds>(g, o, nd, W, d);
-    o += 4u * nd * (1u + W);
-    // the four protocol tables in turn, then the {meta, index} pairs
-    const uint32_t t1 = o + 4u * np[0] * (1u + W), t2 = t1 + 4u * np[1] * (1u + W);
-    const uint32_t t3 = t2 + 4u * np[2] * (1u + W);
-    const uint32_t op = p == 0u ? o : p == 1u ? t1 : p == 2u ? t2 : t3;
-    const uint32_t n = p == 0u ? np[0] : p == 1u ? np[1] : p == 2u ? np[2] : np[3];
-    o = t3 + 4u * np[3] * (1u + W);
-    const uint32_t pr = bm_row<kLds>(g, op, n, W, port);
+    const uint32_t sr = os + 4u * ns + 4u * W * ps, dr = od + 4u * nd + 4u * W * pd, pr = op + 4u * np + 4u * W * pp;
     for (uint32_t w = 0; w < W; ++w) {
         const uint32_t m = bm_u32<kLds>(g, sr + 4u * w) & bm_u32<kLds>(g, dr + 4u * w) & bm_u32<kLds>(g, pr + 4u * w);
         if (m) {
             const uint32_t i = 32u * w + uint32_t(__builtin_ctz(m));
-            rule = bm_u32<kLds>(g, o + 8u * i + 4u);
-            return (bm_u32<kLds>(g, o + 8u * i) >> (8u * p)) & 3u;
+            rule = bm_u32<kLds>(g, orl + 8u * i + 4u);
+            return (bm_u32<kLds>(g, orl + 8u * i) >> (8u * p)) & 3u;
         }
     }
-    (void)nr;
     rule = D.n_rules;
     return 0u;
 }
@@ -517,6 +504,11 @@ __device__ __forceinline__ uint32_t conn_bm(const ConnArgs& a, const ConnDesc& D
 // possible evaluations up front, before the state machine knows which it
 // makes, measured slower: 185 vs 165 us per 4 Mi connections, 256 vs 176
 // counting -- the loads for skipped evaluations are not free.)
+// diagnostics builds only: 1 no evaluation, 2 descriptor read only, 4 no
+// bitmap evaluation (each returns PERMIT or REFLECT from a live input)
+#ifndef CONN_ABLATE
+#define CONN_ABLATE 0
+#endif
 template <bool k16, bool kLdsRules, int kCount>
 __global__ __launch_bounds__(1024) void connect_kernel(ConnArgs a) {
     typedef typename ConnT<k16>::A A;
@@ -561,7 +553,11 @@ __global__ __launch_bounds__(1024) void connect_kernel(ConnArgs a) {
                 // one evalACL call: ACLAction; counting key of its terminating rule
                 auto eval = [&](int k) -> uint32_t {
                     if (di[k] < 0) return 1u;                   // nil ACL: PERMIT, not counted (:476-478)
+                    if constexpr (CONN_ABLATE & 1) return 1u + (sa == da ? 1u : 0u);
                     const ConnDesc D = conn_desc(a, uint32_t(di[k]));
+                    if constexpr (CONN_ABLATE & 2) return 1u + (D.n_rules == sp ? 1u : 0u);
+                    if constexpr (CONN_ABLATE & 4)
+                        if (D.bm_off != 0xFFFFFFFFu) return 1u + (D.n_rules == sp ? 1u : 0u);
                     uint32_t res, rule;
                     if (D.pre) {
                         const uint32_t w = D.pre[uint64_t(k >> 1) * a.n + i];

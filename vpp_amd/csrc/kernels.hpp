@@ -159,7 +159,9 @@ struct ConnDesc {                // one bound ACL for the connection kernel
     const uint32_t* pre;         // classifier slot words (res | slot << 2): [0, N) SYN, [N, 2N) SYN-ACK; or null
     const uint32_t* slot_rule;   // pre: slot -> rule index
     uint32_t bm_off;             // bitmap form (IPv4): byte offset of its tables in the pool; ~0u: none
-    uint32_t pad[3];
+    uint32_t bm_sd;              // bitmap form: source | destination interval counts << 16
+    uint32_t bm_tu;              // bitmap form: TCP | UDP port interval counts << 16
+    uint32_t bm_w;               // bitmap form: u32 words per row
 };
 struct IfAcls {                  // interface -> (inbound, outbound) ConnDesc index, -1 = nil
     int32_t in, out;
@@ -167,9 +169,10 @@ struct IfAcls {                  // interface -> (inbound, outbound) ConnDesc in
 static_assert(sizeof(ConnDesc) == 48 && sizeof(IfAcls) == 8, "connect_kernel reads the staged tables as 16-B / 8-B words");
 // The bitmap form of a linear IPv4 ACL in the connection pool (engine.cpp
 // conn_bitmap4), u32 words from a 16-B aligned base: header {W, ns, nd, nr,
-// n0, n1, n2, n3}, then the src table {ns keys, ns x W row words}, the dst
-// table, the four protocol tables (TCP, UDP by destination port; ICMP and
-// OTHER one row each), then nr {meta, index} pairs.  Keys are the starts of
+// n0, n1, n2, n3} (its counts also in the ACL's ConnDesc), then the src
+// table {ns keys, ns x W row words}, the dst table, the four protocol tables
+// (TCP, UDP by destination port; ICMP and OTHER one row each: n2 = n3 = 1),
+// then nr {meta, index} pairs.  Keys are the starts of
 // the elementary intervals (key 0 first); a row has bit i set when pool
 // rule i matches that interval's addresses (ports); the first match is the
 // lowest set bit of src row & dst row & protocol row.
