@@ -6,8 +6,8 @@ if0/if2 (out), 64 random local ACLs (1-300 rules) on 77 further interfaces,
 half of the connections entering through a global-table interface.  Times
 ``Engine.connect_batch`` over N connections with host arrays in and out
 (PCIe copies included; auto and linear modes) and with device-resident
-tensors (CLS_F_DEVICE, ``hbm_resident``), and the C oracle (one thread) on a sample.  Prints one
-JSON line.  --count 1 times CLS_F_COUNT batches (per-(ACL, rule) counters)
+tensors (CLS_F_DEVICE, ``hbm_resident``: the median wall time of --iters calls),
+and the C oracle (one thread) on a sample.  Prints one JSON line.  --count 1 times CLS_F_COUNT batches (per-(ACL, rule) counters)
 beside the plain ones; --locals sets the number of local ACLs (12: a rule
 pool that fits LDS).
 usage: python tools/conn_bench.py [--n 4194304] [--iters 5] [--locals 64]
@@ -30,7 +30,7 @@ from test_gpu_connect_scale import build, oracle_connections  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=1 << 22)
-    ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--iters", type=int, default=9)
     ap.add_argument("--cpu-sample", type=int, default=20000)
     ap.add_argument("--other-proto", type=int, default=1, help="6%% of packets with protocol > 2")
     ap.add_argument("--locals", type=int, default=64)
@@ -66,17 +66,20 @@ def main():
     torch.cuda.synchronize()
     dev_out = eng.connect_batch(*dargs)
     assert np.array_equal(dev_out.cpu().numpy(), out), "device batch differs"
-    t0 = time.perf_counter()
-    for _ in range(a.iters):
-        dev_out = eng.connect_batch(*dargs)
-    dev_dt = (time.perf_counter() - t0) / a.iters
+    def per_call(count):
+        """median wall time of a.iters device batches (each call returns after
+        its stream has finished)"""
+        ts = []
+        for _ in range(a.iters):
+            t0 = time.perf_counter()
+            eng.connect_batch(*dargs, count=count)
+            ts.append(time.perf_counter() - t0)
+        return float(np.median(ts))
+    dev_dt = per_call(False)
     counted = None
     if a.count:
         eng.connect_batch(*dargs, count=True)
-        t0 = time.perf_counter()
-        for _ in range(a.iters):
-            eng.connect_batch(*dargs, count=True)
-        dt_c = (time.perf_counter() - t0) / a.iters
+        dt_c = per_call(True)
         counted = {"value": round(n / dt_c / 1e6, 3), "unit": "Mconn/s", "ms_per_batch": round(dt_c * 1e3, 3)}
     k = a.cpu_sample
     t1 = time.perf_counter()
