@@ -209,7 +209,7 @@ def main():
     side = torch.cuda.Stream(device=dev) if coll else None
     reduced = [None] * nbuf                   # event after the last all-reduce of each buffer
     ev = []                                   # (before, after) the counter all-reduce, per timed step
-    sev = []                                  # (before, after) each timed step on the launch stream
+    sev = []                                  # one event at the start of each timed step (and one after the last)
     torch.cuda.synchronize()
 
     # Every step runs on one explicit stream (`main`): the engine launches on
@@ -220,15 +220,15 @@ def main():
     def step(i, timing):
         b = i % nbuf
         if timing:
-            s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            # step boundaries: one event per step (step i = boundary i to i + 1),
+            # each event record costs the stream a few microseconds
+            s0 = torch.cuda.Event(enable_timing=True)
             s0.record(main)
+            sev.append(s0)
         if reduced[b] is not None:
             main.wait_event(reduced[b])
         eng.classify(table, pk["src"], pk["dst"], pk["dport"], pk["proto"], verdict=verdict,
                      counters=counters[b], timing=timing, stream=main)
-        if timing:
-            s1.record(main)
-            sev.append((s0, s1))
         if coll:
             done = torch.cuda.Event()
             done.record(main)
@@ -273,6 +273,9 @@ def main():
     for _ in range(args.steps):
         step(i, True)
         i += 1
+    last = torch.cuda.Event(enable_timing=True)
+    last.record(main)
+    sev.append(last)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -280,7 +283,7 @@ def main():
     kms = eng.kernel_times(reset=True)
     avg_k = float(np.mean(kms)) if kms else float("nan")
     med_k = float(np.median(kms)) if kms else float("nan")
-    med_step = float(np.median([a.elapsed_time(b) for a, b in sev])) if sev else float("nan")
+    med_step = float(np.median([a.elapsed_time(b) for a, b in zip(sev, sev[1:])])) if len(sev) > 1 else float("nan")
     ar = [a.elapsed_time(b) for a, b in ev]
     ar_ms = float(np.mean(ar)) if ar else 0.0
     ar_med = float(np.median(ar)) if ar else 0.0
