@@ -2,6 +2,8 @@
 // stream-floor, linear, connection and traffic kernels and their launchers.
 // The classify kernels (kernels_dev.hpp) are instantiated by k4_lds.hip,
 // k4_glb.hip and k16.hip.
+#include <cstdlib>
+
 #include "kernels_dev.hpp"
 
 namespace cls {
@@ -791,12 +793,20 @@ hipError_t launch_finish16(const FinishArgs& f, const Cls4Dev& t, const Cls4Dev&
 
 hipError_t launch_stream(const Pkts4* p4, const Pkts16* p16, uint8_t* verdict, int grid, int variant,
                          hipStream_t s) {
+    // diagnostics: the stream with a dynamic LDS allocation like the classify launch's
+    static const size_t dl = std::getenv("CONTIVCLS_FLOOR_LDS") ? std::strtoul(std::getenv("CONTIVCLS_FLOOR_LDS"), nullptr, 0) : 0;
+    if (dl) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(stream4_kernel<true, true>), hipFuncAttributeMaxDynamicSharedMemorySize, int(dl));
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(stream4_kernel<false, true>), hipFuncAttributeMaxDynamicSharedMemorySize, int(dl));
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(stream4_kernel<true, false>), hipFuncAttributeMaxDynamicSharedMemorySize, int(dl));
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(stream4_kernel<false, false>), hipFuncAttributeMaxDynamicSharedMemorySize, int(dl));
+    }
     if (p4) {
         switch (variant) {
-        case 0: hipLaunchKernelGGL((stream4_kernel<true, true>), dim3(grid), dim3(kClsBlock), 0, s, *p4, verdict); break;
-        case 1: hipLaunchKernelGGL((stream4_kernel<false, true>), dim3(grid), dim3(kClsBlock), 0, s, *p4, verdict); break;
-        case 2: hipLaunchKernelGGL((stream4_kernel<true, false>), dim3(grid), dim3(kClsBlock), 0, s, *p4, verdict); break;
-        default: hipLaunchKernelGGL((stream4_kernel<false, false>), dim3(grid), dim3(kClsBlock), 0, s, *p4, verdict);
+        case 0: hipLaunchKernelGGL((stream4_kernel<true, true>), dim3(grid), dim3(kClsBlock), dl, s, *p4, verdict); break;
+        case 1: hipLaunchKernelGGL((stream4_kernel<false, true>), dim3(grid), dim3(kClsBlock), dl, s, *p4, verdict); break;
+        case 2: hipLaunchKernelGGL((stream4_kernel<true, false>), dim3(grid), dim3(kClsBlock), dl, s, *p4, verdict); break;
+        default: hipLaunchKernelGGL((stream4_kernel<false, false>), dim3(grid), dim3(kClsBlock), dl, s, *p4, verdict);
         }
     } else {
         hipLaunchKernelGGL(stream16_kernel, dim3(grid), dim3(kClsBlock), 0, s, *p16, verdict);

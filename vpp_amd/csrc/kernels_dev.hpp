@@ -36,7 +36,9 @@
 #include "kernels.hpp"
 
 // Diagnostics builds only (tools/build_ablate.sh): skip stages while keeping
-// their inputs live -- 1 slot counting, 2 sublist probes, 4 source lookup.
+// their inputs live -- 1 slot counting, 2 sublist probes, 4 source lookup,
+// 8 port lookup, 16 LDS image staging and counter flush, 32 the whole
+// per-packet evaluation (a mix of the fields, as the stream kernel).
 #ifndef CLS_ABLATE
 #define CLS_ABLATE 0
 #endif
@@ -696,6 +698,19 @@ __device__ __forceinline__ void run_n(const Img<kLds>& im, const Cls4Dev& t, con
 #ifndef CLS_PREFETCH
 #define CLS_PREFETCH 0
 #endif
+// The prefetching loops load the step after the current one, which may lie
+// past the last whole step: clamped to it (the data unused).  The default
+// loop never loads past it.
+#ifndef CLS_CLAMP
+#define CLS_CLAMP (CLS_PREFETCH != 0)
+#endif
+// 1 (default): a step's packet loads issued src, dst, dport, proto, as the
+// stream kernel does (the compiler otherwise issues proto first, for the
+// protocol test): config 3 0.551 against 0.558 ms in one-process A/B
+// (profiles/r03z_ab_load_order_config3.txt)
+#ifndef CLS_LOAD_ORDER
+#define CLS_LOAD_ORDER 1
+#endif
 constexpr int kG = CLS_GROUPS;     // 16-B packet groups per lane per step
 
 // The OTHER queue's fill counter of this workgroup: one LDS word after the
@@ -757,11 +772,11 @@ template <bool kLds, bool kVec, int kMode, int kList, int kD, int kCtr>
 __global__ __launch_bounds__(kClsBlock) void classify4_cls(Cls4Dev t, Cls4Dev o, Pkts4 p, uint8_t* verdict,
                                                            unsigned long long* gslot) {
     extern __shared__ uint4 smem[];
-    if (t.zero)   // the call's rule counters, added to by the finish launch
+    if (t.zero && !(CLS_ABLATE & 64))   // the call's rule counters, added to by the finish launch
         for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < t.n_zero; i += gridDim.x * blockDim.x)
             t.zero[i] = 0ull;
     Img<kLds> im{reinterpret_cast<const uint8_t*>(t.img)};
-    const uint32_t oq_lds = queue_begin<kLds>(t, smem);
+    const uint32_t oq_lds = (CLS_ABLATE & 64) ? 0u : queue_begin<kLds>(t, smem);
     if constexpr (kLds && !(CLS_ABLATE & 16)) stage_lds(t, smem);
 
     const uint32_t nthreads = gridDim.x * blockDim.x;
@@ -797,10 +812,22 @@ __global__ __launch_bounds__(kClsBlock) void classify4_cls(Cls4Dev t, Cls4Dev o,
             (void)ok;
 #pragma unroll
             for (int k = 0; k < kG; ++k) {
-                const uint32_t gi = min(g + uint32_t(k) * nthreads, nfull - 1u);
-                b.s[k] = ldnt(at(S, gi)); b.d[k] = ldnt(at(D, gi));
-                b.dp[k] = ldnt(at(DP, gi));
-                b.pr[k] = CLS_NT_PROTO ? ldnt(at(PR, gi)) : *at(PR, gi);
+                const uint32_t gi = CLS_CLAMP ? min(g + uint32_t(k) * nthreads, nfull - 1u) : g + uint32_t(k) * nthreads;
+                if constexpr (CLS_LOAD_ORDER) {
+                    // issue order src, dst, dport, proto (the stream kernel's)
+                    b.s[k] = ldnt(at(S, gi));
+                    __builtin_amdgcn_sched_barrier(0);
+                    b.d[k] = ldnt(at(D, gi));
+                    __builtin_amdgcn_sched_barrier(0);
+                    b.dp[k] = ldnt(at(DP, gi));
+                    __builtin_amdgcn_sched_barrier(0);
+                    b.pr[k] = CLS_NT_PROTO ? ldnt(at(PR, gi)) : *at(PR, gi);
+                    __builtin_amdgcn_sched_barrier(0);
+                } else {
+                    b.s[k] = ldnt(at(S, gi)); b.d[k] = ldnt(at(D, gi));
+                    b.dp[k] = ldnt(at(DP, gi));
+                    b.pr[k] = CLS_NT_PROTO ? ldnt(at(PR, gi)) : *at(PR, gi);
+                }
             }
         };
         // the step's lookups; its verdict words (4 packets each) into vw
@@ -857,8 +884,13 @@ __global__ __launch_bounds__(kClsBlock) void classify4_cls(Cls4Dev t, Cls4Dev o,
             uint32_t v[kN], ix[kN];
 #pragma unroll
             for (int k = 0; k < kN; ++k) ix[k] = 4u * (g + uint32_t(k / 4) * nthreads) + uint32_t(k % 4);
-            run_n<kN, kLds, kMode, kList, kD, kCtr>(im, t, o, hot_lane, gslot, hot0, sa, da, pa, ra, other, v, sa, ix,
-                                                    oq_lds);
+            if constexpr (CLS_ABLATE & 32) {                    // diagnostics: the stream kernel's mix, no run_n
+#pragma unroll
+                for (int k = 0; k < kN; ++k) v[k] = (sa[k] ^ da[k] ^ pa[k] ^ ra[k] ^ uint32_t(other)) & 3u;
+            } else {
+                run_n<kN, kLds, kMode, kList, kD, kCtr>(im, t, o, hot_lane, gslot, hot0, sa, da, pa, ra, other, v, sa,
+                                                        ix, oq_lds);
+            }
             if constexpr (kCtr == 2) {                           // slot mode: 4 result words per lane
 #pragma unroll
                 for (int k = 0; k < kG; ++k)
@@ -999,6 +1031,7 @@ __global__ __launch_bounds__(kClsBlock) void classify4_cls(Cls4Dev t, Cls4Dev o,
     if constexpr (!kLds) {
         if (hot0) atomicAdd(&gslot[0], (unsigned long long)hot0);
     }
+    if constexpr (CLS_ABLATE & 64) return;
     if constexpr (kLds) flush_lds<kCtr>(t, smem);
     queue_end(t, oq_lds);
 }
