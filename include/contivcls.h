@@ -382,6 +382,14 @@ typedef struct cls_image_v4_header {
 } cls_image_v4_header;
 int cls_compile_v4(const cls_rule* rules, uint32_t n_rules, void* blob, uint64_t cap,
                    uint64_t* need);
+/* Diagnostics (CPU verification): the bitmap form cls_connect_batch gives a
+ * linear IPv4 ACL (per-ACL interval tables of source, destination and each
+ * protocol's destination port, one rule bit row per interval), built from
+ * `rules` and evaluated on the host for n IPv4 packets: evalACL's ACLAction
+ * and the terminating rule (n_rules: default DENY) per packet. */
+int cls_conn_bitmap_eval(const cls_rule* rules, uint32_t n_rules, const uint32_t* src, const uint32_t* dst,
+                         const uint16_t* dport, const uint8_t* proto, uint64_t n, uint8_t* res_out,
+                         uint32_t* rule_out);
 
 /* The 16-byte layout's compiled form (what cls_classify runs for CLS_AF_V16
  * batches): both address families are mapped to 32-bit representatives by a

@@ -46,7 +46,7 @@ SYMBOLS = ["cls_abi_version", "cls_engine_create", "cls_engine_destroy", "cls_la
            "cls_last_kernel_ms", "cls_kernel_times", "cls_kernel_times_reset", "cls_acl_put", "cls_acl_del", "cls_acl_table", "cls_acl_counts",
            "cls_if_id",
            "cls_if_acls", "cls_connect_batch", "cls_gen_traffic_v4", "cls_compile_v4",
-           "cls_compile_v16", "cls_gen_traffic_v16", "cls_stream_floor", "cls_stream_floor_shapes", "cls_conn_counters",
+           "cls_compile_v16", "cls_gen_traffic_v16", "cls_stream_floor", "cls_stream_floor_shapes", "cls_conn_bitmap_eval", "cls_conn_counters",
            "cls_acl_stats"]
 
 
@@ -171,6 +171,7 @@ def bind(path: str):
         "cls_kernel_times": (C.c_int, [vp, C.POINTER(C.c_float), u32, C.POINTER(u32)]),
         "cls_kernel_times_reset": (C.c_int, [vp]),
         "cls_stream_floor": (C.c_int, [vp, C.POINTER(PktSoa), u64, vp, u32, C.POINTER(C.c_float), vp]),
+        "cls_conn_bitmap_eval": (C.c_int, [C.POINTER(ClsRule), u32, vp, vp, vp, vp, u64, vp, vp]),
         "cls_stream_floor_shapes": (C.c_int, [vp, C.POINTER(PktSoa), u64, vp, u32, C.POINTER(C.c_float), u32,
                                               C.POINTER(C.c_uint32), vp]),
         "cls_acl_put": (C.c_int, [vp, C.c_char_p, C.POINTER(ClsRule), u32,

@@ -1659,6 +1659,48 @@ int cls_compile_v4(const cls_rule* rules, uint32_t n, void* blob, uint64_t cap, 
                       has ? &oimg : nullptr);
 }
 
+// Diagnostics (CPU tests): the connection path's bitmap form of an ACL
+// (conn_bitmap4) evaluated on the host, exactly as conn_bm reads it.
+int cls_conn_bitmap_eval(const cls_rule* rules, uint32_t n_rules, const uint32_t* src, const uint32_t* dst,
+                         const uint16_t* dport, const uint8_t* proto, uint64_t n, uint8_t* res_out,
+                         uint32_t* rule_out) {
+    if ((n_rules && !rules) || (n && (!src || !dst || !dport || !proto || !res_out || !rule_out)))
+        return CLS_E_INVAL;
+    std::vector<SemRule> sem;
+    std::string why;
+    const int rc = semantic_rules(rules, n_rules, 4, sem, why);
+    if (rc != CLS_OK) return rc;
+    std::vector<uint32_t> w;
+    if (!conn_bitmap4(conn_rules4(sem), n_rules, size_t(1) << 26, w)) return CLS_E_NOMEM;
+    const uint32_t W = w[0], ns = w[1], nd = w[2], np[4] = {w[4], w[5], w[6], w[7]};
+    const uint32_t os = kConnBmHeader / 4, od = os + ns * (1 + W), t0 = od + nd * (1 + W);
+    const uint32_t t1 = t0 + np[0] * (1 + W), t2 = t1 + np[1] * (1 + W), t3 = t2 + np[2] * (1 + W);
+    const uint32_t orl = t3 + np[3] * (1 + W);
+    auto row = [&](uint32_t o, uint32_t cnt, uint32_t x) {       // last key <= x (key 0 first)
+        uint32_t pos = 0;
+        for (uint32_t i = 1; i < cnt; ++i)
+            if (w[o + i] <= x) pos = i;
+        return o + cnt + W * pos;
+    };
+    for (uint64_t k = 0; k < n; ++k) {
+        const uint32_t p = proto[k] <= 2 ? proto[k] : 3u;
+        const uint32_t tp[4] = {t0, t1, t2, t3};
+        const uint32_t sr = row(os, ns, src[k]), dr = row(od, nd, dst[k]), pr = row(tp[p], np[p], dport[k]);
+        res_out[k] = 0;
+        rule_out[k] = n_rules;
+        for (uint32_t j = 0; j < W; ++j) {
+            const uint32_t m = w[sr + j] & w[dr + j] & w[pr + j];
+            if (m) {
+                const uint32_t i = 32 * j + uint32_t(__builtin_ctz(m));
+                res_out[k] = uint8_t((w[orl + 2 * i] >> (8 * p)) & 3u);
+                rule_out[k] = w[orl + 2 * i + 1];
+                break;
+            }
+        }
+    }
+    return CLS_OK;
+}
+
 int cls_compile_v16(const cls_rule* rules, uint32_t n, void* blob, uint64_t cap, uint64_t* need) {
     if ((n && !rules) || !need) return CLS_E_INVAL;
     std::vector<SemRule> sem;
