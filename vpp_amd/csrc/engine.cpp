@@ -1243,7 +1243,7 @@ int cls_connect_batch(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t*
     };
     std::vector<IfAcls> ifs(std::max<size_t>(1, e->if_acl.size()));
     for (size_t i = 0; i < e->if_acl.size(); ++i)
-        ifs[i] = IfAcls{desc_of(e->if_acl[i].first), desc_of(e->if_acl[i].second)};
+        ifs[i] = IfAcls{desc_of(e->if_acl[i].first), desc_of(e->if_acl[i].second), -1, -1};
     const uint32_t n_ifs = uint32_t(e->if_acl.size());
     if (!dev)
         for (uint64_t i = 0; i < n; ++i)
@@ -1321,6 +1321,10 @@ int cls_connect_batch(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t*
             Table& t = *dtab[big[b]];
             uint32_t* pre = e->s_pre.as<uint32_t>() + b * 2 * n;
             desc[big[b]].pre = pre;
+            for (IfAcls& f : ifs) {                        // the block, also per interface (prefetch)
+                if (f.in == int32_t(big[b])) f.in_pre = int32_t(b);
+                if (f.out == int32_t(big[b])) f.out_pre = int32_t(b);
+            }
             LaunchCfg cfg;
             cfg.stream = s;
             if (!k16) {
@@ -1422,6 +1426,7 @@ int cls_connect_batch(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t*
     HIPC(e, hipMemcpyAsync(e->s_ifs.p, ifs.data(), ifs.size() * sizeof(IfAcls), hipMemcpyHostToDevice, s));
     if (!pool.empty()) HIPC(e, hipMemcpyAsync(e->s_rules.p, pool.data(), pool.size(), hipMemcpyHostToDevice, s));
     a.desc = e->s_desc.as<ConnDesc>();
+    a.pre = big.empty() ? nullptr : e->s_pre.as<uint32_t>();
     a.ifs = e->s_ifs.as<IfAcls>();
     a.rules = e->s_rules.p;
     std::vector<unsigned long long*> tctr;

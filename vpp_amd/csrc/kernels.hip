@@ -407,8 +407,8 @@ __device__ __forceinline__ bool mapped4(const uint4& a) { return (a.x | a.y) == 
 // loads in front of every evaluation.
 __device__ __forceinline__ IfAcls conn_if(const ConnArgs& a, uint32_t j) {
     if (a.meta_lds != 0xFFFFFFFFu) {
-        const v2u v = *lds64_t(a.meta_lds + a.n_desc * uint32_t(sizeof(ConnDesc)) + 8u * j);
-        return IfAcls{int32_t(v.x), int32_t(v.y)};
+        const v4u v = *lds128_t(a.meta_lds + a.n_desc * uint32_t(sizeof(ConnDesc)) + 16u * j);
+        return IfAcls{int32_t(v.x), int32_t(v.y), int32_t(v.z), int32_t(v.w)};
     }
     return a.ifs[j];
 }
@@ -528,7 +528,7 @@ __global__ __launch_bounds__(1024) void connect_kernel(ConnArgs a) {
         const uint32_t* gd = reinterpret_cast<const uint32_t*>(a.desc);
         const uint32_t* gi = reinterpret_cast<const uint32_t*>(a.ifs);
         for (uint32_t j = threadIdx.x; j < nd; j += blockDim.x) *lctr_t(a.meta_lds + 4u * j) = gd[j];
-        for (uint32_t j = threadIdx.x; j < 2u * a.n_ifs; j += blockDim.x) *lctr_t(a.meta_lds + 4u * (nd + j)) = gi[j];
+        for (uint32_t j = threadIdx.x; j < 4u * a.n_ifs; j += blockDim.x) *lctr_t(a.meta_lds + 4u * (nd + j)) = gi[j];
     }
     __syncthreads();
     const A* src = static_cast<const A*>(a.src);
@@ -552,6 +552,18 @@ __global__ __launch_bounds__(1024) void connect_kernel(ConnArgs a) {
                 // source's inbound and the destination's outbound ACL, SYN-ACK
                 // through the destination's inbound and the source's outbound
                 const int32_t di[4] = {S.in, Dif.out, Dif.in, S.out};
+                // the classifier slot words of every call on a large ACL, loaded
+                // now, together: a call testConnection then makes does not wait
+                // for its own global round trip (a call without them reads a
+                // valid dummy word)
+                const int32_t bi[4] = {S.in_pre, Dif.out_pre, Dif.in_pre, S.out_pre};
+                uint32_t pw[4] = {0u, 0u, 0u, 0u};
+                if (a.pre) {                                   // uniform: some ACL is on the classifier
+#pragma unroll
+                    for (int k = 0; k < 4; ++k)
+                        pw[k] = *(bi[k] >= 0 ? a.pre + (2ull * uint32_t(bi[k]) + uint32_t(k >> 1)) * a.n + i
+                                             : a.src_if + i);
+                }
                 // one evalACL call: ACLAction; counting key of its terminating rule
                 auto eval = [&](int k) -> uint32_t {
                     if (di[k] < 0) return 1u;                   // nil ACL: PERMIT, not counted (:476-478)
@@ -562,7 +574,7 @@ __global__ __launch_bounds__(1024) void connect_kernel(ConnArgs a) {
                         if (D.bm_off != 0xFFFFFFFFu) return 1u + (D.n_rules == sp ? 1u : 0u);
                     uint32_t res, rule;
                     if (D.pre) {
-                        const uint32_t w = D.pre[uint64_t(k >> 1) * a.n + i];
+                        const uint32_t w = pw[k];
                         res = w & 3u;
                         rule = kCount != 0 ? D.slot_rule[w >> 2] : 0u;
                     } else if (!k16 && D.bm_off != 0xFFFFFFFFu) {

@@ -165,8 +165,9 @@ struct ConnDesc {                // one bound ACL for the connection kernel
 };
 struct IfAcls {                  // interface -> (inbound, outbound) ConnDesc index, -1 = nil
     int32_t in, out;
+    int32_t in_pre, out_pre;     // their classifier slot words' block in ConnArgs::pre (-1: none)
 };
-static_assert(sizeof(ConnDesc) == 48 && sizeof(IfAcls) == 8, "connect_kernel reads the staged tables as 16-B / 8-B words");
+static_assert(sizeof(ConnDesc) == 48 && sizeof(IfAcls) == 16, "connect_kernel reads the staged tables as 16-B words");
 // The bitmap form of a linear IPv4 ACL in the connection pool (engine.cpp
 // conn_bitmap4), u32 words from a 16-B aligned base: header {W, ns, nd, nr,
 // n0, n1, n2, n3} (its counts also in the ACL's ConnDesc), then the src
@@ -197,6 +198,8 @@ struct ConnArgs {
     uint8_t* out;
     uint32_t n_desc;             // descriptors in desc
     uint32_t meta_lds;           // LDS byte offset of the staged desc + ifs tables; ~0u: global reads
+    const uint32_t* pre;         // classifier slot words of the large ACLs: block b at pre + 2 n b
+                                 // (SYN tuple, then SYN-ACK); null when there are none
 };
 // k16: 16-byte addresses; lds_rules: stage the pool; count: 0 none, 1 LDS
 // counters, 2 global (wave-aggregated) counters; grid: persistent workgroups;
