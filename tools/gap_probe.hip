@@ -33,6 +33,34 @@ struct Big {                        // a kernel argument the size of two Cls4Dev
     uint32_t w[256];
 };
 
+// extra adds per step on R live registers (pacing), R * K adds
+template <int R, int K>
+__global__ __launch_bounds__(1024) void kp(const uint4* S, const uint4* D, const uint2* DP, const uint32_t* PR,
+                                           uint32_t* V, uint32_t nsteps, unsigned long long*, uint32_t, Big) {
+    const uint32_t nthreads = gridDim.x * blockDim.x;
+    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t r[R];
+#pragma unroll
+    for (int i = 0; i < R; ++i) r[i] = tid * uint32_t(i + 1);
+    for (uint32_t g = tid; g < nsteps; g += nthreads) {
+        const uint4 s = ldnt(S + g);
+        const uint4 d = ldnt(D + g);
+        const uint2 dp = ldnt(DP + g);
+        const uint32_t pr = PR[g];
+        const uint32_t v = (s.x ^ s.y ^ s.z ^ s.w ^ d.x ^ d.y ^ d.z ^ d.w ^ dp.x ^ dp.y ^ pr) & 0x03030303u;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+#pragma unroll
+            for (int i = 0; i < R; ++i) r[i] = r[i] * 3u + v;
+        }
+        __builtin_nontemporal_store(v, V + g);
+    }
+    uint32_t x = 0;
+#pragma unroll
+    for (int i = 0; i < R; ++i) x ^= r[i];
+    if (x == 0x9E3779B9u) V[0] = x;
+}
+
 template <bool kBigArg, bool kRegs, bool kPack, bool kZero>
 __global__ __launch_bounds__(1024) void k(const uint4* S, const uint4* D, const uint2* DP, const uint32_t* PR,
                                           uint32_t* V, uint32_t nsteps, unsigned long long* zero, uint32_t nzero,
@@ -135,6 +163,15 @@ int main() {
     if (run(k<false, false, true, false>, "4 + verdict packing", 0)) return 1;
     if (run(k<false, false, false, true>, "5 + counter clearing, barrier", 0)) return 1;
     if (run(k<true, true, true, true>, "6 all of 1-5", L)) return 1;
+    if (run(k<false, false, false, false>, "0 stream", 0)) return 1;
+    // pacing: R registers x K rounds of mad per step
+    if (run(kp<8, 1>, "p 8 regs x 1", 0)) return 1;
+    if (run(kp<8, 4>, "p 8 regs x 4", 0)) return 1;
+    if (run(kp<8, 12>, "p 8 regs x 12", 0)) return 1;
+    if (run(kp<48, 1>, "p 48 regs x 1", 0)) return 1;
+    if (run(kp<48, 2>, "p 48 regs x 2", 0)) return 1;
+    if (run(kp<48, 4>, "p 48 regs x 4", 0)) return 1;
+    if (run(kp<96, 1>, "p 96 regs x 1", 0)) return 1;
     if (run(k<false, false, false, false>, "0 stream", 0)) return 1;
     return 0;
 }
