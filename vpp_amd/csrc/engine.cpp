@@ -123,6 +123,12 @@ struct Table {
     bool conn_bm_built = false;
     DevBuf d_slot_rule;
     DevBuf d_conn_ctr;
+    // recorded on the engine stream behind a rebind's counter clearing; a
+    // counting connection batch on another stream waits for it
+    hipEvent_t conn_ctr_ev = nullptr;
+    ~Table() {
+        if (conn_ctr_ev) (void)hipEventDestroy(conn_ctr_ev);
+    }
     // declared last: destroyed first, so pending device work is waited for
     // before any of the buffers above are freed
     Counters c4, c16;
@@ -1025,13 +1031,18 @@ int cls_acl_put(cls_engine* e, const char* acl_name, const cls_rule* rules, uint
         // acl_renderer.go:186-190): keep the compiled table, move the bindings.
         // A put installs a new ACL (PutACL replaces the message,
         // aclengine_mock.go:707-713), so its connection counters start from
-        // zero either way: clear the kept table's once its pending work is done.
+        // zero either way.  Every connection batch has finished its work on
+        // them (cls_connect_batch synchronises its stream before it returns,
+        // under this mutex), so the clearing is queued on the engine stream
+        // without waiting; a later counting batch on another stream waits for
+        // the event recorded behind it.
         tid = old->second.table_id;
         Table& kt = *same->second;
         if (kt.d_conn_ctr.p) {
             (void)hipSetDevice(e->device);
-            HIPC(e, hipDeviceSynchronize());
-            HIPC(e, hipMemset(kt.d_conn_ctr.p, 0, size_t(kt.n_rules + 1) * 8));
+            HIPC(e, hipMemsetAsync(kt.d_conn_ctr.p, 0, size_t(kt.n_rules + 1) * 8, e->stream));
+            if (!kt.conn_ctr_ev) HIPC(e, hipEventCreateWithFlags(&kt.conn_ctr_ev, hipEventDisableTiming));
+            HIPC(e, hipEventRecord(kt.conn_ctr_ev, e->stream));
         }
         for (auto& b : e->if_acl) {
             if (b.first == int32_t(tid)) b.first = -1;
@@ -1129,7 +1140,10 @@ static bool conn_bitmap4(const std::vector<ConnRule4>& r, uint32_t n_rules, size
     struct Tab {
         std::vector<uint32_t> keys, rows;
     };
-    auto addr_tab = [&](bool dst) {
+    // the interval starts of the six tables first (sorting 2R values each):
+    // the size check needs only their counts, so a table over the cap never
+    // builds its keys x R predicate rows
+    auto addr_keys = [&](bool dst) {
         std::vector<uint64_t> b{0};
         for (const ConnRule4& x : r) {
             const uint32_t a = dst ? x.dst_addr : x.src_addr, m = dst ? x.dst_mask : x.src_mask;
@@ -1140,20 +1154,9 @@ static bool conn_bitmap4(const std::vector<ConnRule4>& r, uint32_t n_rules, size
         std::sort(b.begin(), b.end());
         b.erase(std::unique(b.begin(), b.end()), b.end());
         while (!b.empty() && b.back() > 0xFFFFFFFFull) b.pop_back();
-        Tab t;
-        for (uint64_t k : b) {
-            const uint32_t x = uint32_t(k);
-            t.keys.push_back(x);
-            const size_t at = t.rows.size();
-            t.rows.resize(at + W, 0u);
-            for (uint32_t i = 0; i < R; ++i) {
-                const uint32_t a = dst ? r[i].dst_addr : r[i].src_addr, m = dst ? r[i].dst_mask : r[i].src_mask;
-                if (((x ^ a) & m) == 0) t.rows[at + i / 32] |= 1u << (i % 32);
-            }
-        }
-        return t;
+        return std::vector<uint32_t>(b.begin(), b.end());
     };
-    auto proto_tab = [&](uint32_t p) {
+    auto port_keys = [&](uint32_t p) {
         std::vector<uint32_t> b{0};
         if (p < 2)
             for (const ConnRule4& x : r) {
@@ -1164,26 +1167,39 @@ static bool conn_bitmap4(const std::vector<ConnRule4>& r, uint32_t n_rules, size
             }
         std::sort(b.begin(), b.end());
         b.erase(std::unique(b.begin(), b.end()), b.end());
-        Tab t;
-        for (uint32_t x : b) {
-            t.keys.push_back(x);
-            const size_t at = t.rows.size();
-            t.rows.resize(at + W, 0u);
-            for (uint32_t i = 0; i < R; ++i) {
-                const uint32_t pw = p == 0 ? r[i].port[0] : p == 1 ? r[i].port[1] : 0xFFFF0000u;
-                if (((r[i].meta >> (8 * p)) & 0x80u) && port_in(x, pw)) t.rows[at + i / 32] |= 1u << (i % 32);
-            }
-        }
-        return t;
+        return b;
     };
-    // size first (the rows are R x intervals bits); interval counts fit the
+    // size (the rows are R x intervals bits); interval counts fit the
     // descriptor's 16-bit fields
     size_t words = kConnBmHeader / 4 + 2 * size_t(R);
-    std::vector<Tab> tabs;
+    if (words > cap_words) return false;
+    std::vector<Tab> tabs(6);
     for (int k = 0; k < 6; ++k) {
-        tabs.push_back(k < 2 ? addr_tab(k == 1) : proto_tab(uint32_t(k - 2)));
-        words += tabs.back().keys.size() + tabs.back().rows.size();
-        if (words > cap_words || tabs.back().keys.size() > 0xFFFFu) return false;
+        tabs[k].keys = k < 2 ? addr_keys(k == 1) : port_keys(uint32_t(k - 2));
+        words += tabs[k].keys.size() * (1 + size_t(W));
+        if (words > cap_words || tabs[k].keys.size() > 0xFFFFu) return false;
+    }
+    // then the rows: bit i of an interval's row set when rule i's term holds
+    // at the interval's first value
+    for (int k = 0; k < 6; ++k) {
+        Tab& t = tabs[k];
+        t.rows.assign(t.keys.size() * W, 0u);
+        for (size_t j = 0; j < t.keys.size(); ++j) {
+            const uint32_t x = t.keys[j];
+            uint32_t* row = t.rows.data() + j * W;
+            for (uint32_t i = 0; i < R; ++i) {
+                bool hit;
+                if (k < 2) {
+                    const uint32_t a = k ? r[i].dst_addr : r[i].src_addr, m = k ? r[i].dst_mask : r[i].src_mask;
+                    hit = ((x ^ a) & m) == 0;
+                } else {
+                    const uint32_t p = uint32_t(k - 2);
+                    const uint32_t pw = p == 0 ? r[i].port[0] : p == 1 ? r[i].port[1] : 0xFFFF0000u;
+                    hit = ((r[i].meta >> (8 * p)) & 0x80u) && port_in(x, pw);
+                }
+                if (hit) row[i / 32] |= 1u << (i % 32);
+            }
+        }
     }
     const size_t at = out.size();
     out.insert(out.end(), {W, uint32_t(tabs[0].keys.size()), uint32_t(tabs[1].keys.size()), R,
@@ -1376,7 +1392,11 @@ int cls_connect_batch(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t*
     // longest lane's scan (CONTIVCLS_CONN_BITMAP=0: scans only).
     const char* bme = std::getenv("CONTIVCLS_CONN_BITMAP");
     if (!k16 && n && !(flags & CLS_F_FORCE_LINEAR) && !(bme && std::atoi(bme) == 0)) {
-        const size_t cap = lds_max0 - (count ? size_t(n_ctr) * 4 : 0) - std::min<size_t>(lds_max0 / 8, 8192);
+        // the LDS counters take their share only when they can be LDS counters
+        // at all (otherwise they are global, cmode 2); no subtraction wraps
+        const size_t ctr_b = count ? size_t(n_ctr) * 4 : 0, reserve = std::min<size_t>(lds_max0 / 8, 8192);
+        const size_t ctr_lds = ctr_b + reserve <= lds_max0 ? ctr_b : 0;
+        const size_t cap = lds_max0 - reserve - ctr_lds;
         std::vector<size_t> order;
         for (size_t j = 0; j < desc.size(); ++j)
             if (!desc[j].pre && desc[j].n >= kConnBmMinRules) order.push_back(j);
@@ -1440,6 +1460,7 @@ int cls_connect_batch(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t*
                 HIPC(e, t.d_conn_ctr.ensure(size_t(t.n_rules + 1) * 8));
                 HIPC(e, hipMemsetAsync(t.d_conn_ctr.p, 0, size_t(t.n_rules + 1) * 8, s));
             }
+            if (t.conn_ctr_ev && s != e->stream) HIPC(e, hipStreamWaitEvent(s, t.conn_ctr_ev, 0));
             tctr.push_back(t.d_conn_ctr.as<unsigned long long>());
         }
         HIPC(e, e->s_tctr.ensure(tctr.size() * sizeof(void*)));
