@@ -36,7 +36,7 @@ extern "C" {
  *    nested OTHER image); blob version 3; cls_table_info's n_lctr, ctr16,
  *    list_mode and swap; CLS_F_COUNT; CLS_AF_V16 connections;
  *    cls_acl_stats.  A v1 consumer that ignores `swap` would misread blobs. */
-#define CLS_ABI_VERSION 2
+#define CLS_ABI_VERSION 3
 
 /* ---- status codes ------------------------------------------------------ */
 enum {
@@ -330,14 +330,13 @@ int cls_gen_traffic_v16(cls_engine* e, const cls_traffic_spec16* spec, uint64_t 
  */
 typedef struct cls_image_v4_header {
     uint32_t magic;            /* 0x434C5334 "CLS4" */
-    uint32_t version;          /* 3 (CLS_ABI_VERSION 2) */
+    uint32_t version;          /* 4 (CLS_ABI_VERSION 3) */
     uint32_t n_rules, n_lin, has_cls;
     uint32_t img_bytes, off_bounds, off_iclass, off_cells, off_lists, off_tmpl;
     uint32_t n_bounds, search_top, n_classes, n_tmpl, n_list_entries, n_ctr, lds_bytes;
     uint32_t off_image, off_ctr_rule, off_lin;   /* byte offsets inside the blob */
     uint32_t total_bytes;
-    uint32_t mode;             /* source lookup: 0 interval search, 1 hash LPM, 4 trie,
-                                  6 hash LPM with the cells inline in the entries */
+    uint32_t mode;             /* source lookup: 0 interval search, 1 hash LPM, 4 trie */
     uint32_t default_class;    /* hash LPM: class when no hashed prefix matches */
     uint32_t n_hash;           /* hashed prefix lengths (ascending) */
     uint32_t hash_mask[3], hash_shift[3], hash_cap[3], off_hash[3];
@@ -373,15 +372,15 @@ typedef struct cls_image_v4_header {
                                   cells, uint2 {pointer table byte address, counter base} per
                                   (class, protocol); n_gcells u32 words */
     uint32_t n_gcells;
-    uint32_t sub4;             /* list modes 3-6: sublists as 4-ary node trees of bv_steps_d levels
-                                  (16-B nodes {k1, k2, k3, first child | leaf outcomes}; the
-                                  pointer tables hold root node byte addresses, or the outcome
-                                  when there are 0 levels); else the binary slot form */
-    uint32_t dflt_cell[3];     /* mode 6 (hash LPM of one length, 16-B entries {key, cell TCP,
-                                  cell UDP, cell ICMP}): the cells of addresses no entry holds */
 } cls_image_v4_header;
 int cls_compile_v4(const cls_rule* rules, uint32_t n_rules, void* blob, uint64_t cap,
                    uint64_t* need);
+/* Whether the library has a classify kernel for an image of source lookup
+ * `mode` and `list_mode` (cls_image_v4_header), LDS-resident or in global
+ * memory; rep16: the 16-byte core.  CLS_OK, or CLS_E_INVAL for a combination
+ * no kernel implements -- cls_table_put / cls_acl_put refuse such an image
+ * with CLS_E_INVAL instead of launching another variant's kernel on it. */
+int cls_image_kernel(uint32_t mode, uint32_t list_mode, int lds_resident, int rep16);
 /* Diagnostics (CPU verification): the bitmap form cls_connect_batch gives a
  * linear IPv4 ACL (per-ACL interval tables of source, destination and each
  * protocol's destination port, one rule bit row per interval), built from

@@ -58,8 +58,7 @@ class Image:
             self.hash = []
             for i in range(h.n_hash):
                 cap = h.hash_cap[i]
-                ew = 4 if h.mode == 6 else 2            # mode 6: entries {key, 3 inline cells}
-                tab = np.frombuffer(img, np.uint32, count=2 * ew * cap, offset=h.off_hash[i]).reshape(-1, ew)
+                tab = np.frombuffer(img, np.uint32, count=4 * cap, offset=h.off_hash[i]).reshape(-1, 2)
                 self.hash.append((h.hash_mask[i], h.hash_shift[i], cap, tab, h.hash_mul[i]))
         # list modes 5, 6: wide cells (uint2 {pointer table address, counter base}) in global memory
         self.gcells = (np.frombuffer(blob, np.uint32, count=h.n_gcells, offset=h.off_gcells).reshape(-1, 2)
@@ -75,20 +74,6 @@ class Image:
     def _h1(k, mul, shift):
         L = 32 - shift
         return (((k.astype(np.uint64) * mul) & 0xFFFFFFFF) >> np.uint64(32 - 2 * L)) & ((1 << L) - 1)
-
-    def inline_cells(self, src, proto):
-        """Mode 6: the packet's cell straight from the hash entries (the
-        default class's cells on a miss)."""
-        h = self.h
-        mask, shift, cap, tab, mul = self.hash[0]
-        key = src & np.uint32(mask)
-        e0 = tab[self._h0(key, mul, shift).astype(np.int64)]
-        e1 = tab[cap + self._h1(key, mul, shift).astype(np.int64)]
-        pr = np.minimum(proto, 2).astype(np.int64)
-        idx = np.arange(len(src))
-        dflt = np.array(list(h.dflt_cell), np.int64)[pr]
-        return np.where(e0[:, 0] == key, e0[idx, 1 + pr].astype(np.int64),
-                        np.where(e1[:, 0] == key, e1[idx, 1 + pr].astype(np.int64), dflt))
 
     def source_class(self, src):
         h = self.h
@@ -196,7 +181,7 @@ class Image:
         e = img[(((dp * self.h.port_mul) >> 32) & self.h.port_mask4) // 4]
         return np.where((e & 0xFFFF) == dp, e >> 16, self.h.port_dflt)
 
-    def _classify_bv3(self, cls, src, dst, dport, proto, counters, cells=None):
+    def _classify_bv3(self, cls, src, dst, dport, proto, counters):
         """List mode 3 (port-filtered sublists): cell u32 {pointer table word
         offset | counter base << 14}; table[port class] = initial state
         {outcome | entry slot << 16} (state >> 13 = entry byte address);
@@ -211,18 +196,11 @@ class Image:
             st = img[(wc[:, 0] + pc4) // 4]
             base = wc[:, 1]
         else:
-            cell = cells if cells is not None else img[(self.h.off_cells + cls * self.h.row_bytes + pr * 4) // 4]
+            cell = img[(self.h.off_cells + cls * self.h.row_bytes + pr * 4) // 4]
             st = img[((cell & 0x3FFF) * 4 + pc4) // 4]
             base = cell >> 14
         d = dst.astype(np.int64)
-        if self.h.sub4:
-            # 4-ary node trees: interior {k1, k2, k3, first child}, leaf {k1, k2, k3, outcomes}
-            L = int(self.h.bv_steps_d)
-            for lvl in range(L):
-                a = st // 4
-                c = (img[a] < d).astype(np.int64) + (img[a + 1] < d) + (img[a + 2] < d)
-                st = img[a + 3] + 16 * c if lvl + 1 < L else (img[a + 3] >> (8 * c)) & 0xFF
-        for i in range(int(self.h.bv_steps_d) - 1 if not self.h.sub4 else -1, -1, -1):
+        for i in range(int(self.h.bv_steps_d) - 1, -1, -1):
             a = ((st >> 13) + (8 << i)) // 4
             st = np.where(img[a] < d, img[a + 1], st)
         res = (st & 3).astype(np.uint32)
@@ -275,8 +253,6 @@ class Image:
             res, rule = self.linear(src, dst, dport, proto)
             np.add.at(counters, rule, 1)
             return res.astype(np.uint8), counters
-        if self.h.mode == 6:
-            return self._classify_bv3(None, src, dst, dport, proto, counters, cells=self.inline_cells(src, proto))
         if cls is None:
             cls = self.source_class(src)
         if self.h.list_mode >= 3:

@@ -14,16 +14,11 @@ from cls_image import Image, compile_blob
 from vpp_amd import _abi
 
 
-@pytest.fixture(autouse=True, params=["binary", "sub4_inline"])
-def _source_keyed(monkeypatch, request):
+@pytest.fixture(autouse=True)
+def _source_keyed(monkeypatch):
     """These tests pin list modes of the source-keyed layout; the compiler's
-    choice of orientation (compile.cpp build_cls4) is tested on its own.
-    Every test runs on both sublist forms: binary sublists and row entries
-    (the default), 4-ary node sublists and inline hash cells."""
+    choice of orientation (compile.cpp build_cls4) is tested on its own."""
     monkeypatch.setenv("CONTIVCLS_ORIENT", "src")
-    on = "1" if request.param == "sub4_inline" else "0"
-    monkeypatch.setenv("CONTIVCLS_SUB4", on)
-    monkeypatch.setenv("CONTIVCLS_INLINE", on)
 
 
 def _check(rules, traffic):
@@ -160,3 +155,32 @@ def test_single_port_tables_hash_port_classes(monkeypatch, seed, max_mode):
     img = _check(rules, tr)
     assert img.h.list_mode == max_mode
     assert img.h.n_pclass <= 10
+
+
+def test_image_without_kernel_is_refused():
+    """cls_image_kernel (the check cls_table_put runs before any launch, and
+    the launchers again): combinations no classify kernel implements are
+    CLS_E_INVAL -- the removed inline-cell source mode 6, the source trie or
+    wide cells outside LDS, front-end rows (mode 3) on the IPv4 path, list
+    modes past 6 -- and the implemented ones are CLS_OK."""
+    L = _abi.lib()
+    INVAL = -1
+    for mode, lm, lds, rep16 in [(6, 3, 1, 0), (6, 4, 1, 1), (4, 3, 0, 0), (4, 2, 1, 0), (1, 5, 0, 0),
+                                 (0, 6, 0, 1), (3, 4, 1, 0), (0, 7, 1, 0), (2, 0, 1, 0)]:
+        assert L.cls_image_kernel(mode, lm, lds, rep16) == INVAL, (mode, lm, lds, rep16)
+    for mode, lm, lds, rep16 in [(0, 0, 0, 0), (1, 4, 1, 0), (1, 2, 0, 0), (4, 3, 1, 0), (4, 6, 1, 1),
+                                 (3, 5, 1, 1), (3, 0, 0, 1), (0, 5, 1, 0)]:
+        assert L.cls_image_kernel(mode, lm, lds, rep16) == 0, (mode, lm, lds, rep16)
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_compiled_images_have_kernels(seed):
+    """Every image the compiler emits for random ACLs has a kernel at its
+    own residency (lds_bytes within the workgroup's LDS)."""
+    from aclgen import many_ports_acl, single_port_acl
+    for rules, _ in [random_acl(seed, 200, 0.1), single_port_acl(seed, 90), many_ports_acl(seed, 300, 30)]:
+        h = Image(compile_blob(_abi.CRules(rules))).h
+        if not h.has_cls:
+            continue
+        lds = h.lds_bytes + 16 <= 160 * 1024
+        assert _abi.lib().cls_image_kernel(h.mode, h.list_mode, int(lds), 0) == 0, (h.mode, h.list_mode)

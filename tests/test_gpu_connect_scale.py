@@ -197,20 +197,6 @@ def test_connections16_mixed_families_match_oracle(mode):
 
 
 @pytest.mark.parametrize("fam", [4, 16])
-def test_connections_inline_cells_sub4(fam, monkeypatch):
-    """Slot-mode classify launches over images with inline hash cells and
-    4-ary sublists (CONTIVCLS_INLINE=1, CONTIVCLS_SUB4=1), counters included."""
-    from vpp_amd.engine import Engine
-    monkeypatch.setenv("CONTIVCLS_INLINE", "1")
-    monkeypatch.setenv("CONTIVCLS_SUB4", "1")
-    eng = Engine()
-    try:
-        _run(eng, 3, "classifier", fam, count=True, n=12000)
-    finally:
-        eng.close()
-
-
-@pytest.mark.parametrize("fam", [4, 16])
 @pytest.mark.parametrize("no_lds", [0, 1, 2, 3, 7])
 def test_connection_counters_match_oracle(fam, no_lds, monkeypatch):
     """Per-(ACL, rule) counters with the rule pool in LDS (few locals: the

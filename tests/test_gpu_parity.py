@@ -80,8 +80,8 @@ def test_random_acls_both_kernels(eng, seed, n_rules, weird):
 VARIANTS = {  # kind -> (source lookup mode, list mode)
     "hash_sph": (1, 4), "search_sph": (0, 4),       # hash_*: several hashed prefix lengths
     "hash_cbv": (1, 3), "search_cbv": (0, 3),
-    "inl_sph": (6, 4), "inl_cbv": (6, 3),           # /32 sources: one length, cells inline (mode 6)
-    "hrow_sph": (1, 4), "hrow_cbv": (1, 3),         # the same with CONTIVCLS_INLINE=0: entries hold rows
+    "host_sph": (1, 4), "host_cbv": (1, 3),         # /32 sources only: one hashed length (src kernel mode 2)
+    "hrow_sph": (1, 4), "hrow_cbv": (1, 3),
     "hash_pc": (1, 2), "search_pc": (0, 2), "hash_bv": (1, 1), "search_bv": (0, 1),
     "hash_scan": (1, 0), "search_scan": (0, 0),
     "trie_sph": (4, 4), "trie_cbv": (4, 3)}
@@ -89,8 +89,8 @@ VARIANTS = {  # kind -> (source lookup mode, list mode)
 
 def _host_sources(rules, pool, seed):
     """Every source prefix of the rules (and the traffic pool) as a /32 host
-    inside it: one hashed prefix length, so the compiler can put the cells
-    inline in the hash entries (src mode 6)."""
+    inside it: one hashed prefix length (the rendered global table's shape,
+    the one-length hash kernels)."""
     import random
     from aclgen import _v4
     rng = random.Random(seed)
@@ -108,8 +108,8 @@ def _host_sources(rules, pool, seed):
 
 def variant_acl(kind, seed):
     from aclgen import long_list_acl, many_ports_acl, single_port_acl
-    if kind.startswith("inl"):
-        rules, pool = variant_acl("hrow" + kind[3:], seed)
+    if kind.startswith("host"):
+        rules, pool = variant_acl("hrow" + kind[4:], seed)
         return _host_sources(rules, pool, seed)
     hashed = kind.startswith(("hash", "hrow"))       # trie_*: the search_* tables over the source trie
     if kind.endswith("_sph"):
@@ -131,10 +131,8 @@ def test_all_kernel_variants(eng, seed, kind, monkeypatch):
     template scan; the source trie x both sublist forms) against the oracle."""
     if kind.endswith("_pc"):
         monkeypatch.setenv("CONTIVCLS_LIST_MODE_MAX", "2")
-    # the interval search and the source trie each on the same tables; hash
-    # entries with inline cells and with rows
+    # the interval search and the source trie each on the same tables
     monkeypatch.setenv("CONTIVCLS_TRIE", "1" if kind.startswith("trie") else "0")
-    monkeypatch.setenv("CONTIVCLS_INLINE", "0" if kind.startswith("hrow") else "1")
     monkeypatch.setenv("CONTIVCLS_SRC_SEARCH", "1" if kind.startswith(("search", "trie")) else "0")
     from cls_image import Image, compile_blob
     from vpp_amd import _abi
@@ -142,24 +140,6 @@ def test_all_kernel_variants(eng, seed, kind, monkeypatch):
     h = Image(compile_blob(_abi.CRules(rules))).h
     assert (h.mode, h.list_mode) == VARIANTS[kind], kind
     tr = random_traffic(seed + 11, 30000, pool)
-    _assert_same(_gpu(eng, rules, tr), _oracle(rules, tr))
-
-
-@pytest.mark.parametrize("seed", range(2))
-@pytest.mark.parametrize("kind", ["hash_sph", "inl_sph", "search_cbv", "trie_sph"])
-def test_sub4_sublist_form(eng, seed, kind, monkeypatch):
-    """The 4-ary node sublists (CONTIVCLS_SUB4=1; the default is the binary
-    form) on the sublist variants."""
-    monkeypatch.setenv("CONTIVCLS_SUB4", "1")
-    monkeypatch.setenv("CONTIVCLS_INLINE", "1" if kind.startswith("inl") else "0")
-    monkeypatch.setenv("CONTIVCLS_TRIE", "1" if kind.startswith("trie") else "0")
-    monkeypatch.setenv("CONTIVCLS_SRC_SEARCH", "1" if kind.startswith(("search", "trie")) else "0")
-    from cls_image import Image, compile_blob
-    from vpp_amd import _abi
-    rules, pool = variant_acl(kind, seed)
-    h = Image(compile_blob(_abi.CRules(rules))).h
-    assert (h.mode, h.list_mode) == VARIANTS[kind] and h.sub4 == 1, kind
-    tr = random_traffic(seed + 21, 30000, pool)
     _assert_same(_gpu(eng, rules, tr), _oracle(rules, tr))
 
 

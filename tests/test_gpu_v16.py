@@ -45,14 +45,11 @@ def test_v16_random_acls_both_kernels(eng, seed, n_rules, weird):
 @pytest.mark.parametrize("kind", sorted(VARIANTS))
 def test_v16_all_kernel_variants(eng, seed, kind, monkeypatch):
     """Mixed-family twins of the IPv4 variant tables: every list mode and
-    source lookup of the core behind the front end (inline hash cells for
-    the inl_* tables, the source trie for trie_*), the 4-ary sublist form on
-    odd seeds."""
+    source lookup of the core behind the front end (the source trie for
+    trie_*)."""
     if kind.endswith("_pc"):
         monkeypatch.setenv("CONTIVCLS_LIST_MODE_MAX", "2")
-    monkeypatch.setenv("CONTIVCLS_INLINE", "1" if kind.startswith("inl") else "0")
     monkeypatch.setenv("CONTIVCLS_TRIE", "1" if kind.startswith("trie") else "0")
-    monkeypatch.setenv("CONTIVCLS_SUB4", str(seed % 2))
     rules, pool = variant_acl(kind, seed)
     rules, tr = mix_families(rules, random_traffic(seed + 11, 20000, pool), seed)
     _assert_same(_gpu(eng, rules, tr), _oracle16(rules, tr, fast=True))

@@ -46,7 +46,7 @@ def main():
            _abi.PktSoa(_abi.AF_V4, p(pk["src"]), p(pk["dst"]), None, None, None, p(pk["dport"]), p(pk["proto"])))
     builds = []
     for path in a.libs:
-        L = _abi.bind(os.path.abspath(path))
+        L = _abi.bind(os.path.abspath(path), strict=False)
         h = C.c_void_p()
         assert L.cls_engine_create(C.byref(_abi.Config(0)), C.byref(h)) == 0
         tid = C.c_uint32()

@@ -45,7 +45,7 @@ SYMBOLS = ["cls_abi_version", "cls_engine_create", "cls_engine_destroy", "cls_la
            "cls_table_put", "cls_table_del", "cls_table_get_info", "cls_classify",
            "cls_last_kernel_ms", "cls_kernel_times", "cls_kernel_times_reset", "cls_acl_put", "cls_acl_del", "cls_acl_table", "cls_acl_counts",
            "cls_if_id",
-           "cls_if_acls", "cls_connect_batch", "cls_gen_traffic_v4", "cls_compile_v4",
+           "cls_if_acls", "cls_connect_batch", "cls_gen_traffic_v4", "cls_compile_v4", "cls_image_kernel",
            "cls_compile_v16", "cls_gen_traffic_v16", "cls_stream_floor", "cls_stream_floor_shapes", "cls_conn_bitmap_eval", "cls_conn_counters",
            "cls_acl_stats"]
 
@@ -115,8 +115,7 @@ class ImageHeader(C.Structure):
         ("port_dflt", C.c_uint32),
         ("n_hot", C.c_uint32), ("off_hot", C.c_uint32), ("n_lctr", C.c_uint32), ("ctr16", C.c_uint32),
         ("swap", C.c_uint32), ("off_other", C.c_uint32), ("off_trie", C.c_uint32), ("trie_depth", C.c_uint32),
-        ("off_gcells", C.c_uint32), ("n_gcells", C.c_uint32), ("sub4", C.c_uint32),
-        ("dflt_cell", C.c_uint32 * 3)]
+        ("off_gcells", C.c_uint32), ("n_gcells", C.c_uint32)]
 
 
 class Image16Header(C.Structure):
@@ -146,9 +145,10 @@ def lib():
     return _lib
 
 
-def bind(path: str):
+def bind(path: str, strict: bool = True):
     """Load a build of the library (RTLD_LOCAL: several builds may live in
-    one process -- tools/ab_inproc.py) and declare its signatures."""
+    one process -- tools/ab_inproc.py) and declare its signatures (strict:
+    every symbol of this ABI must be there)."""
     # One HIP runtime per process: PyTorch ships its own libamdhip64.so.7.
     # Load it first so that our NEEDED libamdhip64.so.7 resolves to the same
     # already-loaded runtime (two runtimes in one process cannot share the GPU).
@@ -187,11 +187,14 @@ def bind(path: str):
         "cls_gen_traffic_v4": (C.c_int, [vp, C.POINTER(TrafficSpec), u64, u64, vp, vp, vp, vp,
                                          vp, vp]),
         "cls_compile_v4": (C.c_int, [C.POINTER(ClsRule), u32, vp, u64, C.POINTER(u64)]),
+        "cls_image_kernel": (C.c_int, [u32, u32, C.c_int, C.c_int]),
         "cls_compile_v16": (C.c_int, [C.POINTER(ClsRule), u32, vp, u64, C.POINTER(u64)]),
         "cls_gen_traffic_v16": (C.c_int, [vp, C.POINTER(TrafficSpec16), u64, u64, vp, vp, vp, vp,
                                           vp, vp]),
     }
     for name, (res, args) in sig.items():
+        if not strict and not hasattr(L, name):      # an older build (A/B tools)
+            continue
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args

@@ -1092,25 +1092,12 @@ static bool build_cls4_one(const std::vector<SemRule>& sem, uint32_t n_rules, Cl
 
     std::vector<uint32_t>& w = img.words;
     // trie: the source trie replaces the interval search (mode 0 only);
-    // wide: list modes 3, 4 with the cells in global memory (gcells)
-    // sublist search: the binary form (8-B probes), or 4-ary nodes with
-    // CONTIVCLS_SUB4=1 (16-B reads, half the dependent steps -- but a random
-    // ds_read_b128 costs about two random ds_read_b64 in bank cycles, and the
-    // kernel is bound by those: config 3 0.613 ms against 0.600 binary,
-    // DESIGN.md section 4, item 5)
-    const bool sub4 = env_flag("CONTIVCLS_SUB4");
-    uint32_t L4 = 0;
-    for (const auto& sl : subs) {
-        uint32_t l = 0, cap = 1;
-        while (cap < sl.start.size()) { cap *= 4u; ++l; }
-        if (sl.start.size() > 1 && l == 0) l = 1;
-        L4 = std::max(L4, l);
-    }
+    // wide: list modes 3, 4 with the cells in global memory (gcells).
+    // (Two round-3 variants were measured and removed: sublists as 4-ary
+    // 16-B node trees, 0.613 against 0.600 ms on config 3, and hash entries
+    // carrying their class's cells inline, 0.639 against 0.613 -- a random
+    // ds_read_b128 costs about two random ds_read_b64 in bank cycles.)
     const uint32_t n_hash0 = img.n_hash;
-    // inline cells in 16-B hash entries (src mode 6) with CONTIVCLS_INLINE=1;
-    // by default the entries hold class rows (config 3: 0.639 ms inline
-    // against 0.613, the 16-B probes' bank cycles again)
-    const bool inline_ok = env_flag("CONTIVCLS_INLINE") && ncell == 3;
     auto serialise = [&](uint32_t lm, bool trie, bool wide) -> bool {
         img.mode = trie ? 4u : mode0;
         img.n_hash = trie ? 0u : n_hash0;                 // the trie replaces the hash LPM
@@ -1127,8 +1114,7 @@ static bool build_cls4_one(const std::vector<SemRule>& sem, uint32_t n_rules, Cl
             else if (lm == 1) bv_desc[bv_lists[i]] = build_bv(bv_ents[i], S, bv);
         }
         img.list_mode = lm;
-        img.bv_steps_d = lm >= 3 ? (sub4 ? L4 : D) : lm == 2 ? Sd : S;
-        img.sub4 = lm >= 3 && sub4 ? 1u : 0u;
+        img.bv_steps_d = lm >= 3 ? D : lm == 2 ? Sd : S;
         img.bv_steps_p = lm >= 2 ? 0u : S;
         img.n_pclass = lm >= 3 ? uint32_t(prep.size()) : lm == 2 ? uint32_t(G.size()) : 0u;
         img.bv_wide = 0;
@@ -1239,74 +1225,16 @@ static bool build_cls4_one(const std::vector<SemRule>& sem, uint32_t n_rules, Cl
             w.insert(w.end(), bv.begin(), bv.end());
             w.resize(align4(uint32_t(w.size())));
         }
-        // Inline cells (one hashed prefix length, sublist cells in LDS): an
-        // entry carries its class's three cells, so the probe that finds the
-        // class also delivers the cell (src mode 6; no cell read after it)
-        img.hash_inline = inline_ok && img.mode == 1 && img.n_hash == 1 && lm >= 3 && !wide ? 1u : 0u;
         for (uint32_t i = 0; i < img.n_hash; ++i) {
             w.resize(align4(uint32_t(w.size())));
             img.off_hash[i] = uint32_t(w.size()) * 4;
-            for (uint64_t e : hash_tabs[i]) {
-                const uint32_t row = img.off_cells + uint32_t(e >> 32) * img.row_bytes;
+            for (uint64_t e : hash_tabs[i]) {               // entry {key, byte address of the class's cell row}
                 w.push_back(uint32_t(e));
-                if (img.hash_inline) {               // entry {key, cell TCP, cell UDP, cell ICMP}
-                    for (uint32_t k = 0; k < 3; ++k) w.push_back(w[row / 4 + k]);
-                } else {                             // entry {key, byte address of the class's cell row}
-                    w.push_back(row);
-                }
+                w.push_back(img.off_cells + uint32_t(e >> 32) * img.row_bytes);
             }
             w.resize(align4(uint32_t(w.size())));
         }
-        if (img.hash_inline) {
-            img.mode = 6;
-            for (uint32_t k = 0; k < 3; ++k) img.dflt_cell[k] = w[img.default_row / 4 + k];
-        }
-        if (lm >= 3 && sub4) {
-            // 4-ary sublist nodes (16 B, LDS-aligned): a sublist of n
-            // intervals is a tree of L levels (L uniform: 4^L >= every n).
-            // Interior node {k1, k2, k3, first child's byte address}, leaf
-            // node {k1, k2, k3, outcomes of its 4 intervals, a byte each};
-            // k_i = start - 1 of the i-th quarter (0xFFFFFFFF past the
-            // sublist: never taken); the child (or interval) is c = #(k_i <
-            // dst).  The pointer tables hold root addresses (L = 0: the
-            // outcome itself).
-            w.resize(align4(uint32_t(w.size())));
-            img.off_bv = uint32_t(w.size()) * 4;
-            std::vector<uint32_t> root(subs.size(), 0u);
-            uint32_t q0 = 1;
-            for (uint32_t l = 1; l < L4; ++l) q0 *= 4u;             // leaves per child of the root
-            for (size_t k = 0; k < subs.size(); ++k) {
-                const Sublist& sl = subs[k];
-                const uint32_t n = uint32_t(sl.start.size());
-                if (L4 == 0) { root[k] = sl.out[0]; continue; }
-                // breadth-first: each node's children as one contiguous block
-                struct Job { uint32_t at, lo, q; };         // node word index, first interval, leaves per child
-                std::vector<Job> jobs;
-                root[k] = uint32_t(w.size()) * 4;
-                jobs.push_back({uint32_t(w.size()), 0u, q0});
-                w.resize(w.size() + 4, 0u);
-                for (size_t j = 0; j < jobs.size(); ++j) {
-                    const Job jb = jobs[j];
-                    auto key = [&](uint32_t i) { return i < n ? sl.start[i] - 1u : 0xFFFFFFFFu; };
-                    for (uint32_t i = 1; i < 4; ++i) w[jb.at + i - 1] = key(jb.lo + i * jb.q);
-                    if (jb.q == 1) {                           // leaf
-                        uint32_t o = 0;
-                        for (uint32_t i = 0; i < 4; ++i) o |= (jb.lo + i < n ? sl.out[jb.lo + i] & 0xFFu : 0u) << (8 * i);
-                        w[jb.at + 3] = o;
-                        continue;
-                    }
-                    uint32_t nc = 0;
-                    while (nc < 4 && jb.lo + nc * jb.q < n) ++nc;
-                    w[jb.at + 3] = uint32_t(w.size()) * 4;
-                    const uint32_t first = uint32_t(w.size());
-                    w.resize(w.size() + 4 * nc, 0u);
-                    for (uint32_t c = 0; c < nc; ++c) jobs.push_back({first + 4 * c, jb.lo + c * jb.q, jb.q / 4});
-                }
-            }
-            for (size_t i = 0; i < bv_lists.size(); ++i)
-                for (size_t p = 0; p < prep.size(); ++p) w[ptr_at[i] + p] = root[sub_of[i][p]];
-            w.resize(align4(uint32_t(w.size())));
-        } else if (lm >= 3) {
+        if (lm >= 3) {
             // Sublist region, 8-B slots.  A sublist of n intervals and depth s
             // (2^s >= n) sits at slot A: entries 1 .. n-1 in slots A+1 .. A+n-1
             // as {start - 1, outcome | (A + c) << 16}; the slots a probe may

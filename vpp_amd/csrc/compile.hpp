@@ -134,17 +134,11 @@ struct Cls4Image {
     uint32_t lds_bytes = 0;        // image + counters (u32 per slot), 16 B aligned
     std::vector<uint32_t> ctr_rule;  // slot -> rule index (R = default DENY)
     // source lookup: mode 0 = interval binary search, 1 = hash LPM, 3 = rows
-    // given by the caller (16-byte core), 4 = source trie (off_trie), 6 =
-    // hash LPM with the cells in the entries (hash_inline)
+    // given by the caller (16-byte core), 4 = source trie (off_trie)
     uint32_t mode = 0;
     // mode 4: level 1 (256 u32, indexed by src >> 24) at off_trie, then the
     // nodes and leaves (compile.cpp build_trie); trie_depth = deepest leaf
     uint32_t off_trie = 0, trie_depth = 0;
-    // mode 6: mode 1 with one prefix length whose hash entries are 16 B
-    // {key, the class's TCP, UDP, ICMP cells} (sublist modes 3, 4); a miss
-    // takes dflt_cell (the default class's cells)
-    uint32_t hash_inline = 0;
-    uint32_t dflt_cell[3] = {};
     uint32_t default_class = 0;    // hash mode: class of addresses no hashed prefix covers
     uint32_t n_hash = 0;           // hashed prefix lengths, ascending
     uint32_t hash_mask[kMaxHashLens] = {}, hash_shift[kMaxHashLens] = {};  // shift = 32 - L
@@ -168,9 +162,6 @@ struct Cls4Image {
     // byte offset into gcells (off_cells 0, row_bytes 8 x n_cells)
     std::vector<uint32_t> gcells;
     uint32_t sub_bytes = 0;        // modes 3, 4: end of the pointer tables (< 64 KiB)
-    // modes 3-6: the sublists as 4-ary node trees of bv_steps_d levels
-    // (pointer tables hold root node addresses), else the binary slot form
-    uint32_t sub4 = 0;
     // mode 4: port perfect hash at LDS 0: e = u32 at byte mulhi(port, mul) &
     // mask4, class x 4 = (e & 0xFFFF) == port ? e >> 16 : port_dflt
     uint32_t port_mul = 0, port_mask4 = 0, port_dflt = 0;

@@ -192,6 +192,10 @@ extern "C" {
 
 int cls_abi_version(void) { return CLS_ABI_VERSION; }
 
+int cls_image_kernel(uint32_t mode, uint32_t list_mode, int lds_resident, int rep16) {
+    return cls_kernel_exists(mode, list_mode, lds_resident != 0, rep16 != 0) ? CLS_OK : CLS_E_INVAL;
+}
+
 int cls_engine_create(const cls_config* cfg, cls_engine** out) {
     if (!out) return CLS_E_INVAL;
     *out = nullptr;
@@ -380,9 +384,10 @@ static int table_put_locked(cls_engine* e, const char* name, const cls_rule* rul
             t->has_cls = true;
             t->kernel = 1;
             t->lds_resident = t->img.lds_ok && t->img.lds_bytes + kLdsReserved <= uint32_t(max_lds_bytes());
-            // the trie, inline hash cells and wide cells exist only in LDS-resident images
-            if (!t->lds_resident && (t->img.mode == 4 || t->img.mode == 6 || t->img.list_mode >= 5))
-                return fail(e, CLS_E_INVAL, "compiler produced an LDS-only image that does not fit LDS");
+            // the trie and wide cells exist only in LDS-resident images
+            if (!cls_kernel_exists(t->img.mode, t->img.list_mode, t->lds_resident, false))
+                return fail(e, CLS_E_INVAL, "no classify kernel for the compiled image (mode %u, list mode %u%s)",
+                            t->img.mode, t->img.list_mode, t->lds_resident ? "" : ", global memory");
             rc = upload(e, t->d_img, t->img);
             if (rc == CLS_OK) rc = upload(e, t->d_oimg, t->oimg);
             if (rc == CLS_OK) rc = upload_slot_rule(e, t->d_slot_rule, t->img, t->oimg);
@@ -407,8 +412,9 @@ static int table_put_locked(cls_engine* e, const char* name, const cls_rule* rul
             const Cls4Image& c = q.img.core;
             q.lin = linear4(q.img.sem);
             q.lds_resident = c.lds_ok && c.lds_bytes + kLdsReserved <= uint32_t(max_lds_bytes());
-            if (!q.lds_resident && (c.mode == 4 || c.mode == 6 || c.list_mode >= 5))
-                return fail(e, CLS_E_INVAL, "compiler produced an LDS-only 16-byte image that does not fit LDS");
+            if (!cls_kernel_exists(c.mode, c.list_mode, q.lds_resident, true))
+                return fail(e, CLS_E_INVAL, "no 16-byte classify kernel for the compiled image (mode %u, list mode %u%s)",
+                            c.mode, c.list_mode, q.lds_resident ? "" : ", global memory");
             rc = upload(e, q.d_img, c);
             if (rc == CLS_OK) rc = upload(e, q.d_oimg, q.oimg);
             if (rc == CLS_OK) rc = upload_slot_rule(e, q.d_slot_rule, c, q.oimg);
@@ -531,8 +537,6 @@ static Cls4Dev cls4_dev(const Cls4Image& im, const DevBuf& d_img, const DevBuf& 
     cd.off_hot = im.off_hot;
     cd.n_lctr = im.n_lctr;
     cd.ctr16 = im.ctr16;
-    cd.sub4 = im.sub4;
-    for (int k = 0; k < 3; ++k) cd.dflt_cell[k] = im.dflt_cell[k];
     cd.off_trie = im.off_trie;
     cd.trie_depth = im.trie_depth;
     cd.gcells = im.gcells.empty() ? nullptr
@@ -1552,7 +1556,7 @@ static int write_blob(const Cls4Image* img, const std::vector<LinRule4>& lin, ui
     cls_image_v4_header h;
     std::memset(&h, 0, sizeof h);
     h.magic = magic;
-    h.version = 3;
+    h.version = 4;
     h.n_rules = n;
     h.n_lin = uint32_t(lin.size());
     h.has_cls = img ? 1u : 0u;
@@ -1583,8 +1587,6 @@ static int write_blob(const Cls4Image* img, const std::vector<LinRule4>& lin, ui
         h.n_lctr = im.n_lctr;
         h.ctr16 = im.ctr16;
         h.swap = im.swap;
-        h.sub4 = im.sub4;
-        for (int k = 0; k < 3; ++k) h.dflt_cell[k] = im.dflt_cell[k];
         h.off_trie = im.off_trie;
         h.trie_depth = im.trie_depth;
         h.n_gcells = uint32_t(im.gcells.size());

@@ -52,7 +52,6 @@ struct Cls4Dev {
     uint32_t n_rules;          // R
     uint32_t mode;             // 0 interval search, 1 hash LPM, 4 source trie
     uint32_t off_trie, trie_depth;   // mode 4: level 1 at off_trie (compile.cpp build_trie)
-    uint32_t dflt_cell[3];     // mode 6 (hash entries with inline cells): the default class's cells
     const uint8_t* gcells;     // list modes 5, 6: wide cells (uint2 {pointer table, counter base})
     uint32_t default_row;      // source lookup miss: byte address of the default class's cells
     uint32_t n_hash;
@@ -61,8 +60,7 @@ struct Cls4Dev {
     uint32_t hash_mul[kMaxHashLens], hash_shift1[kMaxHashLens];   // shift1 = 32 - 2 L
     uint32_t list_mode;        // 0 template scan, 1 bit vectors, 2 + global port classes,
                                // 3 port-filtered sublists, 4 + hashed port classes
-    uint32_t bv_steps;         // bit-vector search depth (max over lists, both dims); sub4: levels
-    uint32_t sub4;             // list modes 3-6: 4-ary sublist node trees (compile.hpp Cls4Image::sub4)
+    uint32_t bv_steps;         // bit-vector search depth (max over lists, both dims)
     uint32_t n_hot;            // slots [0, n_hot) are counted in per-lane LDS rows
     uint32_t off_hot;          // byte offset of the rows (n_hot x 64 u32) in LDS
     uint32_t off_ptop;         // list mode 2: port radix
@@ -78,6 +76,20 @@ struct Cls4Dev {
     unsigned long long* zero = nullptr;   // the call's rule counters, cleared by the launch's
     uint32_t n_zero = 0;                  // workgroups before the finish launch adds to them
 };
+
+// Whether the classify dispatchers have a kernel for an image of source
+// lookup `mode` and `list_mode`, LDS-resident or not; rep16: the 16-byte
+// core (mode 3 = rows from the front end's host-route hashes).  The source
+// trie and the wide cells exist only in LDS.
+inline bool cls_kernel_exists(uint32_t mode, uint32_t list_mode, bool lds, bool rep16) {
+    if (list_mode > 6 || (list_mode >= 5 && !lds)) return false;
+    switch (mode) {
+    case 0: case 1: return true;
+    case 3: return rep16;
+    case 4: return lds && list_mode >= 3;
+    default: return false;
+    }
+}
 
 struct LaunchCfg {
     int grid;                  // workgroups (persistent, grid-stride)

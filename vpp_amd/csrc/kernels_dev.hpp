@@ -35,27 +35,12 @@
 
 #include "kernels.hpp"
 
-// Diagnostics builds only (tools/build_ablate.sh): skip stages while keeping
-// their inputs live -- 1 slot counting, 2 sublist probes, 4 source lookup,
-// 8 port lookup, 16 LDS image staging and counter flush, 32 the whole
-// per-packet evaluation (a mix of the fields, as the stream kernel).
-#ifndef CLS_ABLATE
-#define CLS_ABLATE 0
-#endif
-
 namespace cls {
 
 namespace {
 
 constexpr int kBlock = 1024;      // linear kernel
-// 16-byte kernel packet order: 1 wave-contiguous (default), 0 four consecutive per lane
-#ifndef CLS_COAL16
-#define CLS_COAL16 1
-#endif
-#ifndef CLS_BLOCK
-#define CLS_BLOCK 1024
-#endif
-constexpr int kClsBlock = CLS_BLOCK;   // classifier workgroup (one LDS image per workgroup)
+constexpr int kClsBlock = 1024;   // classifier workgroup (one LDS image per workgroup)
 constexpr int kLdsMax = 160 * 1024;
 constexpr uint32_t kLinLdsCounters = 16384;  // linear kernel: LDS counters up to R+1 <= this
 
@@ -262,12 +247,8 @@ __device__ __forceinline__ void classify_n(const Img<kLds>& im, const Cls4Dev& t
         // every port no rule names).
 #pragma unroll
         for (int q = 0; q < N; ++q) {
-            if constexpr (CLS_ABLATE & 8) {
-                pc[q] = dport[q] & 0xFCu;
-            } else {
-                const uint32_t e = im.u32(__umulhi(dport[q], t.port_mul) & t.port_mask4);
-                pc[q] = (e & 0xFFFFu) == dport[q] ? e >> 16 : t.port_dflt;
-            }
+            const uint32_t e = im.u32(__umulhi(dport[q], t.port_mul) & t.port_mask4);
+            pc[q] = (e & 0xFFFFu) == dport[q] ? e >> 16 : t.port_dflt;
         }
     } else if constexpr (kPort >= 2) {
         // Global port class from the radix at image address 0: top[port >> 8]
@@ -281,18 +262,7 @@ __device__ __forceinline__ void classify_n(const Img<kLds>& im, const Cls4Dev& t
         for (int q = 0; q < N; ++q) pc[q] = im.u8(tp[q] + (dport[q] & 0xFFu));
     }
     uint32_t row[N];
-    if constexpr (kMode == 6) {
-        // inline cells: the hash probe below gives the cell itself
-#pragma unroll
-        for (int q = 0; q < N; ++q) row[q] = 0u;
-    } else if constexpr (CLS_ABLATE & 4) {
-#pragma unroll
-        for (int q = 0; q < N; ++q) row[q] = t.default_row + ((src[q] & 1u) ? 0u : 0u) + (src[q] & 0u);
-#pragma unroll
-        for (int q = 0; q < N; ++q) asm volatile("" :: "v"(src[q]));
-    } else {
-        src_row<N, kLds, kMode>(im, t, src, row);
-    }
+    src_row<N, kLds, kMode>(im, t, src, row);
 
     if constexpr (kList >= 3) {
         // Port-filtered sublists.  cell = {pointer table word address | counter
@@ -305,45 +275,7 @@ __device__ __forceinline__ void classify_n(const Img<kLds>& im, const Cls4Dev& t
         // {start - 1, state} 8 << i bytes further and the state moves to the
         // entry when start - 1 < dst: one shift, one compare, one select.
         uint32_t cell[N], st[N];
-        if constexpr (CLS_ABLATE & 8) {
-#pragma unroll
-            for (int q = 0; q < N; ++q) {
-                cell[q] = row[q] + proto[q] + pc[q];
-                st[q] = cell[q] & 0x3Fu;
-            }
-        } else if constexpr (kMode == 6) {
-            // src mode 6: one hashed prefix length, entries {key, cell TCP,
-            // cell UDP, cell ICMP} -- the two cuckoo probes deliver the cell
-            // (a miss: the default class's cells), no cell read after them
-            const uint32_t tab = t.off_hash[0], mask = t.hash_mask[0], mul = t.hash_mul[0];
-            const uint32_t s0 = t.hash_shift[0], s1 = t.hash_shift1[0], L = 32u - s0;
-            const uint32_t tab1 = __builtin_amdgcn_readfirstlane(tab + 16u * t.hash_cap[0]);
-            // The default class's three cells as opaque SGPR values: a select
-            // among t.dflt_cell[0..2] by the lane's protocol would otherwise
-            // become a per-lane load from the kernel arguments, and its
-            // vmcnt(0) wait would drain the packet stream's loads in flight.
-            uint32_t cd0 = t.dflt_cell[0], cd1 = t.dflt_cell[1], cd2 = t.dflt_cell[2];
-            asm volatile("" : "+s"(cd0), "+s"(cd1), "+s"(cd2));
-            uint4 e0[N], e1[N];
-            uint32_t key[N];
-#pragma unroll
-            for (int q = 0; q < N; ++q) {
-                key[q] = src[q] & mask;
-                const uint32_t h = key[q] * mul;
-                e0[q] = im.u128(tab + 16u * (h >> s0));
-                e1[q] = im.u128(tab1 + 16u * __builtin_amdgcn_ubfe(h, s1, L));
-            }
-#pragma unroll
-            for (int q = 0; q < N; ++q) {
-                const uint32_t p = proto[q];
-                const uint32_t c0 = p == 0u ? e0[q].y : p == 1u ? e0[q].z : e0[q].w;
-                const uint32_t c1 = p == 0u ? e1[q].y : p == 1u ? e1[q].z : e1[q].w;
-                const uint32_t cd = p == 0u ? cd0 : p == 1u ? cd1 : cd2;
-                cell[q] = e0[q].x == key[q] ? c0 : (e1[q].x == key[q] ? c1 : cd);
-            }
-#pragma unroll
-            for (int q = 0; q < N; ++q) st[q] = im.u32(((cell[q] & 0x3FFFu) << 2) + pc[q]);
-        } else if constexpr (kWide) {
+        if constexpr (kWide) {
             // cell = {pointer table byte address, counter base}; cell[q] keeps
             // the base (the slot below)
             uint2 wc[N];
@@ -366,41 +298,6 @@ __device__ __forceinline__ void classify_n(const Img<kLds>& im, const Cls4Dev& t
         // (the compiler materialises those uniform guards as lane masks, a
         // few VALU ops per step).
         static_assert(kMaxBvSteps == 7, "step chain below");
-        if constexpr (CLS_ABLATE & 2) {
-#pragma unroll
-            for (int q = 0; q < N; ++q) asm volatile("" :: "v"(dst[q]));   // keep the dst loads
-        } else if (kD < 0 && t.sub4) {
-            // (depth-specialised variants are binary-only: a run-time branch
-            // there cost the hot config-3 kernel 6 %, 0.561 -> 0.598 ms,
-            // profiles/r03j_ab_config3.txt; sub4 images take the kD < 0 kernels)
-            // 4-ary node trees (compile.cpp sub4): L - 1 interior levels
-            // {k1, k2, k3, first child}, then the leaf {k1, k2, k3, outcomes};
-            // c = #(k_i < dst) picks the child / interval.  One ds_read_b128
-            // per level: half the binary form's dependent reads.  L = 0: the
-            // pointer table held the outcome.
-            const uint32_t L = t.bv_steps;
-#pragma unroll
-            for (uint32_t l = 0; l + 1 < 4u; ++l) {
-                if (l + 1 >= L) break;
-                uint4 e[N];
-#pragma unroll
-                for (int q = 0; q < N; ++q) e[q] = im.u128(st[q]);
-#pragma unroll
-                for (int q = 0; q < N; ++q)
-                    st[q] = e[q].w + 16u * (uint32_t(e[q].x < dst[q]) + uint32_t(e[q].y < dst[q]) +
-                                            uint32_t(e[q].z < dst[q]));
-            }
-            if (L > 0) {
-                uint4 e[N];
-#pragma unroll
-                for (int q = 0; q < N; ++q) e[q] = im.u128(st[q]);
-#pragma unroll
-                for (int q = 0; q < N; ++q) {
-                    const uint32_t c = uint32_t(e[q].x < dst[q]) + uint32_t(e[q].y < dst[q]) + uint32_t(e[q].z < dst[q]);
-                    st[q] = (e[q].w >> (8u * c)) & 0xFFu;
-                }
-            }
-        } else {
         if constexpr (kD > 6) sub_step<6>(im, dst, st);
         if constexpr (kD > 5) sub_step<5>(im, dst, st);
         if constexpr (kD > 4) sub_step<4>(im, dst, st);
@@ -416,7 +313,6 @@ __device__ __forceinline__ void classify_n(const Img<kLds>& im, const Cls4Dev& t
             if (t.bv_steps > 2) sub_step<2>(im, dst, st);
             if (t.bv_steps > 1) sub_step<1>(im, dst, st);
             if (t.bv_steps > 0) sub_step<0>(im, dst, st);
-        }
         }
 #pragma unroll
         for (int q = 0; q < N; ++q) {
@@ -592,8 +488,7 @@ __device__ __forceinline__ void run_n(const Img<kLds>& im, const Cls4Dev& t, con
     for (int q = 0; q < N; ++q) {
         if constexpr (kLds && kCtr == 0) {
             addr[q] = slot[q] < t.n_hot ? hot_lane + slot[q] * 256u : t.img_bytes + slot[q] * 4u;
-            if constexpr (CLS_ABLATE & 1) asm volatile("" :: "v"(addr[q]));
-            else __hip_atomic_fetch_add(lctr_t(addr[q]), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_fetch_add(lctr_t(addr[q]), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         } else if constexpr (kLds) {
             // Tiered counters.  A u16 counter lives in half of an LDS word; the
             // lane whose add takes it from 0x7FFF to 0x8000 moves 0x8000 to the
@@ -676,43 +571,6 @@ __device__ __forceinline__ void run_n(const Img<kLds>& im, const Cls4Dev& t, con
     }
 }
 
-#ifndef CLS_GROUPS
-#define CLS_GROUPS 1
-#endif
-// The protocol stream (4 B per lane) as a cached load, the others
-// non-temporal: tools/nt_sweep.hip measured this mix as the fastest stream
-// of the 32 combinations (0.523 vs 0.566 ms per 256 Mi packets all-nt).
-#ifndef CLS_NT_PROTO
-#define CLS_NT_PROTO 0
-#endif
-// 16-byte kernel: dport / proto (2 B / 1 B per lane) non-temporal
-#ifndef CLS_NT16_SMALL
-#define CLS_NT16_SMALL 1
-#endif
-// 0 (default): load and use, the CU's 16 waves overlapping one another's
-// loads and lookups; 1: the next step's loads in flight during this step's
-// lookups (two buffers); 2: two steps ahead (three buffers).  Config 3,
-// in-process A/B on MI355X (profiles/r02s4_prefetch_depth_ab_config3.txt):
-// 0.559 / 0.566 / 0.583 ms -- the buffers' registers cost more than the
-// overlap they buy at 16 waves per CU.
-#ifndef CLS_PREFETCH
-#define CLS_PREFETCH 0
-#endif
-// The prefetching loops load the step after the current one, which may lie
-// past the last whole step: clamped to it (the data unused).  The default
-// loop never loads past it.
-#ifndef CLS_CLAMP
-#define CLS_CLAMP (CLS_PREFETCH != 0)
-#endif
-// 1 (default): a step's packet loads issued src, dst, dport, proto, as the
-// stream kernel does (the compiler otherwise issues proto first, for the
-// protocol test): config 3 0.551 against 0.558 ms in one-process A/B
-// (profiles/r03z_ab_load_order_config3.txt)
-#ifndef CLS_LOAD_ORDER
-#define CLS_LOAD_ORDER 1
-#endif
-constexpr int kG = CLS_GROUPS;     // 16-B packet groups per lane per step
-
 // The OTHER queue's fill counter of this workgroup: one LDS word after the
 // image's LDS (the launch adds 16 bytes of dynamic LDS for it).  Zeroed
 // here, made visible by the barrier of stage_lds (or this one).
@@ -754,7 +612,6 @@ __device__ __forceinline__ void flush_lds(const Cls4Dev& t, uint4* smem) {
     const uint32_t* lctr = reinterpret_cast<const uint32_t*>(lds + t.img_bytes);
     const uint32_t* hrow = reinterpret_cast<const uint32_t*>(lds + t.off_hot);
     uint32_t* part = t.part + size_t(blockIdx.x) * t.n_lctr;
-    if constexpr (CLS_ABLATE & 16) return;
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
     for (uint32_t h = wave; h < t.n_hot; h += blockDim.x >> 6) {
         uint32_t v = hrow[h * 64u + lane];
@@ -772,12 +629,12 @@ template <bool kLds, bool kVec, int kMode, int kList, int kD, int kCtr>
 __global__ __launch_bounds__(kClsBlock) void classify4_cls(Cls4Dev t, Cls4Dev o, Pkts4 p, uint8_t* verdict,
                                                            unsigned long long* gslot) {
     extern __shared__ uint4 smem[];
-    if (t.zero && !(CLS_ABLATE & 64))   // the call's rule counters, added to by the finish launch
+    if (t.zero)   // the call's rule counters, added to by the finish launch
         for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < t.n_zero; i += gridDim.x * blockDim.x)
             t.zero[i] = 0ull;
     Img<kLds> im{reinterpret_cast<const uint8_t*>(t.img)};
-    const uint32_t oq_lds = (CLS_ABLATE & 64) ? 0u : queue_begin<kLds>(t, smem);
-    if constexpr (kLds && !(CLS_ABLATE & 16)) stage_lds(t, smem);
+    const uint32_t oq_lds = queue_begin<kLds>(t, smem);
+    if constexpr (kLds) stage_lds(t, smem);
 
     const uint32_t nthreads = gridDim.x * blockDim.x;
     const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
@@ -785,217 +642,53 @@ __global__ __launch_bounds__(kClsBlock) void classify4_cls(Cls4Dev t, Cls4Dev o,
     const uint32_t hot_lane = t.off_hot + 4u * (threadIdx.x & 63u);
     uint32_t tail_from = 0;
     if constexpr (kVec) {
-        // 4 packets per lane per step, the next step's loads issued before this
-        // step's lookups.  32-bit indices: the host splits batches at 2^30.
+        // 4 packets per lane per step: 16-B (src, dst), 8-B (dport) and 4-B
+        // (proto) loads, one 4-B verdict store.  32-bit indices: the host
+        // splits batches at 2^30.
         const uint32_t nsteps = uint32_t(p.n / 4u);
         const uint4* S = reinterpret_cast<const uint4*>(p.src);
         const uint4* D = reinterpret_cast<const uint4*>(p.dst);
         const uint2* DP = reinterpret_cast<const uint2*>(p.dport);
         const uint32_t* PR = reinterpret_cast<const uint32_t*>(p.proto);
-        // A step takes kG 16-B groups (4 packets each) per lane, group k at
-        // index g + k * nthreads: every load instruction stays coalesced, and
-        // the lookups of the 4 kG packets interleave (more LDS reads in flight
-        // per wave; 16 waves per CU is the ceiling with one LDS image per CU).
-        struct Buf {
-            uint4 s[kG], d[kG];
-            uint2 dp[kG];
-            uint32_t pr[kG];
+        auto step = [&](const uint4& s4, const uint4& d4, const uint2& p2, uint32_t pr, uint32_t g) {
+            const uint32_t sa[4] = {s4.x, s4.y, s4.z, s4.w}, da[4] = {d4.x, d4.y, d4.z, d4.w};
+            const uint32_t pa[4] = {p2.x & 0xFFFFu, p2.x >> 16, p2.y & 0xFFFFu, p2.y >> 16};
+            const uint32_t ra[4] = {pr & 0xFFu, (pr >> 8) & 0xFFu, (pr >> 16) & 0xFFu, pr >> 24};
+            // some protocol byte > 2 (SWAR: bit 7 of each byte of x + 125,
+            // computed without inter-byte carries)
+            const bool other = ((pr | ((pr & 0x7F7F7F7Fu) + 0x7D7D7D7Du)) & 0x80808080u) != 0u;
+            uint32_t v[4];
+            const uint32_t ix[4] = {4u * g, 4u * g + 1u, 4u * g + 2u, 4u * g + 3u};
+            run_n<4, kLds, kMode, kList, kD, kCtr>(im, t, o, hot_lane, gslot, hot0, sa, da, pa, ra, other, v, sa, ix,
+                                                   oq_lds);
+            if constexpr (kCtr == 2)                             // slot mode: 4 result words per lane
+                reinterpret_cast<uint4*>(verdict)[g] = make_uint4(v[0], v[1], v[2], v[3]);
+            else if (verdict)
+                stnt(v[0] | (v[1] << 8) | (v[2] << 16) | (v[3] << 24),
+                     const_cast<uint32_t*>(at(reinterpret_cast<const uint32_t*>(verdict), g)));
         };
-        // The loads are unconditional: a lane past the end re-reads the last
-        // group (its data unused).  Loads under a divergent branch make the
-        // compiler wait for *every* outstanding load (vmcnt(0)) where the
-        // branches join -- the next step's prefetch included, which then
-        // overlaps nothing.
-        const uint32_t span = nthreads * uint32_t(kG);
-        const uint32_t nfull = nsteps / span * span;   // whole grid steps: uniform trip count
-        auto load = [&](Buf& b, uint32_t g, bool ok) {
-            (void)ok;
-#pragma unroll
-            for (int k = 0; k < kG; ++k) {
-                const uint32_t gi = CLS_CLAMP ? min(g + uint32_t(k) * nthreads, nfull - 1u) : g + uint32_t(k) * nthreads;
-                if constexpr (CLS_LOAD_ORDER) {
-                    // issue order src, dst, dport, proto (the stream kernel's)
-                    b.s[k] = ldnt(at(S, gi));
-                    __builtin_amdgcn_sched_barrier(0);
-                    b.d[k] = ldnt(at(D, gi));
-                    __builtin_amdgcn_sched_barrier(0);
-                    b.dp[k] = ldnt(at(DP, gi));
-                    __builtin_amdgcn_sched_barrier(0);
-                    b.pr[k] = CLS_NT_PROTO ? ldnt(at(PR, gi)) : *at(PR, gi);
-                    __builtin_amdgcn_sched_barrier(0);
-                } else {
-                    b.s[k] = ldnt(at(S, gi)); b.d[k] = ldnt(at(D, gi));
-                    b.dp[k] = ldnt(at(DP, gi));
-                    b.pr[k] = CLS_NT_PROTO ? ldnt(at(PR, gi)) : *at(PR, gi);
-                }
-            }
-        };
-        // the step's lookups; its verdict words (4 packets each) into vw
-        auto compute = [&](const Buf& b, uint32_t g, uint32_t (&vw)[kG]) {
-            constexpr int kN = 4 * kG;
-            uint32_t sa[kN], da[kN], pa[kN], ra[kN];
-            bool other = false;
-#pragma unroll
-            for (int k = 0; k < kG; ++k) {
-                sa[4 * k + 0] = b.s[k].x; sa[4 * k + 1] = b.s[k].y; sa[4 * k + 2] = b.s[k].z; sa[4 * k + 3] = b.s[k].w;
-                da[4 * k + 0] = b.d[k].x; da[4 * k + 1] = b.d[k].y; da[4 * k + 2] = b.d[k].z; da[4 * k + 3] = b.d[k].w;
-                pa[4 * k + 0] = b.dp[k].x & 0xFFFFu; pa[4 * k + 1] = b.dp[k].x >> 16;
-                pa[4 * k + 2] = b.dp[k].y & 0xFFFFu; pa[4 * k + 3] = b.dp[k].y >> 16;
-                const uint32_t pr = b.pr[k];
-                ra[4 * k + 0] = pr & 0xFFu; ra[4 * k + 1] = (pr >> 8) & 0xFFu;
-                ra[4 * k + 2] = (pr >> 16) & 0xFFu; ra[4 * k + 3] = pr >> 24;
-                other |= ((pr | ((pr & 0x7F7F7F7Fu) + 0x7D7D7D7Du)) & 0x80808080u) != 0u;
-            }
-            uint32_t v[kN], ix[kN];
-#pragma unroll
-            for (int k = 0; k < kN; ++k) ix[k] = 4u * (g + uint32_t(k / 4) * nthreads) + uint32_t(k % 4);
-            run_n<kN, kLds, kMode, kList, kD, kCtr>(im, t, o, hot_lane, gslot, hot0, sa, da, pa, ra, other, v, sa, ix,
-                                                    oq_lds);
-#pragma unroll
-            for (int k = 0; k < kG; ++k) vw[k] = v[4 * k] | (v[4 * k + 1] << 8) | (v[4 * k + 2] << 16) | (v[4 * k + 3] << 24);
-        };
-        auto store = [&](const uint32_t (&vw)[kG], uint32_t g) {
-            if (verdict) {
-#pragma unroll
-                for (int k = 0; k < kG; ++k)
-                    stnt(vw[k], const_cast<uint32_t*>(at(reinterpret_cast<const uint32_t*>(verdict),
-                                                         g + uint32_t(k) * nthreads)));
-            }
-        };
-        (void)compute;
-        (void)store;
-        auto step = [&](const Buf& b, uint32_t g) {
-            constexpr int kN = 4 * kG;
-            uint32_t sa[kN], da[kN], pa[kN], ra[kN];
-            bool other = false;
-#pragma unroll
-            for (int k = 0; k < kG; ++k) {
-                sa[4 * k + 0] = b.s[k].x; sa[4 * k + 1] = b.s[k].y; sa[4 * k + 2] = b.s[k].z; sa[4 * k + 3] = b.s[k].w;
-                da[4 * k + 0] = b.d[k].x; da[4 * k + 1] = b.d[k].y; da[4 * k + 2] = b.d[k].z; da[4 * k + 3] = b.d[k].w;
-                pa[4 * k + 0] = b.dp[k].x & 0xFFFFu; pa[4 * k + 1] = b.dp[k].x >> 16;
-                pa[4 * k + 2] = b.dp[k].y & 0xFFFFu; pa[4 * k + 3] = b.dp[k].y >> 16;
-                const uint32_t pr = b.pr[k];
-                ra[4 * k + 0] = pr & 0xFFu; ra[4 * k + 1] = (pr >> 8) & 0xFFu;
-                ra[4 * k + 2] = (pr >> 16) & 0xFFu; ra[4 * k + 3] = pr >> 24;
-                // some protocol byte > 2 (SWAR: bit 7 of each byte of x + 125,
-                // computed without inter-byte carries)
-                other |= ((pr | ((pr & 0x7F7F7F7Fu) + 0x7D7D7D7Du)) & 0x80808080u) != 0u;
-            }
-            uint32_t v[kN], ix[kN];
-#pragma unroll
-            for (int k = 0; k < kN; ++k) ix[k] = 4u * (g + uint32_t(k / 4) * nthreads) + uint32_t(k % 4);
-            if constexpr (CLS_ABLATE & 32) {                    // diagnostics: the stream kernel's mix, no run_n
-#pragma unroll
-                for (int k = 0; k < kN; ++k) v[k] = (sa[k] ^ da[k] ^ pa[k] ^ ra[k] ^ uint32_t(other)) & 3u;
-            } else {
-                run_n<kN, kLds, kMode, kList, kD, kCtr>(im, t, o, hot_lane, gslot, hot0, sa, da, pa, ra, other, v, sa,
-                                                        ix, oq_lds);
-            }
-            if constexpr (kCtr == 2) {                           // slot mode: 4 result words per lane
-#pragma unroll
-                for (int k = 0; k < kG; ++k)
-                    reinterpret_cast<uint4*>(verdict)[g + uint32_t(k) * nthreads] =
-                        make_uint4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
-            } else if (verdict) {
-#pragma unroll
-                for (int k = 0; k < kG; ++k)
-                    stnt(v[4 * k] | (v[4 * k + 1] << 8) | (v[4 * k + 2] << 16) | (v[4 * k + 3] << 24),
-                         const_cast<uint32_t*>(at(reinterpret_cast<const uint32_t*>(verdict),
-                                                  g + uint32_t(k) * nthreads)));
-            }
-        };
-        // Full steps over groups [0, nfull) (CLS_PREFETCH above).
-#if CLS_PREFETCH == 3
-        if constexpr (kCtr != 2) {
-            // The next step's loads in flight during this step's lookups, in
-            // an order the vmcnt counter can serve: with a store and loads
-            // both pending the compiler can only wait for vmcnt(0), so a step
-            // first waits for its own loads (issued one step earlier, with
-            // the store before them), then stores the previous step's
-            // verdicts, then issues the next step's loads, then looks up --
-            // the scheduling barriers keep the loads from being hoisted above
-            // that wait.
-            if (nfull) {
-                Buf a, b;
-                uint32_t vw[kG];
-                auto pin = [&](const Buf& c) {
-#pragma unroll
-                    for (int k = 0; k < kG; ++k)
-                        asm volatile("" :: "v"(c.s[k].x), "v"(c.s[k].y), "v"(c.s[k].z), "v"(c.s[k].w),
-                                     "v"(c.d[k].x), "v"(c.d[k].y), "v"(c.d[k].z), "v"(c.d[k].w),
-                                     "v"(c.dp[k].x), "v"(c.dp[k].y), "v"(c.pr[k]));
-                };
-                auto turn = [&](Buf& cur, Buf& nxt, uint32_t g, bool st) {
-                    pin(cur);
-                    __builtin_amdgcn_sched_barrier(0);
-                    if (st) store(vw, g - span);
-                    load(nxt, g + span, true);
-                    __builtin_amdgcn_sched_barrier(0);
-                    compute(cur, g, vw);
-                };
-                uint32_t g = tid;
-                load(a, g, true);
-                turn(a, b, g, false);
-                g += span;
-                while (g < nfull) {
-                    turn(b, a, g, true);
-                    g += span;
-                    if (g >= nfull) break;
-                    turn(a, b, g, true);
-                    g += span;
-                }
-                store(vw, g - span);
-            }
-        } else {
-            for (uint32_t g = tid; g < nfull; g += span) {
-                Buf a;
-                load(a, g, true);
-                step(a, g);
-            }
+        // Whole grid steps first (uniform trip count), plain load and use: the
+        // CU's 16 waves overlap one another's loads and lookups.  (Register
+        // prefetch one or two steps ahead measured slower, 0.566 / 0.583
+        // against 0.559 ms, profiles/r02s4_prefetch_depth_ab_config3.txt: the
+        // buffers' registers cost more than the overlap buys.)  The loads are
+        // issued src, dst, dport, proto, as the stream kernel does (the
+        // compiler otherwise issues proto first, for the protocol test): 0.551
+        // against 0.558 ms, profiles/r03z_ab_load_order_config3.txt.  The
+        // protocol stream is a cached load, the others non-temporal
+        // (tools/nt_sweep.hip: the fastest of the 32 combinations).
+        const uint32_t nfull = nsteps / nthreads * nthreads;
+        for (uint32_t g = tid; g < nfull; g += nthreads) {
+            const uint4 s4 = ldnt(at(S, g));
+            __builtin_amdgcn_sched_barrier(0);
+            const uint4 d4 = ldnt(at(D, g));
+            __builtin_amdgcn_sched_barrier(0);
+            const uint2 p2 = ldnt(at(DP, g));
+            __builtin_amdgcn_sched_barrier(0);
+            const uint32_t pr = *at(PR, g);
+            __builtin_amdgcn_sched_barrier(0);
+            step(s4, d4, p2, pr, g);
         }
-#elif CLS_PREFETCH == 2
-        // two steps of loads in flight: three buffers in turn
-        if (nfull) {
-            Buf a, b, c;
-            uint32_t g = tid;
-            load(a, g, true);
-            load(b, g + span, true);
-            while (g < nfull) {
-                load(c, g + 2u * span, true);
-                step(a, g);
-                g += span;
-                if (g >= nfull) break;
-                load(a, g + 2u * span, true);
-                step(b, g);
-                g += span;
-                if (g >= nfull) break;
-                load(b, g + 2u * span, true);
-                step(c, g);
-                g += span;
-            }
-        }
-#elif CLS_PREFETCH
-        if (nfull) {
-            Buf a, b;
-            uint32_t g = tid;
-            load(a, g, true);
-            while (g < nfull) {
-                load(b, g + span, g + span < nfull);
-                step(a, g);
-                g += span;
-                if (g >= nfull) break;
-                load(a, g + span, g + span < nfull);
-                step(b, g);
-                g += span;
-            }
-        }
-#else
-        for (uint32_t g = tid; g < nfull; g += span) {
-            Buf a;
-            load(a, g, true);
-            step(a, g);
-        }
-#endif
         // leftover groups one at a time
         for (uint32_t gi = nfull + tid; gi < nsteps; gi += nthreads) {
             const uint4 s4 = ldnt(at(S, gi)), d4 = ldnt(at(D, gi));
@@ -1031,7 +724,6 @@ __global__ __launch_bounds__(kClsBlock) void classify4_cls(Cls4Dev t, Cls4Dev o,
     if constexpr (!kLds) {
         if (hot0) atomicAdd(&gslot[0], (unsigned long long)hot0);
     }
-    if constexpr (CLS_ABLATE & 64) return;
     if constexpr (kLds) flush_lds<kCtr>(t, smem);
     queue_end(t, oq_lds);
 }
@@ -1204,7 +896,6 @@ __global__ __launch_bounds__(kClsBlock) void classify16_cls(Cls4Dev t, Cls4Dev o
     // the registers of an IPv4 one, and the kernel must stay within 128
     // VGPRs (1024-thread workgroups) without scratch.  The CU's 16 waves
     // overlap one another's loads and lookups (no prefetch buffer).
-#if CLS_COAL16
     // Wave-contiguous packets: a wave's step covers 256 consecutive packets
     // and lane l takes packets base + 64k + l (k = 0..3), so each 16-B
     // address load instruction reads 1 KiB contiguous per wave (the
@@ -1225,13 +916,8 @@ __global__ __launch_bounds__(kClsBlock) void classify16_cls(Cls4Dev t, Cls4Dev o
         uint32_t dp[4], pr[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            if constexpr (CLS_NT16_SMALL) {
-                dp[k] = __builtin_nontemporal_load(p.dport + base + 64u * k);
-                pr[k] = __builtin_nontemporal_load(p.proto + base + 64u * k);
-            } else {
-                dp[k] = p.dport[base + 64u * k];
-                pr[k] = p.proto[base + 64u * k];
-            }
+            dp[k] = __builtin_nontemporal_load(p.dport + base + 64u * k);
+            pr[k] = __builtin_nontemporal_load(p.proto + base + 64u * k);
         }
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
@@ -1248,36 +934,6 @@ __global__ __launch_bounds__(kClsBlock) void classify16_cls(Cls4Dev t, Cls4Dev o
             }
         }
     }
-#else
-    static_assert(kCtr != 2, "slot mode (connection batches) needs the wave-contiguous order");
-    const uint32_t nsteps = p.vec ? uint32_t(p.n / 4u) : 0u;
-    const uint2* DP = reinterpret_cast<const uint2*>(p.dport);
-    const uint32_t* PR = reinterpret_cast<const uint32_t*>(p.proto);
-    for (uint32_t g = tid; g < nsteps; g += nthreads) {
-        uint4 s[4], d[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            s[k] = ldnt(at(p.src, 4u * g + k));
-            d[k] = ldnt(at(p.dst, 4u * g + k));
-        }
-        const uint2 dp = ldnt(at(DP, g));
-        const uint32_t pr = ldnt(at(PR, g));
-        uint32_t v[4];
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const uint4 s2[2] = {s[2 * h], s[2 * h + 1]}, d2[2] = {d[2 * h], d[2 * h + 1]};
-            const uint32_t w = h ? dp.y : dp.x, r = pr >> (16 * h);
-            uint32_t pa[2] = {w & 0xFFFFu, w >> 16}, ra[2] = {r & 0xFFu, (r >> 8) & 0xFFu}, v2[2];
-            const uint32_t ix[2] = {4u * g + 2u * h, 4u * g + 2u * h + 1u};
-            classify(s2, d2, pa, ra, (ra[0] | ra[1]) > 2u, v2, ix);
-            v[2 * h] = v2[0];
-            v[2 * h + 1] = v2[1];
-        }
-        if (verdict)
-            stnt(v[0] | (v[1] << 8) | (v[2] << 16) | (v[3] << 24),
-                 const_cast<uint32_t*>(at(reinterpret_cast<const uint32_t*>(verdict), g)));
-    }
-#endif
     for (uint32_t i = nsteps * 4u + tid; i < uint32_t(p.n); i += nthreads) {
         const uint4 s1[1] = {ldnt(at(p.src, i))}, d1[1] = {ldnt(at(p.dst, i))};
         uint32_t v[1];
@@ -1320,7 +976,7 @@ static void launch_cls(const Cls4Dev& t, const Pkts4& p, uint8_t* verdict, unsig
         }
     }
     if constexpr (kLds && kVec && (kList == 3 || kList == 4)) {
-        switch (t.sub4 ? -1 : int(t.bv_steps)) {
+        switch (int(t.bv_steps)) {
         case 0: launch_d<kLds, kVec, kMode, kList, 0>(t, p, verdict, gslot, cfg); return;
         case 1: launch_d<kLds, kVec, kMode, kList, 1>(t, p, verdict, gslot, cfg); return;
         case 2: launch_d<kLds, kVec, kMode, kList, 2>(t, p, verdict, gslot, cfg); return;
@@ -1334,26 +990,17 @@ static void launch_cls(const Cls4Dev& t, const Pkts4& p, uint8_t* verdict, unsig
 }
 
 // source lookup variant: 0 interval search, 1 hash LPM, 2 hash LPM with one
-// length, 3 source trie (kMode 4), 4 inline hash cells (kMode 6)
+// length, 3 source trie (kMode 4)
 static inline int src_variant(const Cls4Dev& t) {
-    return t.mode == 6 ? 4 : t.mode == 4 ? 3 : t.mode != 1 ? 0 : t.n_hash == 1 ? 2 : 1;
+    return t.mode == 4 ? 3 : t.mode != 1 ? 0 : t.n_hash == 1 ? 2 : 1;
 }
 
-// Whether the dispatchers below have a kernel for this image (the engine
-// refuses the others before they get here; the launchers check again, so a
-// combination without a case is an error, never another variant's kernel
-// reading the image wrongly).  rep16: the 16-byte core (modes 0-4, 6; mode 3
-// = rows from the host hashes).
+// Whether the dispatchers below have a kernel for this image (kernels.hpp
+// cls_kernel_exists: the engine refuses the others at put time, the
+// launchers check again, so a combination without a case is an error, never
+// another variant's kernel reading the image wrongly).
 static inline bool cls_dispatchable(const Cls4Dev& t, bool lds, bool rep16) {
-    const uint32_t lm = t.list_mode;
-    if (lm > 6 || (lm >= 5 && !lds)) return false;
-    switch (t.mode) {
-    case 0: case 1: return true;
-    case 3: return rep16;
-    case 4: return lds && lm >= 3;
-    case 6: return lds && (lm == 3 || lm == 4);
-    default: return false;
-    }
+    return cls_kernel_exists(t.mode, t.list_mode, lds, rep16);
 }
 
 template <bool kLds, bool kVec>
@@ -1361,19 +1008,14 @@ static void dispatch_cls(const Cls4Dev& t, const Pkts4& p, uint8_t* verdict, uns
                          const LaunchCfg& cfg) {
     const int src = src_variant(t);
     if constexpr (kLds) {
-        // the source trie (sublist modes), inline hash cells (sublist modes,
-        // LDS cells) and the wide cells (LDS-resident images only)
-        if (src >= 3 || t.list_mode >= 5) {
+        // the source trie (sublist modes) and the wide cells (LDS-resident
+        // images only)
+        if (src == 3 || t.list_mode >= 5) {
 #define CLS_TW_CASES(L)                                                                       \
     case 4 * L + 0: launch_cls<kLds, kVec, 0, L>(t, p, verdict, gslot, cfg); return;          \
     case 4 * L + 1: launch_cls<kLds, kVec, 1, L>(t, p, verdict, gslot, cfg); return;          \
     case 4 * L + 2: launch_cls<kLds, kVec, 2, L>(t, p, verdict, gslot, cfg); return;          \
     case 4 * L + 3: launch_cls<kLds, kVec, 4, L>(t, p, verdict, gslot, cfg); return;
-            if (src == 4) {
-                if (t.list_mode == 3) launch_cls<kLds, kVec, 6, 3>(t, p, verdict, gslot, cfg);
-                else if (t.list_mode == 4) launch_cls<kLds, kVec, 6, 4>(t, p, verdict, gslot, cfg);
-                return;
-            }
             switch (src + 4 * int(t.list_mode)) {
                 case 4 * 3 + 3: launch_cls<kLds, kVec, 4, 3>(t, p, verdict, gslot, cfg); return;
                 case 4 * 4 + 3: launch_cls<kLds, kVec, 4, 4>(t, p, verdict, gslot, cfg); return;
@@ -1419,7 +1061,7 @@ static void launch16_cls(const Cls4Dev& t, const Fe16& fe, const Pkts16& p, uint
         }
     }
     if constexpr (kLds && (kList == 3 || kList == 4)) {
-        switch (t.sub4 ? -1 : int(t.bv_steps)) {
+        switch (int(t.bv_steps)) {
         case 0: launch16_d<kLds, kMode, kList, 0, false, kFe>(t, fe, p, verdict, gslot, cfg); return;
         case 1: launch16_d<kLds, kMode, kList, 1, false, kFe>(t, fe, p, verdict, gslot, cfg); return;
         case 2: launch16_d<kLds, kMode, kList, 2, false, kFe>(t, fe, p, verdict, gslot, cfg); return;
@@ -1455,11 +1097,6 @@ static void dispatch16(const Cls4Dev& t, const Fe16& fe, const Pkts16& p, uint8_
     }
     const int src = src_variant(t);
     if constexpr (kLds) {
-        if (src == 4) {                               // inline hash cells over reps
-            if (t.list_mode == 3) launch16_cls<kLds, 6, 3, 0>(t, fe, p, verdict, gslot, cfg);
-            else if (t.list_mode == 4) launch16_cls<kLds, 6, 4, 0>(t, fe, p, verdict, gslot, cfg);
-            return;
-        }
         // the source trie over reps (sublist modes) and the wide cells (LDS-resident images only)
         if (src == 3 || t.list_mode >= 5) {
 #define CLS16_TW_CASES(L)                                                                     \
@@ -1501,11 +1138,6 @@ static void dispatch_slots4(const Cls4Dev& t, const Pkts4& p, uint32_t* out, con
     const int src = src_variant(t);
     if constexpr (kLds) {
         auto al = [](const void* q, uintptr_t a) { return (reinterpret_cast<uintptr_t>(q) & (a - 1)) == 0; };
-        if (src == 4) {                               // inline hash cells
-            if (t.list_mode == 3) launch_d<true, false, 6, 3, -1, 2>(t, p, o, nullptr, cfg);
-            else if (t.list_mode == 4) launch_d<true, false, 6, 4, -1, 2>(t, p, o, nullptr, cfg);
-            return;
-        }
         if (src == 3 || t.list_mode >= 5) {           // source trie / wide cells
 #define CLS_SLOTTW_CASES(L)                                                                        \
     case 4 * L + 0: launch_d<true, false, 0, L, -1, 2>(t, p, o, nullptr, cfg); return;             \
@@ -1571,11 +1203,6 @@ static void dispatch_slots16(const Cls4Dev& t, const Fe16& fe, const Pkts16& p, 
     }
     const int src = src_variant(t);
     if constexpr (kLds) {
-        if (src == 4) {                               // inline hash cells over reps
-            if (t.list_mode == 3) launch16_d<kLds, 6, 3, -1, false, 0, 2>(t, fe, p, o, nullptr, cfg);
-            else if (t.list_mode == 4) launch16_d<kLds, 6, 4, -1, false, 0, 2>(t, fe, p, o, nullptr, cfg);
-            return;
-        }
         if (src == 3 || t.list_mode >= 5) {
 #define CLS16_SLOTTW_CASES(L)                                                                      \
     case 4 * L + 0: launch16_d<kLds, 0, L, -1, false, 0, 2>(t, fe, p, o, nullptr, cfg); return;    \
