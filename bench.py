@@ -216,13 +216,15 @@ def main():
     # torch's current stream, so the step events and the all-reduce's wait
     # event bracket the classify itself.
     main = torch.cuda.Stream(device=dev)
+    sev_pool = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
 
     def step(i, timing):
         b = i % nbuf
         if timing:
             # step boundaries: one event per step (step i = boundary i to i + 1),
-            # each event record costs the stream a few microseconds
-            s0 = torch.cuda.Event(enable_timing=True)
+            # each event record costs the stream a few microseconds; the events
+            # are created before the timed loop (no allocation inside it)
+            s0 = sev_pool[len(sev)]
             s0.record(main)
             sev.append(s0)
         if reduced[b] is not None:
@@ -273,7 +275,7 @@ def main():
     for _ in range(args.steps):
         step(i, True)
         i += 1
-    last = torch.cuda.Event(enable_timing=True)
+    last = sev_pool[len(sev)]
     last.record(main)
     sev.append(last)
     torch.cuda.synchronize()

@@ -273,6 +273,14 @@ typedef struct cls_conn_soa {
     const uint32_t* src_if;    /* interface ids (cls_if_id) */
     const uint32_t* dst_if;
 } cls_conn_soa;
+
+/* The connection path's floor: the average time of a kernel that reads the
+ * 22 bytes of every IPv4 connection of a device batch (src, dst, src_if,
+ * dst_if, sport, dport, proto) and writes one byte, without evaluating
+ * anything, over `reps` launches (whole groups of 4 connections; 16-B aligned
+ * src / dst / src_if / dst_if, 8-B ports, 4-B proto and out). */
+int cls_stream_floor_conn(cls_engine* e, const cls_conn_soa* conns, uint64_t n, uint8_t* out,
+                          uint32_t reps, float* ms, void* stream);
 int cls_connect_batch(cls_engine* e, const cls_conn_soa* conns, uint64_t n,
                       uint8_t* conn_verdict_out, uint32_t flags, void* stream);
 

@@ -81,6 +81,15 @@ def main():
         eng.connect_batch(*dargs, count=True)
         dt_c = per_call(True)
         counted = {"value": round(n / dt_c / 1e6, 3), "unit": "Mconn/s", "ms_per_batch": round(dt_c * 1e3, 3)}
+    # roofline: the 22 algorithmic bytes of an IPv4 connection (src, dst,
+    # src_if, dst_if 4 B each, sport, dport 2 B, proto 1 B read; the verdict
+    # byte written) per HBM-resident batch, beside the stream floor of the
+    # same arrays (cls_stream_floor_conn: the same reads and write, no
+    # evaluation)
+    floor = eng.stream_floor_conn(*dargs, reps=20)
+    roof = {"bound": "hbm", "bytes_per_connection": 22, "peak": 8000.0, "unit": "GB/s",
+            "achieved": round(22 * n / dev_dt / 1e9, 1), "frac": round(22 * n / dev_dt / 8e12, 4),
+            "stream_floor_ms": round(floor, 4), "frac_of_stream_floor": round(floor / (dev_dt * 1e3), 4)}
     k = a.cpu_sample
     t1 = time.perf_counter()
     want, _ = oracle_connections(bind, by_name, ifs, si[:k], di[:k], {f: v[:k] for f, v in tr.items()}, 4)
@@ -92,7 +101,8 @@ def main():
         "pcie_included": True, "global_rules": len(by_name["global"]), "local_acls": a.locals,
         "other_proto": bool(a.other_proto), "hbm_resident_counted": counted,
         "hbm_resident": {"value": round(n / dev_dt / 1e6, 3), "unit": "Mconn/s",
-                         "ms_per_batch": round(dev_dt * 1e3, 3)},
+                         "ms_per_batch": round(dev_dt * 1e3, 4)},
+        "roofline": roof,
         "linear_scan": {"value": round(n / res["linear"][0] / 1e6, 3), "unit": "Mconn/s",
                         "ms_per_batch": round(res["linear"][0] * 1e3, 3)},
         "verdicts": np.bincount(out, minlength=4).tolist(),

@@ -15,7 +15,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # CONTIVCLS_LIB: diagnostics only (A/B timing of kernel build variants)
 LIB_PATH = os.environ.get("CONTIVCLS_LIB") or os.path.join(_HERE, "libcontivcls.so")
 
-SOURCES = ("kernels.hip", "kernels_dev.hpp", "k4_ldsv.hip", "k4_rest.hip", "k16.hip", "kernels.hpp", "compile.cpp",
+SOURCES = ("kernels.hip", "kernels_dev.hpp", "k4_ldsv.hip", "k4_rest.hip", "k4_pair.hip", "k16.hip", "kernels.hpp", "compile.cpp",
            "compile.hpp", "engine.cpp", "goparse.hpp")
 
 
@@ -46,7 +46,7 @@ SYMBOLS = ["cls_abi_version", "cls_engine_create", "cls_engine_destroy", "cls_la
            "cls_last_kernel_ms", "cls_kernel_times", "cls_kernel_times_reset", "cls_acl_put", "cls_acl_del", "cls_acl_table", "cls_acl_counts",
            "cls_if_id",
            "cls_if_acls", "cls_connect_batch", "cls_gen_traffic_v4", "cls_compile_v4", "cls_image_kernel",
-           "cls_compile_v16", "cls_gen_traffic_v16", "cls_stream_floor", "cls_stream_floor_shapes", "cls_conn_bitmap_eval", "cls_conn_counters",
+           "cls_compile_v16", "cls_gen_traffic_v16", "cls_stream_floor", "cls_stream_floor_shapes", "cls_stream_floor_conn", "cls_conn_bitmap_eval", "cls_conn_counters",
            "cls_acl_stats"]
 
 
@@ -174,6 +174,7 @@ def bind(path: str, strict: bool = True):
         "cls_conn_bitmap_eval": (C.c_int, [C.POINTER(ClsRule), u32, vp, vp, vp, vp, u64, vp, vp]),
         "cls_stream_floor_shapes": (C.c_int, [vp, C.POINTER(PktSoa), u64, vp, u32, C.POINTER(C.c_float), u32,
                                               C.POINTER(C.c_uint32), vp]),
+        "cls_stream_floor_conn": (C.c_int, [vp, C.POINTER(ConnSoa), u64, vp, u32, C.POINTER(C.c_float), vp]),
         "cls_acl_put": (C.c_int, [vp, C.c_char_p, C.POINTER(ClsRule), u32,
                                   C.POINTER(C.c_char_p), u32, C.POINTER(C.c_char_p), u32]),
         "cls_acl_del": (C.c_int, [vp, C.c_char_p]),

@@ -489,6 +489,7 @@ constexpr uint32_t kConnClsWork = 2048;            // ... when touches x rules >
 constexpr uint32_t kConnClsDevRules = 2048;        // ... when it has this many rules (device batch)
 constexpr uint32_t kConnBmMinRules = 8;            // linear IPv4 ACLs given the bitmap form (conn_bitmap4) ...
 constexpr size_t kConnBmMaxWords = 12288;          // ... when their tables take at most 48 KiB
+constexpr size_t kConnJobsLds = 16 * kConnJobBytes; // connect_kernel: the 16 waves' job areas (LDS)
 
 static bool aligned(const void* p, size_t a) { return (reinterpret_cast<uintptr_t>(p) % a) == 0; }
 
@@ -1252,6 +1253,7 @@ int cls_connect_batch(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t*
         if (t == e->tables.end()) return -1;
         const Table& T = *t->second;
         ConnDesc d{};
+        d.pre_blk = -1;
         d.n = uint32_t(k16 ? T.conn16.size() : T.conn4.size());
         d.n_rules = T.n_rules;
         d.ctr_off = n_ctr;
@@ -1334,13 +1336,17 @@ int cls_connect_batch(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t*
             if (want) big.push_back(j);
         }
     }
+    // The result words: block b (the ACL big[b]) at pre + 2 b stride, the SYN
+    // tuple's words first, the SYN-ACK tuple's at + stride (a multiple of 4,
+    // so both halves stay 16-B aligned for the pair launch's stores).
+    const uint64_t stride = (n + 3) & ~uint64_t(3);
     if (!big.empty()) {
         if (n > kClsChunk) return fail(e, CLS_E_INVAL, "connection batch above 2^30 with classifier ACLs");
-        HIPC(e, e->s_pre.ensure(big.size() * 2 * n * 4));
+        HIPC(e, e->s_pre.ensure(big.size() * 2 * stride * 4));
         for (size_t b = 0; b < big.size(); ++b) {
             Table& t = *dtab[big[b]];
-            uint32_t* pre = e->s_pre.as<uint32_t>() + b * 2 * n;
-            desc[big[b]].pre = pre;
+            uint32_t* pre = e->s_pre.as<uint32_t>() + b * 2 * stride;
+            desc[big[b]].pre_blk = int32_t(b);
             for (IfAcls& f : ifs) {                        // the block, also per interface (prefetch)
                 if (f.in == int32_t(big[b])) f.in_pre = int32_t(b);
                 if (f.out == int32_t(big[b])) f.out_pre = int32_t(b);
@@ -1350,12 +1356,29 @@ int cls_connect_batch(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t*
             if (!k16) {
                 desc[big[b]].slot_rule = t.d_slot_rule.as<uint32_t>();
                 Cls4Dev cd = table_dev(t);
-                cfg.other = cls4_dev(t.oimg, t.d_oimg, DevBuf(), 0, t.n_rules);
-                cfg.grid = cls_grid(e, true, t.lds_resident, t.img.lds_bytes, n);
                 const uint32_t *s4 = static_cast<const uint32_t*>(src), *d4 = static_cast<const uint32_t*>(dst);
                 const Pkts4 syn = framed(t.img, Pkts4{s4, d4, dp, pr, n}), ack = framed(t.img, Pkts4{d4, s4, sp, pr, n});
-                HIPC(e, launch_classify4_slots(cd, syn, pre, t.lds_resident, cfg));
-                HIPC(e, launch_classify4_slots(cd, ack, pre + n, t.lds_resident, cfg));
+                // Both tuples in one launch when the image is LDS-resident and
+                // the arrays allow 16-B loads; the OTHER image beside the main
+                // one when both fit (no slot counters in this mode)
+                const bool pair = t.lds_resident && aligned(s4, 16) && aligned(d4, 16) && aligned(dp, 8) &&
+                                  aligned(sp, 8) && aligned(pr, 4) && !std::getenv("CONTIVCLS_CONN_NO_PAIR");
+                if (pair) {
+                    uint32_t o_at = (t.img.img_bytes + 15u) & ~15u;
+                    if (o_at + t.oimg.img_bytes > uint32_t(max_lds_bytes())) o_at = 0;
+                    Cls4Dev od = cls4_dev(t.oimg, t.d_oimg, DevBuf(), 0, t.n_rules);
+                    if (o_at) {
+                        od.off_bounds += o_at; od.off_iclass += o_at; od.off_cells += o_at;
+                        od.off_lists += o_at; od.off_tmpl += o_at;
+                    }
+                    cfg.grid = cls_grid(e, true, true, o_at ? o_at + t.oimg.img_bytes : t.img.img_bytes, n);
+                    HIPC(e, launch_classify4_pair(cd, od, o_at, syn, sp, pre, stride, cfg));
+                } else {
+                    cfg.other = cls4_dev(t.oimg, t.d_oimg, DevBuf(), 0, t.n_rules);
+                    cfg.grid = cls_grid(e, true, t.lds_resident, t.img.lds_bytes, n);
+                    HIPC(e, launch_classify4_slots(cd, syn, pre, t.lds_resident, cfg));
+                    HIPC(e, launch_classify4_slots(cd, ack, pre + stride, t.lds_resident, cfg));
+                }
             } else {
                 auto& q = t.p16;
                 desc[big[b]].slot_rule = q.d_slot_rule.as<uint32_t>();
@@ -1371,7 +1394,7 @@ int cls_connect_batch(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t*
                     std::swap(ack.src, ack.dst);
                 }
                 HIPC(e, launch_classify16_slots(cd, fe, syn, pre, q.lds_resident, cfg));
-                HIPC(e, launch_classify16_slots(cd, fe, ack, pre + n, q.lds_resident, cfg));
+                HIPC(e, launch_classify16_slots(cd, fe, ack, pre + stride, q.lds_resident, cfg));
             }
         }
     }
@@ -1381,7 +1404,7 @@ int cls_connect_batch(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t*
     const size_t lds_max0 = size_t(max_lds_bytes());
     for (size_t j = 0; j < desc.size(); ++j) {
         desc[j].bm_off = 0xFFFFFFFFu;
-        if (desc[j].pre) {
+        if (desc[j].pre_blk >= 0) {
             desc[j].n = 0;
             continue;
         }
@@ -1398,12 +1421,12 @@ int cls_connect_batch(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t*
     if (!k16 && n && !(flags & CLS_F_FORCE_LINEAR) && !(bme && std::atoi(bme) == 0)) {
         // the LDS counters take their share only when they can be LDS counters
         // at all (otherwise they are global, cmode 2); no subtraction wraps
-        const size_t ctr_b = count ? size_t(n_ctr) * 4 : 0, reserve = std::min<size_t>(lds_max0 / 8, 8192);
+        const size_t ctr_b = count ? size_t(n_ctr) * 4 : 0, reserve = std::min<size_t>(lds_max0 / 8, 8192) + kConnJobsLds;
         const size_t ctr_lds = ctr_b + reserve <= lds_max0 ? ctr_b : 0;
         const size_t cap = lds_max0 - reserve - ctr_lds;
         std::vector<size_t> order;
         for (size_t j = 0; j < desc.size(); ++j)
-            if (!desc[j].pre && desc[j].n >= kConnBmMinRules) order.push_back(j);
+            if (desc[j].pre_blk < 0 && desc[j].n >= kConnBmMinRules) order.push_back(j);
         std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) { return desc[a].n > desc[b].n; });
         std::vector<uint32_t> words;
         for (size_t j : order) {
@@ -1433,10 +1456,11 @@ int cls_connect_batch(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t*
     // LDS: the rule pool first (every evaluation step reads it), then the u32
     // counters if they fit beside it; otherwise global-memory variants
     // (CONTIVCLS_CONN_NO_LDS, tests: bit 0 rules from global memory, bit 1
-    // global counters, bit 2 descriptor / interface tables from global memory)
+    // global counters, bit 2 descriptor / interface tables from global memory).
+    // The waves' job areas (kConnJobsLds) always go last.
     const char* nl = std::getenv("CONTIVCLS_CONN_NO_LDS");
     const int no_lds = nl ? std::atoi(nl) : 0;
-    const size_t lds_max = size_t(max_lds_bytes());
+    const size_t lds_max = size_t(max_lds_bytes()) - kConnJobsLds;
     const bool lds_rules = n && !pool.empty() && pool.size() <= lds_max && !(no_lds & 1);
     const size_t lds_used = lds_rules ? pool.size() : 0;
     int cmode = 0;
@@ -1451,6 +1475,7 @@ int cls_connect_batch(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t*
     if (!pool.empty()) HIPC(e, hipMemcpyAsync(e->s_rules.p, pool.data(), pool.size(), hipMemcpyHostToDevice, s));
     a.desc = e->s_desc.as<ConnDesc>();
     a.pre = big.empty() ? nullptr : e->s_pre.as<uint32_t>();
+    a.pre_stride = stride;
     a.ifs = e->s_ifs.as<IfAcls>();
     a.rules = e->s_rules.p;
     std::vector<unsigned long long*> tctr;
@@ -1481,12 +1506,16 @@ int cls_connect_batch(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t*
     a.meta_lds = 0xFFFFFFFFu;
     // ... unless they would cost a workgroup per CU (the pool and counters
     // alone leave room for two)
-    auto per_cu_of = [&](size_t b) { return b ? std::max(1, std::min(2, int(lds_max / b))) : 2; };
+    auto per_cu_of = [&](size_t b) {
+        return std::max(1, std::min(2, int(size_t(max_lds_bytes()) / (((b + 15) & ~size_t(15)) + kConnJobsLds))));
+    };
     if (meta_at + meta <= lds_max && per_cu_of(meta_at + meta) == per_cu_of(lds) && !(no_lds & 4)) {
         a.meta_lds = uint32_t(meta_at);
         lds = meta_at + meta;
     }
-    const int per_cu = lds ? std::max(1, std::min(2, int(lds_max / lds))) : 2;
+    a.jobs_lds = uint32_t((lds + 15) & ~size_t(15));
+    lds = a.jobs_lds + kConnJobsLds;
+    const int per_cu = std::max(1, std::min(2, int(size_t(max_lds_bytes()) / lds)));
     const int grid = int(std::max<uint64_t>(1, std::min<uint64_t>(uint64_t(e->n_cu) * per_cu, (n + 1023) / 1024)));
     HIPC(e, launch_connect(a, k16, lds_rules, cmode, grid, lds, s));
     if (cmode && n)
@@ -1496,6 +1525,36 @@ int cls_connect_batch(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t*
     // descriptor, pool and counter buffers are engine scratch: finish before
     // they can be reused (and before the host vectors above go away)
     HIPC(e, hipStreamSynchronize(s));
+    return CLS_OK;
+}
+
+int cls_stream_floor_conn(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t* out, uint32_t reps,
+                          float* ms, void* stream) {
+    if (!e || !c || !out || !ms || c->pkt.af != CLS_AF_V4 || n < 4 || n > kClsChunk) return CLS_E_INVAL;
+    const cls_pkt_soa& pk = c->pkt;
+    if (!aligned(pk.src4, 16) || !aligned(pk.dst4, 16) || !aligned(c->src_if, 16) || !aligned(c->dst_if, 16) ||
+        !aligned(pk.sport, 8) || !aligned(pk.dport, 8) || !aligned(pk.proto, 4) || !aligned(out, 4))
+        return fail(e, CLS_E_INVAL, "cls_stream_floor_conn: device arrays must be 16/8/4-byte aligned");
+    std::lock_guard<std::mutex> g(e->mu);
+    HIPC(e, hipSetDevice(e->device));
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : e->stream;
+    ConnArgs a{};
+    a.src = pk.src4; a.dst = pk.dst4; a.src_if = c->src_if; a.dst_if = c->dst_if;
+    a.sport = pk.sport; a.dport = pk.dport; a.proto = pk.proto; a.out = out; a.n = n;
+    const int grid = int(std::min<uint64_t>(uint64_t(e->n_cu) * 2, (n / 4 + 1023) / 1024));
+    hipEvent_t t0, t1;
+    HIPC(e, hipEventCreate(&t0));
+    HIPC(e, hipEventCreate(&t1));
+    HIPC(e, launch_stream_conn(a, grid, s));          // warm
+    HIPC(e, hipEventRecord(t0, s));
+    for (uint32_t r = 0; r < std::max(1u, reps); ++r) HIPC(e, launch_stream_conn(a, grid, s));
+    HIPC(e, hipEventRecord(t1, s));
+    HIPC(e, hipEventSynchronize(t1));
+    float t = 0.f;
+    HIPC(e, hipEventElapsedTime(&t, t0, t1));
+    *ms = t / float(std::max(1u, reps));
+    (void)hipEventDestroy(t0);
+    (void)hipEventDestroy(t1);
     return CLS_OK;
 }
 

@@ -92,6 +92,23 @@ __global__ __launch_bounds__(kClsBlock) void stream16_kernel(Pkts16 p, uint8_t* 
     }
 }
 
+// The connection batch's HBM stream without the evaluation (the connection
+// path's floor, cls_stream_floor_conn): the 22 bytes of an IPv4 connection
+// (src, dst, src_if, dst_if: 16-B loads; sport, dport: 8-B; proto: 4-B) read
+// and its verdict byte written, 4 connections per lane.
+__global__ __launch_bounds__(1024) void stream_conn_kernel(const uint4* src, const uint4* dst, const uint4* sif,
+                                                           const uint4* dif, const uint2* sp, const uint2* dp,
+                                                           const uint32_t* pr, uint32_t* out, uint32_t nsteps) {
+    for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < nsteps; g += gridDim.x * blockDim.x) {
+        const uint4 a = ldnt(at(src, g)), b = ldnt(at(dst, g)), c = ldnt(at(sif, g)), d = ldnt(at(dif, g));
+        const uint2 e = ldnt(at(sp, g)), f = ldnt(at(dp, g));
+        const uint32_t p = ldnt(at(pr, g));
+        const uint32_t v = (a.x ^ a.y ^ a.z ^ a.w ^ b.x ^ b.y ^ b.z ^ b.w ^ c.x ^ c.y ^ c.z ^ c.w ^ d.x ^ d.y ^ d.z ^
+                            d.w ^ e.x ^ e.y ^ f.x ^ f.y ^ p) & 0x03030303u;
+        stnt(v, const_cast<uint32_t*>(at(reinterpret_cast<const uint32_t*>(out), g)));
+    }
+}
+
 constexpr uint32_t kOtherLds = 4096;   // finish launch: LDS histogram of the OTHER packets' rules
 
 // One launch at the end of a classify call (kernels.hpp FinishArgs).  Blocks
@@ -418,7 +435,7 @@ __device__ __forceinline__ ConnDesc conn_desc(const ConnArgs& a, uint32_t j) {
         const v4u x = *lds128_t(b), y = *lds128_t(b + 16u);
         ConnDesc d;
         d.rule_off = x.x; d.n = x.y; d.n_rules = x.z; d.ctr_off = x.w;
-        d.pre = reinterpret_cast<const uint32_t*>(uint64_t(y.x) | (uint64_t(y.y) << 32));
+        d.pre_blk = int32_t(y.x); d.pad = y.y;
         d.slot_rule = reinterpret_cast<const uint32_t*>(uint64_t(y.z) | (uint64_t(y.w) << 32));
         const v4u z = *lds128_t(b + 32u);
         d.bm_off = z.x; d.bm_sd = z.y; d.bm_tu = z.z; d.bm_w = z.w;
@@ -499,18 +516,29 @@ __device__ __forceinline__ uint32_t conn_bm(const ConnArgs& a, const ConnDesc& D
     return 0u;
 }
 
-// testConnection, one lane per connection: the evaluations in the
-// reference's order, each reading its descriptor (LDS) and then either the
-// classifier's slot word for this connection (and, counting, its slot's
-// rule) or scanning the ACL's rules.  (Loading the slot words of all four
-// possible evaluations up front, before the state machine knows which it
-// makes, measured slower: 185 vs 165 us per 4 Mi connections, 256 vs 176
-// counting -- the loads for skipped evaluations are not free.)
-// diagnostics builds only: 1 no evaluation, 2 descriptor read only, 4 no
-// bitmap evaluation (each returns PERMIT or REFLECT from a live input)
-#ifndef CONN_ABLATE
-#define CONN_ABLATE 0
-#endif
+// testConnection, one lane per connection, in two phases per iteration.
+//
+// 1. Evaluations.  A call on a large ACL reads the classifier's result word
+//    for this connection (classify4_pair / the slot launches); a call on a
+//    linear ACL is a *job*: the bitmap search (IPv4, conn_bm) or the rule
+//    scan.  The jobs of all four possible calls of the wave's 64 connections
+//    are packed into the wave's LDS job area and run 64 at a time, every
+//    lane on one job with its connection's fields fetched from the owning
+//    lane (ds_bpermute).  A lane-per-call loop would make the wave run the
+//    search once per call index in which any of its lanes has a job -- four
+//    passes per wave with ~0.6 jobs per connection -- where packing runs
+//    one.  Jobs are evaluated whether or not testConnection reaches the call
+//    (the call order needs the earlier results); only the calls it makes are
+//    counted.
+// 2. The state machine: testConnection's order and REFLECT short-cuts
+//    (aclengine_mock.go:394-471) over the four results: SYN through the
+//    source's inbound then the destination's outbound ACL, SYN-ACK through
+//    the destination's inbound then the source's outbound ACL.
+//
+// Counting (CLS_F_COUNT): the terminating rule of every call made on a
+// non-nil ACL -> the call's counter space (descriptor ctr_off + rule), in LDS
+// (u32, folded into the u64 counters at the end) or with wave-aggregated
+// global atomics.
 template <bool k16, bool kLdsRules, int kCount>
 __global__ __launch_bounds__(1024) void connect_kernel(ConnArgs a) {
     typedef typename ConnT<k16>::A A;
@@ -531,96 +559,145 @@ __global__ __launch_bounds__(1024) void connect_kernel(ConnArgs a) {
         for (uint32_t j = threadIdx.x; j < 4u * a.n_ifs; j += blockDim.x) *lctr_t(a.meta_lds + 4u * (nd + j)) = gi[j];
     }
     __syncthreads();
+    const uint32_t lane = __lane_id();
+    const uint64_t lt = (1ull << lane) - 1ull;
+    const uint32_t jobs = a.jobs_lds + (threadIdx.x >> 6) * kConnJobBytes, results = jobs + 1024u;
     const A* src = static_cast<const A*>(a.src);
     const A* dst = static_cast<const A*>(a.dst);
     const uint64_t nthreads = uint64_t(gridDim.x) * blockDim.x;
     const uint64_t n_iter = (a.n + nthreads - 1) / nthreads;    // uniform trip count (ballots below)
     for (uint64_t it = 0; it < n_iter; ++it) {
         const uint64_t i = it * nthreads + uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-        uint32_t key[4] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
-        if (i < a.n) {
-            const uint32_t si = a.src_if[i], dj = a.dst_if[i];
-            uint32_t v = 3u;                                    // unknown interface id: Failure
-            if (si < a.n_ifs && dj < a.n_ifs) {
-                const IfAcls S = conn_if(a, si), Dif = conn_if(a, dj);
-                const bool same = si == dj;
-                const A sa = src[i], da = dst[i];
-                const bool s4 = mapped4(sa), d4 = mapped4(da);
-                const uint32_t sp = a.sport[i], dp = a.dport[i], pr = a.proto[i];
-                const uint32_t p = pr <= 2u ? pr : 3u;
-                // the four calls in testConnection's order: SYN through the
-                // source's inbound and the destination's outbound ACL, SYN-ACK
-                // through the destination's inbound and the source's outbound
-                const int32_t di[4] = {S.in, Dif.out, Dif.in, S.out};
-                // the classifier slot words of every call on a large ACL, loaded
-                // now, together: a call testConnection then makes does not wait
-                // for its own global round trip (a call without them reads a
-                // valid dummy word; unconditional -- the same loads under a
-                // uniform "any large ACL" branch measured 19 % slower)
-                const int32_t bi[4] = {S.in_pre, Dif.out_pre, Dif.in_pre, S.out_pre};
-                uint32_t pw[4];
+        const bool live = i < a.n;
+        const uint64_t ic = live ? i : 0;                       // loads stay in bounds
+        const uint32_t si = a.src_if[ic], dj = a.dst_if[ic];
+        const bool ok = live && si < a.n_ifs && dj < a.n_ifs;   // unknown interface id: Failure
+        const IfAcls S = ok ? conn_if(a, si) : IfAcls{-1, -1, -1, -1};
+        const IfAcls Dif = ok ? conn_if(a, dj) : IfAcls{-1, -1, -1, -1};
+        const A sa = src[ic], da = dst[ic];
+        const uint32_t sp = a.sport[ic], dp = a.dport[ic], pr = a.proto[ic];
+        const uint32_t p = pr <= 2u ? pr : 3u;
+        // the four calls in testConnection's order
+        const int32_t di[4] = {S.in, Dif.out, Dif.in, S.out};
+        const int32_t bi[4] = {S.in_pre, Dif.out_pre, Dif.in_pre, S.out_pre};
+        // result words of the calls on large ACLs, loaded together (a call
+        // without one reads a valid dummy word: unconditional loads measured
+        // faster than the same loads under a branch)
+        uint32_t w[4];
 #pragma unroll
-                for (int k = 0; k < 4; ++k)
-                    pw[k] = *(bi[k] >= 0 ? a.pre + (2ull * uint32_t(bi[k]) + uint32_t(k >> 1)) * a.n + i : a.src_if + i);
-                // one evalACL call: ACLAction; counting key of its terminating rule
-                auto eval = [&](int k) -> uint32_t {
-                    if (di[k] < 0) return 1u;                   // nil ACL: PERMIT, not counted (:476-478)
-                    if constexpr (CONN_ABLATE & 1) return 1u + (sa == da ? 1u : 0u);
-                    const ConnDesc D = conn_desc(a, uint32_t(di[k]));
-                    if constexpr (CONN_ABLATE & 2) return 1u + (D.n_rules == sp ? 1u : 0u);
-                    if constexpr (CONN_ABLATE & 4)
-                        if (D.bm_off != 0xFFFFFFFFu) return 1u + (D.n_rules == sp ? 1u : 0u);
-                    uint32_t res, rule;
-                    if (D.pre) {
-                        const uint32_t w = pw[k];
-                        res = w & 3u;
-                        rule = kCount != 0 ? D.slot_rule[w >> 2] : 0u;
-                    } else if (!k16 && D.bm_off != 0xFFFFFFFFu) {
-                        if constexpr (!k16)
-                            res = k < 2 ? conn_bm<kLdsRules>(a, D, sa, da, dp, p, rule)
-                                        : conn_bm<kLdsRules>(a, D, da, sa, sp, p, rule);
-                    } else if (k < 2) {
-                        res = conn_scan<k16, kLdsRules>(a, D, sa, da, s4, d4, dp, p, rule);
-                    } else {
-                        res = conn_scan<k16, kLdsRules>(a, D, da, sa, d4, s4, sp, p, rule);
-                    }
-                    key[k] = D.ctr_off + rule;
-                    return res;
-                };
-                bool srefl = false, drefl = false, done = false;
-                uint32_t r = eval(0);                                                   // SYN: src inbound
+        for (int k = 0; k < 4; ++k)
+            w[k] = *(bi[k] >= 0 ? a.pre + (2ull * uint32_t(bi[k]) + uint32_t(k >> 1)) * a.pre_stride + ic
+                                : a.src_if + ic);
+        // ---- the jobs of the wave, packed ----
+        bool job[4];
+        uint32_t nj = 0, jpos[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            job[k] = di[k] >= 0 && bi[k] < 0;
+            const uint64_t m = __ballot(job[k]);
+            jpos[k] = nj + uint32_t(__popcll(m & lt));
+            nj += uint32_t(__popcll(m));
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (job[k]) *lctr_t(jobs + 4u * jpos[k]) = lane | (uint32_t(k) << 6) | (uint32_t(di[k]) << 8);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (uint32_t j0 = 0; j0 < nj; j0 += 64u) {             // wave-uniform
+            const uint32_t j = j0 + lane;
+            const bool act = j < nj;
+            const uint32_t e = act ? *lctr_t(jobs + 4u * j) : lane;
+            const uint32_t o = e & 63u, k = (e >> 6) & 3u;
+            // the owning lane's connection (every lane takes part in the shuffles)
+            A xs, xd;
+            if constexpr (k16) {
+                xs = make_uint4(__shfl(sa.x, int(o)), __shfl(sa.y, int(o)), __shfl(sa.z, int(o)), __shfl(sa.w, int(o)));
+                xd = make_uint4(__shfl(da.x, int(o)), __shfl(da.y, int(o)), __shfl(da.z, int(o)), __shfl(da.w, int(o)));
+            } else {
+                xs = __shfl(sa, int(o));
+                xd = __shfl(da, int(o));
+            }
+            const uint32_t xdp = __shfl(dp, int(o)), xsp = __shfl(sp, int(o)), xp = __shfl(p, int(o));
+            if (act) {
+                const ConnDesc D = conn_desc(a, e >> 8);
+                const bool syn = k < 2u;
+                uint32_t res, rule;
+                if (!k16 && D.bm_off != 0xFFFFFFFFu) {
+                    if constexpr (!k16)
+                        res = conn_bm<kLdsRules>(a, D, syn ? xs : xd, syn ? xd : xs, syn ? xdp : xsp, xp, rule);
+                } else {
+                    const bool x4s = mapped4(xs), x4d = mapped4(xd);
+                    res = syn ? conn_scan<k16, kLdsRules>(a, D, xs, xd, x4s, x4d, xdp, xp, rule)
+                              : conn_scan<k16, kLdsRules>(a, D, xd, xs, x4d, x4s, xsp, xp, rule);
+                }
+                *lctr_t(results + 16u * o + 4u * k) = res | ((D.ctr_off + rule) << 2);
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // ---- testConnection over the four results ----
+        uint32_t res[4];
+        bool have_job = job[0] || job[1] || job[2] || job[3];
+        v4u rj = {0u, 0u, 0u, 0u};
+        if (have_job) rj = *lds128_t(results + 16u * lane);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) res[k] = di[k] < 0 ? 1u : job[k] ? (rj[k] & 3u) : (w[k] & 3u);   // nil ACL: PERMIT (:476-478)
+        uint32_t v = 3u;
+        bool made[4] = {false, false, false, false};
+        if (ok) {
+            const bool same = si == dj;
+            bool srefl = false, drefl = false, done = false;
+            made[0] = true;
+            uint32_t r = res[0];                                                    // SYN: src inbound
+            if (r == 3u) { v = 3u; done = true; }
+            else if (r == 0u) { v = 0u; done = true; }
+            else if (r == 2u) { srefl = true; drefl = same; }
+            if (!done && !drefl) {                                                  // SYN: dst outbound
+                made[1] = true;
+                r = res[1];
                 if (r == 3u) { v = 3u; done = true; }
                 else if (r == 0u) { v = 0u; done = true; }
-                else if (r == 2u) { srefl = true; drefl = same; }
-                if (!done && !drefl) {                                                  // SYN: dst outbound
-                    r = eval(1);
-                    if (r == 3u) { v = 3u; done = true; }
-                    else if (r == 0u) { v = 0u; done = true; }
-                    else if (r == 2u) { drefl = true; srefl = srefl || same; }
-                }
-                if (!done && !drefl) {                                                  // SYN-ACK: dst inbound
-                    r = eval(2);
-                    if (r == 3u) { v = 3u; done = true; }
-                    else if (r == 0u) { v = 1u; done = true; }
-                }
-                if (!done && !srefl) {                                                  // SYN-ACK: src outbound
-                    r = eval(3);
-                    if (r == 3u) { v = 3u; done = true; }
-                    else if (r == 0u) { v = 1u; done = true; }
-                }
-                if (!done) v = 2u;
+                else if (r == 2u) { drefl = true; srefl = srefl || same; }
             }
-            a.out[i] = uint8_t(v);
+            if (!done && !drefl) {                                                  // SYN-ACK: dst inbound
+                made[2] = true;
+                r = res[2];
+                if (r == 3u) { v = 3u; done = true; }
+                else if (r == 0u) { v = 1u; done = true; }
+            }
+            if (!done && !srefl) {                                                  // SYN-ACK: src outbound
+                made[3] = true;
+                r = res[3];
+                if (r == 3u) { v = 3u; done = true; }
+                else if (r == 0u) { v = 1u; done = true; }
+            }
+            if (!done) v = 2u;
         }
-        if constexpr (kCount == 1) {
+        if (live) a.out[i] = uint8_t(v);
+        if constexpr (kCount != 0) {
+            uint32_t key[4];
 #pragma unroll
-            for (int k = 0; k < 4; ++k)
-                if (key[k] != 0xFFFFFFFFu)
-                    __hip_atomic_fetch_add(lctr_t(a.ctr_lds + 4u * key[k]), 1u, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_WORKGROUP);
-        } else if constexpr (kCount == 2) {
+            for (int k = 0; k < 4; ++k) {
+                key[k] = 0xFFFFFFFFu;
+                if (made[k] && di[k] >= 0) {                    // nil ACLs are not counted
+                    if (job[k]) {
+                        key[k] = rj[k] >> 2;
+                    } else {
+                        const ConnDesc D = conn_desc(a, uint32_t(di[k]));
+                        key[k] = D.ctr_off + D.slot_rule[w[k] >> 2];
+                    }
+                }
+            }
+            if constexpr (kCount == 1) {
 #pragma unroll
-            for (int k = 0; k < 4; ++k) wave_count(a.ctr, key[k]);
+                for (int k = 0; k < 4; ++k)
+                    if (key[k] != 0xFFFFFFFFu)
+                        __hip_atomic_fetch_add(lctr_t(a.ctr_lds + 4u * key[k]), 1u, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP);
+            } else {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) wave_count(a.ctr, key[k]);
+            }
         }
     }
     if constexpr (kCount == 1) {
@@ -824,13 +901,21 @@ hipError_t launch_stream(const Pkts4* p4, const Pkts16* p16, uint8_t* verdict, i
     return hipGetLastError();
 }
 
+hipError_t launch_stream_conn(const ConnArgs& a, int grid, hipStream_t s) {
+    hipLaunchKernelGGL(stream_conn_kernel, dim3(grid), dim3(1024), 0, s, static_cast<const uint4*>(a.src),
+                       static_cast<const uint4*>(a.dst), reinterpret_cast<const uint4*>(a.src_if),
+                       reinterpret_cast<const uint4*>(a.dst_if), reinterpret_cast<const uint2*>(a.sport),
+                       reinterpret_cast<const uint2*>(a.dport), reinterpret_cast<const uint32_t*>(a.proto),
+                       reinterpret_cast<uint32_t*>(a.out), uint32_t(a.n / 4u));
+    return hipGetLastError();
+}
+
 hipError_t launch_connect(const ConnArgs& a, bool k16, bool lds_rules, int count, int grid, size_t lds,
                           hipStream_t s) {
     if (a.n == 0) return hipSuccess;
 #define CONN_CASE(K16, L, C)                                                                               \
     if (k16 == K16 && lds_rules == L && count == C) {                                                      \
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(connect_kernel<K16, L, C>),                \
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));                   \
+        lds_attr(reinterpret_cast<const void*>(connect_kernel<K16, L, C>), lds);                          \
         hipLaunchKernelGGL((connect_kernel<K16, L, C>), dim3(grid), dim3(1024), lds, s, a);                \
         return hipGetLastError();                                                                          \
     }

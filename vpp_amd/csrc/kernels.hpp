@@ -162,14 +162,24 @@ hipError_t launch_classify4_slots(const Cls4Dev& t, const Pkts4& p, uint32_t* ou
                                   const LaunchCfg& cfg);
 hipError_t launch_classify16_slots(const Cls4Dev& t, const Fe16& fe, const Pkts16& p, uint32_t* out,
                                    bool lds_resident, const LaunchCfg& cfg);
+// Both tuples of a connection batch in one launch (LDS-resident IPv4 image):
+// out[i] = the SYN tuple (p.src, p.dst, p.dport) and out[stride + i] the
+// SYN-ACK tuple (p.dst, p.src, sport), result | slot << 2 each.  The OTHER
+// image (o, offsets rebased to LDS byte o_at) is staged beside the main one
+// when o_at != 0, so protocols > 2 are classified from LDS in place.
+// Needs 16-B aligned src / dst / out / out + stride, 8-B dport / sport, 4-B
+// proto; stride a multiple of 4.
+hipError_t launch_classify4_pair(const Cls4Dev& t, const Cls4Dev& o, uint32_t o_at, const Pkts4& p,
+                                 const uint16_t* sport, uint32_t* out, uint64_t stride, const LaunchCfg& cfg);
 
 struct ConnDesc {                // one bound ACL for the connection kernel
     uint32_t rule_off;           // linear ACLs: first rule in the call's rule pool
     uint32_t n;                  // linear rules
     uint32_t n_rules;            // R (default DENY: rule R)
     uint32_t ctr_off;            // counting: counter of rule 0 in the call's counter space
-    const uint32_t* pre;         // classifier slot words (res | slot << 2): [0, N) SYN, [N, 2N) SYN-ACK; or null
-    const uint32_t* slot_rule;   // pre: slot -> rule index
+    int32_t pre_blk;             // classifier slot words' block in ConnArgs::pre (-1: none)
+    uint32_t pad;
+    const uint32_t* slot_rule;   // pre_blk >= 0: slot -> rule index
     uint32_t bm_off;             // bitmap form (IPv4): byte offset of its tables in the pool; ~0u: none
     uint32_t bm_sd;              // bitmap form: source | destination interval counts << 16
     uint32_t bm_tu;              // bitmap form: TCP | UDP port interval counts << 16
@@ -190,6 +200,10 @@ static_assert(sizeof(ConnDesc) == 48 && sizeof(IfAcls) == 16, "connect_kernel re
 // rule i matches that interval's addresses (ports); the first match is the
 // lowest set bit of src row & dst row & protocol row.
 constexpr uint32_t kConnBmHeader = 32;
+// The connection kernel's per-wave job area in LDS (a.jobs_lds): 256 job
+// words (the evaluations of the wave's 64 connections that scan or search a
+// linear ACL), then 256 result words (4 per lane), 2 KiB per wave.
+constexpr uint32_t kConnJobBytes = 2048;
 struct ConnArgs {
     const ConnDesc* desc;
     const IfAcls* ifs;
@@ -210,14 +224,20 @@ struct ConnArgs {
     uint8_t* out;
     uint32_t n_desc;             // descriptors in desc
     uint32_t meta_lds;           // LDS byte offset of the staged desc + ifs tables; ~0u: global reads
-    const uint32_t* pre;         // classifier slot words of the large ACLs: block b at pre + 2 n b
-                                 // (SYN tuple, then SYN-ACK); null when there are none
+    const uint32_t* pre;         // classifier slot words of the large ACLs: block b at pre + 2 b pre_stride
+                                 // (SYN tuple, then SYN-ACK at + pre_stride); null when there are none
+    uint64_t pre_stride;
+    uint32_t jobs_lds;           // LDS byte offset of the per-wave job areas (kConnJobBytes each)
 };
 // k16: 16-byte addresses; lds_rules: stage the pool; count: 0 none, 1 LDS
 // counters, 2 global (wave-aggregated) counters; grid: persistent workgroups;
-// lds: dynamic LDS bytes (pool, LDS counters, a.meta_lds tables)
+// lds: dynamic LDS bytes (pool, LDS counters, a.meta_lds tables, job areas)
 hipError_t launch_connect(const ConnArgs& a, bool k16, bool lds_rules, int count, int grid, size_t lds,
                           hipStream_t s);
+// the connection batch's stream without the evaluation (whole 4-connection
+// groups of an IPv4 batch; 16-B aligned src / dst / src_if / dst_if, 8-B
+// ports, 4-B proto and out)
+hipError_t launch_stream_conn(const ConnArgs& a, int grid, hipStream_t s);
 // tables' connection counters += the call's counters (ConnDesc ctr_off ..
 // + n_rules), which are cleared: one workgroup per descriptor
 hipError_t launch_conn_scatter(const ConnDesc* desc, unsigned long long* const* table_ctr, uint32_t n_desc,

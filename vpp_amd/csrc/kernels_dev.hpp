@@ -35,6 +35,9 @@
 
 #include "kernels.hpp"
 
+#include <mutex>
+#include <unordered_map>
+
 namespace cls {
 
 namespace {
@@ -104,6 +107,19 @@ struct Img {
         }
     }
 };
+
+// A kernel's dynamic-LDS ceiling (hipFuncSetAttribute), raised when a launch
+// needs more than before: one host call per kernel and size, not per launch.
+static inline void lds_attr(const void* f, size_t lds) {
+    static std::mutex mu;
+    static std::unordered_map<const void*, size_t> set;
+    std::lock_guard<std::mutex> g(mu);
+    size_t& v = set[f];
+    if (lds > v) {
+        (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
+        v = lds;
+    }
+}
 
 __device__ __forceinline__ bool port_in(uint32_t dport, uint32_t pw) {
     return ((dport - (pw & 0xFFFFu)) & 0xFFFFu) <= (pw >> 16);
@@ -957,8 +973,7 @@ template <bool kLds, bool kVec, int kMode, int kList, int kD, int kCtr = 0>
 static void launch_d(const Cls4Dev& t, const Pkts4& p, uint8_t* verdict, unsigned long long* gslot,
                      const LaunchCfg& cfg) {
     const size_t lds = (kLds ? t.lds_bytes : 0) + 16;   // + the OTHER queue counter
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(classify4_cls<kLds, kVec, kMode, kList, kD, kCtr>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
+    lds_attr(reinterpret_cast<const void*>(classify4_cls<kLds, kVec, kMode, kList, kD, kCtr>), lds);
     hipLaunchKernelGGL((classify4_cls<kLds, kVec, kMode, kList, kD, kCtr>), dim3(cfg.grid), dim3(kClsBlock), lds,
                        cfg.stream, t, cfg.other, p, verdict, gslot);
 }
@@ -1045,8 +1060,7 @@ template <bool kLds, int kMode, int kList, int kD, bool kLin, int kFe, int kCtr 
 static void launch16_d(const Cls4Dev& t, const Fe16& fe, const Pkts16& p, uint8_t* verdict,
                        unsigned long long* gslot, const LaunchCfg& cfg) {
     const size_t lds = (kLds ? t.lds_bytes : 0) + 16;   // + the OTHER queue counter
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(classify16_cls<kLds, kMode, kList, kD, kLin, kFe, kCtr>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
+    lds_attr(reinterpret_cast<const void*>(classify16_cls<kLds, kMode, kList, kD, kLin, kFe, kCtr>), lds);
     hipLaunchKernelGGL((classify16_cls<kLds, kMode, kList, kD, kLin, kFe, kCtr>), dim3(cfg.grid), dim3(kClsBlock),
                        lds, cfg.stream, t, cfg.other, fe, p, verdict, gslot);
 }

@@ -317,6 +317,19 @@ class Engine:
         self._check(_abi.lib().cls_connect_batch(self.h, C.byref(cs), n, _ptr(out), flags | _abi.F_DEVICE, None))
         return out
 
+    def stream_floor_conn(self, src_if, dst_if, src, dst, proto, sport, dport, reps: int = 20) -> float:
+        """The connection path's HBM floor on a device batch (cls_stream_floor_conn):
+        ms per launch of a kernel that reads the same 22 B per IPv4 connection
+        and writes one byte, with no evaluation."""
+        import torch
+        n = src.shape[0]
+        out = torch.empty(n, dtype=torch.uint8, device=src.device)
+        pk = _abi.PktSoa(_abi.AF_V4, _ptr(src), _ptr(dst), None, None, _ptr(sport), _ptr(dport), _ptr(proto))
+        cs = _abi.ConnSoa(pk, _ptr(src_if), _ptr(dst_if))
+        ms = C.c_float()
+        self._check(_abi.lib().cls_stream_floor_conn(self.h, C.byref(cs), n, _ptr(out), reps, C.byref(ms), None))
+        return ms.value
+
     def conn_counters(self, table, reset: bool = False) -> np.ndarray:
         """Per-rule connection counters of a table (a Table, a table id or an
         installed ACL's name): R + 1 u64, [R] = default DENY."""
