@@ -275,6 +275,7 @@ def main():
     for _ in range(args.steps):
         step(i, True)
         i += 1
+    t_submit = time.perf_counter() - t0      # host time to enqueue the timed steps
     last = sev_pool[len(sev)]
     last.record(main)
     sev.append(last)
@@ -349,6 +350,9 @@ def main():
                                       "step's classify" % (D.backend(), (R + 1) * 8)) if coll else None},
             "settle_ms": round(settle_ms, 1),
             "step_ms_median": round(med_step, 4),
+            # host time to enqueue a step (Python, ctypes, launches, events):
+            # when it reaches ms_per_step the GPU waits for the host
+            "host_submit_ms_per_step": round(t_submit * 1e3 / max(1, args.steps), 4),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
                          "traffic": traffic, "traffic_source": traffic_src,

@@ -424,6 +424,14 @@ typedef struct cls_image_v16_header {
      * min(lo64, 2^48) : 2^48 + min(hi64, 2^64 - 1 - 2^48) (exact when every
      * start has hi64 = 0 and lo64 <= 2^48, or lo64 = 0) */
     uint32_t fe_k8[2];
+    /* src_mode 2 (sources not all host routes, many IPv4 intervals): an
+     * IPv4-mapped source's row from the trie over its IPv4 word at the core
+     * header's off_trie / trie_depth (leaf entries carry the core's class);
+     * any other source's row from the side-0 search (fe_key[0] ...), whose
+     * table holds only the non-IPv4 intervals and rows as values.  src_mode
+     * 1 and 2: the source interval table at off_src_search has
+     * src_search_top keys (8 B when src_search_k8). */
+    uint32_t src_search_top, src_search_k8;
 } cls_image_v16_header;
 int cls_compile_v16(const cls_rule* rules, uint32_t n_rules, void* blob, uint64_t cap,
                     uint64_t* need);

@@ -75,6 +75,24 @@ class Image:
         L = 32 - shift
         return (((k.astype(np.uint64) * mul) & 0xFFFFFFFF) >> np.uint64(32 - 2 * L)) & ((1 << L) - 1)
 
+    def trie_class(self, src):
+        """The source trie at h.off_trie (compile.cpp build_trie): class per
+        host-order IPv4 address."""
+        h = self.h
+        img = np.frombuffer(self._img, np.uint32).astype(np.int64)
+        s = np.asarray(src, np.uint32).astype(np.int64)
+        a = img[(h.off_trie + ((s >> 22) & 0x3FC)) // 4]
+        a = img[(a + ((s >> 14) & 0x3FC)) // 4]
+        ln = (a & 0xFF) + 1
+        a = a >> 8
+        x = s & 0xFFFF
+        for _ in range(h.trie_depth):
+            half = ln >> 1
+            c = a + 4 * half
+            a = np.where((img[c // 4] & 0xFFFF) < x, c, a)
+            ln = ln - half
+        return img[a // 4] >> 16
+
     def source_class(self, src):
         h = self.h
         if h.mode == 4:
@@ -295,26 +313,52 @@ class Image16:
         img = blob[h.core.off_image:h.core.off_image + h.core.img_bytes]
         self._img = img
         self.keys, self.vals = [None, None], [None, None]
+
+        def table(src, koff, voff, top, k8, nval):
+            if k8:                                     # 8-B keys over key8(address)
+                k = np.frombuffer(src, np.uint32, count=2 * top, offset=koff).reshape(-1, 2)
+                keys = [int(b) << 32 | int(a) for a, b in k]
+            else:
+                k = np.frombuffer(src, np.uint32, count=4 * top, offset=koff).reshape(-1, 4)
+                hi = (k[:, 1].astype(object) << 32) | k[:, 0].astype(object)
+                lo = (k[:, 3].astype(object) << 32) | k[:, 2].astype(object)
+                keys = [int(a) << 64 | int(b) for a, b in zip(hi, lo)]
+            if nval is None:                           # the real keys, then all-ones padding
+                pad = (1 << 64) - 1 if k8 else (1 << 128) - 1
+                nval = 1 + sum(1 for x in keys[1:] if x != pad)
+            return keys, np.frombuffer(src, np.uint32, count=nval, offset=voff)
+
         for sd in range(2):
             src = img
             koff, voff = h.fe_key[sd], h.fe_val[sd]
             if sd == 0 and h.src_mode == 1:           # source interval table in the trailer
                 src, koff = blob, h.off_src_search
                 voff = koff + h.src_search_val
-            if h.fe_k8[sd]:                            # 8-B keys over key8(address)
-                k = np.frombuffer(src, np.uint32, count=2 * h.fe_top[sd], offset=koff).reshape(-1, 2)
-                self.keys[sd] = [int(b) << 32 | int(a) for a, b in k]
-            else:
-                k = np.frombuffer(src, np.uint32, count=4 * h.fe_top[sd], offset=koff).reshape(-1, 4)
-                hi = (k[:, 1].astype(object) << 32) | k[:, 0].astype(object)
-                lo = (k[:, 3].astype(object) << 32) | k[:, 2].astype(object)
-                self.keys[sd] = [int(a) << 64 | int(b) for a, b in zip(hi, lo)]
-            self.vals[sd] = np.frombuffer(src, np.uint32, count=h.fe_n[sd], offset=voff)
+            self.keys[sd], self.vals[sd] = table(src, koff, voff, h.fe_top[sd], h.fe_k8[sd], h.fe_n[sd])
+        # src_mode 2: side 0 above is the non-IPv4 search (values: rows); the
+        # whole table with reps is in the trailer (protocols > 2)
+        self.gtab = None
+        if h.src_mode == 2:
+            self.gtab = table(blob, h.off_src_search, h.off_src_search + h.src_search_val, h.src_search_top,
+                              h.src_search_k8, None)
 
-    def rep(self, sd: int, addrs) -> np.ndarray:
+    def rep(self, sd: int, addrs, table=None) -> np.ndarray:
         keys, vals, top = self.keys[sd], self.vals[sd], self.h.fe_top[sd]
-        out = np.empty(len(addrs), np.uint32)
         k8 = self.h.fe_k8[sd]
+        if table is not None:
+            (keys, vals), top, k8 = table, self.h.src_search_top, self.h.src_search_k8
+        if k8:
+            # vectorised: the branch-free search lands on the number of keys
+            # [1, top) below key8(address) (keys ascending, padding all ones)
+            a = np.ascontiguousarray(addrs, np.uint8).reshape(-1, 16)
+            hi = a[:, :8].copy().view(">u8").ravel().astype(np.uint64)
+            lo = a[:, 8:].copy().view(">u8").ravel().astype(np.uint64)
+            k48 = np.uint64(1 << 48)
+            x = np.where(hi == 0, np.minimum(lo, k48), k48 + np.minimum(hi, np.uint64((1 << 64) - 1 - (1 << 48))))
+            kk = np.array(keys[1:top], np.uint64)
+            pos = np.searchsorted(kk, x, side="left")
+            return np.asarray(vals, np.uint32)[pos]
+        out = np.empty(len(addrs), np.uint32)
         for i, a in enumerate(addrs):
             x = int.from_bytes(bytes(a), "big")
             if k8:
@@ -358,8 +402,22 @@ class Image16:
         dst16 = np.asarray(dst16, np.uint8).reshape(-1, 16)
         if self.h.core.swap:                           # destination-keyed
             src16, dst16 = dst16, src16
-        srep = self.rep(0, src16)
         drep = self.rep(1, dst16)
+        if self.h.src_mode == 2:
+            # kernels_dev.hpp src_trie16: IPv4-mapped sources by the trie over
+            # their IPv4 word, the others by the non-IPv4 search (rows);
+            # protocol > 2 takes the rep from the whole table
+            srep = self.rep(0, src16, table=self.gtab)
+            w = np.frombuffer(np.ascontiguousarray(src16).tobytes(), "<u4").reshape(-1, 4)
+            is4 = (w[:, 0] == 0) & (w[:, 1] == 0) & (w[:, 2] == 0xFFFF0000)
+            ip = src16[:, 12:16].astype(np.uint32)
+            ip = (ip[:, 0] << 24) | (ip[:, 1] << 16) | (ip[:, 2] << 8) | ip[:, 3]
+            c4 = self.core.trie_class(ip)
+            rows6 = self.rep(0, src16).astype(np.int64)
+            c6 = (rows6 - self.core.h.off_cells) // self.core.h.row_bytes
+            cls = np.where(is4, c4, c6)
+            return self.core.classify(srep, drep, dport, proto, cls=cls, framed=True)
+        srep = self.rep(0, src16)
         if self.h.src_mode == 1:
             rows = self.src_rows(src16)
             # the hashed row must be the class row of the rep (what the core's

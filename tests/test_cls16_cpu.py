@@ -162,3 +162,99 @@ def test_config5_table_cpu():
                                   tr["proto"], af=16)
     np.testing.assert_array_equal(v, ov)
     np.testing.assert_array_equal(c, oc)
+
+
+# ---- src_mode 2: the IPv4 source trie of the 16-byte layout ----------------
+
+@pytest.mark.parametrize("seed", range(8))
+@pytest.mark.parametrize("kind", ["v4", "mixed", "v16"])
+def test_v16_source_trie_matches_oracle(seed, kind, monkeypatch):
+    """src_mode 2 (forced): IPv4-mapped sources through the trie over their
+    IPv4 word, the others through the non-IPv4 search (rows), protocols > 2
+    through the global table's reps -- against the faithful oracle on IPv4
+    tables widened to 16 bytes, their mixed-family twins and random
+    mixed-family ACLs with malformed rules."""
+    monkeypatch.setenv("CONTIVCLS_V16_SRC_TRIE", "1")
+    if kind == "v16":
+        rules, pool = random_acl16(seed * 101 + 7, 150, 0.1, n_prefixes=60)
+        tr = random_traffic16(seed + 40, 3000, pool)
+    else:
+        rules, pool = random_acl(seed * 101 + 5, 150, 0.1, n_prefixes=80)
+        rules, tr = mix_families(rules, random_traffic(seed + 40, 3000, pool), seed, 0.0 if kind == "v4" else 0.5)
+    img = _check16(rules, tr)
+    if img.core.has_cls:                       # (all-host-route sources keep the hashes, src_mode 1)
+        assert img.h.src_mode in (1, 2)
+
+
+def test_v16_source_trie_edges(monkeypatch):
+    """Addresses at the trie's chunk and /8 boundaries and at the edges of the
+    IPv4-mapped block (::ffff:0.0.0.0, ::ffff:255.255.255.255 and their IPv6
+    neighbours), prefixes ending at those edges, host routes among blocks."""
+    import vpp_amd.model as M
+    monkeypatch.setenv("CONTIVCLS_V16_SRC_TRIE", "1")
+    nets = ["10.0.0.0/8", "10.1.0.0/16", "10.1.255.0/24", "10.2.0.0/15", "10.1.2.3/32", "0.0.0.0/1",
+            "128.0.0.0/1", "255.255.255.255/32", "0.0.0.0/32", "10.255.255.0/24", "11.0.0.0/16",
+            "fd00::/16", "::ffff:0:0/97", "::fffe:0:0/96"]
+    rules = []
+    for k, a in enumerate(nets * 3):
+        d = "" if k % 3 else "192.168.%d.0/24" % k
+        rules.append(M.l4_rule([M.DENY, M.PERMIT, M.REFLECT][k % 3], a, d, ["tcp", "udp"][k % 2],
+                               0, 65535, 0, 65535 if k % 4 else 80))
+    edges = [0x0A000000, 0x0A00FFFF, 0x0A010000, 0x0A01FFFF, 0x0A01FF00, 0x0A0100FF, 0x0A010203, 0x0A010204,
+             0x0AFFFFFF, 0x0B000000, 0x09FFFFFF, 0, 1, 0x7FFFFFFF, 0x80000000, 0xFFFFFFFE, 0xFFFFFFFF,
+             0x0A020000, 0x0A03FFFF, 0x0A040000, 0x0B00FFFF, 0x0B010000]
+    addrs = [(0xFFFF << 32) | a for a in edges] + [(0xFFFF << 32) - 1, (0xFFFF << 32) + (1 << 32),
+                                                  0xFD00 << 112, (0xFFFE << 32) | 5, 0x0A010203]
+    src = np.array([list(a.to_bytes(16, "big")) for a in addrs], np.uint8)
+    n = len(src)
+    dst = np.array([list(((0xFFFF << 32) | 0xC0A80000 | (i * 7)).to_bytes(16, "big")) for i in range(n)], np.uint8)
+    for proto in (0, 1, 2, 47):
+        tr = dict(src=src, dst=dst, dport=np.full(n, 80, np.uint16), proto=np.full(n, proto, np.uint8))
+        img = _check16(rules, tr)
+        assert img.h.src_mode == 2
+
+
+@pytest.mark.parametrize("blocks", [20, 200])
+def test_gen_policy_lists_v16_source_trie(blocks):
+    """The gen-policy.py lists (tests/policy/perf/gen-policy.py:8-65) in the
+    16-byte layout take the source trie by themselves and stay LDS-resident
+    (sublist list mode, like their IPv4 images); 4000 packets -- IPv4-mapped
+    inside and around the blocks, IPv6, protocol 47 -- against the fast
+    oracle, both orientations."""
+    import random
+    from vpp_amd import configurator as C
+    from vpp_amd.renderer.api import PodID
+    from vpp_amd.renderer.traffic import compile_rules
+    pol = C.gen_policy(random.Random(blocks), num_cidrs=blocks)
+    txn = C.PolicyConfigurator({PodID("db", "default"): "10.1.1.1"}).new_txn(False)
+    g = np.random.default_rng(blocks)
+    n = 4000
+    for match in (C.MATCH_INGRESS, C.MATCH_EGRESS):
+        acl = compile_rules(txn.generate_rules(match, [pol]))
+        import os
+        os.environ.pop("CONTIVCLS_ORIENT", None)
+        img = Image16(compile_blob(_abi.CRules(acl), "cls_compile_v16"))
+        os.environ["CONTIVCLS_ORIENT"] = "src"
+        assert img.h.src_mode == 2 and img.core.h.list_mode in (3, 4, 5, 6)
+        assert img.core.h.lds_bytes <= 160 * 1024
+        blk = g.integers(0, blocks + blocks // 10 + 1, n).astype(np.uint64)
+        inblk = (((blk + 0x100) << 16) | g.integers(0, 1 << 16, n).astype(np.uint64)).astype(np.uint64)
+        other = g.integers(0, 1 << 32, n).astype(np.uint64)
+        a, b = (inblk, other) if match == C.MATCH_INGRESS else (other, inblk)
+
+        def wide(x, v6):
+            hi = np.where(v6, np.uint64(0xFD000000 << 32), np.uint64(0))
+            lo = np.where(v6, x, np.uint64(0xFFFF << 32) | x)
+            out = np.empty((n, 16), np.uint8)
+            out[:, :8] = hi.astype(">u8").view(np.uint8).reshape(n, 8)
+            out[:, 8:] = lo.astype(">u8").view(np.uint8).reshape(n, 8)
+            return out
+        v6 = g.random(n) < 0.1
+        src, dst = wide(a, v6), wide(b, g.random(n) < 0.1)
+        ports = np.array([p.number for p in pol.matches[0].ports], np.uint16)
+        dport = np.where(g.random(n) < 0.5, g.choice(ports, n), g.integers(0, 65536, n)).astype(np.uint16)
+        proto = g.choice(np.array([0, 1, 2, 47], np.uint8), n, p=[0.445, 0.445, 0.1, 0.01])
+        v, c = img.classify(src, dst, dport, proto)
+        ov, oc = oracle.classify_fast(oracle.rules_to_c(acl), src, dst, dport, proto, af=16)
+        np.testing.assert_array_equal(v, ov)
+        np.testing.assert_array_equal(c, oc)

@@ -124,9 +124,11 @@ def test_gen_policy_scale_on_gpu(eng, num_cidrs):
 def test_gen_policy_default_scale_on_gpu(eng):
     """gen-policy.py at its defaults (tests/policy/perf/gen-policy.py:8-11:
     1000 blocks x 5 excepts x 20 ports): the pod's ingress list has ~477k
-    rules and compiles to the global-memory image (template scan).  2000
-    packets against the pre-parsed C evalACL oracle, verdicts and per-rule
-    counts."""
+    rules.  In the 16-byte layout it compiles to an LDS-resident image (the
+    IPv4 source trie of src_mode 2, wide cells; tests/test_cls16_cpu.py and
+    test_gen_policy_lists_v16_on_gpu check the blob at scale).  2000 packets
+    through the host path against the pre-parsed C evalACL oracle, verdicts
+    and per-rule counts."""
     import oracle
     from configurator_replay import gen_policy_packets
     from vpp_amd.renderer.api import PodID
@@ -149,3 +151,63 @@ def test_gen_policy_default_scale_on_gpu(eng):
         assert len(set(want_v.tolist())) >= 2
     finally:
         eng.del_table(t)
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("blocks", [200, 1000])
+def test_gen_policy_lists_v16_on_gpu(eng, blocks):
+    """The gen-policy.py lists in the 16-byte layout (IPv4-mapped packets in
+    and around the blocks, 10 % IPv6, ICMP, protocol 47), ingress and egress:
+    the image is LDS-resident (src_mode 2: the IPv4 source trie), 1 Mi
+    device-resident packets bit-exact against the blob interpreter
+    (tests/cls_image.py Image16, verdicts and counters), and a 16 Ki sample
+    against the pre-parsed C evalACL oracle."""
+    import torch
+
+    import oracle
+    from cls_image import Image16, compile_blob
+    from vpp_amd import _abi
+    from vpp_amd.renderer.api import PodID
+    pol = C.gen_policy(random.Random(blocks), num_cidrs=blocks)
+    txn = C.PolicyConfigurator({PodID("db", "default"): "10.1.1.1"}).new_txn(False)
+    g = np.random.default_rng(blocks)
+    n = 1 << 20
+    ports = np.array([p.number for p in pol.matches[0].ports], np.uint16)
+    for match in (C.MATCH_INGRESS, C.MATCH_EGRESS):
+        acl = T.compile_rules(txn.generate_rules(match, [pol]))
+        img = Image16(compile_blob(_abi.CRules(acl), "cls_compile_v16"))
+        t = eng.put_table("gp16", acl)
+        try:
+            info = t.info()
+            assert info["lds_resident_v16"] == 1 and img.h.src_mode == 2
+            blk = g.integers(0, blocks + blocks // 10 + 1, n).astype(np.uint64)
+            inblk = ((blk + 0x100) << np.uint64(16)) | g.integers(0, 1 << 16, n).astype(np.uint64)
+            other = g.integers(0, 1 << 32, n).astype(np.uint64)
+            a, b = (inblk, other) if match == C.MATCH_INGRESS else (other, inblk)
+
+            def wide(x, v6):
+                hi = np.where(v6, np.uint64(0xFD000000 << 32), np.uint64(0))
+                lo = np.where(v6, x, np.uint64(0xFFFF << 32) | x)
+                out = np.empty((n, 16), np.uint8)
+                out[:, :8] = hi.astype(">u8").view(np.uint8).reshape(n, 8)
+                out[:, 8:] = lo.astype(">u8").view(np.uint8).reshape(n, 8)
+                return out
+            src, dst = wide(a, g.random(n) < 0.1), wide(b, g.random(n) < 0.1)
+            dport = np.where(g.random(n) < 0.5, g.choice(ports, n), g.integers(0, 65536, n)).astype(np.uint16)
+            proto = g.choice(np.array([0, 1, 2, 47], np.uint8), n, p=[0.445, 0.445, 0.1, 0.01])
+            d = {k: torch.from_numpy(v.view(np.int16) if v.dtype == np.uint16 else v).to("cuda")
+                 for k, v in dict(src=src, dst=dst, dport=dport, proto=proto).items()}
+            verdict = torch.empty(n, dtype=torch.uint8, device="cuda")
+            counters = torch.zeros(len(acl) + 1, dtype=torch.int64, device="cuda")
+            eng.classify(t, d["src"], d["dst"], d["dport"], d["proto"], verdict, counters)
+            torch.cuda.synchronize()
+            v, c = verdict.cpu().numpy(), counters.cpu().numpy().astype(np.uint64)
+            wv, wc = img.classify(src, dst, dport, proto)
+            assert np.array_equal(v, wv), match
+            assert np.array_equal(c, wc), match
+            k = 1 << 14
+            ov, _ = oracle.classify_fast(oracle.rules_to_c(acl), src[:k], dst[:k], dport[:k], proto[:k], af=16)
+            assert np.array_equal(v[:k], ov), match
+            assert len(set(ov.tolist())) >= 2
+        finally:
+            eng.del_table(t)

@@ -126,3 +126,23 @@ def test_config5_table_on_gpu(eng):
         _assert_same((v.cpu().numpy(), c.cpu().numpy().astype(np.uint64)), want)
     finally:
         eng.del_table(t)
+
+
+@pytest.mark.parametrize("seed", range(4))
+@pytest.mark.parametrize("kind", ["v4", "mixed", "v16"])
+def test_v16_source_trie_on_gpu(eng, seed, kind, monkeypatch):
+    """src_mode 2 (forced): IPv4-mapped sources through the trie over their
+    IPv4 word, the others through the non-IPv4 search, protocols > 2 through
+    the global table -- classify16_cls and the linear cross-check against the
+    oracle, verdicts and counters."""
+    from aclgen import random_acl
+    monkeypatch.setenv("CONTIVCLS_V16_SRC_TRIE", "1")
+    if kind == "v16":
+        rules, pool = random_acl16(seed * 101 + 7, 150, 0.1, n_prefixes=60)
+        tr = random_traffic16(seed + 40, 20000, pool)
+    else:
+        rules, pool = random_acl(seed * 101 + 5, 150, 0.1, n_prefixes=80)
+        rules, tr = mix_families(rules, random_traffic(seed + 40, 20000, pool), seed, 0.0 if kind == "v4" else 0.5)
+    want = _oracle16(rules, tr, fast=True)
+    _assert_same(_gpu(eng, rules, tr), want)
+    _assert_same(_gpu(eng, rules, tr, force_linear=True), want)

@@ -124,7 +124,8 @@ class Image16Header(C.Structure):
                 ("fe_top", C.c_uint32 * 2), ("fe_n", C.c_uint32 * 2)] + [
         (n, C.c_uint32) for n in ("src_mode", "h4", "cap4", "mul4", "k6", "r6", "cap6", "mul6")] + [
         ("fold", C.c_uint32 * 3), ("dflt_row", C.c_uint32 * 2), ("off_src_search", C.c_uint32),
-        ("src_search_val", C.c_uint32), ("fe_k8", C.c_uint32 * 2)]
+        ("src_search_val", C.c_uint32), ("fe_k8", C.c_uint32 * 2), ("src_search_top", C.c_uint32),
+        ("src_search_k8", C.c_uint32)]
 
 
 _lib = None

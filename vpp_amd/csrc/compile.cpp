@@ -638,6 +638,8 @@ bool build_trie(const std::vector<uint32_t>& bounds, uint32_t n, const std::vect
 
 }  // namespace
 
+constexpr uint32_t kV16TrieMin = 64;    // src_mode 2 from this many IPv4 source intervals
+
 uint32_t Cls4Image::row_of(uint32_t addr) const {
     const size_t k = size_t(std::upper_bound(h_bounds.begin(), h_bounds.end(), addr) - h_bounds.begin()) - 1;
     return off_cells + uint32_t(h_iclass[k]) * row_bytes;
@@ -1590,7 +1592,8 @@ static bool build_cls16_one(const std::vector<SemRule>& sem, uint32_t n_rules, C
         img.sem.push_back(r);
     }
     // Source front end: host-route hashes when every source prefix is a host
-    // route (CONTIVCLS_V16_SRC_SEARCH=1 forces the interval search: tests)
+    // route (CONTIVCLS_V16_SRC_SEARCH=1 forces the interval search, src_mode
+    // 0: tests)
     bool hosts = true;
     for (int f = 0; f < 2; ++f)
         for (const auto& r : side[0].pf[f]) hosts = hosts && r.lo == r.hi;
@@ -1599,11 +1602,8 @@ static bool build_cls16_one(const std::vector<SemRule>& sem, uint32_t n_rules, C
 
     // interval tables: per side, keys (start - 1 as u64 hi, lo; padding all
     // ones) then reps
-    auto search_table = [&](int sd, std::vector<uint32_t>& out, uint32_t& top, uint32_t& nval, uint32_t& rel_val,
-                            uint32_t& k8) {
-        std::vector<u128> start;
-        std::vector<uint32_t> rep;
-        side[sd].intervals(start, rep);
+    auto search_list = [&](const std::vector<u128>& start, const std::vector<uint32_t>& rep, std::vector<uint32_t>& out,
+                           uint32_t& top, uint32_t& nval, uint32_t& rel_val, uint32_t& k8) {
         uint32_t K = 1;
         while (K < start.size()) K *= 2;
         top = K;
@@ -1630,12 +1630,74 @@ static bool build_cls16_one(const std::vector<SemRule>& sem, uint32_t n_rules, C
         out.insert(out.end(), rep.begin(), rep.end());
         out.resize(align4(uint32_t(out.size())));
     };
+    auto search_table = [&](int sd, std::vector<uint32_t>& out, uint32_t& top, uint32_t& nval, uint32_t& rel_val,
+                            uint32_t& k8) {
+        std::vector<u128> start;
+        std::vector<uint32_t> rep;
+        side[sd].intervals(start, rep);
+        search_list(start, rep, out, top, nval, rel_val, k8);
+    };
+    // Source front end, src_mode 2 (not every source a host route, many
+    // IPv4 intervals -- e.g. the IP-block lists of gen-policy.py): IPv4-mapped
+    // sources go through a trie over their IPv4 word straight to the class
+    // row (the IPv4 classifier's source trie, compile.cpp build_trie, with the
+    // core's classes), other sources through a search over the non-IPv4
+    // intervals whose values are rows; the whole interval table stays in
+    // global memory for protocols > 2 (they need the rep).
+    // CONTIVCLS_V16_SRC_TRIE=0 / 1: never / whenever sources are not all host
+    // routes (tests).
+    std::vector<u128> s_start;
+    std::vector<uint32_t> s_rep;
+    side[0].intervals(s_start, s_rep);
+    std::vector<uint32_t> v4b, v4rep;                      // intervals of ::ffff:0.0.0.0/96, rel. bounds
+    std::vector<u128> v6start;                            // the others (the IPv4 block as one interval)
+    std::vector<uint32_t> v6rep;
+    {
+        size_t k = size_t(std::upper_bound(s_start.begin(), s_start.end(), kV4Lo) - s_start.begin()) - 1;
+        v4b.push_back(0u);
+        v4rep.push_back(s_rep[k]);
+        for (size_t j = k + 1; j < s_start.size() && s_start[j] <= kV4Hi; ++j) {
+            v4b.push_back(uint32_t(s_start[j] - kV4Lo));
+            v4rep.push_back(s_rep[j]);
+        }
+        for (size_t j = 0; j < s_start.size(); ++j) {
+            if (s_start[j] > kV4Lo && s_start[j] <= kV4Hi) continue;
+            v6start.push_back(s_start[j]);
+            v6rep.push_back(s_rep[j]);
+        }
+    }
+    bool trie = !hosts && v4b.size() >= kV16TrieMin && !std::getenv("CONTIVCLS_V16_SRC_SEARCH");
+    if (const char* e = std::getenv("CONTIVCLS_V16_SRC_TRIE")) trie = !hosts && std::atoi(e) != 0;
+    if (trie) img.src_mode = 2;
     Cls4Opts opt;
-    opt.ext_src = hosts;
+    opt.ext_src = hosts || trie;
     uint32_t rel_key[2] = {}, rel_val[2] = {};
-    for (int sd = hosts ? 1 : 0; sd < 2; ++sd) {
+    for (int sd = opt.ext_src ? 1 : 0; sd < 2; ++sd) {
         rel_key[sd] = uint32_t(opt.tail.size()) * 4;
         search_table(sd, opt.tail, img.fe_top[sd], img.fe_n[sd], rel_val[sd], img.fe_k8[sd]);
+    }
+    // src_mode 2: the non-IPv4 source search (values patched to rows below)
+    // and room for the trie (its size with one provisional class per distinct
+    // rep -- the core's classes can only merge them, so the final trie fits)
+    uint32_t rel_trie = 0, trie_words = 0;
+    std::vector<uint16_t> prov;
+    if (trie) {
+        rel_key[0] = uint32_t(opt.tail.size()) * 4;
+        search_list(v6start, v6rep, opt.tail, img.fe_top[0], img.fe_n[0], rel_val[0], img.fe_k8[0]);
+        std::map<uint32_t, uint16_t> id;
+        for (uint32_t r : v4rep) {
+            if (id.size() >= 0xFFFFu && !id.count(r)) { why = "too many source classes for the IPv4 trie"; return false; }
+            prov.push_back(id.emplace(r, uint16_t(id.size())).first->second);
+        }
+        Trie tr;
+        if (!build_trie(v4b, uint32_t(v4b.size()), prov, 0u, 1u << 22, tr)) { why = "IPv4 source trie too large"; return false; }
+        trie_words = uint32_t(tr.words.size());
+        rel_trie = uint32_t(opt.tail.size()) * 4;
+        opt.tail.resize(opt.tail.size() + trie_words, 0u);
+        opt.tail.resize(align4(uint32_t(opt.tail.size())));
+        img.src_search.clear();
+        uint32_t n0;
+        search_list(s_start, s_rep, img.src_search, img.src_search_top, n0, img.src_search_val, img.src_search_k8);
     }
     // host-route hashes; their values (rows) are patched in once the core is laid out
     std::vector<uint32_t> pfx4, pfx6;                     // prefix index per hashed key
@@ -1649,6 +1711,8 @@ static bool build_cls16_one(const std::vector<SemRule>& sem, uint32_t n_rules, C
         img.fe_top[0] = top0;
         img.fe_n[0] = n0;
         img.src_search_val = rv0;
+        img.src_search_top = top0;
+        img.src_search_k8 = img.fe_k8[0];
         // IPv4-mapped: key = last 4 address bytes as a little-endian word
         std::vector<std::pair<uint32_t, uint32_t>> k4;
         for (uint32_t i = 0; i < side[0].pf[0].size(); ++i)
@@ -1712,6 +1776,20 @@ static bool build_cls16_one(const std::vector<SemRule>& sem, uint32_t n_rules, C
     for (int sd = hosts ? 1 : 0; sd < 2; ++sd) {
         img.fe_key[sd] = tail + rel_key[sd];
         img.fe_val[sd] = tail + rel_val[sd];
+    }
+    if (trie) {
+        Cls4Image& c = img.core;
+        for (uint32_t k = 0; k < img.fe_n[0]; ++k) c.words[img.fe_val[0] / 4 + k] = c.row_of(v6rep[k]);
+        std::vector<uint16_t> cls(v4rep.size());
+        for (size_t k = 0; k < v4rep.size(); ++k) cls[k] = uint16_t((c.row_of(v4rep[k]) - c.off_cells) / c.row_bytes);
+        Trie tr;
+        if (!build_trie(v4b, uint32_t(v4b.size()), cls, tail + rel_trie, 1u << 22, tr) || tr.words.size() > trie_words) {
+            why = "IPv4 source trie does not fit its reserved room";
+            return false;
+        }
+        std::copy(tr.words.begin(), tr.words.end(), c.words.begin() + (tail + rel_trie) / 4);
+        c.off_trie = tail + rel_trie;
+        c.trie_depth = tr.depth;
     }
     if (hosts) {
         Cls4Image& c = img.core;

@@ -256,17 +256,27 @@ bool build_cls4(const std::vector<SemRule>& sem, uint32_t n_rules, Cls4Image& im
 // fold[0] ^ w1 x fold[1] ^ w2 x fold[2] ^ w3, h = f x mul6.  Misses take the
 // family's default row.  The source interval table (src_mode 0's) stays in
 // global memory for the protocol > 2 fallback, which needs the rep.
+//
+// Source front end, src_mode 2 (sources not all host routes, many IPv4
+// intervals -- the IP-block lists of gen-policy.py): IPv4-mapped sources
+// through a trie over the address's IPv4 word straight to the class row (the
+// IPv4 classifier's source trie, at core.off_trie / core.trie_depth, leaves
+// carrying the core's classes), every other source through the interval
+// search of side 0 restricted to the non-IPv4 intervals, whose values are
+// rows (core mode 3).  The whole interval table stays in global memory for
+// protocols > 2, as in src_mode 1.
 struct Cls16Image {
     Cls4Image core;                // classifier over the rules in rep space
     std::vector<SemRule> sem;      // the rules in rep space (linear fallback)
     uint32_t fe_key[2] = {}, fe_val[2] = {}, fe_top[2] = {}, fe_n[2] = {};
     uint32_t fe_k8[2] = {};        // 8-B keys: key8(start) - 1 (see key8)
-    uint32_t src_mode = 0;         // 0: interval search -> rep; 1: host-route hashes -> row
+    uint32_t src_mode = 0;         // 0: interval search -> rep; 1: host-route hashes -> row; 2: IPv4 trie -> row
     uint32_t h4 = 0, cap4 = 0, mul4 = 0;
     uint32_t k6 = 0, r6 = 0, cap6 = 0, mul6 = 0, fold[3] = {};
     uint32_t dflt_row[2] = {};     // per family (0 IPv4, 1 IPv6)
-    std::vector<uint32_t> src_search;  // src_mode 1: the source interval table (keys, reps)
+    std::vector<uint32_t> src_search;  // src_mode 1, 2: the source interval table (keys, reps), global memory
     uint32_t src_search_val = 0;   // byte offset of its reps
+    uint32_t src_search_top = 0, src_search_k8 = 0;   // its padded key count, 8-B keys
 };
 __host__ __device__ inline uint32_t fold6(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3,
                                           const uint32_t* f) {

@@ -108,7 +108,7 @@ struct Table {
         std::vector<LinRule4> lin; // rules in rep space (FORCE_LINEAR)
         Cls4Image oimg;            // protocols > 2, rep space
         DevBuf d_img, d_lin, d_oimg;
-        DevBuf d_src_search;       // src_mode 1: the source interval table (global memory)
+        DevBuf d_src_search;       // src_mode 1, 2: the source interval table (global memory)
         bool lds_resident = false;
         DevBuf d_slot_rule;        // slot mode (connection batches): slot -> rule, core then OTHER image
     } p16;
@@ -424,7 +424,7 @@ static int table_put_locked(cls_engine* e, const char* name, const cls_rule* rul
                 HIPC(e, hipMemcpy(q.d_lin.p, q.lin.data(), q.lin.size() * sizeof(LinRule4), hipMemcpyHostToDevice));
             const int rc2 = counters_init(e, t->c16, &c, &q.oimg, n);
             if (rc2 != CLS_OK) return rc2;
-            if (q.img.src_mode == 1) {
+            if (q.img.src_mode >= 1) {
                 HIPC(e, q.d_src_search.ensure(q.img.src_search.size() * 4));
                 HIPC(e, hipMemcpy(q.d_src_search.p, q.img.src_search.data(), q.img.src_search.size() * 4,
                                   hipMemcpyHostToDevice));
@@ -687,8 +687,12 @@ static Fe16 fe16(const Cls16Image& m, const DevBuf& d_src_search) {
         for (int i = 0; i < 3; ++i) fe.fold[i] = m.fold[i];
         fe.dflt4 = m.dflt_row[0];
         fe.dflt6 = m.dflt_row[1];
+    }
+    if (m.src_mode >= 1) {                         // protocols > 2 need the rep: the global table
         fe.gsrc = d_src_search.as<uint8_t>();
         fe.gval = m.src_search_val;
+        fe.gtop = m.src_search_top;
+        fe.gk8 = m.src_search_k8;
     }
     return fe;
 }
@@ -1813,9 +1817,11 @@ int cls_compile_v16(const cls_rule* rules, uint32_t n, void* blob, uint64_t cap,
     h16.dflt_row[0] = img.dflt_row[0];
     h16.dflt_row[1] = img.dflt_row[1];
     h16.src_search_val = img.src_search_val;
+    h16.src_search_top = img.src_search_top;
+    h16.src_search_k8 = img.src_search_k8;
     const size_t extra = sizeof h16 - sizeof h16.core;
     return write_blob(&img.core, linear4(img.sem), n, 0x434C3136u, reinterpret_cast<const uint8_t*>(&h16) + sizeof h16.core,
-                      extra, blob, cap, need, img.src_mode == 1 ? &img.src_search : nullptr,
+                      extra, blob, cap, need, img.src_mode >= 1 ? &img.src_search : nullptr,
                       offsetof(cls_image_v16_header, off_src_search) - sizeof h16.core, &oimg);
 }
 

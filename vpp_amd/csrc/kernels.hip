@@ -216,7 +216,7 @@ __global__ __launch_bounds__(1024) void finish16_kernel(FinishArgs f, Cls4Dev t,
     finish_body(f, o, verdict, [&](uint32_t k, uint32_t& s, uint32_t& d, uint32_t& dp) {
         const uint4 s16[1] = {p.src[k]}, d16[1] = {p.dst[k]};
         uint32_t s1[1], d1[1];
-        if (fe.src_mode == 1) s1[0] = src_rep_global(fe.gsrc, fe.gval, fe.top[0], fe.k8[0], s16[0]);
+        if (fe.src_mode >= 1) s1[0] = src_rep_global(fe.gsrc, fe.gval, fe.gtop, fe.gk8, s16[0]);
         else fe_rep(gim, fe.key[0], fe.val[0], fe.top[0], fe.k8[0], s16, s1);
         fe_rep(gim, fe.key[1], fe.val[1], fe.top[1], fe.k8[1], d16, d1);
         s = s1[0];

@@ -36,8 +36,9 @@ struct Fe16 {
     uint32_t h4, cap4, mul4, s4_0, s4_1, L4;             // IPv4-mapped hash (s0 = 32 - L, s1 = 32 - 2 L)
     uint32_t k6, r6, cap6, mul6, s6_0, s6_1, L6, fold[3]; // IPv6 hash
     uint32_t dflt4, dflt6;     // rows of the families' sources no prefix covers
-    const uint8_t* gsrc;       // src_mode 1: the source interval table in global memory
-    uint32_t gval;             // (keys at 0, reps at gval; fe.top[0] keys)
+    const uint8_t* gsrc;       // src_mode 1, 2: the source interval table in global memory
+    uint32_t gval;             // (keys at 0, reps at gval; gtop keys, 8 B when gk8)
+    uint32_t gtop, gk8;
 };
 
 struct Cls4Dev {

@@ -852,9 +852,34 @@ __device__ __forceinline__ void src_hash16(const Img<kLds>& im, const Fe16& fe, 
     }
 }
 
+// Source rows of N 16-byte addresses, src_mode 2 (compile.hpp Cls16Image):
+// IPv4-mapped addresses through the trie over their IPv4 word (the core's
+// off_trie / trie_depth, leaves carrying core classes: src_row mode 4), the
+// others through the interval search over the non-IPv4 intervals, whose
+// values are rows -- taken only when some lane of the wave holds one.
+template <int N, bool kLds>
+__device__ __forceinline__ void src_trie16(const Img<kLds>& im, const Cls4Dev& t, const Fe16& fe, const uint4 (&a)[N],
+                                           uint32_t (&row)[N]) {
+    uint32_t ip[N];
+    bool v6 = false;
+#pragma unroll
+    for (int q = 0; q < N; ++q) {
+        ip[q] = __builtin_bswap32(a[q].w);
+        v6 |= !((a[q].x | a[q].y) == 0u && a[q].z == 0xFFFF0000u);
+    }
+    src_row<N, kLds, 4>(im, t, ip, row);
+    if (__any(v6)) {
+        uint32_t r6[N];
+        fe_rep(im, fe.key[0], fe.val[0], fe.top[0], fe.k8[0], a, r6);
+#pragma unroll
+        for (int q = 0; q < N; ++q)
+            row[q] = ((a[q].x | a[q].y) == 0u && a[q].z == 0xFFFF0000u) ? row[q] : r6[q];
+    }
+}
+
 // The source rep of one address from the global-memory interval table
-// (src_mode 1, protocol > 2 lanes only): out of line, so the rare path costs
-// the hot loop no registers.
+// (src_mode 1 and 2, protocol > 2 lanes only): out of line, so the rare path
+// costs the hot loop no registers.
 [[maybe_unused]] __device__ __noinline__ uint32_t src_rep_global(const uint8_t* g, uint32_t gval, uint32_t top, uint32_t k8,
                                                 uint4 a) {
     const uint4 a1[1] = {a};
@@ -877,11 +902,11 @@ __global__ __launch_bounds__(kClsBlock) void classify16_cls(Cls4Dev t, Cls4Dev o
     const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t hot0 = 0;
     const uint32_t hot_lane = t.off_hot + 4u * (threadIdx.x & 63u);
-    // src_mode 1 keeps the source interval table in global memory: reps for
-    // the linear paths (protocol > 2 fallback, CLS_F_FORCE_LINEAR)
+    // src_mode 1 and 2 keep the source interval table in global memory: reps
+    // for the linear paths (protocol > 2 fallback, CLS_F_FORCE_LINEAR)
     const Img<false> gim{fe.gsrc};
     auto src_rep = [&](const auto& a, auto& out) {
-        if constexpr (kFe == 1) fe_rep(gim, 0u, fe.gval, fe.top[0], fe.k8[0], a, out);
+        if constexpr (kFe >= 1) fe_rep(gim, 0u, fe.gval, fe.gtop, fe.gk8, a, out);
         else fe_rep(im, fe.key[0], fe.val[0], fe.top[0], fe.k8[0], a, out);
     };
     auto classify = [&](const auto& s16, const auto& d16, auto& pa, auto& ra, bool other, auto& v, const auto& ix) {
@@ -891,13 +916,14 @@ __global__ __launch_bounds__(kClsBlock) void classify16_cls(Cls4Dev t, Cls4Dev o
         if constexpr (kLin) {
             src_rep(s16, sa);
             lin_n(t, gslot + o.n_ctr, sa, da, pa, ra, v);   // direct rule slots after both images
-        } else if constexpr (kFe == 1) {
-            src_hash16(im, fe, s16, sa);                       // class rows, not reps
+        } else if constexpr (kFe >= 1) {
+            if constexpr (kFe == 1) src_hash16(im, fe, s16, sa);   // class rows, not reps
+            else src_trie16(im, t, fe, s16, sa);
             uint32_t sl[N];
             if (__any(other)) {                                // rare: protocols > 2 need the rep
 #pragma unroll
                 for (int q = 0; q < N; ++q)
-                    sl[q] = ra[q] > 2u ? src_rep_global(fe.gsrc, fe.gval, fe.top[0], fe.k8[0], s16[q]) : 0u;
+                    sl[q] = ra[q] > 2u ? src_rep_global(fe.gsrc, fe.gval, fe.gtop, fe.gk8, s16[q]) : 0u;
             }
             run_n<N, kLds, kMode, kList, kD, kCtr>(im, t, o, hot_lane, gslot, hot0, sa, da, pa, ra, other, v, sl, ix,
                                                    oq_lds);
@@ -1074,7 +1100,7 @@ static void launch16_cls(const Cls4Dev& t, const Fe16& fe, const Pkts16& p, uint
             return;
         }
     }
-    if constexpr (kLds && (kList == 3 || kList == 4)) {
+    if constexpr (kLds && (kList == 3 || kList == 4) && kFe != 2) {
         switch (int(t.bv_steps)) {
         case 0: launch16_d<kLds, kMode, kList, 0, false, kFe>(t, fe, p, verdict, gslot, cfg); return;
         case 1: launch16_d<kLds, kMode, kList, 1, false, kFe>(t, fe, p, verdict, gslot, cfg); return;
@@ -1092,7 +1118,7 @@ template <bool kLds>
 static void dispatch16(const Cls4Dev& t, const Fe16& fe, const Pkts16& p, uint8_t* verdict,
                        unsigned long long* gslot, bool lin, const LaunchCfg& cfg) {
     if (lin) {
-        if (fe.src_mode == 1) launch16_d<kLds, 0, 0, -1, true, 1>(t, fe, p, verdict, gslot, cfg);
+        if (fe.src_mode >= 1) launch16_d<kLds, 0, 0, -1, true, 1>(t, fe, p, verdict, gslot, cfg);
         else launch16_d<kLds, 0, 0, -1, true, 0>(t, fe, p, verdict, gslot, cfg);
         return;
     }
@@ -1105,6 +1131,19 @@ static void dispatch16(const Cls4Dev& t, const Fe16& fe, const Pkts16& p, uint8_
         case 4: launch16_cls<kLds, 3, 4, 1>(t, fe, p, verdict, gslot, cfg); break;
         case 5: if constexpr (kLds) launch16_cls<kLds, 3, 5, 1>(t, fe, p, verdict, gslot, cfg); break;
         case 6: if constexpr (kLds) launch16_cls<kLds, 3, 6, 1>(t, fe, p, verdict, gslot, cfg); break;
+        default: break;
+        }
+        return;
+    }
+    if (fe.src_mode == 2) {                      // rows from the IPv4 trie / non-IPv4 search (core mode 3)
+        switch (t.list_mode) {
+        case 0: launch16_cls<kLds, 3, 0, 2>(t, fe, p, verdict, gslot, cfg); break;
+        case 1: launch16_cls<kLds, 3, 1, 2>(t, fe, p, verdict, gslot, cfg); break;
+        case 2: launch16_cls<kLds, 3, 2, 2>(t, fe, p, verdict, gslot, cfg); break;
+        case 3: launch16_cls<kLds, 3, 3, 2>(t, fe, p, verdict, gslot, cfg); break;
+        case 4: launch16_cls<kLds, 3, 4, 2>(t, fe, p, verdict, gslot, cfg); break;
+        case 5: if constexpr (kLds) launch16_cls<kLds, 3, 5, 2>(t, fe, p, verdict, gslot, cfg); break;
+        case 6: if constexpr (kLds) launch16_cls<kLds, 3, 6, 2>(t, fe, p, verdict, gslot, cfg); break;
         default: break;
         }
         return;
@@ -1202,6 +1241,19 @@ template <bool kLds>
 static void dispatch_slots16(const Cls4Dev& t, const Fe16& fe, const Pkts16& p, uint32_t* out,
                              const LaunchCfg& cfg) {
     uint8_t* o = reinterpret_cast<uint8_t*>(out);
+    if (fe.src_mode == 2) {
+        switch (t.list_mode) {
+        case 0: launch16_d<kLds, 3, 0, -1, false, 2, 2>(t, fe, p, o, nullptr, cfg); break;
+        case 1: launch16_d<kLds, 3, 1, -1, false, 2, 2>(t, fe, p, o, nullptr, cfg); break;
+        case 2: launch16_d<kLds, 3, 2, -1, false, 2, 2>(t, fe, p, o, nullptr, cfg); break;
+        case 3: launch16_d<kLds, 3, 3, -1, false, 2, 2>(t, fe, p, o, nullptr, cfg); break;
+        case 4: launch16_d<kLds, 3, 4, -1, false, 2, 2>(t, fe, p, o, nullptr, cfg); break;
+        case 5: if constexpr (kLds) launch16_d<kLds, 3, 5, -1, false, 2, 2>(t, fe, p, o, nullptr, cfg); break;
+        case 6: if constexpr (kLds) launch16_d<kLds, 3, 6, -1, false, 2, 2>(t, fe, p, o, nullptr, cfg); break;
+        default: break;
+        }
+        return;
+    }
     if (fe.src_mode == 1) {
         switch (t.list_mode) {
         case 0: launch16_d<kLds, 3, 0, -1, false, 1, 2>(t, fe, p, o, nullptr, cfg); break;
