@@ -28,6 +28,7 @@ import "C"
 
 import (
 	"errors"
+	"fmt"
 	"net"
 	"runtime"
 	"strings"
@@ -70,6 +71,10 @@ type podConfig struct {
 // New replaces NewMockACLEngine (aclengine_mock.go:124).  device: HIP device
 // ordinal, -1 for the current one.
 func New(c contiv.API, device int) (*Engine, error) {
+	// the library this binding was written against (include/contivcls.h)
+	if v := C.cls_abi_version(); v != C.CLS_ABI_VERSION {
+		return nil, fmt.Errorf("contivcls: library ABI %d, binding ABI %d", int(v), int(C.CLS_ABI_VERSION))
+	}
 	var e *C.cls_engine
 	var cfg C.cls_config
 	cfg.device = C.int(device)

@@ -160,6 +160,9 @@ struct cls_engine {
     DevBuf s_src, s_dst, s_sport, s_dport, s_proto, s_verdict, s_if_a, s_if_b, s_desc, s_ifs;
     DevBuf s_pre;                  // connection path: classifier slot words per large ACL (8 bytes/connection)
     DevBuf s_rules, s_tctr, s_cctr;  // connection path: rule pool, table counter pointers, call counters
+    // what s_desc, s_ifs, s_rules and s_tctr hold (the last upload): a
+    // connection batch over unchanged bindings uploads nothing
+    std::vector<uint8_t> up_desc, up_ifs, up_rules, up_tctr;
     DevBuf s_pool;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool timed = false;
@@ -1470,13 +1473,24 @@ int cls_connect_batch(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t*
     int cmode = 0;
     if (count && n_ctr) cmode = lds_used + size_t(n_ctr) * 4 <= lds_max && !(no_lds & 2) ? 1 : 2;
     a.ctr_lds = uint32_t(lds_used);
-    HIPC(e, e->s_desc.ensure(std::max<size_t>(1, desc.size()) * sizeof(ConnDesc)));
-    HIPC(e, e->s_ifs.ensure(ifs.size() * sizeof(IfAcls)));
-    HIPC(e, e->s_rules.ensure(std::max<size_t>(16, pool.size())));
-    if (!desc.empty())
-        HIPC(e, hipMemcpyAsync(e->s_desc.p, desc.data(), desc.size() * sizeof(ConnDesc), hipMemcpyHostToDevice, s));
-    HIPC(e, hipMemcpyAsync(e->s_ifs.p, ifs.data(), ifs.size() * sizeof(IfAcls), hipMemcpyHostToDevice, s));
-    if (!pool.empty()) HIPC(e, hipMemcpyAsync(e->s_rules.p, pool.data(), pool.size(), hipMemcpyHostToDevice, s));
+    // the call's tables, uploaded only when they differ from the last upload
+    // (same bindings, same batch kind: nothing to copy)
+    auto upload = [&](DevBuf& d, std::vector<uint8_t>& last, const void* src, size_t bytes, size_t min_bytes) -> int {
+        const void* was = d.p;
+        HIPC(e, d.ensure(std::max(bytes, min_bytes)));
+        const uint8_t* b = static_cast<const uint8_t*>(src);
+        if (d.p == was && last.size() == bytes && (bytes == 0 || std::memcmp(last.data(), b, bytes) == 0))
+            return CLS_OK;
+        if (bytes) HIPC(e, hipMemcpyAsync(d.p, b, bytes, hipMemcpyHostToDevice, s));
+        last.assign(b, b + bytes);
+        return CLS_OK;
+    };
+    {
+        int rc = upload(e->s_desc, e->up_desc, desc.data(), desc.size() * sizeof(ConnDesc), sizeof(ConnDesc));
+        if (rc == CLS_OK) rc = upload(e->s_ifs, e->up_ifs, ifs.data(), ifs.size() * sizeof(IfAcls), sizeof(IfAcls));
+        if (rc == CLS_OK) rc = upload(e->s_rules, e->up_rules, pool.data(), pool.size(), 16);
+        if (rc != CLS_OK) return rc;
+    }
     a.desc = e->s_desc.as<ConnDesc>();
     a.pre = big.empty() ? nullptr : e->s_pre.as<uint32_t>();
     a.pre_stride = stride;
@@ -1496,8 +1510,8 @@ int cls_connect_batch(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t*
             if (t.conn_ctr_ev && s != e->stream) HIPC(e, hipStreamWaitEvent(s, t.conn_ctr_ev, 0));
             tctr.push_back(t.d_conn_ctr.as<unsigned long long>());
         }
-        HIPC(e, e->s_tctr.ensure(tctr.size() * sizeof(void*)));
-        HIPC(e, hipMemcpyAsync(e->s_tctr.p, tctr.data(), tctr.size() * sizeof(void*), hipMemcpyHostToDevice, s));
+        const int rc = upload(e->s_tctr, e->up_tctr, tctr.data(), tctr.size() * sizeof(void*), sizeof(void*));
+        if (rc != CLS_OK) return rc;
     }
     // The descriptor and interface tables go to LDS after the pool and the
     // counters when they fit (else the kernel reads them from global memory).
