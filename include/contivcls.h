@@ -203,6 +203,10 @@ int cls_last_kernel_ms(cls_engine* e, float* ms);
  * durations in launch order; *count = number recorded.  Recording enqueues
  * only events (no host synchronisation); reading blocks on the last one. */
 int cls_kernel_times(cls_engine* e, float* ms, uint32_t cap, uint32_t* count);
+/* The same kernels' start times, milliseconds after the first one's: the
+ * differences are the launch-to-launch period of a stream of timed calls
+ * (each kernel stamps its own start, so no event marker sits between them). */
+int cls_kernel_starts(cls_engine* e, float* ms, uint32_t cap, uint32_t* count);
 int cls_kernel_times_reset(cls_engine* e);
 
 /* Measurement only (bench.py): the classify kernel's HBM stream without the

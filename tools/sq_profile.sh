@@ -1,5 +1,7 @@
 #!/bin/bash
 # SQ/LDS counter passes of the classify kernel (run on the GPU box).
+# usage: tools/sq_profile.sh <tag> [bench.py args]; SQ_CMD="python3 ..." profiles
+# another command (e.g. tools/genpolicy_bench.py) instead of bench.py.
 set -e -o pipefail
 TAG=$1; shift
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
@@ -7,7 +9,7 @@ OUT=$ROOT/gpurun_out/sq_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
 cd /tmp
-B="python3 $ROOT/bench.py --steps 2 --warmup 1 --settle-ms 0 --cpu-sample 0 $@"
+B=${SQ_CMD:-"python3 $ROOT/bench.py --steps 2 --warmup 1 --settle-ms 0 --cpu-sample 0 $@"}
 timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_LDS_BANK_CONFLICT -d $OUT/a -o run --output-format csv -- $B > $OUT/a.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SALU SQ_ACTIVE_INST_LDS SQ_LDS_IDX_ACTIVE SQ_INST_CYCLES_VMEM GRBM_GUI_ACTIVE -d $OUT/b -o run --output-format csv -- $B > $OUT/b.log 2>&1
 python3 - "$OUT" <<'PY'

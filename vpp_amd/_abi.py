@@ -43,7 +43,7 @@ R_ICMP, R_ICMP_CODE, R_ICMP_TYPE, R_ICMPV6, R_ACTIONS = 2048, 4096, 8192, 16384,
 # the exported symbols (checked by tests/test_abi.py against include/contivcls.h)
 SYMBOLS = ["cls_abi_version", "cls_engine_create", "cls_engine_destroy", "cls_last_error",
            "cls_table_put", "cls_table_del", "cls_table_get_info", "cls_classify",
-           "cls_last_kernel_ms", "cls_kernel_times", "cls_kernel_times_reset", "cls_acl_put", "cls_acl_del", "cls_acl_table", "cls_acl_counts",
+           "cls_last_kernel_ms", "cls_kernel_times", "cls_kernel_starts", "cls_kernel_times_reset", "cls_acl_put", "cls_acl_del", "cls_acl_table", "cls_acl_counts",
            "cls_if_id",
            "cls_if_acls", "cls_connect_batch", "cls_gen_traffic_v4", "cls_compile_v4", "cls_image_kernel",
            "cls_compile_v16", "cls_gen_traffic_v16", "cls_stream_floor", "cls_stream_floor_shapes", "cls_stream_floor_conn", "cls_conn_bitmap_eval", "cls_conn_counters",
@@ -170,6 +170,7 @@ def bind(path: str, strict: bool = True):
         "cls_classify": (C.c_int, [vp, u32, C.POINTER(PktSoa), u64, vp, vp, u32, vp]),
         "cls_last_kernel_ms": (C.c_int, [vp, C.POINTER(C.c_float)]),
         "cls_kernel_times": (C.c_int, [vp, C.POINTER(C.c_float), u32, C.POINTER(u32)]),
+        "cls_kernel_starts": (C.c_int, [vp, C.POINTER(C.c_float), u32, C.POINTER(u32)]),
         "cls_kernel_times_reset": (C.c_int, [vp]),
         "cls_stream_floor": (C.c_int, [vp, C.POINTER(PktSoa), u64, vp, u32, C.POINTER(C.c_float), vp]),
         "cls_conn_bitmap_eval": (C.c_int, [C.POINTER(ClsRule), u32, vp, vp, vp, vp, u64, vp, vp]),

@@ -492,11 +492,15 @@ constexpr uint32_t kConnClsWork = 2048;            // ... when touches x rules >
 constexpr uint32_t kConnClsDevRules = 2048;        // ... when it has this many rules (device batch)
 constexpr uint32_t kConnBmMinRules = 8;            // linear IPv4 ACLs given the bitmap form (conn_bitmap4) ...
 constexpr size_t kConnBmMaxWords = 12288;          // ... when their tables take at most 48 KiB
-constexpr size_t kConnJobsLds = 16 * kConnJobBytes; // connect_kernel: the 16 waves' job areas (LDS)
 
 static bool aligned(const void* p, size_t a) { return (reinterpret_cast<uintptr_t>(p) % a) == 0; }
 
-static int timing_begin(cls_engine* e, hipStream_t s) {
+// The event pair of a timed call (CLS_F_TIMING): stamped by the classify
+// launch itself -- start of its first chunk's kernel, end of its last one's
+// (hipExtLaunchKernel, part of the dispatch: no marker packets between the
+// kernels, which cost a step several microseconds each) -- or recorded around
+// the call when it has no classify launch.
+static int timing_pair(cls_engine* e) {
     if (e->ev_used == e->ev_pool.size()) {
         hipEvent_t a, b;
         HIPC(e, hipEventCreate(&a));
@@ -506,7 +510,6 @@ static int timing_begin(cls_engine* e, hipStream_t s) {
     e->ev0 = e->ev_pool[e->ev_used].first;
     e->ev1 = e->ev_pool[e->ev_used].second;
     e->ev_used++;
-    HIPC(e, hipEventRecord(e->ev0, s));
     return CLS_OK;
 }
 
@@ -575,8 +578,12 @@ static int cls_grid(const cls_engine* e, bool use_cls, bool lds_resident, uint32
     if (use_cls) {
         const int by_threads = 2048 / cls_block();
         per_cu = by_threads;
-        if (lds_resident)
-            per_cu = std::max(1, std::min(by_threads, int(max_lds_bytes() / (lds_bytes + kLdsReserved))));
+        // LDS-resident images: one 1024-thread workgroup per CU, also when two
+        // would fit -- half the image stagings and counter rows, and the
+        // stream runs faster in that shape (config 2: 0.0363 against 0.0392
+        // ms, profiles/r04d_bench_c2{_wg1,}.json; the config-3 stream floor
+        // 0.519 against 0.538 ms)
+        if (lds_resident) per_cu = 1;
         if (const char* w = std::getenv("CONTIVCLS_WG_PER_CU"))   // diagnostics
             per_cu = std::max(1, std::min(by_threads, std::atoi(w)));
     }
@@ -652,9 +659,10 @@ static int finish_counts(cls_engine* e, const Table& t, const Counters& c, Scrat
                          uint64_t n, uint8_t* verdict_out, const uint8_t* d_verdict, uint64_t* counters_out,
                          uint32_t flags, hipStream_t s, bool remapped = false) {
     const bool dev = flags & CLS_F_DEVICE;
-    if (!remapped)
+    if (!remapped) {
         HIPC(e, launch_remap(sc->slot_val.as<unsigned long long>(), c.d_csr.as<uint2>(), c.n_slots, co.out, s));
-    HIPC(e, hipEventRecord(sc->done, s));
+        HIPC(e, hipEventRecord(sc->done, s));        // (a finish launch stamps it itself)
+    }
     if (!dev) {
         if (verdict_out && n) HIPC(e, hipMemcpyAsync(verdict_out, d_verdict, n, hipMemcpyDeviceToHost, s));
         std::vector<uint64_t> tmp;
@@ -751,8 +759,9 @@ static int classify16_locked(cls_engine* e, std::shared_ptr<Table> t, const cls_
     cfg.grid = cls_grid(e, true, q.lds_resident, c.lds_bytes, n);
     const bool timing = flags & CLS_F_TIMING;
     if (timing) {
-        const int rc = timing_begin(e, s);
+        const int rc = timing_pair(e);
         if (rc != CLS_OK) return rc;
+        if (!n) HIPC(e, hipEventRecord(e->ev0, s));
     }
     bool zeroed = false, remapped = false;
     if (n) {
@@ -774,12 +783,13 @@ static int classify16_locked(cls_engine* e, std::shared_ptr<Table> t, const cls_
             pc.vec = aligned(pc.dport, 8) && aligned(pc.proto, 4) && (!vo || aligned(vo, 4)) ? 1u : 0u;
             cd.zero = co.zero && !zeroed ? co.out : nullptr;    // the first launch clears the call's counters
             cd.n_zero = t->n_rules + 1;
+            cfg.ev_start = timing && off == 0 ? e->ev0 : nullptr;
+            cfg.ev_stop = timing && off + m >= n ? e->ev1 : nullptr;
             HIPC(e, launch_classify16_cls(cd, fe, pc, vo, slot_val, q.lds_resident, lin, cfg));
             zeroed = true;
             cd.zero = nullptr;
-            if (timing && off + m >= n) HIPC(e, hipEventRecord(e->ev1, s));
             HIPC(e, launch_finish16(finish_args(t->c16, sc, cd, co, q.lds_resident, uint32_t(cfg.grid), off + m >= n),
-                                    cd, cfg.other, fe, pc, vo, s));
+                                    cd, cfg.other, fe, pc, vo, s, off + m >= n ? sc->done : nullptr));
             remapped = true;
         }
     }
@@ -844,8 +854,9 @@ int cls_classify(cls_engine* e, uint32_t table_id, const cls_pkt_soa* pk, uint64
 
     const bool timing = flags & CLS_F_TIMING;
     if (timing) {
-        const int rc = timing_begin(e, s);
+        const int rc = timing_pair(e);
         if (rc != CLS_OK) return rc;
+        if (!(n && use_cls)) HIPC(e, hipEventRecord(e->ev0, s));
     }
     bool zeroed = false, remapped = false;
     if (n) {
@@ -865,12 +876,13 @@ int cls_classify(cls_engine* e, uint32_t table_id, const cls_pkt_soa* pk, uint64
                 uint8_t* vo = d_verdict ? d_verdict + off : nullptr;
                 cd.zero = co.zero && !zeroed ? co.out : nullptr;   // the first launch clears the call's counters
                 cd.n_zero = t->n_rules + 1;
+                cfg.ev_start = timing && off == 0 ? e->ev0 : nullptr;
+                cfg.ev_stop = timing && off + m >= n ? e->ev1 : nullptr;
                 HIPC(e, launch_classify4_cls(cd, pc, vo, slot_val, t->lds_resident, vec, cfg));
                 zeroed = true;
                 cd.zero = nullptr;
-                if (timing && off + m >= n) HIPC(e, hipEventRecord(e->ev1, s));
                 HIPC(e, launch_finish4(finish_args(t->c4, sc, cd, co, t->lds_resident, uint32_t(cfg.grid), off + m >= n),
-                                       cfg.other, pc, vo, s));
+                                       cfg.other, pc, vo, s, off + m >= n ? sc->done : nullptr));
                 remapped = true;
             }
         } else {
@@ -880,8 +892,8 @@ int cls_classify(cls_engine* e, uint32_t table_id, const cls_pkt_soa* pk, uint64
         }
     }
     if (timing) {
-        // ev1 brackets the classify kernel itself (recorded above, before the
-        // fold of the workgroup partials)
+        // ev0 / ev1: the classify kernel's own start and end (stamped by its
+        // launch, before the fold of the workgroup partials)
         if (!(n && use_cls)) HIPC(e, hipEventRecord(e->ev1, s));
         e->timed = true;
     }
@@ -989,6 +1001,17 @@ int cls_kernel_times(cls_engine* e, float* ms, uint32_t cap, uint32_t* count) {
     HIPC(e, hipEventSynchronize(e->ev_pool[e->ev_used - 1].second));
     for (size_t i = 0; i < e->ev_used && i < cap && ms; ++i)
         HIPC(e, hipEventElapsedTime(&ms[i], e->ev_pool[i].first, e->ev_pool[i].second));
+    return CLS_OK;
+}
+
+int cls_kernel_starts(cls_engine* e, float* ms, uint32_t cap, uint32_t* count) {
+    if (!e || !count) return CLS_E_INVAL;
+    std::lock_guard<std::mutex> g(e->mu);
+    *count = uint32_t(e->ev_used);
+    if (e->ev_used == 0) return CLS_OK;
+    HIPC(e, hipEventSynchronize(e->ev_pool[e->ev_used - 1].second));
+    for (size_t i = 0; i < e->ev_used && i < cap && ms; ++i)
+        HIPC(e, hipEventElapsedTime(&ms[i], e->ev_pool[0].first, e->ev_pool[i].first));
     return CLS_OK;
 }
 
@@ -1428,7 +1451,7 @@ int cls_connect_batch(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t*
     if (!k16 && n && !(flags & CLS_F_FORCE_LINEAR) && !(bme && std::atoi(bme) == 0)) {
         // the LDS counters take their share only when they can be LDS counters
         // at all (otherwise they are global, cmode 2); no subtraction wraps
-        const size_t ctr_b = count ? size_t(n_ctr) * 4 : 0, reserve = std::min<size_t>(lds_max0 / 8, 8192) + kConnJobsLds;
+        const size_t ctr_b = count ? size_t(n_ctr) * 4 : 0, reserve = std::min<size_t>(lds_max0 / 8, 8192);
         const size_t ctr_lds = ctr_b + reserve <= lds_max0 ? ctr_b : 0;
         const size_t cap = lds_max0 - reserve - ctr_lds;
         std::vector<size_t> order;
@@ -1463,11 +1486,10 @@ int cls_connect_batch(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t*
     // LDS: the rule pool first (every evaluation step reads it), then the u32
     // counters if they fit beside it; otherwise global-memory variants
     // (CONTIVCLS_CONN_NO_LDS, tests: bit 0 rules from global memory, bit 1
-    // global counters, bit 2 descriptor / interface tables from global memory).
-    // The waves' job areas (kConnJobsLds) always go last.
+    // global counters, bit 2 descriptor / interface tables from global memory)
     const char* nl = std::getenv("CONTIVCLS_CONN_NO_LDS");
     const int no_lds = nl ? std::atoi(nl) : 0;
-    const size_t lds_max = size_t(max_lds_bytes()) - kConnJobsLds;
+    const size_t lds_max = size_t(max_lds_bytes());
     const bool lds_rules = n && !pool.empty() && pool.size() <= lds_max && !(no_lds & 1);
     const size_t lds_used = lds_rules ? pool.size() : 0;
     int cmode = 0;
@@ -1515,8 +1537,9 @@ int cls_connect_batch(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t*
     }
     // The descriptor and interface tables go to LDS after the pool and the
     // counters when they fit (else the kernel reads them from global memory).
-    // Persistent grid: as many 1024-thread workgroups per CU as the LDS
-    // allows, at most two.
+    // Persistent grid: as many 512-thread workgroups per CU as the LDS
+    // allows, at most three (the kernel's registers allow 24 waves per CU);
+    // where it allows only one, one 1024-thread workgroup.
     a.n_desc = uint32_t(desc.size());
     size_t lds = lds_used + (cmode == 1 ? size_t(n_ctr) * 4 : 0);
     const size_t meta_at = (lds + 15) & ~size_t(15);
@@ -1524,18 +1547,16 @@ int cls_connect_batch(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t*
     a.meta_lds = 0xFFFFFFFFu;
     // ... unless they would cost a workgroup per CU (the pool and counters
     // alone leave room for two)
-    auto per_cu_of = [&](size_t b) {
-        return std::max(1, std::min(2, int(size_t(max_lds_bytes()) / (((b + 15) & ~size_t(15)) + kConnJobsLds))));
-    };
+    auto per_cu_of = [&](size_t b) { return b ? std::max(1, std::min(3, int(lds_max / b))) : 3; };
     if (meta_at + meta <= lds_max && per_cu_of(meta_at + meta) == per_cu_of(lds) && !(no_lds & 4)) {
         a.meta_lds = uint32_t(meta_at);
         lds = meta_at + meta;
     }
-    a.jobs_lds = uint32_t((lds + 15) & ~size_t(15));
-    lds = a.jobs_lds + kConnJobsLds;
-    const int per_cu = std::max(1, std::min(2, int(size_t(max_lds_bytes()) / lds)));
-    const int grid = int(std::max<uint64_t>(1, std::min<uint64_t>(uint64_t(e->n_cu) * per_cu, (n + 1023) / 1024)));
-    HIPC(e, launch_connect(a, k16, lds_rules, cmode, grid, lds, s));
+    const int per_cu = per_cu_of(lds);
+    const int block = per_cu >= 2 ? 512 : 1024;
+    const int grid = int(std::max<uint64_t>(1, std::min<uint64_t>(uint64_t(e->n_cu) * per_cu,
+                                                                  (n + block - 1) / block)));
+    HIPC(e, launch_connect(a, k16, lds_rules, cmode, grid, block, lds, s));
     if (cmode && n)
         HIPC(e, launch_conn_scatter(a.desc, e->s_tctr.as<unsigned long long* const>(), uint32_t(desc.size()),
                                     e->s_cctr.as<unsigned long long>(), s));

@@ -522,9 +522,9 @@ __device__ __forceinline__ uint32_t conn_bm(const ConnArgs& a, const ConnDesc& D
 //    for this connection (classify4_pair / the slot launches); a call on a
 //    linear ACL is a *job*: the bitmap search (IPv4, conn_bm) or the rule
 //    scan.  The jobs of all four possible calls of the wave's 64 connections
-//    are packed into the wave's LDS job area and run 64 at a time, every
-//    lane on one job with its connection's fields fetched from the owning
-//    lane (ds_bpermute).  A lane-per-call loop would make the wave run the
+//    are packed (ranks from the calls' ballots, no LDS) and run 64 at a time,
+//    every lane on one job with its connection's fields fetched from the
+//    owning lane (ds_bpermute).  A lane-per-call loop would make the wave run the
 //    search once per call index in which any of its lanes has a job -- four
 //    passes per wave with ~0.6 jobs per connection -- where packing runs
 //    one.  Jobs are evaluated whether or not testConnection reaches the call
@@ -539,6 +539,10 @@ __device__ __forceinline__ uint32_t conn_bm(const ConnArgs& a, const ConnDesc& D
 // non-nil ACL -> the call's counter space (descriptor ctr_off + rule), in LDS
 // (u32, folded into the u64 counters at the end) or with wave-aggregated
 // global atomics.
+// Workgroup size (launch_connect): the kernel holds ~75 VGPRs (6 waves per
+// SIMD), so 24 waves fit a CU -- three 512-thread workgroups where the LDS
+// allows two or more, else one 1024-thread workgroup (16 waves rather than
+// the 8 of one 512-thread one); forcing 64 VGPRs spills to scratch.
 template <bool k16, bool kLdsRules, int kCount>
 __global__ __launch_bounds__(1024) void connect_kernel(ConnArgs a) {
     typedef typename ConnT<k16>::A A;
@@ -561,7 +565,6 @@ __global__ __launch_bounds__(1024) void connect_kernel(ConnArgs a) {
     __syncthreads();
     const uint32_t lane = __lane_id();
     const uint64_t lt = (1ull << lane) - 1ull;
-    const uint32_t jobs = a.jobs_lds + (threadIdx.x >> 6) * kConnJobBytes, results = jobs + 1024u;
     const A* src = static_cast<const A*>(a.src);
     const A* dst = static_cast<const A*>(a.dst);
     const uint64_t nthreads = uint64_t(gridDim.x) * blockDim.x;
@@ -588,26 +591,31 @@ __global__ __launch_bounds__(1024) void connect_kernel(ConnArgs a) {
         for (int k = 0; k < 4; ++k)
             w[k] = *(bi[k] >= 0 ? a.pre + (2ull * uint32_t(bi[k]) + uint32_t(k >> 1)) * a.pre_stride + ic
                                 : a.src_if + ic);
-        // ---- the jobs of the wave, packed ----
+        // ---- the jobs of the wave, packed (registers only) ----
+        // job j of the wave is call k of owner lane o: the ballots of the four
+        // calls give every job a rank (owner side) and every running lane its
+        // job (nth_set_bit); the owner's fields come over ds_bpermute and the
+        // result goes back the same way
         bool job[4];
-        uint32_t nj = 0, jpos[4];
+        uint64_t m[4];
+        uint32_t c[5], jpos[4];
+        c[0] = 0;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             job[k] = di[k] >= 0 && bi[k] < 0;
-            const uint64_t m = __ballot(job[k]);
-            jpos[k] = nj + uint32_t(__popcll(m & lt));
-            nj += uint32_t(__popcll(m));
+            m[k] = __ballot(job[k]);
+            jpos[k] = c[k] + uint32_t(__popcll(m[k] & lt));
+            c[k + 1] = c[k] + uint32_t(__popcll(m[k]));
         }
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-            if (job[k]) *lctr_t(jobs + 4u * jpos[k]) = lane | (uint32_t(k) << 6) | (uint32_t(di[k]) << 8);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const uint32_t nj = c[4];
+        uint32_t rj[4] = {0u, 0u, 0u, 0u};
         for (uint32_t j0 = 0; j0 < nj; j0 += 64u) {             // wave-uniform
             const uint32_t j = j0 + lane;
             const bool act = j < nj;
-            const uint32_t e = act ? *lctr_t(jobs + 4u * j) : lane;
-            const uint32_t o = e & 63u, k = (e >> 6) & 3u;
+            const uint32_t k = uint32_t(j >= c[1]) + uint32_t(j >= c[2]) + uint32_t(j >= c[3]);
+            const uint64_t mk = k == 0u ? m[0] : k == 1u ? m[1] : k == 2u ? m[2] : m[3];
+            const uint32_t ck = k == 0u ? c[0] : k == 1u ? c[1] : k == 2u ? c[2] : c[3];
+            const uint32_t o = act ? nth_set_bit(mk, j - ck) : lane;
             // the owning lane's connection (every lane takes part in the shuffles)
             A xs, xd;
             if constexpr (k16) {
@@ -618,8 +626,11 @@ __global__ __launch_bounds__(1024) void connect_kernel(ConnArgs a) {
                 xd = __shfl(da, int(o));
             }
             const uint32_t xdp = __shfl(dp, int(o)), xsp = __shfl(sp, int(o)), xp = __shfl(p, int(o));
+            const int32_t d0 = __shfl(di[0], int(o)), d1 = __shfl(di[1], int(o));
+            const int32_t d2 = __shfl(di[2], int(o)), d3 = __shfl(di[3], int(o));
+            uint32_t out = 0u;
             if (act) {
-                const ConnDesc D = conn_desc(a, e >> 8);
+                const ConnDesc D = conn_desc(a, uint32_t(k == 0u ? d0 : k == 1u ? d1 : k == 2u ? d2 : d3));
                 const bool syn = k < 2u;
                 uint32_t res, rule;
                 if (!k16 && D.bm_off != 0xFFFFFFFFu) {
@@ -630,16 +641,17 @@ __global__ __launch_bounds__(1024) void connect_kernel(ConnArgs a) {
                     res = syn ? conn_scan<k16, kLdsRules>(a, D, xs, xd, x4s, x4d, xdp, xp, rule)
                               : conn_scan<k16, kLdsRules>(a, D, xd, xs, x4d, x4s, xsp, xp, rule);
                 }
-                *lctr_t(results + 16u * o + 4u * k) = res | ((D.ctr_off + rule) << 2);
+                out = res | ((D.ctr_off + rule) << 2);
+            }
+            // the owners take their results of this pass
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) {
+                const uint32_t r = __shfl(out, int((jpos[kk] - j0) & 63u));
+                if (job[kk] && jpos[kk] >= j0 && jpos[kk] < j0 + 64u) rj[kk] = r;
             }
         }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         // ---- testConnection over the four results ----
         uint32_t res[4];
-        bool have_job = job[0] || job[1] || job[2] || job[3];
-        v4u rj = {0u, 0u, 0u, 0u};
-        if (have_job) rj = *lds128_t(results + 16u * lane);
 #pragma unroll
         for (int k = 0; k < 4; ++k) res[k] = di[k] < 0 ? 1u : job[k] ? (rj[k] & 3u) : (w[k] & 3u);   // nil ACL: PERMIT (:476-478)
         uint32_t v = 3u;
@@ -863,18 +875,22 @@ static uint32_t finish_grid(const FinishArgs& f) {
     return (span + 63u) / 64u + (f.oq ? f.oq_rows : 0u);
 }
 
-hipError_t launch_finish4(const FinishArgs& f, const Cls4Dev& o, const Pkts4& p, uint8_t* verdict, hipStream_t s) {
+hipError_t launch_finish4(const FinishArgs& f, const Cls4Dev& o, const Pkts4& p, uint8_t* verdict, hipStream_t s,
+                          hipEvent_t done) {
     const uint32_t g = finish_grid(f);
-    if (g == 0) return hipSuccess;
-    hipLaunchKernelGGL(finish4_kernel, dim3(g), dim3(1024), 0, s, f, o, p, verdict);
+    if (g == 0) return done ? hipEventRecord(done, s) : hipSuccess;
+    if (done) hipExtLaunchKernelGGL(finish4_kernel, dim3(g), dim3(1024), 0u, s, nullptr, done, 0u, f, o, p, verdict);
+    else hipLaunchKernelGGL(finish4_kernel, dim3(g), dim3(1024), 0, s, f, o, p, verdict);
     return hipGetLastError();
 }
 
 hipError_t launch_finish16(const FinishArgs& f, const Cls4Dev& t, const Cls4Dev& o, const Fe16& fe, const Pkts16& p,
-                           uint8_t* verdict, hipStream_t s) {
+                           uint8_t* verdict, hipStream_t s, hipEvent_t done) {
     const uint32_t g = finish_grid(f);
-    if (g == 0) return hipSuccess;
-    hipLaunchKernelGGL(finish16_kernel, dim3(g), dim3(1024), 0, s, f, t, o, fe, p, verdict);
+    if (g == 0) return done ? hipEventRecord(done, s) : hipSuccess;
+    if (done)
+        hipExtLaunchKernelGGL(finish16_kernel, dim3(g), dim3(1024), 0u, s, nullptr, done, 0u, f, t, o, fe, p, verdict);
+    else hipLaunchKernelGGL(finish16_kernel, dim3(g), dim3(1024), 0, s, f, t, o, fe, p, verdict);
     return hipGetLastError();
 }
 
@@ -910,13 +926,13 @@ hipError_t launch_stream_conn(const ConnArgs& a, int grid, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_connect(const ConnArgs& a, bool k16, bool lds_rules, int count, int grid, size_t lds,
+hipError_t launch_connect(const ConnArgs& a, bool k16, bool lds_rules, int count, int grid, int block, size_t lds,
                           hipStream_t s) {
     if (a.n == 0) return hipSuccess;
 #define CONN_CASE(K16, L, C)                                                                               \
     if (k16 == K16 && lds_rules == L && count == C) {                                                      \
         lds_attr(reinterpret_cast<const void*>(connect_kernel<K16, L, C>), lds);                          \
-        hipLaunchKernelGGL((connect_kernel<K16, L, C>), dim3(grid), dim3(1024), lds, s, a);                \
+        hipLaunchKernelGGL((connect_kernel<K16, L, C>), dim3(grid), dim3(block), lds, s, a);               \
         return hipGetLastError();                                                                          \
     }
     CONN_CASE(false, false, 0) CONN_CASE(false, false, 1) CONN_CASE(false, false, 2)

@@ -96,6 +96,10 @@ struct LaunchCfg {
     int grid;                  // workgroups (persistent, grid-stride)
     hipStream_t stream;
     Cls4Dev other;             // classify kernels: the OTHER image (protocols > 2), global memory
+    // classify kernels: events stamped with the kernel's own start / stop
+    // (hipExtLaunchKernel: part of the dispatch, no marker packets between
+    // kernels); null: none
+    hipEvent_t ev_start = nullptr, ev_stop = nullptr;
 };
 
 // verdict may be null; gslot: u64 slot counters (added to)
@@ -145,9 +149,11 @@ struct FinishArgs {
     uint32_t n_other, n_orules;
 };
 // finish4 / finish16: the OTHER packets' loads from the 4- / 16-byte batch
-hipError_t launch_finish4(const FinishArgs& f, const Cls4Dev& o, const Pkts4& p, uint8_t* verdict, hipStream_t s);
+// done (may be null): an event stamped when the launch completes
+hipError_t launch_finish4(const FinishArgs& f, const Cls4Dev& o, const Pkts4& p, uint8_t* verdict, hipStream_t s,
+                          hipEvent_t done = nullptr);
 hipError_t launch_finish16(const FinishArgs& f, const Cls4Dev& t, const Cls4Dev& o, const Fe16& fe, const Pkts16& p,
-                           uint8_t* verdict, hipStream_t s);
+                           uint8_t* verdict, hipStream_t s, hipEvent_t done = nullptr);
 // the classify kernels' packet stream without the lookups (stream floor);
 // exactly one of p4 / p16; p4 needs 16-B aligned src/dst, 8-B dport, 4-B
 // proto and verdict (variant bit 0: load and use instead of the next step's
@@ -201,10 +207,6 @@ static_assert(sizeof(ConnDesc) == 48 && sizeof(IfAcls) == 16, "connect_kernel re
 // rule i matches that interval's addresses (ports); the first match is the
 // lowest set bit of src row & dst row & protocol row.
 constexpr uint32_t kConnBmHeader = 32;
-// The connection kernel's per-wave job area in LDS (a.jobs_lds): 256 job
-// words (the evaluations of the wave's 64 connections that scan or search a
-// linear ACL), then 256 result words (4 per lane), 2 KiB per wave.
-constexpr uint32_t kConnJobBytes = 2048;
 struct ConnArgs {
     const ConnDesc* desc;
     const IfAcls* ifs;
@@ -228,12 +230,12 @@ struct ConnArgs {
     const uint32_t* pre;         // classifier slot words of the large ACLs: block b at pre + 2 b pre_stride
                                  // (SYN tuple, then SYN-ACK at + pre_stride); null when there are none
     uint64_t pre_stride;
-    uint32_t jobs_lds;           // LDS byte offset of the per-wave job areas (kConnJobBytes each)
 };
 // k16: 16-byte addresses; lds_rules: stage the pool; count: 0 none, 1 LDS
-// counters, 2 global (wave-aggregated) counters; grid: persistent workgroups;
-// lds: dynamic LDS bytes (pool, LDS counters, a.meta_lds tables, job areas)
-hipError_t launch_connect(const ConnArgs& a, bool k16, bool lds_rules, int count, int grid, size_t lds,
+// counters, 2 global (wave-aggregated) counters; grid: persistent workgroups
+// of `block` threads (512 or 1024); lds: dynamic LDS bytes (pool, LDS
+// counters, a.meta_lds tables)
+hipError_t launch_connect(const ConnArgs& a, bool k16, bool lds_rules, int count, int grid, int block, size_t lds,
                           hipStream_t s);
 // the connection batch's stream without the evaluation (whole 4-connection
 // groups of an IPv4 batch; 16-B aligned src / dst / src_if / dst_if, 8-B

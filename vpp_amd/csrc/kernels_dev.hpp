@@ -33,6 +33,8 @@
 // gen4 -- the counter-based splitmix64 traffic stream, generated in HBM.
 #include <hip/hip_runtime.h>
 
+#include <hip/hip_ext.h>
+
 #include "kernels.hpp"
 
 #include <mutex>
@@ -119,6 +121,22 @@ static inline void lds_attr(const void* f, size_t lds) {
         (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
         v = lds;
     }
+}
+
+// Position of the r-th set bit (0-based) of a 64-bit lane mask: six halving
+// steps on popcounts (wave-level job packing without LDS: a lane finds the
+// job it runs from the ballots of the lanes that own jobs).
+__device__ __forceinline__ uint32_t nth_set_bit(uint64_t m, uint32_t r) {
+    uint32_t lo = 0;
+#pragma unroll
+    for (int w = 32; w >= 1; w >>= 1) {
+        const uint32_t c = uint32_t(__popcll((m >> lo) & ((1ull << w) - 1ull)));
+        if (c <= r) {
+            r -= c;
+            lo += uint32_t(w);
+        }
+    }
+    return lo;
 }
 
 __device__ __forceinline__ bool port_in(uint32_t dport, uint32_t pw) {
@@ -1000,8 +1018,12 @@ static void launch_d(const Cls4Dev& t, const Pkts4& p, uint8_t* verdict, unsigne
                      const LaunchCfg& cfg) {
     const size_t lds = (kLds ? t.lds_bytes : 0) + 16;   // + the OTHER queue counter
     lds_attr(reinterpret_cast<const void*>(classify4_cls<kLds, kVec, kMode, kList, kD, kCtr>), lds);
-    hipLaunchKernelGGL((classify4_cls<kLds, kVec, kMode, kList, kD, kCtr>), dim3(cfg.grid), dim3(kClsBlock), lds,
-                       cfg.stream, t, cfg.other, p, verdict, gslot);
+    if (cfg.ev_start || cfg.ev_stop)
+        hipExtLaunchKernelGGL((classify4_cls<kLds, kVec, kMode, kList, kD, kCtr>), dim3(cfg.grid), dim3(kClsBlock),
+                              uint32_t(lds), cfg.stream, cfg.ev_start, cfg.ev_stop, 0u, t, cfg.other, p, verdict, gslot);
+    else
+        hipLaunchKernelGGL((classify4_cls<kLds, kVec, kMode, kList, kD, kCtr>), dim3(cfg.grid), dim3(kClsBlock), lds,
+                           cfg.stream, t, cfg.other, p, verdict, gslot);
 }
 
 // The hot variants (LDS-resident image, vector loads, sublist lists, u32
@@ -1087,8 +1109,13 @@ static void launch16_d(const Cls4Dev& t, const Fe16& fe, const Pkts16& p, uint8_
                        unsigned long long* gslot, const LaunchCfg& cfg) {
     const size_t lds = (kLds ? t.lds_bytes : 0) + 16;   // + the OTHER queue counter
     lds_attr(reinterpret_cast<const void*>(classify16_cls<kLds, kMode, kList, kD, kLin, kFe, kCtr>), lds);
-    hipLaunchKernelGGL((classify16_cls<kLds, kMode, kList, kD, kLin, kFe, kCtr>), dim3(cfg.grid), dim3(kClsBlock),
-                       lds, cfg.stream, t, cfg.other, fe, p, verdict, gslot);
+    if (cfg.ev_start || cfg.ev_stop)
+        hipExtLaunchKernelGGL((classify16_cls<kLds, kMode, kList, kD, kLin, kFe, kCtr>), dim3(cfg.grid),
+                              dim3(kClsBlock), uint32_t(lds), cfg.stream, cfg.ev_start, cfg.ev_stop, 0u, t, cfg.other,
+                              fe, p, verdict, gslot);
+    else
+        hipLaunchKernelGGL((classify16_cls<kLds, kMode, kList, kD, kLin, kFe, kCtr>), dim3(cfg.grid), dim3(kClsBlock),
+                           lds, cfg.stream, t, cfg.other, fe, p, verdict, gslot);
 }
 
 template <bool kLds, int kMode, int kList, int kFe>

@@ -175,13 +175,19 @@ class Engine:
         self._check(_abi.lib().cls_last_kernel_ms(self.h, C.byref(ms)))
         return ms.value
 
-    def kernel_times(self, reset: bool = True):
-        """Durations (ms) of every kernel timed since the last reset."""
+    def _timed(self, fn):
         n = C.c_uint32(0)
-        self._check(_abi.lib().cls_kernel_times(self.h, None, 0, C.byref(n)))
+        self._check(fn(self.h, None, 0, C.byref(n)))
         buf = (C.c_float * max(1, n.value))()
-        self._check(_abi.lib().cls_kernel_times(self.h, buf, n.value, C.byref(n)))
-        out = [buf[i] for i in range(n.value)]
+        self._check(fn(self.h, buf, n.value, C.byref(n)))
+        return [buf[i] for i in range(n.value)]
+
+    def kernel_times(self, reset: bool = True, starts: bool = False):
+        """Durations (ms) of every kernel timed since the last reset; with
+        `starts`, (durations, start times in ms after the first one's)."""
+        out = self._timed(_abi.lib().cls_kernel_times)
+        if starts:
+            out = (out, self._timed(_abi.lib().cls_kernel_starts))
         if reset:
             self._check(_abi.lib().cls_kernel_times_reset(self.h))
         return out
