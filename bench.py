@@ -300,6 +300,7 @@ def main():
     ar_ms = float(np.mean(ar)) if ar else 0.0
     ar_med = float(np.median(ar)) if ar else 0.0
     floor_ms = shape_ms = None
+    shapes = []
     lds = info["lds_bytes"] if af == 4 else info["lds_bytes_v16"]
     resident = info["lds_resident"] if af == 4 else info["lds_resident_v16"]
     two_per_cu = not resident or 2 * (lds + 16) <= 160 * 1024     # the classify launch's workgroups per CU
@@ -375,6 +376,8 @@ def main():
                          "frac_of_stream_floor": round(floor_ms / avg_k, 4) if floor_ms else None,
                          "frac_of_stream_floor_median": round(floor_ms / med_k, 4) if floor_ms else None,
                          "stream_floor_launch_shape_ms": round(shape_ms, 4) if shape_ms else None,
+                         # every stream shape, index = variant << 1 | two workgroups per CU (rank 0)
+                         "stream_floor_shapes_ms": [round(t, 4) for t in shapes],
                          "launch_shape": "%d x 1024-thread workgroups per CU" % (2 if two_per_cu else 1),
                          "frac_of_launch_shape_floor": round(shape_ms / avg_k, 4) if shape_ms else None,
                          "algorithmic_bytes_per_launch": alg_bytes},

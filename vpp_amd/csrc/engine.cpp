@@ -916,18 +916,6 @@ static int stream_shapes(cls_engine* e, const cls_pkt_soa* pk, uint64_t n, uint8
                aligned(verdict, 4))
            : !(pk->af == CLS_AF_V16 && aligned(pk->src16, 16) && aligned(pk->dst16, 16)))
         return fail(e, CLS_E_INVAL, "stream floor: device arrays of the classify kernel's alignment");
-    // diagnostics: the same stream over buffers this library allocates
-    DevBuf own[5];
-    if (v4 && std::getenv("CONTIVCLS_FLOOR_OWN")) {
-        const size_t sz[5] = {n * 4, n * 4, n * 2, n, n};
-        const void* from[5] = {pk->src4, pk->dst4, pk->dport, pk->proto, verdict};
-        for (int i = 0; i < 5; ++i) {
-            HIPC(e, own[i].ensure(sz[i]));
-            HIPC(e, hipMemcpyAsync(own[i].p, from[i], sz[i], hipMemcpyDeviceToDevice, s));
-        }
-        p4 = Pkts4{own[0].as<uint32_t>(), own[1].as<uint32_t>(), own[2].as<uint16_t>(), own[3].as<uint8_t>(), n};
-        verdict = own[4].as<uint8_t>();
-    }
     // the floor is the fastest of the stream shapes: one or two 1024-thread
     // workgroups per CU (the classify kernel runs one when its LDS image
     // takes more than half the CU's LDS), loads one step ahead or not, the

@@ -521,13 +521,13 @@ __device__ __forceinline__ uint32_t conn_bm(const ConnArgs& a, const ConnDesc& D
 // 1. Evaluations.  A call on a large ACL reads the classifier's result word
 //    for this connection (classify4_pair / the slot launches); a call on a
 //    linear ACL is a *job*: the bitmap search (IPv4, conn_bm) or the rule
-//    scan.  The jobs of all four possible calls of the wave's 64 connections
-//    are packed (ranks from the calls' ballots, no LDS) and run 64 at a time,
-//    every lane on one job with its connection's fields fetched from the
-//    owning lane (ds_bpermute).  A lane-per-call loop would make the wave run the
-//    search once per call index in which any of its lanes has a job -- four
-//    passes per wave with ~0.6 jobs per connection -- where packing runs
-//    one.  Jobs are evaluated whether or not testConnection reaches the call
+//    scan.  A call index most of the wave's lanes have a job for runs in
+//    place; the jobs of the other call indices are packed (ranks from the
+//    calls' ballots, no LDS) and run 64 at a time, every lane on one job with
+//    its connection's fields fetched from the owning lane (ds_bpermute).  A
+//    lane-per-call loop alone would make the wave run the search once per
+//    call index in which any of its lanes has a job -- four passes per wave
+//    with ~0.6 jobs per connection -- where packing runs one.  Jobs are evaluated whether or not testConnection reaches the call
 //    (the call order needs the earlier results); only the calls it makes are
 //    counted.
 // 2. The state machine: testConnection's order and REFLECT short-cuts
@@ -591,31 +591,48 @@ __global__ __launch_bounds__(1024) void connect_kernel(ConnArgs a) {
         for (int k = 0; k < 4; ++k)
             w[k] = *(bi[k] >= 0 ? a.pre + (2ull * uint32_t(bi[k]) + uint32_t(k >> 1)) * a.pre_stride + ic
                                 : a.src_if + ic);
-        // ---- the jobs of the wave, packed (registers only) ----
-        // job j of the wave is call k of owner lane o: the ballots of the four
-        // calls give every job a rank (owner side) and every running lane its
-        // job (nth_set_bit); the owner's fields come over ds_bpermute and the
-        // result goes back the same way
+        // ---- the jobs of the wave ----
+        // A call index most of the wave's lanes have a job for runs as one
+        // pass of its own, every lane on its own connection.  The jobs of the
+        // other call indices are packed (registers only): job j of the wave
+        // is call k of owner lane o; the ballots give every job a rank (owner
+        // side) and every running lane its job (nth_set_bit); the owner's
+        // fields come over ds_bpermute and the result goes back the same way
+        // -- a pass per 64 jobs instead of one per call index any lane has.
         bool job[4];
         uint64_t m[4];
-        uint32_t c[5], jpos[4];
+        uint32_t c[5], jpos[4], dense = 0u;
         c[0] = 0;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             job[k] = di[k] >= 0 && bi[k] < 0;
             m[k] = __ballot(job[k]);
+            if (__popcll(m[k]) > 32) {                          // wave-uniform
+                dense |= 1u << k;
+                m[k] = 0ull;
+            }
             jpos[k] = c[k] + uint32_t(__popcll(m[k] & lt));
             c[k + 1] = c[k] + uint32_t(__popcll(m[k]));
         }
-        const uint32_t nj = c[4];
+        const uint32_t nj = c[4], nd = uint32_t(__builtin_popcount(dense));
+        const uint32_t passes = nd + (nj + 63u) / 64u;
         uint32_t rj[4] = {0u, 0u, 0u, 0u};
-        for (uint32_t j0 = 0; j0 < nj; j0 += 64u) {             // wave-uniform
-            const uint32_t j = j0 + lane;
-            const bool act = j < nj;
-            const uint32_t k = uint32_t(j >= c[1]) + uint32_t(j >= c[2]) + uint32_t(j >= c[3]);
-            const uint64_t mk = k == 0u ? m[0] : k == 1u ? m[1] : k == 2u ? m[2] : m[3];
-            const uint32_t ck = k == 0u ? c[0] : k == 1u ? c[1] : k == 2u ? c[2] : c[3];
-            const uint32_t o = act ? nth_set_bit(mk, j - ck) : lane;
+        for (uint32_t pass = 0; pass < passes; ++pass) {      // wave-uniform
+            uint32_t k, o, j0 = 0u;
+            bool act;
+            if (pass < nd) {                                    // a dense call index, in place
+                k = nth_set_bit(dense, pass);
+                o = lane;
+                act = k == 0u ? job[0] : k == 1u ? job[1] : k == 2u ? job[2] : job[3];
+            } else {
+                j0 = (pass - nd) * 64u;
+                const uint32_t j = j0 + lane;
+                act = j < nj;
+                k = uint32_t(j >= c[1]) + uint32_t(j >= c[2]) + uint32_t(j >= c[3]);
+                const uint64_t mk = k == 0u ? m[0] : k == 1u ? m[1] : k == 2u ? m[2] : m[3];
+                const uint32_t ck = k == 0u ? c[0] : k == 1u ? c[1] : k == 2u ? c[2] : c[3];
+                o = act ? nth_set_bit(mk, j - ck) : lane;
+            }
             // the owning lane's connection (every lane takes part in the shuffles)
             A xs, xd;
             if constexpr (k16) {
@@ -644,10 +661,16 @@ __global__ __launch_bounds__(1024) void connect_kernel(ConnArgs a) {
                 out = res | ((D.ctr_off + rule) << 2);
             }
             // the owners take their results of this pass
+            if (pass < nd) {
 #pragma unroll
-            for (int kk = 0; kk < 4; ++kk) {
-                const uint32_t r = __shfl(out, int((jpos[kk] - j0) & 63u));
-                if (job[kk] && jpos[kk] >= j0 && jpos[kk] < j0 + 64u) rj[kk] = r;
+                for (int kk = 0; kk < 4; ++kk)
+                    if (uint32_t(kk) == k && job[kk]) rj[kk] = out;
+            } else {
+#pragma unroll
+                for (int kk = 0; kk < 4; ++kk) {
+                    const uint32_t r = __shfl(out, int((jpos[kk] - j0) & 63u));
+                    if (((m[kk] >> lane) & 1ull) && jpos[kk] >= j0 && jpos[kk] < j0 + 64u) rj[kk] = r;
+                }
             }
         }
         // ---- testConnection over the four results ----
@@ -896,20 +919,12 @@ hipError_t launch_finish16(const FinishArgs& f, const Cls4Dev& t, const Cls4Dev&
 
 hipError_t launch_stream(const Pkts4* p4, const Pkts16* p16, uint8_t* verdict, int grid, int variant,
                          hipStream_t s) {
-    // diagnostics: the stream with a dynamic LDS allocation like the classify launch's
-    static const size_t dl = std::getenv("CONTIVCLS_FLOOR_LDS") ? std::strtoul(std::getenv("CONTIVCLS_FLOOR_LDS"), nullptr, 0) : 0;
-    if (dl) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(stream4_kernel<true, true>), hipFuncAttributeMaxDynamicSharedMemorySize, int(dl));
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(stream4_kernel<false, true>), hipFuncAttributeMaxDynamicSharedMemorySize, int(dl));
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(stream4_kernel<true, false>), hipFuncAttributeMaxDynamicSharedMemorySize, int(dl));
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(stream4_kernel<false, false>), hipFuncAttributeMaxDynamicSharedMemorySize, int(dl));
-    }
     if (p4) {
         switch (variant) {
-        case 0: hipLaunchKernelGGL((stream4_kernel<true, true>), dim3(grid), dim3(kClsBlock), dl, s, *p4, verdict); break;
-        case 1: hipLaunchKernelGGL((stream4_kernel<false, true>), dim3(grid), dim3(kClsBlock), dl, s, *p4, verdict); break;
-        case 2: hipLaunchKernelGGL((stream4_kernel<true, false>), dim3(grid), dim3(kClsBlock), dl, s, *p4, verdict); break;
-        default: hipLaunchKernelGGL((stream4_kernel<false, false>), dim3(grid), dim3(kClsBlock), dl, s, *p4, verdict);
+        case 0: hipLaunchKernelGGL((stream4_kernel<true, true>), dim3(grid), dim3(kClsBlock), 0, s, *p4, verdict); break;
+        case 1: hipLaunchKernelGGL((stream4_kernel<false, true>), dim3(grid), dim3(kClsBlock), 0, s, *p4, verdict); break;
+        case 2: hipLaunchKernelGGL((stream4_kernel<true, false>), dim3(grid), dim3(kClsBlock), 0, s, *p4, verdict); break;
+        default: hipLaunchKernelGGL((stream4_kernel<false, false>), dim3(grid), dim3(kClsBlock), 0, s, *p4, verdict);
         }
     } else {
         hipLaunchKernelGGL(stream16_kernel, dim3(grid), dim3(kClsBlock), 0, s, *p16, verdict);

@@ -951,11 +951,7 @@ __global__ __launch_bounds__(kClsBlock) void classify16_cls(Cls4Dev t, Cls4Dev o
                                                    oq_lds);
         }
     };
-    // 4 packets per lane per step (vector dport / proto / verdict words),
-    // classified two at a time: a 16-byte packet's lookups hold about twice
-    // the registers of an IPv4 one, and the kernel must stay within 128
-    // VGPRs (1024-thread workgroups) without scratch.  The CU's 16 waves
-    // overlap one another's loads and lookups (no prefetch buffer).
+    // 4 packets per lane per step (vector dport / proto / verdict words).
     // Wave-contiguous packets: a wave's step covers 256 consecutive packets
     // and lane l takes packets base + 64k + l (k = 0..3), so each 16-B
     // address load instruction reads 1 KiB contiguous per wave (the
@@ -965,34 +961,67 @@ __global__ __launch_bounds__(kClsBlock) void classify16_cls(Cls4Dev t, Cls4Dev o
     // per instruction.  Whole waves only (nsteps a multiple of 64 groups of 4,
     // wave-uniform); the rest goes to the per-packet tail.
     const uint32_t nsteps = uint32_t(p.n / 256u) * 64u;
-    for (uint32_t g = tid; g < nsteps; g += nthreads) {
-        const uint32_t base = 4u * (g & ~63u) + (g & 63u);
+    struct Step16 {
         uint4 s[4], d[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            s[k] = ldnt(at(p.src, base + 64u * k));
-            d[k] = ldnt(at(p.dst, base + 64u * k));
-        }
         uint32_t dp[4], pr[4];
+    };
+    auto load = [&](Step16& b, uint32_t g) {
+        const uint32_t base = 4u * (g & ~63u) + (g & 63u);
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            dp[k] = __builtin_nontemporal_load(p.dport + base + 64u * k);
-            pr[k] = __builtin_nontemporal_load(p.proto + base + 64u * k);
+            b.s[k] = ldnt(at(p.src, base + 64u * k));
+            b.d[k] = ldnt(at(p.dst, base + 64u * k));
         }
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const uint4 s2[2] = {s[2 * h], s[2 * h + 1]}, d2[2] = {d[2 * h], d[2 * h + 1]};
-            uint32_t pa[2] = {dp[2 * h], dp[2 * h + 1]}, ra[2] = {pr[2 * h], pr[2 * h + 1]}, v2[2];
-            const uint32_t ix[2] = {base + 64u * (2 * h), base + 64u * (2 * h + 1)};
-            classify(s2, d2, pa, ra, (ra[0] | ra[1]) > 2u, v2, ix);
-            if constexpr (kCtr == 2) {                                 // slot mode: res | slot << 2
-                reinterpret_cast<uint32_t*>(verdict)[base + 64u * (2 * h)] = v2[0];
-                reinterpret_cast<uint32_t*>(verdict)[base + 64u * (2 * h + 1)] = v2[1];
-            } else if (verdict) {
-                __builtin_nontemporal_store(uint8_t(v2[0]), verdict + base + 64u * (2 * h));
-                __builtin_nontemporal_store(uint8_t(v2[1]), verdict + base + 64u * (2 * h + 1));
-            }
+        for (int k = 0; k < 4; ++k) {
+            b.dp[k] = __builtin_nontemporal_load(p.dport + base + 64u * k);
+            b.pr[k] = __builtin_nontemporal_load(p.proto + base + 64u * k);
         }
+    };
+    // The step's four packets, G at a time: with the host-route hashes
+    // (src_mode 1) a 16-byte packet's lookups hold about twice the registers
+    // of an IPv4 one, so two, to stay within 128 VGPRs (1024-thread
+    // workgroups) without scratch; the trie and interval front ends fit all
+    // four, whose LDS chains then run interleaved.  The CU's 16 waves overlap
+    // one another's loads and lookups: the next step's loads held in
+    // registers during this step's lookups (two at a time, in the order the
+    // vmcnt counter can serve) measured no faster on the gen-policy lists
+    // (profiles/r04j_genpolicy16_prefetch_ab.txt).
+    constexpr int G = kFe == 1 ? 2 : 4;
+    auto run = [&](const Step16& b, uint32_t g, uint32_t (&v)[4]) {
+        const uint32_t base = 4u * (g & ~63u) + (g & 63u);
+#pragma unroll
+        for (int h = 0; h < 4 / G; ++h) {
+            uint4 sg[G], dg[G];
+            uint32_t pa[G], ra[G], vg[G], ix[G], any = 0u;
+#pragma unroll
+            for (int q = 0; q < G; ++q) {
+                sg[q] = b.s[G * h + q];
+                dg[q] = b.d[G * h + q];
+                pa[q] = b.dp[G * h + q];
+                ra[q] = b.pr[G * h + q];
+                ix[q] = base + 64u * (G * h + q);
+                any |= ra[q];
+            }
+            classify(sg, dg, pa, ra, any > 2u, vg, ix);
+#pragma unroll
+            for (int q = 0; q < G; ++q) v[G * h + q] = vg[q];
+        }
+    };
+    auto put = [&](const uint32_t (&v)[4], uint32_t g) {
+        const uint32_t base = 4u * (g & ~63u) + (g & 63u);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if constexpr (kCtr == 2) reinterpret_cast<uint32_t*>(verdict)[base + 64u * k] = v[k];   // slot mode: res | slot << 2
+            else if (verdict) __builtin_nontemporal_store(uint8_t(v[k]), verdict + base + 64u * k);
+        }
+    };
+    for (uint32_t g = tid; g < nsteps; g += nthreads) {
+        Step16 b;
+        uint32_t v[4];
+        load(b, g);
+        run(b, g, v);
+        put(v, g);
     }
     for (uint32_t i = nsteps * 4u + tid; i < uint32_t(p.n); i += nthreads) {
         const uint4 s1[1] = {ldnt(at(p.src, i))}, d1[1] = {ldnt(at(p.dst, i))};
