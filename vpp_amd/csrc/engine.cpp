@@ -141,6 +141,22 @@ struct AclEntry {
 
 }  // namespace
 
+// The host side of a connection batch over the current bindings: one
+// descriptor per bound table, (in, out) per interface, the large ACLs
+// evaluated by the classifier, the rule pool with the bitmap forms.  A device
+// batch's plan depends only on the bindings and the flags, so it is kept
+// until they change (cls_engine::conn_gen).
+struct ConnPlan {
+    uint64_t key = ~0ull, gen = ~0ull;
+    uint64_t id = 0;                                      // which plan s_desc / s_ifs / s_rules hold (uploaded)
+    std::vector<ConnDesc> desc;
+    std::vector<std::shared_ptr<Table>> dtab;             // table of each descriptor
+    std::vector<IfAcls> ifs;
+    std::vector<uint32_t> big;                            // descriptors of the large ACLs
+    std::vector<uint8_t> pool;
+    uint32_t n_ctr = 0;
+};
+
 struct cls_engine {
     int device = 0;
     int n_cu = 256;
@@ -160,6 +176,10 @@ struct cls_engine {
     DevBuf s_src, s_dst, s_sport, s_dport, s_proto, s_verdict, s_if_a, s_if_b, s_desc, s_ifs;
     DevBuf s_pre;                  // connection path: classifier slot words per large ACL (8 bytes/connection)
     DevBuf s_rules, s_tctr, s_cctr;  // connection path: rule pool, table counter pointers, call counters
+    bool cctr_zero = false;          // s_cctr cleared since its allocation (the scatter launch keeps it zero)
+    uint64_t conn_gen = 0;           // bumped by every change of tables or interface bindings
+    ConnPlan conn_plan;              // the last device batch's plan
+    uint64_t plan_ids = 0, up_plan = ~0ull;   // plan ids; the plan whose tables are on the device
     // what s_desc, s_ifs, s_rules and s_tctr hold (the last upload): a
     // connection batch over unchanged bindings uploads nothing
     std::vector<uint8_t> up_desc, up_ifs, up_rules, up_tctr;
@@ -436,6 +456,7 @@ static int table_put_locked(cls_engine* e, const char* name, const cls_rule* rul
     }
     const uint32_t id = e->next_table++;
     e->tables[id] = t;
+    e->conn_gen++;                  // connection plans see the change
     if (table_id) *table_id = id;
     return CLS_OK;
 }
@@ -452,6 +473,7 @@ int cls_table_del(cls_engine* e, uint32_t table_id) {
     std::lock_guard<std::mutex> g(e->mu);
     HIPC(e, hipSetDevice(e->device));
     if (!e->tables.erase(table_id)) return fail(e, CLS_E_NOTFOUND, "no table %u", table_id);
+    e->conn_gen++;                  // connection plans see the change
     return CLS_OK;
 }
 
@@ -1020,6 +1042,7 @@ static uint32_t if_id_locked(cls_engine* e, const std::string& name) {
     e->if_ids[name] = id;
     e->if_names.push_back(name);
     e->if_acl.push_back({-1, -1});
+    e->conn_gen++;                  // connection plans see the change
     return id;
 }
 
@@ -1033,6 +1056,7 @@ static int acl_del_locked(cls_engine* e, const std::string& name) {
         if (b.second == tid) b.second = -1;
     }
     e->tables.erase(it->second.table_id);
+    e->conn_gen++;                  // connection plans see the change
     e->acls.erase(it);
     e->changes++;
     return CLS_OK;
@@ -1088,11 +1112,13 @@ int cls_acl_put(cls_engine* e, const char* acl_name, const cls_rule* rules, uint
         const uint32_t id = if_id_locked(e, ingress_ifs[i]);
         a.ingress.push_back(id);
         e->if_acl[id].first = int32_t(tid);
+        e->conn_gen++;                  // connection plans see the change
     }
     for (uint32_t i = 0; i < n_egress; ++i) {
         const uint32_t id = if_id_locked(e, egress_ifs[i]);
         a.egress.push_back(id);
         e->if_acl[id].second = int32_t(tid);
+        e->conn_gen++;                  // connection plans see the change
     }
     e->acls[name] = a;
     e->changes++;
@@ -1257,33 +1283,6 @@ int cls_connect_batch(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t*
         return fail(e, CLS_E_INVAL, "device src16/dst16 must be 16-byte aligned");
     HIPC(e, hipSetDevice(e->device));
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : e->stream;
-    // Snapshot the bindings: one descriptor per bound table, (in, out) per
-    // interface.  Linear ACLs' compact rules go to the call's rule pool.
-    std::vector<ConnDesc> desc;
-    std::vector<std::shared_ptr<Table>> dtab;             // table of each descriptor
-    std::unordered_map<int32_t, int32_t> slot;
-    uint32_t n_ctr = 0;
-    auto desc_of = [&](int32_t tid) -> int32_t {
-        if (tid < 0) return -1;
-        auto f = slot.find(tid);
-        if (f != slot.end()) return f->second;
-        auto t = e->tables.find(uint32_t(tid));
-        if (t == e->tables.end()) return -1;
-        const Table& T = *t->second;
-        ConnDesc d{};
-        d.pre_blk = -1;
-        d.n = uint32_t(k16 ? T.conn16.size() : T.conn4.size());
-        d.n_rules = T.n_rules;
-        d.ctr_off = n_ctr;
-        n_ctr += T.n_rules + 1;
-        desc.push_back(d);
-        dtab.push_back(t->second);
-        slot[tid] = int32_t(desc.size() - 1);
-        return int32_t(desc.size() - 1);
-    };
-    std::vector<IfAcls> ifs(std::max<size_t>(1, e->if_acl.size()));
-    for (size_t i = 0; i < e->if_acl.size(); ++i)
-        ifs[i] = IfAcls{desc_of(e->if_acl[i].first), desc_of(e->if_acl[i].second), -1, -1};
     const uint32_t n_ifs = uint32_t(e->if_acl.size());
     if (!dev)
         for (uint64_t i = 0; i < n; ++i)
@@ -1310,50 +1309,158 @@ int cls_connect_batch(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t*
         sp = e->s_sport.as<uint16_t>(); dp = e->s_dport.as<uint16_t>();
         pr = e->s_proto.as<uint8_t>(); o = e->s_verdict.as<uint8_t>();
     }
-    // Large ACLs: the classifier evaluates the SYN tuple (src, dst, dport) and
-    // the SYN-ACK tuple (dst, src, sport) of every connection, one slot-mode
-    // launch each (res | slot << 2 per connection); the connection kernel
-    // then reads those words instead of scanning the ACL, and maps the slot
-    // to its rule only for the calls testConnection makes.  Whole-batch
-    // evaluation keeps the classify launches dense (no compaction).
-    // Which ACLs: with a host batch, those whose linear work would be large --
-    // connections touching the ACL x its rule count >= kConnClsWork x batch
-    // (touches estimated per interface binding from <= 64 Ki sampled
-    // connections, at hashed positions); with a device batch, the ACLs of >=
-    // kConnClsDevRules rules.  CLS_F_CONN_CLS: every imaged ACL.
-    std::vector<uint32_t> big;
-    if (n && !(flags & CLS_F_FORCE_LINEAR) && (n >= kConnClsMinBatch || (flags & CLS_F_CONN_CLS))) {
-        std::vector<uint64_t> touch(dtab.size(), 0);
-        if (!dev && !(flags & CLS_F_CONN_CLS)) {
-            const uint64_t m = std::min<uint64_t>(n, 65536);
-            std::vector<uint64_t> per_if(ifs.size(), 0);
-            for (uint64_t k = 0; k < m; ++k) {
-                // sample k: a splitmix-scrambled position in stratum k (no stride aliasing)
-                uint64_t z = (k + 1) * 0x9E3779B97F4A7C15ull;
-                z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-                z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-                z ^= z >> 31;
-                const uint64_t lo = k * n / m, hi = (k + 1) * n / m;
-                const uint64_t i = lo + z % (hi - lo);
-                per_if[c->src_if[i]] += 1;
-                if (c->dst_if[i] != c->src_if[i]) per_if[c->dst_if[i]] += 1;
+    // The plan (ConnPlan): a device batch reuses the last one while the
+    // bindings and the flags are the same; a host batch picks its large ACLs
+    // from a sample of its connections, so it plans every time.
+    const bool use_big = n && !(flags & CLS_F_FORCE_LINEAR) && (n >= kConnClsMinBatch || (flags & CLS_F_CONN_CLS));
+    const char* bme = std::getenv("CONTIVCLS_CONN_BITMAP");
+    const bool use_bm = !k16 && n && !(flags & CLS_F_FORCE_LINEAR) && !(bme && std::atoi(bme) == 0);
+    const uint64_t key = uint64_t(k16) | uint64_t(count) << 1 | uint64_t(use_big) << 2 |
+                         uint64_t((flags & CLS_F_CONN_CLS) != 0) << 3 | uint64_t(use_bm) << 4;
+    ConnPlan fresh;
+    ConnPlan& P = dev ? e->conn_plan : fresh;
+    const bool planned = dev && P.gen == e->conn_gen && P.key == key;
+    if (!planned) {
+        P = ConnPlan();
+        // Snapshot the bindings: one descriptor per bound table, (in, out) per
+        // interface.  Linear ACLs' compact rules go to the call's rule pool.
+        std::unordered_map<int32_t, int32_t> slot;
+        auto desc_of = [&](int32_t tid) -> int32_t {
+            if (tid < 0) return -1;
+            auto f = slot.find(tid);
+            if (f != slot.end()) return f->second;
+            auto t = e->tables.find(uint32_t(tid));
+            if (t == e->tables.end()) return -1;
+            const Table& T = *t->second;
+            ConnDesc d{};
+            d.pre_blk = -1;
+            d.bm_off = 0xFFFFFFFFu;
+            d.n = uint32_t(k16 ? T.conn16.size() : T.conn4.size());
+            d.n_rules = T.n_rules;
+            d.ctr_off = P.n_ctr;
+            P.n_ctr += T.n_rules + 1;
+            P.desc.push_back(d);
+            P.dtab.push_back(t->second);
+            slot[tid] = int32_t(P.desc.size() - 1);
+            return int32_t(P.desc.size() - 1);
+        };
+        P.ifs.resize(std::max<size_t>(1, e->if_acl.size()));
+        for (size_t i = 0; i < e->if_acl.size(); ++i)
+            P.ifs[i] = IfAcls{desc_of(e->if_acl[i].first), desc_of(e->if_acl[i].second), -1, -1};
+        // Large ACLs: the classifier evaluates the SYN tuple (src, dst, dport)
+        // and the SYN-ACK tuple (dst, src, sport) of every connection in slot
+        // mode (res | slot << 2 per connection); the connection kernel then
+        // reads those words instead of scanning the ACL, and maps the slot to
+        // its rule only for the calls testConnection makes.  Whole-batch
+        // evaluation keeps the classify launches dense (no compaction).
+        // Which ACLs: with a host batch, those whose linear work would be
+        // large -- connections touching the ACL x its rule count >=
+        // kConnClsWork x batch (touches estimated per interface binding from
+        // <= 64 Ki sampled connections, at hashed positions); with a device
+        // batch, the ACLs of >= kConnClsDevRules rules.  CLS_F_CONN_CLS: every
+        // imaged ACL.
+        if (use_big) {
+            std::vector<uint64_t> touch(P.dtab.size(), 0);
+            if (!dev && !(flags & CLS_F_CONN_CLS)) {
+                const uint64_t m = std::min<uint64_t>(n, 65536);
+                std::vector<uint64_t> per_if(P.ifs.size(), 0);
+                for (uint64_t k = 0; k < m; ++k) {
+                    // sample k: a splitmix-scrambled position in stratum k (no stride aliasing)
+                    uint64_t z = (k + 1) * 0x9E3779B97F4A7C15ull;
+                    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+                    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+                    z ^= z >> 31;
+                    const uint64_t lo = k * n / m, hi = (k + 1) * n / m;
+                    const uint64_t i = lo + z % (hi - lo);
+                    per_if[c->src_if[i]] += 1;
+                    if (c->dst_if[i] != c->src_if[i]) per_if[c->dst_if[i]] += 1;
+                }
+                for (size_t f = 0; f < n_ifs; ++f) {
+                    const uint64_t t = per_if[f] * n / m;
+                    if (P.ifs[f].in >= 0) touch[P.ifs[f].in] += t;
+                    if (P.ifs[f].out >= 0 && P.ifs[f].out != P.ifs[f].in) touch[P.ifs[f].out] += t;
+                }
             }
-            for (size_t f = 0; f < n_ifs; ++f) {
-                const uint64_t t = per_if[f] * n / m;
-                if (ifs[f].in >= 0) touch[ifs[f].in] += t;
-                if (ifs[f].out >= 0 && ifs[f].out != ifs[f].in) touch[ifs[f].out] += t;
+            for (uint32_t j = 0; j < P.dtab.size(); ++j) {
+                const Table& t = *P.dtab[j];
+                const bool imaged = k16 ? t.p16.ok : t.has_cls;
+                if (!imaged || t.n_rules < kConnClsMinRules) continue;
+                const bool want = (flags & CLS_F_CONN_CLS) ||
+                                  (dev ? t.n_rules >= kConnClsDevRules
+                                       : double(touch[j]) * t.n_rules >= double(kConnClsWork) * double(n));
+                if (want) P.big.push_back(j);
             }
         }
-        for (uint32_t j = 0; j < dtab.size(); ++j) {
-            const Table& t = *dtab[j];
-            const bool imaged = k16 ? t.p16.ok : t.has_cls;
-            if (!imaged || t.n_rules < kConnClsMinRules) continue;
-            const bool want = (flags & CLS_F_CONN_CLS) ||
-                              (dev ? t.n_rules >= kConnClsDevRules
-                                   : double(touch[j]) * t.n_rules >= double(kConnClsWork) * double(n));
-            if (want) big.push_back(j);
+        // the large ACLs' result-word blocks: block b = the ACL big[b], also
+        // per interface (the connection kernel loads a connection's words
+        // before its descriptors)
+        for (size_t b = 0; b < P.big.size(); ++b) {
+            ConnDesc& d = P.desc[P.big[b]];
+            const Table& t = *P.dtab[P.big[b]];
+            d.pre_blk = int32_t(b);
+            d.n = 0;
+            d.slot_rule = k16 ? t.p16.d_slot_rule.as<uint32_t>() : t.d_slot_rule.as<uint32_t>();
+            for (IfAcls& f : P.ifs) {
+                if (f.in == int32_t(P.big[b])) f.in_pre = int32_t(b);
+                if (f.out == int32_t(P.big[b])) f.out_pre = int32_t(b);
+            }
+        }
+        // the rule pool of the linear ACLs
+        const size_t rb = k16 ? sizeof(ConnRule16) : sizeof(ConnRule4);
+        for (size_t j = 0; j < P.desc.size(); ++j) {
+            if (P.desc[j].pre_blk >= 0) continue;
+            P.desc[j].rule_off = uint32_t(P.pool.size() / rb);
+            const uint8_t* r = k16 ? reinterpret_cast<const uint8_t*>(P.dtab[j]->conn16.data())
+                                   : reinterpret_cast<const uint8_t*>(P.dtab[j]->conn4.data());
+            P.pool.insert(P.pool.end(), r, r + size_t(P.desc[j].n) * rb);
+        }
+        // IPv4: the bitmap form of the longer linear ACLs, longest first, while
+        // the pool (and the LDS counters when counting) still fit LDS -- a wave
+        // then pays a fixed number of reads per evaluation instead of its
+        // longest lane's scan (CONTIVCLS_CONN_BITMAP=0: scans only).
+        if (use_bm) {
+            const size_t lds_max0 = size_t(max_lds_bytes());
+            // the LDS counters take their share only when they can be LDS counters
+            // at all (otherwise they are global, cmode 2); no subtraction wraps
+            const size_t ctr_b = count ? size_t(P.n_ctr) * 4 : 0, reserve = std::min<size_t>(lds_max0 / 8, 8192);
+            const size_t ctr_lds = ctr_b + reserve <= lds_max0 ? ctr_b : 0;
+            const size_t cap = lds_max0 - reserve - ctr_lds;
+            std::vector<size_t> order;
+            for (size_t j = 0; j < P.desc.size(); ++j)
+                if (P.desc[j].pre_blk < 0 && P.desc[j].n >= kConnBmMinRules) order.push_back(j);
+            std::stable_sort(order.begin(), order.end(),
+                             [&](size_t a, size_t b) { return P.desc[a].n > P.desc[b].n; });
+            std::vector<uint32_t> words;
+            for (size_t j : order) {
+                Table& t = *P.dtab[j];
+                if (!t.conn_bm_built) {                         // once per table: rules are immutable
+                    if (!conn_bitmap4(t.conn4, t.n_rules, kConnBmMaxWords, t.conn_bm)) t.conn_bm.clear();
+                    t.conn_bm_built = true;
+                }
+                const size_t used = P.pool.size() + words.size() * 4;
+                if (t.conn_bm.empty() || used + t.conn_bm.size() * 4 > cap) continue;
+                P.desc[j].bm_off = uint32_t(used);              // the pool is a multiple of 32 B, blobs of 16 B
+                const std::vector<uint32_t>& h = t.conn_bm;     // header {W, ns, nd, nr, n0, n1, n2, n3}
+                P.desc[j].bm_sd = h[1] | (h[2] << 16);
+                P.desc[j].bm_tu = h[4] | (h[5] << 16);
+                P.desc[j].bm_w = h[0];
+                words.insert(words.end(), t.conn_bm.begin(), t.conn_bm.end());
+            }
+            const uint8_t* wb = reinterpret_cast<const uint8_t*>(words.data());
+            P.pool.insert(P.pool.end(), wb, wb + words.size() * 4);
+        }
+        P.id = ++e->plan_ids;
+        if (dev) {
+            P.key = key;
+            P.gen = e->conn_gen;
         }
     }
+    std::vector<ConnDesc>& desc = P.desc;
+    std::vector<std::shared_ptr<Table>>& dtab = P.dtab;
+    std::vector<IfAcls>& ifs = P.ifs;
+    const std::vector<uint8_t>& pool = P.pool;
+    const std::vector<uint32_t>& big = P.big;
+    const uint32_t n_ctr = P.n_ctr;
     // The result words: block b (the ACL big[b]) at pre + 2 b stride, the SYN
     // tuple's words first, the SYN-ACK tuple's at + stride (a multiple of 4,
     // so both halves stay 16-B aligned for the pair launch's stores).
@@ -1364,15 +1471,9 @@ int cls_connect_batch(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t*
         for (size_t b = 0; b < big.size(); ++b) {
             Table& t = *dtab[big[b]];
             uint32_t* pre = e->s_pre.as<uint32_t>() + b * 2 * stride;
-            desc[big[b]].pre_blk = int32_t(b);
-            for (IfAcls& f : ifs) {                        // the block, also per interface (prefetch)
-                if (f.in == int32_t(big[b])) f.in_pre = int32_t(b);
-                if (f.out == int32_t(big[b])) f.out_pre = int32_t(b);
-            }
             LaunchCfg cfg;
             cfg.stream = s;
             if (!k16) {
-                desc[big[b]].slot_rule = t.d_slot_rule.as<uint32_t>();
                 Cls4Dev cd = table_dev(t);
                 const uint32_t *s4 = static_cast<const uint32_t*>(src), *d4 = static_cast<const uint32_t*>(dst);
                 const Pkts4 syn = framed(t.img, Pkts4{s4, d4, dp, pr, n}), ack = framed(t.img, Pkts4{d4, s4, sp, pr, n});
@@ -1399,7 +1500,6 @@ int cls_connect_batch(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t*
                 }
             } else {
                 auto& q = t.p16;
-                desc[big[b]].slot_rule = q.d_slot_rule.as<uint32_t>();
                 const Cls4Image& ci = q.img.core;
                 Cls4Dev cd = cls4_dev(ci, q.d_img, q.d_lin, uint32_t(q.lin.size()), t.n_rules);
                 cfg.other = cls4_dev(q.oimg, q.d_oimg, DevBuf(), 0, t.n_rules);
@@ -1415,55 +1515,6 @@ int cls_connect_batch(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t*
                 HIPC(e, launch_classify16_slots(cd, fe, ack, pre + stride, q.lds_resident, cfg));
             }
         }
-    }
-    // the rule pool of the linear ACLs
-    std::vector<uint8_t> pool;
-    const size_t rb = k16 ? sizeof(ConnRule16) : sizeof(ConnRule4);
-    const size_t lds_max0 = size_t(max_lds_bytes());
-    for (size_t j = 0; j < desc.size(); ++j) {
-        desc[j].bm_off = 0xFFFFFFFFu;
-        if (desc[j].pre_blk >= 0) {
-            desc[j].n = 0;
-            continue;
-        }
-        desc[j].rule_off = uint32_t(pool.size() / rb);
-        const uint8_t* r = k16 ? reinterpret_cast<const uint8_t*>(dtab[j]->conn16.data())
-                               : reinterpret_cast<const uint8_t*>(dtab[j]->conn4.data());
-        pool.insert(pool.end(), r, r + size_t(desc[j].n) * rb);
-    }
-    // IPv4: the bitmap form of the longer linear ACLs, longest first, while
-    // the pool (and the LDS counters when counting) still fit LDS -- a wave
-    // then pays a fixed number of reads per evaluation instead of its
-    // longest lane's scan (CONTIVCLS_CONN_BITMAP=0: scans only).
-    const char* bme = std::getenv("CONTIVCLS_CONN_BITMAP");
-    if (!k16 && n && !(flags & CLS_F_FORCE_LINEAR) && !(bme && std::atoi(bme) == 0)) {
-        // the LDS counters take their share only when they can be LDS counters
-        // at all (otherwise they are global, cmode 2); no subtraction wraps
-        const size_t ctr_b = count ? size_t(n_ctr) * 4 : 0, reserve = std::min<size_t>(lds_max0 / 8, 8192);
-        const size_t ctr_lds = ctr_b + reserve <= lds_max0 ? ctr_b : 0;
-        const size_t cap = lds_max0 - reserve - ctr_lds;
-        std::vector<size_t> order;
-        for (size_t j = 0; j < desc.size(); ++j)
-            if (desc[j].pre_blk < 0 && desc[j].n >= kConnBmMinRules) order.push_back(j);
-        std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) { return desc[a].n > desc[b].n; });
-        std::vector<uint32_t> words;
-        for (size_t j : order) {
-            Table& t = *dtab[j];
-            if (!t.conn_bm_built) {                         // once per table: rules are immutable
-                if (!conn_bitmap4(t.conn4, t.n_rules, kConnBmMaxWords, t.conn_bm)) t.conn_bm.clear();
-                t.conn_bm_built = true;
-            }
-            const size_t used = pool.size() + words.size() * 4;
-            if (t.conn_bm.empty() || used + t.conn_bm.size() * 4 > cap) continue;
-            desc[j].bm_off = uint32_t(used);                // the pool is a multiple of 32 B, blobs of 16 B
-            const std::vector<uint32_t>& h = t.conn_bm;     // header {W, ns, nd, nr, n0, n1, n2, n3}
-            desc[j].bm_sd = h[1] | (h[2] << 16);
-            desc[j].bm_tu = h[4] | (h[5] << 16);
-            desc[j].bm_w = h[0];
-            words.insert(words.end(), t.conn_bm.begin(), t.conn_bm.end());
-        }
-        const uint8_t* wb = reinterpret_cast<const uint8_t*>(words.data());
-        pool.insert(pool.end(), wb, wb + words.size() * 4);
     }
     ConnArgs a{};
     a.n_ifs = n_ifs;
@@ -1495,11 +1546,12 @@ int cls_connect_batch(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t*
         last.assign(b, b + bytes);
         return CLS_OK;
     };
-    {
+    if (e->up_plan != P.id) {                             // a kept plan's tables are on the device already
         int rc = upload(e->s_desc, e->up_desc, desc.data(), desc.size() * sizeof(ConnDesc), sizeof(ConnDesc));
         if (rc == CLS_OK) rc = upload(e->s_ifs, e->up_ifs, ifs.data(), ifs.size() * sizeof(IfAcls), sizeof(IfAcls));
         if (rc == CLS_OK) rc = upload(e->s_rules, e->up_rules, pool.data(), pool.size(), 16);
         if (rc != CLS_OK) return rc;
+        e->up_plan = dev ? P.id : ~0ull;
     }
     a.desc = e->s_desc.as<ConnDesc>();
     a.pre = big.empty() ? nullptr : e->s_pre.as<uint32_t>();
@@ -1508,8 +1560,14 @@ int cls_connect_batch(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t*
     a.rules = e->s_rules.p;
     std::vector<unsigned long long*> tctr;
     if (cmode) {
+        // the call counters are zero between calls (the scatter launch clears
+        // what it moves); cleared here only when (re)allocated
+        const size_t had = e->s_cctr.bytes;
         HIPC(e, e->s_cctr.ensure(size_t(n_ctr) * 8));
-        HIPC(e, hipMemsetAsync(e->s_cctr.p, 0, size_t(n_ctr) * 8, s));
+        if (e->s_cctr.bytes != had || !e->cctr_zero) {
+            HIPC(e, hipMemsetAsync(e->s_cctr.p, 0, e->s_cctr.bytes, s));
+            e->cctr_zero = true;
+        }
         a.ctr = e->s_cctr.as<unsigned long long>();
         for (size_t j = 0; j < dtab.size(); ++j) {
             Table& t = *dtab[j];
@@ -1545,9 +1603,12 @@ int cls_connect_batch(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t*
     const int grid = int(std::max<uint64_t>(1, std::min<uint64_t>(uint64_t(e->n_cu) * per_cu,
                                                                   (n + block - 1) / block)));
     HIPC(e, launch_connect(a, k16, lds_rules, cmode, grid, block, lds, s));
-    if (cmode && n)
+    if (cmode && n) {
+        uint32_t max_rules = 0;
+        for (const ConnDesc& d : desc) max_rules = std::max(max_rules, d.n_rules);
         HIPC(e, launch_conn_scatter(a.desc, e->s_tctr.as<unsigned long long* const>(), uint32_t(desc.size()),
-                                    e->s_cctr.as<unsigned long long>(), s));
+                                    max_rules, e->s_cctr.as<unsigned long long>(), s));
+    }
     if (!dev && n) HIPC(e, hipMemcpyAsync(out, o, n, hipMemcpyDeviceToHost, s));
     // descriptor, pool and counter buffers are engine scratch: finish before
     // they can be reused (and before the host vectors above go away)

@@ -521,15 +521,17 @@ __device__ __forceinline__ uint32_t conn_bm(const ConnArgs& a, const ConnDesc& D
 // 1. Evaluations.  A call on a large ACL reads the classifier's result word
 //    for this connection (classify4_pair / the slot launches); a call on a
 //    linear ACL is a *job*: the bitmap search (IPv4, conn_bm) or the rule
-//    scan.  A call index most of the wave's lanes have a job for runs in
-//    place; the jobs of the other call indices are packed (ranks from the
-//    calls' ballots, no LDS) and run 64 at a time, every lane on one job with
-//    its connection's fields fetched from the owning lane (ds_bpermute).  A
-//    lane-per-call loop alone would make the wave run the search once per
-//    call index in which any of its lanes has a job -- four passes per wave
-//    with ~0.6 jobs per connection -- where packing runs one.  Jobs are evaluated whether or not testConnection reaches the call
-//    (the call order needs the earlier results); only the calls it makes are
-//    counted.
+//    scan.  The jobs of all four possible calls of the wave's 64 connections
+//    are packed (ranks from the calls' ballots, no LDS) and run 64 at a time,
+//    every lane on one job with its connection's fields fetched from the
+//    owning lane (ds_bpermute).  A lane-per-call loop would make the wave run the
+//    search once per call index in which any of its lanes has a job -- four
+//    passes per wave with ~0.6 jobs per connection -- where packing runs
+//    one.  (Running a call index most lanes need in place, without the
+//    shuffles, measured slower: 84 -> 90 us at 12 local ACLs, 192 -> 234 us
+//    at 64, profiles/r04k_conn_dense_calls_ab.txt.)  Jobs are evaluated
+//    whether or not testConnection reaches the call (the call order needs
+//    the earlier results); only the calls it makes are counted.
 // 2. The state machine: testConnection's order and REFLECT short-cuts
 //    (aclengine_mock.go:394-471) over the four results: SYN through the
 //    source's inbound then the destination's outbound ACL, SYN-ACK through
@@ -591,48 +593,31 @@ __global__ __launch_bounds__(1024) void connect_kernel(ConnArgs a) {
         for (int k = 0; k < 4; ++k)
             w[k] = *(bi[k] >= 0 ? a.pre + (2ull * uint32_t(bi[k]) + uint32_t(k >> 1)) * a.pre_stride + ic
                                 : a.src_if + ic);
-        // ---- the jobs of the wave ----
-        // A call index most of the wave's lanes have a job for runs as one
-        // pass of its own, every lane on its own connection.  The jobs of the
-        // other call indices are packed (registers only): job j of the wave
-        // is call k of owner lane o; the ballots give every job a rank (owner
-        // side) and every running lane its job (nth_set_bit); the owner's
-        // fields come over ds_bpermute and the result goes back the same way
-        // -- a pass per 64 jobs instead of one per call index any lane has.
+        // ---- the jobs of the wave, packed (registers only) ----
+        // job j of the wave is call k of owner lane o: the ballots of the four
+        // calls give every job a rank (owner side) and every running lane its
+        // job (nth_set_bit); the owner's fields come over ds_bpermute and the
+        // result goes back the same way
         bool job[4];
         uint64_t m[4];
-        uint32_t c[5], jpos[4], dense = 0u;
+        uint32_t c[5], jpos[4];
         c[0] = 0;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             job[k] = di[k] >= 0 && bi[k] < 0;
             m[k] = __ballot(job[k]);
-            if (__popcll(m[k]) > 32) {                          // wave-uniform
-                dense |= 1u << k;
-                m[k] = 0ull;
-            }
             jpos[k] = c[k] + uint32_t(__popcll(m[k] & lt));
             c[k + 1] = c[k] + uint32_t(__popcll(m[k]));
         }
-        const uint32_t nj = c[4], nd = uint32_t(__builtin_popcount(dense));
-        const uint32_t passes = nd + (nj + 63u) / 64u;
+        const uint32_t nj = c[4];
         uint32_t rj[4] = {0u, 0u, 0u, 0u};
-        for (uint32_t pass = 0; pass < passes; ++pass) {      // wave-uniform
-            uint32_t k, o, j0 = 0u;
-            bool act;
-            if (pass < nd) {                                    // a dense call index, in place
-                k = nth_set_bit(dense, pass);
-                o = lane;
-                act = k == 0u ? job[0] : k == 1u ? job[1] : k == 2u ? job[2] : job[3];
-            } else {
-                j0 = (pass - nd) * 64u;
-                const uint32_t j = j0 + lane;
-                act = j < nj;
-                k = uint32_t(j >= c[1]) + uint32_t(j >= c[2]) + uint32_t(j >= c[3]);
-                const uint64_t mk = k == 0u ? m[0] : k == 1u ? m[1] : k == 2u ? m[2] : m[3];
-                const uint32_t ck = k == 0u ? c[0] : k == 1u ? c[1] : k == 2u ? c[2] : c[3];
-                o = act ? nth_set_bit(mk, j - ck) : lane;
-            }
+        for (uint32_t j0 = 0; j0 < nj; j0 += 64u) {             // wave-uniform
+            const uint32_t j = j0 + lane;
+            const bool act = j < nj;
+            const uint32_t k = uint32_t(j >= c[1]) + uint32_t(j >= c[2]) + uint32_t(j >= c[3]);
+            const uint64_t mk = k == 0u ? m[0] : k == 1u ? m[1] : k == 2u ? m[2] : m[3];
+            const uint32_t ck = k == 0u ? c[0] : k == 1u ? c[1] : k == 2u ? c[2] : c[3];
+            const uint32_t o = act ? nth_set_bit(mk, j - ck) : lane;
             // the owning lane's connection (every lane takes part in the shuffles)
             A xs, xd;
             if constexpr (k16) {
@@ -661,16 +646,10 @@ __global__ __launch_bounds__(1024) void connect_kernel(ConnArgs a) {
                 out = res | ((D.ctr_off + rule) << 2);
             }
             // the owners take their results of this pass
-            if (pass < nd) {
 #pragma unroll
-                for (int kk = 0; kk < 4; ++kk)
-                    if (uint32_t(kk) == k && job[kk]) rj[kk] = out;
-            } else {
-#pragma unroll
-                for (int kk = 0; kk < 4; ++kk) {
-                    const uint32_t r = __shfl(out, int((jpos[kk] - j0) & 63u));
-                    if (((m[kk] >> lane) & 1ull) && jpos[kk] >= j0 && jpos[kk] < j0 + 64u) rj[kk] = r;
-                }
+            for (int kk = 0; kk < 4; ++kk) {
+                const uint32_t r = __shfl(out, int((jpos[kk] - j0) & 63u));
+                if (job[kk] && jpos[kk] >= j0 && jpos[kk] < j0 + 64u) rj[kk] = r;
             }
         }
         // ---- testConnection over the four results ----
@@ -717,18 +696,31 @@ __global__ __launch_bounds__(1024) void connect_kernel(ConnArgs a) {
                 if (made[k] && di[k] >= 0) {                    // nil ACLs are not counted
                     if (job[k]) {
                         key[k] = rj[k] >> 2;
-                    } else {
+                    } else {                                    // a large ACL: its slot's rule
                         const ConnDesc D = conn_desc(a, uint32_t(di[k]));
                         key[k] = D.ctr_off + D.slot_rule[w[k] >> 2];
                     }
                 }
             }
             if constexpr (kCount == 1) {
+                // a popular rule (the global ACL's) would serialise the LDS
+                // atomic over the lanes holding it: the wave adds its first
+                // key once with the count of lanes holding it, the rest lane
+                // by lane
 #pragma unroll
-                for (int k = 0; k < 4; ++k)
-                    if (key[k] != 0xFFFFFFFFu)
+                for (int k = 0; k < 4; ++k) {
+                    const uint64_t pend = __ballot(key[k] != 0xFFFFFFFFu);
+                    if (!pend) continue;                        // wave-uniform
+                    const int leader = __builtin_ctzll(pend);
+                    const uint32_t lk = __shfl(key[k], leader);
+                    const uint64_t same = __ballot(key[k] == lk);
+                    if (int(lane) == leader)
+                        __hip_atomic_fetch_add(lctr_t(a.ctr_lds + 4u * lk), uint32_t(__popcll(same)), __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP);
+                    else if (key[k] != 0xFFFFFFFFu && key[k] != lk)
                         __hip_atomic_fetch_add(lctr_t(a.ctr_lds + 4u * key[k]), 1u, __ATOMIC_RELAXED,
                                                __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
             } else {
 #pragma unroll
                 for (int k = 0; k < 4; ++k) wave_count(a.ctr, key[k]);
@@ -744,19 +736,20 @@ __global__ __launch_bounds__(1024) void connect_kernel(ConnArgs a) {
     }
 }
 
-// The call's counters -> the tables' connection counters (one workgroup per
-// descriptor; a table has one descriptor per call), cleared for the next call.
+// The call's counters -> the tables' connection counters, cleared for the
+// next call (so the call counters stay zero between calls).  Workgroup
+// (x, y): descriptor x (a table has one descriptor per call), counters
+// 256 y .. 256 y + 255 -- one counter per thread, not a loop per table.
 __global__ __launch_bounds__(256) void conn_scatter_kernel(const ConnDesc* __restrict__ desc,
                                                            unsigned long long* const* __restrict__ table_ctr,
                                                            unsigned long long* __restrict__ call_ctr) {
     const ConnDesc D = desc[blockIdx.x];
-    unsigned long long* out = table_ctr[blockIdx.x];
-    for (uint32_t r = threadIdx.x; r <= D.n_rules; r += blockDim.x) {
-        const unsigned long long v = call_ctr[D.ctr_off + r];
-        if (v) {
-            atomicAdd(&out[r], v);
-            call_ctr[D.ctr_off + r] = 0ull;
-        }
+    const uint32_t r = blockIdx.y * blockDim.x + threadIdx.x;
+    if (r > D.n_rules) return;
+    const unsigned long long v = call_ctr[D.ctr_off + r];
+    if (v) {
+        atomicAdd(&table_ctr[blockIdx.x][r], v);
+        call_ctr[D.ctr_off + r] = 0ull;
     }
 }
 
@@ -959,9 +952,10 @@ hipError_t launch_connect(const ConnArgs& a, bool k16, bool lds_rules, int count
 }
 
 hipError_t launch_conn_scatter(const ConnDesc* desc, unsigned long long* const* table_ctr, uint32_t n_desc,
-                               unsigned long long* call_ctr, hipStream_t s) {
+                               uint32_t max_rules, unsigned long long* call_ctr, hipStream_t s) {
     if (n_desc == 0) return hipSuccess;
-    hipLaunchKernelGGL(conn_scatter_kernel, dim3(n_desc), dim3(256), 0, s, desc, table_ctr, call_ctr);
+    hipLaunchKernelGGL(conn_scatter_kernel, dim3(n_desc, max_rules / 256u + 1u), dim3(256), 0, s, desc, table_ctr,
+                       call_ctr);
     return hipGetLastError();
 }
 

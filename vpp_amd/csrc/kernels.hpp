@@ -242,9 +242,10 @@ hipError_t launch_connect(const ConnArgs& a, bool k16, bool lds_rules, int count
 // ports, 4-B proto and out)
 hipError_t launch_stream_conn(const ConnArgs& a, int grid, hipStream_t s);
 // tables' connection counters += the call's counters (ConnDesc ctr_off ..
-// + n_rules), which are cleared: one workgroup per descriptor
+// + n_rules), which are cleared: a workgroup per descriptor and 256
+// counters (max_rules: the largest n_rules of the descriptors)
 hipError_t launch_conn_scatter(const ConnDesc* desc, unsigned long long* const* table_ctr, uint32_t n_desc,
-                               unsigned long long* call_ctr, hipStream_t s);
+                               uint32_t max_rules, unsigned long long* call_ctr, hipStream_t s);
 
 struct TrafficDev {
     uint64_t seed;

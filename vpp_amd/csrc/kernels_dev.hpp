@@ -480,14 +480,15 @@ __device__ __forceinline__ void wave_count_cold(unsigned long long* gslot, uint3
 // every slot has a u32 LDS counter; 1 -- u16 LDS counters for slots <
 // n_lctr (compile.hpp Cls4Image counter tiers), global counters above.
 // pr_any: some packet of the group has a protocol outside TCP/UDP/ICMP; those
-// packets are classified on the OTHER image `o` (global memory) from `sl`
-// (their source, or its rep on the 16-byte path).
-template <int N, bool kLds, int kMode, int kList, int kD, int kCtr>
+// packets are queued for the finish launch (counting) or classified on the
+// OTHER image `o` in place (slot mode, full queue) from sl(q): packet q's
+// source, or on the 16-byte path its rep -- computed only for those.
+template <int N, bool kLds, int kMode, int kList, int kD, int kCtr, typename SrcOf>
 __device__ __forceinline__ void run_n(const Img<kLds>& im, const Cls4Dev& t, const Cls4Dev& o, uint32_t hot_lane,
                                       unsigned long long* gslot, uint32_t& hot0,
                                       const uint32_t (&s)[N], const uint32_t (&d)[N],
                                       const uint32_t (&dp)[N], const uint32_t (&pr)[N],
-                                      bool pr_any, uint32_t (&res)[N], const uint32_t (&sl)[N],
+                                      bool pr_any, uint32_t (&res)[N], const SrcOf& sl,
                                       const uint32_t (&idx)[N], uint32_t oq_lds) {
     uint32_t slot[N];
     classify_n<N, kLds, kMode, kList, kD>(im, t, s, d, dp, pr, res, slot);
@@ -509,7 +510,7 @@ __device__ __forceinline__ void run_n(const Img<kLds>& im, const Cls4Dev& t, con
 #pragma unroll
             for (int q = 0; q < N; ++q) {
                 if (pr[q] > 2u) {
-                    const uint32_t s1[1] = {sl[q]}, d1[1] = {d[q]}, p1[1] = {dp[q]}, z1[1] = {0u};
+                    const uint32_t s1[1] = {sl(q)}, d1[1] = {d[q]}, p1[1] = {dp[q]}, z1[1] = {0u};
                     uint32_t r1[1], k1[1];
                     classify_n<1, false, 0, 0, -1>(oim, o, s1, d1, p1, z1, r1, k1);
                     res[q] = r1[0] | ((t.n_ctr + k1[0]) << 2);
@@ -521,7 +522,9 @@ __device__ __forceinline__ void run_n(const Img<kLds>& im, const Cls4Dev& t, con
 #pragma unroll
     for (int q = 0; q < N; ++q) {
         if constexpr (kLds && kCtr == 0) {
-            addr[q] = slot[q] < t.n_hot ? hot_lane + slot[q] * 256u : t.img_bytes + slot[q] * 4u;
+            // a packet of protocol > 2 (counted by its OTHER evaluation) adds
+            // to a spare word after the OTHER queue counter instead: no branch
+            addr[q] = pr[q] > 2u ? oq_lds + 4u : slot[q] < t.n_hot ? hot_lane + slot[q] * 256u : t.img_bytes + slot[q] * 4u;
             __hip_atomic_fetch_add(lctr_t(addr[q]), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         } else if constexpr (kLds) {
             // Tiered counters.  A u16 counter lives in half of an LDS word; the
@@ -569,38 +572,44 @@ __device__ __forceinline__ void run_n(const Img<kLds>& im, const Cls4Dev& t, con
     // image's).
     if (__any(pr_any)) {
         const Img<false> oim{reinterpret_cast<const uint8_t*>(o.img)};
+        // one queue reservation for the wave's OTHER packets of all N slots
+        uint64_t m[N];
+        uint32_t pre[N + 1];
+        pre[0] = 0u;
 #pragma unroll
         for (int q = 0; q < N; ++q) {
-            const bool oth = pr[q] > 2u;
-            if constexpr (kLds && kCtr == 0) {                        // undo the main image's count
-                if (oth)
-                    __hip_atomic_fetch_add(lctr_t(addr[q]), ~0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            }
-            bool now = oth;
-            const unsigned long long m = __ballot(oth);
-            if (m && t.oq) {
-                // this workgroup's queue segment, its fill counted in LDS
-                const int leader = __builtin_ctzll(m);
-                uint32_t base = 0;
-                if (int(__lane_id()) == leader)
-                    base = __hip_atomic_fetch_add(lctr_t(oq_lds), uint32_t(__popcll(m)), __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_WORKGROUP);
-                base = __shfl(base, leader);
-                const uint32_t pos = base + uint32_t(__popcll(m & ((1ull << __lane_id()) - 1ull)));
-                if (oth && pos < t.oq_cap) {
+            m[q] = __ballot(pr[q] > 2u);
+            pre[q + 1] = pre[q] + uint32_t(__popcll(m[q]));
+        }
+        uint32_t base = 0u;
+        if (t.oq) {
+            // this workgroup's queue segment, its fill counted in LDS
+            if (__lane_id() == 0u)
+                base = __hip_atomic_fetch_add(lctr_t(oq_lds), pre[N], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            base = __shfl(base, 0);
+        }
+        const uint64_t lt = (1ull << __lane_id()) - 1ull;
+#pragma unroll
+        for (int q = 0; q < N; ++q) {
+            bool now = pr[q] > 2u;
+            if (t.oq && now) {
+                const uint32_t pos = base + pre[q] + uint32_t(__popcll(m[q] & lt));
+                if (pos < t.oq_cap) {
                     t.oq[gridDim.x + blockIdx.x * t.oq_cap + pos] = idx[q];
                     now = false;
                 }
             }
-            uint32_t key = 0xFFFFFFFFu;
-            if (now) {                                                 // only these lanes load
-                const uint32_t s1[1] = {sl[q]}, d1[1] = {d[q]}, p1[1] = {dp[q]}, z1[1] = {0u};
-                uint32_t r1[1], k1[1];
-                classify_n<1, false, 0, 0, -1>(oim, o, s1, d1, p1, z1, r1, k1);
-                res[q] = r1[0];
-                key = t.n_ctr + k1[0];
+            if (__any(now)) {                                          // the queue is full: here and now
+                uint32_t key = 0xFFFFFFFFu;
+                if (now) {                                             // only these lanes load
+                    const uint32_t s1[1] = {sl(q)}, d1[1] = {d[q]}, p1[1] = {dp[q]}, z1[1] = {0u};
+                    uint32_t r1[1], k1[1];
+                    classify_n<1, false, 0, 0, -1>(oim, o, s1, d1, p1, z1, r1, k1);
+                    res[q] = r1[0];
+                    key = t.n_ctr + k1[0];
+                }
+                wave_count(gslot, key);
             }
-            wave_count(gslot, key);
         }
     }
 }
@@ -693,8 +702,8 @@ __global__ __launch_bounds__(kClsBlock) void classify4_cls(Cls4Dev t, Cls4Dev o,
             const bool other = ((pr | ((pr & 0x7F7F7F7Fu) + 0x7D7D7D7Du)) & 0x80808080u) != 0u;
             uint32_t v[4];
             const uint32_t ix[4] = {4u * g, 4u * g + 1u, 4u * g + 2u, 4u * g + 3u};
-            run_n<4, kLds, kMode, kList, kD, kCtr>(im, t, o, hot_lane, gslot, hot0, sa, da, pa, ra, other, v, sa, ix,
-                                                   oq_lds);
+            run_n<4, kLds, kMode, kList, kD, kCtr>(im, t, o, hot_lane, gslot, hot0, sa, da, pa, ra, other, v,
+                                                   [&](int q) { return sa[q]; }, ix, oq_lds);
             if constexpr (kCtr == 2)                             // slot mode: 4 result words per lane
                 reinterpret_cast<uint4*>(verdict)[g] = make_uint4(v[0], v[1], v[2], v[3]);
             else if (verdict)
@@ -735,7 +744,7 @@ __global__ __launch_bounds__(kClsBlock) void classify4_cls(Cls4Dev t, Cls4Dev o,
             const uint32_t ix[4] = {4u * gi, 4u * gi + 1u, 4u * gi + 2u, 4u * gi + 3u};
             run_n<4, kLds, kMode, kList, -1, kCtr>(im, t, o, hot_lane, gslot, hot0, sa, da, pa, ra,
                                                    ((pr | ((pr & 0x7F7F7F7Fu) + 0x7D7D7D7Du)) & 0x80808080u) != 0u,
-                                                   v, sa, ix, oq_lds);
+                                                   v, [&](int q) { return sa[q]; }, ix, oq_lds);
             if constexpr (kCtr == 2)
                 reinterpret_cast<uint4*>(verdict)[gi] = make_uint4(v[0], v[1], v[2], v[3]);
             else if (verdict)
@@ -748,8 +757,8 @@ __global__ __launch_bounds__(kClsBlock) void classify4_cls(Cls4Dev t, Cls4Dev o,
         const uint32_t sa[1] = {p.src[i]}, da[1] = {p.dst[i]}, pa[1] = {p.dport[i]}, ra[1] = {p.proto[i]};
         uint32_t v[1];
         const uint32_t ix[1] = {i};
-        run_n<1, kLds, kMode, kList, -1, kCtr>(im, t, o, hot_lane, gslot, hot0, sa, da, pa, ra, ra[0] > 2u, v, sa,
-                                               ix, oq_lds);
+        run_n<1, kLds, kMode, kList, -1, kCtr>(im, t, o, hot_lane, gslot, hot0, sa, da, pa, ra, ra[0] > 2u, v,
+                                               [&](int q) { return sa[q]; }, ix, oq_lds);
         if constexpr (kCtr == 2) reinterpret_cast<uint32_t*>(verdict)[i] = v[0];   // slot mode: res | slot << 2
         else if (verdict) verdict[i] = uint8_t(v[0]);
     }
@@ -937,18 +946,15 @@ __global__ __launch_bounds__(kClsBlock) void classify16_cls(Cls4Dev t, Cls4Dev o
         } else if constexpr (kFe >= 1) {
             if constexpr (kFe == 1) src_hash16(im, fe, s16, sa);   // class rows, not reps
             else src_trie16(im, t, fe, s16, sa);
-            uint32_t sl[N];
-            if (__any(other)) {                                // rare: protocols > 2 need the rep
-#pragma unroll
-                for (int q = 0; q < N; ++q)
-                    sl[q] = ra[q] > 2u ? src_rep_global(fe.gsrc, fe.gval, fe.gtop, fe.gk8, s16[q]) : 0u;
-            }
-            run_n<N, kLds, kMode, kList, kD, kCtr>(im, t, o, hot_lane, gslot, hot0, sa, da, pa, ra, other, v, sl, ix,
-                                                   oq_lds);
+            // protocols > 2 need the source's rep (the OTHER image is in rep
+            // space): only for a packet classified in place, not queued
+            run_n<N, kLds, kMode, kList, kD, kCtr>(
+                im, t, o, hot_lane, gslot, hot0, sa, da, pa, ra, other, v,
+                [&](int q) { return src_rep_global(fe.gsrc, fe.gval, fe.gtop, fe.gk8, s16[q]); }, ix, oq_lds);
         } else {
             src_rep(s16, sa);
-            run_n<N, kLds, kMode, kList, kD, kCtr>(im, t, o, hot_lane, gslot, hot0, sa, da, pa, ra, other, v, sa, ix,
-                                                   oq_lds);
+            run_n<N, kLds, kMode, kList, kD, kCtr>(im, t, o, hot_lane, gslot, hot0, sa, da, pa, ra, other, v,
+                                                   [&](int q) { return sa[q]; }, ix, oq_lds);
         }
     };
     // 4 packets per lane per step (vector dport / proto / verdict words).
