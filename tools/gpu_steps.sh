@@ -13,9 +13,15 @@
 #                      with rocprofv3 kernel stats
 #   gp16:<lib,...>     gen-policy ingress lists, 16-byte layout, 10 % IPv6
 #   gp:<layout>        gen-policy 20-block list: 64 / 256 Mi packets, TCP/UDP only
+#   gpmix:<layout>     the 20-block list without protocol 47, without ICMP
+#   gpb:<bytes>:<layout>:<blocks>  a gen-policy ingress list compiled with an
+#                      LDS budget of <bytes> (CONTIVCLS_LDS_BUDGET: counter tiers)
 #   ab:<config>:<lib>  one-process A/B of the classify kernel against a variant
 #   sq:<config>        SQ counter passes of the classify kernel (tools/sq_profile.sh)
+#   sqgp:<layout>:<blocks>  the same for a gen-policy ingress list
 #   pmc:<config>       HBM traffic PMC passes (tools/gpu_pmc.sh)
+#   fetchgp:<layout>:<blocks>  FETCH_SIZE of the classify kernel on a gen-policy
+#                      ingress list against its algorithmic bytes
 set -e -o pipefail
 TAG=$1; shift
 R=$(cd "$(dirname "$0")/.." && pwd)
@@ -66,12 +72,37 @@ for step in "$@"; do
     done
     timeout -k 10 300 python tools/genpolicy_bench.py --layout $arg --blocks 20 --match ingress --packets 67108864 --iters 5 --mix 0.5 0.5 0 0 > $O/gp${arg}_tcpudp.jsonl 2> $O/gp${arg}_tcpudp.err
     echo "-- TCP/UDP only"; python3 tools/jl.py $O/gp${arg}_tcpudp.jsonl kernel_ms Gpps_kernel hbm_frac_kernel ;;
+  gpmix)
+    for mix in "0.445 0.445 0.11 0" "0.495 0.495 0 0.01"; do
+      timeout -k 10 300 python tools/genpolicy_bench.py --layout $arg --blocks 20 --match ingress --packets 67108864 --iters 5 --mix $mix > $O/gpmix$arg.jsonl 2> $O/gpmix$arg.err
+      echo "-- mix $mix"; python3 tools/jl.py $O/gpmix$arg.jsonl kernel_ms Gpps_kernel hbm_frac_kernel
+    done ;;
+  gpb)
+    bud=${arg%%:*}; rest=${arg#*:}; lay=${rest%%:*}; nb=${rest#*:}
+    CONTIVCLS_LDS_BUDGET=$bud timeout -k 10 300 python tools/genpolicy_bench.py --layout $lay --v6 0.1 --blocks $nb --match ingress --packets 67108864 --iters 5 > $O/gpb_${bud}_${lay}_$nb.jsonl 2> $O/gpb_${bud}_${lay}_$nb.err
+    python3 tools/jl.py $O/gpb_${bud}_${lay}_$nb.jsonl rules ctr16 lds_slots slots kernel_ms Gpps_kernel ;;
   ab)
     cfg=${arg%%:*}; v=${arg#*:}
     bash tools/gpu_ab.sh $TAG $cfg $(lib $v) ;;
   sq)
     bash tools/sq_profile.sh ${TAG}_c$arg --config $arg > /dev/null 2>&1
     cat gpurun_out/sq_${TAG}_c$arg/summary.txt ;;
+  sqgp)
+    lay=${arg%%:*}; nb=${arg#*:}
+    SQ_CMD="python3 $R/tools/genpolicy_bench.py --layout $lay --v6 0.1 --blocks $nb --match ingress --iters 2 --packets 67108864" bash tools/sq_profile.sh ${TAG}_gp${lay}_$nb > /dev/null 2>&1
+    cat gpurun_out/sq_${TAG}_gp${lay}_$nb/summary.txt ;;
+  fetchgp)
+    lay=${arg%%:*}; nb=${arg#*:}
+    (cd /tmp && timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $O/fetch_gp${lay}_$nb -o run --output-format csv -- python3 $R/tools/genpolicy_bench.py --layout $lay --v6 0.1 --blocks $nb --match ingress --iters 2 --packets 67108864 > $O/fetch_gp${lay}_$nb.log 2>&1)
+    python3 - $O/fetch_gp${lay}_$nb $lay <<'PY'
+import csv, glob, sys
+vals = [float(r["Counter_Value"]) for f in glob.glob(sys.argv[1] + "/*/run_counter_collection.csv")
+        for r in csv.DictReader(open(f)) if "classify" in r["Kernel_Name"] and r["Counter_Name"] == "FETCH_SIZE"]
+alg = (12 if sys.argv[2] == "4" else 36) * 67108864 - 67108864       # reads only (the verdict byte is written)
+for v in vals:
+    print("FETCH_SIZE %.0f KiB -> %.3f GB read (x2, gfx950), %.3fx the %.3f GB algorithmic reads" % (v, v * 2048 / 1e9, v * 2048 / alg, alg / 1e9))
+PY
+    ;;
   pmc)
     bash tools/gpu_pmc.sh ${TAG}_pmc$arg $arg > /dev/null 2>&1
     grep -h "ratio\|source_hash" gpurun_out/${TAG}_pmc$arg/pmc.json ;;

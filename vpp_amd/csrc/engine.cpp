@@ -175,6 +175,7 @@ struct cls_engine {
     // scratch for host-pointer batches
     DevBuf s_src, s_dst, s_sport, s_dport, s_proto, s_verdict, s_if_a, s_if_b, s_desc, s_ifs;
     DevBuf s_pre;                  // connection path: classifier slot words per large ACL (8 bytes/connection)
+    DevBuf s_pq;                   // connection path: the pair launch's OTHER queue
     DevBuf s_rules, s_tctr, s_cctr;  // connection path: rule pool, table counter pointers, call counters
     bool cctr_zero = false;          // s_cctr cleared since its allocation (the scatter launch keeps it zero)
     uint64_t conn_gen = 0;           // bumped by every change of tables or interface bindings
@@ -1484,14 +1485,16 @@ int cls_connect_batch(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t*
                                   aligned(sp, 8) && aligned(pr, 4) && !std::getenv("CONTIVCLS_CONN_NO_PAIR");
                 if (pair) {
                     uint32_t o_at = (t.img.img_bytes + 15u) & ~15u;
-                    if (o_at + t.oimg.img_bytes > uint32_t(max_lds_bytes())) o_at = 0;
+                    // (+ 32: the queue fill word after the images)
+                    if (o_at + t.oimg.img_bytes + 32u > uint32_t(max_lds_bytes())) o_at = 0;
                     Cls4Dev od = cls4_dev(t.oimg, t.d_oimg, DevBuf(), 0, t.n_rules);
                     if (o_at) {
                         od.off_bounds += o_at; od.off_iclass += o_at; od.off_cells += o_at;
                         od.off_lists += o_at; od.off_tmpl += o_at;
                     }
                     cfg.grid = cls_grid(e, true, true, o_at ? o_at + t.oimg.img_bytes : t.img.img_bytes, n);
-                    HIPC(e, launch_classify4_pair(cd, od, o_at, syn, sp, pre, stride, cfg));
+                    HIPC(e, e->s_pq.ensure(size_t(cfg.grid) * pair_queue_words(n, cfg.grid) * 4));
+                    HIPC(e, launch_classify4_pair(cd, od, o_at, syn, sp, pre, stride, e->s_pq.as<uint32_t>(), cfg));
                 } else {
                     cfg.other = cls4_dev(t.oimg, t.d_oimg, DevBuf(), 0, t.n_rules);
                     cfg.grid = cls_grid(e, true, t.lds_resident, t.img.lds_bytes, n);

@@ -10,28 +10,29 @@
 // stages the image once per workgroup and reads each connection's fields
 // once (13 B), writing 8 B.  The OTHER image (protocols > 2: networks alone
 // decide, evalACL's switch has no case) is staged beside the main image
-// when both fit LDS (no slot counters in this mode), so those connections
-// are classified from LDS in place instead of by a chain of global loads.
+// when both fit LDS (no slot counters in this mode).  Those connections are
+// queued (the workgroup's segment of oq, its fill counted in LDS) and
+// classified on the OTHER image after the workgroup's main loop, one per
+// lane: the OTHER chain (interval search, candidate scan) then runs once per
+// 1024 of them instead of once per wave step that holds any.
 #include "kernels_dev.hpp"
 
 namespace cls {
 
 namespace {
 
+static_assert(kClsBlock == kPairBlock, "pair_queue_words sizes the queue for this block");
+
 template <int kMode, int kList, int kD>
 __global__ __launch_bounds__(kClsBlock) void classify4_pair(Cls4Dev t, Cls4Dev o, uint32_t o_at, Pkts4 p,
-                                                            const uint16_t* sport, uint32_t* out, uint64_t stride) {
+                                                            const uint16_t* sport, uint32_t* out, uint64_t stride,
+                                                            uint32_t* oq, uint32_t oq_seg, uint32_t q_lds) {
     extern __shared__ uint4 smem[];
-    {
-        const uint4* a = reinterpret_cast<const uint4*>(t.img);
-        for (uint32_t i = threadIdx.x; i < t.img_bytes / 16u; i += blockDim.x) smem[i] = a[i];
-        if (o_at) {
-            const uint4* b = reinterpret_cast<const uint4*>(o.img);
-            uint4* ob = smem + o_at / 16u;
-            for (uint32_t i = threadIdx.x; i < o.img_bytes / 16u; i += blockDim.x) ob[i] = b[i];
-        }
-        __syncthreads();
-    }
+    typedef __attribute__((address_space(3))) uint32_t* lctr_t;
+    if (threadIdx.x == 0) *lctr_t(q_lds) = 0u;          // the queue fill (made visible by the barrier below)
+    lds_copy(smem, reinterpret_cast<const uint4*>(t.img), t.img_bytes / 16u);
+    if (o_at) lds_copy(smem + o_at / 16u, reinterpret_cast<const uint4*>(o.img), o.img_bytes / 16u);
+    __syncthreads();
     const Img<true> im{nullptr};
     const Img<false> og{reinterpret_cast<const uint8_t*>(o.img)};
     // protocols > 2, both tuples of one connection -- SYN (s, d, dp) and
@@ -75,46 +76,25 @@ __global__ __launch_bounds__(kClsBlock) void classify4_pair(Cls4Dev t, Cls4Dev o
             w1[q] = r1[q] | (k1[q] << 2);
         }
         // Some protocol byte > 2 (SWAR, as classify4_cls): those connections
-        // are packed over the wave -- job j is packet q of owner lane o, from
-        // the four packet slots' ballots (nth_set_bit) -- and run 64 at a
-        // time, each lane on one connection's two tuples: one pass of the
-        // OTHER image's chain per wave step instead of one per packet slot
-        // and tuple (a wave step holds ~15 such connections at 6 %).
+        // go to the workgroup's queue (one reservation per wave step); their
+        // words above are overwritten after the main loop
         if (__any(((pr | ((pr & 0x7F7F7F7Fu) + 0x7D7D7D7Du)) & 0x80808080u) != 0u)) {
             uint64_t m[4];
-            uint32_t c[5], jp[4];
+            uint32_t c[5];
             c[0] = 0;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 m[q] = __ballot(ra[q] > 2u);
-                jp[q] = c[q] + uint32_t(__popcll(m[q] & lt));
                 c[q + 1] = c[q] + uint32_t(__popcll(m[q]));
             }
-            for (uint32_t j0 = 0; j0 < c[4]; j0 += 64u) {        // wave-uniform
-                const uint32_t j = j0 + lane;
-                const bool act = j < c[4];
-                const uint32_t q = uint32_t(j >= c[1]) + uint32_t(j >= c[2]) + uint32_t(j >= c[3]);
-                const uint64_t mq = q == 0u ? m[0] : q == 1u ? m[1] : q == 2u ? m[2] : m[3];
-                const uint32_t cq = q == 0u ? c[0] : q == 1u ? c[1] : q == 2u ? c[2] : c[3];
-                const int ow = int(act ? nth_set_bit(mq, j - cq) : lane);
-                auto pick = [&](const uint32_t (&v)[4]) {
-                    const uint32_t x0 = __shfl(v[0], ow), x1 = __shfl(v[1], ow);
-                    const uint32_t x2 = __shfl(v[2], ow), x3 = __shfl(v[3], ow);
-                    return q == 0u ? x0 : q == 1u ? x1 : q == 2u ? x2 : x3;
-                };
-                const uint32_t xs = pick(sa), xd = pick(da), xdp = pick(dpa), xsp = pick(spa);
-                uint32_t v0 = 0u, v1 = 0u;
-                if (act) other2(xs, xd, xdp, xsp, v0, v1);
+            uint32_t base = 0u;
+            if (lane == 0u)
+                base = __hip_atomic_fetch_add(lctr_t(q_lds), c[4], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            base = __shfl(base, 0);
 #pragma unroll
-                for (int qq = 0; qq < 4; ++qq) {
-                    const int src = int((jp[qq] - j0) & 63u);
-                    const uint32_t y0 = __shfl(v0, src), y1 = __shfl(v1, src);
-                    if (ra[qq] > 2u && jp[qq] >= j0 && jp[qq] < j0 + 64u) {
-                        w0[qq] = y0;
-                        w1[qq] = y1;
-                    }
-                }
-            }
+            for (int q = 0; q < 4; ++q)
+                if (ra[q] > 2u) oq[uint64_t(blockIdx.x) * oq_seg + base + c[q] + uint32_t(__popcll(m[q] & lt))] =
+                    4u * g + uint32_t(q);
         }
         OS[g] = make_uint4(w0[0], w0[1], w0[2], w0[3]);
         OA[g] = make_uint4(w1[0], w1[1], w1[2], w1[3]);
@@ -135,44 +115,57 @@ __global__ __launch_bounds__(kClsBlock) void classify4_pair(Cls4Dev t, Cls4Dev o
         out[i] = w0;
         out[stride + i] = w1;
     }
+    // the queued connections of protocol > 2, one per lane (the barrier
+    // orders their words after the main loop's stores of the same words)
+    __syncthreads();
+    const uint32_t nq = *lctr_t(q_lds);
+    for (uint32_t j = threadIdx.x; j < nq; j += blockDim.x) {
+        const uint32_t i = oq[uint64_t(blockIdx.x) * oq_seg + j];
+        uint32_t w0, w1;
+        other2(p.src[i], p.dst[i], p.dport[i], sport[i], w0, w1);
+        out[i] = w0;
+        out[stride + i] = w1;
+    }
 }
 
 template <int kMode, int kList, int kD>
 void launch_pair_d(const Cls4Dev& t, const Cls4Dev& o, uint32_t o_at, const Pkts4& p, const uint16_t* sport,
-                   uint32_t* out, uint64_t stride, const LaunchCfg& cfg) {
-    const size_t lds = o_at ? o_at + o.img_bytes : t.img_bytes;
+                   uint32_t* out, uint64_t stride, uint32_t* oq, const LaunchCfg& cfg) {
+    const uint32_t q_lds = ((o_at ? o_at + o.img_bytes : t.img_bytes) + 15u) & ~15u;   // the queue fill word
+    const size_t lds = q_lds + 16u;
     lds_attr(reinterpret_cast<const void*>(classify4_pair<kMode, kList, kD>), lds);
     hipLaunchKernelGGL((classify4_pair<kMode, kList, kD>), dim3(cfg.grid), dim3(kClsBlock), lds, cfg.stream, t, o,
-                       o_at, p, sport, out, stride);
+                       o_at, p, sport, out, stride, oq, uint32_t(pair_queue_words(p.n, cfg.grid)), q_lds);
 }
 
 // sublist modes: the search depth as a template argument (the rendered
 // global tables' one-length hash, as the hot classify kernel)
 template <int kMode, int kList>
 void launch_pair(const Cls4Dev& t, const Cls4Dev& o, uint32_t o_at, const Pkts4& p, const uint16_t* sport,
-                 uint32_t* out, uint64_t stride, const LaunchCfg& cfg) {
+                 uint32_t* out, uint64_t stride, uint32_t* oq, const LaunchCfg& cfg) {
     if constexpr (kMode == 2 && (kList == 3 || kList == 4)) {
         switch (t.bv_steps) {
-        case 0: launch_pair_d<kMode, kList, 0>(t, o, o_at, p, sport, out, stride, cfg); return;
-        case 1: launch_pair_d<kMode, kList, 1>(t, o, o_at, p, sport, out, stride, cfg); return;
-        case 2: launch_pair_d<kMode, kList, 2>(t, o, o_at, p, sport, out, stride, cfg); return;
-        case 3: launch_pair_d<kMode, kList, 3>(t, o, o_at, p, sport, out, stride, cfg); return;
-        case 4: launch_pair_d<kMode, kList, 4>(t, o, o_at, p, sport, out, stride, cfg); return;
-        case 5: launch_pair_d<kMode, kList, 5>(t, o, o_at, p, sport, out, stride, cfg); return;
+        case 0: launch_pair_d<kMode, kList, 0>(t, o, o_at, p, sport, out, stride, oq, cfg); return;
+        case 1: launch_pair_d<kMode, kList, 1>(t, o, o_at, p, sport, out, stride, oq, cfg); return;
+        case 2: launch_pair_d<kMode, kList, 2>(t, o, o_at, p, sport, out, stride, oq, cfg); return;
+        case 3: launch_pair_d<kMode, kList, 3>(t, o, o_at, p, sport, out, stride, oq, cfg); return;
+        case 4: launch_pair_d<kMode, kList, 4>(t, o, o_at, p, sport, out, stride, oq, cfg); return;
+        case 5: launch_pair_d<kMode, kList, 5>(t, o, o_at, p, sport, out, stride, oq, cfg); return;
         default: break;
         }
     }
-    launch_pair_d<kMode, kList, -1>(t, o, o_at, p, sport, out, stride, cfg);
+    launch_pair_d<kMode, kList, -1>(t, o, o_at, p, sport, out, stride, oq, cfg);
 }
 
 }  // namespace
 
 hipError_t launch_classify4_pair(const Cls4Dev& t, const Cls4Dev& o, uint32_t o_at, const Pkts4& p,
-                                 const uint16_t* sport, uint32_t* out, uint64_t stride, const LaunchCfg& cfg) {
+                                 const uint16_t* sport, uint32_t* out, uint64_t stride, uint32_t* oq,
+                                 const LaunchCfg& cfg) {
     if (!cls_dispatchable(t, true, false) || o.mode != 0 || o.list_mode != 0) return hipErrorInvalidValue;
     const int src = src_variant(t);
 #define PAIR_CASE(S, M, L) \
-    case 8 * S + L: launch_pair<M, L>(t, o, o_at, p, sport, out, stride, cfg); break;
+    case 8 * S + L: launch_pair<M, L>(t, o, o_at, p, sport, out, stride, oq, cfg); break;
     switch (8 * src + int(t.list_mode)) {
         PAIR_CASE(0, 0, 0) PAIR_CASE(0, 0, 1) PAIR_CASE(0, 0, 2) PAIR_CASE(0, 0, 3) PAIR_CASE(0, 0, 4)
         PAIR_CASE(0, 0, 5) PAIR_CASE(0, 0, 6)

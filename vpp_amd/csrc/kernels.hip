@@ -550,10 +550,7 @@ __global__ __launch_bounds__(1024) void connect_kernel(ConnArgs a) {
     typedef typename ConnT<k16>::A A;
     extern __shared__ uint4 smem[];
     typedef __attribute__((address_space(3))) uint32_t* lctr_t;
-    if constexpr (kLdsRules) {
-        const uint4* g = static_cast<const uint4*>(a.rules);
-        for (uint32_t j = threadIdx.x; j < a.rules_bytes / 16u; j += blockDim.x) smem[j] = g[j];
-    }
+    if constexpr (kLdsRules) lds_copy(smem, static_cast<const uint4*>(a.rules), a.rules_bytes / 16u);
     if constexpr (kCount == 1) {
         for (uint32_t j = threadIdx.x; j < a.n_ctr; j += blockDim.x) *lctr_t(a.ctr_lds + 4u * j) = 0u;
     }
@@ -703,24 +700,13 @@ __global__ __launch_bounds__(1024) void connect_kernel(ConnArgs a) {
                 }
             }
             if constexpr (kCount == 1) {
-                // a popular rule (the global ACL's) would serialise the LDS
-                // atomic over the lanes holding it: the wave adds its first
-                // key once with the count of lanes holding it, the rest lane
-                // by lane
+                // (aggregating a wave's equal keys first measured slower:
+                // 136.5 -> 142.5 us at 12 local ACLs, profiles/r04l_conn_ab.txt)
 #pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const uint64_t pend = __ballot(key[k] != 0xFFFFFFFFu);
-                    if (!pend) continue;                        // wave-uniform
-                    const int leader = __builtin_ctzll(pend);
-                    const uint32_t lk = __shfl(key[k], leader);
-                    const uint64_t same = __ballot(key[k] == lk);
-                    if (int(lane) == leader)
-                        __hip_atomic_fetch_add(lctr_t(a.ctr_lds + 4u * lk), uint32_t(__popcll(same)), __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_WORKGROUP);
-                    else if (key[k] != 0xFFFFFFFFu && key[k] != lk)
+                for (int k = 0; k < 4; ++k)
+                    if (key[k] != 0xFFFFFFFFu)
                         __hip_atomic_fetch_add(lctr_t(a.ctr_lds + 4u * key[k]), 1u, __ATOMIC_RELAXED,
                                                __HIP_MEMORY_SCOPE_WORKGROUP);
-                }
             } else {
 #pragma unroll
                 for (int k = 0; k < 4; ++k) wave_count(a.ctr, key[k]);

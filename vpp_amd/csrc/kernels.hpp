@@ -173,11 +173,21 @@ hipError_t launch_classify16_slots(const Cls4Dev& t, const Fe16& fe, const Pkts1
 // out[i] = the SYN tuple (p.src, p.dst, p.dport) and out[stride + i] the
 // SYN-ACK tuple (p.dst, p.src, sport), result | slot << 2 each.  The OTHER
 // image (o, offsets rebased to LDS byte o_at) is staged beside the main one
-// when o_at != 0, so protocols > 2 are classified from LDS in place.
+// when o_at != 0.  Connections of protocol > 2 go to the workgroup's
+// segment of oq (pair_queue_words entries per workgroup) and are classified
+// on the OTHER image after the workgroup's main loop, one per lane.
 // Needs 16-B aligned src / dst / out / out + stride, 8-B dport / sport, 4-B
 // proto; stride a multiple of 4.
 hipError_t launch_classify4_pair(const Cls4Dev& t, const Cls4Dev& o, uint32_t o_at, const Pkts4& p,
-                                 const uint16_t* sport, uint32_t* out, uint64_t stride, const LaunchCfg& cfg);
+                                 const uint16_t* sport, uint32_t* out, uint64_t stride, uint32_t* oq,
+                                 const LaunchCfg& cfg);
+// the OTHER queue segment of one pair-launch workgroup (kPairBlock threads):
+// every connection its lanes visit, 4 per lane per step
+constexpr int kPairBlock = 1024;
+inline uint64_t pair_queue_words(uint64_t n, int grid) {
+    const uint64_t nsteps = n / 4, nthreads = uint64_t(grid) * kPairBlock;
+    return 4ull * kPairBlock * ((nsteps + nthreads - 1) / nthreads);
+}
 
 struct ConnDesc {                // one bound ACL for the connection kernel
     uint32_t rule_off;           // linear ACLs: first rule in the call's rule pool

@@ -634,11 +634,28 @@ __device__ __forceinline__ void queue_end(const Cls4Dev& t, uint32_t oq_lds) {
 }
 
 
+// Copy n16 16-byte words from global memory into LDS, every thread's loads
+// of a round in flight together (8 per thread: 128 KiB per round at 1024
+// threads) before any is written -- a copy loop of one load and one store
+// per trip waits a full memory latency per 16 KiB.
+__device__ __forceinline__ void lds_copy(uint4* dst, const uint4* src, uint32_t n16) {
+    constexpr int K = 8;
+    for (uint32_t base = 0; base < n16; base += K * blockDim.x) {
+        uint4 v[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k)          // (clamped, not guarded: the loads stay in registers)
+            v[k] = src[min(base + uint32_t(k) * blockDim.x + threadIdx.x, n16 - 1u)];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const uint32_t i = base + uint32_t(k) * blockDim.x + threadIdx.x;
+            if (i < n16) dst[i] = v[k];
+        }
+    }
+}
+
 // Stage the read-only image into LDS (at address 0) and zero the counters.
 __device__ __forceinline__ void stage_lds(const Cls4Dev& t, uint4* smem) {
-    const uint4* src4 = reinterpret_cast<const uint4*>(t.img);
-    const uint32_t n4 = t.img_bytes / 16u;
-    for (uint32_t i = threadIdx.x; i < n4; i += blockDim.x) smem[i] = src4[i];
+    lds_copy(smem, reinterpret_cast<const uint4*>(t.img), t.img_bytes / 16u);
     uint32_t* lctr = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(smem) + t.img_bytes);
     for (uint32_t i = threadIdx.x; i < (t.lds_bytes - t.img_bytes) / 4u; i += blockDim.x) lctr[i] = 0u;
     __syncthreads();
