@@ -11,6 +11,7 @@
 #   conn:<lib,...>     connection batches at 12 and 64 local ACLs per build
 #                      (default = vpp_amd/libcontivcls.so, else variants/lib_<x>.so),
 #                      with rocprofv3 kernel stats
+#   connn:<n>          connection batches of n connections, 12 local ACLs, kernel stats
 #   gp16:<lib,...>     gen-policy ingress lists, 16-byte layout, 10 % IPv6
 #   gp:<layout>        gen-policy 20-block list: 64 / 256 Mi packets, TCP/UDP only
 #   gpmix:<layout>     the 20-block list without protocol 47, without ICMP
@@ -19,6 +20,7 @@
 #   ab:<config>:<lib>  one-process A/B of the classify kernel against a variant
 #   sq:<config>        SQ counter passes of the classify kernel (tools/sq_profile.sh)
 #   sqgp:<layout>:<blocks>  the same for a gen-policy ingress list
+#   sqconn:<locals>    the same for the connection batch's kernels
 #   pmc:<config>       HBM traffic PMC passes (tools/gpu_pmc.sh)
 #   fetchgp:<layout>:<blocks>  FETCH_SIZE of the classify kernel on a gen-policy
 #                      ingress list against its algorithmic bytes
@@ -60,6 +62,10 @@ for step in "$@"; do
         python3 tools/kstats.py $O/conn_${v}_$loc/run_kernel_stats.csv | grep -E "connect|pair"
       done
     done ;;
+  connn)
+    (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/connn_$arg -o run --output-format csv -- python3 $R/tools/conn_bench.py --locals 12 --n $arg --cpu-sample 0 > $O/connn_$arg.json 2> $O/connn_$arg.err)
+    python3 tools/jl.py $O/connn_$arg.json hbm_resident hbm_resident_counted
+    python3 tools/kstats.py $O/connn_$arg/run_kernel_stats.csv | grep -E "connect|pair|stream_conn" ;;
   gp16)
     for v in $(echo $arg | tr , ' '); do
       CONTIVCLS_LIB=$(lib $v) timeout -k 10 300 python tools/genpolicy_bench.py --layout 16 --v6 0.1 --blocks 20 200 1000 --match ingress --packets 67108864 --iters 5 > $O/gp16_$v.jsonl 2> $O/gp16_$v.err
@@ -103,6 +109,9 @@ for v in vals:
     print("FETCH_SIZE %.0f KiB -> %.3f GB read (x2, gfx950), %.3fx the %.3f GB algorithmic reads" % (v, v * 2048 / 1e9, v * 2048 / alg, alg / 1e9))
 PY
     ;;
+  sqconn)
+    SQ_KERNELS=connect_kernel,classify4_pair SQ_CMD="python3 $R/tools/conn_bench.py --locals $arg --count 0 --iters 2 --cpu-sample 0" bash tools/sq_profile.sh ${TAG}_conn$arg > /dev/null 2>&1
+    cat gpurun_out/sq_${TAG}_conn$arg/summary.txt ;;
   pmc)
     bash tools/gpu_pmc.sh ${TAG}_pmc$arg $arg > /dev/null 2>&1
     grep -h "ratio\|source_hash" gpurun_out/${TAG}_pmc$arg/pmc.json ;;

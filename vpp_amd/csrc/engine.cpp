@@ -155,6 +155,7 @@ struct ConnPlan {
     std::vector<uint32_t> big;                            // descriptors of the large ACLs
     std::vector<uint8_t> pool;
     uint32_t n_ctr = 0;
+    uint32_t bm_steps = 0;                                // lower-bound steps of the largest bitmap table
 };
 
 struct cls_engine {
@@ -1445,6 +1446,8 @@ int cls_connect_batch(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t*
                 P.desc[j].bm_sd = h[1] | (h[2] << 16);
                 P.desc[j].bm_tu = h[4] | (h[5] << 16);
                 P.desc[j].bm_w = h[0];
+                for (uint32_t len : {h[1], h[2], h[4], h[5]})   // ceil(log2(len)) steps take a table to one key
+                    while ((1u << P.bm_steps) < len) ++P.bm_steps;
                 words.insert(words.end(), t.conn_bm.begin(), t.conn_bm.end());
             }
             const uint8_t* wb = reinterpret_cast<const uint8_t*>(words.data());
@@ -1559,6 +1562,7 @@ int cls_connect_batch(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t*
     a.desc = e->s_desc.as<ConnDesc>();
     a.pre = big.empty() ? nullptr : e->s_pre.as<uint32_t>();
     a.pre_stride = stride;
+    a.bm_steps = P.bm_steps;
     a.ifs = e->s_ifs.as<IfAcls>();
     a.rules = e->s_rules.p;
     std::vector<unsigned long long*> tctr;

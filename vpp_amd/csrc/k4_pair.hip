@@ -66,14 +66,19 @@ __global__ __launch_bounds__(kClsBlock) void classify4_pair(Cls4Dev t, Cls4Dev o
         const uint32_t dpa[4] = {dp2.x & 0xFFFFu, dp2.x >> 16, dp2.y & 0xFFFFu, dp2.y >> 16};
         const uint32_t spa[4] = {sp2.x & 0xFFFFu, sp2.x >> 16, sp2.y & 0xFFFFu, sp2.y >> 16};
         const uint32_t ra[4] = {pr & 0xFFu, (pr >> 8) & 0xFFu, (pr >> 16) & 0xFFu, pr >> 24};
-        uint32_t r0[4], k0[4], r1[4], k1[4];
-        classify_n<4, true, kMode, kList, kD>(im, t, sa, da, dpa, ra, r0, k0);
-        classify_n<4, true, kMode, kList, kD>(im, t, da, sa, spa, ra, r1, k1);
+        // both tuples of the four connections as one group of eight: their
+        // eight chains of dependent LDS reads run interleaved
+        const uint32_t s8[8] = {sa[0], sa[1], sa[2], sa[3], da[0], da[1], da[2], da[3]};
+        const uint32_t d8[8] = {da[0], da[1], da[2], da[3], sa[0], sa[1], sa[2], sa[3]};
+        const uint32_t p8[8] = {dpa[0], dpa[1], dpa[2], dpa[3], spa[0], spa[1], spa[2], spa[3]};
+        const uint32_t r8[8] = {ra[0], ra[1], ra[2], ra[3], ra[0], ra[1], ra[2], ra[3]};
+        uint32_t res8[8], k8[8];
+        classify_n<8, true, kMode, kList, kD>(im, t, s8, d8, p8, r8, res8, k8);
         uint32_t w0[4], w1[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            w0[q] = r0[q] | (k0[q] << 2);
-            w1[q] = r1[q] | (k1[q] << 2);
+            w0[q] = res8[q] | (k8[q] << 2);
+            w1[q] = res8[4 + q] | (k8[4 + q] << 2);
         }
         // Some protocol byte > 2 (SWAR, as classify4_cls): those connections
         // go to the workgroup's queue (one reservation per wave step); their

@@ -492,9 +492,11 @@ __device__ __forceinline__ uint32_t conn_bm(const ConnArgs& a, const ConnDesc& D
     const uint32_t np = p == 0u ? n0 : p == 1u ? n1 : 1u;
     // the three branch-free lower bounds (last key <= x; key 0 first) in
     // lock-step, their reads in flight together: a finished search re-reads
-    // its current key (h = 0), which still holds
+    // its current key (h = 0), which still holds.  The trip count is the
+    // launch's (a.bm_steps, the largest table's), the same for every lane: a
+    // loop on each lane's own lengths costs the wave exec-mask work per trip
     uint32_t ps = 0, ls = ns, pd = 0, ld = nd, pp = 0, lp = np;
-    while ((ls | ld | lp) > 1u) {
+    for (uint32_t it = 0; it < a.bm_steps; ++it) {
         const uint32_t hs = ls >> 1, hd = ld >> 1, hp = lp >> 1;
         const uint32_t ks = bm_u32<kLds>(g, os + 4u * (ps + hs)), kd = bm_u32<kLds>(g, od + 4u * (pd + hd));
         const uint32_t kp = bm_u32<kLds>(g, op + 4u * (pp + hp));

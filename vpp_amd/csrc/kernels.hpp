@@ -240,6 +240,7 @@ struct ConnArgs {
     const uint32_t* pre;         // classifier slot words of the large ACLs: block b at pre + 2 b pre_stride
                                  // (SYN tuple, then SYN-ACK at + pre_stride); null when there are none
     uint64_t pre_stride;
+    uint32_t bm_steps;           // bitmap forms: lower-bound steps of the largest interval table
 };
 // k16: 16-byte addresses; lds_rules: stage the pool; count: 0 none, 1 LDS
 // counters, 2 global (wave-aggregated) counters; grid: persistent workgroups
