@@ -275,3 +275,65 @@ def test_global_tables_match_oracle(fam, count, monkeypatch):
         _run(eng, 11, "linear", fam, count=count, n=8000, n_local=12)
     finally:
         eng.close()
+
+
+@pytest.mark.parametrize("count", [False, True])
+def test_device_plan_follows_binding_changes(count):
+    """A device batch keeps its plan (descriptors, interface table, rule pool)
+    until a table or binding changes (engine.cpp ConnPlan / conn_gen): after
+    a replaced ACL, a deleted one, a re-put of equal rules on other
+    interfaces (the rebind path) and a new interface, the same device batch
+    must follow the new bindings -- verdicts and counters against the
+    oracle, before and after."""
+    import torch
+    from vpp_amd.engine import Engine
+    eng = Engine()
+    try:
+        ifs, bind, by_name, pool, spec = build(eng, 3, n_local=16, n_if=40)
+        n = 20000
+        tr = traffic(3, n, pool, spec, 4)
+        rng = np.random.default_rng(3)
+        ifs.append("if_new")                               # bound below; its id exists from now on
+        bind["if_new"] = [None, None]
+        ids = np.array([eng.if_id(x) for x in ifs], np.uint32)
+        si = rng.integers(0, len(ifs), n)
+        di = np.where(rng.random(n) < 0.1, si, rng.integers(0, len(ifs), n))
+        host = [ids[si], ids[di], tr["src"], tr["dst"], tr["proto"], tr["sport"], tr["dport"]]
+        dv = [torch.from_numpy(np.ascontiguousarray(x).view({4: np.int32, 2: np.int16, 1: np.uint8}[x.dtype.itemsize]))
+              .to("cuda") for x in host]
+        torch.cuda.synchronize()
+
+        def check():
+            got = eng.connect_batch(*dv, count=count).cpu().numpy()
+            want, wcounts = oracle_connections(bind, by_name, ifs, si, di, tr, 4)
+            bad = np.nonzero(got != want)[0]
+            assert bad.size == 0, (bad[:10], got[bad[:10]], want[bad[:10]])
+            if count:
+                for name in by_name:
+                    c = eng.conn_counters(name, reset=True)
+                    assert np.array_equal(c, wcounts[name]), name
+
+        check()
+        check()                                            # the kept plan, nothing uploaded
+        # replace local0 with other rules on other interfaces
+        for i in ifs:
+            bind[i] = [None if x == "local0" else x for x in bind[i]]
+        rules0, _ = random_acl(7777, 150, weird=0.0)
+        assert eng.acl_put("local0", rules0, ["if5", "if_new"], ["if6"]) == 0
+        by_name["local0"] = rules0
+        bind["if5"][0] = bind["if_new"][0] = "local0"
+        bind["if6"][1] = "local0"
+        # delete local1
+        assert eng.acl_del("local1") == 0
+        for i in ifs:
+            bind[i] = [None if x == "local1" else x for x in bind[i]]
+        del by_name["local1"]
+        # re-put local2's rules on other interfaces (same table, new bindings)
+        for i in ifs:
+            bind[i] = [None if x == "local2" else x for x in bind[i]]
+        assert eng.acl_put("local2", by_name["local2"], ["if7"], ["if8", "if_new"]) == 0
+        bind["if7"][0] = "local2"
+        bind["if8"][1] = bind["if_new"][1] = "local2"
+        check()
+    finally:
+        eng.close()
