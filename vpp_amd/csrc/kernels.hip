@@ -576,8 +576,10 @@ __global__ __launch_bounds__(1024) void connect_kernel(ConnArgs a) {
         const uint64_t ic = live ? i : 0;                       // loads stay in bounds
         const uint32_t si = a.src_if[ic], dj = a.dst_if[ic];
         const bool ok = live && si < a.n_ifs && dj < a.n_ifs;   // unknown interface id: Failure
-        const IfAcls S = ok ? conn_if(a, si) : IfAcls{-1, -1, -1, -1};
-        const IfAcls Dif = ok ? conn_if(a, dj) : IfAcls{-1, -1, -1, -1};
+        // both lookups unconditional (an in-range index), the unknown case selected after
+        const IfAcls S0 = conn_if(a, ok ? si : 0u), D0 = conn_if(a, ok ? dj : 0u);
+        const IfAcls S = ok ? S0 : IfAcls{-1, -1, -1, -1};
+        const IfAcls Dif = ok ? D0 : IfAcls{-1, -1, -1, -1};
         const A sa = src[ic], da = dst[ic];
         const uint32_t sp = a.sport[ic], dp = a.dport[ic], pr = a.proto[ic];
         const uint32_t p = pr <= 2u ? pr : 3u;
@@ -655,37 +657,32 @@ __global__ __launch_bounds__(1024) void connect_kernel(ConnArgs a) {
         uint32_t res[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) res[k] = di[k] < 0 ? 1u : job[k] ? (rj[k] & 3u) : (w[k] & 3u);   // nil ACL: PERMIT (:476-478)
-        uint32_t v = 3u;
-        bool made[4] = {false, false, false, false};
-        if (ok) {
-            const bool same = si == dj;
-            bool srefl = false, drefl = false, done = false;
-            made[0] = true;
-            uint32_t r = res[0];                                                    // SYN: src inbound
-            if (r == 3u) { v = 3u; done = true; }
-            else if (r == 0u) { v = 0u; done = true; }
-            else if (r == 2u) { srefl = true; drefl = same; }
-            if (!done && !drefl) {                                                  // SYN: dst outbound
-                made[1] = true;
-                r = res[1];
-                if (r == 3u) { v = 3u; done = true; }
-                else if (r == 0u) { v = 0u; done = true; }
-                else if (r == 2u) { drefl = true; srefl = srefl || same; }
-            }
-            if (!done && !drefl) {                                                  // SYN-ACK: dst inbound
-                made[2] = true;
-                r = res[2];
-                if (r == 3u) { v = 3u; done = true; }
-                else if (r == 0u) { v = 1u; done = true; }
-            }
-            if (!done && !srefl) {                                                  // SYN-ACK: src outbound
-                made[3] = true;
-                r = res[3];
-                if (r == 3u) { v = 3u; done = true; }
-                else if (r == 0u) { v = 1u; done = true; }
-            }
-            if (!done) v = 2u;
-        }
+        // straight-line selects, no per-lane branches: the wave's lanes take
+        // different paths through the REFLECT short-cuts
+        const bool same = si == dj;
+        uint32_t v = 3u;                                                        // Failure (unknown interface)
+        bool made[4];
+        uint32_t r = res[0];                                                    // SYN: src inbound
+        made[0] = ok;
+        bool done = ok && (r == 3u || r == 0u);
+        v = ok && r == 3u ? 3u : ok && r == 0u ? 0u : v;
+        bool srefl = ok && r == 2u, drefl = srefl && same;
+        made[1] = ok && !done && !drefl;                                        // SYN: dst outbound
+        r = res[1];
+        v = made[1] && r == 3u ? 3u : made[1] && r == 0u ? 0u : v;
+        done = done || (made[1] && (r == 3u || r == 0u));
+        const bool dr1 = made[1] && r == 2u;
+        drefl = drefl || dr1;
+        srefl = srefl || (dr1 && same);
+        made[2] = ok && !done && !drefl;                                        // SYN-ACK: dst inbound
+        r = res[2];
+        v = made[2] && r == 3u ? 3u : made[2] && r == 0u ? 1u : v;
+        done = done || (made[2] && (r == 3u || r == 0u));
+        made[3] = ok && !done && !srefl;                                        // SYN-ACK: src outbound
+        r = res[3];
+        v = made[3] && r == 3u ? 3u : made[3] && r == 0u ? 1u : v;
+        done = done || (made[3] && (r == 3u || r == 0u));
+        v = ok && !done ? 2u : v;
         if (live) a.out[i] = uint8_t(v);
         if constexpr (kCount != 0) {
             uint32_t key[4];
