@@ -49,3 +49,20 @@ def test_flag_values_match_header():
     assert flags == {"DEVICE": _abi.F_DEVICE, "NO_VERDICT": _abi.F_NO_VERDICT, "ACCUMULATE": _abi.F_ACCUMULATE,
                      "FORCE_LINEAR": _abi.F_FORCE_LINEAR, "TIMING": _abi.F_TIMING, "CONN_CLS": _abi.F_CONN_CLS,
                      "COUNT": _abi.F_COUNT}
+
+
+def test_timing_entry_points_refuse_null_engine():
+    """cls_kernel_times / cls_kernel_starts / cls_kernel_times_reset /
+    cls_last_kernel_ms: a null engine or count pointer is CLS_E_INVAL, no
+    device call (the timing pair is stamped by the classify launch itself)."""
+    import ctypes as C
+    from vpp_amd import _abi
+    L = _abi.lib()
+    n = C.c_uint32(0)
+    buf = (C.c_float * 4)()
+    for fn in (L.cls_kernel_times, L.cls_kernel_starts):
+        assert fn(None, buf, 4, C.byref(n)) == _abi.E_INVAL
+        assert fn(None, None, 0, None) == _abi.E_INVAL
+    assert L.cls_kernel_times_reset(None) == _abi.E_INVAL
+    ms = C.c_float(0)
+    assert L.cls_last_kernel_ms(None, C.byref(ms)) == _abi.E_INVAL
