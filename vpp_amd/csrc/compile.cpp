@@ -826,9 +826,28 @@ static bool build_cls4_one(const std::vector<SemRule>& sem, uint32_t n_rules, Cl
     std::vector<uint32_t> class_order;
     {
         std::vector<double> span(n_classes, 0.0);
-        for (uint32_t k = 0; k < n_real_bounds; ++k) {
-            const double hi = k + 1 < n_real_bounds ? double(bounds[k + 1]) : 4294967296.0;
-            span[iclass[k]] += hi - double(bounds[k]);
+        if (opt && !opt->src_weight.empty()) {
+            // the sources' own weights (Cls4Opts::src_weight), summed per interval
+            const auto& w = opt->src_weight;
+            std::vector<double> pre(w.size() + 1, 0.0);
+            for (size_t j = 0; j < w.size(); ++j) pre[j + 1] = pre[j] + w[j].second;
+            auto below = [&](uint64_t x) {            // weight of the values < x
+                size_t lo = 0, hi = w.size();
+                while (lo < hi) {
+                    const size_t mid = (lo + hi) / 2;
+                    if (uint64_t(w[mid].first) < x) lo = mid + 1; else hi = mid;
+                }
+                return pre[lo];
+            };
+            for (uint32_t k = 0; k < n_real_bounds; ++k) {
+                const uint64_t hi = k + 1 < n_real_bounds ? uint64_t(bounds[k + 1]) : (1ull << 32);
+                span[iclass[k]] += below(hi) - below(bounds[k]);
+            }
+        } else {
+            for (uint32_t k = 0; k < n_real_bounds; ++k) {
+                const double hi = k + 1 < n_real_bounds ? double(bounds[k + 1]) : 4294967296.0;
+                span[iclass[k]] += hi - double(bounds[k]);
+            }
         }
         hot_class = uint32_t(std::max_element(span.begin(), span.end()) - span.begin());
         if (opt && opt->hot_addr >= 0) {
@@ -1771,6 +1790,23 @@ static bool build_cls16_one(const std::vector<SemRule>& sem, uint32_t n_rules, C
         opt.tail.resize(align4(uint32_t(opt.tail.size())));
     }
     opt.hot_addr = side[0].root[0];                       // IPv4 sources matching no prefix
+    {
+        // each source rep's address space: IPv4-mapped parts in IPv4
+        // addresses, the rest scaled so all of it weighs as much as the IPv4
+        // block (the slot order then follows the addresses, not the reps)
+        std::map<uint32_t, double> w;
+        for (size_t j = 0; j < s_start.size(); ++j) {
+            const u128 lo = s_start[j];
+            const bool last = j + 1 == s_start.size();
+            const u128 hi = last ? ~u128(0) : s_start[j + 1] - 1;     // inclusive
+            const u128 a = lo > kV4Lo ? lo : kV4Lo, b = hi < kV4Hi ? hi : kV4Hi;
+            double v4 = 0.0;
+            if (a <= b) v4 = double(uint64_t(b - a)) + 1.0;
+            const double all = double(uint64_t((hi - lo) >> 64)) * 18446744073709551616.0 + double(uint64_t(hi - lo)) + 1.0;
+            w[s_rep[j]] += v4 + (all - v4) / 79228162514264337593543950336.0;   // / 2^96
+        }
+        opt.src_weight.assign(w.begin(), w.end());
+    }
     if (!build_cls4_one(img.sem, n_rules, img.core, why, &opt)) return false;
     const uint32_t tail = img.core.off_tail;
     for (int sd = hosts ? 1 : 0; sd < 2; ++sd) {

@@ -200,6 +200,11 @@ struct Cls4Image {
 struct Cls4Opts {
     std::vector<uint32_t> tail;    // extra read-only words appended to the image
     int64_t hot_addr = -1;         // the hot class is this address's (default: the widest)
+    // The address space each source value stands for, as sorted (value,
+    // weight) pairs (default: 1 per value).  A core compiled in rep space
+    // (the 16-byte layout) passes its reps' real widths, so the slot order
+    // below ranks classes by the addresses they cover, not by their reps.
+    std::vector<std::pair<uint32_t, double>> src_weight;
     bool ext_src = false;          // no source lookup sections (mode 3: the caller finds rows)
     // The OTHER image: one cell per class for protocol values outside
     // ProtocolType (evalACL's switch has no case for them,
