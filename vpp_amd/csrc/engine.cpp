@@ -1496,7 +1496,7 @@ int cls_connect_batch(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t*
                         od.off_lists += o_at; od.off_tmpl += o_at;
                     }
                     cfg.grid = cls_grid(e, true, true, o_at ? o_at + t.oimg.img_bytes : t.img.img_bytes, n);
-                    HIPC(e, e->s_pq.ensure(size_t(cfg.grid) * pair_queue_words(n, cfg.grid) * 4));
+                    HIPC(e, e->s_pq.ensure(size_t(cfg.grid) * pair_queue_words(n, cfg.grid) * 16));
                     HIPC(e, launch_classify4_pair(cd, od, o_at, syn, sp, pre, stride, e->s_pq.as<uint32_t>(), cfg));
                 } else {
                     cfg.other = cls4_dev(t.oimg, t.d_oimg, DevBuf(), 0, t.n_rules);

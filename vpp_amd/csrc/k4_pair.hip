@@ -11,7 +11,8 @@
 // once (13 B), writing 8 B.  The OTHER image (protocols > 2: networks alone
 // decide, evalACL's switch has no case) is staged beside the main image
 // when both fit LDS (no slot counters in this mode).  Those connections are
-// queued (the workgroup's segment of oq, its fill counted in LDS) and
+// queued with their fields (16-B entries in the workgroup's segment of oq,
+// its fill counted in LDS) and
 // classified on the OTHER image after the workgroup's main loop, one per
 // lane: the OTHER chain (interval search, candidate scan) then runs once per
 // 1024 of them instead of once per wave step that holds any.
@@ -58,51 +59,77 @@ __global__ __launch_bounds__(kClsBlock) void classify4_pair(Cls4Dev t, Cls4Dev o
     const uint32_t* PR = reinterpret_cast<const uint32_t*>(p.proto);
     uint4* OS = reinterpret_cast<uint4*>(out);
     uint4* OA = reinterpret_cast<uint4*>(out + stride);
-    for (uint32_t g = tid; g < nsteps; g += nthreads) {
-        const uint4 s4 = ldnt(at(S, g)), d4 = ldnt(at(D, g));
-        const uint2 dp2 = ldnt(at(DP, g)), sp2 = ldnt(at(SP, g));
-        const uint32_t pr = ldnt(at(PR, g));
-        const uint32_t sa[4] = {s4.x, s4.y, s4.z, s4.w}, da[4] = {d4.x, d4.y, d4.z, d4.w};
-        const uint32_t dpa[4] = {dp2.x & 0xFFFFu, dp2.x >> 16, dp2.y & 0xFFFFu, dp2.y >> 16};
-        const uint32_t spa[4] = {sp2.x & 0xFFFFu, sp2.x >> 16, sp2.y & 0xFFFFu, sp2.y >> 16};
-        const uint32_t ra[4] = {pr & 0xFFu, (pr >> 8) & 0xFFu, (pr >> 16) & 0xFFu, pr >> 24};
-        // both tuples of the four connections as one group of eight: their
-        // eight chains of dependent LDS reads run interleaved
-        const uint32_t s8[8] = {sa[0], sa[1], sa[2], sa[3], da[0], da[1], da[2], da[3]};
-        const uint32_t d8[8] = {da[0], da[1], da[2], da[3], sa[0], sa[1], sa[2], sa[3]};
-        const uint32_t p8[8] = {dpa[0], dpa[1], dpa[2], dpa[3], spa[0], spa[1], spa[2], spa[3]};
-        const uint32_t r8[8] = {ra[0], ra[1], ra[2], ra[3], ra[0], ra[1], ra[2], ra[3]};
-        uint32_t res8[8], k8[8];
-        classify_n<8, true, kMode, kList, kD>(im, t, s8, d8, p8, r8, res8, k8);
-        uint32_t w0[4], w1[4];
+    uint4* OQ = reinterpret_cast<uint4*>(oq);       // queued: {index, src, dst, dport | sport << 16}
+    // G groups of four connections per lane per iteration: two (16 chains,
+    // 108 VGPRs) measured slower than one, 41.9 against 40.8 us
+    // (profiles/r04h2_pair_ab.txt)
+    constexpr int G = 1;
+    for (uint32_t g0 = tid; g0 < nsteps; g0 += G * nthreads) {
+        uint32_t s8[8 * G], d8[8 * G], p8[8 * G], r8[8 * G], prs[G];
+        bool live[G];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            w0[q] = res8[q] | (k8[q] << 2);
-            w1[q] = res8[4 + q] | (k8[4 + q] << 2);
-        }
-        // Some protocol byte > 2 (SWAR, as classify4_cls): those connections
-        // go to the workgroup's queue (one reservation per wave step); their
-        // words above are overwritten after the main loop
-        if (__any(((pr | ((pr & 0x7F7F7F7Fu) + 0x7D7D7D7Du)) & 0x80808080u) != 0u)) {
-            uint64_t m[4];
-            uint32_t c[5];
-            c[0] = 0;
+        for (int h = 0; h < G; ++h) {
+            const uint32_t g = g0 + uint32_t(h) * nthreads;
+            live[h] = h == 0 || g < nsteps;
+            const uint32_t gc = live[h] ? g : g0;
+            const uint4 s4 = ldnt(at(S, gc)), d4 = ldnt(at(D, gc));
+            const uint2 dp2 = ldnt(at(DP, gc)), sp2 = ldnt(at(SP, gc));
+            const uint32_t pr = ldnt(at(PR, gc));
+            prs[h] = pr;
+            const uint32_t sa[4] = {s4.x, s4.y, s4.z, s4.w}, da[4] = {d4.x, d4.y, d4.z, d4.w};
+            const uint32_t dpa[4] = {dp2.x & 0xFFFFu, dp2.x >> 16, dp2.y & 0xFFFFu, dp2.y >> 16};
+            const uint32_t spa[4] = {sp2.x & 0xFFFFu, sp2.x >> 16, sp2.y & 0xFFFFu, sp2.y >> 16};
+            // both tuples of the four connections as one group of eight: their
+            // eight chains of dependent LDS reads run interleaved
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                m[q] = __ballot(ra[q] > 2u);
-                c[q + 1] = c[q] + uint32_t(__popcll(m[q]));
+                const uint32_t r = (pr >> (8 * q)) & 0xFFu;
+                s8[8 * h + q] = sa[q]; s8[8 * h + 4 + q] = da[q];
+                d8[8 * h + q] = da[q]; d8[8 * h + 4 + q] = sa[q];
+                p8[8 * h + q] = dpa[q]; p8[8 * h + 4 + q] = spa[q];
+                r8[8 * h + q] = r; r8[8 * h + 4 + q] = r;
             }
-            uint32_t base = 0u;
-            if (lane == 0u)
-                base = __hip_atomic_fetch_add(lctr_t(q_lds), c[4], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            base = __shfl(base, 0);
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-                if (ra[q] > 2u) oq[uint64_t(blockIdx.x) * oq_seg + base + c[q] + uint32_t(__popcll(m[q] & lt))] =
-                    4u * g + uint32_t(q);
         }
-        OS[g] = make_uint4(w0[0], w0[1], w0[2], w0[3]);
-        OA[g] = make_uint4(w1[0], w1[1], w1[2], w1[3]);
+        uint32_t res8[8 * G], k8[8 * G];
+        classify_n<8 * G, true, kMode, kList, kD>(im, t, s8, d8, p8, r8, res8, k8);
+#pragma unroll
+        for (int h = 0; h < G; ++h) {
+            const uint32_t g = g0 + uint32_t(h) * nthreads, pr = prs[h];
+            uint32_t w0[4], w1[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                w0[q] = res8[8 * h + q] | (k8[8 * h + q] << 2);
+                w1[q] = res8[8 * h + 4 + q] | (k8[8 * h + 4 + q] << 2);
+            }
+            // Some protocol byte > 2 (SWAR, as classify4_cls): those connections
+            // go to the workgroup's queue (one reservation per wave step); their
+            // words above are overwritten after the main loop
+            const bool oth = live[h] && ((pr | ((pr & 0x7F7F7F7Fu) + 0x7D7D7D7Du)) & 0x80808080u) != 0u;
+            if (__any(oth)) {
+                uint64_t m[4];
+                uint32_t c[5];
+                c[0] = 0;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    m[q] = __ballot(oth && ((pr >> (8 * q)) & 0xFFu) > 2u);
+                    c[q + 1] = c[q] + uint32_t(__popcll(m[q]));
+                }
+                uint32_t base = 0u;
+                if (lane == 0u)
+                    base = __hip_atomic_fetch_add(lctr_t(q_lds), c[4], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                base = __shfl(base, 0);
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    if ((m[q] >> lane) & 1u)
+                        OQ[uint64_t(blockIdx.x) * oq_seg + base + c[q] + uint32_t(__popcll(m[q] & lt))] =
+                            make_uint4(4u * g + uint32_t(q), s8[8 * h + q], d8[8 * h + q],
+                                       p8[8 * h + q] | (p8[8 * h + 4 + q] << 16));
+            }
+            if (live[h]) {
+                OS[g] = make_uint4(w0[0], w0[1], w0[2], w0[3]);
+                OA[g] = make_uint4(w1[0], w1[1], w1[2], w1[3]);
+            }
+        }
     }
     for (uint32_t i = nsteps * 4u + tid; i < uint32_t(p.n); i += nthreads) {
         const uint32_t s = p.src[i], d = p.dst[i], dp = p.dport[i], sp = sport[i], pr = p.proto[i];
@@ -120,16 +147,17 @@ __global__ __launch_bounds__(kClsBlock) void classify4_pair(Cls4Dev t, Cls4Dev o
         out[i] = w0;
         out[stride + i] = w1;
     }
-    // the queued connections of protocol > 2, one per lane (the barrier
+    // the queued connections of protocol > 2, one per lane, their fields
+    // from the queue entry (no gather from the connection arrays; the barrier
     // orders their words after the main loop's stores of the same words)
     __syncthreads();
     const uint32_t nq = *lctr_t(q_lds);
     for (uint32_t j = threadIdx.x; j < nq; j += blockDim.x) {
-        const uint32_t i = oq[uint64_t(blockIdx.x) * oq_seg + j];
+        const uint4 e = OQ[uint64_t(blockIdx.x) * oq_seg + j];
         uint32_t w0, w1;
-        other2(p.src[i], p.dst[i], p.dport[i], sport[i], w0, w1);
-        out[i] = w0;
-        out[stride + i] = w1;
+        other2(e.y, e.z, e.w & 0xFFFFu, e.w >> 16, w0, w1);
+        out[e.x] = w0;
+        out[stride + e.x] = w1;
     }
 }
 

@@ -181,8 +181,8 @@ hipError_t launch_classify16_slots(const Cls4Dev& t, const Fe16& fe, const Pkts1
 hipError_t launch_classify4_pair(const Cls4Dev& t, const Cls4Dev& o, uint32_t o_at, const Pkts4& p,
                                  const uint16_t* sport, uint32_t* out, uint64_t stride, uint32_t* oq,
                                  const LaunchCfg& cfg);
-// the OTHER queue segment of one pair-launch workgroup (kPairBlock threads):
-// every connection its lanes visit, 4 per lane per step
+// the OTHER queue segment of one pair-launch workgroup (kPairBlock threads),
+// in 16-B entries: every connection its lanes visit, 4 per lane per step
 constexpr int kPairBlock = 1024;
 inline uint64_t pair_queue_words(uint64_t n, int grid) {
     const uint64_t nsteps = n / 4, nthreads = uint64_t(grid) * kPairBlock;
