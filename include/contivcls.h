@@ -36,7 +36,10 @@ extern "C" {
  *    nested OTHER image); blob version 3; cls_table_info's n_lctr, ctr16,
  *    list_mode and swap; CLS_F_COUNT; CLS_AF_V16 connections;
  *    cls_acl_stats.  A v1 consumer that ignores `swap` would misread blobs. */
-#define CLS_ABI_VERSION 3
+/* 4: cls_config's device list (multi-device engines); engine-owned batches
+ *    (cls_batch_*); cls_classify_batch / cls_batch_connect; the in-library
+ *    RCCL counter all-reduce (cls_comm_*); cls_shard_range. */
+#define CLS_ABI_VERSION 4
 
 /* ---- status codes ------------------------------------------------------ */
 enum {
@@ -44,7 +47,7 @@ enum {
     CLS_E_INVAL = -1,    /* bad argument / malformed rule (would panic in Go) */
     CLS_E_NOMEM = -2,
     CLS_E_HIP = -3,      /* HIP runtime error */
-    CLS_E_RCCL = -4,     /* reserved: collective error */
+    CLS_E_RCCL = -4,     /* RCCL (the counter all-reduce) unavailable or failed */
     CLS_E_NOTFOUND = -5, /* unknown table / ACL name */
     CLS_E_NODEV = -6     /* no usable gfx950 device */
 };
@@ -138,15 +141,36 @@ enum {
 
 typedef struct cls_engine cls_engine;
 
+/* An engine over one device (n_devices = 0: `device`) or over several
+ * (n_devices > 0: devices[0 .. n_devices), `device` ignored).
+ * A multi-device engine keeps one ACL configuration: every table is compiled
+ * once and uploaded to every device (replicated), and batches (cls_batch_*)
+ * shard contiguously over the devices.  Calls that take raw packet pointers
+ * (cls_classify, cls_connect_batch, cls_gen_traffic_*) run on the first
+ * device.  Over distinct devices the engine creates an RCCL communicator
+ * (single-process ncclCommInitAll) at creation, so batch hit counters merge
+ * with an all-reduce over xGMI; a list that repeats a device (diagnostics:
+ * shards on one GPU) has no communicator and its counters are summed on the
+ * host when read. */
 typedef struct cls_config {
     int device;                /* HIP device ordinal; -1 = current device */
-    uint32_t reserved[7];
+    uint32_t n_devices;        /* 0: one device (`device`); else the length of `devices` */
+    const int* devices;        /* HIP device ordinals (n_devices of them) */
+    uint32_t reserved[4];
 } cls_config;
 
 /* ---- engine lifetime ---------------------------------------------------- */
-/* Replaces NewMockACLEngine (aclengine_mock.go:124). */
+/* Replaces NewMockACLEngine (aclengine_mock.go:124).  Destroy batches
+ * (cls_batch_destroy) before their engine. */
 int cls_engine_create(const cls_config* cfg, cls_engine** out);
 void cls_engine_destroy(cls_engine* e);
+/* Devices of the engine (1 for a single-device engine). */
+int cls_engine_devices(const cls_engine* e, uint32_t* n_devices);
+/* The engine of device `index` of a multi-device engine (0: `e` itself):
+ * a borrowed handle for the single-device calls on that device (timing,
+ * stream floors, raw device pointers of that device); configuration calls on
+ * it are refused (configure through `e`). */
+int cls_device_engine(cls_engine* e, uint32_t index, cls_engine** dev);
 const char* cls_last_error(const cls_engine* e);
 int cls_abi_version(void);
 
@@ -332,6 +356,88 @@ typedef struct cls_traffic_spec16 {
 int cls_gen_traffic_v16(cls_engine* e, const cls_traffic_spec16* spec, uint64_t first,
                         uint64_t n, uint8_t* src16, uint8_t* dst16, uint16_t* sport,
                         uint16_t* dport, uint8_t* proto, void* stream);
+
+/* ---- engine-owned batches (SURVEY 8(b) ownership, 8(e) sharding) --------
+ * A batch is device memory the engine owns, so a caller that must not let
+ * the library keep its pointers (cgo) can still run the HBM-resident path:
+ * upload once (or generate on the device), classify many times, download
+ * what it needs.  Packets [0, n) shard contiguously over the engine's
+ * devices (cls_shard_range): shard g = [g n / G, (g + 1) n / G) lives in
+ * device g's HBM.  Fields are structure-of-arrays, each array 256-B aligned
+ * per shard (the classify kernels' 16-B loads): addresses u32 (CLS_AF_V4)
+ * or 16 bytes (CLS_AF_V16), ports u16, protocol and verdict u8, interface
+ * ids u32 (CLS_BATCH_CONN).  With CLS_BATCH_MIRROR the batch also owns a
+ * pinned host copy of every field (hipHostMalloc; cls_batch_mirror) that
+ * the caller fills or reads in place: uploads and downloads with a NULL
+ * host pointer move it at DMA speed.  Without it, upload / download go
+ * through the engine's pinned staging buffers.
+ * Work on a batch runs on its devices' engine streams; a call returns once
+ * the work is enqueued unless it returns host data (counters_out,
+ * downloads, cls_batch_counters, cls_batch_wait). */
+typedef struct cls_batch cls_batch;
+enum {
+    CLS_BF_SRC = 0, CLS_BF_DST = 1, CLS_BF_SPORT = 2, CLS_BF_DPORT = 3, CLS_BF_PROTO = 4,
+    CLS_BF_VERDICT = 5,        /* cls_classify_batch: ACLAction; cls_batch_connect: ConnectionAction */
+    CLS_BF_SRC_IF = 6, CLS_BF_DST_IF = 7,   /* CLS_BATCH_CONN only */
+    CLS_BF_COUNT = 8
+};
+enum {
+    CLS_BATCH_CONN = 1u << 0,    /* also interface ids (connection batches) */
+    CLS_BATCH_MIRROR = 1u << 1   /* a pinned host mirror of every field */
+};
+/* Shard g of n packets over G devices: [g n / G, (g + 1) n / G). */
+int cls_shard_range(uint64_t n, uint32_t n_shards, uint32_t shard, uint64_t* first, uint64_t* count);
+int cls_batch_create(cls_engine* e, uint32_t af, uint64_t n, uint32_t flags, cls_batch** out);
+void cls_batch_destroy(cls_batch* b);
+int cls_batch_shards(const cls_batch* b, uint32_t* n_shards);
+int cls_batch_shard(const cls_batch* b, uint32_t shard, int* device, uint64_t* first, uint64_t* n);
+/* Device address of a field's array in shard `shard` (for a caller's own
+ * kernels, e.g. a capture path writing packets in place). */
+int cls_batch_field(cls_batch* b, uint32_t shard, uint32_t field, void** dev_ptr);
+/* Host address of a field's pinned mirror (whole batch, packet order). */
+int cls_batch_mirror(cls_batch* b, uint32_t field, void** host_ptr);
+/* Packets [first, first + n) of one field from `src` (NULL: the mirror). */
+int cls_batch_upload(cls_batch* b, uint32_t field, uint64_t first, uint64_t n, const void* src);
+/* ... to `dst` (NULL: the mirror).  Waits for the batch's work. */
+int cls_batch_download(cls_batch* b, uint32_t field, uint64_t first, uint64_t n, void* dst);
+/* The synthetic stream into the batch on the devices: packet i of the batch
+ * is stream packet stream_first + i (the same stream as cls_gen_traffic_*). */
+int cls_batch_gen_traffic_v4(cls_batch* b, const cls_traffic_spec* spec, uint64_t stream_first);
+int cls_batch_gen_traffic_v16(cls_batch* b, const cls_traffic_spec16* spec, uint64_t stream_first);
+/* evalACL over every packet of the batch (verdicts into CLS_BF_VERDICT) with
+ * the table's hit counters (as cls_classify) summed over the shards: by the
+ * engine's RCCL communicator when it has one (an all-reduce over the
+ * devices -- and over the processes of cls_comm_init -- on a side stream, so
+ * it overlaps the next call's classify; two counter buffers alternate), else
+ * on the host when read.  counters_out (host, R + 1): wait and write them
+ * (CLS_F_ACCUMULATE: add); NULL: only enqueue (cls_batch_counters reads the
+ * last call's).  Flags: CLS_F_NO_VERDICT, CLS_F_FORCE_LINEAR, CLS_F_TIMING
+ * (each device's classify kernel is timed on that device's engine:
+ * cls_kernel_times of cls_device_engine), CLS_F_ACCUMULATE. */
+int cls_classify_batch(cls_engine* e, uint32_t table_id, cls_batch* b, uint64_t* counters_out, uint32_t flags);
+/* Counters of the batch's last cls_classify_batch (n_out >= R + 1 of that
+ * table); waits for them. */
+int cls_batch_counters(cls_batch* b, uint64_t* out, uint32_t n_out);
+/* testConnection over a CLS_BATCH_CONN batch (as cls_connect_batch with
+ * device memory; ConnectionAction into CLS_BF_VERDICT), every device its
+ * shard; CLS_F_COUNT counts into each device's copy of the tables'
+ * connection counters (cls_conn_counters sums them).  Returns when done. */
+int cls_batch_connect(cls_engine* e, cls_batch* b, uint32_t flags);
+/* Wait for every device's work on the batch. */
+int cls_batch_wait(cls_batch* b);
+
+/* ---- the hit-counter all-reduce over processes (RCCL) --------------------
+ * One process per GPU (or per group of GPUs): process 0 makes an id
+ * (cls_comm_unique_id), every process receives it out of band and calls
+ * cls_comm_init with the same n_procs; device g of process p is rank
+ * p * G + g of n_procs * G (every process's engine has G devices).  From
+ * then on cls_classify_batch all-reduces its counters over all ranks.
+ * n_procs = 1 with id NULL: a communicator over this engine's devices alone
+ * (ncclCommInitAll; also at one device).  Replaces an earlier communicator. */
+int cls_comm_unique_id(void* id128);
+int cls_comm_init(cls_engine* e, uint32_t n_procs, uint32_t proc, const void* id128);
+/* Ranks of the engine's communicator (0: none) and its first device's rank. */
+int cls_comm_info(cls_engine* e, uint32_t* n_ranks, uint32_t* rank0);
 
 /* ---- offline compilation (no device needed) -----------------------------
  * Compiles an ACL exactly as cls_table_put does and writes the IPv4 device

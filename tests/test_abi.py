@@ -24,7 +24,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert _abi.lib().cls_abi_version() == 3
+    assert _abi.lib().cls_abi_version() == _abi.ABI_VERSION == 4
 
 
 def test_engine_create_without_gpu_fails_loudly():

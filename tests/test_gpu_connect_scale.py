@@ -337,3 +337,74 @@ def test_device_plan_follows_binding_changes(count):
         check()
     finally:
         eng.close()
+
+
+@pytest.mark.parametrize("env", [{}, {"CONTIVCLS_PAIR_OTHER_GLOBAL": "1"}, {"CONTIVCLS_PAIR_QCAP": "3"},
+                                 {"CONTIVCLS_PAIR_OTHER_GLOBAL": "1", "CONTIVCLS_PAIR_QCAP": "0"}])
+def test_pair_launch_tail_and_other_protocols(env, monkeypatch):
+    """classify4_pair (k4_pair.hip) on a batch of 4k + 3 connections with
+    protocol-47 connections everywhere, the last three included (the scalar
+    tail's direct OTHER path): the OTHER image beside the main one in LDS or
+    read from global memory (o_at = 0), the OTHER queue roomy or nearly
+    full / empty so that connections overflow to in-place classification.
+    Verdicts and counters against orc_test_connection."""
+    from vpp_amd.engine import Engine
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    eng = Engine()
+    try:
+        ifs, bind, by_name, pool, spec = build(eng, 21, n_local=6, n_if=16)
+        n = 4 * 4000 + 3
+        tr = traffic(21, n, pool, spec, 4)
+        rng = np.random.default_rng(21)
+        other = rng.random(n) < 0.05
+        other[-3:] = True
+        tr["proto"] = np.where(other, 47, tr["proto"]).astype(np.uint8)
+        ids = np.array([eng.if_id(x) for x in ifs], np.uint32)
+        si = rng.integers(0, 3, n)                      # the global ACL's interfaces: the pair launch
+        di = rng.integers(0, len(ifs), n)
+        args = [ids[si], ids[di], tr["src"], tr["dst"], tr["proto"], tr["sport"], tr["dport"]]
+        got = eng.connect_batch(*args, mode="classifier", count=True)
+        want, wcounts = oracle_connections(bind, by_name, ifs, si, di, tr, 4)
+        bad = np.nonzero(got != want)[0]
+        assert bad.size == 0, (bad[:10], got[bad[:10]], want[bad[:10]])
+        for name in by_name:
+            assert np.array_equal(eng.conn_counters(name, reset=True), wcounts[name]), name
+    finally:
+        eng.close()
+
+
+def test_conn_counters_do_not_wait_for_other_streams():
+    """cls_conn_counters waits for the table's last counting batch (an event),
+    not for the device: a long torch kernel on another stream is still
+    running when the counters come back, bit-exact."""
+    import time
+
+    import torch
+    from vpp_amd.engine import Engine
+    eng = Engine()
+    try:
+        ifs, bind, by_name, pool, spec = build(eng, 8, n_local=6, n_if=16)
+        n = 6000
+        tr = traffic(8, n, pool, spec, 4)
+        rng = np.random.default_rng(8)
+        ids = np.array([eng.if_id(x) for x in ifs], np.uint32)
+        si, di = rng.integers(0, len(ifs), n), rng.integers(0, len(ifs), n)
+        eng.connect_batch(ids[si], ids[di], tr["src"], tr["dst"], tr["proto"], tr["sport"], tr["dport"], count=True)
+        _, want = oracle_connections(bind, by_name, ifs, si, di, tr, 4)
+        side = torch.cuda.Stream()
+        done = torch.cuda.Event()
+        with torch.cuda.stream(side):
+            torch.cuda._sleep(int(3e9))                 # ~1 s of spinning on `side`
+            done.record(side)
+        t0 = time.perf_counter()
+        got = {name: eng.conn_counters(name) for name in by_name}
+        dt = time.perf_counter() - t0
+        still = not done.query()
+        side.synchronize()
+        assert still, "the sleep kernel finished before the counters were read"
+        assert dt < 0.5, dt
+        for name in by_name:
+            assert np.array_equal(got[name], want[name]), name
+    finally:
+        eng.close()

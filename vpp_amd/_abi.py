@@ -16,7 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CONTIVCLS_LIB") or os.path.join(_HERE, "libcontivcls.so")
 
 SOURCES = ("kernels.hip", "kernels_dev.hpp", "k4_ldsv.hip", "k4_rest.hip", "k4_pair.hip", "k16.hip", "kernels.hpp", "compile.cpp",
-           "compile.hpp", "engine.cpp", "goparse.hpp")
+           "compile.hpp", "engine.cpp", "goparse.hpp", "engine_int.hpp", "fleet.cpp")
 
 
 def source_hash() -> str:
@@ -34,6 +34,10 @@ OK, E_INVAL, E_NOMEM, E_HIP, E_RCCL, E_NOTFOUND, E_NODEV = 0, -1, -2, -3, -4, -5
 # flags
 F_DEVICE, F_NO_VERDICT, F_ACCUMULATE, F_FORCE_LINEAR, F_TIMING, F_CONN_CLS, F_COUNT = 1, 2, 4, 8, 16, 32, 64
 AF_V4, AF_V16 = 4, 16
+# batch fields and flags (cls_batch_*)
+BF_SRC, BF_DST, BF_SPORT, BF_DPORT, BF_PROTO, BF_VERDICT, BF_SRC_IF, BF_DST_IF = range(8)
+BATCH_CONN, BATCH_MIRROR = 1, 2
+ABI_VERSION = 4
 
 R_MATCHES, R_MACIP, R_IPRULE, R_IP, R_OTHER = 1, 2, 4, 8, 16
 R_TCP, R_TCP_SRC, R_TCP_DST = 32, 64, 128
@@ -47,7 +51,11 @@ SYMBOLS = ["cls_abi_version", "cls_engine_create", "cls_engine_destroy", "cls_la
            "cls_if_id",
            "cls_if_acls", "cls_connect_batch", "cls_gen_traffic_v4", "cls_compile_v4", "cls_image_kernel",
            "cls_compile_v16", "cls_gen_traffic_v16", "cls_stream_floor", "cls_stream_floor_shapes", "cls_stream_floor_conn", "cls_conn_bitmap_eval", "cls_conn_counters",
-           "cls_acl_stats"]
+           "cls_acl_stats", "cls_engine_devices", "cls_device_engine", "cls_shard_range", "cls_batch_create",
+           "cls_batch_destroy", "cls_batch_shards", "cls_batch_shard", "cls_batch_field", "cls_batch_mirror",
+           "cls_batch_upload", "cls_batch_download", "cls_batch_gen_traffic_v4", "cls_batch_gen_traffic_v16",
+           "cls_classify_batch", "cls_batch_counters", "cls_batch_connect", "cls_batch_wait", "cls_comm_unique_id",
+           "cls_comm_init", "cls_comm_info"]
 
 
 class ClsRule(C.Structure):
@@ -72,7 +80,8 @@ class ConnSoa(C.Structure):
 
 
 class Config(C.Structure):
-    _fields_ = [("device", C.c_int), ("reserved", C.c_uint32 * 7)]
+    _fields_ = [("device", C.c_int), ("n_devices", C.c_uint32), ("devices", C.POINTER(C.c_int)),
+                ("reserved", C.c_uint32 * 4)]
 
 
 class TableInfo(C.Structure):
@@ -152,11 +161,15 @@ def bind(path: str, strict: bool = True):
     every symbol of this ABI must be there)."""
     # One HIP runtime per process: PyTorch ships its own libamdhip64.so.7.
     # Load it first so that our NEEDED libamdhip64.so.7 resolves to the same
-    # already-loaded runtime (two runtimes in one process cannot share the GPU).
-    try:
-        import torch  # noqa: F401
-    except ImportError:
-        pass
+    # already-loaded runtime (two runtimes in one process cannot share the
+    # GPU).  CONTIVCLS_NO_TORCH=1: a torch-free host (the C ABI alone, as a
+    # cgo host would use it -- tools/native_c3.py); the library then runs on
+    # /opt/rocm's HIP runtime.
+    if os.environ.get("CONTIVCLS_NO_TORCH") != "1":
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
     L = C.CDLL(path, mode=os.RTLD_LOCAL | os.RTLD_NOW)
     vp, u32, u64, i32 = C.c_void_p, C.c_uint32, C.c_uint64, C.c_int32
     sig = {
@@ -194,6 +207,26 @@ def bind(path: str, strict: bool = True):
         "cls_compile_v16": (C.c_int, [C.POINTER(ClsRule), u32, vp, u64, C.POINTER(u64)]),
         "cls_gen_traffic_v16": (C.c_int, [vp, C.POINTER(TrafficSpec16), u64, u64, vp, vp, vp, vp,
                                           vp, vp]),
+        "cls_engine_devices": (C.c_int, [vp, C.POINTER(u32)]),
+        "cls_device_engine": (C.c_int, [vp, u32, C.POINTER(vp)]),
+        "cls_shard_range": (C.c_int, [u64, u32, u32, C.POINTER(u64), C.POINTER(u64)]),
+        "cls_batch_create": (C.c_int, [vp, u32, u64, u32, C.POINTER(vp)]),
+        "cls_batch_destroy": (None, [vp]),
+        "cls_batch_shards": (C.c_int, [vp, C.POINTER(u32)]),
+        "cls_batch_shard": (C.c_int, [vp, u32, C.POINTER(C.c_int), C.POINTER(u64), C.POINTER(u64)]),
+        "cls_batch_field": (C.c_int, [vp, u32, u32, C.POINTER(vp)]),
+        "cls_batch_mirror": (C.c_int, [vp, u32, C.POINTER(vp)]),
+        "cls_batch_upload": (C.c_int, [vp, u32, u64, u64, vp]),
+        "cls_batch_download": (C.c_int, [vp, u32, u64, u64, vp]),
+        "cls_batch_gen_traffic_v4": (C.c_int, [vp, C.POINTER(TrafficSpec), u64]),
+        "cls_batch_gen_traffic_v16": (C.c_int, [vp, C.POINTER(TrafficSpec16), u64]),
+        "cls_classify_batch": (C.c_int, [vp, u32, vp, vp, u32]),
+        "cls_batch_counters": (C.c_int, [vp, vp, u32]),
+        "cls_batch_connect": (C.c_int, [vp, vp, u32]),
+        "cls_batch_wait": (C.c_int, [vp]),
+        "cls_comm_unique_id": (C.c_int, [vp]),
+        "cls_comm_init": (C.c_int, [vp, u32, u32, vp]),
+        "cls_comm_info": (C.c_int, [vp, C.POINTER(u32), C.POINTER(u32)]),
     }
     for name, (res, args) in sig.items():
         if not strict and not hasattr(L, name):      # an older build (A/B tools)

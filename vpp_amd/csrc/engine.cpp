@@ -21,30 +21,11 @@
 
 #include "../../include/contivcls.h"
 #include "compile.hpp"
+#include "engine_int.hpp"
 #include "kernels.hpp"
 
 using namespace cls;
 
-namespace {
-
-struct DevBuf {
-    void* p = nullptr;
-    size_t bytes = 0;
-    ~DevBuf() { if (p) (void)hipFree(p); }
-    hipError_t ensure(size_t n) {
-        if (n <= bytes) return hipSuccess;
-        if (p) { (void)hipFree(p); p = nullptr; bytes = 0; }
-        hipError_t e = hipMalloc(&p, n < 256 ? 256 : n);
-        if (e == hipSuccess) bytes = n < 256 ? 256 : n;
-        return e;
-    }
-    template <typename T> T* as() const { return static_cast<T*>(p); }
-};
-
-// Counter scratch of one (table variant, stream): concurrent classifies of
-// one table on different streams never share a counter buffer
-// (include/contivcls.h, threading).  slot_val is all zero between calls: the
-// remap kernel reads and clears it.
 // OTHER queue (protocols > 2 deferred to the finish launch): per workgroup
 // room for 1/16 of its packets, at most 16 Ki entries (64 KiB per workgroup:
 // the queue exists per (table, stream), and a full segment classifies in
@@ -56,162 +37,9 @@ static uint32_t other_cap(uint64_t n, int grid) {
     return uint32_t(std::min<uint64_t>(16384, std::max<uint64_t>(1024, want)));
 }
 
-struct Scratch {
-    DevBuf part;                   // per-workgroup LDS counter rows [rows][n_lctr]
-    DevBuf oq;                     // OTHER queue {fill per workgroup, segments of indices}
-    DevBuf slot_val;               // u64 per slot: global-tier counters, folded partials
-    DevBuf out;                    // u64 rule counters when the caller gives none on device
-    hipEvent_t done = nullptr;     // recorded after the call's last kernel
-};
-
-// Slot counters of one classifier image (or of the linear kernel alone):
-// slots [0, n_ctr) of the image, then R + 1 direct rule slots.
-struct Counters {
-    uint32_t n_slots = 0;
-    uint32_t n_lctr = 0;           // slots counted in LDS (their partial rows)
-    uint32_t n_image = 0;          // slots of the classifier images; the direct rule slots follow
-    DevBuf d_csr;                  // uint2 {slot, rule}, grouped by rule
-    DevBuf d_slot_rule;            // finish launch: u32 per slot (rule, or kHotRule | h), then the hot rules
-    uint32_t n_hot = 0;
-    DevBuf d_other_map;            // finish launch: compact rule index per OTHER slot, then those rules
-    uint32_t n_other = 0, n_orules = 0;
-    std::map<hipStream_t, std::unique_ptr<Scratch>> sc;
-    ~Counters() {
-        for (auto& kv : sc)
-            if (kv.second->done) {
-                (void)hipEventSynchronize(kv.second->done);   // device work may still read the buffers
-                (void)hipEventDestroy(kv.second->done);
-            }
-    }
-};
-
-struct Table {
-    std::string name;
-    uint32_t n_rules = 0;
-    std::string sig;           // the rules as given (rule_sig): a re-put of equal rules keeps this table
-    // linear (ballot) table, also the protocol>2 fallback
-    std::vector<LinRule4> lin4;
-    DevBuf d_lin4;
-    // IPv4 classifier
-    bool has_cls = false;
-    Cls4Image img;
-    DevBuf d_img;
-    Cls4Image oimg;            // protocols > 2 (compile.hpp Cls4Opts::other), read from global memory
-    DevBuf d_oimg;
-    int kernel = 0;            // 0 linear, 1 classifier
-    bool lds_resident = false;
-    // 16-byte layout (IPv6 / IPv4-mapped): classifier over 32-bit reps
-    struct {
-        bool ok = false;
-        std::string why;           // why there is none
-        Cls16Image img;
-        std::vector<LinRule4> lin; // rules in rep space (FORCE_LINEAR)
-        Cls4Image oimg;            // protocols > 2, rep space
-        DevBuf d_img, d_lin, d_oimg;
-        DevBuf d_src_search;       // src_mode 1, 2: the source interval table (global memory)
-        bool lds_resident = false;
-        DevBuf d_slot_rule;        // slot mode (connection batches): slot -> rule, core then OTHER image
-    } p16;
-    // connection path: compact linear rules (cls_connect_batch's rule pool),
-    // slot -> rule of the v4 images (slot mode), and the per-rule connection
-    // counters (CLS_F_COUNT; allocated on first use, R + 1 u64)
-    std::vector<ConnRule4> conn4;
-    std::vector<ConnRule16> conn16;
-    // the bitmap form of conn4 (conn_bitmap4), built on the first connection
-    // batch that wants it; empty when its tables exceed kConnBmMaxWords
-    std::vector<uint32_t> conn_bm;
-    bool conn_bm_built = false;
-    DevBuf d_slot_rule;
-    DevBuf d_conn_ctr;
-    // recorded on the engine stream behind a rebind's counter clearing; a
-    // counting connection batch on another stream waits for it
-    hipEvent_t conn_ctr_ev = nullptr;
-    ~Table() {
-        if (conn_ctr_ev) (void)hipEventDestroy(conn_ctr_ev);
-    }
-    // declared last: destroyed first, so pending device work is waited for
-    // before any of the buffers above are freed
-    Counters c4, c16;
-};
-
-struct AclEntry {
-    uint32_t table_id = 0;
-    std::vector<uint32_t> ingress, egress;
-};
-
-}  // namespace
-
-// The host side of a connection batch over the current bindings: one
-// descriptor per bound table, (in, out) per interface, the large ACLs
-// evaluated by the classifier, the rule pool with the bitmap forms.  A device
-// batch's plan depends only on the bindings and the flags, so it is kept
-// until they change (cls_engine::conn_gen).
-struct ConnPlan {
-    uint64_t key = ~0ull, gen = ~0ull;
-    uint64_t id = 0;                                      // which plan s_desc / s_ifs / s_rules hold (uploaded)
-    std::vector<ConnDesc> desc;
-    std::vector<std::shared_ptr<Table>> dtab;             // table of each descriptor
-    std::vector<IfAcls> ifs;
-    std::vector<uint32_t> big;                            // descriptors of the large ACLs
-    std::vector<uint8_t> pool;
-    uint32_t n_ctr = 0;
-    uint32_t bm_steps = 0;                                // lower-bound steps of the largest bitmap table
-};
-
-struct cls_engine {
-    int device = 0;
-    int n_cu = 256;
-    hipStream_t stream = nullptr;
-    std::mutex mu;
-    std::string err;
-    std::map<uint32_t, std::shared_ptr<Table>> tables;
-    uint32_t next_table = 1;
-    // ACLConfig
-    std::map<std::string, AclEntry> acls;
-    std::unordered_map<std::string, uint32_t> if_ids;
-    std::vector<std::string> if_names;
-    std::vector<std::pair<int32_t, int32_t>> if_acl;   // per if id: (inbound, outbound) table id
-    uint32_t changes = 0;
-    uint32_t compiles = 0, rebinds = 0;   // cls_acl_put: tables compiled / puts that kept the table
-    // scratch for host-pointer batches
-    DevBuf s_src, s_dst, s_sport, s_dport, s_proto, s_verdict, s_if_a, s_if_b, s_desc, s_ifs;
-    DevBuf s_pre;                  // connection path: classifier slot words per large ACL (8 bytes/connection)
-    DevBuf s_pq;                   // connection path: the pair launch's OTHER queue
-    DevBuf s_rules, s_tctr, s_cctr;  // connection path: rule pool, table counter pointers, call counters
-    bool cctr_zero = false;          // s_cctr cleared since its allocation (the scatter launch keeps it zero)
-    uint64_t conn_gen = 0;           // bumped by every change of tables or interface bindings
-    ConnPlan conn_plan;              // the last device batch's plan
-    uint64_t plan_ids = 0, up_plan = ~0ull;   // plan ids; the plan whose tables are on the device
-    // what s_desc, s_ifs, s_rules and s_tctr hold (the last upload): a
-    // connection batch over unchanged bindings uploads nothing
-    std::vector<uint8_t> up_desc, up_ifs, up_rules, up_tctr;
-    DevBuf s_pool;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
-    bool timed = false;
-    // per-launch timing (CLS_F_TIMING): event pairs, recycled after a reset
-    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pool;
-    size_t ev_used = 0;
-};
-
-static int fail(cls_engine* e, int code, const char* fmt, ...) {
-    if (e) {
-        char buf[512];
-        va_list ap;
-        va_start(ap, fmt);
-        vsnprintf(buf, sizeof buf, fmt, ap);
-        va_end(ap);
-        e->err = buf;
-    }
-    return code;
-}
-
-#define HIPC(e, expr)                                                                    \
-    do {                                                                                 \
-        hipError_t _h = (expr);                                                          \
-        if (_h != hipSuccess)                                                            \
-            return fail((e), CLS_E_HIP, "%s: %s (%s:%d)", #expr, hipGetErrorString(_h),  \
-                        __FILE__, __LINE__);                                             \
-    } while (0)
+static int acl_put_locked(cls_engine* e, const char* acl_name, const cls_rule* rules, uint32_t n_rules,
+                          const char* const* ingress_ifs, uint32_t n_ingress, const char* const* egress_ifs,
+                          uint32_t n_egress);
 
 extern "C" {
 
@@ -221,12 +49,14 @@ int cls_image_kernel(uint32_t mode, uint32_t list_mode, int lds_resident, int re
     return cls_kernel_exists(mode, list_mode, lds_resident != 0, rep16 != 0) ? CLS_OK : CLS_E_INVAL;
 }
 
-int cls_engine_create(const cls_config* cfg, cls_engine** out) {
-    if (!out) return CLS_E_INVAL;
+}  // extern "C"
+
+// One device's engine (cls_engine_create, fleet.cpp, builds multi-device
+// engines from these).  device < 0: the current device.
+int engine_open(int dev, cls_engine** out) {
     *out = nullptr;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return CLS_E_NODEV;
-    int dev = cfg && cfg->device >= 0 ? cfg->device : -1;
     if (dev < 0 && hipGetDevice(&dev) != hipSuccess) return CLS_E_NODEV;
     if (dev >= ndev) return CLS_E_NODEV;
     hipDeviceProp_t prop;
@@ -247,18 +77,28 @@ int cls_engine_create(const cls_config* cfg, cls_engine** out) {
     return CLS_OK;
 }
 
-void cls_engine_destroy(cls_engine* e) {
-    if (!e) return;
+// Waits for the engine's device work (its streams only: other engines and
+// torch streams on the device are not waited for), then frees it.
+void engine_close(cls_engine* e) {
     (void)hipSetDevice(e->device);
-    (void)hipDeviceSynchronize();
-    e->tables.clear();
+    if (e->stream) (void)hipStreamSynchronize(e->stream);
+    if (e->coll) (void)hipStreamSynchronize(e->coll);
+    e->conn_plan = ConnPlan();
+    e->tables.clear();                 // each table's Counters wait for their streams' work
     for (auto& pr : e->ev_pool) {
         (void)hipEventDestroy(pr.first);
         (void)hipEventDestroy(pr.second);
     }
+    for (int k = 0; k < 2; ++k) {
+        if (e->stage_ev[k]) (void)hipEventDestroy(e->stage_ev[k]);
+        if (e->stage[k]) (void)hipHostFree(e->stage[k]);
+    }
+    if (e->coll) (void)hipStreamDestroy(e->coll);
     if (e->stream) (void)hipStreamDestroy(e->stream);
     delete e;
 }
+
+extern "C" {
 
 const char* cls_last_error(const cls_engine* e) { return e ? e->err.c_str() : "null engine"; }
 
@@ -385,8 +225,13 @@ static int upload(cls_engine* e, DevBuf& d, const Cls4Image& im) {
 // The counter scratch of (table variant, stream), created on first use.
 static int scratch_of(cls_engine* e, Counters& c, uint32_t n_rules, hipStream_t s, Scratch** out);
 
-static int table_put_locked(cls_engine* e, const char* name, const cls_rule* rules, uint32_t n,
-                            uint32_t* table_id) {
+}  // extern "C"
+
+// A table's host form: the rules compiled once (evalACL semantics, both
+// layouts, the connection path's compact rules).  No device work, so a
+// multi-device engine compiles each table once and uploads it per device.
+static int table_compile(cls_engine* e, const char* name, const cls_rule* rules, uint32_t n,
+                         std::shared_ptr<Table>& out) {
     if (n && !rules) return fail(e, CLS_E_INVAL, "rules is NULL");
     auto t = std::make_shared<Table>();
     t->name = name ? name : "";
@@ -398,64 +243,120 @@ static int table_put_locked(cls_engine* e, const char* name, const cls_rule* rul
     if (rc != CLS_OK) return fail(e, rc, "%s", why.c_str());
     t->lin4 = linear4(sem);
     t->conn4 = conn_rules4(sem);
-    HIPC(e, hipSetDevice(e->device));
-    HIPC(e, t->d_lin4.ensure(std::max<size_t>(1, t->lin4.size()) * sizeof(LinRule4)));
-    if (!t->lin4.empty())
-        HIPC(e, hipMemcpy(t->d_lin4.p, t->lin4.data(), t->lin4.size() * sizeof(LinRule4), hipMemcpyHostToDevice));
     // classifier for anything but tiny tables
     t->kernel = 0;
-    if (sem.size() > 8) {
-        if (build_pair(sem, n, t->img, t->oimg, why)) {
-            t->has_cls = true;
-            t->kernel = 1;
-            t->lds_resident = t->img.lds_ok && t->img.lds_bytes + kLdsReserved <= uint32_t(max_lds_bytes());
-            // the trie and wide cells exist only in LDS-resident images
-            if (!cls_kernel_exists(t->img.mode, t->img.list_mode, t->lds_resident, false))
-                return fail(e, CLS_E_INVAL, "no classify kernel for the compiled image (mode %u, list mode %u%s)",
-                            t->img.mode, t->img.list_mode, t->lds_resident ? "" : ", global memory");
-            rc = upload(e, t->d_img, t->img);
-            if (rc == CLS_OK) rc = upload(e, t->d_oimg, t->oimg);
-            if (rc == CLS_OK) rc = upload_slot_rule(e, t->d_slot_rule, t->img, t->oimg);
-            if (rc != CLS_OK) return rc;
-        }
-    }
-    {
-        const int rc2 = counters_init(e, t->c4, t->has_cls ? &t->img : nullptr, t->has_cls ? &t->oimg : nullptr, n);
-        if (rc2 != CLS_OK) return rc2;
+    if (sem.size() > 8 && build_pair(sem, n, t->img, t->oimg, why)) {
+        t->has_cls = true;
+        t->kernel = 1;
+        t->lds_resident = t->img.lds_ok && t->img.lds_bytes + kLdsReserved <= uint32_t(max_lds_bytes());
+        // the trie and wide cells exist only in LDS-resident images
+        if (!cls_kernel_exists(t->img.mode, t->img.list_mode, t->lds_resident, false))
+            return fail(e, CLS_E_INVAL, "no classify kernel for the compiled image (mode %u, list mode %u%s)",
+                        t->img.mode, t->img.list_mode, t->lds_resident ? "" : ", global memory");
     }
     // 16-byte layout: both families' reductions over one rep space
-    {
-        auto& q = t->p16;
-        std::vector<SemRule> s16;
-        rc = semantic_rules(rules, n, 0, s16, why);
-        if (rc != CLS_OK) return fail(e, rc, "%s", why.c_str());
-        t->conn16 = conn_rules16(s16);
-        std::string why16;
-        q.ok = build_cls16(s16, n, q.img, why16) && build_other4(q.img.sem, n, q.oimg, why16);
-        q.why = why16;
-        if (q.ok) {
-            const Cls4Image& c = q.img.core;
-            q.lin = linear4(q.img.sem);
-            q.lds_resident = c.lds_ok && c.lds_bytes + kLdsReserved <= uint32_t(max_lds_bytes());
-            if (!cls_kernel_exists(c.mode, c.list_mode, q.lds_resident, true))
-                return fail(e, CLS_E_INVAL, "no 16-byte classify kernel for the compiled image (mode %u, list mode %u%s)",
-                            c.mode, c.list_mode, q.lds_resident ? "" : ", global memory");
-            rc = upload(e, q.d_img, c);
-            if (rc == CLS_OK) rc = upload(e, q.d_oimg, q.oimg);
-            if (rc == CLS_OK) rc = upload_slot_rule(e, q.d_slot_rule, c, q.oimg);
-            if (rc != CLS_OK) return rc;
-            HIPC(e, q.d_lin.ensure(std::max<size_t>(1, q.lin.size()) * sizeof(LinRule4)));
-            if (!q.lin.empty())
-                HIPC(e, hipMemcpy(q.d_lin.p, q.lin.data(), q.lin.size() * sizeof(LinRule4), hipMemcpyHostToDevice));
-            const int rc2 = counters_init(e, t->c16, &c, &q.oimg, n);
-            if (rc2 != CLS_OK) return rc2;
-            if (q.img.src_mode >= 1) {
-                HIPC(e, q.d_src_search.ensure(q.img.src_search.size() * 4));
-                HIPC(e, hipMemcpy(q.d_src_search.p, q.img.src_search.data(), q.img.src_search.size() * 4,
-                                  hipMemcpyHostToDevice));
-            }
+    auto& q = t->p16;
+    std::vector<SemRule> s16;
+    rc = semantic_rules(rules, n, 0, s16, why);
+    if (rc != CLS_OK) return fail(e, rc, "%s", why.c_str());
+    t->conn16 = conn_rules16(s16);
+    std::string why16;
+    q.ok = build_cls16(s16, n, q.img, why16) && build_other4(q.img.sem, n, q.oimg, why16);
+    q.why = why16;
+    if (q.ok) {
+        const Cls4Image& c = q.img.core;
+        q.lin = linear4(q.img.sem);
+        q.lds_resident = c.lds_ok && c.lds_bytes + kLdsReserved <= uint32_t(max_lds_bytes());
+        if (!cls_kernel_exists(c.mode, c.list_mode, q.lds_resident, true))
+            return fail(e, CLS_E_INVAL, "no 16-byte classify kernel for the compiled image (mode %u, list mode %u%s)",
+                        c.mode, c.list_mode, q.lds_resident ? "" : ", global memory");
+    }
+    out = std::move(t);
+    return CLS_OK;
+}
+
+std::shared_ptr<Table> table_clone_host(const Table& s) {
+    auto t = std::make_shared<Table>();
+    t->name = s.name;
+    t->n_rules = s.n_rules;
+    t->sig = s.sig;
+    t->lin4 = s.lin4;
+    t->has_cls = s.has_cls;
+    t->img = s.img;
+    t->oimg = s.oimg;
+    t->kernel = s.kernel;
+    t->lds_resident = s.lds_resident;
+    t->p16.ok = s.p16.ok;
+    t->p16.why = s.p16.why;
+    t->p16.img = s.p16.img;
+    t->p16.lin = s.p16.lin;
+    t->p16.oimg = s.p16.oimg;
+    t->p16.lds_resident = s.p16.lds_resident;
+    t->conn4 = s.conn4;
+    t->conn16 = s.conn16;
+    t->conn_bm = s.conn_bm;
+    t->conn_bm_built = s.conn_bm_built;
+    t->conn_epoch = s.conn_epoch;
+    return t;
+}
+
+// The device copies of a compiled table on this engine's device.
+int table_upload(cls_engine* e, Table& t) {
+    HIPC(e, hipSetDevice(e->device));
+    HIPC(e, t.d_lin4.ensure(std::max<size_t>(1, t.lin4.size()) * sizeof(LinRule4)));
+    if (!t.lin4.empty())
+        HIPC(e, hipMemcpy(t.d_lin4.p, t.lin4.data(), t.lin4.size() * sizeof(LinRule4), hipMemcpyHostToDevice));
+    int rc = CLS_OK;
+    if (t.has_cls) {
+        rc = upload(e, t.d_img, t.img);
+        if (rc == CLS_OK) rc = upload(e, t.d_oimg, t.oimg);
+        if (rc == CLS_OK) rc = upload_slot_rule(e, t.d_slot_rule, t.img, t.oimg);
+        if (rc != CLS_OK) return rc;
+    }
+    rc = counters_init(e, t.c4, t.has_cls ? &t.img : nullptr, t.has_cls ? &t.oimg : nullptr, t.n_rules);
+    if (rc != CLS_OK) return rc;
+    auto& q = t.p16;
+    if (q.ok) {
+        const Cls4Image& c = q.img.core;
+        rc = upload(e, q.d_img, c);
+        if (rc == CLS_OK) rc = upload(e, q.d_oimg, q.oimg);
+        if (rc == CLS_OK) rc = upload_slot_rule(e, q.d_slot_rule, c, q.oimg);
+        if (rc != CLS_OK) return rc;
+        HIPC(e, q.d_lin.ensure(std::max<size_t>(1, q.lin.size()) * sizeof(LinRule4)));
+        if (!q.lin.empty())
+            HIPC(e, hipMemcpy(q.d_lin.p, q.lin.data(), q.lin.size() * sizeof(LinRule4), hipMemcpyHostToDevice));
+        rc = counters_init(e, t.c16, &c, &q.oimg, t.n_rules);
+        if (rc != CLS_OK) return rc;
+        if (q.img.src_mode >= 1) {
+            HIPC(e, q.d_src_search.ensure(q.img.src_search.size() * 4));
+            HIPC(e, hipMemcpy(q.d_src_search.p, q.img.src_search.data(), q.img.src_search.size() * 4,
+                              hipMemcpyHostToDevice));
         }
     }
+    return CLS_OK;
+}
+
+extern "C" {
+
+// Configuration calls are made on the primary engine; a peer (a device of a
+// multi-device engine, cls_device_engine) mirrors it.
+static int refuse_peer(cls_engine* e) {
+    return fail(e, CLS_E_INVAL, "configure a multi-device engine through its primary engine");
+}
+
+// A table (or a dropped binding) is gone: the kept connection plan must not
+// hold its device buffers until the next device batch replans.
+static void drop_conn_plan(cls_engine* e) {
+    e->conn_plan = ConnPlan();
+    e->up_plan = ~0ull;
+}
+
+static int table_put_locked(cls_engine* e, const char* name, const cls_rule* rules, uint32_t n,
+                            uint32_t* table_id) {
+    std::shared_ptr<Table> t;
+    int rc = table_compile(e, name, rules, n, t);
+    if (rc == CLS_OK) rc = table_upload(e, *t);
+    if (rc != CLS_OK) return rc;
     const uint32_t id = e->next_table++;
     e->tables[id] = t;
     e->conn_gen++;                  // connection plans see the change
@@ -467,16 +368,20 @@ int cls_table_put(cls_engine* e, const char* name, const cls_rule* rules, uint32
                   uint32_t* table_id) {
     if (!e) return CLS_E_INVAL;
     std::lock_guard<std::mutex> g(e->mu);
-    return table_put_locked(e, name, rules, n_rules, table_id);
+    if (e->primary) return refuse_peer(e);
+    const int rc = table_put_locked(e, name, rules, n_rules, table_id);
+    return rc == CLS_OK ? sync_peers(e) : rc;
 }
 
 int cls_table_del(cls_engine* e, uint32_t table_id) {
     if (!e) return CLS_E_INVAL;
     std::lock_guard<std::mutex> g(e->mu);
+    if (e->primary) return refuse_peer(e);
     HIPC(e, hipSetDevice(e->device));
     if (!e->tables.erase(table_id)) return fail(e, CLS_E_NOTFOUND, "no table %u", table_id);
     e->conn_gen++;                  // connection plans see the change
-    return CLS_OK;
+    drop_conn_plan(e);
+    return sync_peers(e);
 }
 
 int cls_table_get_info(cls_engine* e, uint32_t table_id, cls_table_info* info) {
@@ -829,6 +734,13 @@ int cls_classify(cls_engine* e, uint32_t table_id, const cls_pkt_soa* pk, uint64
                  uint8_t* verdict_out, uint64_t* counters_out, uint32_t flags, void* stream) {
     if (!e || !pk) return CLS_E_INVAL;
     std::lock_guard<std::mutex> g(e->mu);
+    return classify_locked(e, table_id, pk, n, verdict_out, counters_out, flags, stream);
+}
+
+}  // extern "C"
+
+int classify_locked(cls_engine* e, uint32_t table_id, const cls_pkt_soa* pk, uint64_t n,
+                    uint8_t* verdict_out, uint64_t* counters_out, uint32_t flags, void* stream) {
     auto it = e->tables.find(table_id);
     if (it == e->tables.end()) return fail(e, CLS_E_NOTFOUND, "no table %u", table_id);
     std::shared_ptr<Table> t = it->second;
@@ -924,6 +836,8 @@ int cls_classify(cls_engine* e, uint32_t table_id, const cls_pkt_soa* pk, uint64
     if (co.zero && !zeroed) HIPC(e, launch_fold(nullptr, 0, 0, slot_val, co.out, t->n_rules + 1, s));
     return finish_counts(e, *t, t->c4, sc, co, n, verdict_out, d_verdict, counters_out, flags, s, remapped);
 }
+
+extern "C" {
 
 // Each stream shape's time (cls_stream_floor_shapes): shape = variant << 1 |
 // (two workgroups per CU), 8 shapes for the IPv4 layout, 2 for the 16-byte one.
@@ -1059,6 +973,7 @@ static int acl_del_locked(cls_engine* e, const std::string& name) {
     }
     e->tables.erase(it->second.table_id);
     e->conn_gen++;                  // connection plans see the change
+    drop_conn_plan(e);
     e->acls.erase(it);
     e->changes++;
     return CLS_OK;
@@ -1069,6 +984,16 @@ int cls_acl_put(cls_engine* e, const char* acl_name, const cls_rule* rules, uint
                 uint32_t n_egress) {
     if (!e || !acl_name) return CLS_E_INVAL;
     std::lock_guard<std::mutex> g(e->mu);
+    if (e->primary) return refuse_peer(e);
+    const int rc = acl_put_locked(e, acl_name, rules, n_rules, ingress_ifs, n_ingress, egress_ifs, n_egress);
+    return rc == CLS_OK ? sync_peers(e) : rc;
+}
+
+}  // extern "C"
+
+static int acl_put_locked(cls_engine* e, const char* acl_name, const cls_rule* rules, uint32_t n_rules,
+                          const char* const* ingress_ifs, uint32_t n_ingress, const char* const* egress_ifs,
+                          uint32_t n_egress) {
     if (n_ingress + n_egress == 0) return fail(e, CLS_E_INVAL, "ACL with empty interfaces");
     if (n_rules && !rules) return fail(e, CLS_E_INVAL, "rules is NULL");
     const std::string name(acl_name);
@@ -1093,6 +1018,7 @@ int cls_acl_put(cls_engine* e, const char* acl_name, const cls_rule* rules, uint
             if (!kt.conn_ctr_ev) HIPC(e, hipEventCreateWithFlags(&kt.conn_ctr_ev, hipEventDisableTiming));
             HIPC(e, hipEventRecord(kt.conn_ctr_ev, e->stream));
         }
+        kt.conn_epoch++;                // a multi-device engine's peers clear their copies
         for (auto& b : e->if_acl) {
             if (b.first == int32_t(tid)) b.first = -1;
             if (b.second == int32_t(tid)) b.second = -1;
@@ -1127,6 +1053,8 @@ int cls_acl_put(cls_engine* e, const char* acl_name, const cls_rule* rules, uint
     return CLS_OK;
 }
 
+extern "C" {
+
 int cls_acl_stats(cls_engine* e, uint32_t* n_compiles, uint32_t* n_rebinds) {
     if (!e) return CLS_E_INVAL;
     std::lock_guard<std::mutex> g(e->mu);
@@ -1138,7 +1066,9 @@ int cls_acl_stats(cls_engine* e, uint32_t* n_compiles, uint32_t* n_rebinds) {
 int cls_acl_del(cls_engine* e, const char* acl_name) {
     if (!e || !acl_name) return CLS_E_INVAL;
     std::lock_guard<std::mutex> g(e->mu);
-    return acl_del_locked(e, acl_name);
+    if (e->primary) return refuse_peer(e);
+    const int rc = acl_del_locked(e, acl_name);
+    return rc == CLS_OK ? sync_peers(e) : rc;
 }
 
 int cls_acl_table(cls_engine* e, const char* acl_name, uint32_t* table_id) {
@@ -1161,8 +1091,9 @@ int cls_acl_counts(cls_engine* e, uint32_t* n_acls, uint32_t* n_changes) {
 int cls_if_id(cls_engine* e, const char* if_name, uint32_t* id) {
     if (!e || !if_name || !id) return CLS_E_INVAL;
     std::lock_guard<std::mutex> g(e->mu);
+    if (e->primary) return refuse_peer(e);
     *id = if_id_locked(e, if_name);
-    return CLS_OK;
+    return sync_peers(e);
 }
 
 int cls_if_acls(cls_engine* e, uint32_t if_id, int32_t* in_table, int32_t* out_table) {
@@ -1272,6 +1203,21 @@ int cls_connect_batch(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t*
                       uint32_t flags, void* stream) {
     if (!e || !c || (n && !out)) return CLS_E_INVAL;
     std::lock_guard<std::mutex> g(e->mu);
+    return connect_locked(e, c, n, out, flags, stream, true);
+}
+
+}  // extern "C"
+
+// The OTHER queue of a pair launch: a fixed segment per workgroup (its
+// overflow is classified in place), so the buffer does not grow with the
+// batch.  CONTIVCLS_PAIR_QCAP: tests, to reach the in-place path.
+static uint32_t pair_qcap(uint64_t n, int grid) {
+    if (const char* c = std::getenv("CONTIVCLS_PAIR_QCAP")) return uint32_t(std::strtoul(c, nullptr, 0));
+    return uint32_t(std::min<uint64_t>(pair_queue_words(n, grid), 16384));
+}
+
+int connect_locked(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t* out, uint32_t flags, void* stream,
+                   bool sync) {
     const cls_pkt_soa& pk = c->pkt;
     const bool k16 = pk.af == CLS_AF_V16;
     if (!k16 && pk.af != CLS_AF_V4) return fail(e, CLS_E_INVAL, "af must be CLS_AF_V4 or CLS_AF_V16");
@@ -1490,14 +1436,17 @@ int cls_connect_batch(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t*
                     uint32_t o_at = (t.img.img_bytes + 15u) & ~15u;
                     // (+ 32: the queue fill word after the images)
                     if (o_at + t.oimg.img_bytes + 32u > uint32_t(max_lds_bytes())) o_at = 0;
+                    if (std::getenv("CONTIVCLS_PAIR_OTHER_GLOBAL")) o_at = 0;   // tests: the global-memory OTHER path
                     Cls4Dev od = cls4_dev(t.oimg, t.d_oimg, DevBuf(), 0, t.n_rules);
                     if (o_at) {
                         od.off_bounds += o_at; od.off_iclass += o_at; od.off_cells += o_at;
                         od.off_lists += o_at; od.off_tmpl += o_at;
                     }
                     cfg.grid = cls_grid(e, true, true, o_at ? o_at + t.oimg.img_bytes : t.img.img_bytes, n);
-                    HIPC(e, e->s_pq.ensure(size_t(cfg.grid) * pair_queue_words(n, cfg.grid) * 16));
-                    HIPC(e, launch_classify4_pair(cd, od, o_at, syn, sp, pre, stride, e->s_pq.as<uint32_t>(), cfg));
+                    const uint32_t qcap = pair_qcap(n, cfg.grid);
+                    HIPC(e, e->s_pq.ensure(size_t(cfg.grid) * std::max<uint32_t>(1, qcap) * 16));
+                    HIPC(e, launch_classify4_pair(cd, od, o_at, syn, sp, pre, stride, e->s_pq.as<uint32_t>(), qcap,
+                                                  cfg));
                 } else {
                     cfg.other = cls4_dev(t.oimg, t.d_oimg, DevBuf(), 0, t.n_rules);
                     cfg.grid = cls_grid(e, true, t.lds_resident, t.img.lds_bytes, n);
@@ -1548,8 +1497,10 @@ int cls_connect_batch(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t*
         const uint8_t* b = static_cast<const uint8_t*>(src);
         if (d.p == was && last.size() == bytes && (bytes == 0 || std::memcmp(last.data(), b, bytes) == 0))
             return CLS_OK;
-        if (bytes) HIPC(e, hipMemcpyAsync(d.p, b, bytes, hipMemcpyHostToDevice, s));
         last.assign(b, b + bytes);
+        // from the engine's copy: it outlives the call (an unsynchronised
+        // batch, sync = false, may still be copying when this returns)
+        if (bytes) HIPC(e, hipMemcpyAsync(d.p, last.data(), bytes, hipMemcpyHostToDevice, s));
         return CLS_OK;
     };
     if (e->up_plan != P.id) {                             // a kept plan's tables are on the device already
@@ -1571,10 +1522,11 @@ int cls_connect_batch(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t*
         // what it moves); cleared here only when (re)allocated
         const size_t had = e->s_cctr.bytes;
         HIPC(e, e->s_cctr.ensure(size_t(n_ctr) * 8));
-        if (e->s_cctr.bytes != had || !e->cctr_zero) {
+        if (e->s_cctr.bytes != had || !e->cctr_zero)
             HIPC(e, hipMemsetAsync(e->s_cctr.p, 0, e->s_cctr.bytes, s));
-            e->cctr_zero = true;
-        }
+        // zero again only once the scatter launch (which clears what it
+        // moves) is queued: an early return below forces the memset next time
+        e->cctr_zero = false;
         a.ctr = e->s_cctr.as<unsigned long long>();
         for (size_t j = 0; j < dtab.size(); ++j) {
             Table& t = *dtab[j];
@@ -1615,13 +1567,25 @@ int cls_connect_batch(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t*
         for (const ConnDesc& d : desc) max_rules = std::max(max_rules, d.n_rules);
         HIPC(e, launch_conn_scatter(a.desc, e->s_tctr.as<unsigned long long* const>(), uint32_t(desc.size()),
                                     max_rules, e->s_cctr.as<unsigned long long>(), s));
+        e->cctr_zero = true;
+        // cls_conn_counters waits for this batch's scatter, not the device
+        for (size_t j = 0; j < dtab.size(); ++j) {
+            Table& t = *dtab[j];
+            if (!t.conn_ev) HIPC(e, hipEventCreateWithFlags(&t.conn_ev, hipEventDisableTiming));
+            HIPC(e, hipEventRecord(t.conn_ev, s));
+        }
+    } else if (cmode) {
+        e->cctr_zero = true;            // n == 0: nothing was counted
     }
     if (!dev && n) HIPC(e, hipMemcpyAsync(out, o, n, hipMemcpyDeviceToHost, s));
     // descriptor, pool and counter buffers are engine scratch: finish before
-    // they can be reused (and before the host vectors above go away)
-    HIPC(e, hipStreamSynchronize(s));
+    // they can be reused (and before the host vectors above go away); a
+    // batch of a multi-device engine synchronises all its devices at the end
+    if (sync || !dev) HIPC(e, hipStreamSynchronize(s));
     return CLS_OK;
 }
+
+extern "C" {
 
 int cls_stream_floor_conn(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t* out, uint32_t reps,
                           float* ms, void* stream) {
@@ -1653,21 +1617,42 @@ int cls_stream_floor_conn(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint
     return CLS_OK;
 }
 
+// One device's connection counters of a table, added to `acc`: waits for
+// the last counting batch's scatter and a rebind's clearing (events), not
+// for other work on the device.
+static int conn_counters_dev(cls_engine* d, uint32_t table_id, std::vector<uint64_t>& acc, uint32_t reset) {
+    auto it = d->tables.find(table_id);
+    if (it == d->tables.end()) return fail(d, CLS_E_NOTFOUND, "no table %u", table_id);
+    Table& t = *it->second;
+    if (!t.d_conn_ctr.p) return CLS_OK;
+    HIPC(d, hipSetDevice(d->device));
+    const size_t bytes = size_t(t.n_rules + 1) * 8;
+    std::vector<uint64_t> h(t.n_rules + 1);
+    if (t.conn_ev) HIPC(d, hipStreamWaitEvent(d->stream, t.conn_ev, 0));
+    if (t.conn_ctr_ev) HIPC(d, hipStreamWaitEvent(d->stream, t.conn_ctr_ev, 0));
+    HIPC(d, hipMemcpyAsync(h.data(), t.d_conn_ctr.p, bytes, hipMemcpyDeviceToHost, d->stream));
+    if (reset) HIPC(d, hipMemsetAsync(t.d_conn_ctr.p, 0, bytes, d->stream));
+    HIPC(d, hipStreamSynchronize(d->stream));
+    for (size_t i = 0; i < h.size(); ++i) acc[i] += h[i];
+    return CLS_OK;
+}
+
 int cls_conn_counters(cls_engine* e, uint32_t table_id, uint64_t* counters_out, uint32_t reset) {
     if (!e || !counters_out) return CLS_E_INVAL;
     std::lock_guard<std::mutex> g(e->mu);
     auto it = e->tables.find(table_id);
     if (it == e->tables.end()) return fail(e, CLS_E_NOTFOUND, "no table %u", table_id);
-    Table& t = *it->second;
-    HIPC(e, hipSetDevice(e->device));
-    const size_t bytes = size_t(t.n_rules + 1) * 8;
-    if (!t.d_conn_ctr.p) {
-        std::memset(counters_out, 0, bytes);
-        return CLS_OK;
+    std::vector<uint64_t> acc(size_t(it->second->n_rules) + 1, 0);
+    // a multi-device engine: the sum over its devices (each counts its own
+    // shard of every connection batch)
+    for (size_t i = 0; i < n_dev_engines(e); ++i) {
+        cls_engine* d = dev_engine(e, i);
+        std::unique_lock<std::mutex> lk(d->mu, std::defer_lock);
+        if (d != e) lk.lock();
+        const int rc = conn_counters_dev(d, table_id, acc, reset);
+        if (rc != CLS_OK) return d == e ? rc : fail(e, rc, "device %d: %s", d->device, d->err.c_str());
     }
-    HIPC(e, hipDeviceSynchronize());          // every stream's connection batches on this table
-    HIPC(e, hipMemcpy(counters_out, t.d_conn_ctr.p, bytes, hipMemcpyDeviceToHost));
-    if (reset) HIPC(e, hipMemset(t.d_conn_ctr.p, 0, bytes));
+    std::memcpy(counters_out, acc.data(), acc.size() * 8);
     return CLS_OK;
 }
 
@@ -1677,6 +1662,13 @@ int cls_gen_traffic_v4(cls_engine* e, const cls_traffic_spec* sp, uint64_t first
                        uint8_t* proto, void* stream) {
     if (!e || !sp) return CLS_E_INVAL;
     std::lock_guard<std::mutex> g(e->mu);
+    return gen4_locked(e, sp, first, n, src4, dst4, sport, dport, proto, stream, true);
+}
+
+}  // extern "C"
+
+int gen4_locked(cls_engine* e, const cls_traffic_spec* sp, uint64_t first, uint64_t n, uint32_t* src4,
+                uint32_t* dst4, uint16_t* sport, uint16_t* dport, uint8_t* proto, void* stream, bool sync) {
     HIPC(e, hipSetDevice(e->device));
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : e->stream;
     const size_t bp = size_t(sp->n_pod_ips) * 4, bd = size_t(sp->n_dst) * 4, bl = sp->n_dst,
@@ -1697,9 +1689,13 @@ int cls_gen_traffic_v4(cls_engine* e, const cls_traffic_spec* sp, uint64_t first
     if (bl) HIPC(e, hipMemcpyAsync(base + al(bp) + al(bd), sp->dst_lens, bl, hipMemcpyHostToDevice, s));
     if (bq) HIPC(e, hipMemcpyAsync(base + al(bp) + al(bd) + al(bl), sp->ports, bq, hipMemcpyHostToDevice, s));
     HIPC(e, launch_gen4(t, first, n, src4, dst4, sport, dport, proto, s));
-    HIPC(e, hipStreamSynchronize(s));   // the pools are engine scratch
+    // the pools are engine scratch (sync = false: the caller synchronises
+    // before the next use)
+    if (sync) HIPC(e, hipStreamSynchronize(s));
     return CLS_OK;
 }
+
+extern "C" {
 
 // Blob of cls_compile_v4 / cls_compile_v16: header (v4 header, then `extra`
 // bytes of a larger header), image, slot -> rule map, linear rules.
@@ -1793,9 +1789,16 @@ int cls_gen_traffic_v16(cls_engine* e, const cls_traffic_spec16* sp, uint64_t fi
                         uint8_t* src16, uint8_t* dst16, uint16_t* sport, uint16_t* dport, uint8_t* proto,
                         void* stream) {
     if (!e || !sp) return CLS_E_INVAL;
+    std::lock_guard<std::mutex> g(e->mu);
+    return gen16_locked(e, sp, first, n, src16, dst16, sport, dport, proto, stream, true);
+}
+
+}  // extern "C"
+
+int gen16_locked(cls_engine* e, const cls_traffic_spec16* sp, uint64_t first, uint64_t n, uint8_t* src16,
+                 uint8_t* dst16, uint16_t* sport, uint16_t* dport, uint8_t* proto, void* stream, bool sync) {
     if ((src16 && !aligned(src16, 16)) || (dst16 && !aligned(dst16, 16)))
         return fail(e, CLS_E_INVAL, "src16/dst16 must be 16-byte aligned");
-    std::lock_guard<std::mutex> g(e->mu);
     HIPC(e, hipSetDevice(e->device));
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : e->stream;
     // pools as (hi, lo) u64 pairs in address order
@@ -1824,9 +1827,11 @@ int cls_gen_traffic_v16(cls_engine* e, const cls_traffic_spec16* sp, uint64_t fi
     if (bq) HIPC(e, hipMemcpyAsync(base + al(bp) + al(bd) + al(bl), sp->ports, bq, hipMemcpyHostToDevice, s));
     HIPC(e, launch_gen16(t, first, n, reinterpret_cast<uint4*>(src16), reinterpret_cast<uint4*>(dst16), sport, dport,
                          proto, s));
-    HIPC(e, hipStreamSynchronize(s));   // the pools are engine scratch
+    if (sync) HIPC(e, hipStreamSynchronize(s));   // the pools are engine scratch
     return CLS_OK;
 }
+
+extern "C" {
 
 int cls_compile_v4(const cls_rule* rules, uint32_t n, void* blob, uint64_t cap, uint64_t* need) {
     if ((n && !rules) || !need) return CLS_E_INVAL;

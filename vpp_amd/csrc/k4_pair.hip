@@ -120,10 +120,15 @@ __global__ __launch_bounds__(kClsBlock) void classify4_pair(Cls4Dev t, Cls4Dev o
                 base = __shfl(base, 0);
 #pragma unroll
                 for (int q = 0; q < 4; ++q)
-                    if ((m[q] >> lane) & 1u)
-                        OQ[uint64_t(blockIdx.x) * oq_seg + base + c[q] + uint32_t(__popcll(m[q] & lt))] =
-                            make_uint4(4u * g + uint32_t(q), s8[8 * h + q], d8[8 * h + q],
-                                       p8[8 * h + q] | (p8[8 * h + 4 + q] << 16));
+                    if ((m[q] >> lane) & 1u) {
+                        const uint32_t k = base + c[q] + uint32_t(__popcll(m[q] & lt));
+                        if (k < oq_seg)
+                            OQ[uint64_t(blockIdx.x) * oq_seg + k] =
+                                make_uint4(4u * g + uint32_t(q), s8[8 * h + q], d8[8 * h + q],
+                                           p8[8 * h + q] | (p8[8 * h + 4 + q] << 16));
+                        else    // the segment is full (a fixed size per workgroup): classify in place
+                            other2(s8[8 * h + q], d8[8 * h + q], p8[8 * h + q], p8[8 * h + 4 + q], w0[q], w1[q]);
+                    }
             }
             if (live[h]) {
                 OS[g] = make_uint4(w0[0], w0[1], w0[2], w0[3]);
@@ -151,7 +156,7 @@ __global__ __launch_bounds__(kClsBlock) void classify4_pair(Cls4Dev t, Cls4Dev o
     // from the queue entry (no gather from the connection arrays; the barrier
     // orders their words after the main loop's stores of the same words)
     __syncthreads();
-    const uint32_t nq = *lctr_t(q_lds);
+    const uint32_t nq = min(*lctr_t(q_lds), oq_seg);
     for (uint32_t j = threadIdx.x; j < nq; j += blockDim.x) {
         const uint4 e = OQ[uint64_t(blockIdx.x) * oq_seg + j];
         uint32_t w0, w1;
@@ -163,42 +168,42 @@ __global__ __launch_bounds__(kClsBlock) void classify4_pair(Cls4Dev t, Cls4Dev o
 
 template <int kMode, int kList, int kD>
 void launch_pair_d(const Cls4Dev& t, const Cls4Dev& o, uint32_t o_at, const Pkts4& p, const uint16_t* sport,
-                   uint32_t* out, uint64_t stride, uint32_t* oq, const LaunchCfg& cfg) {
+                   uint32_t* out, uint64_t stride, uint32_t* oq, uint32_t oq_cap, const LaunchCfg& cfg) {
     const uint32_t q_lds = ((o_at ? o_at + o.img_bytes : t.img_bytes) + 15u) & ~15u;   // the queue fill word
     const size_t lds = q_lds + 16u;
     lds_attr(reinterpret_cast<const void*>(classify4_pair<kMode, kList, kD>), lds);
     hipLaunchKernelGGL((classify4_pair<kMode, kList, kD>), dim3(cfg.grid), dim3(kClsBlock), lds, cfg.stream, t, o,
-                       o_at, p, sport, out, stride, oq, uint32_t(pair_queue_words(p.n, cfg.grid)), q_lds);
+                       o_at, p, sport, out, stride, oq, oq_cap, q_lds);
 }
 
 // sublist modes: the search depth as a template argument (the rendered
 // global tables' one-length hash, as the hot classify kernel)
 template <int kMode, int kList>
 void launch_pair(const Cls4Dev& t, const Cls4Dev& o, uint32_t o_at, const Pkts4& p, const uint16_t* sport,
-                 uint32_t* out, uint64_t stride, uint32_t* oq, const LaunchCfg& cfg) {
+                 uint32_t* out, uint64_t stride, uint32_t* oq, uint32_t oq_cap, const LaunchCfg& cfg) {
     if constexpr (kMode == 2 && (kList == 3 || kList == 4)) {
         switch (t.bv_steps) {
-        case 0: launch_pair_d<kMode, kList, 0>(t, o, o_at, p, sport, out, stride, oq, cfg); return;
-        case 1: launch_pair_d<kMode, kList, 1>(t, o, o_at, p, sport, out, stride, oq, cfg); return;
-        case 2: launch_pair_d<kMode, kList, 2>(t, o, o_at, p, sport, out, stride, oq, cfg); return;
-        case 3: launch_pair_d<kMode, kList, 3>(t, o, o_at, p, sport, out, stride, oq, cfg); return;
-        case 4: launch_pair_d<kMode, kList, 4>(t, o, o_at, p, sport, out, stride, oq, cfg); return;
-        case 5: launch_pair_d<kMode, kList, 5>(t, o, o_at, p, sport, out, stride, oq, cfg); return;
+        case 0: launch_pair_d<kMode, kList, 0>(t, o, o_at, p, sport, out, stride, oq, oq_cap, cfg); return;
+        case 1: launch_pair_d<kMode, kList, 1>(t, o, o_at, p, sport, out, stride, oq, oq_cap, cfg); return;
+        case 2: launch_pair_d<kMode, kList, 2>(t, o, o_at, p, sport, out, stride, oq, oq_cap, cfg); return;
+        case 3: launch_pair_d<kMode, kList, 3>(t, o, o_at, p, sport, out, stride, oq, oq_cap, cfg); return;
+        case 4: launch_pair_d<kMode, kList, 4>(t, o, o_at, p, sport, out, stride, oq, oq_cap, cfg); return;
+        case 5: launch_pair_d<kMode, kList, 5>(t, o, o_at, p, sport, out, stride, oq, oq_cap, cfg); return;
         default: break;
         }
     }
-    launch_pair_d<kMode, kList, -1>(t, o, o_at, p, sport, out, stride, oq, cfg);
+    launch_pair_d<kMode, kList, -1>(t, o, o_at, p, sport, out, stride, oq, oq_cap, cfg);
 }
 
 }  // namespace
 
 hipError_t launch_classify4_pair(const Cls4Dev& t, const Cls4Dev& o, uint32_t o_at, const Pkts4& p,
                                  const uint16_t* sport, uint32_t* out, uint64_t stride, uint32_t* oq,
-                                 const LaunchCfg& cfg) {
+                                 uint32_t oq_cap, const LaunchCfg& cfg) {
     if (!cls_dispatchable(t, true, false) || o.mode != 0 || o.list_mode != 0) return hipErrorInvalidValue;
     const int src = src_variant(t);
 #define PAIR_CASE(S, M, L) \
-    case 8 * S + L: launch_pair<M, L>(t, o, o_at, p, sport, out, stride, oq, cfg); break;
+    case 8 * S + L: launch_pair<M, L>(t, o, o_at, p, sport, out, stride, oq, oq_cap, cfg); break;
     switch (8 * src + int(t.list_mode)) {
         PAIR_CASE(0, 0, 0) PAIR_CASE(0, 0, 1) PAIR_CASE(0, 0, 2) PAIR_CASE(0, 0, 3) PAIR_CASE(0, 0, 4)
         PAIR_CASE(0, 0, 5) PAIR_CASE(0, 0, 6)

@@ -174,15 +174,17 @@ hipError_t launch_classify16_slots(const Cls4Dev& t, const Fe16& fe, const Pkts1
 // SYN-ACK tuple (p.dst, p.src, sport), result | slot << 2 each.  The OTHER
 // image (o, offsets rebased to LDS byte o_at) is staged beside the main one
 // when o_at != 0.  Connections of protocol > 2 go to the workgroup's
-// segment of oq (pair_queue_words entries per workgroup) and are classified
+// segment of oq (oq_cap entries per workgroup) and are classified
 // on the OTHER image after the workgroup's main loop, one per lane.
 // Needs 16-B aligned src / dst / out / out + stride, 8-B dport / sport, 4-B
 // proto; stride a multiple of 4.
 hipError_t launch_classify4_pair(const Cls4Dev& t, const Cls4Dev& o, uint32_t o_at, const Pkts4& p,
                                  const uint16_t* sport, uint32_t* out, uint64_t stride, uint32_t* oq,
-                                 const LaunchCfg& cfg);
-// the OTHER queue segment of one pair-launch workgroup (kPairBlock threads),
-// in 16-B entries: every connection its lanes visit, 4 per lane per step
+                                 uint32_t oq_cap, const LaunchCfg& cfg);
+// The OTHER queue segment of one pair-launch workgroup (kPairBlock threads)
+// that holds every connection its lanes visit, 4 per lane per step, in 16-B
+// entries; the engine caps the segment (oq_cap entries; the overflow is
+// classified in place)
 constexpr int kPairBlock = 1024;
 inline uint64_t pair_queue_words(uint64_t n, int grid) {
     const uint64_t nsteps = n / 4, nthreads = uint64_t(grid) * kPairBlock;

@@ -37,8 +37,9 @@
 
 #include "kernels.hpp"
 
+#include <map>
 #include <mutex>
-#include <unordered_map>
+#include <utility>
 
 namespace cls {
 
@@ -111,12 +112,16 @@ struct Img {
 };
 
 // A kernel's dynamic-LDS ceiling (hipFuncSetAttribute), raised when a launch
-// needs more than before: one host call per kernel and size, not per launch.
+// needs more than before: one host call per (device, kernel) and size, not
+// per launch.  The attribute is the current device's (a multi-device engine
+// launches the same kernels on every device).
 static inline void lds_attr(const void* f, size_t lds) {
     static std::mutex mu;
-    static std::unordered_map<const void*, size_t> set;
+    static std::map<std::pair<int, const void*>, size_t> set;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
     std::lock_guard<std::mutex> g(mu);
-    size_t& v = set[f];
+    size_t& v = set[{dev, f}];
     if (lds > v) {
         (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
         v = lds;

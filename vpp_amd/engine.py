@@ -56,21 +56,87 @@ class Table:
 
 
 class Engine:
-    """One gfx950 device."""
+    """One gfx950 device, or (``devices``) a multi-device engine: tables
+    compiled once and replicated, batches sharded over the devices, hit
+    counters merged by the library's RCCL all-reduce (include/contivcls.h)."""
 
-    def __init__(self, device: int = -1):
+    def __init__(self, device: int = -1, devices=None):
         L = _abi.lib()
-        cfg = _abi.Config(device)
+        if devices:
+            self._devs = (C.c_int * len(devices))(*devices)
+            cfg = _abi.Config(-1, len(devices), C.cast(self._devs, C.POINTER(C.c_int)))
+        else:
+            cfg = _abi.Config(device, 0, None)
         h = C.c_void_p()
         rc = L.cls_engine_create(C.byref(cfg), C.byref(h))
         if rc != 0:
-            raise ClsError("cls_engine_create failed (rc=%d): no usable gfx950 device" % rc)
+            raise ClsError("cls_engine_create failed (rc=%d): %s" % (
+                rc, "RCCL communicator" if rc == _abi.E_RCCL else "no usable gfx950 device"))
         self.h = h
+        self._owned = True
+
+    @classmethod
+    def _view(cls, handle) -> "Engine":
+        v = cls.__new__(cls)
+        v.h = handle
+        v._owned = False
+        return v
 
     def close(self):
-        if getattr(self, "h", None):
+        if getattr(self, "h", None) and getattr(self, "_owned", True):
             _abi.lib().cls_engine_destroy(self.h)
-            self.h = None
+        self.h = None
+
+    # -- devices, batches, the counter all-reduce (ABI 4) -------------------
+    def n_devices(self) -> int:
+        n = C.c_uint32(0)
+        self._check(_abi.lib().cls_engine_devices(self.h, C.byref(n)))
+        return n.value
+
+    def device_engine(self, index: int) -> "Engine":
+        """Borrowed single-device view of device ``index`` (timing, stream
+        floors, raw device pointers of that device)."""
+        d = C.c_void_p()
+        self._check(_abi.lib().cls_device_engine(self.h, index, C.byref(d)))
+        return Engine._view(d)
+
+    def batch(self, n: int, af: int = _abi.AF_V4, conn: bool = False, mirror: bool = False) -> "Batch":
+        return Batch(self, n, af, conn, mirror)
+
+    def classify_batch(self, table: Table, batch: "Batch", counters: bool = True, timing: bool = False,
+                       no_verdict: bool = False, force_linear: bool = False):
+        """cls_classify_batch: verdicts stay in the batch (CLS_BF_VERDICT);
+        returns the merged hit counters (uint64[R+1]) or, counters=False,
+        None after only enqueueing the work."""
+        flags = (_abi.F_TIMING if timing else 0) | (_abi.F_NO_VERDICT if no_verdict else 0) | \
+            (_abi.F_FORCE_LINEAR if force_linear else 0)
+        out = np.zeros(table.n_rules + 1, np.uint64) if counters else None
+        self._check(_abi.lib().cls_classify_batch(self.h, table.id, batch.h, _ptr(out), flags))
+        return out
+
+    def connect_batch_b(self, batch: "Batch", mode: str = "auto", count: bool = False):
+        """cls_batch_connect: ConnectionAction per connection into the batch."""
+        flags = {"auto": 0, "classifier": _abi.F_CONN_CLS, "linear": _abi.F_FORCE_LINEAR}[mode]
+        if count:
+            flags |= _abi.F_COUNT
+        self._check(_abi.lib().cls_batch_connect(self.h, batch.h, flags))
+
+    @staticmethod
+    def comm_unique_id() -> bytes:
+        buf = (C.c_uint8 * 128)()
+        rc = _abi.lib().cls_comm_unique_id(buf)
+        if rc != 0:
+            raise ClsError("cls_comm_unique_id failed (rc=%d)" % rc)
+        return bytes(buf)
+
+    def comm_init(self, n_procs: int = 1, proc: int = 0, uid: Optional[bytes] = None):
+        ib = (C.c_uint8 * 128).from_buffer_copy(uid) if uid is not None else None
+        self._check(_abi.lib().cls_comm_init(self.h, n_procs, proc, ib))
+
+    def comm_info(self):
+        n, r = C.c_uint32(0), C.c_uint32(0)
+        self._check(_abi.lib().cls_comm_info(self.h, C.byref(n), C.byref(r)))
+        return n.value, r.value
 
     def __del__(self):
         try:
@@ -347,6 +413,133 @@ class Engine:
         out = np.zeros(info.n_rules + 1, np.uint64)
         self._check(_abi.lib().cls_conn_counters(self.h, tid, _ptr(out), 1 if reset else 0))
         return out
+
+
+_BF_BYTES = {_abi.BF_SPORT: 2, _abi.BF_DPORT: 2, _abi.BF_PROTO: 1, _abi.BF_VERDICT: 1,
+             _abi.BF_SRC_IF: 4, _abi.BF_DST_IF: 4}
+_NP = {1: np.uint8, 2: np.uint16, 4: np.uint32}
+
+
+def shard_range(n: int, n_shards: int, shard: int):
+    """(first, count) of shard ``shard`` of n packets (cls_shard_range)."""
+    a, b = C.c_uint64(0), C.c_uint64(0)
+    rc = _abi.lib().cls_shard_range(n, n_shards, shard, C.byref(a), C.byref(b))
+    if rc != 0:
+        raise ClsError("cls_shard_range(%d, %d, %d): rc=%d" % (n, n_shards, shard, rc))
+    return a.value, b.value
+
+
+class Batch:
+    """An engine-owned packet (or connection) batch in HBM, sharded over the
+    engine's devices (cls_batch_*): no torch, no caller pointer kept."""
+
+    def __init__(self, engine: Engine, n: int, af: int = _abi.AF_V4, conn: bool = False, mirror: bool = False):
+        self.engine, self.n, self.af = engine, n, af
+        flags = (_abi.BATCH_CONN if conn else 0) | (_abi.BATCH_MIRROR if mirror else 0)
+        h = C.c_void_p()
+        engine._check(_abi.lib().cls_batch_create(engine.h, af, n, flags, C.byref(h)))
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None):
+            _abi.lib().cls_batch_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _elem(self, field: int) -> int:
+        return _BF_BYTES.get(field, 16 if self.af == _abi.AF_V16 else 4)
+
+    def shards(self):
+        """[(device, first, n)] per shard."""
+        k = C.c_uint32(0)
+        self.engine._check(_abi.lib().cls_batch_shards(self.h, C.byref(k)))
+        out = []
+        for g in range(k.value):
+            d, a, b = C.c_int(0), C.c_uint64(0), C.c_uint64(0)
+            self.engine._check(_abi.lib().cls_batch_shard(self.h, g, C.byref(d), C.byref(a), C.byref(b)))
+            out.append((d.value, a.value, b.value))
+        return out
+
+    def field_ptr(self, shard: int, field: int) -> int:
+        p = C.c_void_p()
+        self.engine._check(_abi.lib().cls_batch_field(self.h, shard, field, C.byref(p)))
+        return p.value
+
+    def mirror(self, field: int) -> np.ndarray:
+        """The pinned host mirror of a field (CLS_BATCH_MIRROR) as a numpy view."""
+        p = C.c_void_p()
+        self.engine._check(_abi.lib().cls_batch_mirror(self.h, field, C.byref(p)))
+        eb = self._elem(field)
+        buf = (C.c_uint8 * (self.n * eb)).from_address(p.value)
+        a = np.frombuffer(buf, np.uint8)
+        return a.reshape(-1, 16) if eb == 16 else a.view(_NP[eb])
+
+    def upload(self, field: int, arr=None, first: int = 0, n: Optional[int] = None):
+        """Packets [first, first+n) of a field from ``arr`` (None: the mirror)."""
+        eb = self._elem(field)
+        if arr is not None:
+            arr = np.ascontiguousarray(arr, np.uint8 if eb == 16 else _NP[eb])
+            n = len(arr) if n is None else n
+        n = (self.n - first) if n is None else n
+        self.engine._check(_abi.lib().cls_batch_upload(self.h, field, first, n, _ptr(arr)))
+
+    def download(self, field: int, first: int = 0, n: Optional[int] = None, mirror: bool = False):
+        n = (self.n - first) if n is None else n
+        eb = self._elem(field)
+        if mirror:
+            self.engine._check(_abi.lib().cls_batch_download(self.h, field, first, n, None))
+            return None
+        out = np.zeros((n, 16) if eb == 16 else n, np.uint8 if eb == 16 else _NP[eb])
+        self.engine._check(_abi.lib().cls_batch_download(self.h, field, first, n, _ptr(out)))
+        return out
+
+    def gen_traffic(self, spec: dict, stream_first: int = 0):
+        """The synthetic stream generated on the devices: batch packet i =
+        stream packet stream_first + i."""
+        if self.af == _abi.AF_V16:
+            ts, keep = _spec16(spec)
+            self.engine._check(_abi.lib().cls_batch_gen_traffic_v16(self.h, C.byref(ts), stream_first))
+        else:
+            ts, keep = _spec4(spec)
+            self.engine._check(_abi.lib().cls_batch_gen_traffic_v4(self.h, C.byref(ts), stream_first))
+        del keep
+
+    def counters(self, n_rules: int) -> np.ndarray:
+        out = np.zeros(n_rules + 1, np.uint64)
+        self.engine._check(_abi.lib().cls_batch_counters(self.h, _ptr(out), n_rules + 1))
+        return out
+
+    def wait(self):
+        self.engine._check(_abi.lib().cls_batch_wait(self.h))
+
+
+def _spec4(spec: dict):
+    pods = np.ascontiguousarray(spec.get("pod_ips", []), np.uint32)
+    da = np.ascontiguousarray(spec.get("dst_addrs", []), np.uint32)
+    dl = np.ascontiguousarray(spec.get("dst_lens", []), np.uint8)
+    ports = np.ascontiguousarray(spec.get("ports", []), np.uint16)
+    ts = _abi.TrafficSpec(spec["seed"], spec.get("pct_pod_src", 60), spec.get("pct_rule_dst", 50),
+                          spec.get("pct_table_port", 50), spec.get("pct_icmp", 0),
+                          pods.ctypes.data, len(pods), da.ctypes.data, dl.ctypes.data, len(da),
+                          ports.ctypes.data, len(ports))
+    return ts, (pods, da, dl, ports)
+
+
+def _spec16(spec: dict):
+    pods = np.ascontiguousarray(spec.get("pod_ips", np.zeros((0, 16))), np.uint8)
+    da = np.ascontiguousarray(spec.get("dst_addrs", np.zeros((0, 16))), np.uint8)
+    dl = np.ascontiguousarray(spec.get("dst_lens", []), np.uint8)
+    ports = np.ascontiguousarray(spec.get("ports", []), np.uint16)
+    ts = _abi.TrafficSpec16(spec["seed"], spec.get("pct_pod_src", 60), spec.get("pct_rule_dst", 50),
+                            spec.get("pct_table_port", 50), spec.get("pct_icmp", 0),
+                            pods.ctypes.data, len(pods), da.ctypes.data, dl.ctypes.data, len(da),
+                            ports.ctypes.data, len(ports))
+    return ts, (pods, da, dl, ports)
 
 
 def _ip16(ip: Optional[bytes]) -> Optional[bytes]:
