@@ -53,6 +53,10 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="CPU baseline threads (default: every core this process may use)")
     ap.add_argument("--no-stream-floor", action="store_true", help="skip the live stream-floor measurement")
+    ap.add_argument("--native", action="store_true",
+                    help="the product path through the C ABI alone: an engine-owned batch (cls_batch_*), "
+                         "cls_classify_batch, and the library's own RCCL counter all-reduce (cls_comm_init); "
+                         "torch only for the launcher's control plane (gloo), never on the GPU")
     ap.add_argument("--events", type=int, default=1, choices=[0, 1, 2],
                     help="1 (the reported line): the classify kernels stamp their own start/end events "
                          "(hipExtLaunchKernel; the step period is start-to-start); diagnostics: 2 adds an "
@@ -169,6 +173,8 @@ def main():
         sys.exit(launch_ranks(args))          # nothing has touched the GPU in this process
     if world != args.gpus:
         sys.exit("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
+    if args.native:
+        return main_native(args, rank, world, local)
     # under torch.distributed.run (also with one rank) the counters are merged
     # by a real collective; a plain N=1 run has no process group
     import torch
@@ -386,6 +392,188 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def main_native(args, rank, world, local):
+    """--native: the measured path as a cgo host runs it -- no torch tensor,
+    stream or collective touches the GPU.  Per rank: one engine on its GPU,
+    the table compiled and uploaded (cls_table_put), an engine-owned batch
+    generated in HBM (cls_batch_gen_traffic_v4, rank r's packets [r N,
+    (r+1) N) of the stream), and per step one cls_classify_batch: the
+    classify kernels on the engine stream, then the library's ncclAllReduce
+    of the hit counters on its side stream, overlapping the next step (two
+    counter buffers alternate).  Under torch.distributed.run the ranks join
+    one RCCL communicator (cls_comm_init with rank 0's id, exchanged over a
+    gloo group that also carries the barriers and max-over-ranks); a plain
+    N=1 run has no communicator."""
+    import ctypes as C
+
+    dist = None
+    if "WORLD_SIZE" in os.environ:
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+    else:
+        os.environ["CONTIVCLS_NO_TORCH"] = "1"     # a plain N=1 run: torch is never imported
+    from vpp_amd import _abi, workload
+    from vpp_amd.engine import Engine
+
+    def max_over(vals):
+        if dist is None:
+            return vals
+        import torch
+        t = torch.tensor(vals, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return [float(x) for x in t]
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    acl, spec, n_default = workload.config(args.config)
+    strong = args.config == 4
+    n = args.packets or (-(-n_default // world) if strong else n_default)
+    af = spec.get("layout", 4)
+    eng = Engine(local)                        # one rank per GPU (RCCL: one rank per device)
+    if dist is not None:
+        uid = [Engine.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        eng.comm_init(world, rank, uid[0])
+    table = eng.put_table("contiv/vpp-policy-GLOBAL", acl.rules)
+    info = table.info()
+    R = table.n_rules
+    b = eng.batch(n, af=af)
+    b.gen_traffic(spec, rank * n)
+    b.wait()
+
+    def step(timing):
+        eng.classify_batch(table, b, counters=False, timing=timing)
+
+    i = 0
+    t_settle = time.perf_counter()
+    while True:
+        for _ in range(8):
+            step(False)
+            i += 1
+        b.wait()
+        short = (time.perf_counter() - t_settle) * 1e3 < args.settle_ms
+        if not max_over([1.0 if short else 0.0])[0]:
+            break
+    settle_ms = (time.perf_counter() - t_settle) * 1e3
+    for _ in range(args.warmup):
+        step(False)
+    b.wait()
+    eng.kernel_times(reset=True)
+    barrier()
+    b.wait()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(args.events >= 1)
+    t_submit = time.perf_counter() - t0
+    b.wait()                                   # every kernel and the last all-reduce
+    barrier()
+    wall = time.perf_counter() - t0
+    kms, starts = eng.kernel_times(reset=True, starts=True)
+    counters = b.counters(R)
+    avg_k = float(np.mean(kms)) if kms else float("nan")
+    med_k = float(np.median(kms)) if kms else float("nan")
+    periods = list(np.diff(starts)) if len(starts) > 1 else []
+    med_step = float(np.median(periods)) if periods else float("nan")
+    # the stream floor over the batch's own device arrays
+    shapes = []
+    lds = info["lds_bytes"] if af == 4 else info["lds_bytes_v16"]
+    resident = info["lds_resident"] if af == 4 else info["lds_resident_v16"]
+    two_per_cu = not resident or 2 * (lds + 16) <= 160 * 1024
+    floor_ms = shape_ms = None
+    if not args.no_stream_floor:
+        m = min(n, 1 << 30)
+        m -= m % (256 if af == 16 else 4)
+        p = lambda f: b.field_ptr(0, f)  # noqa: E731
+        if af == 16:
+            pk = _abi.PktSoa(_abi.AF_V16, None, None, p(_abi.BF_SRC), p(_abi.BF_DST), None, p(_abi.BF_DPORT),
+                             p(_abi.BF_PROTO))
+        else:
+            pk = _abi.PktSoa(_abi.AF_V4, p(_abi.BF_SRC), p(_abi.BF_DST), None, None, None, p(_abi.BF_DPORT),
+                             p(_abi.BF_PROTO))
+        ms = (C.c_float * 8)()
+        cnt = C.c_uint32(0)
+        eng._check(_abi.lib().cls_stream_floor_shapes(eng.h, C.byref(pk), m, p(_abi.BF_VERDICT), 10, ms, 8,
+                                                       C.byref(cnt), None))
+        shapes = [ms[k] * (n / m) for k in range(cnt.value)]
+        floor_ms = min(shapes)
+        shape_ms = min(t for k, t in enumerate(shapes) if (k & 1) == int(two_per_cu) or len(shapes) < 2)
+    wall, k_max, kmed_max = max_over([wall, avg_k, med_k])
+    if floor_ms is not None:
+        floor_ms, shape_ms = max_over([floor_ms, shape_ms])
+    ok_sum = int(counters.sum()) == n * world
+    if rank == 0:
+        total = n * world * args.steps
+        mpps = total / wall / 1e6
+        alg_bytes = n * BYTES_PER_PKT[af] + (R + 1) * 8
+        achieved = alg_bytes / (avg_k / 1e3) / 1e9
+        traffic, traffic_src = pmc_traffic(args.config, n)
+        cpu = None
+        if world == 1 and args.cpu_sample:
+            cpu = cpu_baseline(acl, spec, args.cpu_sample, args.faithful_sample, args.cpu_threads)
+        if af == 4:
+            wl = "config%d: %d-rule global ACL (%d pods), %d IPv4 TCP/UDP packets per GPU" % (
+                args.config, R, len(spec["pod_ips"]), n)
+            if strong:
+                wl += " (%d-packet batch sharded over %d GPU%s)" % (n * world, world, "s" if world > 1 else "")
+        else:
+            wl = ("config%d: %d-rule global ACL (%d pods, half IPv6, dst port ranges), %d mixed IPv4/IPv6 "
+                  "packets per GPU (10%% ICMP)" % (args.config, R, len(spec["pod_ips"]), n))
+        comm = eng.comm_info()
+        line = {
+            "metric": "Mpps classified at 10k ACL rules, 1/8 GPU; % of HBM roofline",
+            "value": round(mpps, 2),
+            "unit": "Mpps",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(wall / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "strong" if strong else "weak",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic (splitmix64 stream generated in HBM, seed %#x; rules rendered from a "
+                    "synthetic 1000-pod policy set)" % spec["seed"],
+            "config": {"workload": wl,
+                       "rules": R, "packets_per_gpu": n,
+                       "layout": "IPv4 SoA, 12 B/packet" if af == 4 else "16-byte address SoA, 36 B/packet",
+                       "kernel": "classifier" if info["kernel"] == 1 else "linear",
+                       "lds_bytes": lds, "lds_resident": resident,
+                       "parallelism": "dp%d" % world,
+                       "path": "native: C ABI only (cls_batch_*, cls_classify_batch), no torch on the GPU",
+                       "collective": ("counter all-reduce in the library: ncclAllReduce u64 sum over %d RCCL "
+                                      "ranks (cls_comm_init), %d B, side stream overlapping the next step's "
+                                      "classify" % (comm[0], (R + 1) * 8)) if comm[0] else None},
+            "counters_sum_ok": ok_sum,
+            "settle_ms": round(settle_ms, 1),
+            "step_ms_median": round(med_step, 4),
+            "host_submit_ms_per_step": round(t_submit * 1e3 / max(1, args.steps), 4),
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                         "traffic": traffic, "traffic_source": traffic_src,
+                         "kernel_ms_avg": round(avg_k, 4),
+                         "kernel_ms_median": round(med_k, 4),
+                         "kernel_ms_avg_max_rank": round(k_max, 4),
+                         "kernel_ms_median_max_rank": round(kmed_max, 4),
+                         "stream_floor_ms": round(floor_ms, 4) if floor_ms is not None else None,
+                         "frac_of_stream_floor": round(floor_ms / avg_k, 4) if floor_ms else None,
+                         "stream_floor_launch_shape_ms": round(shape_ms, 4) if shape_ms else None,
+                         "stream_floor_shapes_ms": [round(t, 4) for t in shapes],
+                         "launch_shape": "%d x 1024-thread workgroups per CU" % (2 if two_per_cu else 1),
+                         "frac_of_launch_shape_floor": round(shape_ms / avg_k, 4) if shape_ms else None,
+                         "algorithmic_bytes_per_launch": alg_bytes},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    b.close()
+    eng.close()
+    if dist is not None:
+        dist.destroy_process_group()
+    if not ok_sum:
+        sys.exit("bench.py --native: the merged counters do not sum to the packets of all ranks")
 
 
 if __name__ == "__main__":

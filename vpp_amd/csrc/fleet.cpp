@@ -19,6 +19,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 
@@ -170,6 +171,7 @@ struct BatchShard {
     uint64_t first = 0, n = 0;         // its packets [first, first + n) of the batch
     DevBuf mem;                        // every field's array
     size_t off[CLS_BF_COUNT] = {};     // byte offsets in mem (256-B aligned)
+    DevBuf fmem[CLS_BF_COUNT];         // CONTIVCLS_BATCH_LAYOUT=1 (measurement): one allocation per field
     // the hit counters of the last two classify calls (u64, R + 1): a
     // buffer is written again only after its all-reduce has finished
     DevBuf ctr[2];
@@ -214,6 +216,7 @@ void shard_of(uint64_t n, uint32_t G, uint32_t g, uint64_t& first, uint64_t& cou
 
 template <typename T>
 T* fld(const BatchShard& s, uint32_t f) {
+    if (s.fmem[f].p) return static_cast<T*>(s.fmem[f].p);
     return reinterpret_cast<T*>(static_cast<uint8_t*>(s.mem.p) + s.off[f]);
 }
 
@@ -319,11 +322,16 @@ int read_counters(cls_batch* b, std::vector<uint64_t>& out) {
         BatchShard& s = b->sh[i];
         cls_engine* d = s.d;
         HIPC(e, hipSetDevice(d->device));
-        int rc = side_stream(d);
-        if (rc != CLS_OK) return relay(e, d, rc);
-        HIPC(e, hipStreamWaitEvent(d->coll, b->reduced ? s.reduced[k] : s.classified[k], 0));
-        HIPC(e, hipMemcpyAsync(h.data(), s.ctr[k].p, size_t(b->n_ctr) * 8, hipMemcpyDeviceToHost, d->coll));
-        HIPC(e, hipStreamSynchronize(d->coll));
+        if (b->reduced) {                        // behind the all-reduce, on its stream
+            int rc = side_stream(d);
+            if (rc != CLS_OK) return relay(e, d, rc);
+            HIPC(e, hipStreamWaitEvent(d->coll, s.reduced[k], 0));
+            HIPC(e, hipMemcpyAsync(h.data(), s.ctr[k].p, size_t(b->n_ctr) * 8, hipMemcpyDeviceToHost, d->coll));
+            HIPC(e, hipStreamSynchronize(d->coll));
+        } else {                                 // behind the classify, on the engine stream
+            HIPC(e, hipMemcpyAsync(h.data(), s.ctr[k].p, size_t(b->n_ctr) * 8, hipMemcpyDeviceToHost, d->stream));
+            HIPC(e, hipStreamSynchronize(d->stream));
+        }
         for (size_t r = 0; r < h.size(); ++r) out[r] += h[r];
     }
     return CLS_OK;
@@ -490,14 +498,28 @@ int cls_batch_create(cls_engine* e, uint32_t af, uint64_t n, uint32_t flags, cls
         BatchShard& s = b->sh[gi];
         s.d = dev_engine(e, gi);
         shard_of(n, G, gi, s.first, s.n);
+        // One allocation; array f starts a further (f + 1) x 4352 B (4 KiB +
+        // 256 B) past the previous one's 256-B aligned end, so the fields'
+        // streams do not walk the same HBM channels in step: config 3's
+        // kernel 0.550-0.552 ms against 0.564-0.566 ms packed back to back
+        // and 0.553-0.560 ms with one allocation per field
+        // (profiles/r05c_batch_layout_ab.txt).
+        // CONTIVCLS_BATCH_LAYOUT (measurement): 0 packed, 1 per field.
+        const char* lay = std::getenv("CONTIVCLS_BATCH_LAYOUT");
+        const int layout = lay ? std::atoi(lay) : 2;
         size_t at = 0;
+        HIPC(e, hipSetDevice(s.d->device));
         for (uint32_t f = 0; f < CLS_BF_COUNT; ++f) {
             if (!b->has(f)) continue;
+            const size_t bytes = al(s.n * field_bytes(af, f) + 256);   // + 256: whole 16-B groups past the end
+            if (layout == 1) {
+                HIPC(e, s.fmem[f].ensure(bytes));
+                continue;
+            }
             s.off[f] = at;
-            at += al(s.n * field_bytes(af, f) + 256);      // + 256: whole 16-B groups past the end
+            at += bytes + (layout == 2 ? 4352 * size_t(f + 1) : 0);
         }
-        HIPC(e, hipSetDevice(s.d->device));
-        HIPC(e, s.mem.ensure(at));
+        if (layout != 1) HIPC(e, s.mem.ensure(at));
         for (int k = 0; k < 2; ++k) {
             HIPC(e, hipEventCreateWithFlags(&s.classified[k], hipEventDisableTiming));
             HIPC(e, hipEventCreateWithFlags(&s.reduced[k], hipEventDisableTiming));
@@ -539,6 +561,11 @@ void cls_batch_destroy(cls_batch* b) {
                 (void)hipFree(s.mem.p);
                 s.mem.p = nullptr;
             }
+            for (DevBuf& m : s.fmem)
+                if (m.p) {
+                    (void)hipFree(m.p);
+                    m.p = nullptr;
+                }
         }
         if (b->mirror) (void)hipHostFree(b->mirror);
     }
@@ -643,8 +670,11 @@ int cls_classify_batch(cls_engine* e, uint32_t table_id, cls_batch* b, uint64_t*
         const int rc = classify_locked(d, table_id, &p, s.n, fld<uint8_t>(s, CLS_BF_VERDICT),
                                        s.ctr[k].as<uint64_t>(), pass | CLS_F_DEVICE, d->stream);
         if (rc != CLS_OK) return relay(e, d, rc);
-        HIPC(e, hipEventRecord(s.classified[k], d->stream));
-        s.rec_cls[k] = true;
+        // the all-reduce's dependency (an event record costs the stream a
+        // few microseconds: without a communicator the readers synchronise
+        // the stream instead)
+        if (comm) HIPC(e, hipEventRecord(s.classified[k], d->stream));
+        s.rec_cls[k] = comm;
     }
     if (comm) {
         // every device's counters summed in place over xGMI (and over the
