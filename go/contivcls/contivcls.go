@@ -71,14 +71,39 @@ type podConfig struct {
 // New replaces NewMockACLEngine (aclengine_mock.go:124).  device: HIP device
 // ordinal, -1 for the current one.
 func New(c contiv.API, device int) (*Engine, error) {
+	return NewMulti(c, []int{device})
+}
+
+// NewMulti: one engine over several devices (SURVEY 8(e)).  Every table is
+// compiled once and replicated to every device; Batch packets shard over the
+// devices; over distinct devices the hit counters of ClassifyBatchDevice are
+// merged by the library's RCCL all-reduce over xGMI.
+func NewMulti(c contiv.API, devices []int) (*Engine, error) {
 	// the library this binding was written against (include/contivcls.h)
 	if v := C.cls_abi_version(); v != C.CLS_ABI_VERSION {
 		return nil, fmt.Errorf("contivcls: library ABI %d, binding ABI %d", int(v), int(C.CLS_ABI_VERSION))
 	}
+	if len(devices) == 0 {
+		return nil, errors.New("contivcls: no device")
+	}
 	var e *C.cls_engine
 	var cfg C.cls_config
-	cfg.device = C.int(device)
-	if rc := C.cls_engine_create(&cfg, &e); rc != C.CLS_OK {
+	cfg.device = C.int(devices[0])
+	if len(devices) > 1 {
+		// the device list lives in C memory for the call (cfg is Go memory)
+		dl := (*[1 << 10]C.int)(C.malloc(C.size_t(len(devices)) * C.size_t(unsafe.Sizeof(C.int(0)))))[:len(devices):len(devices)]
+		defer C.free(unsafe.Pointer(&dl[0]))
+		for i, d := range devices {
+			dl[i] = C.int(d)
+		}
+		cfg.n_devices = C.uint32_t(len(devices))
+		cfg.devices = &dl[0]
+	}
+	switch rc := C.cls_engine_create(&cfg, &e); rc {
+	case C.CLS_OK:
+	case C.CLS_E_RCCL:
+		return nil, errors.New("contivcls: RCCL communicator over the devices failed")
+	default:
 		return nil, errors.New("contivcls: no usable gfx950 device")
 	}
 	return &Engine{e: e, Contiv: c, pods: map[podmodel.ID]*podConfig{},
@@ -697,4 +722,161 @@ func pinAll(p *runtime.Pinner, ptrs ...interface{}) {
 	for _, x := range ptrs {
 		p.Pin(x)
 	}
+}
+
+// ---- HBM-resident batches (ABI 4) -------------------------------------------
+// A Batch is engine-owned memory: packets stay in HBM between calls and no
+// Go pointer is ever kept by the library (cgo rule).  With mirror the batch
+// also owns pinned host arrays (Mirror*) that Go fills in place; Upload(f,
+// nil) then moves them at DMA speed.
+
+// Batch fields (CLS_BF_*).
+const (
+	FieldSrc     = uint32(C.CLS_BF_SRC)
+	FieldDst     = uint32(C.CLS_BF_DST)
+	FieldSport   = uint32(C.CLS_BF_SPORT)
+	FieldDport   = uint32(C.CLS_BF_DPORT)
+	FieldProto   = uint32(C.CLS_BF_PROTO)
+	FieldVerdict = uint32(C.CLS_BF_VERDICT)
+	FieldSrcIf   = uint32(C.CLS_BF_SRC_IF)
+	FieldDstIf   = uint32(C.CLS_BF_DST_IF)
+)
+
+type Batch struct {
+	en *Engine
+	b  *C.cls_batch
+	N  int
+	V6 bool
+}
+
+// NewBatch: n IPv4 (v6 false: host-order u32 addresses) or 16-byte packets;
+// conn adds interface ids (ConnectBatchDevice).
+func (en *Engine) NewBatch(n int, v6, conn, mirror bool) (*Batch, error) {
+	en.Lock()
+	defer en.Unlock()
+	af := C.uint32_t(C.CLS_AF_V4)
+	if v6 {
+		af = C.CLS_AF_V16
+	}
+	fl := C.uint32_t(0)
+	if conn {
+		fl |= C.CLS_BATCH_CONN
+	}
+	if mirror {
+		fl |= C.CLS_BATCH_MIRROR
+	}
+	var b *C.cls_batch
+	if rc := C.cls_batch_create(en.e, af, C.uint64_t(n), fl, &b); rc != C.CLS_OK {
+		return nil, en.lastErr()
+	}
+	return &Batch{en: en, b: b, N: n, V6: v6}, nil
+}
+
+// Close frees the batch (before its engine).
+func (b *Batch) Close() {
+	if b.b != nil {
+		C.cls_batch_destroy(b.b)
+		b.b = nil
+	}
+}
+
+// MirrorU32 / MirrorU16 / MirrorU8: the pinned host array of a field (C
+// memory: Go may keep and fill these slices).
+func (b *Batch) MirrorU32(f uint32) []uint32 {
+	var p unsafe.Pointer
+	C.cls_batch_mirror(b.b, C.uint32_t(f), &p)
+	return unsafe.Slice((*uint32)(p), b.N)
+}
+func (b *Batch) MirrorU16(f uint32) []uint16 {
+	var p unsafe.Pointer
+	C.cls_batch_mirror(b.b, C.uint32_t(f), &p)
+	return unsafe.Slice((*uint16)(p), b.N)
+}
+func (b *Batch) MirrorU8(f uint32) []uint8 {
+	var p unsafe.Pointer
+	C.cls_batch_mirror(b.b, C.uint32_t(f), &p)
+	return unsafe.Slice((*uint8)(p), b.N)
+}
+
+// Upload packets [first, first+n) of a field from src (a Go slice of the
+// field's element type, pinned for the call), or from the mirror (src nil).
+func (b *Batch) Upload(f uint32, first, n int, src unsafe.Pointer) error {
+	if rc := C.cls_batch_upload(b.b, C.uint32_t(f), C.uint64_t(first), C.uint64_t(n), src); rc != C.CLS_OK {
+		return b.en.lastErr()
+	}
+	return nil
+}
+
+// Verdicts of packets [first, first+n) (waits for the batch's work).
+func (b *Batch) Verdicts(first, n int) ([]uint8, error) {
+	out := make([]uint8, n)
+	if n == 0 {
+		return out, nil
+	}
+	if rc := C.cls_batch_download(b.b, C.CLS_BF_VERDICT, C.uint64_t(first), C.uint64_t(n),
+		unsafe.Pointer(&out[0])); rc != C.CLS_OK {
+		return nil, b.en.lastErr()
+	}
+	return out, nil
+}
+
+// ClassifyBatchDevice: evalACL over the whole batch on its devices; the hit
+// counters summed over the shards (and over processes, CommInit).  wait
+// false only enqueues (Counters reads the last call's).
+func (en *Engine) ClassifyBatchDevice(t *Table, b *Batch, wait bool) ([]uint64, error) {
+	var out []uint64
+	var op *C.uint64_t
+	if wait {
+		out = make([]uint64, t.NRules+1)
+		op = (*C.uint64_t)(&out[0])
+	}
+	if rc := C.cls_classify_batch(en.e, C.uint32_t(t.ID), b.b, op, 0); rc != C.CLS_OK {
+		return nil, en.lastErr()
+	}
+	return out, nil
+}
+
+// Counters of the batch's last ClassifyBatchDevice.
+func (b *Batch) Counters(t *Table) ([]uint64, error) {
+	out := make([]uint64, t.NRules+1)
+	if rc := C.cls_batch_counters(b.b, (*C.uint64_t)(&out[0]), C.uint32_t(len(out))); rc != C.CLS_OK {
+		return nil, b.en.lastErr()
+	}
+	return out, nil
+}
+
+// ConnectBatchDevice: testConnection over a conn batch (ConnectionAction per
+// connection into FieldVerdict).
+func (en *Engine) ConnectBatchDevice(b *Batch, count bool) error {
+	fl := C.uint32_t(0)
+	if count {
+		fl |= C.CLS_F_COUNT
+	}
+	if rc := C.cls_batch_connect(en.e, b.b, fl); rc != C.CLS_OK {
+		return en.lastErr()
+	}
+	return nil
+}
+
+// CommUniqueID / CommInit: one process per GPU (or GPU group) joins one RCCL
+// communicator for the counter merge; process 0 makes the id, the others get
+// it out of band.
+func CommUniqueID() ([128]byte, error) {
+	var id [128]byte
+	if rc := C.cls_comm_unique_id(unsafe.Pointer(&id[0])); rc != C.CLS_OK {
+		return id, errors.New("contivcls: RCCL unavailable")
+	}
+	return id, nil
+}
+
+func (en *Engine) CommInit(nProcs, proc int, id *[128]byte) error {
+	var p unsafe.Pointer
+	if id != nil {
+		p = C.CBytes(id[:])
+		defer C.free(p)
+	}
+	if rc := C.cls_comm_init(en.e, C.uint32_t(nProcs), C.uint32_t(proc), p); rc != C.CLS_OK {
+		return en.lastErr()
+	}
+	return nil
 }
