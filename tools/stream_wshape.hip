@@ -37,7 +37,7 @@ __device__ __forceinline__ uint32_t mix(uint4 s, uint4 d, uint2 dp, uint32_t pr)
 
 // S4 / RO: grid-stride over 4-packet groups (store = 0: only when m == magic,
 // which the host never makes true)
-template <int kStore>
+template <int kStore>   // 1: every group; 0: none; -4 / -16: one group in 4 / 16 (a quarter / sixteenth of the bytes)
 __global__ __launch_bounds__(1024) void s4_kernel(const uint4* S, const uint4* D, const uint2* DP, const uint32_t* PR,
                                                   uint32_t* V, uint32_t ngroups, uint32_t magic) {
     const uint32_t nthreads = gridDim.x * blockDim.x;
@@ -52,7 +52,13 @@ __global__ __launch_bounds__(1024) void s4_kernel(const uint4* S, const uint4* D
         const uint32_t pr = PR[g];
         __builtin_amdgcn_sched_barrier(0);
         const uint32_t m = mix(s, d, dp, pr);
-        if (kStore || m == magic) __builtin_nontemporal_store(m, V + g);
+        // -4 / -16: sparse lanes (partial lines); -104 / -116: whole wave
+        // instructions of one wave step in 4 / 16 (full lines, a quarter /
+        // sixteenth of the bytes)
+        const bool st = kStore == 1 ? true : kStore == 0 ? false
+                        : kStore > -100 ? (g & uint32_t(-kStore - 1)) == 0u
+                                        : ((g >> 6) & uint32_t(-kStore - 101)) == 0u;
+        if (st || m == magic) __builtin_nontemporal_store(m, V + g);
     }
 }
 
@@ -176,15 +182,10 @@ int main() {
     for (int round = 0; round < 2; ++round) {
         timed("S4", b12, true, [&] { s4_kernel<1><<<ncu, 1024>>>(src, dst, dp, pr, v, G, 0); });
         timed("RO", b11, false, [&] { s4_kernel<0><<<ncu, 1024>>>(src, dst, dp, pr, v, G, 0xFFFFFFFFu); });
-        timed("S4C", b12, true, [&] { chunk_kernel<0><<<ncu, 1024>>>(src, dst, dp, pr, v, nch); });
-        timed("S16L", b12, true, [&] { chunk_kernel<1><<<ncu, 1024>>>(src, dst, dp, pr, v, nch); });
-        timed("S16L-d", b12, true, [&] { chunk_kernel<2><<<ncu, 1024>>>(src, dst, dp, pr, v, nch); });
-        timed("B0", b12, true, [&] { s4b_kernel<0><<<ncu, 1024>>>(src, dst, dp, pr, v, G); });
-        timed("B2 nt", b12, true, [&] { s4b_kernel<2><<<ncu, 1024>>>(src, dst, dp, pr, v, G); });
-        timed("B3 sc0nt", b12, true, [&] { s4b_kernel<3><<<ncu, 1024>>>(src, dst, dp, pr, v, G); });
-        timed("B16 sc1", b12, true, [&] { s4b_kernel<16><<<ncu, 1024>>>(src, dst, dp, pr, v, G); });
-        timed("B18 sc1nt", b12, true, [&] { s4b_kernel<18><<<ncu, 1024>>>(src, dst, dp, pr, v, G); });
-        timed("B19 all", b12, true, [&] { s4b_kernel<19><<<ncu, 1024>>>(src, dst, dp, pr, v, G); });
+        timed("S4/4", b11 + double(N) / 4, false, [&] { s4_kernel<-4><<<ncu, 1024>>>(src, dst, dp, pr, v, G, 0xFFFFFFFFu); });
+        timed("S4/16", b11 + double(N) / 16, false, [&] { s4_kernel<-16><<<ncu, 1024>>>(src, dst, dp, pr, v, G, 0xFFFFFFFFu); });
+        timed("W4 full", b11 + double(N) / 4, false, [&] { s4_kernel<-104><<<ncu, 1024>>>(src, dst, dp, pr, v, G, 0xFFFFFFFFu); });
+        timed("W16 full", b11 + double(N) / 16, false, [&] { s4_kernel<-116><<<ncu, 1024>>>(src, dst, dp, pr, v, G, 0xFFFFFFFFu); });
     }
     return 0;
 }

@@ -29,12 +29,13 @@ using namespace cls;
 // OTHER queue (protocols > 2 deferred to the finish launch): per workgroup
 // room for 1/16 of its packets, at most 16 Ki entries (64 KiB per workgroup:
 // the queue exists per (table, stream), and a full segment classifies in
-// place, so a cap costs only speed on batches with > 6 % protocol > 2).
-// CONTIVCLS_OTHER_CAP: tests, to reach the in-place path.
+// place, so a cap costs only speed on batches with > 6 % protocol > 2),
+// split into one segment per wave (kOtherSegs): the entries per segment.
+// CONTIVCLS_OTHER_CAP (per workgroup): tests, to reach the in-place path.
 static uint32_t other_cap(uint64_t n, int grid) {
-    if (const char* c = std::getenv("CONTIVCLS_OTHER_CAP")) return uint32_t(std::strtoul(c, nullptr, 0));
+    if (const char* c = std::getenv("CONTIVCLS_OTHER_CAP")) return uint32_t(std::strtoul(c, nullptr, 0)) / kOtherSegs;
     const uint64_t want = (n / uint64_t(std::max(grid, 1)) + 15) / 16;
-    return uint32_t(std::min<uint64_t>(16384, std::max<uint64_t>(1024, want)));
+    return uint32_t(std::min<uint64_t>(16384, std::max<uint64_t>(1024, want))) / kOtherSegs;
 }
 
 static int acl_put_locked(cls_engine* e, const char* acl_name, const cls_rule* rules, uint32_t n_rules,
@@ -538,7 +539,7 @@ static int scratch_of(cls_engine* e, Counters& c, uint32_t n_rules, hipStream_t 
 
 // The OTHER queue of a launch of `grid` workgroups with segments of `cap`.
 static int other_queue(cls_engine* e, Scratch* sc, int grid, uint32_t cap, hipStream_t s, uint32_t** out) {
-    const size_t need = (size_t(grid) + size_t(grid) * cap) * 4;
+    const size_t need = (size_t(grid) * kOtherSegs * (1 + size_t(cap))) * 4;
     if (need > sc->oq.bytes) {
         HIPC(e, hipStreamSynchronize(s));       // earlier launches on this stream may still read it
         HIPC(e, sc->oq.ensure(need));

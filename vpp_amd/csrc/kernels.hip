@@ -116,7 +116,7 @@ constexpr uint32_t kOtherLds = 4096;   // finish launch: LDS histogram of the OT
 // (rows w, w + 16, ...: 256 contiguous bytes per load instruction), wave 0
 // adds the slot's global counter and moves the total to its rule (hot rules:
 // summed in LDS over the tile first, one atomic per tile).  Blocks after:
-// one OTHER queue row each (the packets one classify workgroup queued),
+// one classify workgroup's OTHER queue segments each (its waves' packets),
 // every lane on one packet, counted per rule in LDS (compact rule indices)
 // and added once per (block, rule).  No block waits for another: the OTHER
 // packets are counted straight into their rules, the tiles read only what
@@ -172,7 +172,13 @@ __device__ __forceinline__ void finish_body(const FinishArgs& f, const Cls4Dev& 
     }
     const uint32_t r = blockIdx.x - ntile;
     if (!f.oq || r >= f.oq_rows) return;
-    const uint32_t n = f.oq[r];
+    // the classify workgroup's kOtherSegs wave segments, taken as one list
+    uint32_t cnt[kOtherSegs], n = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < kOtherSegs; ++w) {
+        cnt[w] = f.oq[r * kOtherSegs + w];
+        n += cnt[w];
+    }
     if (n == 0) return;                          // the usual case: no OTHER packet in this row
     const bool lds = f.n_orules <= kOtherLds;
     if (lds) {
@@ -182,7 +188,9 @@ __device__ __forceinline__ void finish_body(const FinishArgs& f, const Cls4Dev& 
     const Img<false> oim{reinterpret_cast<const uint8_t*>(o.img)};
     const uint32_t* orule = f.other_map + f.n_other;
     for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
-        const uint32_t k = f.oq[f.oq_rows + r * f.oq_cap + i];
+        uint32_t w = 0, at = i;
+        while (at >= cnt[w]) at -= cnt[w++];     // i < n: stops inside a non-empty segment
+        const uint32_t k = f.oq[f.oq_rows * kOtherSegs + (r * kOtherSegs + w) * f.oq_cap + at];
         uint32_t s1[1], d1[1], p1[1];
         load(k, s1[0], d1[0], p1[0]);
         const uint32_t z1[1] = {0u};

@@ -71,7 +71,7 @@ struct Cls4Dev {
     uint32_t n_lctr;           // LDS-resident image: slots [0, n_lctr) counted in LDS, the rest in gslot
     uint32_t ctr16;            // LDS counters are u16 (compile.hpp counter tiers)
     uint32_t* part;            // LDS-resident image: per-workgroup slot counters [grid][n_lctr]
-    uint32_t* oq;              // OTHER queue {fill per workgroup, segments of oq_cap indices}
+    uint32_t* oq;              // OTHER queue {fill per wave, a segment of oq_cap indices per wave}
                                // (null: classify such packets in place)
     uint32_t oq_cap;
     unsigned long long* zero = nullptr;   // the call's rule counters, cleared by the launch's
@@ -128,6 +128,7 @@ hipError_t launch_remap(unsigned long long* slot_val, const uint2* csr, uint32_t
 // summed per tile in LDS -- then their n_hot rule ids) and clear slot_val;
 // without remap (an earlier chunk of a long batch) slot_val += partials.
 // out must be cleared before (the classify launch's zero).
+constexpr uint32_t kOtherSegs = 16;   // OTHER queue segments per classify workgroup (its waves)
 constexpr uint32_t kHotRule = 0x80000000u;
 constexpr uint32_t kMaxHotRules = 64;
 struct FinishArgs {
@@ -139,10 +140,12 @@ struct FinishArgs {
     uint32_t n_hot;
     unsigned long long* out;
     bool remap;
-    // the OTHER queue of the classify launch (rows = its workgroups; null:
-    // none): blocks after the tiles classify the queued packets (protocols
-    // > 2) on the OTHER image and count them per rule -- other_map: compact
-    // rule index of each of the n_other OTHER slots, then the n_orules rules
+    // the OTHER queue of the classify launch (null: none): oq_rows (its
+    // workgroups) x kOtherSegs fills, then as many segments of oq_cap
+    // entries, one per classify wave; blocks after the tiles classify a
+    // workgroup's queued packets (protocols > 2) on the OTHER image and count
+    // them per rule -- other_map: compact rule index of each of the n_other
+    // OTHER slots, then the n_orules rules
     const uint32_t* oq;
     uint32_t oq_rows, oq_cap;
     const uint32_t* other_map;

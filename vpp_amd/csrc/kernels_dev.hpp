@@ -488,13 +488,17 @@ __device__ __forceinline__ void wave_count_cold(unsigned long long* gslot, uint3
 // packets are queued for the finish launch (counting) or classified on the
 // OTHER image `o` in place (slot mode, full queue) from sl(q): packet q's
 // source, or on the 16-byte path its rep -- computed only for those.
+// The OTHER queue row of this wave, and the first entry after the fills.
+__device__ __forceinline__ uint32_t queue_row() { return blockIdx.x * kOtherSegs + (threadIdx.x >> 6); }
+__device__ __forceinline__ uint32_t queue_row0() { return gridDim.x * kOtherSegs; }
+
 template <int N, bool kLds, int kMode, int kList, int kD, int kCtr, typename SrcOf>
 __device__ __forceinline__ void run_n(const Img<kLds>& im, const Cls4Dev& t, const Cls4Dev& o, uint32_t hot_lane,
                                       unsigned long long* gslot, uint32_t& hot0,
                                       const uint32_t (&s)[N], const uint32_t (&d)[N],
                                       const uint32_t (&dp)[N], const uint32_t (&pr)[N],
                                       bool pr_any, uint32_t (&res)[N], const SrcOf& sl,
-                                      const uint32_t (&idx)[N], uint32_t oq_lds) {
+                                      const uint32_t (&idx)[N], uint32_t oq_lds, uint32_t& wq) {
     uint32_t slot[N];
     classify_n<N, kLds, kMode, kList, kD>(im, t, s, d, dp, pr, res, slot);
     // One LDS atomic per packet, no branch.  Hot slots (< n_hot: default DENY
@@ -570,8 +574,8 @@ __device__ __forceinline__ void run_n(const Img<kLds>& im, const Cls4Dev& t, con
     // Protocols outside TCP/UDP/ICMP fall through evalACL's switch
     // (aclengine_mock.go:508-664): networks alone decide.  Rare; taken per
     // wave only when some lane holds such a packet.  Such a packet's index
-    // goes to the OTHER queue (t.oq: count, then indices), which other_kernel
-    // classifies on the OTHER image after this launch (verdict and count);
+    // goes to its wave's segment of the OTHER queue (t.oq), which the finish
+    // launch classifies on the OTHER image after this launch (verdict, count);
     // when the queue is full, here and now (the OTHER image's interval
     // search and candidate scan from global memory, its slots after the main
     // image's).
@@ -586,13 +590,10 @@ __device__ __forceinline__ void run_n(const Img<kLds>& im, const Cls4Dev& t, con
             m[q] = __ballot(pr[q] > 2u);
             pre[q + 1] = pre[q] + uint32_t(__popcll(m[q]));
         }
-        uint32_t base = 0u;
-        if (t.oq) {
-            // this workgroup's queue segment, its fill counted in LDS
-            if (__lane_id() == 0u)
-                base = __hip_atomic_fetch_add(lctr_t(oq_lds), pre[N], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            base = __shfl(base, 0);
-        }
+        // this wave's own queue segment, its fill a wave-uniform register:
+        // no LDS atomic (and no wait for its return) per wave step
+        const uint32_t base = wq;
+        if (t.oq) wq += pre[N];
         const uint64_t lt = (1ull << __lane_id()) - 1ull;
 #pragma unroll
         for (int q = 0; q < N; ++q) {
@@ -600,7 +601,7 @@ __device__ __forceinline__ void run_n(const Img<kLds>& im, const Cls4Dev& t, con
             if (t.oq && now) {
                 const uint32_t pos = base + pre[q] + uint32_t(__popcll(m[q] & lt));
                 if (pos < t.oq_cap) {
-                    t.oq[gridDim.x + blockIdx.x * t.oq_cap + pos] = idx[q];
+                    t.oq[queue_row0() + queue_row() * t.oq_cap + pos] = idx[q];
                     now = false;
                 }
             }
@@ -619,9 +620,11 @@ __device__ __forceinline__ void run_n(const Img<kLds>& im, const Cls4Dev& t, con
     }
 }
 
-// The OTHER queue's fill counter of this workgroup: one LDS word after the
-// image's LDS (the launch adds 16 bytes of dynamic LDS for it).  Zeroed
-// here, made visible by the barrier of stage_lds (or this one).
+// The OTHER queue: one segment of t.oq_cap entries per wave (kOtherSegs per
+// workgroup), after the fills of all segments (kernels.hpp FinishArgs).
+// queue_begin also clears a spare LDS word after the image's LDS (the launch
+// adds 16 bytes of dynamic LDS): the hot loop counts protocol > 2 packets
+// there instead of branching (they are counted by their OTHER evaluation).
 template <bool kLds>
 __device__ __forceinline__ uint32_t queue_begin(const Cls4Dev& t, uint4* smem) {
     const uint32_t a = kLds ? t.lds_bytes : 0u;
@@ -630,12 +633,9 @@ __device__ __forceinline__ uint32_t queue_begin(const Cls4Dev& t, uint4* smem) {
     return a;
 }
 
-// End of a launch: the workgroup's queue fill -> oq[blockIdx.x] (other_kernel).
-__device__ __forceinline__ void queue_end(const Cls4Dev& t, uint32_t oq_lds) {
-    if (!t.oq) return;
-    __syncthreads();
-    if (threadIdx.x == 0)
-        t.oq[blockIdx.x] = min(*reinterpret_cast<const __attribute__((address_space(3))) uint32_t*>(oq_lds), t.oq_cap);
+// End of a launch: each wave's queue fill -> oq[its row] (the finish launch).
+__device__ __forceinline__ void queue_end(const Cls4Dev& t, uint32_t wq) {
+    if (t.oq && __lane_id() == 0u) t.oq[queue_row()] = min(wq, t.oq_cap);
 }
 
 
@@ -699,6 +699,7 @@ __global__ __launch_bounds__(kClsBlock) void classify4_cls(Cls4Dev t, Cls4Dev o,
             t.zero[i] = 0ull;
     Img<kLds> im{reinterpret_cast<const uint8_t*>(t.img)};
     const uint32_t oq_lds = queue_begin<kLds>(t, smem);
+    uint32_t wq = 0;                                       // this wave's OTHER queue fill
     if constexpr (kLds) stage_lds(t, smem);
 
     const uint32_t nthreads = gridDim.x * blockDim.x;
@@ -725,7 +726,7 @@ __global__ __launch_bounds__(kClsBlock) void classify4_cls(Cls4Dev t, Cls4Dev o,
             uint32_t v[4];
             const uint32_t ix[4] = {4u * g, 4u * g + 1u, 4u * g + 2u, 4u * g + 3u};
             run_n<4, kLds, kMode, kList, kD, kCtr>(im, t, o, hot_lane, gslot, hot0, sa, da, pa, ra, other, v,
-                                                   [&](int q) { return sa[q]; }, ix, oq_lds);
+                                                   [&](int q) { return sa[q]; }, ix, oq_lds, wq);
             if constexpr (kCtr == 2)                             // slot mode: 4 result words per lane
                 reinterpret_cast<uint4*>(verdict)[g] = make_uint4(v[0], v[1], v[2], v[3]);
             else if (verdict)
@@ -766,7 +767,7 @@ __global__ __launch_bounds__(kClsBlock) void classify4_cls(Cls4Dev t, Cls4Dev o,
             const uint32_t ix[4] = {4u * gi, 4u * gi + 1u, 4u * gi + 2u, 4u * gi + 3u};
             run_n<4, kLds, kMode, kList, -1, kCtr>(im, t, o, hot_lane, gslot, hot0, sa, da, pa, ra,
                                                    ((pr | ((pr & 0x7F7F7F7Fu) + 0x7D7D7D7Du)) & 0x80808080u) != 0u,
-                                                   v, [&](int q) { return sa[q]; }, ix, oq_lds);
+                                                   v, [&](int q) { return sa[q]; }, ix, oq_lds, wq);
             if constexpr (kCtr == 2)
                 reinterpret_cast<uint4*>(verdict)[gi] = make_uint4(v[0], v[1], v[2], v[3]);
             else if (verdict)
@@ -780,7 +781,7 @@ __global__ __launch_bounds__(kClsBlock) void classify4_cls(Cls4Dev t, Cls4Dev o,
         uint32_t v[1];
         const uint32_t ix[1] = {i};
         run_n<1, kLds, kMode, kList, -1, kCtr>(im, t, o, hot_lane, gslot, hot0, sa, da, pa, ra, ra[0] > 2u, v,
-                                               [&](int q) { return sa[q]; }, ix, oq_lds);
+                                               [&](int q) { return sa[q]; }, ix, oq_lds, wq);
         if constexpr (kCtr == 2) reinterpret_cast<uint32_t*>(verdict)[i] = v[0];   // slot mode: res | slot << 2
         else if (verdict) verdict[i] = uint8_t(v[0]);
     }
@@ -790,7 +791,7 @@ __global__ __launch_bounds__(kClsBlock) void classify4_cls(Cls4Dev t, Cls4Dev o,
         if (hot0) atomicAdd(&gslot[0], (unsigned long long)hot0);
     }
     if constexpr (kLds) flush_lds<kCtr>(t, smem);
-    queue_end(t, oq_lds);
+    queue_end(t, wq);
 }
 
 // ---------------------------------------------------------------------------
@@ -946,6 +947,7 @@ __global__ __launch_bounds__(kClsBlock) void classify16_cls(Cls4Dev t, Cls4Dev o
             t.zero[i] = 0ull;
     Img<kLds> im{reinterpret_cast<const uint8_t*>(t.img)};
     const uint32_t oq_lds = queue_begin<kLds>(t, smem);
+    uint32_t wq = 0;                                       // this wave's OTHER queue fill
     if constexpr (kLds) stage_lds(t, smem);
     const uint32_t nthreads = gridDim.x * blockDim.x;
     const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
@@ -972,11 +974,11 @@ __global__ __launch_bounds__(kClsBlock) void classify16_cls(Cls4Dev t, Cls4Dev o
             // space): only for a packet classified in place, not queued
             run_n<N, kLds, kMode, kList, kD, kCtr>(
                 im, t, o, hot_lane, gslot, hot0, sa, da, pa, ra, other, v,
-                [&](int q) { return src_rep_global(fe.gsrc, fe.gval, fe.gtop, fe.gk8, s16[q]); }, ix, oq_lds);
+                [&](int q) { return src_rep_global(fe.gsrc, fe.gval, fe.gtop, fe.gk8, s16[q]); }, ix, oq_lds, wq);
         } else {
             src_rep(s16, sa);
             run_n<N, kLds, kMode, kList, kD, kCtr>(im, t, o, hot_lane, gslot, hot0, sa, da, pa, ra, other, v,
-                                                   [&](int q) { return sa[q]; }, ix, oq_lds);
+                                                   [&](int q) { return sa[q]; }, ix, oq_lds, wq);
         }
     };
     // 4 packets per lane per step (vector dport / proto / verdict words).
@@ -1065,7 +1067,7 @@ __global__ __launch_bounds__(kClsBlock) void classify16_cls(Cls4Dev t, Cls4Dev o
         if (hot0) atomicAdd(&gslot[0], (unsigned long long)hot0);
     }
     if constexpr (kLds) flush_lds<kCtr>(t, smem);
-    queue_end(t, oq_lds);
+    queue_end(t, wq);
 }
 
 }  // namespace
