@@ -580,7 +580,6 @@ __device__ __forceinline__ void run_n(const Img<kLds>& im, const Cls4Dev& t, con
     // search and candidate scan from global memory, its slots after the main
     // image's).
     if (__any(pr_any)) {
-        const Img<false> oim{reinterpret_cast<const uint8_t*>(o.img)};
         // one queue reservation for the wave's OTHER packets of all N slots
         uint64_t m[N];
         uint32_t pre[N + 1];
@@ -590,31 +589,44 @@ __device__ __forceinline__ void run_n(const Img<kLds>& im, const Cls4Dev& t, con
             m[q] = __ballot(pr[q] > 2u);
             pre[q + 1] = pre[q] + uint32_t(__popcll(m[q]));
         }
+        const uint64_t lt = (1ull << __lane_id()) - 1ull;
         // this wave's own queue segment, its fill a wave-uniform register:
         // no LDS atomic (and no wait for its return) per wave step
         const uint32_t base = wq;
-        if (t.oq) wq += pre[N];
-        const uint64_t lt = (1ull << __lane_id()) - 1ull;
+        if (t.oq && base + pre[N] <= t.oq_cap) {          // wave-uniform: room for all of them
+            wq = base + pre[N];
+            uint32_t* seg = t.oq + queue_row0() + queue_row() * t.oq_cap + base;
 #pragma unroll
-        for (int q = 0; q < N; ++q) {
-            bool now = pr[q] > 2u;
-            if (t.oq && now) {
-                const uint32_t pos = base + pre[q] + uint32_t(__popcll(m[q] & lt));
-                if (pos < t.oq_cap) {
-                    t.oq[queue_row0() + queue_row() * t.oq_cap + pos] = idx[q];
-                    now = false;
+            for (int q = 0; q < N; ++q)
+                if (pr[q] > 2u) seg[pre[q] + uint32_t(__popcll(m[q] & lt))] = idx[q];
+        } else {
+            // the segment is full (or there is none): what fits is queued,
+            // the rest classified here and now (an out-of-line function for
+            // this rare path cost config 3 11 %: the call changed the hot
+            // loop's register allocation, profiles/r05k_bench_c3_noinline.json)
+            if (t.oq) wq = min(base + pre[N], t.oq_cap);
+#pragma unroll
+            for (int q = 0; q < N; ++q) {
+                bool now = pr[q] > 2u;
+                if (t.oq && now) {
+                    const uint32_t pos = base + pre[q] + uint32_t(__popcll(m[q] & lt));
+                    if (pos < t.oq_cap) {
+                        t.oq[queue_row0() + queue_row() * t.oq_cap + pos] = idx[q];
+                        now = false;
+                    }
                 }
-            }
-            if (__any(now)) {                                          // the queue is full: here and now
-                uint32_t key = 0xFFFFFFFFu;
-                if (now) {                                             // only these lanes load
-                    const uint32_t s1[1] = {sl(q)}, d1[1] = {d[q]}, p1[1] = {dp[q]}, z1[1] = {0u};
-                    uint32_t r1[1], k1[1];
-                    classify_n<1, false, 0, 0, -1>(oim, o, s1, d1, p1, z1, r1, k1);
-                    res[q] = r1[0];
-                    key = t.n_ctr + k1[0];
+                if (__any(now)) {                              // here and now
+                    uint32_t key = 0xFFFFFFFFu;
+                    if (now) {                                 // only these lanes load
+                        const Img<false> oim{reinterpret_cast<const uint8_t*>(o.img)};
+                        const uint32_t s1[1] = {sl(q)}, d1[1] = {d[q]}, p1[1] = {dp[q]}, z1[1] = {0u};
+                        uint32_t r1[1], k1[1];
+                        classify_n<1, false, 0, 0, -1>(oim, o, s1, d1, p1, z1, r1, k1);
+                        res[q] = r1[0];
+                        key = t.n_ctr + k1[0];
+                    }
+                    wave_count(gslot, key);
                 }
-                wave_count(gslot, key);
             }
         }
     }
