@@ -283,7 +283,7 @@ int cls_if_acls(cls_engine* e, uint32_t if_id, int32_t* in_table, int32_t* out_t
  * aligned on the device; IPv4-mapped = IPv4, as Go's To4) -- Connection*
  * takes any net.IP (:243-390).  A device batch's interface id outside the
  * engine's ids gives CLS_CONN_FAILURE for that connection (a host batch is
- * rejected with CLS_E_INVAL).
+ * rejected with CLS_E_INVAL).  At most 2^30 connections per call.
  * Large ACLs: in batches >= 65536, an ACL with a compiled classifier image
  * whose linear work would be large (host batch: connections touching it x
  * its rules >= 2048 x batch, touches estimated from a hashed sample of <= 64

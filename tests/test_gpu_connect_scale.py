@@ -408,3 +408,49 @@ def test_conn_counters_do_not_wait_for_other_streams():
             assert np.array_equal(got[name], want[name]), name
     finally:
         eng.close()
+
+
+@pytest.mark.parametrize("no_jobs", ["0", "1"])
+@pytest.mark.parametrize("count", [False, True])
+def test_ipv4_job_lists_and_shuffles(no_jobs, count, monkeypatch):
+    """The connection kernel's two ways to hand a wave's jobs to its lanes
+    (IPv4): the per-wave job lists in LDS (the default where they fit) and
+    the owner search with shuffles (CONTIVCLS_CONN_NO_JOBS=1, and launches
+    whose LDS is full) -- verdicts and counters against the oracle."""
+    from vpp_amd.engine import Engine
+    if no_jobs == "1":
+        monkeypatch.setenv("CONTIVCLS_CONN_NO_JOBS", "1")
+    eng = Engine()
+    try:
+        _run(eng, 31, "device_auto", 4, count=count, n=16000, n_local=24)
+    finally:
+        eng.close()
+
+
+@pytest.mark.parametrize("pre_slots", ["0", "1"])
+def test_counted_large_acl_words(pre_slots, monkeypatch):
+    """Counting batches: the pair launch writes each large-ACL word's counter
+    index (descriptor base + rule) and the connection kernel adds it directly,
+    or (CONTIVCLS_CONN_PRE_SLOTS=1) writes slots the kernel maps to rules --
+    per-(ACL, rule) counters against the oracle, protocol-47 connections
+    included (their OTHER-image slots)."""
+    from vpp_amd.engine import Engine
+    monkeypatch.setenv("CONTIVCLS_CONN_PRE_SLOTS", pre_slots)
+    eng = Engine()
+    try:
+        ifs, bind, by_name, pool, spec = build(eng, 41, n_local=10, n_if=24)
+        n = 4 * 6000 + 1
+        tr = traffic(41, n, pool, spec, 4)
+        rng = np.random.default_rng(41)
+        tr["proto"] = np.where(rng.random(n) < 0.04, 47, tr["proto"]).astype(np.uint8)
+        ids = np.array([eng.if_id(x) for x in ifs], np.uint32)
+        si = np.where(rng.random(n) < 0.5, rng.integers(0, 3, n), rng.integers(0, len(ifs), n))
+        di = rng.integers(0, len(ifs), n)
+        got = eng.connect_batch(ids[si], ids[di], tr["src"], tr["dst"], tr["proto"], tr["sport"], tr["dport"],
+                                mode="classifier", count=True)
+        want, wcounts = oracle_connections(bind, by_name, ifs, si, di, tr, 4)
+        assert np.array_equal(got, want)
+        for name in by_name:
+            assert np.array_equal(eng.conn_counters(name, reset=True), wcounts[name]), name
+    finally:
+        eng.close()

@@ -81,6 +81,14 @@ def main():
         eng.connect_batch(*dargs, count=True)
         dt_c = per_call(True)
         counted = {"value": round(n / dt_c / 1e6, 3), "unit": "Mconn/s", "ms_per_batch": round(dt_c * 1e3, 3)}
+        # how the counted calls spread over the (ACL, rule) counters: the
+        # shares of the largest counters (contention of the counter atomics)
+        cs = np.concatenate([eng.conn_counters(name).astype(np.float64) for name in by_name])
+        tot = cs.sum()
+        top = np.sort(cs)[::-1][:8] / max(tot, 1.0)
+        counted["calls_per_connection"] = round(tot / (n * (a.iters + 1)), 3)
+        counted["top_counter_shares"] = [round(float(x), 4) for x in top]
+        counted["nonzero_counters"] = int((cs > 0).sum())
     # roofline: the 22 algorithmic bytes of an IPv4 connection (src, dst,
     # src_if, dst_if 4 B each, sport, dport 2 B, proto 1 B read; the verdict
     # byte written) per HBM-resident batch, beside the stream floor of the

@@ -1228,6 +1228,8 @@ int connect_locked(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t* ou
         return fail(e, CLS_E_INVAL, "missing connection arrays");
     const bool dev = flags & CLS_F_DEVICE, count = flags & CLS_F_COUNT;
     const size_t ab = k16 ? 16 : 4;                       // address bytes
+    // the kernels index connections with 32-bit offsets
+    if (n > kClsChunk) return fail(e, CLS_E_INVAL, "connection batch above 2^30 connections");
     if (dev && k16 && n && (!aligned(src, 16) || !aligned(dst, 16)))
         return fail(e, CLS_E_INVAL, "device src16/dst16 must be 16-byte aligned");
     HIPC(e, hipSetDevice(e->device));
@@ -1414,14 +1416,33 @@ int connect_locked(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t* ou
     const uint32_t n_ctr = P.n_ctr;
     // The result words: block b (the ACL big[b]) at pre + 2 b stride, the SYN
     // tuple's words first, the SYN-ACK tuple's at + stride (a multiple of 4,
-    // so both halves stay 16-B aligned for the pair launch's stores).
+    // so both halves stay 16-B aligned for the pair launch's stores).  In
+    // byte mode (pre_res8 below) block b is stride bytes at pre + b stride.
     const uint64_t stride = (n + 3) & ~uint64_t(3);
+    // Both tuples of a large ACL in one launch (classify4_pair) when the image
+    // is LDS-resident and the arrays allow its 16-B loads.  When every large
+    // ACL takes that launch and the batch counts, the launch writes each
+    // word's counter index (descriptor counter base + the slot's rule)
+    // instead of its slot: the connection kernel then counts a large-ACL call
+    // without a descriptor read and a dependent slot -> rule gather.
+    auto pair_ok = [&](const Table& t) {
+        const uint32_t *s4 = static_cast<const uint32_t*>(src), *d4 = static_cast<const uint32_t*>(dst);
+        return !k16 && t.lds_resident && aligned(s4, 16) && aligned(d4, 16) && aligned(dp, 8) && aligned(sp, 8) &&
+               aligned(pr, 4) && !std::getenv("CONTIVCLS_CONN_NO_PAIR");
+    };
+    bool all_pair = !big.empty();
+    for (uint32_t b : big) all_pair = all_pair && pair_ok(*dtab[b]);
+    const bool pre_rules = count && all_pair && !std::getenv("CONTIVCLS_CONN_PRE_SLOTS");
+    // ... and a batch that does not count needs only the ACLActions: one byte
+    // per connection for both tuples (the words would be 8 B)
+    const bool pre_res8 = !count && all_pair && !std::getenv("CONTIVCLS_CONN_PRE_WORDS");
     if (!big.empty()) {
         if (n > kClsChunk) return fail(e, CLS_E_INVAL, "connection batch above 2^30 with classifier ACLs");
-        HIPC(e, e->s_pre.ensure(big.size() * 2 * stride * 4));
+        HIPC(e, e->s_pre.ensure(big.size() * (pre_res8 ? stride : 2 * stride * 4)));
         for (size_t b = 0; b < big.size(); ++b) {
             Table& t = *dtab[big[b]];
-            uint32_t* pre = e->s_pre.as<uint32_t>() + b * 2 * stride;
+            uint32_t* pre = pre_res8 ? reinterpret_cast<uint32_t*>(e->s_pre.as<uint8_t>() + b * stride)
+                                     : e->s_pre.as<uint32_t>() + b * 2 * stride;
             LaunchCfg cfg;
             cfg.stream = s;
             if (!k16) {
@@ -1431,9 +1452,7 @@ int connect_locked(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t* ou
                 // Both tuples in one launch when the image is LDS-resident and
                 // the arrays allow 16-B loads; the OTHER image beside the main
                 // one when both fit (no slot counters in this mode)
-                const bool pair = t.lds_resident && aligned(s4, 16) && aligned(d4, 16) && aligned(dp, 8) &&
-                                  aligned(sp, 8) && aligned(pr, 4) && !std::getenv("CONTIVCLS_CONN_NO_PAIR");
-                if (pair) {
+                if (pair_ok(t)) {
                     uint32_t o_at = (t.img.img_bytes + 15u) & ~15u;
                     // (+ 32: the queue fill word after the images)
                     if (o_at + t.oimg.img_bytes + 32u > uint32_t(max_lds_bytes())) o_at = 0;
@@ -1447,7 +1466,8 @@ int connect_locked(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t* ou
                     const uint32_t qcap = pair_qcap(n, cfg.grid);
                     HIPC(e, e->s_pq.ensure(size_t(cfg.grid) * std::max<uint32_t>(1, qcap) * 16));
                     HIPC(e, launch_classify4_pair(cd, od, o_at, syn, sp, pre, stride, e->s_pq.as<uint32_t>(), qcap,
-                                                  cfg));
+                                                  pre_rules ? t.d_slot_rule.as<uint32_t>() : nullptr,
+                                                  desc[big[b]].ctr_off, pre_res8, cfg));
                 } else {
                     cfg.other = cls4_dev(t.oimg, t.d_oimg, DevBuf(), 0, t.n_rules);
                     cfg.grid = cls_grid(e, true, t.lds_resident, t.img.lds_bytes, n);
@@ -1514,6 +1534,8 @@ int connect_locked(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t* ou
     a.desc = e->s_desc.as<ConnDesc>();
     a.pre = big.empty() ? nullptr : e->s_pre.as<uint32_t>();
     a.pre_stride = stride;
+    a.pre_rules = pre_rules ? 1u : 0u;
+    a.pre_res8 = pre_res8 ? 1u : 0u;
     a.bm_steps = P.bm_steps;
     a.ifs = e->s_ifs.as<IfAcls>();
     a.rules = e->s_rules.p;
@@ -1558,8 +1580,27 @@ int connect_locked(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t* ou
         a.meta_lds = uint32_t(meta_at);
         lds = meta_at + meta;
     }
-    const int per_cu = per_cu_of(lds);
-    const int block = per_cu >= 2 ? 512 : 1024;
+    int per_cu = per_cu_of(lds);
+    int block = per_cu >= 2 ? 512 : 1024;
+    // IPv4: the waves' job lists (512 B per wave) after the rest, when they
+    // cost no workgroup per CU; else the kernel's owner search and shuffles
+    // (CONTIVCLS_CONN_NO_JOBS: tests)
+    a.job_lds = 0xFFFFFFFFu;
+    const size_t job_at = (lds + 15) & ~size_t(15), job_b = size_t(block / 64) * 512;
+    if (!k16 && job_at + job_b <= lds_max && (per_cu == 1 || per_cu_of(job_at + job_b) == per_cu) &&
+        !std::getenv("CONTIVCLS_CONN_NO_JOBS")) {
+        a.job_lds = uint32_t(job_at);
+        lds = job_at + job_b;
+    }
+    if (std::getenv("CONTIVCLS_DEBUG_CONN")) {              // diagnostics: the launch's LDS plan
+        size_t nbm = 0;
+        for (const ConnDesc& d : desc) nbm += d.bm_off != 0xFFFFFFFFu;
+        std::fprintf(stderr, "connect: n %llu desc %zu big %zu bitmaps %zu pool %zu lds_rules %d ctr %u cmode %d "
+                     "meta %s jobs %s lds %zu per_cu %d block %d bm_steps %u\n", (unsigned long long)n, desc.size(),
+                     big.size(), nbm, pool.size(), int(lds_rules), n_ctr, cmode,
+                     a.meta_lds != 0xFFFFFFFFu ? "lds" : "global", a.job_lds != 0xFFFFFFFFu ? "lds" : "shuffle", lds,
+                     per_cu, block, P.bm_steps);
+    }
     const int grid = int(std::max<uint64_t>(1, std::min<uint64_t>(uint64_t(e->n_cu) * per_cu,
                                                                   (n + block - 1) / block)));
     HIPC(e, launch_connect(a, k16, lds_rules, cmode, grid, block, lds, s));

@@ -422,7 +422,6 @@ __device__ __forceinline__ bool conn_match(const ConnRule16& r, const uint4& s, 
 }
 __device__ __forceinline__ uint32_t conn_index(const ConnRule4& r) { return r.index; }
 __device__ __forceinline__ uint32_t conn_index(const ConnRule16& r) { return r.index_fam >> 2; }
-__device__ __forceinline__ bool mapped4(uint32_t) { return true; }
 __device__ __forceinline__ bool mapped4(const uint4& a) { return (a.x | a.y) == 0u && a.z == 0xFFFF0000u; }
 
 // The call's descriptor and interface tables: staged in LDS at a.meta_lds
@@ -555,8 +554,11 @@ __device__ __forceinline__ uint32_t conn_bm(const ConnArgs& a, const ConnDesc& D
 // SIMD), so 24 waves fit a CU -- three 512-thread workgroups where the LDS
 // allows two or more, else one 1024-thread workgroup (16 waves rather than
 // the 8 of one 512-thread one); forcing 64 VGPRs spills to scratch.
-template <bool k16, bool kLdsRules, int kCount>
-__global__ __launch_bounds__(1024) void connect_kernel(ConnArgs a) {
+// kJobs (IPv4): the waves' job lists in LDS (a.job_lds); else the owner
+// search and shuffles (16-byte batches, and IPv4 launches whose LDS is
+// full: the job lists would displace LDS counters or bitmap forms)
+template <bool k16, bool kLdsRules, int kCount, bool kJobs>
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(6))) void connect_kernel(ConnArgs a) {
     typedef typename ConnT<k16>::A A;
     extern __shared__ uint4 smem[];
     typedef __attribute__((address_space(3))) uint32_t* lctr_t;
@@ -576,20 +578,29 @@ __global__ __launch_bounds__(1024) void connect_kernel(ConnArgs a) {
     const uint64_t lt = (1ull << lane) - 1ull;
     const A* src = static_cast<const A*>(a.src);
     const A* dst = static_cast<const A*>(a.dst);
-    const uint64_t nthreads = uint64_t(gridDim.x) * blockDim.x;
-    const uint64_t n_iter = (a.n + nthreads - 1) / nthreads;    // uniform trip count (ballots below)
-    for (uint64_t it = 0; it < n_iter; ++it) {
-        const uint64_t i = it * nthreads + uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-        const bool live = i < a.n;
-        const uint64_t ic = live ? i : 0;                       // loads stay in bounds
-        const uint32_t si = a.src_if[ic], dj = a.dst_if[ic];
+    // 32-bit connection indices (the host splits batches at 2^30): SGPR base
+    // + 32-bit VGPR offset addressing, no 64-bit index arithmetic per load
+    const uint32_t n = uint32_t(a.n);
+    const uint32_t nthreads = gridDim.x * blockDim.x;
+    const uint32_t n_iter = (n + nthreads - 1u) / nthreads;     // uniform trip count (ballots below)
+    const uint32_t stride = uint32_t(a.pre_stride);
+    // IPv4: this wave's job list in LDS, 64 entries of 8 B {owner lane | call
+    // << 6 | descriptor << 8, port | protocol << 16}; a job's lane writes its
+    // result word over the entry's first word
+    const uint32_t jq = a.job_lds + (threadIdx.x >> 6) * 512u;
+    for (uint32_t it = 0; it < n_iter; ++it) {
+        const uint32_t i = it * nthreads + blockIdx.x * blockDim.x + threadIdx.x;
+        const bool live = i < n;
+        const uint32_t ic = live ? i : 0u;                      // loads stay in bounds
+        // every field's load first, together
+        const uint32_t si = *at(a.src_if, ic), dj = *at(a.dst_if, ic);
+        const A sa = *at(src, ic), da = *at(dst, ic);
+        const uint32_t sp = *at(a.sport, ic), dp = *at(a.dport, ic), pr = *at(a.proto, ic);
         const bool ok = live && si < a.n_ifs && dj < a.n_ifs;   // unknown interface id: Failure
         // both lookups unconditional (an in-range index), the unknown case selected after
         const IfAcls S0 = conn_if(a, ok ? si : 0u), D0 = conn_if(a, ok ? dj : 0u);
         const IfAcls S = ok ? S0 : IfAcls{-1, -1, -1, -1};
         const IfAcls Dif = ok ? D0 : IfAcls{-1, -1, -1, -1};
-        const A sa = src[ic], da = dst[ic];
-        const uint32_t sp = a.sport[ic], dp = a.dport[ic], pr = a.proto[ic];
         const uint32_t p = pr <= 2u ? pr : 3u;
         // the four calls in testConnection's order
         const int32_t di[4] = {S.in, Dif.out, Dif.in, S.out};
@@ -600,13 +611,15 @@ __global__ __launch_bounds__(1024) void connect_kernel(ConnArgs a) {
         uint32_t w[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k)
-            w[k] = *(bi[k] >= 0 ? a.pre + (2ull * uint32_t(bi[k]) + uint32_t(k >> 1)) * a.pre_stride + ic
-                                : a.src_if + ic);
-        // ---- the jobs of the wave, packed (registers only) ----
+            w[k] = a.pre_res8 ? uint32_t(bi[k] >= 0 ? reinterpret_cast<const uint8_t*>(a.pre)[uint64_t(uint32_t(bi[k])) *
+                                                                                           stride + ic]
+                                                   : 0u) >> (2 * (k >> 1))
+                              : *(bi[k] >= 0 ? a.pre + (uint64_t(2u * uint32_t(bi[k]) + uint32_t(k >> 1)) * stride + ic)
+                                             : at(a.src_if, ic));
+        // ---- the jobs of the wave, packed ----
         // job j of the wave is call k of owner lane o: the ballots of the four
-        // calls give every job a rank (owner side) and every running lane its
-        // job (nth_set_bit); the owner's fields come over ds_bpermute and the
-        // result goes back the same way
+        // calls give every job a rank; the jobs run 64 at a time, every lane
+        // on one job
         bool job[4];
         uint64_t m[4];
         uint32_t c[5], jpos[4];
@@ -623,42 +636,77 @@ __global__ __launch_bounds__(1024) void connect_kernel(ConnArgs a) {
         for (uint32_t j0 = 0; j0 < nj; j0 += 64u) {             // wave-uniform
             const uint32_t j = j0 + lane;
             const bool act = j < nj;
-            const uint32_t k = uint32_t(j >= c[1]) + uint32_t(j >= c[2]) + uint32_t(j >= c[3]);
-            const uint64_t mk = k == 0u ? m[0] : k == 1u ? m[1] : k == 2u ? m[2] : m[3];
-            const uint32_t ck = k == 0u ? c[0] : k == 1u ? c[1] : k == 2u ? c[2] : c[3];
-            const uint32_t o = act ? nth_set_bit(mk, j - ck) : lane;
-            // the owning lane's connection (every lane takes part in the shuffles)
-            A xs, xd;
-            if constexpr (k16) {
-                xs = make_uint4(__shfl(sa.x, int(o)), __shfl(sa.y, int(o)), __shfl(sa.z, int(o)), __shfl(sa.w, int(o)));
-                xd = make_uint4(__shfl(da.x, int(o)), __shfl(da.y, int(o)), __shfl(da.z, int(o)), __shfl(da.w, int(o)));
-            } else {
-                xs = __shfl(sa, int(o));
-                xd = __shfl(da, int(o));
-            }
-            const uint32_t xdp = __shfl(dp, int(o)), xsp = __shfl(sp, int(o)), xp = __shfl(p, int(o));
-            const int32_t d0 = __shfl(di[0], int(o)), d1 = __shfl(di[1], int(o));
-            const int32_t d2 = __shfl(di[2], int(o)), d3 = __shfl(di[3], int(o));
             uint32_t out = 0u;
-            if (act) {
-                const ConnDesc D = conn_desc(a, uint32_t(k == 0u ? d0 : k == 1u ? d1 : k == 2u ? d2 : d3));
-                const bool syn = k < 2u;
-                uint32_t res, rule;
-                if (!k16 && D.bm_off != 0xFFFFFFFFu) {
-                    if constexpr (!k16)
-                        res = conn_bm<kLdsRules>(a, D, syn ? xs : xd, syn ? xd : xs, syn ? xdp : xsp, xp, rule);
-                } else {
-                    const bool x4s = mapped4(xs), x4d = mapped4(xd);
-                    res = syn ? conn_scan<k16, kLdsRules>(a, D, xs, xd, x4s, x4d, xdp, xp, rule)
-                              : conn_scan<k16, kLdsRules>(a, D, xd, xs, x4d, x4s, xsp, xp, rule);
-                }
-                out = res | ((D.ctr_off + rule) << 2);
-            }
-            // the owners take their results of this pass
+            if constexpr (kJobs) {
+                // IPv4: the owners write their jobs into the wave's LDS list
+                // (entry = rank - j0), the lane of a rank reads its entry and
+                // takes the owner's addresses with two shuffles -- where a
+                // search of the ballots for the owner (nth_set_bit) and nine
+                // shuffles cost ~60 VALU instructions per pass
+                typedef __attribute__((address_space(3))) v2u* lds64w_t;
 #pragma unroll
-            for (int kk = 0; kk < 4; ++kk) {
-                const uint32_t r = __shfl(out, int((jpos[kk] - j0) & 63u));
-                if (job[kk] && jpos[kk] >= j0 && jpos[kk] < j0 + 64u) rj[kk] = r;
+                for (int k = 0; k < 4; ++k)
+                    if (job[k] && jpos[k] - j0 < 64u)
+                        *lds64w_t(jq + 8u * (jpos[k] - j0)) =
+                            v2u{lane | uint32_t(k) << 6 | uint32_t(di[k]) << 8, (k < 2 ? dp : sp) | (p << 16)};
+                const v2u e = *lds64_t(jq + 8u * lane);
+                const uint32_t o = act ? (e.x & 63u) : lane, kk = (e.x >> 6) & 3u;
+                const uint32_t xs = __shfl(uint32_t(sa), int(o)), xd = __shfl(uint32_t(da), int(o));
+                if (act) {
+                    const ConnDesc D = conn_desc(a, e.x >> 8);
+                    const uint32_t port = e.y & 0xFFFFu, xp = e.y >> 16;
+                    const uint32_t s1 = kk < 2u ? xs : xd, d1 = kk < 2u ? xd : xs;
+                    uint32_t res, rule;
+                    if (D.bm_off != 0xFFFFFFFFu) res = conn_bm<kLdsRules>(a, D, s1, d1, port, xp, rule);
+                    else res = conn_scan<false, kLdsRules>(a, D, A(s1), A(d1), true, true, port, xp, rule);
+                    out = res | ((D.ctr_off + rule) << 2);
+                }
+                // the result over the entry's first word, then the owners read it
+                if (act) *(__attribute__((address_space(3))) uint32_t*)(jq + 8u * lane) = out;
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if (job[k] && jpos[k] - j0 < 64u)
+                        rj[k] = *(const __attribute__((address_space(3))) uint32_t*)(jq + 8u * (jpos[k] - j0));
+            } else {
+                const uint32_t k = uint32_t(j >= c[1]) + uint32_t(j >= c[2]) + uint32_t(j >= c[3]);
+                const uint64_t mk = k == 0u ? m[0] : k == 1u ? m[1] : k == 2u ? m[2] : m[3];
+                const uint32_t ck = k == 0u ? c[0] : k == 1u ? c[1] : k == 2u ? c[2] : c[3];
+                const uint32_t o = act ? nth_set_bit(mk, j - ck) : lane;
+                // the owning lane's connection (every lane takes part in the shuffles)
+                A xs, xd;
+                if constexpr (k16) {
+                    xs = make_uint4(__shfl(sa.x, int(o)), __shfl(sa.y, int(o)), __shfl(sa.z, int(o)), __shfl(sa.w, int(o)));
+                    xd = make_uint4(__shfl(da.x, int(o)), __shfl(da.y, int(o)), __shfl(da.z, int(o)), __shfl(da.w, int(o)));
+                } else {
+                    xs = __shfl(sa, int(o));
+                    xd = __shfl(da, int(o));
+                }
+                const uint32_t xdp = __shfl(dp, int(o)), xsp = __shfl(sp, int(o)), xp = __shfl(p, int(o));
+                const int32_t d0 = __shfl(di[0], int(o)), d1 = __shfl(di[1], int(o));
+                const int32_t d2 = __shfl(di[2], int(o)), d3 = __shfl(di[3], int(o));
+                if (act) {
+                    const ConnDesc D = conn_desc(a, uint32_t(k == 0u ? d0 : k == 1u ? d1 : k == 2u ? d2 : d3));
+                    const bool syn = k < 2u;
+                    uint32_t res, rule;
+                    if constexpr (!k16) {
+                        if (D.bm_off != 0xFFFFFFFFu)
+                            res = conn_bm<kLdsRules>(a, D, syn ? xs : xd, syn ? xd : xs, syn ? xdp : xsp, xp, rule);
+                        else
+                            res = conn_scan<false, kLdsRules>(a, D, syn ? xs : xd, syn ? xd : xs, true, true,
+                                                              syn ? xdp : xsp, xp, rule);
+                    } else {
+                        const bool x4s = mapped4(xs), x4d = mapped4(xd);
+                        res = syn ? conn_scan<k16, kLdsRules>(a, D, xs, xd, x4s, x4d, xdp, xp, rule)
+                                  : conn_scan<k16, kLdsRules>(a, D, xd, xs, x4d, x4s, xsp, xp, rule);
+                    }
+                    out = res | ((D.ctr_off + rule) << 2);
+                }
+                // the owners take their results of this pass
+#pragma unroll
+                for (int kk = 0; kk < 4; ++kk) {
+                    const uint32_t r = __shfl(out, int((jpos[kk] - j0) & 63u));
+                    if (job[kk] && jpos[kk] >= j0 && jpos[kk] < j0 + 64u) rj[kk] = r;
+                }
             }
         }
         // ---- testConnection over the four results ----
@@ -700,7 +748,9 @@ __global__ __launch_bounds__(1024) void connect_kernel(ConnArgs a) {
                 if (made[k] && di[k] >= 0) {                    // nil ACLs are not counted
                     if (job[k]) {
                         key[k] = rj[k] >> 2;
-                    } else {                                    // a large ACL: its slot's rule
+                    } else if (a.pre_rules) {                   // a large ACL: the word's counter index
+                        key[k] = w[k] >> 2;
+                    } else {                                    // ... or its slot's rule
                         const ConnDesc D = conn_desc(a, uint32_t(di[k]));
                         key[k] = D.ctr_off + D.slot_rule[w[k] >> 2];
                     }
@@ -930,16 +980,19 @@ hipError_t launch_stream_conn(const ConnArgs& a, int grid, hipStream_t s) {
 hipError_t launch_connect(const ConnArgs& a, bool k16, bool lds_rules, int count, int grid, int block, size_t lds,
                           hipStream_t s) {
     if (a.n == 0) return hipSuccess;
-#define CONN_CASE(K16, L, C)                                                                               \
-    if (k16 == K16 && lds_rules == L && count == C) {                                                      \
-        lds_attr(reinterpret_cast<const void*>(connect_kernel<K16, L, C>), lds);                          \
-        hipLaunchKernelGGL((connect_kernel<K16, L, C>), dim3(grid), dim3(block), lds, s, a);               \
+    const bool jobs = a.job_lds != 0xFFFFFFFFu;
+#define CONN_CASE(K16, L, C, J)                                                                            \
+    if (k16 == K16 && lds_rules == L && count == C && jobs == J) {                                         \
+        lds_attr(reinterpret_cast<const void*>(connect_kernel<K16, L, C, J>), lds);                       \
+        hipLaunchKernelGGL((connect_kernel<K16, L, C, J>), dim3(grid), dim3(block), lds, s, a);            \
         return hipGetLastError();                                                                          \
     }
-    CONN_CASE(false, false, 0) CONN_CASE(false, false, 1) CONN_CASE(false, false, 2)
-    CONN_CASE(false, true, 0) CONN_CASE(false, true, 1) CONN_CASE(false, true, 2)
-    CONN_CASE(true, false, 0) CONN_CASE(true, false, 1) CONN_CASE(true, false, 2)
-    CONN_CASE(true, true, 0) CONN_CASE(true, true, 1) CONN_CASE(true, true, 2)
+    CONN_CASE(false, false, 0, true) CONN_CASE(false, false, 1, true) CONN_CASE(false, false, 2, true)
+    CONN_CASE(false, true, 0, true) CONN_CASE(false, true, 1, true) CONN_CASE(false, true, 2, true)
+    CONN_CASE(false, false, 0, false) CONN_CASE(false, false, 1, false) CONN_CASE(false, false, 2, false)
+    CONN_CASE(false, true, 0, false) CONN_CASE(false, true, 1, false) CONN_CASE(false, true, 2, false)
+    CONN_CASE(true, false, 0, false) CONN_CASE(true, false, 1, false) CONN_CASE(true, false, 2, false)
+    CONN_CASE(true, true, 0, false) CONN_CASE(true, true, 1, false) CONN_CASE(true, true, 2, false)
 #undef CONN_CASE
     return hipErrorInvalidValue;
 }

@@ -181,9 +181,14 @@ hipError_t launch_classify16_slots(const Cls4Dev& t, const Fe16& fe, const Pkts1
 // on the OTHER image after the workgroup's main loop, one per lane.
 // Needs 16-B aligned src / dst / out / out + stride, 8-B dport / sport, 4-B
 // proto; stride a multiple of 4.
+// slot_rule (may be null): write each word's counter index ctr_base +
+// slot_rule[slot] in place of the slot (counting connection batches); res8
+// (batches that do not count): only the two ACLActions, one byte per
+// connection (SYN result | SYN-ACK result << 2) at out, 1/8 of the words' bytes
 hipError_t launch_classify4_pair(const Cls4Dev& t, const Cls4Dev& o, uint32_t o_at, const Pkts4& p,
                                  const uint16_t* sport, uint32_t* out, uint64_t stride, uint32_t* oq,
-                                 uint32_t oq_cap, const LaunchCfg& cfg);
+                                 uint32_t oq_cap, const uint32_t* slot_rule, uint32_t ctr_base, bool res8,
+                                 const LaunchCfg& cfg);
 // The OTHER queue segment of one pair-launch workgroup (kPairBlock threads)
 // that holds every connection its lanes visit, 4 per lane per step, in 16-B
 // entries; the engine caps the segment (oq_cap entries; the overflow is
@@ -245,7 +250,11 @@ struct ConnArgs {
     const uint32_t* pre;         // classifier slot words of the large ACLs: block b at pre + 2 b pre_stride
                                  // (SYN tuple, then SYN-ACK at + pre_stride); null when there are none
     uint64_t pre_stride;
+    uint32_t pre_rules;          // the words carry counter indices (descriptor base + rule), not slots
+    uint32_t pre_res8;           // block b is one byte per connection at (uint8_t*) pre + b pre_stride:
+                                 // SYN result | SYN-ACK result << 2 (batches that do not count)
     uint32_t bm_steps;           // bitmap forms: lower-bound steps of the largest interval table
+    uint32_t job_lds;            // IPv4: LDS byte offset of the waves' job lists (512 B per wave)
 };
 // k16: 16-byte addresses; lds_rules: stage the pool; count: 0 none, 1 LDS
 // counters, 2 global (wave-aggregated) counters; grid: persistent workgroups
