@@ -427,15 +427,21 @@ def test_ipv4_job_lists_and_shuffles(no_jobs, count, monkeypatch):
         eng.close()
 
 
-@pytest.mark.parametrize("pre_slots", ["0", "1"])
-def test_counted_large_acl_words(pre_slots, monkeypatch):
+@pytest.mark.parametrize("words", ["u16", "u32", "slots"])
+def test_counted_large_acl_words(words, monkeypatch):
     """Counting batches: the pair launch writes each large-ACL word's counter
-    index (descriptor base + rule) and the connection kernel adds it directly,
-    or (CONTIVCLS_CONN_PRE_SLOTS=1) writes slots the kernel maps to rules --
-    per-(ACL, rule) counters against the oracle, protocol-47 connections
-    included (their OTHER-image slots)."""
+    index (descriptor base + rule) as u16 words (indices below 2^14) or
+    (CONTIVCLS_CONN_PRE_WORDS=1) u32 words, and the connection kernel adds it
+    directly, or (CONTIVCLS_CONN_PRE_SLOTS=1) writes slots the kernel maps to
+    rules -- per-(ACL, rule) counters against the oracle, protocol-47
+    connections included (their OTHER-image slots).  Uncounted batches of the
+    same connections (one result byte per connection, or u32 words) give the
+    same verdicts."""
     from vpp_amd.engine import Engine
-    monkeypatch.setenv("CONTIVCLS_CONN_PRE_SLOTS", pre_slots)
+    if words == "u32":
+        monkeypatch.setenv("CONTIVCLS_CONN_PRE_WORDS", "1")
+    if words == "slots":
+        monkeypatch.setenv("CONTIVCLS_CONN_PRE_SLOTS", "1")
     eng = Engine()
     try:
         ifs, bind, by_name, pool, spec = build(eng, 41, n_local=10, n_if=24)
@@ -452,5 +458,69 @@ def test_counted_large_acl_words(pre_slots, monkeypatch):
         assert np.array_equal(got, want)
         for name in by_name:
             assert np.array_equal(eng.conn_counters(name, reset=True), wcounts[name]), name
+        plain = eng.connect_batch(ids[si], ids[di], tr["src"], tr["dst"], tr["proto"], tr["sport"], tr["dport"],
+                                  mode="classifier")
+        assert np.array_equal(plain, want)
+    finally:
+        eng.close()
+
+
+@pytest.mark.parametrize("same_if", [False, True])
+def test_counted_batch_beyond_workgroup_bound(same_if):
+    """u16 LDS call counters (kConnWgConns connections per workgroup): a
+    counted batch of 12 Mi connections -- more than the resident workgroups
+    may take, so the launch grows its grid -- counts exactly what the same
+    connections count in 4 Mi pieces (counters are linear in the batch).
+    same_if: one connection, repeated, from if0 to if0 (inbound and outbound
+    ACL the global one): its calls pile onto one or two counters, far past a
+    u16 per workgroup without the bound."""
+    import torch
+    from vpp_amd.engine import Engine
+    eng = Engine()
+    try:
+        ifs, bind, by_name, pool, spec = build(eng, 9, n_local=12, cfg=3)
+        n, piece = 12 << 20, 4 << 20
+        tr = traffic(9, n, pool, spec, 4)
+        rng = np.random.default_rng(9)
+        ids = np.array([eng.if_id(x) for x in ifs], np.uint32)
+        if same_if:
+            si = di = np.zeros(n, np.int64)
+            tr = {f: np.repeat(v[:1], n, axis=0) for f, v in tr.items()}
+        else:
+            si, di = rng.integers(0, len(ifs), n), rng.integers(0, len(ifs), n)
+        args = [ids[si], ids[di], tr["src"], tr["dst"], tr["proto"], tr["sport"], tr["dport"]]
+        dv = [torch.from_numpy(np.ascontiguousarray(x).view({4: np.int32, 2: np.int16, 1: np.uint8}[x.dtype.itemsize]))
+              .to("cuda") for x in args]
+        whole = eng.connect_batch(*dv, count=True).cpu().numpy()
+        got = {name: eng.conn_counters(name, reset=True) for name in by_name}
+        parts = np.concatenate([eng.connect_batch(*[x[a:a + piece] for x in dv], count=True).cpu().numpy()
+                                for a in range(0, n, piece)])
+        assert np.array_equal(whole, parts)
+        total = 0
+        for name in by_name:
+            want = eng.conn_counters(name, reset=True)
+            assert np.array_equal(got[name], want), name
+            total += int(want.sum())
+        assert total > n // 2
+        if same_if:
+            assert got["global"].max() >= n              # the first call (src inbound) is always made
+    finally:
+        eng.close()
+
+
+@pytest.mark.parametrize("flush", ["rows", "atomic"])
+@pytest.mark.parametrize("ctr16", ["0", "1"])
+def test_counter_widths_and_flush_paths(flush, ctr16, monkeypatch):
+    """LDS call counters as u32 or u16 pairs, leaving the launch as
+    per-workgroup rows (summed by the rows launch) or by device atomics into
+    the copies of the call counters: per-(ACL, rule) counters against
+    orc_test_connection."""
+    from vpp_amd.engine import Engine
+    monkeypatch.setenv("CONTIVCLS_CONN_CTR16", ctr16)
+    if flush == "atomic":
+        monkeypatch.setenv("CONTIVCLS_CONN_FLUSH_ATOMIC", "1")
+    eng = Engine()
+    try:
+        _run(eng, 21, "device_auto", 4, count=True, n=20000, n_local=12)
     finally:
         eng.close()

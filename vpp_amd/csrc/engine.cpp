@@ -1373,7 +1373,7 @@ int connect_locked(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t* ou
             const size_t lds_max0 = size_t(max_lds_bytes());
             // the LDS counters take their share only when they can be LDS counters
             // at all (otherwise they are global, cmode 2); no subtraction wraps
-            const size_t ctr_b = count ? size_t(P.n_ctr) * 4 : 0, reserve = std::min<size_t>(lds_max0 / 8, 8192);
+            const size_t ctr_b = count ? size_t(conn_lds_ctr_bytes(P.n_ctr)) : 0, reserve = std::min<size_t>(lds_max0 / 8, 8192);
             const size_t ctr_lds = ctr_b + reserve <= lds_max0 ? ctr_b : 0;
             const size_t cap = lds_max0 - reserve - ctr_lds;
             std::vector<size_t> order;
@@ -1436,13 +1436,16 @@ int connect_locked(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t* ou
     // ... and a batch that does not count needs only the ACLActions: one byte
     // per connection for both tuples (the words would be 8 B)
     const bool pre_res8 = !count && all_pair && !std::getenv("CONTIVCLS_CONN_PRE_WORDS");
+    // ... and a counting one u16 words when every counter index fits 14 bits
+    const uint32_t pre_bytes = pre_res8 ? 1u : pre_rules && P.n_ctr <= (1u << 14) &&
+                                                       !std::getenv("CONTIVCLS_CONN_PRE_WORDS") ? 2u : 4u;
     if (!big.empty()) {
         if (n > kClsChunk) return fail(e, CLS_E_INVAL, "connection batch above 2^30 with classifier ACLs");
-        HIPC(e, e->s_pre.ensure(big.size() * (pre_res8 ? stride : 2 * stride * 4)));
+        HIPC(e, e->s_pre.ensure(big.size() * (pre_res8 ? stride : 2 * stride * pre_bytes)));
         for (size_t b = 0; b < big.size(); ++b) {
             Table& t = *dtab[big[b]];
-            uint32_t* pre = pre_res8 ? reinterpret_cast<uint32_t*>(e->s_pre.as<uint8_t>() + b * stride)
-                                     : e->s_pre.as<uint32_t>() + b * 2 * stride;
+            uint32_t* pre = reinterpret_cast<uint32_t*>(e->s_pre.as<uint8_t>() +
+                                                        b * (pre_res8 ? stride : 2 * stride * pre_bytes));
             LaunchCfg cfg;
             cfg.stream = s;
             if (!k16) {
@@ -1467,7 +1470,7 @@ int connect_locked(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t* ou
                     HIPC(e, e->s_pq.ensure(size_t(cfg.grid) * std::max<uint32_t>(1, qcap) * 16));
                     HIPC(e, launch_classify4_pair(cd, od, o_at, syn, sp, pre, stride, e->s_pq.as<uint32_t>(), qcap,
                                                   pre_rules ? t.d_slot_rule.as<uint32_t>() : nullptr,
-                                                  desc[big[b]].ctr_off, pre_res8, cfg));
+                                                  desc[big[b]].ctr_off, pre_bytes, cfg));
                 } else {
                     cfg.other = cls4_dev(t.oimg, t.d_oimg, DevBuf(), 0, t.n_rules);
                     cfg.grid = cls_grid(e, true, t.lds_resident, t.img.lds_bytes, n);
@@ -1508,7 +1511,7 @@ int connect_locked(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t* ou
     const bool lds_rules = n && !pool.empty() && pool.size() <= lds_max && !(no_lds & 1);
     const size_t lds_used = lds_rules ? pool.size() : 0;
     int cmode = 0;
-    if (count && n_ctr) cmode = lds_used + size_t(n_ctr) * 4 <= lds_max && !(no_lds & 2) ? 1 : 2;
+    if (count && n_ctr) cmode = lds_used + conn_lds_ctr_bytes(n_ctr) <= lds_max && !(no_lds & 2) ? 1 : 2;
     a.ctr_lds = uint32_t(lds_used);
     // the call's tables, uploaded only when they differ from the last upload
     // (same bindings, same batch kind: nothing to copy)
@@ -1535,7 +1538,8 @@ int connect_locked(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t* ou
     a.pre = big.empty() ? nullptr : e->s_pre.as<uint32_t>();
     a.pre_stride = stride;
     a.pre_rules = pre_rules ? 1u : 0u;
-    a.pre_res8 = pre_res8 ? 1u : 0u;
+    a.pre_bytes = pre_bytes;
+    a.n_big = uint32_t(big.size());
     a.bm_steps = P.bm_steps;
     a.ifs = e->s_ifs.as<IfAcls>();
     a.rules = e->s_rules.p;
@@ -1544,7 +1548,7 @@ int connect_locked(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t* ou
         // the call counters are zero between calls (the scatter launch clears
         // what it moves); cleared here only when (re)allocated
         const size_t had = e->s_cctr.bytes;
-        HIPC(e, e->s_cctr.ensure(size_t(n_ctr) * 8));
+        HIPC(e, e->s_cctr.ensure(size_t(n_ctr) * 8 * kConnCtrCopies));
         if (e->s_cctr.bytes != had || !e->cctr_zero)
             HIPC(e, hipMemsetAsync(e->s_cctr.p, 0, e->s_cctr.bytes, s));
         // zero again only once the scatter launch (which clears what it
@@ -1569,53 +1573,112 @@ int connect_locked(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t* ou
     // allows, at most three (the kernel's registers allow 24 waves per CU);
     // where it allows only one, one 1024-thread workgroup.
     a.n_desc = uint32_t(desc.size());
-    size_t lds = lds_used + (cmode == 1 ? size_t(n_ctr) * 4 : 0);
-    const size_t meta_at = (lds + 15) & ~size_t(15);
     const size_t meta = desc.size() * sizeof(ConnDesc) + ifs.size() * sizeof(IfAcls);
-    a.meta_lds = 0xFFFFFFFFu;
-    // ... unless they would cost a workgroup per CU (the pool and counters
-    // alone leave room for two)
     auto per_cu_of = [&](size_t b) { return b ? std::max(1, std::min(3, int(lds_max / b))) : 3; };
-    if (meta_at + meta <= lds_max && per_cu_of(meta_at + meta) == per_cu_of(lds) && !(no_lds & 4)) {
-        a.meta_lds = uint32_t(meta_at);
-        lds = meta_at + meta;
-    }
-    int per_cu = per_cu_of(lds);
-    int block = per_cu >= 2 ? 512 : 1024;
-    // IPv4: the waves' job lists (512 B per wave) after the rest, when they
-    // cost no workgroup per CU; else the kernel's owner search and shuffles
+    // The launch's LDS plan for counters of ctr_b bytes: the descriptor and
+    // interface tables after the pool and counters unless they would cost a
+    // workgroup per CU, then (IPv4) the waves' job lists (512 B per wave) on
+    // the same terms -- else the kernel's owner search and shuffles
     // (CONTIVCLS_CONN_NO_JOBS: tests)
-    a.job_lds = 0xFFFFFFFFu;
-    const size_t job_at = (lds + 15) & ~size_t(15), job_b = size_t(block / 64) * 512;
-    if (!k16 && job_at + job_b <= lds_max && (per_cu == 1 || per_cu_of(job_at + job_b) == per_cu) &&
-        !std::getenv("CONTIVCLS_CONN_NO_JOBS")) {
-        a.job_lds = uint32_t(job_at);
-        lds = job_at + job_b;
+    struct LdsPlan {
+        size_t lds;
+        uint32_t meta_lds, job_lds;
+        int per_cu, block;
+    };
+    auto plan_of = [&](size_t ctr_b) {
+        LdsPlan q{lds_used + ctr_b, 0xFFFFFFFFu, 0xFFFFFFFFu, 0, 0};
+        const size_t meta_at = (q.lds + 15) & ~size_t(15);
+        if (meta_at + meta <= lds_max && per_cu_of(meta_at + meta) == per_cu_of(q.lds) && !(no_lds & 4)) {
+            q.meta_lds = uint32_t(meta_at);
+            q.lds = meta_at + meta;
+        }
+        q.per_cu = per_cu_of(q.lds);
+        q.block = q.per_cu >= 2 ? 512 : 1024;
+        const size_t job_at = (q.lds + 15) & ~size_t(15), job_b = size_t(q.block / 64) * 512;
+        if (!k16 && job_at + job_b <= lds_max && (q.per_cu == 1 || per_cu_of(job_at + job_b) == q.per_cu) &&
+            !std::getenv("CONTIVCLS_CONN_NO_JOBS")) {
+            q.job_lds = uint32_t(job_at);
+            q.lds = job_at + job_b;
+        }
+        return q;
+    };
+    // LDS counters: u32, or u16 pairs (half the LDS, a bound on a workgroup's
+    // connections) when those fit where u32 do not, or hold more workgroups
+    // per CU, or make room for the job lists (CONTIVCLS_CONN_CTR16=0/1: tests)
+    LdsPlan plan = plan_of(cmode == 1 ? conn_lds_ctr_bytes(n_ctr) : 0);
+    a.ctr16 = cmode == 1 ? 1u : 0u;
+    if (cmode == 1) {
+        const LdsPlan p32 = plan_of(size_t(n_ctr) * 4);
+        const char* c16 = std::getenv("CONTIVCLS_CONN_CTR16");
+        const bool use32 = c16 ? c16[0] == '0'
+                               : p32.lds <= lds_max && p32.per_cu >= plan.per_cu &&
+                                     (p32.job_lds != 0xFFFFFFFFu || plan.job_lds == 0xFFFFFFFFu);
+        if (use32 && p32.lds <= lds_max) {
+            plan = p32;
+            a.ctr16 = 0u;
+        }
+    }
+    size_t lds = plan.lds;
+    a.meta_lds = plan.meta_lds;
+    a.job_lds = plan.job_lds;
+    const int per_cu = plan.per_cu, block = plan.block;
+    // Persistent grid: as many 512-thread workgroups per CU as the LDS
+    // allows, at most three (the kernel's registers allow 24 waves per CU);
+    // where it allows only one, one 1024-thread workgroup.  u16 counters: at
+    // most kConnWgConns connections per workgroup -- a larger batch runs k
+    // full rounds of the resident grid (equal workgroups, no partial round)
+    const uint64_t resident = uint64_t(e->n_cu) * per_cu;
+    uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>(resident, (n + block - 1) / block));
+    if (a.ctr16) {
+        const uint64_t per_wg = uint64_t(kConnWgConns / block) * block;
+        if (n > grid * per_wg) grid = resident * ((n + resident * per_wg - 1) / (resident * per_wg));
     }
     if (std::getenv("CONTIVCLS_DEBUG_CONN")) {              // diagnostics: the launch's LDS plan
         size_t nbm = 0;
         for (const ConnDesc& d : desc) nbm += d.bm_off != 0xFFFFFFFFu;
         std::fprintf(stderr, "connect: n %llu desc %zu big %zu bitmaps %zu pool %zu lds_rules %d ctr %u cmode %d "
-                     "meta %s jobs %s lds %zu per_cu %d block %d bm_steps %u\n", (unsigned long long)n, desc.size(),
+                     "meta %s jobs %s lds %zu ctr16 %u per_cu %d block %d grid %llu bm_steps %u\n", (unsigned long long)n, desc.size(),
                      big.size(), nbm, pool.size(), int(lds_rules), n_ctr, cmode,
                      a.meta_lds != 0xFFFFFFFFu ? "lds" : "global", a.job_lds != 0xFFFFFFFFu ? "lds" : "shuffle", lds,
-                     per_cu, block, P.bm_steps);
+                     a.ctr16, per_cu, block, (unsigned long long)grid, P.bm_steps);
     }
-    const int grid = int(std::max<uint64_t>(1, std::min<uint64_t>(uint64_t(e->n_cu) * per_cu,
-                                                                  (n + block - 1) / block)));
-    HIPC(e, launch_connect(a, k16, lds_rules, cmode, grid, block, lds, s));
+    // LDS counters leave the launch as one row per workgroup, summed into the
+    // tables' counters by the rows launch (CONTIVCLS_CONN_FLUSH_ATOMIC: device
+    // atomics into the copies of the call counters and the scatter launch,
+    // tests)
+    const uint32_t nw = a.ctr16 ? (n_ctr + 1u) / 2u : n_ctr;
+    a.ctr_rows = nullptr;
+    if (cmode == 1 && n && !std::getenv("CONTIVCLS_CONN_FLUSH_ATOMIC")) {
+        HIPC(e, e->s_crows.ensure(size_t(grid) * nw * 4));
+        a.ctr_rows = e->s_crows.as<uint32_t>();
+    }
+    HIPC(e, launch_connect(a, k16, lds_rules, cmode, int(grid), block, lds, s));
     if (cmode && n) {
         uint32_t max_rules = 0;
         for (const ConnDesc& d : desc) max_rules = std::max(max_rules, d.n_rules);
-        HIPC(e, launch_conn_scatter(a.desc, e->s_tctr.as<unsigned long long* const>(), uint32_t(desc.size()),
-                                    max_rules, e->s_cctr.as<unsigned long long>(), s));
+        if (a.ctr_rows) {
+            HIPC(e, launch_conn_rows(a.ctr_rows, uint32_t(grid), nw, a.ctr16 != 0, n_ctr, a.desc,
+                                     uint32_t(desc.size()), e->s_tctr.as<unsigned long long* const>(), s));
+        } else {
+            HIPC(e, launch_conn_scatter(a.desc, e->s_tctr.as<unsigned long long* const>(), uint32_t(desc.size()),
+                                        max_rules, e->s_cctr.as<unsigned long long>(), kConnCtrCopies, true, n_ctr,
+                                        s));
+        }
         e->cctr_zero = true;
         // cls_conn_counters waits for this batch's scatter, not the device
-        for (size_t j = 0; j < dtab.size(); ++j) {
-            Table& t = *dtab[j];
-            if (!t.conn_ev) HIPC(e, hipEventCreateWithFlags(&t.conn_ev, hipEventDisableTiming));
-            HIPC(e, hipEventRecord(t.conn_ev, s));
+        std::shared_ptr<SharedEvent> ev;
+        for (auto& x : e->conn_evs)
+            if (x.use_count() == 1) {
+                ev = x;
+                break;
+            }
+        if (!ev) {
+            ev = std::make_shared<SharedEvent>();
+            HIPC(e, hipEventCreateWithFlags(&ev->ev, hipEventDisableTiming));
+            e->conn_evs.push_back(ev);
         }
+        HIPC(e, hipEventRecord(ev->ev, s));
+        for (size_t j = 0; j < dtab.size(); ++j) dtab[j]->conn_ev = ev;
     } else if (cmode) {
         e->cctr_zero = true;            // n == 0: nothing was counted
     }
@@ -1670,7 +1733,7 @@ static int conn_counters_dev(cls_engine* d, uint32_t table_id, std::vector<uint6
     HIPC(d, hipSetDevice(d->device));
     const size_t bytes = size_t(t.n_rules + 1) * 8;
     std::vector<uint64_t> h(t.n_rules + 1);
-    if (t.conn_ev) HIPC(d, hipStreamWaitEvent(d->stream, t.conn_ev, 0));
+    if (t.conn_ev) HIPC(d, hipStreamWaitEvent(d->stream, t.conn_ev->ev, 0));
     if (t.conn_ctr_ev) HIPC(d, hipStreamWaitEvent(d->stream, t.conn_ctr_ev, 0));
     HIPC(d, hipMemcpyAsync(h.data(), t.d_conn_ctr.p, bytes, hipMemcpyDeviceToHost, d->stream));
     if (reset) HIPC(d, hipMemsetAsync(t.d_conn_ctr.p, 0, bytes, d->stream));

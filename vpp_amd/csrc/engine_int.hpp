@@ -66,6 +66,17 @@ struct Counters {
     }
 };
 
+// An event shared by the tables of one counting connection batch.
+struct SharedEvent {
+    hipEvent_t ev = nullptr;
+    SharedEvent() = default;
+    SharedEvent(const SharedEvent&) = delete;
+    SharedEvent& operator=(const SharedEvent&) = delete;
+    ~SharedEvent() {
+        if (ev) (void)hipEventDestroy(ev);
+    }
+};
+
 struct Table {
     std::string name;
     uint32_t n_rules = 0;
@@ -108,14 +119,14 @@ struct Table {
     // counting connection batch on another stream waits for it
     hipEvent_t conn_ctr_ev = nullptr;
     // recorded behind the last counting connection batch's scatter into
-    // d_conn_ctr: cls_conn_counters waits for it (not for the whole device)
-    hipEvent_t conn_ev = nullptr;
+    // d_conn_ctr: cls_conn_counters waits for it (not for the whole device);
+    // one event per batch, shared by the batch's tables
+    std::shared_ptr<SharedEvent> conn_ev;
     // bumped whenever the connection counters are cleared by a rebind (a
     // multi-device engine's peers clear their copies when it moves)
     uint64_t conn_epoch = 0;
     ~Table() {
         if (conn_ctr_ev) (void)hipEventDestroy(conn_ctr_ev);
-        if (conn_ev) (void)hipEventDestroy(conn_ev);
     }
     // declared last: destroyed first, so pending device work is waited for
     // before any of the buffers above are freed
@@ -165,7 +176,11 @@ struct cls_engine {
     DevBuf s_pre;                  // connection path: classifier slot words per large ACL (8 bytes/connection)
     DevBuf s_pq;                   // connection path: the pair launch's OTHER queue
     DevBuf s_rules, s_tctr, s_cctr;  // connection path: rule pool, table counter pointers, call counters
+    DevBuf s_crows;                  // ... LDS counter rows of the workgroups
     bool cctr_zero = false;          // s_cctr cleared since its allocation (the scatter launch keeps it zero)
+    // counting connection batches' scatter events (Table::conn_ev), reused
+    // once no table holds them: one record per batch, not one per table
+    std::vector<std::shared_ptr<SharedEvent>> conn_evs;
     uint64_t conn_gen = 0;           // bumped by every change of tables or interface bindings
     ConnPlan conn_plan;              // the last device batch's plan
     uint64_t plan_ids = 0, up_plan = ~0ull;   // plan ids; the plan whose tables are on the device

@@ -29,7 +29,7 @@ __global__ __launch_bounds__(kClsBlock) void classify4_pair(Cls4Dev t, Cls4Dev o
                                                             const uint16_t* sport, uint32_t* out, uint64_t stride,
                                                             uint32_t* oq, uint32_t oq_seg, uint32_t q_lds,
                                                             const uint32_t* slot_rule, uint32_t ctr_base,
-                                                            uint32_t res8) {
+                                                            uint32_t wbytes) {
     extern __shared__ uint4 smem[];
     typedef __attribute__((address_space(3))) uint32_t* lctr_t;
     const uint32_t lane = __lane_id();
@@ -72,10 +72,15 @@ __global__ __launch_bounds__(kClsBlock) void classify4_pair(Cls4Dev t, Cls4Dev o
     const Img<false> og{reinterpret_cast<const uint8_t*>(o.img)};
     // a word's payload: the slot, or (counting) its counter index
     auto key = [&](uint32_t slot) { return slot_rule ? ctr_base + slot_rule[slot] : slot; };
-    // one connection's two words, or (res8) its two results in one byte
+    // one connection's two words: u32, u16 (wbytes 2: the host keeps the
+    // counter indices below 2^14), or (wbytes 1) its two results in one byte
+    uint16_t* const out16 = reinterpret_cast<uint16_t*>(out);
     auto put = [&](uint32_t i, uint32_t w0, uint32_t w1) {
-        if (res8) {
+        if (wbytes == 1u) {
             reinterpret_cast<uint8_t*>(out)[i] = uint8_t((w0 & 3u) | (w1 & 3u) << 2);
+        } else if (wbytes == 2u) {
+            out16[i] = uint16_t(w0);
+            out16[stride + i] = uint16_t(w1);
         } else {
             out[i] = w0;
             out[stride + i] = w1;
@@ -146,11 +151,14 @@ __global__ __launch_bounds__(kClsBlock) void classify4_pair(Cls4Dev t, Cls4Dev o
                         other2(s8[q], d8[q], p8[q], p8[4 + q], w0[q], w1[q]);
                 }
         }
-        if (res8) {                                     // both results of the 4 connections: 4 bytes
+        if (wbytes == 1u) {                             // both results of the 4 connections: 4 bytes
             uint32_t v = 0;
 #pragma unroll
             for (int q = 0; q < 4; ++q) v |= ((w0[q] & 3u) | (w1[q] & 3u) << 2) << (8 * q);
             reinterpret_cast<uint32_t*>(out)[g] = v;
+        } else if (wbytes == 2u) {                      // 4 u16 words per tuple: 8 bytes each
+            reinterpret_cast<uint2*>(out16)[g] = make_uint2(w0[0] | w0[1] << 16, w0[2] | w0[3] << 16);
+            reinterpret_cast<uint2*>(out16 + stride)[g] = make_uint2(w1[0] | w1[1] << 16, w1[2] | w1[3] << 16);
         } else {
             OS[g] = make_uint4(w0[0], w0[1], w0[2], w0[3]);
             OA[g] = make_uint4(w1[0], w1[1], w1[2], w1[3]);
@@ -187,12 +195,12 @@ __global__ __launch_bounds__(kClsBlock) void classify4_pair(Cls4Dev t, Cls4Dev o
 template <int kMode, int kList, int kD>
 void launch_pair_d(const Cls4Dev& t, const Cls4Dev& o, uint32_t o_at, const Pkts4& p, const uint16_t* sport,
                    uint32_t* out, uint64_t stride, uint32_t* oq, uint32_t oq_cap, const uint32_t* slot_rule,
-                   uint32_t ctr_base, bool res8, const LaunchCfg& cfg) {
+                   uint32_t ctr_base, uint32_t wbytes, const LaunchCfg& cfg) {
     const uint32_t q_lds = ((o_at ? o_at + o.img_bytes : t.img_bytes) + 15u) & ~15u;   // the queue fill word
     const size_t lds = q_lds + 16u;
     lds_attr(reinterpret_cast<const void*>(classify4_pair<kMode, kList, kD>), lds);
     hipLaunchKernelGGL((classify4_pair<kMode, kList, kD>), dim3(cfg.grid), dim3(kClsBlock), lds, cfg.stream, t, o,
-                       o_at, p, sport, out, stride, oq, oq_cap, q_lds, slot_rule, ctr_base, uint32_t(res8));
+                       o_at, p, sport, out, stride, oq, oq_cap, q_lds, slot_rule, ctr_base, wbytes);
 }
 
 // sublist modes: the search depth as a template argument (the rendered
@@ -200,31 +208,31 @@ void launch_pair_d(const Cls4Dev& t, const Cls4Dev& o, uint32_t o_at, const Pkts
 template <int kMode, int kList>
 void launch_pair(const Cls4Dev& t, const Cls4Dev& o, uint32_t o_at, const Pkts4& p, const uint16_t* sport,
                  uint32_t* out, uint64_t stride, uint32_t* oq, uint32_t oq_cap, const uint32_t* slot_rule,
-                 uint32_t ctr_base, bool res8, const LaunchCfg& cfg) {
+                 uint32_t ctr_base, uint32_t wbytes, const LaunchCfg& cfg) {
     if constexpr (kMode == 2 && (kList == 3 || kList == 4)) {
         switch (t.bv_steps) {
-        case 0: launch_pair_d<kMode, kList, 0>(t, o, o_at, p, sport, out, stride, oq, oq_cap, slot_rule, ctr_base, res8, cfg); return;
-        case 1: launch_pair_d<kMode, kList, 1>(t, o, o_at, p, sport, out, stride, oq, oq_cap, slot_rule, ctr_base, res8, cfg); return;
-        case 2: launch_pair_d<kMode, kList, 2>(t, o, o_at, p, sport, out, stride, oq, oq_cap, slot_rule, ctr_base, res8, cfg); return;
-        case 3: launch_pair_d<kMode, kList, 3>(t, o, o_at, p, sport, out, stride, oq, oq_cap, slot_rule, ctr_base, res8, cfg); return;
-        case 4: launch_pair_d<kMode, kList, 4>(t, o, o_at, p, sport, out, stride, oq, oq_cap, slot_rule, ctr_base, res8, cfg); return;
-        case 5: launch_pair_d<kMode, kList, 5>(t, o, o_at, p, sport, out, stride, oq, oq_cap, slot_rule, ctr_base, res8, cfg); return;
+        case 0: launch_pair_d<kMode, kList, 0>(t, o, o_at, p, sport, out, stride, oq, oq_cap, slot_rule, ctr_base, wbytes, cfg); return;
+        case 1: launch_pair_d<kMode, kList, 1>(t, o, o_at, p, sport, out, stride, oq, oq_cap, slot_rule, ctr_base, wbytes, cfg); return;
+        case 2: launch_pair_d<kMode, kList, 2>(t, o, o_at, p, sport, out, stride, oq, oq_cap, slot_rule, ctr_base, wbytes, cfg); return;
+        case 3: launch_pair_d<kMode, kList, 3>(t, o, o_at, p, sport, out, stride, oq, oq_cap, slot_rule, ctr_base, wbytes, cfg); return;
+        case 4: launch_pair_d<kMode, kList, 4>(t, o, o_at, p, sport, out, stride, oq, oq_cap, slot_rule, ctr_base, wbytes, cfg); return;
+        case 5: launch_pair_d<kMode, kList, 5>(t, o, o_at, p, sport, out, stride, oq, oq_cap, slot_rule, ctr_base, wbytes, cfg); return;
         default: break;
         }
     }
-    launch_pair_d<kMode, kList, -1>(t, o, o_at, p, sport, out, stride, oq, oq_cap, slot_rule, ctr_base, res8, cfg);
+    launch_pair_d<kMode, kList, -1>(t, o, o_at, p, sport, out, stride, oq, oq_cap, slot_rule, ctr_base, wbytes, cfg);
 }
 
 }  // namespace
 
 hipError_t launch_classify4_pair(const Cls4Dev& t, const Cls4Dev& o, uint32_t o_at, const Pkts4& p,
                                  const uint16_t* sport, uint32_t* out, uint64_t stride, uint32_t* oq,
-                                 uint32_t oq_cap, const uint32_t* slot_rule, uint32_t ctr_base, bool res8,
+                                 uint32_t oq_cap, const uint32_t* slot_rule, uint32_t ctr_base, uint32_t wbytes,
                                  const LaunchCfg& cfg) {
     if (!cls_dispatchable(t, true, false) || o.mode != 0 || o.list_mode != 0) return hipErrorInvalidValue;
     const int src = src_variant(t);
 #define PAIR_CASE(S, M, L) \
-    case 8 * S + L: launch_pair<M, L>(t, o, o_at, p, sport, out, stride, oq, oq_cap, slot_rule, ctr_base, res8, cfg); break;
+    case 8 * S + L: launch_pair<M, L>(t, o, o_at, p, sport, out, stride, oq, oq_cap, slot_rule, ctr_base, wbytes, cfg); break;
     switch (8 * src + int(t.list_mode)) {
         PAIR_CASE(0, 0, 0) PAIR_CASE(0, 0, 1) PAIR_CASE(0, 0, 2) PAIR_CASE(0, 0, 3) PAIR_CASE(0, 0, 4)
         PAIR_CASE(0, 0, 5) PAIR_CASE(0, 0, 6)

@@ -557,6 +557,12 @@ __device__ __forceinline__ uint32_t conn_bm(const ConnArgs& a, const ConnDesc& D
 // kJobs (IPv4): the waves' job lists in LDS (a.job_lds); else the owner
 // search and shuffles (16-byte batches, and IPv4 launches whose LDS is
 // full: the job lists would displace LDS counters or bitmap forms)
+#ifndef CONN_LEAD_ROUNDS
+#define CONN_LEAD_ROUNDS 0
+#endif
+#ifndef CONN_NO_EARLY
+#define CONN_NO_EARLY 0
+#endif
 template <bool k16, bool kLdsRules, int kCount, bool kJobs>
 __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(6))) void connect_kernel(ConnArgs a) {
     typedef typename ConnT<k16>::A A;
@@ -564,8 +570,11 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(6))) void 
     typedef __attribute__((address_space(3))) uint32_t* lctr_t;
     if constexpr (kLdsRules) lds_copy(smem, static_cast<const uint4*>(a.rules), a.rules_bytes / 16u);
     if constexpr (kCount == 1) {
-        for (uint32_t j = threadIdx.x; j < a.n_ctr; j += blockDim.x) *lctr_t(a.ctr_lds + 4u * j) = 0u;
+        const uint32_t nw = a.ctr16 ? (a.n_ctr + 1u) / 2u : a.n_ctr;
+        for (uint32_t j = threadIdx.x; j < nw; j += blockDim.x) *lctr_t(a.ctr_lds + 4u * j) = 0u;
     }
+    // this workgroup's copy of the call counters
+    unsigned long long* const gctr = a.ctr + uint64_t(blockIdx.x % kConnCtrCopies) * a.n_ctr;
     if (a.meta_lds != 0xFFFFFFFFu) {
         const uint32_t nd = a.n_desc * uint32_t(sizeof(ConnDesc)) / 4u;
         const uint32_t* gd = reinterpret_cast<const uint32_t*>(a.desc);
@@ -592,10 +601,32 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(6))) void 
         const uint32_t i = it * nthreads + blockIdx.x * blockDim.x + threadIdx.x;
         const bool live = i < n;
         const uint32_t ic = live ? i : 0u;                      // loads stay in bounds
-        // every field's load first, together
+        // every field's load first, together -- with the large ACLs' result
+        // words when there are at most kConnEarlyBlocks of them (wave-uniform)
         const uint32_t si = *at(a.src_if, ic), dj = *at(a.dst_if, ic);
         const A sa = *at(src, ic), da = *at(dst, ic);
         const uint32_t sp = *at(a.sport, ic), dp = *at(a.dport, ic), pr = *at(a.proto, ic);
+        const bool early = !CONN_NO_EARLY && a.n_big <= kConnEarlyBlocks;
+        uint32_t ew[kConnEarlyBlocks][2] = {};                 // [block][SYN, SYN-ACK]
+        if (early) {
+#pragma unroll
+            for (uint32_t b = 0; b < kConnEarlyBlocks; ++b)
+                if (b < a.n_big) {
+                    if (a.pre_bytes == 1u) {
+                        const uint32_t x = reinterpret_cast<const uint8_t*>(a.pre)[uint64_t(b) * stride + ic];
+                        ew[b][0] = x;
+                        ew[b][1] = x >> 2;
+                    } else if (a.pre_bytes == 2u) {
+                        const uint16_t* p16 = reinterpret_cast<const uint16_t*>(a.pre) + uint64_t(2u * b) * stride + ic;
+                        ew[b][0] = p16[0];
+                        ew[b][1] = p16[stride];
+                    } else {
+                        const uint32_t* p32 = a.pre + uint64_t(2u * b) * stride + ic;
+                        ew[b][0] = p32[0];
+                        ew[b][1] = p32[stride];
+                    }
+                }
+        }
         const bool ok = live && si < a.n_ifs && dj < a.n_ifs;   // unknown interface id: Failure
         // both lookups unconditional (an in-range index), the unknown case selected after
         const IfAcls S0 = conn_if(a, ok ? si : 0u), D0 = conn_if(a, ok ? dj : 0u);
@@ -611,11 +642,16 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(6))) void 
         uint32_t w[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k)
-            w[k] = a.pre_res8 ? uint32_t(bi[k] >= 0 ? reinterpret_cast<const uint8_t*>(a.pre)[uint64_t(uint32_t(bi[k])) *
-                                                                                           stride + ic]
-                                                   : 0u) >> (2 * (k >> 1))
-                              : *(bi[k] >= 0 ? a.pre + (uint64_t(2u * uint32_t(bi[k]) + uint32_t(k >> 1)) * stride + ic)
-                                             : at(a.src_if, ic));
+            w[k] = early ? (bi[k] == 1 ? ew[1][k >> 1] : ew[0][k >> 1])
+                 : a.pre_bytes == 1u
+                       ? uint32_t(*(bi[k] >= 0 ? reinterpret_cast<const uint8_t*>(a.pre) + uint64_t(uint32_t(bi[k])) * stride + ic
+                                               : reinterpret_cast<const uint8_t*>(a.src_if) + ic)) >> (2 * (k >> 1))
+                   : a.pre_bytes == 2u
+                       ? uint32_t(*(bi[k] >= 0 ? reinterpret_cast<const uint16_t*>(a.pre) +
+                                                     (uint64_t(2u * uint32_t(bi[k]) + uint32_t(k >> 1)) * stride + ic)
+                                               : reinterpret_cast<const uint16_t*>(a.src_if) + ic))
+                       : *(bi[k] >= 0 ? a.pre + (uint64_t(2u * uint32_t(bi[k]) + uint32_t(k >> 1)) * stride + ic)
+                                      : at(a.src_if, ic));
         // ---- the jobs of the wave, packed ----
         // job j of the wave is call k of owner lane o: the ballots of the four
         // calls give every job a rank; the jobs run 64 at a time, every lane
@@ -760,21 +796,56 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(6))) void 
                 // (aggregating a wave's equal keys first measured slower:
                 // 136.5 -> 142.5 us at 12 local ACLs, profiles/r04l_conn_ab.txt)
 #pragma unroll
-                for (int k = 0; k < 4; ++k)
-                    if (key[k] != 0xFFFFFFFFu)
-                        __hip_atomic_fetch_add(lctr_t(a.ctr_lds + 4u * key[k]), 1u, __ATOMIC_RELAXED,
+                for (int k = 0; k < 4; ++k) {
+                    uint32_t kk = key[k], add = 1u;
+#if CONN_LEAD_ROUNDS
+                    // same-address LDS atomics serialise: the lanes holding
+                    // the first active lane's key add once, by that lane
+#pragma unroll
+                    for (int round = 0; round < CONN_LEAD_ROUNDS; ++round) {
+                        const uint64_t act = __ballot(kk != 0xFFFFFFFFu && add == 1u);
+                        if (act) {
+                            const int leader = int(__builtin_ctzll(act));
+                            const uint32_t sk = uint32_t(__builtin_amdgcn_readlane(int(kk), leader));
+                            const uint64_t same = __ballot(kk == sk && add == 1u);
+                            if (kk == sk && add == 1u) {
+                                if (int(lane) == leader) add = uint32_t(__popcll(same));
+                                else kk = 0xFFFFFFFFu;
+                            }
+                        }
+                    }
+#endif
+                    if (kk != 0xFFFFFFFFu)
+                        __hip_atomic_fetch_add(lctr_t(a.ctr_lds + 4u * (a.ctr16 ? kk >> 1 : kk)),
+                                               a.ctr16 ? add << (16u * (kk & 1u)) : add, __ATOMIC_RELAXED,
                                                __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
             } else {
 #pragma unroll
-                for (int k = 0; k < 4; ++k) wave_count(a.ctr, key[k]);
+                for (int k = 0; k < 4; ++k) wave_count(gctr, key[k]);
             }
         }
     }
     if constexpr (kCount == 1) {
         __syncthreads();
-        for (uint32_t j = threadIdx.x; j < a.n_ctr; j += blockDim.x) {
-            const uint32_t c = *lctr_t(a.ctr_lds + 4u * j);
-            if (c) atomicAdd(&a.ctr[j], (unsigned long long)c);
+        if (a.ctr_rows) {
+            // the words as this workgroup's row: plain coalesced stores, summed
+            // by the rows launch (device atomics from every workgroup at the
+            // end of the launch serialise per address)
+            const uint32_t nw = a.ctr16 ? (a.n_ctr + 1u) / 2u : a.n_ctr;
+            uint32_t* row = a.ctr_rows + uint64_t(blockIdx.x) * nw;
+            for (uint32_t j = threadIdx.x; j < nw; j += blockDim.x) row[j] = *lctr_t(a.ctr_lds + 4u * j);
+        } else if (a.ctr16) {
+            for (uint32_t j = threadIdx.x; j < (a.n_ctr + 1u) / 2u; j += blockDim.x) {
+                const uint32_t c = *lctr_t(a.ctr_lds + 4u * j);
+                if (c & 0xFFFFu) atomicAdd(&gctr[2u * j], (unsigned long long)(c & 0xFFFFu));
+                if (c >> 16) atomicAdd(&gctr[2u * j + 1u], (unsigned long long)(c >> 16));
+            }
+        } else {
+            for (uint32_t j = threadIdx.x; j < a.n_ctr; j += blockDim.x) {
+                const uint32_t c = *lctr_t(a.ctr_lds + 4u * j);
+                if (c) atomicAdd(&gctr[j], (unsigned long long)c);
+            }
         }
     }
 }
@@ -785,16 +856,62 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(6))) void 
 // 256 y .. 256 y + 255 -- one counter per thread, not a loop per table.
 __global__ __launch_bounds__(256) void conn_scatter_kernel(const ConnDesc* __restrict__ desc,
                                                            unsigned long long* const* __restrict__ table_ctr,
-                                                           unsigned long long* __restrict__ call_ctr) {
+                                                           unsigned long long* __restrict__ call_ctr,
+                                                           uint32_t n_slabs, uint32_t clear, uint32_t n_ctr) {
     const ConnDesc D = desc[blockIdx.x];
     const uint32_t r = blockIdx.y * blockDim.x + threadIdx.x;
     if (r > D.n_rules) return;
-    const unsigned long long v = call_ctr[D.ctr_off + r];
-    if (v) {
-        atomicAdd(&table_ctr[blockIdx.x][r], v);
-        call_ctr[D.ctr_off + r] = 0ull;
+    unsigned long long v = 0;
+#pragma unroll 16
+    for (uint32_t c = 0; c < n_slabs; ++c) {                // the slabs: copies or partial sums
+        unsigned long long* p = call_ctr + uint64_t(c) * n_ctr + D.ctr_off + r;
+        const unsigned long long x = *p;
+        v += x;
+        if (clear && x) *p = 0ull;
+    }
+    if (v) atomicAdd(&table_ctr[blockIdx.x][r], v);
+}
+
+// Rows -> the tables' connection counters: thread (word w, slab g) sums word
+// w over rows g kConnRowsPerSlab .. + kConnRowsPerSlab - 1 (the loads in
+// flight together, coalesced over w) and adds each nonzero counter of the
+// word to its table's counter (the descriptor found by bisection over the
+// ascending counter bases) -- at most one add per slab and counter.
+__device__ __forceinline__ void conn_ctr_add(const ConnDesc* __restrict__ desc, uint32_t n_desc,
+                                             unsigned long long* const* __restrict__ table_ctr, uint32_t c,
+                                             unsigned long long v) {
+    uint32_t lo = 0, hi = n_desc;                    // the last descriptor with ctr_off <= c
+    while (hi - lo > 1u) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (desc[mid].ctr_off <= c) lo = mid;
+        else hi = mid;
+    }
+    atomicAdd(&table_ctr[lo][c - desc[lo].ctr_off], v);
+}
+__global__ __launch_bounds__(256) void conn_rows_kernel(const uint32_t* __restrict__ rows, uint32_t n_rows,
+                                                        uint32_t nw, uint32_t ctr16, uint32_t n_ctr,
+                                                        const ConnDesc* __restrict__ desc, uint32_t n_desc,
+                                                        unsigned long long* const* __restrict__ table_ctr) {
+    const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= nw) return;
+    const uint32_t r0 = blockIdx.y * kConnRowsPerSlab;
+    uint32_t x[kConnRowsPerSlab];
+#pragma unroll
+    for (uint32_t k = 0; k < kConnRowsPerSlab; ++k) x[k] = r0 + k < n_rows ? rows[uint64_t(r0 + k) * nw + w] : 0u;
+    unsigned long long lo = 0, hi = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kConnRowsPerSlab; ++k) {
+        lo += ctr16 ? (x[k] & 0xFFFFu) : x[k];
+        hi += x[k] >> 16;
+    }
+    if (ctr16) {
+        if (lo) conn_ctr_add(desc, n_desc, table_ctr, 2u * w, lo);
+        if (hi && 2u * w + 1u < n_ctr) conn_ctr_add(desc, n_desc, table_ctr, 2u * w + 1u, hi);
+    } else if (lo) {
+        conn_ctr_add(desc, n_desc, table_ctr, w, lo);
     }
 }
+
 
 constexpr uint64_t kGolden = 0x9E3779B97F4A7C15ull;
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {
@@ -997,11 +1114,21 @@ hipError_t launch_connect(const ConnArgs& a, bool k16, bool lds_rules, int count
     return hipErrorInvalidValue;
 }
 
+hipError_t launch_conn_rows(const uint32_t* rows, uint32_t n_rows, uint32_t nw, bool ctr16, uint32_t n_ctr,
+                            const ConnDesc* desc, uint32_t n_desc, unsigned long long* const* table_ctr,
+                            hipStream_t s) {
+    if (n_rows == 0 || nw == 0 || n_desc == 0) return hipSuccess;
+    hipLaunchKernelGGL(conn_rows_kernel, dim3((nw + 255u) / 256u, (n_rows + kConnRowsPerSlab - 1u) / kConnRowsPerSlab),
+                       dim3(256), 0, s, rows, n_rows, nw, ctr16 ? 1u : 0u, n_ctr, desc, n_desc, table_ctr);
+    return hipGetLastError();
+}
+
 hipError_t launch_conn_scatter(const ConnDesc* desc, unsigned long long* const* table_ctr, uint32_t n_desc,
-                               uint32_t max_rules, unsigned long long* call_ctr, hipStream_t s) {
+                               uint32_t max_rules, unsigned long long* call_ctr, uint32_t n_slabs, bool clear,
+                               uint32_t n_ctr, hipStream_t s) {
     if (n_desc == 0) return hipSuccess;
     hipLaunchKernelGGL(conn_scatter_kernel, dim3(n_desc, max_rules / 256u + 1u), dim3(256), 0, s, desc, table_ctr,
-                       call_ctr);
+                       call_ctr, n_slabs, clear ? 1u : 0u, n_ctr);
     return hipGetLastError();
 }
 

@@ -182,12 +182,14 @@ hipError_t launch_classify16_slots(const Cls4Dev& t, const Fe16& fe, const Pkts1
 // Needs 16-B aligned src / dst / out / out + stride, 8-B dport / sport, 4-B
 // proto; stride a multiple of 4.
 // slot_rule (may be null): write each word's counter index ctr_base +
-// slot_rule[slot] in place of the slot (counting connection batches); res8
-// (batches that do not count): only the two ACLActions, one byte per
-// connection (SYN result | SYN-ACK result << 2) at out, 1/8 of the words' bytes
+// slot_rule[slot] in place of the slot (counting connection batches).
+// wbytes: 4 -- u32 words (SYN at out[i], SYN-ACK at out[stride + i]); 2 --
+// u16 words at the same element offsets (counter indices < 2^14); 1 -- only
+// the two ACLActions, one byte per connection (SYN result | SYN-ACK result
+// << 2) at byte i (batches that do not count)
 hipError_t launch_classify4_pair(const Cls4Dev& t, const Cls4Dev& o, uint32_t o_at, const Pkts4& p,
                                  const uint16_t* sport, uint32_t* out, uint64_t stride, uint32_t* oq,
-                                 uint32_t oq_cap, const uint32_t* slot_rule, uint32_t ctr_base, bool res8,
+                                 uint32_t oq_cap, const uint32_t* slot_rule, uint32_t ctr_base, uint32_t wbytes,
                                  const LaunchCfg& cfg);
 // The OTHER queue segment of one pair-launch workgroup (kPairBlock threads)
 // that holds every connection its lanes visit, 4 per lane per step, in 16-B
@@ -227,6 +229,19 @@ static_assert(sizeof(ConnDesc) == 48 && sizeof(IfAcls) == 16, "connect_kernel re
 // rule i matches that interval's addresses (ports); the first match is the
 // lowest set bit of src row & dst row & protocol row.
 constexpr uint32_t kConnBmHeader = 32;
+// Connection counting: the call counters come in kConnCtrCopies copies, so
+// that the workgroups' end-of-launch adds to a popular counter spread over
+// that many addresses (same-address device atomics serialise); the scatter
+// launch sums the copies.  LDS counters are u16 pairs: a workgroup takes at
+// most kConnWgConns connections per launch (4 calls each stay below 2^16).
+// Connection batches with at most this many large ACLs load every one's
+// result words together with the connection's fields (no second dependent
+// global round trip behind the interface lookup).
+constexpr uint32_t kConnEarlyBlocks = 2;
+constexpr uint32_t kConnCtrCopies = 16;
+constexpr uint32_t kConnWgConns = 16383;
+__host__ __device__ constexpr uint32_t conn_lds_ctr_bytes(uint32_t n_ctr) { return (n_ctr + 1u) / 2u * 4u; }
+
 struct ConnArgs {
     const ConnDesc* desc;
     const IfAcls* ifs;
@@ -234,8 +249,14 @@ struct ConnArgs {
     const void* rules;           // ConnRule4 / ConnRule16 pool (global memory)
     uint32_t rules_bytes;        // staged into LDS at address 0 when the launch says so
     uint32_t n_ctr;              // counting: counter space (sum of R + 1 over the descriptors)
-    uint32_t ctr_lds;            // counting: LDS byte offset of the u32 counters (LDS variant)
-    unsigned long long* ctr;     // counting: the call's u64 counters (n_ctr)
+    uint32_t ctr_lds;            // counting: LDS byte offset of the counters (LDS variant; u16
+                                 // pairs: counter j in half j & 1 of word j >> 1, a workgroup
+                                 // evaluates at most kConnWgConns connections per launch)
+    uint32_t ctr16;              // counting, LDS variant: u16 counter pairs (else u32 counters)
+    uint32_t* ctr_rows;          // counting, LDS variant: workgroup b stores its LDS counter words
+                                 // as row b (null: device atomics into the copies of ctr)
+    unsigned long long* ctr;     // counting: the call's u64 counters, kConnCtrCopies copies of
+                                 // n_ctr (workgroup b adds to copy b % kConnCtrCopies)
     const uint32_t* src_if;
     const uint32_t* dst_if;
     const void* src;             // u32 host order, or 16-B network-order addresses
@@ -250,9 +271,13 @@ struct ConnArgs {
     const uint32_t* pre;         // classifier slot words of the large ACLs: block b at pre + 2 b pre_stride
                                  // (SYN tuple, then SYN-ACK at + pre_stride); null when there are none
     uint64_t pre_stride;
+    uint32_t n_big;              // blocks at pre (the large ACLs); <= kConnEarlyBlocks: every block's
+                                 // words loaded with the connection's fields, before the interfaces
     uint32_t pre_rules;          // the words carry counter indices (descriptor base + rule), not slots
-    uint32_t pre_res8;           // block b is one byte per connection at (uint8_t*) pre + b pre_stride:
-                                 // SYN result | SYN-ACK result << 2 (batches that do not count)
+    uint32_t pre_bytes;          // the words' width: 4; 2 (u16 counter-index words, block b at
+                                 // (uint16_t*) pre + 2 b pre_stride); 1 (block b is one byte per
+                                 // connection at (uint8_t*) pre + b pre_stride: SYN result |
+                                 // SYN-ACK result << 2, batches that do not count)
     uint32_t bm_steps;           // bitmap forms: lower-bound steps of the largest interval table
     uint32_t job_lds;            // IPv4: LDS byte offset of the waves' job lists (512 B per wave)
 };
@@ -269,8 +294,18 @@ hipError_t launch_stream_conn(const ConnArgs& a, int grid, hipStream_t s);
 // tables' connection counters += the call's counters (ConnDesc ctr_off ..
 // + n_rules), which are cleared: a workgroup per descriptor and 256
 // counters (max_rules: the largest n_rules of the descriptors)
+// rows of the LDS counter words (n_rows rows of nw words; ctr16: u16 pairs)
+// -> the tables' connection counters (descriptor d's counters start at
+// desc[d].ctr_off, ascending), summed kConnRowsPerSlab rows per thread
+constexpr uint32_t kConnRowsPerSlab = 64;
+hipError_t launch_conn_rows(const uint32_t* rows, uint32_t n_rows, uint32_t nw, bool ctr16, uint32_t n_ctr,
+                            const ConnDesc* desc, uint32_t n_desc, unsigned long long* const* table_ctr,
+                            hipStream_t s);
+// the call counters (n_slabs copies of n_ctr u64, summed; clear: zero what
+// was read) -> the tables' connection counters
 hipError_t launch_conn_scatter(const ConnDesc* desc, unsigned long long* const* table_ctr, uint32_t n_desc,
-                               uint32_t max_rules, unsigned long long* call_ctr, hipStream_t s);
+                               uint32_t max_rules, unsigned long long* call_ctr, uint32_t n_slabs, bool clear,
+                               uint32_t n_ctr, hipStream_t s);
 
 struct TrafficDev {
     uint64_t seed;
