@@ -340,13 +340,16 @@ def test_device_plan_follows_binding_changes(count):
 
 
 @pytest.mark.parametrize("env", [{}, {"CONTIVCLS_PAIR_OTHER_GLOBAL": "1"}, {"CONTIVCLS_PAIR_QCAP": "3"},
-                                 {"CONTIVCLS_PAIR_OTHER_GLOBAL": "1", "CONTIVCLS_PAIR_QCAP": "0"}])
+                                 {"CONTIVCLS_PAIR_OTHER_GLOBAL": "1", "CONTIVCLS_PAIR_QCAP": "0"},
+                                 {"CONTIVCLS_PAIR_LQ": "0"}, {"CONTIVCLS_PAIR_LQ": "2", "CONTIVCLS_PAIR_QCAP": "4"},
+                                 {"CONTIVCLS_PAIR_LQ": "3"}])
 def test_pair_launch_tail_and_other_protocols(env, monkeypatch):
     """classify4_pair (k4_pair.hip) on a batch of 4k + 3 connections with
     protocol-47 connections everywhere, the last three included (the scalar
     tail's direct OTHER path): the OTHER image beside the main one in LDS or
     read from global memory (o_at = 0), the OTHER queue roomy or nearly
-    full / empty so that connections overflow to in-place classification.
+    full / empty so that connections overflow to in-place classification,
+    its entries in LDS, in global memory (CONTIVCLS_PAIR_LQ=0) or in both.
     Verdicts and counters against orc_test_connection."""
     from vpp_amd.engine import Engine
     for k, v in env.items():
@@ -509,14 +512,15 @@ def test_counted_batch_beyond_workgroup_bound(same_if):
 
 
 @pytest.mark.parametrize("flush", ["rows", "atomic"])
-@pytest.mark.parametrize("ctr16", ["0", "1"])
-def test_counter_widths_and_flush_paths(flush, ctr16, monkeypatch):
-    """LDS call counters as u32 or u16 pairs, leaving the launch as
+@pytest.mark.parametrize("plan", ["32j", "16j", "32s", "16s"])
+def test_counter_widths_and_flush_paths(flush, plan, monkeypatch):
+    """LDS call counters as u32 or u16 pairs, with job lists (two workgroups
+    per CU, the 128-VGPR kernel) or shuffles, leaving the launch as
     per-workgroup rows (summed by the rows launch) or by device atomics into
     the copies of the call counters: per-(ACL, rule) counters against
     orc_test_connection."""
     from vpp_amd.engine import Engine
-    monkeypatch.setenv("CONTIVCLS_CONN_CTR16", ctr16)
+    monkeypatch.setenv("CONTIVCLS_CONN_PLAN", plan)
     if flush == "atomic":
         monkeypatch.setenv("CONTIVCLS_CONN_FLUSH_ATOMIC", "1")
     eng = Engine()

@@ -35,6 +35,7 @@ def main():
     ap.add_argument("--other-proto", type=int, default=1, help="6%% of packets with protocol > 2")
     ap.add_argument("--locals", type=int, default=64)
     ap.add_argument("--count", type=int, default=1)
+    ap.add_argument("--no-check", action="store_true", help="diagnostic builds: skip the parity asserts")
     a = ap.parse_args()
     from vpp_amd.engine import Engine
     eng = Engine()
@@ -57,7 +58,8 @@ def main():
         for _ in range(a.iters):
             out = eng.connect_batch(*args, mode=mode)
         res[mode] = ((time.perf_counter() - t0) / a.iters, out)
-    assert np.array_equal(res["linear"][1], res["auto"][1]), "linear and classifier modes differ"
+    if not a.no_check:
+        assert np.array_equal(res["linear"][1], res["auto"][1]), "linear and classifier modes differ"
     dt, out = res["auto"]
     # HBM-resident batch (CLS_F_DEVICE): no PCIe in the timed region
     import torch
@@ -65,7 +67,8 @@ def main():
              .to("cuda") for x in (args[0], args[1], args[2], args[3], args[4], args[5], args[6])]
     torch.cuda.synchronize()
     dev_out = eng.connect_batch(*dargs)
-    assert np.array_equal(dev_out.cpu().numpy(), out), "device batch differs"
+    if not a.no_check:
+        assert np.array_equal(dev_out.cpu().numpy(), out), "device batch differs"
     def per_call(count):
         """median wall time of a.iters device batches (each call returns after
         its stream has finished)"""
@@ -95,7 +98,8 @@ def main():
             rc = fn(h, csr, n, op, fl, None)
             ts.append(time.perf_counter() - t0)
             assert rc == 0
-        assert np.array_equal(out.cpu().numpy(), dev_out.cpu().numpy())
+        if not a.no_check:
+            assert np.array_equal(out.cpu().numpy(), dev_out.cpu().numpy())
         return float(np.median(ts[1:]))
     abi_dt = per_call_abi(False)
     counted = None
@@ -126,7 +130,8 @@ def main():
     t1 = time.perf_counter()
     want, _ = oracle_connections(bind, by_name, ifs, si[:k], di[:k], {f: v[:k] for f, v in tr.items()}, 4)
     cpu_dt = time.perf_counter() - t1
-    assert np.array_equal(out[:k], want), "connection verdicts differ from the oracle"
+    if not a.no_check:
+        assert np.array_equal(out[:k], want), "connection verdicts differ from the oracle"
     print(json.dumps({
         "metric": "connections classified per second (testConnection, up to 4 ACL evaluations each)",
         "value": round(n / dt / 1e6, 3), "unit": "Mconn/s", "n": n, "ms_per_batch": round(dt * 1e3, 3),

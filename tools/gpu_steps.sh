@@ -56,7 +56,7 @@ for step in "$@"; do
   conn)
     for v in $(echo $arg | tr , ' '); do
       for loc in 12 64; do
-        (cd /tmp && CONTIVCLS_LIB=$(lib $v) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/conn_${v}_$loc -o run --output-format csv -- python3 $R/tools/conn_bench.py --locals $loc --cpu-sample 20000 > $O/conn_${v}_$loc.json 2> $O/conn_${v}_$loc.err)
+        (cd /tmp && CONTIVCLS_LIB=$(lib $v) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/conn_${v}_$loc -o run --output-format csv -- python3 $R/tools/conn_bench.py --locals $loc --cpu-sample $([ $v = default ] && echo 20000 || echo "0 --no-check") > $O/conn_${v}_$loc.json 2> $O/conn_${v}_$loc.err)
         echo "-- $v, $loc local ACLs"
         python3 tools/jl.py $O/conn_${v}_$loc.json hbm_resident hbm_resident_counted
         python3 tools/kstats.py $O/conn_${v}_$loc/run_kernel_stats.csv | grep -E "connect|pair"

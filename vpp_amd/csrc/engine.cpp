@@ -1212,8 +1212,10 @@ int cls_connect_batch(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t*
 // The OTHER queue of a pair launch: a fixed segment per workgroup (its
 // overflow is classified in place), so the buffer does not grow with the
 // batch.  CONTIVCLS_PAIR_QCAP: tests, to reach the in-place path.
+// the OTHER queue entries of a pair-launch workgroup (CONTIVCLS_PAIR_QCAP:
+// per wave, tests)
 static uint32_t pair_qcap(uint64_t n, int grid) {
-    if (const char* c = std::getenv("CONTIVCLS_PAIR_QCAP")) return uint32_t(std::strtoul(c, nullptr, 0));
+    if (const char* c = std::getenv("CONTIVCLS_PAIR_QCAP")) return uint32_t(std::strtoul(c, nullptr, 0)) * (kPairBlock / 64);
     return uint32_t(std::min<uint64_t>(pair_queue_words(n, grid), 16384));
 }
 
@@ -1466,11 +1468,22 @@ int connect_locked(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t* ou
                         od.off_lists += o_at; od.off_tmpl += o_at;
                     }
                     cfg.grid = cls_grid(e, true, true, o_at ? o_at + t.oimg.img_bytes : t.img.img_bytes, n);
-                    const uint32_t qcap = pair_qcap(n, cfg.grid);
-                    HIPC(e, e->s_pq.ensure(size_t(cfg.grid) * std::max<uint32_t>(1, qcap) * 16));
-                    HIPC(e, launch_classify4_pair(cd, od, o_at, syn, sp, pre, stride, e->s_pq.as<uint32_t>(), qcap,
+                    // the OTHER queue, one segment per wave: its first entries
+                    // in the LDS left after the images (one workgroup per CU
+                    // either way), the rest in global memory
+                    // (CONTIVCLS_PAIR_QCAP / CONTIVCLS_PAIR_LQ: entries per
+                    // wave in all / in LDS, tests)
+                    const uint32_t nwv = kPairBlock / 64;
+                    const uint32_t qw = (pair_qcap(n, cfg.grid) + nwv - 1) / nwv;
+                    const uint32_t q_lds = ((o_at ? o_at + t.oimg.img_bytes : t.img.img_bytes) + 15u) & ~15u;
+                    uint32_t lq_cap = std::min<uint32_t>(qw, (uint32_t(max_lds_bytes()) - q_lds) / 16u / nwv);
+                    if (const char* lqe = std::getenv("CONTIVCLS_PAIR_LQ"))
+                        lq_cap = std::min<uint32_t>(lq_cap, uint32_t(std::strtoul(lqe, nullptr, 0)));
+                    const uint32_t gq = qw - lq_cap;
+                    HIPC(e, e->s_pq.ensure(size_t(cfg.grid) * nwv * std::max<uint32_t>(1, gq) * 16));
+                    HIPC(e, launch_classify4_pair(cd, od, o_at, syn, sp, pre, stride, e->s_pq.as<uint32_t>(), gq,
                                                   pre_rules ? t.d_slot_rule.as<uint32_t>() : nullptr,
-                                                  desc[big[b]].ctr_off, pre_bytes, cfg));
+                                                  desc[big[b]].ctr_off, pre_bytes, lq_cap, cfg));
                 } else {
                     cfg.other = cls4_dev(t.oimg, t.d_oimg, DevBuf(), 0, t.n_rules);
                     cfg.grid = cls_grid(e, true, t.lds_resident, t.img.lds_bytes, n);
@@ -1508,8 +1521,11 @@ int connect_locked(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t* ou
     const char* nl = std::getenv("CONTIVCLS_CONN_NO_LDS");
     const int no_lds = nl ? std::atoi(nl) : 0;
     const size_t lds_max = size_t(max_lds_bytes());
-    const bool lds_rules = n && !pool.empty() && pool.size() <= lds_max && !(no_lds & 1);
-    const size_t lds_used = lds_rules ? pool.size() : 0;
+    const bool lds_rules = n && !pool.empty() && pool.size() + 16 + kConnStateEntries <= lds_max && !(no_lds & 1);
+    // the pool at LDS 0, then the state machine's table, then the rest
+    const size_t sm_at = lds_rules ? (pool.size() + 15) & ~size_t(15) : 0;
+    const size_t lds_used = sm_at + kConnStateEntries;
+    a.sm_lds = uint32_t(sm_at);
     int cmode = 0;
     if (count && n_ctr) cmode = lds_used + conn_lds_ctr_bytes(n_ctr) <= lds_max && !(no_lds & 2) ? 1 : 2;
     a.ctr_lds = uint32_t(lds_used);
@@ -1574,18 +1590,22 @@ int connect_locked(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t* ou
     // where it allows only one, one 1024-thread workgroup.
     a.n_desc = uint32_t(desc.size());
     const size_t meta = desc.size() * sizeof(ConnDesc) + ifs.size() * sizeof(IfAcls);
-    auto per_cu_of = [&](size_t b) { return b ? std::max(1, std::min(3, int(lds_max / b))) : 3; };
     // The launch's LDS plan for counters of ctr_b bytes: the descriptor and
     // interface tables after the pool and counters unless they would cost a
-    // workgroup per CU, then (IPv4) the waves' job lists (512 B per wave) on
-    // the same terms -- else the kernel's owner search and shuffles
-    // (CONTIVCLS_CONN_NO_JOBS: tests)
+    // workgroup per CU, then (IPv4, `jobs`) the waves' job lists (512 B per
+    // wave) on the same terms -- else the kernel's owner search and shuffles
+    // (CONTIVCLS_CONN_NO_JOBS: tests).  Counting with LDS counters and job
+    // lists or 16-byte addresses, the kernel holds up to 96 VGPRs (kernels.hip
+    // connect_kernel): at most two 512-thread workgroups per CU.
     struct LdsPlan {
         size_t lds;
         uint32_t meta_lds, job_lds;
         int per_cu, block;
     };
-    auto plan_of = [&](size_t ctr_b) {
+    auto plan_of = [&](size_t ctr_b, bool jobs) {
+        jobs = jobs && !k16 && !std::getenv("CONTIVCLS_CONN_NO_JOBS");
+        const int cu_cap = cmode == 1 && (jobs || k16) ? 2 : 3;
+        auto per_cu_of = [&](size_t b) { return b ? std::max(1, std::min(cu_cap, int(lds_max / b))) : cu_cap; };
         LdsPlan q{lds_used + ctr_b, 0xFFFFFFFFu, 0xFFFFFFFFu, 0, 0};
         const size_t meta_at = (q.lds + 15) & ~size_t(15);
         if (meta_at + meta <= lds_max && per_cu_of(meta_at + meta) == per_cu_of(q.lds) && !(no_lds & 4)) {
@@ -1595,28 +1615,41 @@ int connect_locked(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t* ou
         q.per_cu = per_cu_of(q.lds);
         q.block = q.per_cu >= 2 ? 512 : 1024;
         const size_t job_at = (q.lds + 15) & ~size_t(15), job_b = size_t(q.block / 64) * 512;
-        if (!k16 && job_at + job_b <= lds_max && (q.per_cu == 1 || per_cu_of(job_at + job_b) == q.per_cu) &&
-            !std::getenv("CONTIVCLS_CONN_NO_JOBS")) {
+        if (jobs && job_at + job_b <= lds_max && (q.per_cu == 1 || per_cu_of(job_at + job_b) == q.per_cu)) {
             q.job_lds = uint32_t(job_at);
             q.lds = job_at + job_b;
         }
         return q;
     };
-    // LDS counters: u32, or u16 pairs (half the LDS, a bound on a workgroup's
-    // connections) when those fit where u32 do not, or hold more workgroups
-    // per CU, or make room for the job lists (CONTIVCLS_CONN_CTR16=0/1: tests)
-    LdsPlan plan = plan_of(cmode == 1 ? conn_lds_ctr_bytes(n_ctr) : 0);
-    a.ctr16 = cmode == 1 ? 1u : 0u;
+    LdsPlan plan = plan_of(0, true);
+    a.ctr16 = 0u;
     if (cmode == 1) {
-        const LdsPlan p32 = plan_of(size_t(n_ctr) * 4);
-        const char* c16 = std::getenv("CONTIVCLS_CONN_CTR16");
-        const bool use32 = c16 ? c16[0] == '0'
-                               : p32.lds <= lds_max && p32.per_cu >= plan.per_cu &&
-                                     (p32.job_lds != 0xFFFFFFFFu || plan.job_lds == 0xFFFFFFFFu);
-        if (use32 && p32.lds <= lds_max) {
-            plan = p32;
-            a.ctr16 = 0u;
+        // LDS counters: u32, or u16 pairs (half the LDS, a bound on a
+        // workgroup's connections); with job lists (at most two workgroups
+        // per CU) or without (three where the LDS allows).  CONTIVCLS_CONN_PLAN
+        // = 32j / 16j / 32s / 16s forces one (tests, measurements).
+        const size_t b32 = size_t(n_ctr) * 4, b16 = conn_lds_ctr_bytes(n_ctr);
+        const LdsPlan c[4] = {plan_of(b32, true), plan_of(b16, true), plan_of(b32, false), plan_of(b16, false)};
+        int pick = -1;
+        if (const char* f = std::getenv("CONTIVCLS_CONN_PLAN")) {
+            const std::string v(f);
+            pick = v == "32j" ? 0 : v == "16j" ? 1 : v == "32s" ? 2 : v == "16s" ? 3 : -1;
+            if (pick >= 0 && c[pick].lds > lds_max) pick = -1;
         }
+        if (pick < 0) {
+            // the job lists first, then workgroups per CU, then u16 (12 local
+            // ACLs, ms per counted batch: 16j 0.1367, 32j 0.1379, 32s 0.1468, 16s
+            // 0.1571; 64: 16j 0.2289, 32 (no room for job lists) 0.2367, 16s
+            // 0.2449 -- profiles/r05zh_conn_counted_plans.txt)
+            auto score = [&](int k) {
+                return c[k].lds > lds_max ? -1 : (c[k].job_lds != 0xFFFFFFFFu ? 8 : 0) + 2 * c[k].per_cu + (k % 2 == 1);
+            };
+            pick = 0;
+            for (int k = 1; k < 4; ++k)
+                if (score(k) > score(pick)) pick = k;
+        }
+        plan = c[pick];
+        a.ctr16 = pick % 2 ? 1u : 0u;
     }
     size_t lds = plan.lds;
     a.meta_lds = plan.meta_lds;

@@ -11,27 +11,36 @@
 // once (13 B), writing 8 B.  The OTHER image (protocols > 2: networks alone
 // decide, evalACL's switch has no case) is staged beside the main image
 // when both fit LDS (no slot counters in this mode).  Those connections are
-// queued with their fields (16-B entries in the workgroup's segment of oq,
-// its fill counted in LDS) and
-// classified on the OTHER image after the workgroup's main loop, one per
-// lane: the OTHER chain (interval search, candidate scan) then runs once per
-// 1024 of them instead of once per wave step that holds any.
+// queued with their fields (16-B entries in the wave's segment: first in the
+// LDS left after the images, then in global memory, its fill a wave-uniform
+// register) and classified on the OTHER image after the wave's main loop,
+// one per lane: the OTHER chain (interval search, candidate scan) then runs
+// once per 64 of them instead of once per wave step that holds any, and no
+// wave waits for the others (no workgroup barrier before the drain).
 #include "kernels_dev.hpp"
 
 namespace cls {
 
 namespace {
 
+#ifndef PAIR_PF2
+#define PAIR_PF2 0
+#endif
+#ifndef PAIR_STAGE_ONLY
+#define PAIR_STAGE_ONLY 0
+#endif
+#ifndef PAIR_NOQ
+#define PAIR_NOQ 0
+#endif
 static_assert(kClsBlock == kPairBlock, "pair_queue_words sizes the queue for this block");
 
 template <int kMode, int kList, int kD>
 __global__ __launch_bounds__(kClsBlock) void classify4_pair(Cls4Dev t, Cls4Dev o, uint32_t o_at, Pkts4 p,
                                                             const uint16_t* sport, uint32_t* out, uint64_t stride,
-                                                            uint32_t* oq, uint32_t oq_seg, uint32_t q_lds,
+                                                            uint32_t* oq, uint32_t gqw, uint32_t q_lds,
                                                             const uint32_t* slot_rule, uint32_t ctr_base,
-                                                            uint32_t wbytes) {
+                                                            uint32_t wbytes, uint32_t lqw) {
     extern __shared__ uint4 smem[];
-    typedef __attribute__((address_space(3))) uint32_t* lctr_t;
     const uint32_t lane = __lane_id();
     const uint64_t lt = (1ull << lane) - 1ull;
     const uint32_t nthreads = gridDim.x * blockDim.x;
@@ -44,7 +53,11 @@ __global__ __launch_bounds__(kClsBlock) void classify4_pair(Cls4Dev t, Cls4Dev o
     const uint32_t* PR = reinterpret_cast<const uint32_t*>(p.proto);
     uint4* OS = reinterpret_cast<uint4*>(out);
     uint4* OA = reinterpret_cast<uint4*>(out + stride);
-    uint4* OQ = reinterpret_cast<uint4*>(oq);       // queued: {index, src, dst, dport | sport << 16}
+    // the wave's queue segment: {index, src, dst, dport | sport << 16}
+    const uint32_t wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const uint32_t lq = q_lds + 16u * lqw * (threadIdx.x >> 6);
+    uint4* const GQ = reinterpret_cast<uint4*>(oq) + uint64_t(wave) * gqw;
+    uint32_t wq = 0;                                    // the segment's fill (wave-uniform)
     // Four connections' fields per lane, fetched one step ahead: a batch of a
     // few Mi connections gives each lane only a few steps, each of which
     // would otherwise start with a full memory latency (the kernel waited on
@@ -64,10 +77,18 @@ __global__ __launch_bounds__(kClsBlock) void classify4_pair(Cls4Dev t, Cls4Dev o
     };
     Fields nx{};
     if (tid < nsteps) fetch(tid, nx);
-    if (threadIdx.x == 0) *lctr_t(q_lds) = 0u;          // the queue fill (made visible by the barrier below)
-    lds_copy(smem, reinterpret_cast<const uint4*>(t.img), t.img_bytes / 16u);
-    if (o_at) lds_copy(smem + o_at / 16u, reinterpret_cast<const uint4*>(o.img), o.img_bytes / 16u);
+#if PAIR_PF2
+    Fields nx2{};
+    if (tid + nthreads < nsteps) fetch(tid + nthreads, nx2);
+#endif
+    // both images in one round of loads (a second round is a second memory
+    // latency before the first step)
+    lds_copy2(smem, reinterpret_cast<const uint4*>(t.img), t.img_bytes / 16u, o_at / 16u,
+              reinterpret_cast<const uint4*>(o.img), o_at ? o.img_bytes / 16u : 0u);
     __syncthreads();
+#if PAIR_STAGE_ONLY
+    if (nsteps != 0xFFFFFFFFu) return;
+#endif
     const Img<true> im{nullptr};
     const Img<false> og{reinterpret_cast<const uint8_t*>(o.img)};
     // a word's payload: the slot, or (counting) its counter index
@@ -99,7 +120,12 @@ __global__ __launch_bounds__(kClsBlock) void classify4_pair(Cls4Dev t, Cls4Dev o
     };
     for (uint32_t g = tid; g < nsteps; g += nthreads) {
         const Fields f = nx;
+#if PAIR_PF2
+        nx = nx2;
+        if (g + 2u * nthreads < nsteps) fetch(g + 2u * nthreads, nx2);
+#else
         if (g + nthreads < nsteps) fetch(g + nthreads, nx);
+#endif
         const uint32_t pr = f.pr;
         const uint32_t sa[4] = {f.s4.x, f.s4.y, f.s4.z, f.s4.w}, da[4] = {f.d4.x, f.d4.y, f.d4.z, f.d4.w};
         const uint32_t dpa[4] = {f.dp2.x & 0xFFFFu, f.dp2.x >> 16, f.dp2.y & 0xFFFFu, f.dp2.y >> 16};
@@ -124,8 +150,8 @@ __global__ __launch_bounds__(kClsBlock) void classify4_pair(Cls4Dev t, Cls4Dev o
             w1[q] = rv[4 + q] | (key(k8[4 + q]) << 2);
         }
         // Some protocol byte > 2 (SWAR, as classify4_cls): those connections
-        // go to the workgroup's queue (one reservation per wave step); their
-        // words above are overwritten after the main loop
+        // go to the wave's queue segment; their words above are overwritten
+        // after the main loop
         const bool oth = ((pr | ((pr & 0x7F7F7F7Fu) + 0x7D7D7D7Du)) & 0x80808080u) != 0u;
         if (__any(oth)) {
             uint64_t m[4];
@@ -136,18 +162,18 @@ __global__ __launch_bounds__(kClsBlock) void classify4_pair(Cls4Dev t, Cls4Dev o
                 m[q] = __ballot(oth && ((pr >> (8 * q)) & 0xFFu) > 2u);
                 c[q + 1] = c[q] + uint32_t(__popcll(m[q]));
             }
-            uint32_t base = 0u;
-            if (lane == 0u)
-                base = __hip_atomic_fetch_add(lctr_t(q_lds), c[4], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            base = __shfl(base, 0);
+            const uint32_t base = wq;
+            wq += c[4];
 #pragma unroll
             for (int q = 0; q < 4; ++q)
                 if ((m[q] >> lane) & 1u) {
                     const uint32_t k = base + c[q] + uint32_t(__popcll(m[q] & lt));
-                    if (k < oq_seg)
-                        OQ[uint64_t(blockIdx.x) * oq_seg + k] =
-                            make_uint4(4u * g + uint32_t(q), s8[q], d8[q], p8[q] | (p8[4 + q] << 16));
-                    else    // the segment is full (a fixed size per workgroup): classify in place
+                    const uint4 ent = make_uint4(4u * g + uint32_t(q), s8[q], d8[q], p8[q] | (p8[4 + q] << 16));
+                    if (k < lqw)                // the LDS part of the segment
+                        *lds128w_t(lq + 16u * k) = v4u{ent.x, ent.y, ent.z, ent.w};
+                    else if (k - lqw < gqw)
+                        GQ[k - lqw] = ent;
+                    else    // the segment is full (a fixed size per wave): classify in place
                         other2(s8[q], d8[q], p8[q], p8[4 + q], w0[q], w1[q]);
                 }
         }
@@ -179,13 +205,19 @@ __global__ __launch_bounds__(kClsBlock) void classify4_pair(Cls4Dev t, Cls4Dev o
         }
         put(i, w0, w1);
     }
-    // the queued connections of protocol > 2, one per lane, their fields
-    // from the queue entry (no gather from the connection arrays; the barrier
-    // orders their words after the main loop's stores of the same words)
-    __syncthreads();
-    const uint32_t nq = min(*lctr_t(q_lds), oq_seg);
-    for (uint32_t j = threadIdx.x; j < nq; j += blockDim.x) {
-        const uint4 e = OQ[uint64_t(blockIdx.x) * oq_seg + j];
+    // the wave's queued connections of protocol > 2, one per lane, their
+    // fields from the queue entry (no gather from the connection arrays); the
+    // wave's own main-loop stores of the same words complete first
+    __threadfence_block();
+    const uint32_t nq = PAIR_NOQ ? 0u : min(wq, lqw + gqw);
+    for (uint32_t j = lane; j < nq; j += 64u) {
+        uint4 e;
+        if (j < lqw) {
+            const v4u x = *lds128_t(lq + 16u * j);
+            e = make_uint4(x.x, x.y, x.z, x.w);
+        } else {
+            e = GQ[j - lqw];
+        }
         uint32_t w0, w1;
         other2(e.y, e.z, e.w & 0xFFFFu, e.w >> 16, w0, w1);
         put(e.x, w0, w1);
@@ -195,12 +227,12 @@ __global__ __launch_bounds__(kClsBlock) void classify4_pair(Cls4Dev t, Cls4Dev o
 template <int kMode, int kList, int kD>
 void launch_pair_d(const Cls4Dev& t, const Cls4Dev& o, uint32_t o_at, const Pkts4& p, const uint16_t* sport,
                    uint32_t* out, uint64_t stride, uint32_t* oq, uint32_t oq_cap, const uint32_t* slot_rule,
-                   uint32_t ctr_base, uint32_t wbytes, const LaunchCfg& cfg) {
-    const uint32_t q_lds = ((o_at ? o_at + o.img_bytes : t.img_bytes) + 15u) & ~15u;   // the queue fill word
-    const size_t lds = q_lds + 16u;
+                   uint32_t ctr_base, uint32_t wbytes, uint32_t lq_cap, const LaunchCfg& cfg) {
+    const uint32_t q_lds = ((o_at ? o_at + o.img_bytes : t.img_bytes) + 15u) & ~15u;   // the waves' LDS segments
+    const size_t lds = q_lds + size_t(lq_cap) * 16u * (kPairBlock / 64);
     lds_attr(reinterpret_cast<const void*>(classify4_pair<kMode, kList, kD>), lds);
     hipLaunchKernelGGL((classify4_pair<kMode, kList, kD>), dim3(cfg.grid), dim3(kClsBlock), lds, cfg.stream, t, o,
-                       o_at, p, sport, out, stride, oq, oq_cap, q_lds, slot_rule, ctr_base, wbytes);
+                       o_at, p, sport, out, stride, oq, oq_cap, q_lds, slot_rule, ctr_base, wbytes, lq_cap);
 }
 
 // sublist modes: the search depth as a template argument (the rendered
@@ -208,19 +240,19 @@ void launch_pair_d(const Cls4Dev& t, const Cls4Dev& o, uint32_t o_at, const Pkts
 template <int kMode, int kList>
 void launch_pair(const Cls4Dev& t, const Cls4Dev& o, uint32_t o_at, const Pkts4& p, const uint16_t* sport,
                  uint32_t* out, uint64_t stride, uint32_t* oq, uint32_t oq_cap, const uint32_t* slot_rule,
-                 uint32_t ctr_base, uint32_t wbytes, const LaunchCfg& cfg) {
+                 uint32_t ctr_base, uint32_t wbytes, uint32_t lq_cap, const LaunchCfg& cfg) {
     if constexpr (kMode == 2 && (kList == 3 || kList == 4)) {
         switch (t.bv_steps) {
-        case 0: launch_pair_d<kMode, kList, 0>(t, o, o_at, p, sport, out, stride, oq, oq_cap, slot_rule, ctr_base, wbytes, cfg); return;
-        case 1: launch_pair_d<kMode, kList, 1>(t, o, o_at, p, sport, out, stride, oq, oq_cap, slot_rule, ctr_base, wbytes, cfg); return;
-        case 2: launch_pair_d<kMode, kList, 2>(t, o, o_at, p, sport, out, stride, oq, oq_cap, slot_rule, ctr_base, wbytes, cfg); return;
-        case 3: launch_pair_d<kMode, kList, 3>(t, o, o_at, p, sport, out, stride, oq, oq_cap, slot_rule, ctr_base, wbytes, cfg); return;
-        case 4: launch_pair_d<kMode, kList, 4>(t, o, o_at, p, sport, out, stride, oq, oq_cap, slot_rule, ctr_base, wbytes, cfg); return;
-        case 5: launch_pair_d<kMode, kList, 5>(t, o, o_at, p, sport, out, stride, oq, oq_cap, slot_rule, ctr_base, wbytes, cfg); return;
+        case 0: launch_pair_d<kMode, kList, 0>(t, o, o_at, p, sport, out, stride, oq, oq_cap, slot_rule, ctr_base, wbytes, lq_cap, cfg); return;
+        case 1: launch_pair_d<kMode, kList, 1>(t, o, o_at, p, sport, out, stride, oq, oq_cap, slot_rule, ctr_base, wbytes, lq_cap, cfg); return;
+        case 2: launch_pair_d<kMode, kList, 2>(t, o, o_at, p, sport, out, stride, oq, oq_cap, slot_rule, ctr_base, wbytes, lq_cap, cfg); return;
+        case 3: launch_pair_d<kMode, kList, 3>(t, o, o_at, p, sport, out, stride, oq, oq_cap, slot_rule, ctr_base, wbytes, lq_cap, cfg); return;
+        case 4: launch_pair_d<kMode, kList, 4>(t, o, o_at, p, sport, out, stride, oq, oq_cap, slot_rule, ctr_base, wbytes, lq_cap, cfg); return;
+        case 5: launch_pair_d<kMode, kList, 5>(t, o, o_at, p, sport, out, stride, oq, oq_cap, slot_rule, ctr_base, wbytes, lq_cap, cfg); return;
         default: break;
         }
     }
-    launch_pair_d<kMode, kList, -1>(t, o, o_at, p, sport, out, stride, oq, oq_cap, slot_rule, ctr_base, wbytes, cfg);
+    launch_pair_d<kMode, kList, -1>(t, o, o_at, p, sport, out, stride, oq, oq_cap, slot_rule, ctr_base, wbytes, lq_cap, cfg);
 }
 
 }  // namespace
@@ -228,11 +260,11 @@ void launch_pair(const Cls4Dev& t, const Cls4Dev& o, uint32_t o_at, const Pkts4&
 hipError_t launch_classify4_pair(const Cls4Dev& t, const Cls4Dev& o, uint32_t o_at, const Pkts4& p,
                                  const uint16_t* sport, uint32_t* out, uint64_t stride, uint32_t* oq,
                                  uint32_t oq_cap, const uint32_t* slot_rule, uint32_t ctr_base, uint32_t wbytes,
-                                 const LaunchCfg& cfg) {
+                                 uint32_t lq_cap, const LaunchCfg& cfg) {
     if (!cls_dispatchable(t, true, false) || o.mode != 0 || o.list_mode != 0) return hipErrorInvalidValue;
     const int src = src_variant(t);
 #define PAIR_CASE(S, M, L) \
-    case 8 * S + L: launch_pair<M, L>(t, o, o_at, p, sport, out, stride, oq, oq_cap, slot_rule, ctr_base, wbytes, cfg); break;
+    case 8 * S + L: launch_pair<M, L>(t, o, o_at, p, sport, out, stride, oq, oq_cap, slot_rule, ctr_base, wbytes, lq_cap, cfg); break;
     switch (8 * src + int(t.list_mode)) {
         PAIR_CASE(0, 0, 0) PAIR_CASE(0, 0, 1) PAIR_CASE(0, 0, 2) PAIR_CASE(0, 0, 3) PAIR_CASE(0, 0, 4)
         PAIR_CASE(0, 0, 5) PAIR_CASE(0, 0, 6)

@@ -550,10 +550,13 @@ __device__ __forceinline__ uint32_t conn_bm(const ConnArgs& a, const ConnDesc& D
 // non-nil ACL -> the call's counter space (descriptor ctr_off + rule), in LDS
 // (u32, folded into the u64 counters at the end) or with wave-aggregated
 // global atomics.
-// Workgroup size (launch_connect): the kernel holds ~75 VGPRs (6 waves per
+// Workgroup size (launch_connect): the kernel holds ~80 VGPRs (6 waves per
 // SIMD), so 24 waves fit a CU -- three 512-thread workgroups where the LDS
 // allows two or more, else one 1024-thread workgroup (16 waves rather than
-// the 8 of one 512-thread one); forcing 64 VGPRs spills to scratch.
+// the 8 of one 512-thread one); forcing 64 VGPRs spills to scratch.  The
+// LDS-counter variants with job lists or 16-byte addresses (kCount 1, kJobs
+// or k16) take up to 128 VGPRs (94: no spill, where 80 spilled 20 B) and at
+// most two workgroups per CU (the host's plan).
 // kJobs (IPv4): the waves' job lists in LDS (a.job_lds); else the owner
 // search and shuffles (16-byte batches, and IPv4 launches whose LDS is
 // full: the job lists would displace LDS counters or bitmap forms)
@@ -563,8 +566,44 @@ __device__ __forceinline__ uint32_t conn_bm(const ConnArgs& a, const ConnDesc& D
 #ifndef CONN_NO_EARLY
 #define CONN_NO_EARLY 0
 #endif
+#ifndef CONN_NO_LUT
+#define CONN_NO_LUT 0
+#endif
+// testConnection's order over the four call results (res: ACLAction of
+// the SYN src-inbound, SYN dst-outbound, SYN-ACK dst-inbound and SYN-ACK
+// src-outbound calls; a nil ACL's is PERMIT) and its REFLECT short-cuts
+// (aclengine_mock.go:394-471): the verdict | the calls made << 2.  same: the
+// two interfaces are one; !ok: an unknown interface (Failure, no calls).
+__device__ __forceinline__ uint32_t conn_state(const uint32_t res[4], bool same, bool ok) {
+    uint32_t v = 3u;                                                        // Failure (unknown interface)
+    bool made[4];
+    uint32_t r = res[0];                                                    // SYN: src inbound
+    made[0] = ok;
+    bool done = ok && (r == 3u || r == 0u);
+    v = ok && r == 3u ? 3u : ok && r == 0u ? 0u : v;
+    bool srefl = ok && r == 2u, drefl = srefl && same;
+    made[1] = ok && !done && !drefl;                                        // SYN: dst outbound
+    r = res[1];
+    v = made[1] && r == 3u ? 3u : made[1] && r == 0u ? 0u : v;
+    done = done || (made[1] && (r == 3u || r == 0u));
+    const bool dr1 = made[1] && r == 2u;
+    drefl = drefl || dr1;
+    srefl = srefl || (dr1 && same);
+    made[2] = ok && !done && !drefl;                                        // SYN-ACK: dst inbound
+    r = res[2];
+    v = made[2] && r == 3u ? 3u : made[2] && r == 0u ? 1u : v;
+    done = done || (made[2] && (r == 3u || r == 0u));
+    made[3] = ok && !done && !srefl;                                        // SYN-ACK: src outbound
+    r = res[3];
+    v = made[3] && r == 3u ? 3u : made[3] && r == 0u ? 1u : v;
+    done = done || (made[3] && (r == 3u || r == 0u));
+    v = ok && !done ? 2u : v;
+    return v | uint32_t(made[0]) << 2 | uint32_t(made[1]) << 3 | uint32_t(made[2]) << 4 | uint32_t(made[3]) << 5;
+}
+
 template <bool k16, bool kLdsRules, int kCount, bool kJobs>
-__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(6))) void connect_kernel(ConnArgs a) {
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kCount == 1 && (kJobs || k16) ? 4 : 6))) void connect_kernel(
+    ConnArgs a) {
     typedef typename ConnT<k16>::A A;
     extern __shared__ uint4 smem[];
     typedef __attribute__((address_space(3))) uint32_t* lctr_t;
@@ -575,6 +614,13 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(6))) void 
     }
     // this workgroup's copy of the call counters
     unsigned long long* const gctr = a.ctr + uint64_t(blockIdx.x % kConnCtrCopies) * a.n_ctr;
+    // the state machine's table (kConnStateEntries bytes): entry res0 | res1
+    // << 2 | res2 << 4 | res3 << 6 | same << 8 | !ok << 9
+    for (uint32_t x = threadIdx.x; x < kConnStateEntries; x += blockDim.x) {
+        const uint32_t r4[4] = {x & 3u, (x >> 2) & 3u, (x >> 4) & 3u, (x >> 6) & 3u};
+        *reinterpret_cast<__attribute__((address_space(3))) uint8_t*>(a.sm_lds + x) =
+            uint8_t(conn_state(r4, (x >> 8) & 1u, !((x >> 9) & 1u)));
+    }
     if (a.meta_lds != 0xFFFFFFFFu) {
         const uint32_t nd = a.n_desc * uint32_t(sizeof(ConnDesc)) / 4u;
         const uint32_t* gd = reinterpret_cast<const uint32_t*>(a.desc);
@@ -606,24 +652,18 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(6))) void 
         const uint32_t si = *at(a.src_if, ic), dj = *at(a.dst_if, ic);
         const A sa = *at(src, ic), da = *at(dst, ic);
         const uint32_t sp = *at(a.sport, ic), dp = *at(a.dport, ic), pr = *at(a.proto, ic);
-        const bool early = !CONN_NO_EARLY && a.n_big <= kConnEarlyBlocks;
-        uint32_t ew[kConnEarlyBlocks][2] = {};                 // [block][SYN, SYN-ACK]
+        // (u8 / u16 words, packed: one register per block)
+        const bool early = !CONN_NO_EARLY && a.n_big <= kConnEarlyBlocks && a.pre_bytes <= 2u;
+        uint32_t ew[kConnEarlyBlocks] = {};                    // [block]: SYN | SYN-ACK << (8 or 16)
         if (early) {
 #pragma unroll
             for (uint32_t b = 0; b < kConnEarlyBlocks; ++b)
                 if (b < a.n_big) {
                     if (a.pre_bytes == 1u) {
-                        const uint32_t x = reinterpret_cast<const uint8_t*>(a.pre)[uint64_t(b) * stride + ic];
-                        ew[b][0] = x;
-                        ew[b][1] = x >> 2;
-                    } else if (a.pre_bytes == 2u) {
-                        const uint16_t* p16 = reinterpret_cast<const uint16_t*>(a.pre) + uint64_t(2u * b) * stride + ic;
-                        ew[b][0] = p16[0];
-                        ew[b][1] = p16[stride];
+                        ew[b] = reinterpret_cast<const uint8_t*>(a.pre)[uint64_t(b) * stride + ic];
                     } else {
-                        const uint32_t* p32 = a.pre + uint64_t(2u * b) * stride + ic;
-                        ew[b][0] = p32[0];
-                        ew[b][1] = p32[stride];
+                        const uint16_t* p16 = reinterpret_cast<const uint16_t*>(a.pre) + uint64_t(2u * b) * stride + ic;
+                        ew[b] = uint32_t(p16[0]) | uint32_t(p16[stride]) << 16;
                     }
                 }
         }
@@ -642,7 +682,8 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(6))) void 
         uint32_t w[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k)
-            w[k] = early ? (bi[k] == 1 ? ew[1][k >> 1] : ew[0][k >> 1])
+            w[k] = early ? ((bi[k] == 1 ? ew[1] : ew[0]) >> ((k >> 1) * (a.pre_bytes == 1u ? 2u : 16u))) &
+                               (a.pre_bytes == 1u ? 0xFFu : 0xFFFFu)
                  : a.pre_bytes == 1u
                        ? uint32_t(*(bi[k] >= 0 ? reinterpret_cast<const uint8_t*>(a.pre) + uint64_t(uint32_t(bi[k])) * stride + ic
                                                : reinterpret_cast<const uint8_t*>(a.src_if) + ic)) >> (2 * (k >> 1))
@@ -749,32 +790,20 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(6))) void 
         uint32_t res[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) res[k] = di[k] < 0 ? 1u : job[k] ? (rj[k] & 3u) : (w[k] & 3u);   // nil ACL: PERMIT (:476-478)
-        // straight-line selects, no per-lane branches: the wave's lanes take
-        // different paths through the REFLECT short-cuts
-        const bool same = si == dj;
-        uint32_t v = 3u;                                                        // Failure (unknown interface)
+        // the state machine from the workgroup's table: one LDS byte for the
+        // verdict and the calls made (a ~60-instruction select chain per lane
+        // otherwise)
+#if CONN_NO_LUT
+        const uint32_t sm = conn_state(res, si == dj, ok);
+#else
+        const uint32_t sm = *reinterpret_cast<const __attribute__((address_space(3))) uint8_t*>(
+            a.sm_lds + (res[0] | res[1] << 2 | res[2] << 4 | res[3] << 6 | uint32_t(si == dj) << 8 |
+                        uint32_t(!ok) << 9));
+#endif
+        const uint32_t v = sm & 3u;
         bool made[4];
-        uint32_t r = res[0];                                                    // SYN: src inbound
-        made[0] = ok;
-        bool done = ok && (r == 3u || r == 0u);
-        v = ok && r == 3u ? 3u : ok && r == 0u ? 0u : v;
-        bool srefl = ok && r == 2u, drefl = srefl && same;
-        made[1] = ok && !done && !drefl;                                        // SYN: dst outbound
-        r = res[1];
-        v = made[1] && r == 3u ? 3u : made[1] && r == 0u ? 0u : v;
-        done = done || (made[1] && (r == 3u || r == 0u));
-        const bool dr1 = made[1] && r == 2u;
-        drefl = drefl || dr1;
-        srefl = srefl || (dr1 && same);
-        made[2] = ok && !done && !drefl;                                        // SYN-ACK: dst inbound
-        r = res[2];
-        v = made[2] && r == 3u ? 3u : made[2] && r == 0u ? 1u : v;
-        done = done || (made[2] && (r == 3u || r == 0u));
-        made[3] = ok && !done && !srefl;                                        // SYN-ACK: src outbound
-        r = res[3];
-        v = made[3] && r == 3u ? 3u : made[3] && r == 0u ? 1u : v;
-        done = done || (made[3] && (r == 3u || r == 0u));
-        v = ok && !done ? 2u : v;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) made[k] = (sm >> (2 + k)) & 1u;
         if (live) a.out[i] = uint8_t(v);
         if constexpr (kCount != 0) {
             uint32_t key[4];

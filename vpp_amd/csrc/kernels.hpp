@@ -176,9 +176,10 @@ hipError_t launch_classify16_slots(const Cls4Dev& t, const Fe16& fe, const Pkts1
 // out[i] = the SYN tuple (p.src, p.dst, p.dport) and out[stride + i] the
 // SYN-ACK tuple (p.dst, p.src, sport), result | slot << 2 each.  The OTHER
 // image (o, offsets rebased to LDS byte o_at) is staged beside the main one
-// when o_at != 0.  Connections of protocol > 2 go to the workgroup's
-// segment of oq (oq_cap entries per workgroup) and are classified
-// on the OTHER image after the workgroup's main loop, one per lane.
+// when o_at != 0.  Connections of protocol > 2 go to the wave's queue
+// segment -- lq_cap entries in the LDS after the images, then oq_cap in oq
+// (segment w of the grid's waves) -- and are classified on the OTHER image
+// after the wave's main loop, one per lane (in place when the segment is full).
 // Needs 16-B aligned src / dst / out / out + stride, 8-B dport / sport, 4-B
 // proto; stride a multiple of 4.
 // slot_rule (may be null): write each word's counter index ctr_base +
@@ -190,7 +191,7 @@ hipError_t launch_classify16_slots(const Cls4Dev& t, const Fe16& fe, const Pkts1
 hipError_t launch_classify4_pair(const Cls4Dev& t, const Cls4Dev& o, uint32_t o_at, const Pkts4& p,
                                  const uint16_t* sport, uint32_t* out, uint64_t stride, uint32_t* oq,
                                  uint32_t oq_cap, const uint32_t* slot_rule, uint32_t ctr_base, uint32_t wbytes,
-                                 const LaunchCfg& cfg);
+                                 uint32_t lq_cap, const LaunchCfg& cfg);
 // The OTHER queue segment of one pair-launch workgroup (kPairBlock threads)
 // that holds every connection its lanes visit, 4 per lane per step, in 16-B
 // entries; the engine caps the segment (oq_cap entries; the overflow is
@@ -237,6 +238,9 @@ constexpr uint32_t kConnBmHeader = 32;
 // Connection batches with at most this many large ACLs load every one's
 // result words together with the connection's fields (no second dependent
 // global round trip behind the interface lookup).
+// The connection kernel's state-machine table: one byte per (4 call
+// results, same interface, unknown interface).
+constexpr uint32_t kConnStateEntries = 1024;
 constexpr uint32_t kConnEarlyBlocks = 2;
 constexpr uint32_t kConnCtrCopies = 16;
 constexpr uint32_t kConnWgConns = 16383;
@@ -252,6 +256,7 @@ struct ConnArgs {
     uint32_t ctr_lds;            // counting: LDS byte offset of the counters (LDS variant; u16
                                  // pairs: counter j in half j & 1 of word j >> 1, a workgroup
                                  // evaluates at most kConnWgConns connections per launch)
+    uint32_t sm_lds;             // LDS byte offset of the state machine's table (kConnStateEntries B)
     uint32_t ctr16;              // counting, LDS variant: u16 counter pairs (else u32 counters)
     uint32_t* ctr_rows;          // counting, LDS variant: workgroup b stores its LDS counter words
                                  // as row b (null: device atomics into the copies of ctr)

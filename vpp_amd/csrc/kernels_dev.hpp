@@ -81,6 +81,7 @@ typedef const __attribute__((address_space(3))) uint16_t* lds16_t;
 typedef const __attribute__((address_space(3))) uint32_t* lds32_t;
 typedef const __attribute__((address_space(3))) v2u* lds64_t;
 typedef const __attribute__((address_space(3))) v4u* lds128_t;
+typedef __attribute__((address_space(3))) v4u* lds128w_t;
 template <bool kLds>
 struct Img {
     const uint8_t* g;
@@ -492,6 +493,9 @@ __device__ __forceinline__ void wave_count_cold(unsigned long long* gslot, uint3
 __device__ __forceinline__ uint32_t queue_row() { return blockIdx.x * kOtherSegs + (threadIdx.x >> 6); }
 __device__ __forceinline__ uint32_t queue_row0() { return gridDim.x * kOtherSegs; }
 
+#ifndef OQ_NO_STORE
+#define OQ_NO_STORE 0
+#endif
 template <int N, bool kLds, int kMode, int kList, int kD, int kCtr, typename SrcOf>
 __device__ __forceinline__ void run_n(const Img<kLds>& im, const Cls4Dev& t, const Cls4Dev& o, uint32_t hot_lane,
                                       unsigned long long* gslot, uint32_t& hot0,
@@ -598,7 +602,7 @@ __device__ __forceinline__ void run_n(const Img<kLds>& im, const Cls4Dev& t, con
             uint32_t* seg = t.oq + queue_row0() + queue_row() * t.oq_cap + base;
 #pragma unroll
             for (int q = 0; q < N; ++q)
-                if (pr[q] > 2u) seg[pre[q] + uint32_t(__popcll(m[q] & lt))] = idx[q];
+                if (pr[q] > 2u && !OQ_NO_STORE) seg[pre[q] + uint32_t(__popcll(m[q] & lt))] = idx[q];
         } else {
             // the segment is full (or there is none): what fits is queued,
             // the rest classified here and now (an out-of-line function for
@@ -666,6 +670,28 @@ __device__ __forceinline__ void lds_copy(uint4* dst, const uint4* src, uint32_t 
         for (int k = 0; k < K; ++k) {
             const uint32_t i = base + uint32_t(k) * blockDim.x + threadIdx.x;
             if (i < n16) dst[i] = v[k];
+        }
+    }
+}
+
+// Two source arrays into LDS in one round of loads where the block's
+// threads can hold them (K = 10 16-B loads per thread, 160 KiB at 1024
+// threads): n1 at dst, n2 at dst + at2 (16-B units).
+__device__ __forceinline__ void lds_copy2(uint4* dst, const uint4* src1, uint32_t n1, uint32_t at2, const uint4* src2,
+                                          uint32_t n2) {
+    constexpr int K = 10;
+    const uint32_t n = n1 + n2;
+    for (uint32_t base = 0; base < n; base += K * blockDim.x) {
+        uint4 v[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {       // (clamped, not guarded: the loads stay in registers)
+            const uint32_t i = min(base + uint32_t(k) * blockDim.x + threadIdx.x, n - 1u);
+            v[k] = i < n1 ? src1[i] : src2[i - n1];
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const uint32_t i = base + uint32_t(k) * blockDim.x + threadIdx.x;
+            if (i < n) dst[i < n1 ? i : at2 + (i - n1)] = v[k];
         }
     }
 }
