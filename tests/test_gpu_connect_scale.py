@@ -528,3 +528,29 @@ def test_counter_widths_and_flush_paths(flush, plan, monkeypatch):
         _run(eng, 21, "device_auto", 4, count=True, n=20000, n_local=12)
     finally:
         eng.close()
+
+
+def test_pair_launch_partial_last_step_matches_linear():
+    """classify4_pair with two steps per lane, the second taken by a prefix
+    of the grid's lanes only, and 5 % protocol-47 connections: the wave's
+    OTHER queue fill must come from lane 0 (the lanes past the prefix keep
+    stale copies).  Every connection against the pure-scan mode (mode
+    "linear", no classifier)."""
+    from vpp_amd.engine import Engine
+    eng = Engine()
+    try:
+        ifs, bind, by_name, pool, spec = build(eng, 31, n_local=4, n_if=12)
+        n = 4 * 256 * 1024 + 4 * 700 + 3
+        tr = traffic(31, n, pool, spec, 4)
+        rng = np.random.default_rng(31)
+        tr["proto"] = np.where(rng.random(n) < 0.05, 47, tr["proto"]).astype(np.uint8)
+        ids = np.array([eng.if_id(x) for x in ifs], np.uint32)
+        si = rng.integers(0, 3, n)                      # the global ACL's interfaces: the pair launch
+        di = rng.integers(0, len(ifs), n)
+        args = [ids[si], ids[di], tr["src"], tr["dst"], tr["proto"], tr["sport"], tr["dport"]]
+        got = eng.connect_batch(*args, mode="classifier")
+        want = eng.connect_batch(*args, mode="linear")
+        bad = np.nonzero(got != want)[0]
+        assert bad.size == 0, (bad[:10], got[bad[:10]], want[bad[:10]])
+    finally:
+        eng.close()

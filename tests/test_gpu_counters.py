@@ -170,10 +170,11 @@ def test_stream_floor(eng):
 
 @pytest.mark.parametrize("cap", [None, "0", "1000"])
 @pytest.mark.parametrize("v16", [False, True])
-def test_other_protocols_queue(eng, monkeypatch, cap, v16):
-    """Protocols outside ProtocolType (30 % here): queued for the OTHER image
-    and classified after the launch, or in place once the queue is full
-    (CONTIVCLS_OTHER_CAP); every path equals the oracle."""
+@pytest.mark.parametrize("share", [0.3, 0.02])
+def test_other_protocols_queue(eng, monkeypatch, cap, v16, share):
+    """Protocols outside ProtocolType (30 % or 2 % here): queued for the
+    OTHER image and classified after the launch, or in place once the queue
+    is full (CONTIVCLS_OTHER_CAP); every path equals the oracle."""
     from aclgen import random_acl16, random_traffic16
     if cap is not None:
         monkeypatch.setenv("CONTIVCLS_OTHER_CAP", cap)
@@ -184,7 +185,7 @@ def test_other_protocols_queue(eng, monkeypatch, cap, v16):
         rules, pool = random_acl(23, 300, 0.0)
         tr = random_traffic(4, 70001, pool)
     rng = np.random.default_rng(9)
-    tr["proto"][rng.random(len(tr["proto"])) < 0.3] = 47
+    tr["proto"][rng.random(len(tr["proto"])) < share] = 47
     t = eng.put_table("other", rules)
     try:
         v, c = eng.classify(t, tr["src"], tr["dst"], tr["dport"], tr["proto"])

@@ -154,6 +154,7 @@ __global__ __launch_bounds__(kClsBlock) void classify4_pair(Cls4Dev t, Cls4Dev o
         // after the main loop
         const bool oth = ((pr | ((pr & 0x7F7F7F7Fu) + 0x7D7D7D7Du)) & 0x80808080u) != 0u;
         if (__any(oth)) {
+            wq = __builtin_amdgcn_readfirstlane(wq);     // (lanes done with the loop keep stale copies)
             uint64_t m[4];
             uint32_t c[5];
             c[0] = 0;
@@ -209,7 +210,8 @@ __global__ __launch_bounds__(kClsBlock) void classify4_pair(Cls4Dev t, Cls4Dev o
     // fields from the queue entry (no gather from the connection arrays); the
     // wave's own main-loop stores of the same words complete first
     __threadfence_block();
-    const uint32_t nq = PAIR_NOQ ? 0u : min(wq, lqw + gqw);
+    // lane 0's fill is current: the main loop's active lanes are a prefix
+    const uint32_t nq = PAIR_NOQ ? 0u : min(__builtin_amdgcn_readlane(wq, 0), lqw + gqw);
     for (uint32_t j = lane; j < nq; j += 64u) {
         uint4 e;
         if (j < lqw) {

@@ -595,8 +595,11 @@ __device__ __forceinline__ void run_n(const Img<kLds>& im, const Cls4Dev& t, con
         }
         const uint64_t lt = (1ull << __lane_id()) - 1ull;
         // this wave's own queue segment, its fill a wave-uniform register:
-        // no LDS atomic (and no wait for its return) per wave step
-        const uint32_t base = wq;
+        // no LDS atomic (and no wait for its return) per wave step; read
+        // from the first active lane, so that the segment's address is
+        // scalar (lanes done with a tail loop keep stale copies, but the
+        // loops' active lanes are a prefix: lane 0 is current)
+        const uint32_t base = __builtin_amdgcn_readfirstlane(wq);
         if (t.oq && base + pre[N] <= t.oq_cap) {          // wave-uniform: room for all of them
             wq = base + pre[N];
             uint32_t* seg = t.oq + queue_row0() + queue_row() * t.oq_cap + base;
