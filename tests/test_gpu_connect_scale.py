@@ -554,3 +554,41 @@ def test_pair_launch_partial_last_step_matches_linear():
         assert bad.size == 0, (bad[:10], got[bad[:10]], want[bad[:10]])
     finally:
         eng.close()
+
+
+@pytest.mark.parametrize("count", [False, True])
+def test_two_large_acls(count):
+    """Two large ACLs (the config-3 global table and a 3,000-rule random one,
+    bound on interfaces of their own, most connections through them): two
+    pair-launch blocks, both loaded with the connection's fields (the early
+    words, kConnEarlyBlocks), result bytes or counter-index words; verdicts
+    and per-(ACL, rule) counters against orc_test_connection."""
+    import torch
+    from vpp_amd.engine import Engine
+    eng = Engine()
+    try:
+        ifs, bind, by_name, pool, spec = build(eng, 13, n_local=6, n_if=20, cfg=3)
+        big2, _ = random_acl(4242, 3000, 0.0)
+        assert eng.acl_put("big2", big2, ["bx0", "bx1"], ["bx1", "bx2"]) == 0
+        by_name["big2"] = big2
+        ifs = ifs + ["bx0", "bx1", "bx2"]
+        bind.update({"bx0": ["big2", None], "bx1": ["big2", "big2"], "bx2": [None, "big2"]})
+        n = 24000
+        tr = traffic(13, n, pool, spec, 4)
+        rng = np.random.default_rng(13)
+        ids = np.array([eng.if_id(x) for x in ifs], np.uint32)
+        hot = np.array([0, 1, 2, len(ifs) - 3, len(ifs) - 2, len(ifs) - 1])   # the two large ACLs' interfaces
+        si = np.where(rng.random(n) < 0.6, rng.choice(hot, n), rng.integers(0, len(ifs), n))
+        di = np.where(rng.random(n) < 0.6, rng.choice(hot, n), rng.integers(0, len(ifs), n))
+        args = [ids[si], ids[di], tr["src"], tr["dst"], tr["proto"], tr["sport"], tr["dport"]]
+        dv = [torch.from_numpy(np.ascontiguousarray(x).view({4: np.int32, 2: np.int16, 1: np.uint8}[x.dtype.itemsize]))
+              .to("cuda") for x in args]
+        got = eng.connect_batch(*dv, count=count).cpu().numpy()
+        want, wcounts = oracle_connections(bind, by_name, ifs, si, di, tr, 4)
+        assert np.array_equal(got, want)
+        if count:
+            for name in by_name:
+                assert np.array_equal(eng.conn_counters(name, reset=True), wcounts[name]), name
+            assert wcounts["big2"].sum() > 1000 and wcounts["global"].sum() > 1000
+    finally:
+        eng.close()

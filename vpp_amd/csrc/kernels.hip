@@ -560,15 +560,6 @@ __device__ __forceinline__ uint32_t conn_bm(const ConnArgs& a, const ConnDesc& D
 // kJobs (IPv4): the waves' job lists in LDS (a.job_lds); else the owner
 // search and shuffles (16-byte batches, and IPv4 launches whose LDS is
 // full: the job lists would displace LDS counters or bitmap forms)
-#ifndef CONN_LEAD_ROUNDS
-#define CONN_LEAD_ROUNDS 0
-#endif
-#ifndef CONN_NO_EARLY
-#define CONN_NO_EARLY 0
-#endif
-#ifndef CONN_NO_LUT
-#define CONN_NO_LUT 0
-#endif
 // testConnection's order over the four call results (res: ACLAction of
 // the SYN src-inbound, SYN dst-outbound, SYN-ACK dst-inbound and SYN-ACK
 // src-outbound calls; a nil ACL's is PERMIT) and its REFLECT short-cuts
@@ -653,7 +644,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kCount == 
         const A sa = *at(src, ic), da = *at(dst, ic);
         const uint32_t sp = *at(a.sport, ic), dp = *at(a.dport, ic), pr = *at(a.proto, ic);
         // (u8 / u16 words, packed: one register per block)
-        const bool early = !CONN_NO_EARLY && a.n_big <= kConnEarlyBlocks && a.pre_bytes <= 2u;
+        const bool early = a.n_big <= kConnEarlyBlocks && a.pre_bytes <= 2u;
         uint32_t ew[kConnEarlyBlocks] = {};                    // [block]: SYN | SYN-ACK << (8 or 16)
         if (early) {
 #pragma unroll
@@ -793,13 +784,9 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kCount == 
         // the state machine from the workgroup's table: one LDS byte for the
         // verdict and the calls made (a ~60-instruction select chain per lane
         // otherwise)
-#if CONN_NO_LUT
-        const uint32_t sm = conn_state(res, si == dj, ok);
-#else
         const uint32_t sm = *reinterpret_cast<const __attribute__((address_space(3))) uint8_t*>(
             a.sm_lds + (res[0] | res[1] << 2 | res[2] << 4 | res[3] << 6 | uint32_t(si == dj) << 8 |
                         uint32_t(!ok) << 9));
-#endif
         const uint32_t v = sm & 3u;
         bool made[4];
 #pragma unroll
@@ -826,24 +813,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kCount == 
                 // 136.5 -> 142.5 us at 12 local ACLs, profiles/r04l_conn_ab.txt)
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
-                    uint32_t kk = key[k], add = 1u;
-#if CONN_LEAD_ROUNDS
-                    // same-address LDS atomics serialise: the lanes holding
-                    // the first active lane's key add once, by that lane
-#pragma unroll
-                    for (int round = 0; round < CONN_LEAD_ROUNDS; ++round) {
-                        const uint64_t act = __ballot(kk != 0xFFFFFFFFu && add == 1u);
-                        if (act) {
-                            const int leader = int(__builtin_ctzll(act));
-                            const uint32_t sk = uint32_t(__builtin_amdgcn_readlane(int(kk), leader));
-                            const uint64_t same = __ballot(kk == sk && add == 1u);
-                            if (kk == sk && add == 1u) {
-                                if (int(lane) == leader) add = uint32_t(__popcll(same));
-                                else kk = 0xFFFFFFFFu;
-                            }
-                        }
-                    }
-#endif
+                    const uint32_t kk = key[k], add = 1u;
                     if (kk != 0xFFFFFFFFu)
                         __hip_atomic_fetch_add(lctr_t(a.ctr_lds + 4u * (a.ctr16 ? kk >> 1 : kk)),
                                                a.ctr16 ? add << (16u * (kk & 1u)) : add, __ATOMIC_RELAXED,
