@@ -818,8 +818,9 @@ int classify_locked(cls_engine* e, uint32_t table_id, const cls_pkt_soa* pk, uin
                 HIPC(e, launch_classify4_cls(cd, pc, vo, slot_val, t->lds_resident, vec, cfg));
                 zeroed = true;
                 cd.zero = nullptr;
-                HIPC(e, launch_finish4(finish_args(t->c4, sc, cd, co, t->lds_resident, uint32_t(cfg.grid), off + m >= n),
-                                       cfg.other, pc, vo, s, off + m >= n ? sc->done : nullptr));
+                FinishArgs fa = finish_args(t->c4, sc, cd, co, t->lds_resident, uint32_t(cfg.grid), off + m >= n);
+                fa.qmask = 1u;                      // the IPv4 launch's queue entries (run_n kMaskQ)
+                HIPC(e, launch_finish4(fa, cfg.other, pc, vo, s, off + m >= n ? sc->done : nullptr));
                 remapped = true;
             }
         } else {

@@ -190,16 +190,23 @@ __device__ __forceinline__ void finish_body(const FinishArgs& f, const Cls4Dev& 
     for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
         uint32_t w = 0, at = i;
         while (at >= cnt[w]) at -= cnt[w++];     // i < n: stops inside a non-empty segment
-        const uint32_t k = f.oq[f.oq_rows * kOtherSegs + (r * kOtherSegs + w) * f.oq_cap + at];
-        uint32_t s1[1], d1[1], p1[1];
-        load(k, s1[0], d1[0], p1[0]);
-        const uint32_t z1[1] = {0u};
-        uint32_t r1[1], k1[1];
-        classify_n<1, false, 0, 0, -1>(oim, o, s1, d1, p1, z1, r1, k1);
-        if (verdict) verdict[k] = uint8_t(r1[0]);
-        const uint32_t c = f.other_map[k1[0]];
-        if (lds) atomicAdd(&h[c], 1u);
-        else wave_count(f.out, orule[c]);
+        const uint32_t e = f.oq[f.oq_rows * kOtherSegs + (r * kOtherSegs + w) * f.oq_cap + at];
+        // one packet, or (qmask) the packets 4 g + q of the entry's mask
+        uint32_t mask = f.qmask ? e >> 28 : 1u;
+        const uint32_t kb = f.qmask ? (e & 0x0FFFFFFFu) << 2 : e;
+        while (mask) {
+            const uint32_t k = kb + (f.qmask ? uint32_t(__builtin_ctz(mask)) : 0u);
+            mask &= mask - 1u;
+            uint32_t s1[1], d1[1], p1[1];
+            load(k, s1[0], d1[0], p1[0]);
+            const uint32_t z1[1] = {0u};
+            uint32_t r1[1], k1[1];
+            classify_n<1, false, 0, 0, -1>(oim, o, s1, d1, p1, z1, r1, k1);
+            if (verdict) verdict[k] = uint8_t(r1[0]);
+            const uint32_t c = f.other_map[k1[0]];
+            if (lds) atomicAdd(&h[c], 1u);
+            else wave_count(f.out, orule[c]);
+        }
     }
     if (lds) {
         __syncthreads();

@@ -148,6 +148,8 @@ struct FinishArgs {
     // OTHER slots, then the n_orules rules
     const uint32_t* oq;
     uint32_t oq_rows, oq_cap;
+    uint32_t qmask = 0;          // entries are (packet >> 2) | mask << 28: the packets 4 g + q of the
+                                 // mask's bits (IPv4 launches: one entry per lane and wave step)
     const uint32_t* other_map;
     uint32_t n_other, n_orules;
 };

@@ -496,7 +496,7 @@ __device__ __forceinline__ uint32_t queue_row0() { return gridDim.x * kOtherSegs
 #ifndef OQ_NO_STORE
 #define OQ_NO_STORE 0
 #endif
-template <int N, bool kLds, int kMode, int kList, int kD, int kCtr, typename SrcOf>
+template <int N, bool kLds, int kMode, int kList, int kD, int kCtr, bool kMaskQ = false, typename SrcOf>
 __device__ __forceinline__ void run_n(const Img<kLds>& im, const Cls4Dev& t, const Cls4Dev& o, uint32_t hot_lane,
                                       unsigned long long* gslot, uint32_t& hot0,
                                       const uint32_t (&s)[N], const uint32_t (&d)[N],
@@ -584,6 +584,25 @@ __device__ __forceinline__ void run_n(const Img<kLds>& im, const Cls4Dev& t, con
     // search and candidate scan from global memory, its slots after the main
     // image's).
     if (__any(pr_any)) {
+        if constexpr (kMaskQ) {
+            // IPv4 launches (packets idx[q] = idx[0] + q, idx[0] a multiple of
+            // 4, or one packet): one entry per lane holding OTHER packets,
+            // (idx[0] >> 2) | their slots' mask << 28 (FinishArgs::qmask) --
+            // one rank and one store per lane instead of one per slot
+            uint32_t qm = 0u;
+#pragma unroll
+            for (int q = 0; q < N; ++q) qm |= (pr[q] > 2u ? 1u : 0u) << q;
+            const uint32_t ent = N == 1 ? (idx[0] >> 2) | (qm << (28u + (idx[0] & 3u)))
+                                        : (idx[0] >> 2) | (qm << 28);
+            const uint64_t lb = __ballot(qm != 0u);
+            const uint32_t base0 = __builtin_amdgcn_readfirstlane(wq), c = uint32_t(__popcll(lb));
+            if (t.oq && base0 + c <= t.oq_cap) {                 // wave-uniform: room for all of them
+                wq = base0 + c;
+                if (qm) t.oq[queue_row0() + queue_row() * t.oq_cap + base0 +
+                             uint32_t(__popcll(lb & ((1ull << __lane_id()) - 1ull)))] = ent;
+                return;
+            }
+        }
         // one queue reservation for the wave's OTHER packets of all N slots
         uint64_t m[N];
         uint32_t pre[N + 1];
@@ -605,7 +624,9 @@ __device__ __forceinline__ void run_n(const Img<kLds>& im, const Cls4Dev& t, con
             uint32_t* seg = t.oq + queue_row0() + queue_row() * t.oq_cap + base;
 #pragma unroll
             for (int q = 0; q < N; ++q)
-                if (pr[q] > 2u && !OQ_NO_STORE) seg[pre[q] + uint32_t(__popcll(m[q] & lt))] = idx[q];
+                if (pr[q] > 2u && !OQ_NO_STORE)
+                    seg[pre[q] + uint32_t(__popcll(m[q] & lt))] =
+                        kMaskQ ? (idx[q] >> 2) | (1u << (28u + (idx[q] & 3u))) : idx[q];
         } else {
             // the segment is full (or there is none): what fits is queued,
             // the rest classified here and now (an out-of-line function for
@@ -618,7 +639,8 @@ __device__ __forceinline__ void run_n(const Img<kLds>& im, const Cls4Dev& t, con
                 if (t.oq && now) {
                     const uint32_t pos = base + pre[q] + uint32_t(__popcll(m[q] & lt));
                     if (pos < t.oq_cap) {
-                        t.oq[queue_row0() + queue_row() * t.oq_cap + pos] = idx[q];
+                        t.oq[queue_row0() + queue_row() * t.oq_cap + pos] =
+                            kMaskQ ? (idx[q] >> 2) | (1u << (28u + (idx[q] & 3u))) : idx[q];
                         now = false;
                     }
                 }
@@ -766,8 +788,8 @@ __global__ __launch_bounds__(kClsBlock) void classify4_cls(Cls4Dev t, Cls4Dev o,
             const bool other = ((pr | ((pr & 0x7F7F7F7Fu) + 0x7D7D7D7Du)) & 0x80808080u) != 0u;
             uint32_t v[4];
             const uint32_t ix[4] = {4u * g, 4u * g + 1u, 4u * g + 2u, 4u * g + 3u};
-            run_n<4, kLds, kMode, kList, kD, kCtr>(im, t, o, hot_lane, gslot, hot0, sa, da, pa, ra, other, v,
-                                                   [&](int q) { return sa[q]; }, ix, oq_lds, wq);
+            run_n<4, kLds, kMode, kList, kD, kCtr, true>(im, t, o, hot_lane, gslot, hot0, sa, da, pa, ra, other, v,
+                                                         [&](int q) { return sa[q]; }, ix, oq_lds, wq);
             if constexpr (kCtr == 2)                             // slot mode: 4 result words per lane
                 reinterpret_cast<uint4*>(verdict)[g] = make_uint4(v[0], v[1], v[2], v[3]);
             else if (verdict)
@@ -806,9 +828,9 @@ __global__ __launch_bounds__(kClsBlock) void classify4_cls(Cls4Dev t, Cls4Dev o,
             const uint32_t ra[4] = {pr & 0xFFu, (pr >> 8) & 0xFFu, (pr >> 16) & 0xFFu, pr >> 24};
             uint32_t v[4];
             const uint32_t ix[4] = {4u * gi, 4u * gi + 1u, 4u * gi + 2u, 4u * gi + 3u};
-            run_n<4, kLds, kMode, kList, -1, kCtr>(im, t, o, hot_lane, gslot, hot0, sa, da, pa, ra,
-                                                   ((pr | ((pr & 0x7F7F7F7Fu) + 0x7D7D7D7Du)) & 0x80808080u) != 0u,
-                                                   v, [&](int q) { return sa[q]; }, ix, oq_lds, wq);
+            run_n<4, kLds, kMode, kList, -1, kCtr, true>(im, t, o, hot_lane, gslot, hot0, sa, da, pa, ra,
+                                                         ((pr | ((pr & 0x7F7F7F7Fu) + 0x7D7D7D7Du)) & 0x80808080u) != 0u,
+                                                         v, [&](int q) { return sa[q]; }, ix, oq_lds, wq);
             if constexpr (kCtr == 2)
                 reinterpret_cast<uint4*>(verdict)[gi] = make_uint4(v[0], v[1], v[2], v[3]);
             else if (verdict)
@@ -821,8 +843,8 @@ __global__ __launch_bounds__(kClsBlock) void classify4_cls(Cls4Dev t, Cls4Dev o,
         const uint32_t sa[1] = {p.src[i]}, da[1] = {p.dst[i]}, pa[1] = {p.dport[i]}, ra[1] = {p.proto[i]};
         uint32_t v[1];
         const uint32_t ix[1] = {i};
-        run_n<1, kLds, kMode, kList, -1, kCtr>(im, t, o, hot_lane, gslot, hot0, sa, da, pa, ra, ra[0] > 2u, v,
-                                               [&](int q) { return sa[q]; }, ix, oq_lds, wq);
+        run_n<1, kLds, kMode, kList, -1, kCtr, true>(im, t, o, hot_lane, gslot, hot0, sa, da, pa, ra, ra[0] > 2u, v,
+                                                     [&](int q) { return sa[q]; }, ix, oq_lds, wq);
         if constexpr (kCtr == 2) reinterpret_cast<uint32_t*>(verdict)[i] = v[0];   // slot mode: res | slot << 2
         else if (verdict) verdict[i] = uint8_t(v[0]);
     }
