@@ -592,3 +592,31 @@ def test_two_large_acls(count):
             assert wcounts["big2"].sum() > 1000 and wcounts["global"].sum() > 1000
     finally:
         eng.close()
+
+
+def test_device_batch_out_tensor():
+    """connect_batch(out=...) writes the verdicts into the caller's tensor
+    (the same values as a fresh one) and refuses a wrong one."""
+    import torch
+    from vpp_amd.engine import Engine
+    from vpp_amd._abi import ClsError
+    eng = Engine()
+    try:
+        ifs, bind, by_name, pool, spec = build(eng, 17, n_local=4, n_if=10)
+        n = 9001
+        tr = traffic(17, n, pool, spec, 4)
+        rng = np.random.default_rng(17)
+        ids = np.array([eng.if_id(x) for x in ifs], np.uint32)
+        args = [ids[rng.integers(0, len(ifs), n)], ids[rng.integers(0, len(ifs), n)], tr["src"], tr["dst"],
+                tr["proto"], tr["sport"], tr["dport"]]
+        dv = [torch.from_numpy(np.ascontiguousarray(x).view({4: np.int32, 2: np.int16, 1: np.uint8}[x.dtype.itemsize]))
+              .to("cuda") for x in args]
+        fresh = eng.connect_batch(*dv)
+        out = torch.full((n,), 7, dtype=torch.uint8, device="cuda")
+        got = eng.connect_batch(*dv, out=out)
+        assert got.data_ptr() == out.data_ptr()
+        assert torch.equal(out, fresh)
+        with pytest.raises(ClsError):
+            eng.connect_batch(*dv, out=torch.empty(n - 1, dtype=torch.uint8, device="cuda"))
+    finally:
+        eng.close()

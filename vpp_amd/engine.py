@@ -336,18 +336,20 @@ class Engine:
         return a.value, b.value
 
     def connect_batch(self, src_if, dst_if, src, dst, proto, sport, dport, mode: str = "auto",
-                      count: bool = False) -> np.ndarray:
+                      count: bool = False, out=None) -> np.ndarray:
         """testConnection over a batch (cls_connect_batch).  Addresses: host-order
         u32 (IPv4) or n x 16 network-order bytes (IPv6, IPv4-mapped = IPv4).
         mode: "auto" (ACLs with a classifier image use it for batches >=
         65536), "classifier" (at any size) or "linear" (every ACL scanned).
         count: add every evalACL call's terminating rule to the tables'
-        connection counters (conn_counters)."""
+        connection counters (conn_counters).  out (device batches): a
+        contiguous uint8 GPU tensor of n verdicts to write instead of a new
+        one."""
         flags = {"auto": 0, "classifier": _abi.F_CONN_CLS, "linear": _abi.F_FORCE_LINEAR}[mode]
         if count:
             flags |= _abi.F_COUNT
         if _is_torch(src):
-            return self._connect_batch_device(src_if, dst_if, src, dst, proto, sport, dport, flags)
+            return self._connect_batch_device(src_if, dst_if, src, dst, proto, sport, dport, flags, out)
         v16 = np.asarray(src).ndim == 2
         if v16:
             s = np.ascontiguousarray(src, np.uint8).reshape(-1, 16)
@@ -367,20 +369,24 @@ class Engine:
         self._check(_abi.lib().cls_connect_batch(self.h, C.byref(cs), n, _ptr(out), flags, None))
         return out
 
-    def _connect_batch_device(self, src_if, dst_if, src, dst, proto, sport, dport, flags):
+    def _connect_batch_device(self, src_if, dst_if, src, dst, proto, sport, dport, flags, out=None):
         """Device-resident batch (CLS_F_DEVICE): contiguous GPU tensors of 4-byte
         interface ids, 4-byte (or n x 16 uint8) addresses, 2-byte ports and
         1-byte protocols, already written (the call runs on the engine's
-        stream).  Returns a uint8 tensor."""
+        stream).  Returns a uint8 tensor (`out` when given)."""
         import torch
         v16 = src.dim() == 2
-        arrs = [src_if, dst_if, src, dst, sport, dport, proto]
-        sizes = [4, 4, 1 if v16 else 4, 1 if v16 else 4, 2, 2, 1]
+        arrs = (src_if, dst_if, src, dst, sport, dport, proto)
+        sizes = (4, 4, 1 if v16 else 4, 1 if v16 else 4, 2, 2, 1)
         n = src.shape[0]
         for x, sz in zip(arrs, sizes):
             if not (_is_torch(x) and x.is_cuda and x.is_contiguous() and x.element_size() == sz and x.shape[0] == n):
-                raise ClsError("device connection batch: contiguous GPU tensors of element sizes %s" % sizes)
-        out = torch.empty(n, dtype=torch.uint8, device=src.device)
+                raise ClsError("device connection batch: contiguous GPU tensors of element sizes %s" % (sizes,))
+        if out is None:
+            out = torch.empty(n, dtype=torch.uint8, device=src.device)
+        elif not (_is_torch(out) and out.is_cuda and out.is_contiguous() and out.element_size() == 1 and
+                  out.shape[0] == n):
+            raise ClsError("device connection batch: out must be a contiguous uint8 GPU tensor of n elements")
         if v16:
             pk = _abi.PktSoa(_abi.AF_V16, None, None, _ptr(src), _ptr(dst), _ptr(sport), _ptr(dport), _ptr(proto))
         else:
