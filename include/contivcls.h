@@ -39,7 +39,11 @@ extern "C" {
 /* 4: cls_config's device list (multi-device engines); engine-owned batches
  *    (cls_batch_*); cls_classify_batch / cls_batch_connect; the in-library
  *    RCCL counter all-reduce (cls_comm_*); cls_shard_range. */
-#define CLS_ABI_VERSION 4
+/* 5: cls_engine_set_option (tuning / diagnostic switches; the library no
+ *    longer reads the process environment); cls_compile_v4 / v16 take an
+ *    option string; entry points restore the caller's current device; over
+ *    distinct devices an engine without RCCL keeps host-summed counters. */
+#define CLS_ABI_VERSION 5
 
 /* ---- status codes ------------------------------------------------------ */
 enum {
@@ -150,8 +154,9 @@ typedef struct cls_engine cls_engine;
  * device.  Over distinct devices the engine creates an RCCL communicator
  * (single-process ncclCommInitAll) at creation, so batch hit counters merge
  * with an all-reduce over xGMI; a list that repeats a device (diagnostics:
- * shards on one GPU) has no communicator and its counters are summed on the
- * host when read. */
+ * shards on one GPU), or a host where RCCL cannot be loaded or initialised,
+ * has no communicator and its counters are summed on the host when read
+ * (cls_comm_info reports 0 ranks; cls_last_error keeps the RCCL reason). */
 typedef struct cls_config {
     int device;                /* HIP device ordinal; -1 = current device */
     uint32_t n_devices;        /* 0: one device (`device`); else the length of `devices` */
@@ -173,6 +178,19 @@ int cls_engine_devices(const cls_engine* e, uint32_t* n_devices);
 int cls_device_engine(cls_engine* e, uint32_t index, cls_engine** dev);
 const char* cls_last_error(const cls_engine* e);
 int cls_abi_version(void);
+/* Diagnostics, tests and measurements: one tuning switch of the engine (and
+ * of every device of a multi-device engine), `value` NULL for its default.
+ * The switches force compiler choices (list_mode, list_mode_max, trie, wide,
+ * orient=src|dst, lds_budget, src_search, phash_dense, v16_src_search,
+ * v16_src_trie) for later cls_table_put / cls_acl_put compiles, and launch
+ * plans (other_cap, wg_per_cu, conn_bitmap, conn_pair, conn_pre_rules,
+ * conn_pre_narrow, pair_qcap, pair_lq, pair_other_global, conn_no_lds,
+ * conn_jobs, conn_plan=32j|16j|32s|16s, conn_flush_atomic, batch_layout,
+ * debug_modes, debug_conn, debug_floor) for later calls; every one keeps
+ * verdicts and counters exact.  The library never reads the environment:
+ * an engine runs its defaults unless told otherwise here.  CLS_E_INVAL for
+ * an unknown key or a malformed value. */
+int cls_engine_set_option(cls_engine* e, const char* key, const char* value);
 
 /* ---- rule tables (one compiled, device-resident ACL) -------------------
  * cls_table_put compiles an ACL's rules (evalACL semantics,
@@ -492,7 +510,7 @@ typedef struct cls_image_v4_header {
     uint32_t n_gcells;
 } cls_image_v4_header;
 int cls_compile_v4(const cls_rule* rules, uint32_t n_rules, void* blob, uint64_t cap,
-                   uint64_t* need);
+                   uint64_t* need, const char* options);   /* "key=value,..." (cls_engine_set_option's compiler keys) or NULL */
 /* Whether the library has a classify kernel for an image of source lookup
  * `mode` and `list_mode` (cls_image_v4_header), LDS-resident or in global
  * memory; rep16: the 16-byte core.  CLS_OK, or CLS_E_INVAL for a combination
@@ -544,7 +562,7 @@ typedef struct cls_image_v16_header {
     uint32_t src_search_top, src_search_k8;
 } cls_image_v16_header;
 int cls_compile_v16(const cls_rule* rules, uint32_t n_rules, void* blob, uint64_t cap,
-                    uint64_t* need);
+                    uint64_t* need, const char* options);
 
 #ifdef __cplusplus
 }

@@ -16,14 +16,18 @@ import numpy as np
 from vpp_amd import _abi
 
 
-def compile_blob(crules, fn="cls_compile_v4") -> bytes:
+def compile_blob(crules, fn="cls_compile_v4", options=None) -> bytes:
+    """The compiler's image blob, under the test's library switches
+    (libopts.CURRENT, the ``libopt`` fixture) and ``options``."""
+    from libopts import option_string
     f = getattr(_abi.lib(), fn)
     need = C.c_uint64(0)
-    rc = f(crules.ptr(), crules.n, None, 0, C.byref(need))
+    opt = option_string(options)
+    rc = f(crules.ptr(), crules.n, None, 0, C.byref(need), opt)
     if rc != 0:
         raise RuntimeError("%s rc=%d" % (fn, rc))
     buf = C.create_string_buffer(need.value)
-    rc = f(crules.ptr(), crules.n, buf, need.value, C.byref(need))
+    rc = f(crules.ptr(), crules.n, buf, need.value, C.byref(need), opt)
     if rc != 0:
         raise RuntimeError("%s rc=%d" % (fn, rc))
     return buf.raw

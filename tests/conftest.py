@@ -11,3 +11,12 @@ for p in (ROOT, os.path.join(ROOT, "tests")):
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (gfx950) GPU")
+
+
+@pytest.fixture
+def libopt():
+    """Library tuning switches for one test (tests/libopts.py)."""
+    from libopts import LibOpts
+    o = LibOpts()
+    yield o
+    o.undo()

@@ -24,7 +24,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert _abi.lib().cls_abi_version() == _abi.ABI_VERSION == 4
+    assert _abi.lib().cls_abi_version() == _abi.ABI_VERSION == 5
 
 
 def test_engine_create_without_gpu_fails_loudly():
@@ -66,3 +66,30 @@ def test_timing_entry_points_refuse_null_engine():
     assert L.cls_kernel_times_reset(None) == _abi.E_INVAL
     ms = C.c_float(0)
     assert L.cls_last_kernel_ms(None, C.byref(ms)) == _abi.E_INVAL
+
+
+def test_compile_options_are_checked():
+    """The compiler's option string (cls_compile_v4 / v16; the same keys as
+    cls_engine_set_option): unknown keys and malformed values are refused."""
+    import ctypes as C
+    from aclgen import random_acl
+    rules, _ = random_acl(1, 40, 0.0)
+    cr = _abi.CRules(rules)
+    need = C.c_uint64(0)
+    f = _abi.lib().cls_compile_v4
+    assert f(cr.ptr(), cr.n, None, 0, C.byref(need), None) == 0
+    assert f(cr.ptr(), cr.n, None, 0, C.byref(need), b"orient=dst,list_mode_max=2,trie=0") == 0
+    for bad in (b"bogus=1", b"orient=sideways", b"list_mode_max=two", b"trie"):
+        assert f(cr.ptr(), cr.n, None, 0, C.byref(need), bad) == _abi.E_INVAL, bad
+
+
+def test_library_never_reads_the_environment():
+    """Tuning switches are engine options (cls_engine_set_option), not
+    environment variables: no getenv in the library's sources."""
+    import os
+    import re
+    d = os.path.join(os.path.dirname(_abi.__file__), "csrc")
+    for f in sorted(os.listdir(d)):
+        if f.endswith((".cpp", ".hpp", ".hip")):
+            with open(os.path.join(d, f)) as fh:
+                assert not re.search(r"\bgetenv\b|secure_getenv|environ\b", fh.read()), f

@@ -20,10 +20,10 @@ from vpp_amd import _abi
 
 
 @pytest.fixture(autouse=True)
-def _source_keyed(monkeypatch):
+def _source_keyed(libopt):
     """These tests pin list modes of the source-keyed layout; the compiler's
     choice of orientation (compile.cpp build_cls4) is tested on its own."""
-    monkeypatch.setenv("CONTIVCLS_ORIENT", "src")
+    libopt.set("orient", "src")
 
 
 def _img16(rules):
@@ -50,10 +50,10 @@ def test_v16_compiler_matches_oracle(seed, n_rules, weird):
 
 @pytest.mark.parametrize("seed", range(4))
 @pytest.mark.parametrize("cap", [0, 1, 2, 3, 4])
-def test_v16_list_modes(seed, cap, monkeypatch):
+def test_v16_list_modes(seed, cap, libopt):
     """Every list mode of the core, over mixed-family twins of IPv4 tables."""
     from aclgen import long_list_acl, many_ports_acl, single_port_acl
-    monkeypatch.setenv("CONTIVCLS_LIST_MODE_MAX", str(cap))
+    libopt.set("list_mode_max", str(cap))
     gen = [single_port_acl(seed + 3, 120), random_acl(seed + 9, 120, 0.0), many_ports_acl(seed, 300, 30),
            long_list_acl(seed + 1, 200)][seed % 4]
     rules, pool = gen
@@ -140,9 +140,9 @@ def _host_src_acl(seed, n_rules=200):
 
 @pytest.mark.parametrize("seed", range(6))
 @pytest.mark.parametrize("forced_search", [False, True])
-def test_v16_source_host_hashes(seed, forced_search, monkeypatch):
+def test_v16_source_host_hashes(seed, forced_search, libopt):
     if forced_search:
-        monkeypatch.setenv("CONTIVCLS_V16_SRC_SEARCH", "1")
+        libopt.set("v16_src_search", "1")
     rules, pool = _host_src_acl(seed)
     rules, tr = mix_families(rules, random_traffic(seed, 4000, pool), seed)
     img = _check16(rules, tr)
@@ -168,13 +168,13 @@ def test_config5_table_cpu():
 
 @pytest.mark.parametrize("seed", range(8))
 @pytest.mark.parametrize("kind", ["v4", "mixed", "v16"])
-def test_v16_source_trie_matches_oracle(seed, kind, monkeypatch):
+def test_v16_source_trie_matches_oracle(seed, kind, libopt):
     """src_mode 2 (forced): IPv4-mapped sources through the trie over their
     IPv4 word, the others through the non-IPv4 search (rows), protocols > 2
     through the global table's reps -- against the faithful oracle on IPv4
     tables widened to 16 bytes, their mixed-family twins and random
     mixed-family ACLs with malformed rules."""
-    monkeypatch.setenv("CONTIVCLS_V16_SRC_TRIE", "1")
+    libopt.set("v16_src_trie", "1")
     if kind == "v16":
         rules, pool = random_acl16(seed * 101 + 7, 150, 0.1, n_prefixes=60)
         tr = random_traffic16(seed + 40, 3000, pool)
@@ -186,12 +186,12 @@ def test_v16_source_trie_matches_oracle(seed, kind, monkeypatch):
         assert img.h.src_mode in (1, 2)
 
 
-def test_v16_source_trie_edges(monkeypatch):
+def test_v16_source_trie_edges(libopt):
     """Addresses at the trie's chunk and /8 boundaries and at the edges of the
     IPv4-mapped block (::ffff:0.0.0.0, ::ffff:255.255.255.255 and their IPv6
     neighbours), prefixes ending at those edges, host routes among blocks."""
     import vpp_amd.model as M
-    monkeypatch.setenv("CONTIVCLS_V16_SRC_TRIE", "1")
+    libopt.set("v16_src_trie", "1")
     nets = ["10.0.0.0/8", "10.1.0.0/16", "10.1.255.0/24", "10.2.0.0/15", "10.1.2.3/32", "0.0.0.0/1",
             "128.0.0.0/1", "255.255.255.255/32", "0.0.0.0/32", "10.255.255.0/24", "11.0.0.0/16",
             "fd00::/16", "::ffff:0:0/97", "::fffe:0:0/96"]
@@ -231,10 +231,10 @@ def test_gen_policy_lists_v16_source_trie(blocks):
     n = 4000
     for match in (C.MATCH_INGRESS, C.MATCH_EGRESS):
         acl = compile_rules(txn.generate_rules(match, [pol]))
-        import os
-        os.environ.pop("CONTIVCLS_ORIENT", None)
+        import libopts
+        keyed = libopts.CURRENT.pop("orient")      # the compiler's own orientation here
         img = Image16(compile_blob(_abi.CRules(acl), "cls_compile_v16"))
-        os.environ["CONTIVCLS_ORIENT"] = "src"
+        libopts.CURRENT["orient"] = keyed
         assert img.h.src_mode == 2 and img.core.h.list_mode in (3, 4, 5, 6)
         assert img.core.h.lds_bytes <= 160 * 1024
         blk = g.integers(0, blocks + blocks // 10 + 1, n).astype(np.uint64)

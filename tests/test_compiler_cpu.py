@@ -15,10 +15,10 @@ from vpp_amd import _abi
 
 
 @pytest.fixture(autouse=True)
-def _source_keyed(monkeypatch):
+def _source_keyed(libopt):
     """These tests pin list modes of the source-keyed layout; the compiler's
     choice of orientation (compile.cpp build_cls4) is tested on its own."""
-    monkeypatch.setenv("CONTIVCLS_ORIENT", "src")
+    libopt.set("orient", "src")
 
 
 def _check(rules, traffic):
@@ -86,7 +86,7 @@ def test_many_port_ranges_use_per_list_port_search(seed, host_src):
 
 
 @pytest.mark.parametrize("max_mode", [2, 3])
-def test_port_class_radix_edges(monkeypatch, max_mode):
+def test_port_class_radix_edges(libopt, max_mode):
     """Port classes at chunk edges (255/256, 65535) and ranges inside one
     256-port chunk: every port of every boundary checked against the oracle."""
     from vpp_amd import model as M
@@ -102,7 +102,7 @@ def test_port_class_radix_edges(monkeypatch, max_mode):
               dst=rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32),
               dport=np.tile(np.array(ports, np.uint16), 40),
               proto=rng.choice(np.array([0, 1, 2], np.uint8), n))
-    monkeypatch.setenv("CONTIVCLS_LIST_MODE_MAX", str(max_mode))
+    libopt.set("list_mode_max", str(max_mode))
     img = _check(rules, tr)
     assert img.h.list_mode <= max_mode
 
@@ -120,10 +120,10 @@ def test_empty_acl_denies_everything():
 
 @pytest.mark.parametrize("seed", range(6))
 @pytest.mark.parametrize("max_mode", [1, 2])
-def test_capped_list_modes_match_oracle(monkeypatch, seed, max_mode):
+def test_capped_list_modes_match_oracle(libopt, seed, max_mode):
     """The lower bit-vector list modes (what tables with > 16-entry lists or
     too many port classes get) stay exact when selected explicitly."""
-    monkeypatch.setenv("CONTIVCLS_LIST_MODE_MAX", str(max_mode))
+    libopt.set("list_mode_max", str(max_mode))
     rules, pool = random_acl(seed * 7 + 3, 150, 0.0, n_prefixes=4 if seed % 2 else 24)
     img = _check(rules, random_traffic(seed, 5000, pool))
     assert img.h.list_mode <= max_mode
@@ -145,11 +145,11 @@ def test_compact_lists_edge_addresses(seed):
 
 @pytest.mark.parametrize("seed", range(6))
 @pytest.mark.parametrize("max_mode", [3, 4])
-def test_single_port_tables_hash_port_classes(monkeypatch, seed, max_mode):
+def test_single_port_tables_hash_port_classes(libopt, seed, max_mode):
     """Rendered-shape tables (single dst ports): merged port classes, the
     perfect-hash port lookup (list mode 4) and, capped, the radix (mode 3)."""
     from aclgen import single_port_acl
-    monkeypatch.setenv("CONTIVCLS_LIST_MODE_MAX", str(max_mode))
+    libopt.set("list_mode_max", str(max_mode))
     rules, pool = single_port_acl(seed + 31, 70, n_prefixes=6 if seed % 2 else 20)
     tr = random_traffic(seed, 5000, pool)
     img = _check(rules, tr)

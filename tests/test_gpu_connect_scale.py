@@ -169,15 +169,13 @@ def test_connections_at_scale_match_oracle(seed, mode):
 
 @pytest.mark.parametrize("no_lds", [0, 1, 6])
 @pytest.mark.parametrize("bitmap", ["1", "0"])
-def test_connections_bitmap_form_match_oracle(bitmap, no_lds, monkeypatch):
+def test_connections_bitmap_form_match_oracle(bitmap, no_lds):
     """Device batches with the default selection: the linear IPv4 ACLs (1-300
     random rules) in the bitmap form (engine.cpp conn_bitmap4) or scanned
-    (CONTIVCLS_CONN_BITMAP=0), the pool in LDS or (no_lds 1) global memory,
+    (option conn_bitmap=0), the pool in LDS or (no_lds 1) global memory,
     the counters and tables in global memory (no_lds 6); verdicts and per-(ACL, rule) counters against orc_test_connection."""
     from vpp_amd.engine import Engine
-    monkeypatch.setenv("CONTIVCLS_CONN_BITMAP", bitmap)
-    monkeypatch.setenv("CONTIVCLS_CONN_NO_LDS", str(no_lds))
-    eng = Engine()
+    eng = Engine(options={"conn_bitmap": bitmap, "conn_no_lds": no_lds})
     try:
         _run(eng, 11 + no_lds, "device_auto", 4, count=True, n=16000, n_local=24)
     finally:
@@ -198,13 +196,12 @@ def test_connections16_mixed_families_match_oracle(mode):
 
 @pytest.mark.parametrize("fam", [4, 16])
 @pytest.mark.parametrize("no_lds", [0, 1, 2, 3, 7])
-def test_connection_counters_match_oracle(fam, no_lds, monkeypatch):
+def test_connection_counters_match_oracle(fam, no_lds):
     """Per-(ACL, rule) counters with the rule pool in LDS (few locals: the
     pool fits) or in global memory, the counters in LDS or global memory,
     the descriptor and interface tables in LDS or (bit 2) global memory."""
     from vpp_amd.engine import Engine
-    monkeypatch.setenv("CONTIVCLS_CONN_NO_LDS", str(no_lds))
-    eng = Engine()
+    eng = Engine(options={"conn_no_lds": no_lds})
     try:
         _run(eng, 7 + no_lds, "classifier", fam, count=True, n=8000, n_local=12)
     finally:
@@ -264,13 +261,12 @@ def test_device_batch_unknown_interface_is_failure():
 
 @pytest.mark.parametrize("fam", [4, 16])
 @pytest.mark.parametrize("count", [False, True])
-def test_global_tables_match_oracle(fam, count, monkeypatch):
+def test_global_tables_match_oracle(fam, count):
     """The connection kernel with its descriptor and interface tables read
-    from global memory (CONTIVCLS_CONN_NO_LDS bit 2; the default stages them
+    from global memory (option conn_no_lds bit 2; the default stages them
     in LDS): the same verdicts and counters."""
     from vpp_amd.engine import Engine
-    monkeypatch.setenv("CONTIVCLS_CONN_NO_LDS", "4")
-    eng = Engine()
+    eng = Engine(options={"conn_no_lds": 4})
     try:
         _run(eng, 11, "linear", fam, count=count, n=8000, n_local=12)
     finally:
@@ -339,22 +335,20 @@ def test_device_plan_follows_binding_changes(count):
         eng.close()
 
 
-@pytest.mark.parametrize("env", [{}, {"CONTIVCLS_PAIR_OTHER_GLOBAL": "1"}, {"CONTIVCLS_PAIR_QCAP": "3"},
-                                 {"CONTIVCLS_PAIR_OTHER_GLOBAL": "1", "CONTIVCLS_PAIR_QCAP": "0"},
-                                 {"CONTIVCLS_PAIR_LQ": "0"}, {"CONTIVCLS_PAIR_LQ": "2", "CONTIVCLS_PAIR_QCAP": "4"},
-                                 {"CONTIVCLS_PAIR_LQ": "3"}])
-def test_pair_launch_tail_and_other_protocols(env, monkeypatch):
+@pytest.mark.parametrize("opts", [{}, {"pair_other_global": 1}, {"pair_qcap": 3},
+                                  {"pair_other_global": 1, "pair_qcap": 0},
+                                  {"pair_lq": 0}, {"pair_lq": 2, "pair_qcap": 4},
+                                  {"pair_lq": 3}])
+def test_pair_launch_tail_and_other_protocols(opts):
     """classify4_pair (k4_pair.hip) on a batch of 4k + 3 connections with
     protocol-47 connections everywhere, the last three included (the scalar
     tail's direct OTHER path): the OTHER image beside the main one in LDS or
     read from global memory (o_at = 0), the OTHER queue roomy or nearly
     full / empty so that connections overflow to in-place classification,
-    its entries in LDS, in global memory (CONTIVCLS_PAIR_LQ=0) or in both.
+    its entries in LDS, in global memory (option pair_lq=0) or in both.
     Verdicts and counters against orc_test_connection."""
     from vpp_amd.engine import Engine
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
-    eng = Engine()
+    eng = Engine(options=opts)
     try:
         ifs, bind, by_name, pool, spec = build(eng, 21, n_local=6, n_if=16)
         n = 4 * 4000 + 3
@@ -415,15 +409,13 @@ def test_conn_counters_do_not_wait_for_other_streams():
 
 @pytest.mark.parametrize("no_jobs", ["0", "1"])
 @pytest.mark.parametrize("count", [False, True])
-def test_ipv4_job_lists_and_shuffles(no_jobs, count, monkeypatch):
+def test_ipv4_job_lists_and_shuffles(no_jobs, count):
     """The connection kernel's two ways to hand a wave's jobs to its lanes
     (IPv4): the per-wave job lists in LDS (the default where they fit) and
-    the owner search with shuffles (CONTIVCLS_CONN_NO_JOBS=1, and launches
+    the owner search with shuffles (option conn_jobs=0, and launches
     whose LDS is full) -- verdicts and counters against the oracle."""
     from vpp_amd.engine import Engine
-    if no_jobs == "1":
-        monkeypatch.setenv("CONTIVCLS_CONN_NO_JOBS", "1")
-    eng = Engine()
+    eng = Engine(options={"conn_jobs": 0} if no_jobs == "1" else None)
     try:
         _run(eng, 31, "device_auto", 4, count=count, n=16000, n_local=24)
     finally:
@@ -431,21 +423,17 @@ def test_ipv4_job_lists_and_shuffles(no_jobs, count, monkeypatch):
 
 
 @pytest.mark.parametrize("words", ["u16", "u32", "slots"])
-def test_counted_large_acl_words(words, monkeypatch):
+def test_counted_large_acl_words(words):
     """Counting batches: the pair launch writes each large-ACL word's counter
     index (descriptor base + rule) as u16 words (indices below 2^14) or
-    (CONTIVCLS_CONN_PRE_WORDS=1) u32 words, and the connection kernel adds it
-    directly, or (CONTIVCLS_CONN_PRE_SLOTS=1) writes slots the kernel maps to
+    (option conn_pre_narrow=0) u32 words, and the connection kernel adds it
+    directly, or (option conn_pre_rules=0) writes slots the kernel maps to
     rules -- per-(ACL, rule) counters against the oracle, protocol-47
     connections included (their OTHER-image slots).  Uncounted batches of the
     same connections (one result byte per connection, or u32 words) give the
     same verdicts."""
     from vpp_amd.engine import Engine
-    if words == "u32":
-        monkeypatch.setenv("CONTIVCLS_CONN_PRE_WORDS", "1")
-    if words == "slots":
-        monkeypatch.setenv("CONTIVCLS_CONN_PRE_SLOTS", "1")
-    eng = Engine()
+    eng = Engine(options={"u16": {}, "u32": {"conn_pre_narrow": 0}, "slots": {"conn_pre_rules": 0}}[words])
     try:
         ifs, bind, by_name, pool, spec = build(eng, 41, n_local=10, n_if=24)
         n = 4 * 6000 + 1
@@ -513,17 +501,14 @@ def test_counted_batch_beyond_workgroup_bound(same_if):
 
 @pytest.mark.parametrize("flush", ["rows", "atomic"])
 @pytest.mark.parametrize("plan", ["32j", "16j", "32s", "16s"])
-def test_counter_widths_and_flush_paths(flush, plan, monkeypatch):
+def test_counter_widths_and_flush_paths(flush, plan):
     """LDS call counters as u32 or u16 pairs, with job lists (two workgroups
     per CU, the 128-VGPR kernel) or shuffles, leaving the launch as
     per-workgroup rows (summed by the rows launch) or by device atomics into
     the copies of the call counters: per-(ACL, rule) counters against
     orc_test_connection."""
     from vpp_amd.engine import Engine
-    monkeypatch.setenv("CONTIVCLS_CONN_PLAN", plan)
-    if flush == "atomic":
-        monkeypatch.setenv("CONTIVCLS_CONN_FLUSH_ATOMIC", "1")
-    eng = Engine()
+    eng = Engine(options={"conn_plan": plan, "conn_flush_atomic": int(flush == "atomic")})
     try:
         _run(eng, 21, "device_auto", 4, count=True, n=20000, n_local=12)
     finally:

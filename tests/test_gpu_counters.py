@@ -4,7 +4,7 @@ Counter tiers (vpp_amd/csrc/compile.hpp Cls4Image): the classifier image
 stays in LDS whenever it fits; its per-slot hit counters are u32 LDS words,
 else u16 LDS halves (a 0x8000 carry moved to the global slot counter), else
 only the first n_lctr slots in LDS and the rest counted in global memory.
-CONTIVCLS_LDS_BUDGET shrinks the budget so small random ACLs exercise every
+The lds_budget option shrinks the budget so small random ACLs exercise every
 tier, and the global-image variant; verdicts and per-rule counters must equal
 the evalACL oracle's (mock/aclengine/aclengine_mock.go:473-668) bit for bit.
 
@@ -29,10 +29,10 @@ def eng():
     e.close()
 
 
-def _layout(rules, monkeypatch):
+def _layout(rules, libopt):
     from cls_image import Image, compile_blob
     from vpp_amd import _abi
-    monkeypatch.setenv("CONTIVCLS_ORIENT", "src")
+    libopt.set("orient", "src")
     return Image(compile_blob(_abi.CRules(rules))).h
 
 
@@ -49,16 +49,16 @@ def _budget(h, tier):
     return 256                                   # "global": no image of this table fits
 
 
-def _check(eng, rules, tr, monkeypatch, tier):
-    h = _layout(rules, monkeypatch)
+def _check(eng, rules, tr, libopt, tier):
+    h = _layout(rules, libopt)
     assert h.has_cls
-    monkeypatch.setenv("CONTIVCLS_LDS_BUDGET", str(_budget(h, tier)))
-    monkeypatch.setenv("CONTIVCLS_LIST_MODE", str(h.list_mode))   # the layout the budget was sized on
+    libopt.set("lds_budget", str(_budget(h, tier)), eng)
+    libopt.set("list_mode", str(h.list_mode), eng)   # the layout the budget was sized on
     # and its source lookup: under a smaller budget the compiler would take
     # the smaller interval table instead of the trie, and its counters would
     # fit another tier
-    monkeypatch.setenv("CONTIVCLS_TRIE", "1" if h.mode == 4 else "0")
-    monkeypatch.setenv("CONTIVCLS_ORIENT", "src")
+    libopt.set("trie", "1" if h.mode == 4 else "0", eng)
+    libopt.set("orient", "src", eng)
     t = eng.put_table("tier", rules)
     try:
         info = t.info()
@@ -83,23 +83,23 @@ def _check(eng, rules, tr, monkeypatch, tier):
 
 @pytest.mark.parametrize("tier", ["u32", "u16", "partial", "global"])
 @pytest.mark.parametrize("seed,weird", [(0, 0.05), (1, 0.0), (2, 0.02), (3, 0.0), (0, 0.0)])
-def test_counter_tiers_random_acls(eng, monkeypatch, seed, weird, tier):
+def test_counter_tiers_random_acls(eng, libopt, seed, weird, tier):
     """List modes 4 (seeds 0, 2), 3 (seeds 1, 3) and 0 (seed 0 without weird rules)."""
     rules, pool = random_acl(seed * 101 + 17, 400, weird)
     tr = random_traffic(seed + 3, 40003, pool)      # ICMP and protocols > 2 included
-    _check(eng, rules, tr, monkeypatch, tier)
+    _check(eng, rules, tr, libopt, tier)
 
 
 @pytest.mark.parametrize("tier", ["u16", "partial", "global"])
-def test_counter_tiers_sublist_mode(eng, monkeypatch, tier):
+def test_counter_tiers_sublist_mode(eng, libopt, tier):
     """The rendered-table shape (list mode 4, hashed source classes)."""
     rules, pool = single_port_acl(7, 300, n_prefixes=3)
     tr = random_traffic(9, 65536 + 77, pool)
-    info = _check(eng, rules, tr, monkeypatch, tier)
+    info = _check(eng, rules, tr, libopt, tier)
     assert info["list_mode"] == 4 or tier == "global"
 
 
-def test_u16_counter_carry(eng, monkeypatch):
+def test_u16_counter_carry(eng, libopt):
     """More than 0x8000 hits on one slot inside one workgroup: the u16
     counters carry to the global slot counters exactly."""
     rules, pool = single_port_acl(11, 120, n_prefixes=3)
@@ -109,8 +109,8 @@ def test_u16_counter_carry(eng, monkeypatch):
     tr = dict(src=np.full(n, a, np.uint32), dst=np.full(n, a, np.uint32),
               dport=np.full(n, 80, np.uint16), proto=np.zeros(n, np.uint8))
     tr["proto"][rng.integers(0, n, 1000)] = 1
-    _check(eng, rules, tr, monkeypatch, "u16")
-    _check(eng, rules, tr, monkeypatch, "partial")
+    _check(eng, rules, tr, libopt, "u16")
+    _check(eng, rules, tr, libopt, "partial")
 
 
 def test_two_streams_one_table(eng):
@@ -171,13 +171,13 @@ def test_stream_floor(eng):
 @pytest.mark.parametrize("cap", [None, "0", "1000"])
 @pytest.mark.parametrize("v16", [False, True])
 @pytest.mark.parametrize("share", [0.3, 0.02])
-def test_other_protocols_queue(eng, monkeypatch, cap, v16, share):
+def test_other_protocols_queue(eng, libopt, cap, v16, share):
     """Protocols outside ProtocolType (30 % or 2 % here): queued for the
     OTHER image and classified after the launch, or in place once the queue
-    is full (CONTIVCLS_OTHER_CAP); every path equals the oracle."""
+    is full (option other_cap); every path equals the oracle."""
     from aclgen import random_acl16, random_traffic16
     if cap is not None:
-        monkeypatch.setenv("CONTIVCLS_OTHER_CAP", cap)
+        libopt.set("other_cap", cap, eng)
     if v16:
         rules, pool = random_acl16(23, 300, 0.0)
         tr = random_traffic16(4, 70001, pool)

@@ -14,10 +14,10 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.fixture(autouse=True)
-def _source_keyed(monkeypatch):
+def _source_keyed(libopt, eng):
     """These tests pin list modes of the source-keyed layout; the compiler's
     choice of orientation (compile.cpp build_cls4) is tested on its own."""
-    monkeypatch.setenv("CONTIVCLS_ORIENT", "src")
+    libopt.set("orient", "src", eng)
 
 
 SCENARIOS = load_scenarios()
@@ -124,16 +124,16 @@ def variant_acl(kind, seed):
 
 @pytest.mark.parametrize("seed", range(3))
 @pytest.mark.parametrize("kind", sorted(VARIANTS))
-def test_all_kernel_variants(eng, seed, kind, monkeypatch):
+def test_all_kernel_variants(eng, seed, kind, libopt):
     """The classifier variants (hash-LPM / interval-search source lookup x
     port-filtered sublists with hashed / radix port classes / bit vectors
     with global port classes / bit vectors with per-list port search /
     template scan; the source trie x both sublist forms) against the oracle."""
     if kind.endswith("_pc"):
-        monkeypatch.setenv("CONTIVCLS_LIST_MODE_MAX", "2")
+        libopt.set("list_mode_max", "2", eng)
     # the interval search and the source trie each on the same tables
-    monkeypatch.setenv("CONTIVCLS_TRIE", "1" if kind.startswith("trie") else "0")
-    monkeypatch.setenv("CONTIVCLS_SRC_SEARCH", "1" if kind.startswith(("search", "trie")) else "0")
+    libopt.set("trie", "1" if kind.startswith("trie") else "0", eng)
+    libopt.set("src_search", "1" if kind.startswith(("search", "trie")) else "0", eng)
     from cls_image import Image, compile_blob
     from vpp_amd import _abi
     rules, pool = variant_acl(kind, seed)

@@ -1,7 +1,7 @@
 """GPU: the source trie (src mode 4) and wide global cells (list modes 5, 6).
 
 classify4_cls over trie images, wide-cell images (forced on small tables with
-CONTIVCLS_WIDE / CONTIVCLS_TRIE, in every counter tier the LDS budget leaves),
+options wide / trie, in every counter tier the LDS budget leaves),
 and the gen-policy.py lists at 200 blocks (trie, LDS cells) and at the
 1000-block default (trie, wide cells, > 2^18 counter slots) -- verdicts and
 per-rule counters equal the evalACL oracle (aclengine_mock.go:473-668) on
@@ -34,10 +34,10 @@ def _oracle(rules, tr):
 
 @pytest.mark.parametrize("seed", range(4))
 @pytest.mark.parametrize("trie,wide", [("1", "0"), ("1", "1"), ("0", "1")])
-def test_forced_trie_wide_match_oracle(eng, monkeypatch, seed, trie, wide):
-    monkeypatch.setenv("CONTIVCLS_ORIENT", "src")
-    monkeypatch.setenv("CONTIVCLS_TRIE", trie)
-    monkeypatch.setenv("CONTIVCLS_WIDE", wide)
+def test_forced_trie_wide_match_oracle(eng, libopt, seed, trie, wide):
+    libopt.set("orient", "src", eng)
+    libopt.set("trie", trie, eng)
+    libopt.set("wide", wide, eng)
     rules, pool = single_port_acl(seed * 17 + 5, 200, n_prefixes=60)
     tr = random_traffic(seed, 50000, pool)
     t = eng.put_table("tw", rules)
@@ -56,19 +56,19 @@ def test_forced_trie_wide_match_oracle(eng, monkeypatch, seed, trie, wide):
 
 
 @pytest.mark.parametrize("partial", [False, True])
-def test_wide_cells_counter_tiers(eng, monkeypatch, partial):
+def test_wide_cells_counter_tiers(eng, libopt, partial):
     """Wide cells with every slot in LDS, and with a budget that leaves two
     thirds of the slots to the global counters."""
     from cls_image import Image, compile_blob
     from vpp_amd import _abi
-    monkeypatch.setenv("CONTIVCLS_ORIENT", "src")
-    monkeypatch.setenv("CONTIVCLS_WIDE", "1")
+    libopt.set("orient", "src", eng)
+    libopt.set("wide", "1", eng)
     rules, pool = single_port_acl(77, 400, n_prefixes=120)
     if partial:
         h = Image(compile_blob(_abi.CRules(rules))).h
         a16 = lambda x: (x + 15) & ~15
         budget = h.img_bytes + h.n_hot * 256 + a16(2 * max(h.n_hot, h.n_ctr // 3))
-        monkeypatch.setenv("CONTIVCLS_LDS_BUDGET", str(budget))
+        libopt.set("lds_budget", str(budget), eng)
     tr = random_traffic(5, 200000, pool)
     t = eng.put_table("tiers", rules)
     try:
@@ -125,17 +125,14 @@ def test_gen_policy_trie_wide_on_gpu(eng, blocks, n_oracle, match):
 
 
 @pytest.mark.parametrize("trie,wide", [("1", "1"), ("0", "1")])
-def test_connection_slot_mode_over_trie_wide(monkeypatch, trie, wide):
+def test_connection_slot_mode_over_trie_wide(trie, wide):
     """Connection batches (the config-3 global ACL and 64 local ACLs, every
     imaged one compiled with wide cells, with / without the trie) evaluate
     them with the classifier's slot mode: equal to orc_test_connection,
     counters included."""
     from test_gpu_connect_scale import _run
     from vpp_amd.engine import Engine
-    monkeypatch.setenv("CONTIVCLS_ORIENT", "src")
-    monkeypatch.setenv("CONTIVCLS_TRIE", trie)
-    monkeypatch.setenv("CONTIVCLS_WIDE", wide)
-    e = Engine()
+    e = Engine(options={"orient": "src", "trie": trie, "wide": wide})
     try:
         _run(e, 3, "classifier", 4, True)
     finally:

@@ -43,13 +43,13 @@ def test_v16_random_acls_both_kernels(eng, seed, n_rules, weird):
 
 @pytest.mark.parametrize("seed", range(2))
 @pytest.mark.parametrize("kind", sorted(VARIANTS))
-def test_v16_all_kernel_variants(eng, seed, kind, monkeypatch):
+def test_v16_all_kernel_variants(eng, seed, kind, libopt):
     """Mixed-family twins of the IPv4 variant tables: every list mode and
     source lookup of the core behind the front end (the source trie for
     trie_*)."""
     if kind.endswith("_pc"):
-        monkeypatch.setenv("CONTIVCLS_LIST_MODE_MAX", "2")
-    monkeypatch.setenv("CONTIVCLS_TRIE", "1" if kind.startswith("trie") else "0")
+        libopt.set("list_mode_max", "2", eng)
+    libopt.set("trie", "1" if kind.startswith("trie") else "0", eng)
     rules, pool = variant_acl(kind, seed)
     rules, tr = mix_families(rules, random_traffic(seed + 11, 20000, pool), seed)
     _assert_same(_gpu(eng, rules, tr), _oracle16(rules, tr, fast=True))
@@ -130,13 +130,13 @@ def test_config5_table_on_gpu(eng):
 
 @pytest.mark.parametrize("seed", range(4))
 @pytest.mark.parametrize("kind", ["v4", "mixed", "v16"])
-def test_v16_source_trie_on_gpu(eng, seed, kind, monkeypatch):
+def test_v16_source_trie_on_gpu(eng, seed, kind, libopt):
     """src_mode 2 (forced): IPv4-mapped sources through the trie over their
     IPv4 word, the others through the non-IPv4 search, protocols > 2 through
     the global table -- classify16_cls and the linear cross-check against the
     oracle, verdicts and counters."""
     from aclgen import random_acl
-    monkeypatch.setenv("CONTIVCLS_V16_SRC_TRIE", "1")
+    libopt.set("v16_src_trie", "1", eng)
     if kind == "v16":
         rules, pool = random_acl16(seed * 101 + 7, 150, 0.1, n_prefixes=60)
         tr = random_traffic16(seed + 40, 20000, pool)

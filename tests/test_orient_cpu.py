@@ -33,8 +33,8 @@ def _same(got, want):
 
 @pytest.mark.parametrize("seed", range(6))
 @pytest.mark.parametrize("n_rules,weird", [(60, 0.0), (200, 0.01), (400, 0.0)])
-def test_destination_keyed_v4(seed, n_rules, weird, monkeypatch):
-    monkeypatch.setenv("CONTIVCLS_ORIENT", "dst")
+def test_destination_keyed_v4(seed, n_rules, weird, libopt):
+    libopt.set("orient", "dst")
     rules, pool = random_acl(seed * 31 + n_rules, n_rules, weird)
     img = _img(rules)
     if not img.has_cls:
@@ -46,8 +46,8 @@ def test_destination_keyed_v4(seed, n_rules, weird, monkeypatch):
 
 
 @pytest.mark.parametrize("seed", range(4))
-def test_destination_keyed_v16(seed, monkeypatch):
-    monkeypatch.setenv("CONTIVCLS_ORIENT", "dst")
+def test_destination_keyed_v16(seed, libopt):
+    libopt.set("orient", "dst")
     rules, pool = random_acl16(seed + 40, 150, 0.02)
     img = _img(rules, "cls_compile_v16")
     assert img.h.core.swap == 1

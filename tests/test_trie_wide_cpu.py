@@ -46,9 +46,9 @@ def _chunk_edges(pool, n, seed):
 
 @pytest.mark.parametrize("seed", range(10))
 @pytest.mark.parametrize("n_prefixes", [24, 120])
-def test_trie_matches_oracle(monkeypatch, seed, n_prefixes):
-    monkeypatch.setenv("CONTIVCLS_ORIENT", "src")
-    monkeypatch.setenv("CONTIVCLS_TRIE", "1")
+def test_trie_matches_oracle(libopt, seed, n_prefixes):
+    libopt.set("orient", "src")
+    libopt.set("trie", "1")
     rules, pool = single_port_acl(seed * 7 + 3, 160, n_prefixes=n_prefixes)
     tr = random_traffic(seed, 4000, pool)
     tr["src"][::3] = _chunk_edges(pool, len(tr["src"][::3]), seed)
@@ -60,12 +60,12 @@ def test_trie_matches_oracle(monkeypatch, seed, n_prefixes):
 
 @pytest.mark.parametrize("seed", range(8))
 @pytest.mark.parametrize("trie", ["0", "1"])
-def test_wide_cells_match_oracle(monkeypatch, seed, trie):
-    """Wide cells forced (CONTIVCLS_WIDE=1), with the trie or the interval
+def test_wide_cells_match_oracle(libopt, seed, trie):
+    """Wide cells forced (option wide=1), with the trie or the interval
     search behind them."""
-    monkeypatch.setenv("CONTIVCLS_ORIENT", "src")
-    monkeypatch.setenv("CONTIVCLS_WIDE", "1")
-    monkeypatch.setenv("CONTIVCLS_TRIE", trie)
+    libopt.set("orient", "src")
+    libopt.set("wide", "1")
+    libopt.set("trie", trie)
     rules, pool = single_port_acl(seed * 13 + 1, 140, n_prefixes=40)
     tr = random_traffic(seed + 100, 4000, pool)
     img = _check(rules, tr)
@@ -75,11 +75,11 @@ def test_wide_cells_match_oracle(monkeypatch, seed, trie):
 
 
 @pytest.mark.parametrize("seed", range(4))
-def test_wide_cells_hash_sources(monkeypatch, seed):
+def test_wide_cells_hash_sources(libopt, seed):
     """Wide cells behind the hash LPM (rendered global tables: pod /32s)."""
     from vpp_amd import workload
-    monkeypatch.setenv("CONTIVCLS_ORIENT", "src")
-    monkeypatch.setenv("CONTIVCLS_WIDE", "1")
+    libopt.set("orient", "src")
+    libopt.set("wide", "1")
     acl, spec, _ = workload.config(2)
     tr = oracle.gen_traffic_v4(spec, seed * 5000, 5000)
     img = _check(acl.rules, tr, fast=True)
@@ -87,10 +87,10 @@ def test_wide_cells_hash_sources(monkeypatch, seed):
 
 
 @pytest.mark.parametrize("seed", range(6))
-def test_trie_with_random_weird_rules(monkeypatch, seed):
+def test_trie_with_random_weird_rules(libopt, seed):
     """Adversarial rules (parse failures, nil sections, reversed ranges) over a
     trie image when the compiler picks one."""
-    monkeypatch.setenv("CONTIVCLS_TRIE", "1")
+    libopt.set("trie", "1")
     rules, pool = random_acl(seed * 31 + 9, 120, 0.1, n_prefixes=60)
     tr = random_traffic(seed, 3000, pool)
     tr["src"][::4] = _chunk_edges(pool, len(tr["src"][::4]), seed)

@@ -36,9 +36,11 @@ def main():
     ap.add_argument("--locals", type=int, default=64)
     ap.add_argument("--count", type=int, default=1)
     ap.add_argument("--no-check", action="store_true", help="diagnostic builds: skip the parity asserts")
+    ap.add_argument("--opt", action="append", default=[], metavar="KEY=VALUE",
+                    help="library tuning switch (cls_engine_set_option), repeatable")
     a = ap.parse_args()
     from vpp_amd.engine import Engine
-    eng = Engine()
+    eng = Engine(options=dict(o.split("=", 1) for o in a.opt))
     ifs, bind, by_name, pool, spec = build(eng, 0, cfg=3, n_local=a.locals)
     n = a.n
     tr = random_traffic(7, n, pool, other_proto=bool(a.other_proto))

@@ -100,11 +100,13 @@ def main():
                     help="shares of TCP, UDP, ICMP, protocol 47")
     ap.add_argument("--layout", type=int, default=4, choices=[4, 16])
     ap.add_argument("--v6", type=float, default=0.0, help="16-byte layout: share of IPv6 addresses")
+    ap.add_argument("--opt", action="append", default=[], metavar="KEY=VALUE",
+                    help="library tuning switch (cls_engine_set_option), repeatable")
     a = ap.parse_args()
     from vpp_amd import configurator as C
     from vpp_amd.engine import Engine
     from vpp_amd.renderer.api import PodID
-    eng = Engine()
+    eng = Engine(options=dict(o.split("=", 1) for o in a.opt))
     for nb in a.blocks:
         pol = C.gen_policy(random.Random(nb), num_cidrs=nb)
         txn = C.PolicyConfigurator({PodID("db", "default"): "10.1.1.1"}).new_txn(False)

@@ -16,7 +16,7 @@
 #   gp:<layout>        gen-policy 20-block list: 64 / 256 Mi packets, TCP/UDP only
 #   gpmix:<layout>     the 20-block list without protocol 47, without ICMP
 #   gpb:<bytes>:<layout>:<blocks>  a gen-policy ingress list compiled with an
-#                      LDS budget of <bytes> (CONTIVCLS_LDS_BUDGET: counter tiers)
+#                      LDS budget of <bytes> (option lds_budget: counter tiers)
 #   ab:<config>:<lib>  one-process A/B of the classify kernel against a variant
 #   sq:<config>        SQ counter passes of the classify kernel (tools/sq_profile.sh)
 #   sqgp:<layout>:<blocks>  the same for a gen-policy ingress list
@@ -85,7 +85,7 @@ for step in "$@"; do
     done ;;
   gpb)
     bud=${arg%%:*}; rest=${arg#*:}; lay=${rest%%:*}; nb=${rest#*:}
-    CONTIVCLS_LDS_BUDGET=$bud timeout -k 10 300 python tools/genpolicy_bench.py --layout $lay --v6 0.1 --blocks $nb --match ingress --packets 67108864 --iters 5 > $O/gpb_${bud}_${lay}_$nb.jsonl 2> $O/gpb_${bud}_${lay}_$nb.err
+    timeout -k 10 300 python tools/genpolicy_bench.py --opt lds_budget=$bud --layout $lay --v6 0.1 --blocks $nb --match ingress --packets 67108864 --iters 5 > $O/gpb_${bud}_${lay}_$nb.jsonl 2> $O/gpb_${bud}_${lay}_$nb.err
     python3 tools/jl.py $O/gpb_${bud}_${lay}_$nb.jsonl rules ctr16 lds_slots slots kernel_ms Gpps_kernel ;;
   ab)
     cfg=${arg%%:*}; v=${arg#*:}

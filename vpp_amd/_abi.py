@@ -16,7 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CONTIVCLS_LIB") or os.path.join(_HERE, "libcontivcls.so")
 
 SOURCES = ("kernels.hip", "kernels_dev.hpp", "k4_ldsv.hip", "k4_rest.hip", "k4_pair.hip", "k16.hip", "kernels.hpp", "compile.cpp",
-           "compile.hpp", "engine.cpp", "goparse.hpp", "engine_int.hpp", "fleet.cpp")
+           "compile.hpp", "engine.cpp", "goparse.hpp", "engine_int.hpp", "fleet.cpp", "options.cpp", "options.hpp")
 
 
 def source_hash() -> str:
@@ -37,7 +37,7 @@ AF_V4, AF_V16 = 4, 16
 # batch fields and flags (cls_batch_*)
 BF_SRC, BF_DST, BF_SPORT, BF_DPORT, BF_PROTO, BF_VERDICT, BF_SRC_IF, BF_DST_IF = range(8)
 BATCH_CONN, BATCH_MIRROR = 1, 2
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 R_MATCHES, R_MACIP, R_IPRULE, R_IP, R_OTHER = 1, 2, 4, 8, 16
 R_TCP, R_TCP_SRC, R_TCP_DST = 32, 64, 128
@@ -45,7 +45,7 @@ R_UDP, R_UDP_SRC, R_UDP_DST = 256, 512, 1024
 R_ICMP, R_ICMP_CODE, R_ICMP_TYPE, R_ICMPV6, R_ACTIONS = 2048, 4096, 8192, 16384, 32768
 
 # the exported symbols (checked by tests/test_abi.py against include/contivcls.h)
-SYMBOLS = ["cls_abi_version", "cls_engine_create", "cls_engine_destroy", "cls_last_error",
+SYMBOLS = ["cls_abi_version", "cls_engine_create", "cls_engine_destroy", "cls_last_error", "cls_engine_set_option",
            "cls_table_put", "cls_table_del", "cls_table_get_info", "cls_classify",
            "cls_last_kernel_ms", "cls_kernel_times", "cls_kernel_starts", "cls_kernel_times_reset", "cls_acl_put", "cls_acl_del", "cls_acl_table", "cls_acl_counts",
            "cls_if_id",
@@ -177,6 +177,7 @@ def bind(path: str, strict: bool = True):
         "cls_engine_create": (C.c_int, [C.POINTER(Config), C.POINTER(vp)]),
         "cls_engine_destroy": (None, [vp]),
         "cls_last_error": (C.c_char_p, [vp]),
+        "cls_engine_set_option": (C.c_int, [vp, C.c_char_p, C.c_char_p]),
         "cls_table_put": (C.c_int, [vp, C.c_char_p, C.POINTER(ClsRule), u32, C.POINTER(u32)]),
         "cls_table_del": (C.c_int, [vp, u32]),
         "cls_table_get_info": (C.c_int, [vp, u32, C.POINTER(TableInfo)]),
@@ -202,9 +203,9 @@ def bind(path: str, strict: bool = True):
         "cls_acl_stats": (C.c_int, [vp, C.POINTER(u32), C.POINTER(u32)]),
         "cls_gen_traffic_v4": (C.c_int, [vp, C.POINTER(TrafficSpec), u64, u64, vp, vp, vp, vp,
                                          vp, vp]),
-        "cls_compile_v4": (C.c_int, [C.POINTER(ClsRule), u32, vp, u64, C.POINTER(u64)]),
+        "cls_compile_v4": (C.c_int, [C.POINTER(ClsRule), u32, vp, u64, C.POINTER(u64), C.c_char_p]),
         "cls_image_kernel": (C.c_int, [u32, u32, C.c_int, C.c_int]),
-        "cls_compile_v16": (C.c_int, [C.POINTER(ClsRule), u32, vp, u64, C.POINTER(u64)]),
+        "cls_compile_v16": (C.c_int, [C.POINTER(ClsRule), u32, vp, u64, C.POINTER(u64), C.c_char_p]),
         "cls_gen_traffic_v16": (C.c_int, [vp, C.POINTER(TrafficSpec16), u64, u64, vp, vp, vp, vp,
                                           vp, vp]),
         "cls_engine_devices": (C.c_int, [vp, C.POINTER(u32)]),

@@ -274,11 +274,6 @@ struct TmplHash {
 
 uint32_t align4(uint32_t w) { return (w + 3u) & ~3u; }
 
-// an environment switch set to a non-zero number (diagnostics and tests)
-bool env_flag(const char* name) {
-    const char* v = std::getenv(name);
-    return v && std::atoi(v) != 0;
-}
 
 // Two-table cuckoo hash of (key, class): table 0 at [0, cap), table 1 at
 // [cap, 2 cap); entry = key | class << 32.
@@ -646,11 +641,11 @@ uint32_t Cls4Image::row_of(uint32_t addr) const {
 }
 
 // LDS of one classify workgroup available to the image and its counters
-// (CONTIVCLS_LDS_BUDGET: diagnostics and tests, to exercise the counter tiers
+// (option lds_budget: diagnostics and tests, to exercise the counter tiers
 // with small tables).
 uint32_t lds_budget() {
-    if (const char* b = std::getenv("CONTIVCLS_LDS_BUDGET"))
-        return std::min<uint32_t>(kLdsBudget - kLdsReserved, uint32_t(std::strtoul(b, nullptr, 0)));
+    const int b = compile_opts().lds_budget;
+    if (b >= 0) return std::min<uint32_t>(kLdsBudget - kLdsReserved, uint32_t(b));
     return kLdsBudget - kLdsReserved;
 }
 
@@ -774,8 +769,8 @@ static bool build_cls4_one(const std::vector<SemRule>& sem, uint32_t n_rules, Cl
             img.mode = 0;                            // the OTHER image: interval search (Cls4Opts)
         } else if (opt && opt->ext_src) {
             img.mode = 3;                            // the caller maps addresses to rows
-        } else if (keys.size() <= kMaxHashLens && !env_flag("CONTIVCLS_SRC_SEARCH")) {
-            // (CONTIVCLS_SRC_SEARCH=1: the interval search always -- tests)
+        } else if (keys.size() <= kMaxHashLens && !compile_opts().src_search) {
+            // (option src_search: the interval search always -- tests)
             img.mode = 1;
             img.default_class = dflt;
             for (const auto& kv : keys) {
@@ -1036,10 +1031,9 @@ static bool build_cls4_one(const std::vector<SemRule>& sem, uint32_t n_rules, Cl
             // word of it (MI355X LDS: bank = (a/4) mod 32), so distinct ports
             // never collide.  Dense tables (load > 1/2) take a longer search
             // for a collision-free multiplier: 18 ports in 32 slots succeed
-            // with p ~ 0.3 % per multiplier.  CONTIVCLS_PHASH_DENSE=0: at
+            // with p ~ 0.3 % per multiplier.  Option phash_dense=0: at
             // least 2 slots per port (diagnostics / A/B).
-            const char* dn = std::getenv("CONTIVCLS_PHASH_DENSE");
-            const bool dense = !(dn && std::atoi(dn) == 0);
+            const bool dense = compile_opts().phash_dense;
             uint64_t z = 0x243F6A8885A308D3ull;           // splitmix64 stream of odd multipliers
             for (uint32_t L = 4; L <= 11 && !phash_mul; ++L) {
                 const bool half = (1u << L) >= 2 * special.size();
@@ -1079,9 +1073,9 @@ static bool build_cls4_one(const std::vector<SemRule>& sem, uint32_t n_rules, Cl
             }
         }
     }
-    // diagnostics / tests: cap the list mode (CONTIVCLS_LIST_MODE_MAX)
-    if (const char* mx = std::getenv("CONTIVCLS_LIST_MODE_MAX")) {
-        const uint32_t cap = uint32_t(std::strtoul(mx, nullptr, 0));
+    // diagnostics / tests: cap the list mode (option list_mode_max)
+    if (compile_opts().list_mode_max >= 0) {
+        const uint32_t cap = uint32_t(compile_opts().list_mode_max);
         if (lmode > cap)
             lmode = cap >= 3 && lmode >= 3 ? 3u
                   : cap >= 2 && lmode >= 2 ? 2u : (cap >= 1 && std::max(Sd, Sp) <= kMaxBvSteps ? 1u : 0u);
@@ -1179,7 +1173,7 @@ static bool build_cls4_one(const std::vector<SemRule>& sem, uint32_t n_rules, Cl
         if (trie) {
             Trie tr;
             if (!build_trie(bounds, n_real_bounds, iclass, uint32_t(w.size()) * 4, lds_budget(), tr)) {
-                if (std::getenv("CONTIVCLS_DEBUG_MODES"))
+                if (compile_opts().debug_modes)
                     std::fprintf(stderr, "trie: does not fit (%zu words at depth %u)\n", tr.words.size(), tr.depth);
                 return false;
             }
@@ -1344,7 +1338,7 @@ static bool build_cls4_one(const std::vector<SemRule>& sem, uint32_t n_rules, Cl
     // image resident and the coldest slots counted in global memory (Cls4Image
     // counter tiers).  With neither, the image stays in global memory (list
     // mode 1 when possible: its cells need no list scan).
-    const bool dbg = std::getenv("CONTIVCLS_DEBUG_MODES") != nullptr;   // diagnostics
+    const bool dbg = compile_opts().debug_modes;   // diagnostics
     const uint32_t budget = lds_budget();
     std::vector<uint32_t> seq;
     for (uint32_t lm = lmode;;) {
@@ -1354,9 +1348,9 @@ static bool build_cls4_one(const std::vector<SemRule>& sem, uint32_t n_rules, Cl
     }
     if (opt && opt->other) seq.assign(1, 0u);     // the OTHER image: template scan (Cls4Opts)
     // diagnostics / tests: exactly this list mode when it is available
-    // (CONTIVCLS_LIST_MODE), so a test's LDS budget picks the counter tier
-    else if (const char* f = std::getenv("CONTIVCLS_LIST_MODE")) {
-        const uint32_t lm = uint32_t(std::strtoul(f, nullptr, 0));
+    // (option list_mode), so a test's LDS budget picks the counter tier
+    else if (compile_opts().list_mode >= 0) {
+        const uint32_t lm = uint32_t(compile_opts().list_mode);
         if (std::find(seq.begin(), seq.end(), lm) != seq.end()) seq.assign(1, lm);
     }
     // block offset field: 16 bits in 8-B units (modes 1, 2); mode 3: the
@@ -1367,13 +1361,11 @@ static bool build_cls4_one(const std::vector<SemRule>& sem, uint32_t n_rules, Cl
                                    : img.img_bytes / 8u <= 0xFFFFu && img.ctr_rule.size() <= 0xFFFFu);
     };
     // The source trie where the interval search would run (sublist modes;
-    // CONTIVCLS_TRIE=0 / 1: never / only -- diagnostics and tests), preferred
+    // option trie=0 / 1: never / only -- diagnostics and tests), preferred
     // when it fits; wide cells only once no LDS-cell image fits
-    // (CONTIVCLS_WIDE=1: first -- tests).
-    const char* tenv = std::getenv("CONTIVCLS_TRIE");
-    const char* wenv = std::getenv("CONTIVCLS_WIDE");
-    const int tmode = tenv ? std::atoi(tenv) : -1;
-    const bool wide_first = wenv && std::atoi(wenv) == 1, wide_never = wenv && std::atoi(wenv) == 0;
+    // (option wide=1: first -- tests).
+    const int tmode = compile_opts().trie;
+    const bool wide_first = compile_opts().wide == 1, wide_never = compile_opts().wide == 0;
     // (the 16-byte core searching reps takes them too; not the OTHER image).
     // Behind a hash LPM the trie is the second choice (two probes beat it
     // when the hash tables fit; large ones -- many prefixes of few lengths,
@@ -1611,12 +1603,12 @@ static bool build_cls16_one(const std::vector<SemRule>& sem, uint32_t n_rules, C
         img.sem.push_back(r);
     }
     // Source front end: host-route hashes when every source prefix is a host
-    // route (CONTIVCLS_V16_SRC_SEARCH=1 forces the interval search, src_mode
+    // route (option v16_src_search=1 forces the interval search, src_mode
     // 0: tests)
     bool hosts = true;
     for (int f = 0; f < 2; ++f)
         for (const auto& r : side[0].pf[f]) hosts = hosts && r.lo == r.hi;
-    if (const char* e = std::getenv("CONTIVCLS_V16_SRC_SEARCH")) hosts = hosts && std::atoi(e) == 0;
+    if (compile_opts().v16_src_search >= 0) hosts = hosts && compile_opts().v16_src_search == 0;
     img.src_mode = hosts ? 1u : 0u;
 
     // interval tables: per side, keys (start - 1 as u64 hi, lo; padding all
@@ -1663,7 +1655,7 @@ static bool build_cls16_one(const std::vector<SemRule>& sem, uint32_t n_rules, C
     // core's classes), other sources through a search over the non-IPv4
     // intervals whose values are rows; the whole interval table stays in
     // global memory for protocols > 2 (they need the rep).
-    // CONTIVCLS_V16_SRC_TRIE=0 / 1: never / whenever sources are not all host
+    // option v16_src_trie=0 / 1: never / whenever sources are not all host
     // routes (tests).
     std::vector<u128> s_start;
     std::vector<uint32_t> s_rep;
@@ -1685,8 +1677,8 @@ static bool build_cls16_one(const std::vector<SemRule>& sem, uint32_t n_rules, C
             v6rep.push_back(s_rep[j]);
         }
     }
-    bool trie = !hosts && v4b.size() >= kV16TrieMin && !std::getenv("CONTIVCLS_V16_SRC_SEARCH");
-    if (const char* e = std::getenv("CONTIVCLS_V16_SRC_TRIE")) trie = !hosts && std::atoi(e) != 0;
+    bool trie = !hosts && v4b.size() >= kV16TrieMin && compile_opts().v16_src_search < 0;
+    if (compile_opts().v16_src_trie >= 0) trie = !hosts && compile_opts().v16_src_trie != 0;
     if (trie) img.src_mode = 2;
     Cls4Opts opt;
     opt.ext_src = hosts || trie;
@@ -1881,12 +1873,8 @@ bool good_enough(const Cls4Image& m) {
     return m.lds_ok && m.n_lctr == m.n_ctr && m.list_mode >= 1 && m.list_mode <= 4;
 }
 
-// CONTIVCLS_ORIENT=src|dst (diagnostics, tests): one orientation only
-int forced_orient() {
-    const char* f = std::getenv("CONTIVCLS_ORIENT");
-    if (!f) return -1;
-    return std::strcmp(f, "dst") == 0 ? 1 : 0;
-}
+// option orient=src|dst (diagnostics, tests): one orientation only
+int forced_orient() { return compile_opts().orient; }
 
 }  // namespace
 

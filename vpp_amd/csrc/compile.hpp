@@ -33,6 +33,7 @@
 
 #include "../../include/contivcls.h"
 #include "goparse.hpp"
+#include "options.hpp"
 
 namespace cls {
 

@@ -31,9 +31,9 @@ using namespace cls;
 // the queue exists per (table, stream), and a full segment classifies in
 // place, so a cap costs only speed on batches with > 6 % protocol > 2),
 // split into one segment per wave (kOtherSegs): the entries per segment.
-// CONTIVCLS_OTHER_CAP (per workgroup): tests, to reach the in-place path.
-static uint32_t other_cap(uint64_t n, int grid) {
-    if (const char* c = std::getenv("CONTIVCLS_OTHER_CAP")) return uint32_t(std::strtoul(c, nullptr, 0)) / kOtherSegs;
+// Option other_cap (per workgroup): tests, to reach the in-place path.
+static uint32_t other_cap(const cls_engine* e, uint64_t n, int grid) {
+    if (e->opts.other_cap) return e->opts.other_cap / kOtherSegs;
     const uint64_t want = (n / uint64_t(std::max(grid, 1)) + 15) / 16;
     return uint32_t(std::min<uint64_t>(16384, std::max<uint64_t>(1024, want))) / kOtherSegs;
 }
@@ -102,6 +102,7 @@ void engine_close(cls_engine* e) {
 extern "C" {
 
 const char* cls_last_error(const cls_engine* e) { return e ? e->err.c_str() : "null engine"; }
+
 
 // ---------------------------------------------------------------------------
 // The slot -> rule map of a table variant as the remap kernel reads it: every
@@ -234,6 +235,7 @@ static int scratch_of(cls_engine* e, Counters& c, uint32_t n_rules, hipStream_t 
 static int table_compile(cls_engine* e, const char* name, const cls_rule* rules, uint32_t n,
                          std::shared_ptr<Table>& out) {
     if (n && !rules) return fail(e, CLS_E_INVAL, "rules is NULL");
+    const CompileScope scope(e->opts);      // the engine's compiler options
     auto t = std::make_shared<Table>();
     t->name = name ? name : "";
     t->n_rules = n;
@@ -345,6 +347,26 @@ static int refuse_peer(cls_engine* e) {
     return fail(e, CLS_E_INVAL, "configure a multi-device engine through its primary engine");
 }
 
+// Diagnostics and tests: one tuning switch (options.hpp) on the engine and,
+// for a multi-device engine, on every device's engine.
+int cls_engine_set_option(cls_engine* e, const char* key, const char* value) {
+    if (!e) return CLS_E_INVAL;
+    std::lock_guard<std::mutex> g(e->mu);
+    const DeviceGuard dg;        // the caller's device again on return
+    if (e->primary) return refuse_peer(e);
+    std::string why;
+    Opts o = e->opts;
+    if (!opts_set(o, key, value, why)) return fail(e, CLS_E_INVAL, "%s", why.c_str());
+    e->opts = o;
+    for (cls_engine* p : e->peers) {
+        std::lock_guard<std::mutex> gp(p->mu);
+        p->opts = o;
+    }
+    // a kept connection plan was made under the old options
+    e->conn_gen++;
+    return sync_peers(e);
+}
+
 // A table (or a dropped binding) is gone: the kept connection plan must not
 // hold its device buffers until the next device batch replans.
 static void drop_conn_plan(cls_engine* e) {
@@ -369,6 +391,7 @@ int cls_table_put(cls_engine* e, const char* name, const cls_rule* rules, uint32
                   uint32_t* table_id) {
     if (!e) return CLS_E_INVAL;
     std::lock_guard<std::mutex> g(e->mu);
+    const DeviceGuard dg;        // the caller's device again on return
     if (e->primary) return refuse_peer(e);
     const int rc = table_put_locked(e, name, rules, n_rules, table_id);
     return rc == CLS_OK ? sync_peers(e) : rc;
@@ -377,6 +400,7 @@ int cls_table_put(cls_engine* e, const char* name, const cls_rule* rules, uint32
 int cls_table_del(cls_engine* e, uint32_t table_id) {
     if (!e) return CLS_E_INVAL;
     std::lock_guard<std::mutex> g(e->mu);
+    const DeviceGuard dg;        // the caller's device again on return
     if (e->primary) return refuse_peer(e);
     HIPC(e, hipSetDevice(e->device));
     if (!e->tables.erase(table_id)) return fail(e, CLS_E_NOTFOUND, "no table %u", table_id);
@@ -514,8 +538,8 @@ static int cls_grid(const cls_engine* e, bool use_cls, bool lds_resident, uint32
         // ms, profiles/r04d_bench_c2{_wg1,}.json; the config-3 stream floor
         // 0.519 against 0.538 ms)
         if (lds_resident) per_cu = 1;
-        if (const char* w = std::getenv("CONTIVCLS_WG_PER_CU"))   // diagnostics
-            per_cu = std::max(1, std::min(by_threads, std::atoi(w)));
+        if (e->opts.wg_per_cu > 0)   // diagnostics
+            per_cu = std::max(1, std::min(by_threads, e->opts.wg_per_cu));
     }
     const uint64_t want = (n + 4ull * 1024 - 1) / (4ull * 1024);
     return int(std::max<uint64_t>(1, std::min<uint64_t>(uint64_t(e->n_cu) * per_cu, want)));
@@ -697,7 +721,7 @@ static int classify16_locked(cls_engine* e, std::shared_ptr<Table> t, const cls_
     if (n) {
         Cls4Dev cd = cls4_dev(c, q.d_img, q.d_lin, uint32_t(q.lin.size()), t->n_rules);
         cfg.other = cls4_dev(q.oimg, q.d_oimg, DevBuf(), 0, t->n_rules);
-        cd.oq_cap = other_cap(std::min<uint64_t>(n, kClsChunk), cfg.grid);
+        cd.oq_cap = other_cap(e, std::min<uint64_t>(n, kClsChunk), cfg.grid);
         {
             const int rc = other_queue(e, sc, cfg.grid, cd.oq_cap, s, &cd.oq);
             if (rc != CLS_OK) return rc;
@@ -735,6 +759,7 @@ int cls_classify(cls_engine* e, uint32_t table_id, const cls_pkt_soa* pk, uint64
                  uint8_t* verdict_out, uint64_t* counters_out, uint32_t flags, void* stream) {
     if (!e || !pk) return CLS_E_INVAL;
     std::lock_guard<std::mutex> g(e->mu);
+    const DeviceGuard dg;        // the caller's device again on return
     return classify_locked(e, table_id, pk, n, verdict_out, counters_out, flags, stream);
 }
 
@@ -800,7 +825,7 @@ int classify_locked(cls_engine* e, uint32_t table_id, const cls_pkt_soa* pk, uin
         if (use_cls) {
             Cls4Dev cd = table_dev(*t);
             cfg.other = cls4_dev(t->oimg, t->d_oimg, DevBuf(), 0, t->n_rules);
-            cd.oq_cap = other_cap(std::min<uint64_t>(n, kClsChunk), cfg.grid);
+            cd.oq_cap = other_cap(e, std::min<uint64_t>(n, kClsChunk), cfg.grid);
             {
                 const int rc = other_queue(e, sc, cfg.grid, cd.oq_cap, s, &cd.oq);
                 if (rc != CLS_OK) return rc;
@@ -865,7 +890,7 @@ static int stream_shapes(cls_engine* e, const cls_pkt_soa* pk, uint64_t n, uint8
     HIPC(e, hipEventCreate(&b));
     int rc = CLS_OK;
     const uint32_t k = std::max<uint32_t>(1, reps);
-    const bool dbg = std::getenv("CONTIVCLS_DEBUG_FLOOR") != nullptr;
+    const bool dbg = e->opts.debug_floor;
     out.clear();
     for (int shape = 0; shape < (v4 ? 8 : 2) && rc == CLS_OK; ++shape) {
         const int grid = e->n_cu * (1 + (shape & 1)), variant = shape >> 1;
@@ -894,6 +919,7 @@ int cls_stream_floor(cls_engine* e, const cls_pkt_soa* pk, uint64_t n, uint8_t* 
                      float* ms, void* stream) {
     if (!e || !ms) return CLS_E_INVAL;
     std::lock_guard<std::mutex> g(e->mu);
+    const DeviceGuard dg;        // the caller's device again on return
     std::vector<float> t;
     const int rc = stream_shapes(e, pk, n, verdict, reps, t, stream);
     if (rc != CLS_OK) return rc;
@@ -905,6 +931,7 @@ int cls_stream_floor_shapes(cls_engine* e, const cls_pkt_soa* pk, uint64_t n, ui
                             float* ms, uint32_t cap, uint32_t* count, void* stream) {
     if (!e || !count || (cap && !ms)) return CLS_E_INVAL;
     std::lock_guard<std::mutex> g(e->mu);
+    const DeviceGuard dg;        // the caller's device again on return
     std::vector<float> t;
     const int rc = stream_shapes(e, pk, n, verdict, reps, t, stream);
     if (rc != CLS_OK) return rc;
@@ -986,6 +1013,7 @@ int cls_acl_put(cls_engine* e, const char* acl_name, const cls_rule* rules, uint
                 uint32_t n_egress) {
     if (!e || !acl_name) return CLS_E_INVAL;
     std::lock_guard<std::mutex> g(e->mu);
+    const DeviceGuard dg;        // the caller's device again on return
     if (e->primary) return refuse_peer(e);
     const int rc = acl_put_locked(e, acl_name, rules, n_rules, ingress_ifs, n_ingress, egress_ifs, n_egress);
     return rc == CLS_OK ? sync_peers(e) : rc;
@@ -1068,6 +1096,7 @@ int cls_acl_stats(cls_engine* e, uint32_t* n_compiles, uint32_t* n_rebinds) {
 int cls_acl_del(cls_engine* e, const char* acl_name) {
     if (!e || !acl_name) return CLS_E_INVAL;
     std::lock_guard<std::mutex> g(e->mu);
+    const DeviceGuard dg;        // the caller's device again on return
     if (e->primary) return refuse_peer(e);
     const int rc = acl_del_locked(e, acl_name);
     return rc == CLS_OK ? sync_peers(e) : rc;
@@ -1093,6 +1122,7 @@ int cls_acl_counts(cls_engine* e, uint32_t* n_acls, uint32_t* n_changes) {
 int cls_if_id(cls_engine* e, const char* if_name, uint32_t* id) {
     if (!e || !if_name || !id) return CLS_E_INVAL;
     std::lock_guard<std::mutex> g(e->mu);
+    const DeviceGuard dg;        // the caller's device again on return
     if (e->primary) return refuse_peer(e);
     *id = if_id_locked(e, if_name);
     return sync_peers(e);
@@ -1205,6 +1235,7 @@ int cls_connect_batch(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t*
                       uint32_t flags, void* stream) {
     if (!e || !c || (n && !out)) return CLS_E_INVAL;
     std::lock_guard<std::mutex> g(e->mu);
+    const DeviceGuard dg;        // the caller's device again on return
     return connect_locked(e, c, n, out, flags, stream, true);
 }
 
@@ -1212,11 +1243,10 @@ int cls_connect_batch(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t*
 
 // The OTHER queue of a pair launch: a fixed segment per workgroup (its
 // overflow is classified in place), so the buffer does not grow with the
-// batch.  CONTIVCLS_PAIR_QCAP: tests, to reach the in-place path.
-// the OTHER queue entries of a pair-launch workgroup (CONTIVCLS_PAIR_QCAP:
-// per wave, tests)
-static uint32_t pair_qcap(uint64_t n, int grid) {
-    if (const char* c = std::getenv("CONTIVCLS_PAIR_QCAP")) return uint32_t(std::strtoul(c, nullptr, 0)) * (kPairBlock / 64);
+// batch: the entries of a pair-launch workgroup (option pair_qcap: per
+// wave, tests, to reach the in-place path).
+static uint32_t pair_qcap(const cls_engine* e, uint64_t n, int grid) {
+    if (e->opts.pair_qcap_set) return e->opts.pair_qcap * (kPairBlock / 64);
     return uint32_t(std::min<uint64_t>(pair_queue_words(n, grid), 16384));
 }
 
@@ -1267,8 +1297,7 @@ int connect_locked(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t* ou
     // bindings and the flags are the same; a host batch picks its large ACLs
     // from a sample of its connections, so it plans every time.
     const bool use_big = n && !(flags & CLS_F_FORCE_LINEAR) && (n >= kConnClsMinBatch || (flags & CLS_F_CONN_CLS));
-    const char* bme = std::getenv("CONTIVCLS_CONN_BITMAP");
-    const bool use_bm = !k16 && n && !(flags & CLS_F_FORCE_LINEAR) && !(bme && std::atoi(bme) == 0);
+    const bool use_bm = !k16 && n && !(flags & CLS_F_FORCE_LINEAR) && e->opts.conn_bitmap;
     const uint64_t key = uint64_t(k16) | uint64_t(count) << 1 | uint64_t(use_big) << 2 |
                          uint64_t((flags & CLS_F_CONN_CLS) != 0) << 3 | uint64_t(use_bm) << 4;
     ConnPlan fresh;
@@ -1371,7 +1400,7 @@ int connect_locked(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t* ou
         // IPv4: the bitmap form of the longer linear ACLs, longest first, while
         // the pool (and the LDS counters when counting) still fit LDS -- a wave
         // then pays a fixed number of reads per evaluation instead of its
-        // longest lane's scan (CONTIVCLS_CONN_BITMAP=0: scans only).
+        // longest lane's scan (option conn_bitmap=0: scans only).
         if (use_bm) {
             const size_t lds_max0 = size_t(max_lds_bytes());
             // the LDS counters take their share only when they can be LDS counters
@@ -1431,17 +1460,17 @@ int connect_locked(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t* ou
     auto pair_ok = [&](const Table& t) {
         const uint32_t *s4 = static_cast<const uint32_t*>(src), *d4 = static_cast<const uint32_t*>(dst);
         return !k16 && t.lds_resident && aligned(s4, 16) && aligned(d4, 16) && aligned(dp, 8) && aligned(sp, 8) &&
-               aligned(pr, 4) && !std::getenv("CONTIVCLS_CONN_NO_PAIR");
+               aligned(pr, 4) && e->opts.conn_pair;
     };
     bool all_pair = !big.empty();
     for (uint32_t b : big) all_pair = all_pair && pair_ok(*dtab[b]);
-    const bool pre_rules = count && all_pair && !std::getenv("CONTIVCLS_CONN_PRE_SLOTS");
+    const bool pre_rules = count && all_pair && e->opts.conn_pre_rules;
     // ... and a batch that does not count needs only the ACLActions: one byte
     // per connection for both tuples (the words would be 8 B)
-    const bool pre_res8 = !count && all_pair && !std::getenv("CONTIVCLS_CONN_PRE_WORDS");
+    const bool pre_res8 = !count && all_pair && e->opts.conn_pre_narrow;
     // ... and a counting one u16 words when every counter index fits 14 bits
     const uint32_t pre_bytes = pre_res8 ? 1u : pre_rules && P.n_ctr <= (1u << 14) &&
-                                                       !std::getenv("CONTIVCLS_CONN_PRE_WORDS") ? 2u : 4u;
+                                                       e->opts.conn_pre_narrow ? 2u : 4u;
     if (!big.empty()) {
         if (n > kClsChunk) return fail(e, CLS_E_INVAL, "connection batch above 2^30 with classifier ACLs");
         HIPC(e, e->s_pre.ensure(big.size() * (pre_res8 ? stride : 2 * stride * pre_bytes)));
@@ -1462,7 +1491,7 @@ int connect_locked(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t* ou
                     uint32_t o_at = (t.img.img_bytes + 15u) & ~15u;
                     // (+ 32: the queue fill word after the images)
                     if (o_at + t.oimg.img_bytes + 32u > uint32_t(max_lds_bytes())) o_at = 0;
-                    if (std::getenv("CONTIVCLS_PAIR_OTHER_GLOBAL")) o_at = 0;   // tests: the global-memory OTHER path
+                    if (e->opts.pair_other_global) o_at = 0;   // tests: the global-memory OTHER path
                     Cls4Dev od = cls4_dev(t.oimg, t.d_oimg, DevBuf(), 0, t.n_rules);
                     if (o_at) {
                         od.off_bounds += o_at; od.off_iclass += o_at; od.off_cells += o_at;
@@ -1472,14 +1501,13 @@ int connect_locked(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t* ou
                     // the OTHER queue, one segment per wave: its first entries
                     // in the LDS left after the images (one workgroup per CU
                     // either way), the rest in global memory
-                    // (CONTIVCLS_PAIR_QCAP / CONTIVCLS_PAIR_LQ: entries per
+                    // (options pair_qcap / pair_lq: entries per
                     // wave in all / in LDS, tests)
                     const uint32_t nwv = kPairBlock / 64;
-                    const uint32_t qw = (pair_qcap(n, cfg.grid) + nwv - 1) / nwv;
+                    const uint32_t qw = (pair_qcap(e, n, cfg.grid) + nwv - 1) / nwv;
                     const uint32_t q_lds = ((o_at ? o_at + t.oimg.img_bytes : t.img.img_bytes) + 15u) & ~15u;
                     uint32_t lq_cap = std::min<uint32_t>(qw, (uint32_t(max_lds_bytes()) - q_lds) / 16u / nwv);
-                    if (const char* lqe = std::getenv("CONTIVCLS_PAIR_LQ"))
-                        lq_cap = std::min<uint32_t>(lq_cap, uint32_t(std::strtoul(lqe, nullptr, 0)));
+                    if (e->opts.pair_lq >= 0) lq_cap = std::min<uint32_t>(lq_cap, uint32_t(e->opts.pair_lq));
                     const uint32_t gq = qw - lq_cap;
                     HIPC(e, e->s_pq.ensure(size_t(cfg.grid) * nwv * std::max<uint32_t>(1, gq) * 16));
                     HIPC(e, launch_classify4_pair(cd, od, o_at, syn, sp, pre, stride, e->s_pq.as<uint32_t>(), gq,
@@ -1517,10 +1545,9 @@ int connect_locked(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t* ou
     a.sport = sp; a.dport = dp; a.proto = pr; a.n = n; a.out = o;
     // LDS: the rule pool first (every evaluation step reads it), then the u32
     // counters if they fit beside it; otherwise global-memory variants
-    // (CONTIVCLS_CONN_NO_LDS, tests: bit 0 rules from global memory, bit 1
+    // (option conn_no_lds, tests: bit 0 rules from global memory, bit 1
     // global counters, bit 2 descriptor / interface tables from global memory)
-    const char* nl = std::getenv("CONTIVCLS_CONN_NO_LDS");
-    const int no_lds = nl ? std::atoi(nl) : 0;
+    const int no_lds = e->opts.conn_no_lds;
     const size_t lds_max = size_t(max_lds_bytes());
     const bool lds_rules = n && !pool.empty() && pool.size() + 16 + kConnStateEntries <= lds_max && !(no_lds & 1);
     // the pool at LDS 0, then the state machine's table, then the rest
@@ -1595,7 +1622,7 @@ int connect_locked(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t* ou
     // interface tables after the pool and counters unless they would cost a
     // workgroup per CU, then (IPv4, `jobs`) the waves' job lists (512 B per
     // wave) on the same terms -- else the kernel's owner search and shuffles
-    // (CONTIVCLS_CONN_NO_JOBS: tests).  Counting with LDS counters and job
+    // (option conn_jobs=0: tests).  Counting with LDS counters and job
     // lists or 16-byte addresses, the kernel holds up to 96 VGPRs (kernels.hip
     // connect_kernel): at most two 512-thread workgroups per CU.
     struct LdsPlan {
@@ -1604,7 +1631,7 @@ int connect_locked(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t* ou
         int per_cu, block;
     };
     auto plan_of = [&](size_t ctr_b, bool jobs) {
-        jobs = jobs && !k16 && !std::getenv("CONTIVCLS_CONN_NO_JOBS");
+        jobs = jobs && !k16 && e->opts.conn_jobs;
         const int cu_cap = cmode == 1 && (jobs || k16) ? 2 : 3;
         auto per_cu_of = [&](size_t b) { return b ? std::max(1, std::min(cu_cap, int(lds_max / b))) : cu_cap; };
         LdsPlan q{lds_used + ctr_b, 0xFFFFFFFFu, 0xFFFFFFFFu, 0, 0};
@@ -1627,15 +1654,14 @@ int connect_locked(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t* ou
     if (cmode == 1) {
         // LDS counters: u32, or u16 pairs (half the LDS, a bound on a
         // workgroup's connections); with job lists (at most two workgroups
-        // per CU) or without (three where the LDS allows).  CONTIVCLS_CONN_PLAN
+        // per CU) or without (three where the LDS allows).  Option conn_plan
         // = 32j / 16j / 32s / 16s forces one (tests, measurements).
         const size_t b32 = size_t(n_ctr) * 4, b16 = conn_lds_ctr_bytes(n_ctr);
         const LdsPlan c[4] = {plan_of(b32, true), plan_of(b16, true), plan_of(b32, false), plan_of(b16, false)};
         int pick = -1;
-        if (const char* f = std::getenv("CONTIVCLS_CONN_PLAN")) {
-            const std::string v(f);
-            pick = v == "32j" ? 0 : v == "16j" ? 1 : v == "32s" ? 2 : v == "16s" ? 3 : -1;
-            if (pick >= 0 && c[pick].lds > lds_max) pick = -1;
+        if (e->opts.conn_plan >= 0) {
+            pick = e->opts.conn_plan;
+            if (c[pick].lds > lds_max) pick = -1;
         }
         if (pick < 0) {
             // the job lists first, then workgroups per CU, then u16 (12 local
@@ -1667,7 +1693,7 @@ int connect_locked(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t* ou
         const uint64_t per_wg = uint64_t(kConnWgConns / block) * block;
         if (n > grid * per_wg) grid = resident * ((n + resident * per_wg - 1) / (resident * per_wg));
     }
-    if (std::getenv("CONTIVCLS_DEBUG_CONN")) {              // diagnostics: the launch's LDS plan
+    if (e->opts.debug_conn) {              // diagnostics: the launch's LDS plan
         size_t nbm = 0;
         for (const ConnDesc& d : desc) nbm += d.bm_off != 0xFFFFFFFFu;
         std::fprintf(stderr, "connect: n %llu desc %zu big %zu bitmaps %zu pool %zu lds_rules %d ctr %u cmode %d "
@@ -1677,12 +1703,12 @@ int connect_locked(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t* ou
                      a.ctr16, per_cu, block, (unsigned long long)grid, P.bm_steps);
     }
     // LDS counters leave the launch as one row per workgroup, summed into the
-    // tables' counters by the rows launch (CONTIVCLS_CONN_FLUSH_ATOMIC: device
+    // tables' counters by the rows launch (option conn_flush_atomic: device
     // atomics into the copies of the call counters and the scatter launch,
     // tests)
     const uint32_t nw = a.ctr16 ? (n_ctr + 1u) / 2u : n_ctr;
     a.ctr_rows = nullptr;
-    if (cmode == 1 && n && !std::getenv("CONTIVCLS_CONN_FLUSH_ATOMIC")) {
+    if (cmode == 1 && n && !e->opts.conn_flush_atomic) {
         HIPC(e, e->s_crows.ensure(size_t(grid) * nw * 4));
         a.ctr_rows = e->s_crows.as<uint32_t>();
     }
@@ -1734,6 +1760,7 @@ int cls_stream_floor_conn(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint
         !aligned(pk.sport, 8) || !aligned(pk.dport, 8) || !aligned(pk.proto, 4) || !aligned(out, 4))
         return fail(e, CLS_E_INVAL, "cls_stream_floor_conn: device arrays must be 16/8/4-byte aligned");
     std::lock_guard<std::mutex> g(e->mu);
+    const DeviceGuard dg;        // the caller's device again on return
     HIPC(e, hipSetDevice(e->device));
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : e->stream;
     ConnArgs a{};
@@ -1779,6 +1806,7 @@ static int conn_counters_dev(cls_engine* d, uint32_t table_id, std::vector<uint6
 int cls_conn_counters(cls_engine* e, uint32_t table_id, uint64_t* counters_out, uint32_t reset) {
     if (!e || !counters_out) return CLS_E_INVAL;
     std::lock_guard<std::mutex> g(e->mu);
+    const DeviceGuard dg;        // the caller's device again on return
     auto it = e->tables.find(table_id);
     if (it == e->tables.end()) return fail(e, CLS_E_NOTFOUND, "no table %u", table_id);
     std::vector<uint64_t> acc(size_t(it->second->n_rules) + 1, 0);
@@ -1801,6 +1829,7 @@ int cls_gen_traffic_v4(cls_engine* e, const cls_traffic_spec* sp, uint64_t first
                        uint8_t* proto, void* stream) {
     if (!e || !sp) return CLS_E_INVAL;
     std::lock_guard<std::mutex> g(e->mu);
+    const DeviceGuard dg;        // the caller's device again on return
     return gen4_locked(e, sp, first, n, src4, dst4, sport, dport, proto, stream, true);
 }
 
@@ -1929,6 +1958,7 @@ int cls_gen_traffic_v16(cls_engine* e, const cls_traffic_spec16* sp, uint64_t fi
                         void* stream) {
     if (!e || !sp) return CLS_E_INVAL;
     std::lock_guard<std::mutex> g(e->mu);
+    const DeviceGuard dg;        // the caller's device again on return
     return gen16_locked(e, sp, first, n, src16, dst16, sport, dport, proto, stream, true);
 }
 
@@ -1947,7 +1977,14 @@ int gen16_locked(cls_engine* e, const cls_traffic_spec16* sp, uint64_t first, ui
             for (int k = 0; k < 16; ++k) v[2 * j + k / 8] = (v[2 * j + k / 8] << 8) | b[16 * size_t(j) + k];
         return v;
     };
+    // the pairs live in the engine (an unsynchronised upload still reads
+    // them after the call returns); an earlier such upload finishes first
+    if (e->gen_pending) HIPC(e, hipStreamSynchronize(s));
+    e->gen_pending = false;
     const std::vector<uint64_t> pods = pairs(sp->pod_ips, sp->n_pod_ips), dsta = pairs(sp->dst_addrs, sp->n_dst);
+    std::vector<uint64_t>& hp = e->gen_pairs;
+    hp.assign(pods.begin(), pods.end());
+    hp.insert(hp.end(), dsta.begin(), dsta.end());
     const size_t bp = pods.size() * 8, bd = dsta.size() * 8, bl = sp->n_dst, bq = size_t(sp->n_ports) * 2;
     auto al = [](size_t x) { return (x + 15) & ~size_t(15); };
     HIPC(e, e->s_pool.ensure(al(bp) + al(bd) + al(bl) + al(bq) + 16));
@@ -1960,10 +1997,11 @@ int gen16_locked(cls_engine* e, const cls_traffic_spec16* sp, uint64_t first, ui
     t.dst_addrs = reinterpret_cast<const uint64_t*>(base + al(bp));
     t.dst_lens = base + al(bp) + al(bd); t.n_dst = sp->n_dst;
     t.ports = reinterpret_cast<const uint16_t*>(base + al(bp) + al(bd) + al(bl)); t.n_ports = sp->n_ports;
-    if (bp) HIPC(e, hipMemcpyAsync(base, pods.data(), bp, hipMemcpyHostToDevice, s));
-    if (bd) HIPC(e, hipMemcpyAsync(base + al(bp), dsta.data(), bd, hipMemcpyHostToDevice, s));
+    if (bp) HIPC(e, hipMemcpyAsync(base, hp.data(), bp, hipMemcpyHostToDevice, s));
+    if (bd) HIPC(e, hipMemcpyAsync(base + al(bp), hp.data() + pods.size(), bd, hipMemcpyHostToDevice, s));
     if (bl) HIPC(e, hipMemcpyAsync(base + al(bp) + al(bd), sp->dst_lens, bl, hipMemcpyHostToDevice, s));
     if (bq) HIPC(e, hipMemcpyAsync(base + al(bp) + al(bd) + al(bl), sp->ports, bq, hipMemcpyHostToDevice, s));
+    e->gen_pending = !sync;
     HIPC(e, launch_gen16(t, first, n, reinterpret_cast<uint4*>(src16), reinterpret_cast<uint4*>(dst16), sport, dport,
                          proto, s));
     if (sync) HIPC(e, hipStreamSynchronize(s));   // the pools are engine scratch
@@ -1972,10 +2010,14 @@ int gen16_locked(cls_engine* e, const cls_traffic_spec16* sp, uint64_t first, ui
 
 extern "C" {
 
-int cls_compile_v4(const cls_rule* rules, uint32_t n, void* blob, uint64_t cap, uint64_t* need) {
+int cls_compile_v4(const cls_rule* rules, uint32_t n, void* blob, uint64_t cap, uint64_t* need,
+                   const char* options) {
     if ((n && !rules) || !need) return CLS_E_INVAL;
     std::vector<SemRule> sem;
     std::string why;
+    Opts o;
+    if (!opts_parse(o, options, why)) return CLS_E_INVAL;
+    const CompileScope scope(o);
     int rc = semantic_rules(rules, n, 4, sem, why);
     if (rc != CLS_OK) return rc;
     std::vector<LinRule4> lin = linear4(sem);
@@ -2027,10 +2069,14 @@ int cls_conn_bitmap_eval(const cls_rule* rules, uint32_t n_rules, const uint32_t
     return CLS_OK;
 }
 
-int cls_compile_v16(const cls_rule* rules, uint32_t n, void* blob, uint64_t cap, uint64_t* need) {
+int cls_compile_v16(const cls_rule* rules, uint32_t n, void* blob, uint64_t cap, uint64_t* need,
+                    const char* options) {
     if ((n && !rules) || !need) return CLS_E_INVAL;
     std::vector<SemRule> sem;
     std::string why;
+    Opts o;
+    if (!opts_parse(o, options, why)) return CLS_E_INVAL;
+    const CompileScope scope(o);
     int rc = semantic_rules(rules, n, 0, sem, why);
     if (rc != CLS_OK) return rc;
     Cls16Image img;

@@ -16,8 +16,25 @@
 #include "../../include/contivcls.h"
 #include "compile.hpp"
 #include "kernels.hpp"
+#include "options.hpp"
 
 using namespace cls;
+
+// The caller's current device, restored when an entry point returns: the
+// library sets each engine's device for its work and leaves the calling
+// thread's HIP state as it found it.
+struct DeviceGuard {
+    int dev = -1;
+    DeviceGuard() {
+        if (hipGetDevice(&dev) != hipSuccess) dev = -1;
+    }
+    ~DeviceGuard() {
+        int now = -1;
+        if (dev >= 0 && hipGetDevice(&now) == hipSuccess && now != dev) (void)hipSetDevice(dev);
+    }
+    DeviceGuard(const DeviceGuard&) = delete;
+    DeviceGuard& operator=(const DeviceGuard&) = delete;
+};
 
 struct DevBuf {
     void* p = nullptr;
@@ -159,6 +176,7 @@ struct ConnPlan {
 struct cls_engine {
     int device = 0;
     int n_cu = 256;
+    Opts opts;                     // tuning / diagnostic switches (cls_engine_set_option)
     hipStream_t stream = nullptr;
     std::mutex mu;
     std::string err;
@@ -188,6 +206,11 @@ struct cls_engine {
     // connection batch over unchanged bindings uploads nothing
     std::vector<uint8_t> up_desc, up_ifs, up_rules, up_tctr;
     DevBuf s_pool;
+    // the 16-byte traffic generator's address pools as (hi, lo) pairs: the
+    // host source of an unsynchronised upload (gen16_locked, sync = false)
+    // outlives the call; gen_pending: such an upload may still be reading it
+    std::vector<uint64_t> gen_pairs;
+    bool gen_pending = false;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool timed = false;
     // per-launch timing (CLS_F_TIMING): event pairs, recycled after a reset

@@ -131,6 +131,16 @@ int comm_make(cls_engine* e, uint32_t n_procs, uint32_t proc, const void* id) {
                     n_procs);
     comm_release(e);
     std::vector<ncclComm_t> comms(G, nullptr);
+    // a failed init leaves none of its communicators behind
+    struct Undo {
+        std::vector<ncclComm_t>& c;
+        bool keep = false;
+        ~Undo() {
+            if (!keep)
+                for (ncclComm_t x : c)
+                    if (x) (void)rccl().comm_destroy(x);
+        }
+    } undo{comms};
     std::vector<int> devs(G);
     for (size_t g = 0; g < G; ++g) devs[g] = dev_engine(e, g)->device;
     if (!id) {
@@ -154,6 +164,7 @@ int comm_make(cls_engine* e, uint32_t n_procs, uint32_t proc, const void* id) {
         }
         RCCLC(e, r.group_end());
     }
+    undo.keep = true;
     for (size_t g = 0; g < G; ++g) {
         cls_engine* d = dev_engine(e, g);
         d->comm = comms[g];
@@ -171,12 +182,24 @@ struct BatchShard {
     uint64_t first = 0, n = 0;         // its packets [first, first + n) of the batch
     DevBuf mem;                        // every field's array
     size_t off[CLS_BF_COUNT] = {};     // byte offsets in mem (256-B aligned)
-    DevBuf fmem[CLS_BF_COUNT];         // CONTIVCLS_BATCH_LAYOUT=1 (measurement): one allocation per field
+    DevBuf fmem[CLS_BF_COUNT];         // option batch_layout=1 (measurement): one allocation per field
     // the hit counters of the last two classify calls (u64, R + 1): a
     // buffer is written again only after its all-reduce has finished
     DevBuf ctr[2];
     hipEvent_t classified[2] = {nullptr, nullptr}, reduced[2] = {nullptr, nullptr};
     bool rec_cls[2] = {false, false}, rec_red[2] = {false, false};
+    BatchShard() = default;
+    BatchShard(const BatchShard&) = delete;
+    BatchShard& operator=(const BatchShard&) = delete;
+    // on the shard's device: its events, then (members) its buffers -- also
+    // on cls_batch_create's error paths
+    ~BatchShard() {
+        if (d) (void)hipSetDevice(d->device);
+        for (int k = 0; k < 2; ++k) {
+            if (classified[k]) (void)hipEventDestroy(classified[k]);
+            if (reduced[k]) (void)hipEventDestroy(reduced[k]);
+        }
+    }
 };
 
 size_t field_bytes(uint32_t af, uint32_t f) {
@@ -392,6 +415,7 @@ int sync_peers(cls_engine* e) {
 extern "C" {
 
 int cls_engine_create(const cls_config* cfg, cls_engine** out) {
+    const DeviceGuard dg;        // the caller's device again on return
     if (!out) return CLS_E_INVAL;
     *out = nullptr;
     std::vector<int> want;
@@ -404,6 +428,7 @@ int cls_engine_create(const cls_config* cfg, cls_engine** out) {
     cls_engine* e = nullptr;
     int rc = engine_open(want[0], &e);
     if (rc != CLS_OK) return rc;
+    std::unique_ptr<cls_engine, void (*)(cls_engine*)> guard(e, cls_engine_destroy);
     bool distinct = true;
     for (size_t i = 1; i < want.size() && rc == CLS_OK; ++i) {
         cls_engine* p = nullptr;
@@ -413,17 +438,26 @@ int cls_engine_create(const cls_config* cfg, cls_engine** out) {
         e->peers.push_back(p);
         for (size_t j = 0; j < i; ++j) distinct = distinct && dev_engine(e, j)->device != p->device;
     }
-    // distinct devices: the counter all-reduce over xGMI from the start
-    if (rc == CLS_OK && want.size() > 1 && distinct) rc = comm_make(e, 1, 0, nullptr);
-    if (rc != CLS_OK) {
-        cls_engine_destroy(e);
-        return rc;
+    if (rc != CLS_OK) return rc;
+    // distinct devices: the counter all-reduce over xGMI from the start.
+    // Without RCCL (not loadable, or its init fails) the engine still runs
+    // every device and sums the counters on the host (cls_comm_info: 0
+    // ranks); cls_last_error keeps the reason, and an explicit cls_comm_init
+    // reports CLS_E_RCCL.
+    if (want.size() > 1 && distinct && comm_make(e, 1, 0, nullptr) != CLS_OK) {
+        for (size_t i = 0; i < n_dev_engines(e); ++i) {
+            cls_engine* d = dev_engine(e, i);
+            d->comm = nullptr;
+            d->comm_ranks = d->comm_rank = 0;
+        }
+        e->err = "no counter all-reduce (host-summed counters): " + e->err;
     }
-    *out = e;
+    *out = guard.release();
     return CLS_OK;
 }
 
 void cls_engine_destroy(cls_engine* e) {
+    const DeviceGuard dg;        // the caller's device again on return
     if (!e || e->primary) return;      // a peer belongs to its primary
     bool comm = false;
     for (size_t i = 0; i < n_dev_engines(e); ++i) comm = comm || dev_engine(e, i)->comm;
@@ -465,6 +499,7 @@ int cls_comm_unique_id(void* id128) {
 int cls_comm_init(cls_engine* e, uint32_t n_procs, uint32_t proc, const void* id128) {
     if (!e) return CLS_E_INVAL;
     std::lock_guard<std::mutex> g(e->mu);
+    const DeviceGuard dg;        // the caller's device again on return
     if (e->primary) return fail(e, CLS_E_INVAL, "cls_comm_init: use the primary engine");
     PeerLocks pl(e);
     return comm_make(e, n_procs, proc, id128);
@@ -482,6 +517,7 @@ int cls_batch_create(cls_engine* e, uint32_t af, uint64_t n, uint32_t flags, cls
     if (!e || !out) return CLS_E_INVAL;
     *out = nullptr;
     std::lock_guard<std::mutex> g(e->mu);
+    const DeviceGuard dg;        // the caller's device again on return
     if (e->primary) return fail(e, CLS_E_INVAL, "create batches on the primary engine");
     if (af != CLS_AF_V4 && af != CLS_AF_V16) return fail(e, CLS_E_INVAL, "af must be CLS_AF_V4 or CLS_AF_V16");
     if (flags & ~uint32_t(CLS_BATCH_CONN | CLS_BATCH_MIRROR)) return fail(e, CLS_E_INVAL, "unknown batch flags");
@@ -492,7 +528,7 @@ int cls_batch_create(cls_engine* e, uint32_t af, uint64_t n, uint32_t flags, cls
     b->flags = flags;
     b->n = n;
     const uint32_t G = uint32_t(n_dev_engines(e));
-    b->sh.resize(G);
+    b->sh = std::vector<BatchShard>(G);
     auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
     for (uint32_t gi = 0; gi < G; ++gi) {
         BatchShard& s = b->sh[gi];
@@ -504,9 +540,8 @@ int cls_batch_create(cls_engine* e, uint32_t af, uint64_t n, uint32_t flags, cls
         // kernel 0.550-0.552 ms against 0.564-0.566 ms packed back to back
         // and 0.553-0.560 ms with one allocation per field
         // (profiles/r05c_batch_layout_ab.txt).
-        // CONTIVCLS_BATCH_LAYOUT (measurement): 0 packed, 1 per field.
-        const char* lay = std::getenv("CONTIVCLS_BATCH_LAYOUT");
-        const int layout = lay ? std::atoi(lay) : 2;
+        // Option batch_layout (measurement): 0 packed, 1 per field.
+        const int layout = e->opts.batch_layout;
         size_t at = 0;
         HIPC(e, hipSetDevice(s.d->device));
         for (uint32_t f = 0; f < CLS_BF_COUNT; ++f) {
@@ -544,30 +579,18 @@ void cls_batch_destroy(cls_batch* b) {
     cls_engine* e = b->e;
     {
         std::lock_guard<std::mutex> g(e->mu);
+        const DeviceGuard dg;        // the caller's device again on return
         PeerLocks pl(e);
+        // the shards' last readers first; their destructors free the events
+        // and buffers on each shard's device
         for (BatchShard& s : b->sh) {
             (void)hipSetDevice(s.d->device);
             (void)hipStreamSynchronize(s.d->stream);
             if (s.d->coll) (void)hipStreamSynchronize(s.d->coll);
-            for (int k = 0; k < 2; ++k) {
-                (void)hipEventDestroy(s.classified[k]);
-                (void)hipEventDestroy(s.reduced[k]);
-                if (s.ctr[k].p) {
-                    (void)hipFree(s.ctr[k].p);
-                    s.ctr[k].p = nullptr;
-                }
-            }
-            if (s.mem.p) {
-                (void)hipFree(s.mem.p);
-                s.mem.p = nullptr;
-            }
-            for (DevBuf& m : s.fmem)
-                if (m.p) {
-                    (void)hipFree(m.p);
-                    m.p = nullptr;
-                }
         }
         if (b->mirror) (void)hipHostFree(b->mirror);
+        b->mirror = nullptr;
+        b->sh.clear();
     }
     delete b;
 }
@@ -601,6 +624,7 @@ int cls_batch_mirror(cls_batch* b, uint32_t field, void** host_ptr) {
 int cls_batch_upload(cls_batch* b, uint32_t field, uint64_t first, uint64_t n, const void* src) {
     if (!b) return CLS_E_INVAL;
     std::lock_guard<std::mutex> g(b->e->mu);
+    const DeviceGuard dg;        // the caller's device again on return
     PeerLocks pl(b->e);
     return batch_move(b, field, first, n, const_cast<uint8_t*>(static_cast<const uint8_t*>(src)), true);
 }
@@ -608,6 +632,7 @@ int cls_batch_upload(cls_batch* b, uint32_t field, uint64_t first, uint64_t n, c
 int cls_batch_download(cls_batch* b, uint32_t field, uint64_t first, uint64_t n, void* dst) {
     if (!b) return CLS_E_INVAL;
     std::lock_guard<std::mutex> g(b->e->mu);
+    const DeviceGuard dg;        // the caller's device again on return
     PeerLocks pl(b->e);
     return batch_move(b, field, first, n, static_cast<uint8_t*>(dst), false);
 }
@@ -616,6 +641,7 @@ int cls_batch_gen_traffic_v4(cls_batch* b, const cls_traffic_spec* spec, uint64_
     if (!b || !spec) return CLS_E_INVAL;
     cls_engine* e = b->e;
     std::lock_guard<std::mutex> g(e->mu);
+    const DeviceGuard dg;        // the caller's device again on return
     if (b->af != CLS_AF_V4) return fail(e, CLS_E_INVAL, "cls_batch_gen_traffic_v4 on a 16-byte batch");
     PeerLocks pl(e);
     for (BatchShard& s : b->sh) {
@@ -632,6 +658,7 @@ int cls_batch_gen_traffic_v16(cls_batch* b, const cls_traffic_spec16* spec, uint
     if (!b || !spec) return CLS_E_INVAL;
     cls_engine* e = b->e;
     std::lock_guard<std::mutex> g(e->mu);
+    const DeviceGuard dg;        // the caller's device again on return
     if (b->af != CLS_AF_V16) return fail(e, CLS_E_INVAL, "cls_batch_gen_traffic_v16 on an IPv4 batch");
     PeerLocks pl(e);
     for (BatchShard& s : b->sh) {
@@ -647,6 +674,7 @@ int cls_batch_gen_traffic_v16(cls_batch* b, const cls_traffic_spec16* spec, uint
 int cls_classify_batch(cls_engine* e, uint32_t table_id, cls_batch* b, uint64_t* counters_out, uint32_t flags) {
     if (!e || !b) return CLS_E_INVAL;
     std::lock_guard<std::mutex> g(e->mu);
+    const DeviceGuard dg;        // the caller's device again on return
     if (b->e != e) return fail(e, CLS_E_INVAL, "the batch belongs to another engine");
     auto it = e->tables.find(table_id);
     if (it == e->tables.end()) return fail(e, CLS_E_NOTFOUND, "no table %u", table_id);
@@ -717,6 +745,7 @@ int cls_classify_batch(cls_engine* e, uint32_t table_id, cls_batch* b, uint64_t*
 int cls_batch_counters(cls_batch* b, uint64_t* out, uint32_t n_out) {
     if (!b || !out) return CLS_E_INVAL;
     std::lock_guard<std::mutex> g(b->e->mu);
+    const DeviceGuard dg;        // the caller's device again on return
     PeerLocks pl(b->e);
     if (b->cur >= 0 && n_out < b->n_ctr) return fail(b->e, CLS_E_INVAL, "counters need %u entries", b->n_ctr);
     std::vector<uint64_t> c;
@@ -729,6 +758,7 @@ int cls_batch_counters(cls_batch* b, uint64_t* out, uint32_t n_out) {
 int cls_batch_connect(cls_engine* e, cls_batch* b, uint32_t flags) {
     if (!e || !b) return CLS_E_INVAL;
     std::lock_guard<std::mutex> g(e->mu);
+    const DeviceGuard dg;        // the caller's device again on return
     if (b->e != e) return fail(e, CLS_E_INVAL, "the batch belongs to another engine");
     if (!(b->flags & CLS_BATCH_CONN)) return fail(e, CLS_E_INVAL, "not a connection batch (CLS_BATCH_CONN)");
     PeerLocks pl(e);
@@ -750,6 +780,7 @@ int cls_batch_wait(cls_batch* b) {
     if (!b) return CLS_E_INVAL;
     cls_engine* e = b->e;
     std::lock_guard<std::mutex> g(e->mu);
+    const DeviceGuard dg;        // the caller's device again on return
     PeerLocks pl(e);
     for (BatchShard& s : b->sh) {
         HIPC(e, hipSetDevice(s.d->device));

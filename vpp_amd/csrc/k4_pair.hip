@@ -23,15 +23,6 @@ namespace cls {
 
 namespace {
 
-#ifndef PAIR_PF2
-#define PAIR_PF2 0
-#endif
-#ifndef PAIR_STAGE_ONLY
-#define PAIR_STAGE_ONLY 0
-#endif
-#ifndef PAIR_NOQ
-#define PAIR_NOQ 0
-#endif
 static_assert(kClsBlock == kPairBlock, "pair_queue_words sizes the queue for this block");
 
 template <int kMode, int kList, int kD>
@@ -77,18 +68,11 @@ __global__ __launch_bounds__(kClsBlock) void classify4_pair(Cls4Dev t, Cls4Dev o
     };
     Fields nx{};
     if (tid < nsteps) fetch(tid, nx);
-#if PAIR_PF2
-    Fields nx2{};
-    if (tid + nthreads < nsteps) fetch(tid + nthreads, nx2);
-#endif
     // both images in one round of loads (a second round is a second memory
     // latency before the first step)
     lds_copy2(smem, reinterpret_cast<const uint4*>(t.img), t.img_bytes / 16u, o_at / 16u,
               reinterpret_cast<const uint4*>(o.img), o_at ? o.img_bytes / 16u : 0u);
     __syncthreads();
-#if PAIR_STAGE_ONLY
-    if (nsteps != 0xFFFFFFFFu) return;
-#endif
     const Img<true> im{nullptr};
     const Img<false> og{reinterpret_cast<const uint8_t*>(o.img)};
     // a word's payload: the slot, or (counting) its counter index
@@ -120,12 +104,7 @@ __global__ __launch_bounds__(kClsBlock) void classify4_pair(Cls4Dev t, Cls4Dev o
     };
     for (uint32_t g = tid; g < nsteps; g += nthreads) {
         const Fields f = nx;
-#if PAIR_PF2
-        nx = nx2;
-        if (g + 2u * nthreads < nsteps) fetch(g + 2u * nthreads, nx2);
-#else
         if (g + nthreads < nsteps) fetch(g + nthreads, nx);
-#endif
         const uint32_t pr = f.pr;
         const uint32_t sa[4] = {f.s4.x, f.s4.y, f.s4.z, f.s4.w}, da[4] = {f.d4.x, f.d4.y, f.d4.z, f.d4.w};
         const uint32_t dpa[4] = {f.dp2.x & 0xFFFFu, f.dp2.x >> 16, f.dp2.y & 0xFFFFu, f.dp2.y >> 16};
@@ -211,7 +190,7 @@ __global__ __launch_bounds__(kClsBlock) void classify4_pair(Cls4Dev t, Cls4Dev o
     // wave's own main-loop stores of the same words complete first
     __threadfence_block();
     // lane 0's fill is current: the main loop's active lanes are a prefix
-    const uint32_t nq = PAIR_NOQ ? 0u : min(__builtin_amdgcn_readlane(wq, 0), lqw + gqw);
+    const uint32_t nq = min(__builtin_amdgcn_readlane(wq, 0), lqw + gqw);
     for (uint32_t j = lane; j < nq; j += 64u) {
         uint4 e;
         if (j < lqw) {
@@ -232,7 +211,7 @@ void launch_pair_d(const Cls4Dev& t, const Cls4Dev& o, uint32_t o_at, const Pkts
                    uint32_t ctr_base, uint32_t wbytes, uint32_t lq_cap, const LaunchCfg& cfg) {
     const uint32_t q_lds = ((o_at ? o_at + o.img_bytes : t.img_bytes) + 15u) & ~15u;   // the waves' LDS segments
     const size_t lds = q_lds + size_t(lq_cap) * 16u * (kPairBlock / 64);
-    lds_attr(reinterpret_cast<const void*>(classify4_pair<kMode, kList, kD>), lds);
+    lds_attr<classify4_pair<kMode, kList, kD>>();
     hipLaunchKernelGGL((classify4_pair<kMode, kList, kD>), dim3(cfg.grid), dim3(kClsBlock), lds, cfg.stream, t, o,
                        o_at, p, sport, out, stride, oq, oq_cap, q_lds, slot_rule, ctr_base, wbytes, lq_cap);
 }

@@ -1106,7 +1106,7 @@ hipError_t launch_connect(const ConnArgs& a, bool k16, bool lds_rules, int count
     const bool jobs = a.job_lds != 0xFFFFFFFFu;
 #define CONN_CASE(K16, L, C, J)                                                                            \
     if (k16 == K16 && lds_rules == L && count == C && jobs == J) {                                         \
-        lds_attr(reinterpret_cast<const void*>(connect_kernel<K16, L, C, J>), lds);                       \
+        lds_attr<connect_kernel<K16, L, C, J>>();                                                          \
         hipLaunchKernelGGL((connect_kernel<K16, L, C, J>), dim3(grid), dim3(block), lds, s, a);            \
         return hipGetLastError();                                                                          \
     }

@@ -37,8 +37,7 @@
 
 #include "kernels.hpp"
 
-#include <map>
-#include <mutex>
+#include <atomic>
 #include <utility>
 
 namespace cls {
@@ -112,21 +111,25 @@ struct Img {
     }
 };
 
-// A kernel's dynamic-LDS ceiling (hipFuncSetAttribute), raised when a launch
-// needs more than before: one host call per (device, kernel) and size, not
-// per launch.  The attribute is the current device's (a multi-device engine
-// launches the same kernels on every device).
-static inline void lds_attr(const void* f, size_t lds) {
-    static std::mutex mu;
-    static std::map<std::pair<int, const void*>, size_t> set;
+// A kernel's dynamic-LDS ceiling (hipFuncSetAttribute), raised once per
+// (kernel, device) to the CU's whole LDS less the kernel's static LDS: the
+// attribute is only a ceiling (a launch's occupancy follows the LDS it asks
+// for), so no launch needs a host call, a lock or a lookup -- one static
+// bit mask per kernel instantiation, a bit per device.  The attribute is the
+// current device's (a multi-device engine launches the same kernels on
+// every device).
+template <auto K>
+inline void lds_attr() {
+    static std::atomic<uint64_t> done{0};
     int dev = 0;
     (void)hipGetDevice(&dev);
-    std::lock_guard<std::mutex> g(mu);
-    size_t& v = set[{dev, f}];
-    if (lds > v) {
-        (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
-        v = lds;
-    }
+    const uint64_t bit = 1ull << (dev & 63);
+    if (done.load(std::memory_order_acquire) & bit) return;
+    const void* f = reinterpret_cast<const void*>(K);
+    hipFuncAttributes fa{};
+    const size_t st = hipFuncGetAttributes(&fa, f) == hipSuccess ? fa.sharedSizeBytes : 0;
+    (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, int(size_t(kLdsMax) - st));
+    done.fetch_or(bit, std::memory_order_release);
 }
 
 // Position of the r-th set bit (0-based) of a 64-bit lane mask: six halving
@@ -493,9 +496,6 @@ __device__ __forceinline__ void wave_count_cold(unsigned long long* gslot, uint3
 __device__ __forceinline__ uint32_t queue_row() { return blockIdx.x * kOtherSegs + (threadIdx.x >> 6); }
 __device__ __forceinline__ uint32_t queue_row0() { return gridDim.x * kOtherSegs; }
 
-#ifndef OQ_NO_STORE
-#define OQ_NO_STORE 0
-#endif
 template <int N, bool kLds, int kMode, int kList, int kD, int kCtr, bool kMaskQ = false, typename SrcOf>
 __device__ __forceinline__ void run_n(const Img<kLds>& im, const Cls4Dev& t, const Cls4Dev& o, uint32_t hot_lane,
                                       unsigned long long* gslot, uint32_t& hot0,
@@ -624,7 +624,7 @@ __device__ __forceinline__ void run_n(const Img<kLds>& im, const Cls4Dev& t, con
             uint32_t* seg = t.oq + queue_row0() + queue_row() * t.oq_cap + base;
 #pragma unroll
             for (int q = 0; q < N; ++q)
-                if (pr[q] > 2u && !OQ_NO_STORE)
+                if (pr[q] > 2u)
                     seg[pre[q] + uint32_t(__popcll(m[q] & lt))] =
                         kMaskQ ? (idx[q] >> 2) | (1u << (28u + (idx[q] & 3u))) : idx[q];
         } else {
@@ -1139,7 +1139,7 @@ template <bool kLds, bool kVec, int kMode, int kList, int kD, int kCtr = 0>
 static void launch_d(const Cls4Dev& t, const Pkts4& p, uint8_t* verdict, unsigned long long* gslot,
                      const LaunchCfg& cfg) {
     const size_t lds = (kLds ? t.lds_bytes : 0) + 16;   // + the OTHER queue counter
-    lds_attr(reinterpret_cast<const void*>(classify4_cls<kLds, kVec, kMode, kList, kD, kCtr>), lds);
+    lds_attr<classify4_cls<kLds, kVec, kMode, kList, kD, kCtr>>();
     if (cfg.ev_start || cfg.ev_stop)
         hipExtLaunchKernelGGL((classify4_cls<kLds, kVec, kMode, kList, kD, kCtr>), dim3(cfg.grid), dim3(kClsBlock),
                               uint32_t(lds), cfg.stream, cfg.ev_start, cfg.ev_stop, 0u, t, cfg.other, p, verdict, gslot);
@@ -1230,7 +1230,7 @@ template <bool kLds, int kMode, int kList, int kD, bool kLin, int kFe, int kCtr 
 static void launch16_d(const Cls4Dev& t, const Fe16& fe, const Pkts16& p, uint8_t* verdict,
                        unsigned long long* gslot, const LaunchCfg& cfg) {
     const size_t lds = (kLds ? t.lds_bytes : 0) + 16;   // + the OTHER queue counter
-    lds_attr(reinterpret_cast<const void*>(classify16_cls<kLds, kMode, kList, kD, kLin, kFe, kCtr>), lds);
+    lds_attr<classify16_cls<kLds, kMode, kList, kD, kLin, kFe, kCtr>>();
     if (cfg.ev_start || cfg.ev_stop)
         hipExtLaunchKernelGGL((classify16_cls<kLds, kMode, kList, kD, kLin, kFe, kCtr>), dim3(cfg.grid),
                               dim3(kClsBlock), uint32_t(lds), cfg.stream, cfg.ev_start, cfg.ev_stop, 0u, t, cfg.other,

@@ -16,6 +16,7 @@ would: the protobuf ACLs by name, pods and interface names.
 from __future__ import annotations
 
 import ctypes as C
+import weakref
 from typing import Optional
 
 import numpy as np
@@ -60,7 +61,7 @@ class Engine:
     compiled once and replicated, batches sharded over the devices, hit
     counters merged by the library's RCCL all-reduce (include/contivcls.h)."""
 
-    def __init__(self, device: int = -1, devices=None):
+    def __init__(self, device: int = -1, devices=None, options: Optional[dict] = None):
         L = _abi.lib()
         if devices:
             self._devs = (C.c_int * len(devices))(*devices)
@@ -74,16 +75,35 @@ class Engine:
                 rc, "RCCL communicator" if rc == _abi.E_RCCL else "no usable gfx950 device"))
         self.h = h
         self._owned = True
+        self._batches = weakref.WeakSet()       # closed before the engine (cls_engine_destroy)
+        self._views = []                        # device_engine() views: invalid once the engine closes
+        for k, v in (options or {}).items():
+            self.set_option(k, v)
 
     @classmethod
     def _view(cls, handle) -> "Engine":
         v = cls.__new__(cls)
         v.h = handle
         v._owned = False
+        v._batches = weakref.WeakSet()
+        v._views = []
         return v
+
+    def set_option(self, key: str, value=None):
+        """cls_engine_set_option: a tuning / diagnostic switch of this engine
+        (tests and measurements: forced list modes, counter tiers, launch
+        plans; include/contivcls.h), ``None`` for its default.  The library
+        never reads the environment."""
+        v = None if value is None else str(value).encode()
+        self._check(_abi.lib().cls_engine_set_option(self.h, key.encode(), v))
 
     def close(self):
         if getattr(self, "h", None) and getattr(self, "_owned", True):
+            # the batches (and borrowed device views) hold this engine's handle
+            for b in list(getattr(self, "_batches", ())):
+                b.close()
+            for v in getattr(self, "_views", ()):
+                v.h = None
             _abi.lib().cls_engine_destroy(self.h)
         self.h = None
 
@@ -98,7 +118,9 @@ class Engine:
         floors, raw device pointers of that device)."""
         d = C.c_void_p()
         self._check(_abi.lib().cls_device_engine(self.h, index, C.byref(d)))
-        return Engine._view(d)
+        v = Engine._view(d)
+        self._views.append(v)
+        return v
 
     def batch(self, n: int, af: int = _abi.AF_V4, conn: bool = False, mirror: bool = False) -> "Batch":
         return Batch(self, n, af, conn, mirror)
@@ -445,6 +467,7 @@ class Batch:
         h = C.c_void_p()
         engine._check(_abi.lib().cls_batch_create(engine.h, af, n, flags, C.byref(h)))
         self.h = h
+        engine._batches.add(self)
 
     def close(self):
         if getattr(self, "h", None):
