@@ -14,10 +14,21 @@ sharded contiguously over the ranks (strong scaling, 2 Gi / N per GPU).  The
 default run is weak: 256 Mi packets per GPU, so N = 8 classifies config 4's
 2 Gi packets.
 
+The measured path is the product's (main_native): the C ABI alone -- an
+engine-owned batch in HBM, cls_classify_batch, and at N>1 the library's own
+ncclAllReduce of the hit counters (cls_comm_init) -- with torch only as the
+launcher's control plane (a gloo group for the RCCL id, barriers and
+max-over-ranks), never on the GPU.  --torch runs the same step through the
+torch harness instead (torch tensors and streams, torch.distributed's
+all-reduce).
+
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
 N>1: one rank per GPU.  Under torch.distributed.run (WORLD_SIZE set) the
 ranks run directly; otherwise bench.py starts torch.distributed.run itself as
 a child process, before anything touches the GPU, and exits with its status.
+Ranks sharing a GPU (fewer devices than ranks: a rehearsal on a one-GPU box)
+run without an RCCL communicator -- RCCL needs one rank per device -- and
+sum their counters over the gloo group.
 """
 from __future__ import annotations
 
@@ -53,10 +64,14 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="CPU baseline threads (default: every core this process may use)")
     ap.add_argument("--no-stream-floor", action="store_true", help="skip the live stream-floor measurement")
-    ap.add_argument("--native", action="store_true",
-                    help="the product path through the C ABI alone: an engine-owned batch (cls_batch_*), "
-                         "cls_classify_batch, and the library's own RCCL counter all-reduce (cls_comm_init); "
-                         "torch only for the launcher's control plane (gloo), never on the GPU")
+    ap.add_argument("--torch", action="store_true",
+                    help="the torch harness instead of the product path: torch tensors and streams on the GPU, "
+                         "counters merged by torch.distributed (the default, main_native, is the C ABI alone: "
+                         "cls_batch_*, cls_classify_batch and the library's RCCL all-reduce)")
+    ap.add_argument("--native", action="store_true", help="(the default) the product path through the C ABI")
+    ap.add_argument("--dump", default="",
+                    help="tests: directory for every rank's verdicts (verdict_r<rank>.npy) and the merged "
+                         "counters (counters.npy, rank 0)")
     ap.add_argument("--events", type=int, default=1, choices=[0, 1, 2],
                     help="1 (the reported line): the classify kernels stamp their own start/end events "
                          "(hipExtLaunchKernel; the step period is start-to-start); diagnostics: 2 adds an "
@@ -173,7 +188,7 @@ def main():
         sys.exit(launch_ranks(args))          # nothing has touched the GPU in this process
     if world != args.gpus:
         sys.exit("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
-    if args.native:
+    if not args.torch:
         return main_native(args, rank, world, local)
     # under torch.distributed.run (also with one rank) the counters are merged
     # by a real collective; a plain N=1 run has no process group
@@ -405,13 +420,20 @@ def main_native(args, rank, world, local):
     counter buffers alternate).  Under torch.distributed.run the ranks join
     one RCCL communicator (cls_comm_init with rank 0's id, exchanged over a
     gloo group that also carries the barriers and max-over-ranks); a plain
-    N=1 run has no communicator."""
+    N=1 run has no communicator.  Ranks that share a GPU (fewer devices
+    than ranks: a rehearsal on a one-GPU box) have no communicator either --
+    RCCL needs one rank per device -- and sum their counters over gloo."""
     import ctypes as C
 
     dist = None
+    device, shared = local, False
     if "WORLD_SIZE" in os.environ:
+        import torch
         import torch.distributed as dist
         dist.init_process_group("gloo")
+        n_dev = torch.cuda.device_count()      # (counting devices does not initialise the GPU)
+        if n_dev and world > n_dev:
+            device, shared = local % n_dev, True
     else:
         os.environ["CONTIVCLS_NO_TORCH"] = "1"     # a plain N=1 run: torch is never imported
     from vpp_amd import _abi, workload
@@ -433,8 +455,8 @@ def main_native(args, rank, world, local):
     strong = args.config == 4
     n = args.packets or (-(-n_default // world) if strong else n_default)
     af = spec.get("layout", 4)
-    eng = Engine(local)                        # one rank per GPU (RCCL: one rank per device)
-    if dist is not None:
+    eng = Engine(device)                       # one rank per GPU (RCCL: one rank per device)
+    if dist is not None and not shared:
         uid = [Engine.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         eng.comm_init(world, rank, uid[0])
@@ -474,6 +496,17 @@ def main_native(args, rank, world, local):
     wall = time.perf_counter() - t0
     kms, starts = eng.kernel_times(reset=True, starts=True)
     counters = b.counters(R)
+    if shared:
+        # no communicator: the ranks' counters summed over the gloo group
+        import torch
+        t = torch.from_numpy(counters.astype(np.int64))
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        counters = t.numpy().astype(np.uint64)
+    if args.dump:
+        os.makedirs(args.dump, exist_ok=True)
+        np.save(os.path.join(args.dump, "verdict_r%d.npy" % rank), b.download(_abi.BF_VERDICT))
+        if rank == 0:
+            np.save(os.path.join(args.dump, "counters.npy"), counters)
     avg_k = float(np.mean(kms)) if kms else float("nan")
     med_k = float(np.median(kms)) if kms else float("nan")
     periods = list(np.diff(starts)) if len(starts) > 1 else []
@@ -546,7 +579,10 @@ def main_native(args, rank, world, local):
                        "path": "native: C ABI only (cls_batch_*, cls_classify_batch), no torch on the GPU",
                        "collective": ("counter all-reduce in the library: ncclAllReduce u64 sum over %d RCCL "
                                       "ranks (cls_comm_init), %d B, side stream overlapping the next step's "
-                                      "classify" % (comm[0], (R + 1) * 8)) if comm[0] else None},
+                                      "classify" % (comm[0], (R + 1) * 8)) if comm[0] else
+                                     ("counters summed over gloo after the timed steps (%d ranks share a GPU: "
+                                      "RCCL needs one rank per device; rehearsal, not a scaling number)" % world)
+                                     if shared else None},
             "counters_sum_ok": ok_sum,
             "settle_ms": round(settle_ms, 1),
             "step_ms_median": round(med_step, 4),

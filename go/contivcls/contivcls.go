@@ -11,18 +11,23 @@
 // (vpp_amd/engine.py, class ACLEngine) calls exactly the same C symbols in
 // the same order and is what the parity tests exercise; keep the two in step.
 //
-// Ownership (cgo rule): every pointer handed to the C ABI is valid only for
-// the duration of the call; the engine deep-copies rules and keeps no caller
-// pointer.  The packet / connection SoA structs are Go values that hold Go
-// slice addresses, so those slices are pinned (runtime.Pinner, Go >= 1.21)
-// for the call; rule records hold only C strings (C.CString).
+// Go 1.9 (the reference's toolchain, .travis.yml:7-8): no runtime.Pinner,
+// no unsafe.Slice, no post-1.9 library call.  Ownership (cgo rule): every
+// pointer handed to the C ABI is valid only for the duration of the call;
+// the engine deep-copies rules and keeps no caller pointer.  Packet and
+// connection arrays go to the static C shims of include/contivcls_go.h as
+// one scalar pointer per slice (pointer-free Go memory, which cgo allows for
+// the call), and the shims build the ABI's SoA records on the C stack -- a
+// Go value holding Go pointers never crosses.  Rule records hold only C
+// strings (C.CString).  The shims themselves run on the GPU in
+// tests/test_gpu_go_shims.py (go/shimtest/shimtest.c, gcc).
 package contivcls
 
 /*
 #cgo CFLAGS: -I${SRCDIR}/../../include
 #cgo LDFLAGS: -L${SRCDIR}/../../vpp_amd -lcontivcls -Wl,-rpath,${SRCDIR}/../../vpp_amd
 #include <stdlib.h>
-#include "contivcls.h"
+#include "contivcls_go.h"
 */
 import "C"
 
@@ -30,7 +35,6 @@ import (
 	"errors"
 	"fmt"
 	"net"
-	"runtime"
 	"strings"
 	"sync"
 	"unsafe"
@@ -80,29 +84,19 @@ func New(c contiv.API, device int) (*Engine, error) {
 // merged by the library's RCCL all-reduce over xGMI.
 func NewMulti(c contiv.API, devices []int) (*Engine, error) {
 	// the library this binding was written against (include/contivcls.h)
-	if v := C.cls_abi_version(); v != C.CLS_ABI_VERSION {
-		return nil, fmt.Errorf("contivcls: library ABI %d, binding ABI %d", int(v), int(C.CLS_ABI_VERSION))
+	if v := C.cls_abi_version(); v != C.clsg_abi_version() {
+		return nil, fmt.Errorf("contivcls: library ABI %d, binding ABI %d", int(v), int(C.clsg_abi_version()))
 	}
 	if len(devices) == 0 {
 		return nil, errors.New("contivcls: no device")
 	}
 	var e *C.cls_engine
-	var cfg C.cls_config
-	cfg.device = C.int(devices[0])
-	if len(devices) > 1 {
-		// the device list lives in C memory for the call (cfg is Go memory)
-		dl := (*[1 << 10]C.int)(C.malloc(C.size_t(len(devices)) * C.size_t(unsafe.Sizeof(C.int(0)))))[:len(devices):len(devices)]
-		defer C.free(unsafe.Pointer(&dl[0]))
-		for i, d := range devices {
-			dl[i] = C.int(d)
-		}
-		cfg.n_devices = C.uint32_t(len(devices))
-		cfg.devices = &dl[0]
+	dl := make([]C.int, len(devices)) // pointer-free Go memory: the shim builds cls_config
+	for i, d := range devices {
+		dl[i] = C.int(d)
 	}
-	switch rc := C.cls_engine_create(&cfg, &e); rc {
+	switch rc := C.clsg_engine_create(&dl[0], C.uint32_t(len(dl)), &e); rc {
 	case C.CLS_OK:
-	case C.CLS_E_RCCL:
-		return nil, errors.New("contivcls: RCCL communicator over the devices failed")
 	default:
 		return nil, errors.New("contivcls: no usable gfx950 device")
 	}
@@ -499,15 +493,14 @@ func (en *Engine) ConnectionBatch(calls []Conn, count bool) ([]aclengine.Connect
 	if n == 0 {
 		return out, nil
 	}
-	// cs is Go memory holding pointers to Go memory: cgo allows that only
-	// for pinned memory, for the length of the call (runtime.Pinner).
-	var pin runtime.Pinner
-	defer pin.Unpin()
-	pinAll(&pin, &sif[0], &dif[0], &sport[0], &dport[0], &proto[0])
-	var cs C.cls_conn_soa
-	cs.src_if, cs.dst_if = (*C.uint32_t)(&sif[0]), (*C.uint32_t)(&dif[0])
-	cs.pkt.sport, cs.pkt.dport = (*C.uint16_t)(&sport[0]), (*C.uint16_t)(&dport[0])
-	cs.pkt.proto = (*C.uint8_t)(&proto[0])
+	// every slice goes to the shim as its own pointer (pointer-free Go
+	// memory); the shim builds cls_conn_soa on the C stack
+	res := make([]uint8, n)
+	flags := C.uint32_t(0)
+	if count {
+		flags |= C.CLS_F_COUNT
+	}
+	var rc C.int
 	if v4 {
 		s4, d4 := make([]uint32, n), make([]uint32, n)
 		for k := 0; k < n; k++ {
@@ -515,34 +508,24 @@ func (en *Engine) ConnectionBatch(calls []Conn, count bool) ([]aclengine.Connect
 			s4[k] = uint32(a[0])<<24 | uint32(a[1])<<16 | uint32(a[2])<<8 | uint32(a[3])
 			d4[k] = uint32(b[0])<<24 | uint32(b[1])<<16 | uint32(b[2])<<8 | uint32(b[3])
 		}
-		pinAll(&pin, &s4[0], &d4[0])
-		cs.pkt.af = C.CLS_AF_V4
-		cs.pkt.src4, cs.pkt.dst4 = (*C.uint32_t)(&s4[0]), (*C.uint32_t)(&d4[0])
-		return en.connect(&cs, n, idx, out, count)
-	}
-	s16, d16 := make([]byte, 16*n), make([]byte, 16*n)
-	for k := 0; k < n; k++ {
-		a, b := sip[k].To16(), dip[k].To16()
-		if a == nil || b == nil {
-			return nil, errors.New("connection endpoint is not an IPv4 or IPv6 address")
+		rc = C.clsg_connect_v4(en.e, (*C.uint32_t)(&sif[0]), (*C.uint32_t)(&dif[0]), (*C.uint32_t)(&s4[0]),
+			(*C.uint32_t)(&d4[0]), (*C.uint16_t)(&sport[0]), (*C.uint16_t)(&dport[0]), (*C.uint8_t)(&proto[0]),
+			C.uint64_t(n), (*C.uint8_t)(&res[0]), flags)
+	} else {
+		s16, d16 := make([]byte, 16*n), make([]byte, 16*n)
+		for k := 0; k < n; k++ {
+			a, b := sip[k].To16(), dip[k].To16()
+			if a == nil || b == nil {
+				return nil, errors.New("connection endpoint is not an IPv4 or IPv6 address")
+			}
+			copy(s16[16*k:], a)
+			copy(d16[16*k:], b)
 		}
-		copy(s16[16*k:], a)
-		copy(d16[16*k:], b)
+		rc = C.clsg_connect_v16(en.e, (*C.uint32_t)(&sif[0]), (*C.uint32_t)(&dif[0]), (*C.uint8_t)(&s16[0]),
+			(*C.uint8_t)(&d16[0]), (*C.uint16_t)(&sport[0]), (*C.uint16_t)(&dport[0]), (*C.uint8_t)(&proto[0]),
+			C.uint64_t(n), (*C.uint8_t)(&res[0]), flags)
 	}
-	pinAll(&pin, &s16[0], &d16[0])
-	cs.pkt.af = C.CLS_AF_V16
-	cs.pkt.src16, cs.pkt.dst16 = (*C.uint8_t)(&s16[0]), (*C.uint8_t)(&d16[0])
-	return en.connect(&cs, n, idx, out, count)
-}
-
-func (en *Engine) connect(cs *C.cls_conn_soa, n int, idx []int, out []aclengine.ConnectionAction,
-	count bool) ([]aclengine.ConnectionAction, error) {
-	res := make([]uint8, n)
-	flags := C.uint32_t(0)
-	if count {
-		flags |= C.CLS_F_COUNT
-	}
-	if rc := C.cls_connect_batch(en.e, cs, C.uint64_t(n), (*C.uint8_t)(&res[0]), flags, nil); rc != C.CLS_OK {
+	if rc != C.CLS_OK {
 		return nil, en.lastErr()
 	}
 	for k, i := range idx {
@@ -634,17 +617,11 @@ func (en *Engine) ClassifyBatch(t *Table, src, dst []uint32, dport []uint16,
 	for i, p := range proto {
 		pr[i] = uint8(p)
 	}
-	var pin runtime.Pinner // pk holds Go pointers: pinned for the call
-	defer pin.Unpin()
-	pinAll(&pin, &src[0], &dst[0], &dport[0], &pr[0])
-	var pk C.cls_pkt_soa
-	pk.af = C.CLS_AF_V4
-	pk.src4, pk.dst4 = (*C.uint32_t)(&src[0]), (*C.uint32_t)(&dst[0])
-	pk.dport, pk.proto = (*C.uint16_t)(&dport[0]), (*C.uint8_t)(&pr[0])
 	en.Lock()
 	defer en.Unlock()
-	if rc := C.cls_classify(en.e, C.uint32_t(t.ID), &pk, C.uint64_t(n), (*C.uint8_t)(&verdict[0]),
-		(*C.uint64_t)(&counters[0]), 0, nil); rc != C.CLS_OK {
+	if rc := C.clsg_classify_v4(en.e, C.uint32_t(t.ID), (*C.uint32_t)(&src[0]), (*C.uint32_t)(&dst[0]),
+		(*C.uint16_t)(&dport[0]), (*C.uint8_t)(&pr[0]), C.uint64_t(n), (*C.uint8_t)(&verdict[0]),
+		(*C.uint64_t)(&counters[0]), 0); rc != C.CLS_OK {
 		return nil, nil, en.lastErr()
 	}
 	return verdict, counters, nil
@@ -673,17 +650,11 @@ func (en *Engine) ClassifyBatchIP(t *Table, src, dst []net.IP, dport []uint16,
 		copy(d16[16*i:], b)
 		pr[i] = uint8(proto[i])
 	}
-	var pin runtime.Pinner // pk holds Go pointers: pinned for the call
-	defer pin.Unpin()
-	pinAll(&pin, &s16[0], &d16[0], &dport[0], &pr[0])
-	var pk C.cls_pkt_soa
-	pk.af = C.CLS_AF_V16
-	pk.src16, pk.dst16 = (*C.uint8_t)(&s16[0]), (*C.uint8_t)(&d16[0])
-	pk.dport, pk.proto = (*C.uint16_t)(&dport[0]), (*C.uint8_t)(&pr[0])
 	en.Lock()
 	defer en.Unlock()
-	if rc := C.cls_classify(en.e, C.uint32_t(t.ID), &pk, C.uint64_t(n), (*C.uint8_t)(&verdict[0]),
-		(*C.uint64_t)(&counters[0]), 0, nil); rc != C.CLS_OK {
+	if rc := C.clsg_classify_v16(en.e, C.uint32_t(t.ID), (*C.uint8_t)(&s16[0]), (*C.uint8_t)(&d16[0]),
+		(*C.uint16_t)(&dport[0]), (*C.uint8_t)(&pr[0]), C.uint64_t(n), (*C.uint8_t)(&verdict[0]),
+		(*C.uint64_t)(&counters[0]), 0); rc != C.CLS_OK {
 		return nil, nil, en.lastErr()
 	}
 	return verdict, counters, nil
@@ -713,15 +684,6 @@ func (en *Engine) ConnCounters(aclName string, reset bool) ([]uint64, error) {
 		return nil, en.lastErr()
 	}
 	return out, nil
-}
-
-// pinAll pins the base of every Go slice whose address goes into a C struct
-// that lives in Go memory (cls_pkt_soa, cls_conn_soa): cgo forbids passing Go
-// memory that holds unpinned Go pointers (cgocheck=1 panics).  Needs Go 1.21+.
-func pinAll(p *runtime.Pinner, ptrs ...interface{}) {
-	for _, x := range ptrs {
-		p.Pin(x)
-	}
 }
 
 // ---- HBM-resident batches (ABI 4) -------------------------------------------
@@ -781,25 +743,33 @@ func (b *Batch) Close() {
 }
 
 // MirrorU32 / MirrorU16 / MirrorU8: the pinned host array of a field (C
-// memory: Go may keep and fill these slices).
+// memory: Go may keep and fill these slices), nil without CLS_BATCH_MIRROR.
+// Go 1.9 slices C memory through a large array type (no unsafe.Slice).
 func (b *Batch) MirrorU32(f uint32) []uint32 {
-	var p unsafe.Pointer
-	C.cls_batch_mirror(b.b, C.uint32_t(f), &p)
-	return unsafe.Slice((*uint32)(p), b.N)
+	p := C.clsg_batch_mirror(b.b, C.uint32_t(f))
+	if p == nil {
+		return nil
+	}
+	return (*[1 << 32]uint32)(p)[:b.N:b.N]
 }
 func (b *Batch) MirrorU16(f uint32) []uint16 {
-	var p unsafe.Pointer
-	C.cls_batch_mirror(b.b, C.uint32_t(f), &p)
-	return unsafe.Slice((*uint16)(p), b.N)
+	p := C.clsg_batch_mirror(b.b, C.uint32_t(f))
+	if p == nil {
+		return nil
+	}
+	return (*[1 << 33]uint16)(p)[:b.N:b.N]
 }
 func (b *Batch) MirrorU8(f uint32) []uint8 {
-	var p unsafe.Pointer
-	C.cls_batch_mirror(b.b, C.uint32_t(f), &p)
-	return unsafe.Slice((*uint8)(p), b.N)
+	p := C.clsg_batch_mirror(b.b, C.uint32_t(f))
+	if p == nil {
+		return nil
+	}
+	return (*[1 << 34]uint8)(p)[:b.N:b.N]
 }
 
-// Upload packets [first, first+n) of a field from src (a Go slice of the
-// field's element type, pinned for the call), or from the mirror (src nil).
+// Upload packets [first, first+n) of a field from src (the base of a Go
+// slice of the field's element type: pointer-free Go memory, valid for the
+// call), or from the mirror (src nil).
 func (b *Batch) Upload(f uint32, first, n int, src unsafe.Pointer) error {
 	if rc := C.cls_batch_upload(b.b, C.uint32_t(f), C.uint64_t(first), C.uint64_t(n), src); rc != C.CLS_OK {
 		return b.en.lastErr()
