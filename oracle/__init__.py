@@ -94,6 +94,10 @@ def lib():
         L.orc_parse_ip.argtypes = [C.c_char_p, C.c_char_p, C.POINTER(C.c_int)]
         L.orc_cidr_contains.restype = C.c_int
         L.orc_cidr_contains.argtypes = [C.c_char_p, C.c_char_p, C.c_int]
+        L.orc_connect_fast.restype = C.c_int
+        L.orc_connect_fast.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p,
+                                       C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                       C.c_uint64, C.c_void_p, C.c_int]
         L.orc_gen_traffic_v16.restype = None
         L.orc_gen_traffic_v16.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64] + [C.c_void_p] * 5
         L.orc_gen_traffic_v4.restype = None
@@ -234,6 +238,31 @@ class FastTable:
         if rc != 0:
             raise RuntimeError("orc_classify_fast rc=%d" % rc)
         return verdict, counters
+
+
+def connect_fast(tables, if_in, if_out, si, di, tr, af=4, nthreads=0):
+    """testConnection over a batch on the fast port (orc_connect_fast,
+    OpenMP): tables = [FastTable]; interface f binds tables[if_in[f]]
+    inbound and tables[if_out[f]] outbound (-1: no ACL); connection i from
+    interface si[i] to di[i], fields of tr (src, dst, proto, sport, dport)."""
+    import numpy as np
+    hs = (C.c_void_p * max(1, len(tables)))(*[t.h for t in tables])
+    ii = np.ascontiguousarray(if_in, np.int32)
+    io = np.ascontiguousarray(if_out, np.int32)
+    a = np.ascontiguousarray(si, np.uint32)
+    b = np.ascontiguousarray(di, np.uint32)
+    adt = np.uint8 if af == 16 else np.uint32
+    s = np.ascontiguousarray(tr["src"], adt)
+    d = np.ascontiguousarray(tr["dst"], adt)
+    pr = np.ascontiguousarray(tr["proto"], np.uint8)
+    sp = np.ascontiguousarray(tr["sport"], np.uint16)
+    dp = np.ascontiguousarray(tr["dport"], np.uint16)
+    out = np.zeros(len(pr), np.uint8)
+    rc = lib().orc_connect_fast(hs, _p(ii), _p(io), len(ii), _p(a), _p(b), af, _p(s), _p(d), _p(pr), _p(sp),
+                                _p(dp), len(pr), _p(out), nthreads)
+    if rc != 0:
+        raise RuntimeError("orc_connect_fast rc=%d" % rc)
+    return out
 
 
 def classify_fast(crules, src, dst, dport, proto, af=4, nthreads=0):

@@ -595,6 +595,63 @@ int orc_classify_fast(const orc_ctable* t, int af, const void* src, const void* 
 }
 
 /* ---------------------------------------------------------------------------
+ * Fast CPU port of a batch of testConnection calls (the connection line's
+ * CPU baseline): the ACLs pre-parsed (orc_compile), testConnection's order
+ * and REFLECT short-cuts exactly as orc_test_connection_hits (itself
+ * aclengine_mock.go:394-471), OpenMP across connections.  Interface f binds
+ * table if_in[f] inbound and if_out[f] outbound (-1: no ACL, evalACL's nil
+ * ACL: PERMIT); connection i enters on si[i] and leaves on di[i].
+ * ------------------------------------------------------------------------ */
+static inline int fast_call(const orc_ctable* const* tabs, int32_t t, const go_ip* s, const go_ip* d, int proto,
+                            uint16_t port) {
+    int32_t hit;
+    if (t < 0) return CLS_ACL_PERMIT;
+    return fast_eval(tabs[t], s, d, proto, port, &hit);
+}
+
+int orc_connect_fast(const orc_ctable* const* tabs, const int32_t* if_in, const int32_t* if_out, uint32_t n_ifs,
+                     const uint32_t* si, const uint32_t* di, int af, const void* src, const void* dst,
+                     const uint8_t* proto, const uint16_t* sport, const uint16_t* dport, uint64_t n,
+                     uint8_t* out, int nthreads) {
+#ifdef _OPENMP
+    if (nthreads <= 0) nthreads = omp_get_max_threads();
+#pragma omp parallel for schedule(static) num_threads(nthreads)
+#endif
+    for (int64_t i = 0; i < (int64_t)n; i++) {
+        const uint32_t a = si[i], b = di[i];
+        if (a >= n_ifs || b >= n_ifs) { out[i] = CLS_CONN_FAILURE; continue; }
+        go_ip s, d;
+        load_ip(af, src, (uint64_t)i, s.b, &s.len);
+        load_ip(af, dst, (uint64_t)i, d.b, &d.len);
+        const int same = a == b, p = proto[i];
+        int src_refl = 0, dst_refl = 0, r;
+        uint8_t v = CLS_CONN_ALLOW;
+        r = fast_call(tabs, if_in[a], &s, &d, p, dport[i]);                     /* SYN: src inbound */
+        if (r == CLS_ACL_FAILURE) { out[i] = CLS_CONN_FAILURE; continue; }
+        if (r == CLS_ACL_DENY) { out[i] = CLS_CONN_DENY_SYN; continue; }
+        if (r == CLS_ACL_REFLECT) { src_refl = 1; if (same) dst_refl = 1; }
+        if (!dst_refl) {                                                         /* SYN: dst outbound */
+            r = fast_call(tabs, if_out[b], &s, &d, p, dport[i]);
+            if (r == CLS_ACL_FAILURE) { out[i] = CLS_CONN_FAILURE; continue; }
+            if (r == CLS_ACL_DENY) { out[i] = CLS_CONN_DENY_SYN; continue; }
+            if (r == CLS_ACL_REFLECT) { dst_refl = 1; if (same) src_refl = 1; }
+        }
+        if (!dst_refl) {                                                         /* SYN-ACK: dst inbound */
+            r = fast_call(tabs, if_in[b], &d, &s, p, sport[i]);
+            if (r == CLS_ACL_FAILURE) { out[i] = CLS_CONN_FAILURE; continue; }
+            if (r == CLS_ACL_DENY) { out[i] = CLS_CONN_DENY_SYN_ACK; continue; }
+        }
+        if (!src_refl) {                                                         /* SYN-ACK: src outbound */
+            r = fast_call(tabs, if_out[a], &d, &s, p, sport[i]);
+            if (r == CLS_ACL_FAILURE) { out[i] = CLS_CONN_FAILURE; continue; }
+            if (r == CLS_ACL_DENY) { out[i] = CLS_CONN_DENY_SYN_ACK; continue; }
+        }
+        out[i] = v;
+    }
+    return 0;
+}
+
+/* ---------------------------------------------------------------------------
  * Synthetic traffic generator (definition in DESIGN.md "Traffic"), identical
  * to the device generator in the product.  Used to check the device stream.
  * ------------------------------------------------------------------------ */

@@ -46,3 +46,39 @@ def test_fast_matches_faithful_weird_random_v4(seed):
     rules, pool = random_acl(seed * 7 + 1, [20, 120, 400][seed % 3], 0.25)
     tr = random_traffic(seed + 100, 4096, pool, other_proto=True)
     _pin(rules, tr)
+
+
+@pytest.mark.parametrize("seed", [0, 3])
+def test_fast_connections_match_faithful(seed):
+    """orc_connect_fast (the connection line's OpenMP CPU baseline) against
+    orc_test_connection_hits (testConnection restated literally,
+    aclengine_mock.go:394-471) on the connection-scale layout: the config-2
+    global table and 12 random local ACLs with malformed rules, 4000
+    connections with same-interface pairs and protocol 47."""
+    from test_gpu_connect_scale import build, oracle_connections
+
+    class Rec:
+        def __init__(self):
+            self.acls = []
+
+        def acl_put(self, name, rules, ing, eg):
+            self.acls.append((name, rules, ing, eg))
+            return 0
+
+    rec = Rec()
+    ifs, bind, by_name, pool, spec = build(rec, seed, n_local=12, n_if=24, cfg=2)
+    names = [a[0] for a in rec.acls]
+    tabs = [oracle.FastTable(oracle.rules_to_c(by_name[x])) for x in names]
+    if_in = [names.index(bind[f][0]) if bind[f][0] else -1 for f in ifs]
+    if_out = [names.index(bind[f][1]) if bind[f][1] else -1 for f in ifs]
+    m = 4000
+    rng = np.random.default_rng(seed)
+    tr = random_traffic(seed + 7, m, pool, other_proto=True)
+    mix = rng.random(m) < 0.4
+    tr["src"][mix] = rng.choice(spec["pod_ips"].astype(np.uint32), mix.sum())
+    si = rng.integers(0, len(ifs), m)
+    di = np.where(rng.random(m) < 0.1, si, rng.integers(0, len(ifs), m))
+    got = oracle.connect_fast(tabs, if_in, if_out, si, di, tr, nthreads=4)
+    want, _ = oracle_connections(bind, by_name, ifs, si, di, tr, 4)
+    np.testing.assert_array_equal(got, want)
+    assert len(set(want.tolist())) >= 3

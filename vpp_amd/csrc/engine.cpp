@@ -82,6 +82,7 @@ int engine_open(int dev, cls_engine** out) {
 // torch streams on the device are not waited for), then frees it.
 void engine_close(cls_engine* e) {
     (void)hipSetDevice(e->device);
+    (void)conn_quiesce(e);
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     if (e->coll) (void)hipStreamSynchronize(e->coll);
     e->conn_plan = ConnPlan();
@@ -370,6 +371,7 @@ int cls_engine_set_option(cls_engine* e, const char* key, const char* value) {
 // A table (or a dropped binding) is gone: the kept connection plan must not
 // hold its device buffers until the next device batch replans.
 static void drop_conn_plan(cls_engine* e) {
+    (void)conn_quiesce(e);          // a stream-ordered batch may still read the plan's tables
     e->conn_plan = ConnPlan();
     e->up_plan = ~0ull;
 }
@@ -1043,6 +1045,8 @@ static int acl_put_locked(cls_engine* e, const char* acl_name, const cls_rule* r
         tid = old->second.table_id;
         Table& kt = *same->second;
         if (kt.d_conn_ctr.p) {
+            const int qrc = conn_quiesce(e);           // a counting batch on another stream may still add
+            if (qrc != CLS_OK) return qrc;
             (void)hipSetDevice(e->device);
             HIPC(e, hipMemsetAsync(kt.d_conn_ctr.p, 0, size_t(kt.n_rules + 1) * 8, e->stream));
             if (!kt.conn_ctr_ev) HIPC(e, hipEventCreateWithFlags(&kt.conn_ctr_ev, hipEventDisableTiming));
@@ -1236,7 +1240,8 @@ int cls_connect_batch(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t*
     if (!e || !c || (n && !out)) return CLS_E_INVAL;
     std::lock_guard<std::mutex> g(e->mu);
     const DeviceGuard dg;        // the caller's device again on return
-    return connect_locked(e, c, n, out, flags, stream, true);
+    // host arrays: returns with the verdicts; CLS_F_DEVICE: stream-ordered
+    return connect_locked(e, c, n, out, flags, stream, false);
 }
 
 }  // extern "C"
@@ -1267,6 +1272,20 @@ int connect_locked(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t* ou
         return fail(e, CLS_E_INVAL, "device src16/dst16 must be 16-byte aligned");
     HIPC(e, hipSetDevice(e->device));
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : e->stream;
+    // Device batches are stream-ordered (the call returns once its launches
+    // are queued, like cls_classify with CLS_F_DEVICE) and share the engine's
+    // connection scratch: the last batch's stream, if another, is waited for
+    // on the GPU (an event recorded on it now); a scratch buffer grows, and
+    // the plan or its uploads change, only once that batch has finished.
+    if (e->conn_last && e->conn_last != s) {
+        if (!e->conn_sync_ev) HIPC(e, hipEventCreateWithFlags(&e->conn_sync_ev, hipEventDisableTiming));
+        HIPC(e, hipEventRecord(e->conn_sync_ev, e->conn_last));
+        HIPC(e, hipStreamWaitEvent(s, e->conn_sync_ev, 0));
+    }
+    auto grow = [&](DevBuf& d, size_t bytes) -> hipError_t {
+        if (bytes > d.bytes && conn_quiesce(e) != CLS_OK) return hipErrorUnknown;
+        return d.ensure(bytes);
+    };
     const uint32_t n_ifs = uint32_t(e->if_acl.size());
     if (!dev)
         for (uint64_t i = 0; i < n; ++i)
@@ -1277,10 +1296,10 @@ int connect_locked(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t* ou
     const uint8_t* pr = pk.proto;
     uint8_t* o = out;
     if (!dev && n) {
-        HIPC(e, e->s_src.ensure(n * ab)); HIPC(e, e->s_dst.ensure(n * ab));
-        HIPC(e, e->s_if_a.ensure(n * 4)); HIPC(e, e->s_if_b.ensure(n * 4));
-        HIPC(e, e->s_sport.ensure(n * 2)); HIPC(e, e->s_dport.ensure(n * 2));
-        HIPC(e, e->s_proto.ensure(n)); HIPC(e, e->s_verdict.ensure(n));
+        HIPC(e, grow(e->s_src, n * ab)); HIPC(e, grow(e->s_dst, n * ab));
+        HIPC(e, grow(e->s_if_a, n * 4)); HIPC(e, grow(e->s_if_b, n * 4));
+        HIPC(e, grow(e->s_sport, n * 2)); HIPC(e, grow(e->s_dport, n * 2));
+        HIPC(e, grow(e->s_proto, n)); HIPC(e, grow(e->s_verdict, n));
         HIPC(e, hipMemcpyAsync(e->s_src.p, src, n * ab, hipMemcpyHostToDevice, s));
         HIPC(e, hipMemcpyAsync(e->s_dst.p, dst, n * ab, hipMemcpyHostToDevice, s));
         HIPC(e, hipMemcpyAsync(e->s_if_a.p, sif, n * 4, hipMemcpyHostToDevice, s));
@@ -1304,6 +1323,10 @@ int connect_locked(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t* ou
     ConnPlan& P = dev ? e->conn_plan : fresh;
     const bool planned = dev && P.gen == e->conn_gen && P.key == key;
     if (!planned) {
+        if (dev) {
+            const int qrc = conn_quiesce(e);        // the kept plan's tables may be in use
+            if (qrc != CLS_OK) return qrc;
+        }
         P = ConnPlan();
         // Snapshot the bindings: one descriptor per bound table, (in, out) per
         // interface.  Linear ACLs' compact rules go to the call's rule pool.
@@ -1473,7 +1496,7 @@ int connect_locked(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t* ou
                                                        e->opts.conn_pre_narrow ? 2u : 4u;
     if (!big.empty()) {
         if (n > kClsChunk) return fail(e, CLS_E_INVAL, "connection batch above 2^30 with classifier ACLs");
-        HIPC(e, e->s_pre.ensure(big.size() * (pre_res8 ? stride : 2 * stride * pre_bytes)));
+        HIPC(e, grow(e->s_pre, big.size() * (pre_res8 ? stride : 2 * stride * pre_bytes)));
         for (size_t b = 0; b < big.size(); ++b) {
             Table& t = *dtab[big[b]];
             uint32_t* pre = reinterpret_cast<uint32_t*>(e->s_pre.as<uint8_t>() +
@@ -1509,7 +1532,7 @@ int connect_locked(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t* ou
                     uint32_t lq_cap = std::min<uint32_t>(qw, (uint32_t(max_lds_bytes()) - q_lds) / 16u / nwv);
                     if (e->opts.pair_lq >= 0) lq_cap = std::min<uint32_t>(lq_cap, uint32_t(e->opts.pair_lq));
                     const uint32_t gq = qw - lq_cap;
-                    HIPC(e, e->s_pq.ensure(size_t(cfg.grid) * nwv * std::max<uint32_t>(1, gq) * 16));
+                    HIPC(e, grow(e->s_pq, size_t(cfg.grid) * nwv * std::max<uint32_t>(1, gq) * 16));
                     HIPC(e, launch_classify4_pair(cd, od, o_at, syn, sp, pre, stride, e->s_pq.as<uint32_t>(), gq,
                                                   pre_rules ? t.d_slot_rule.as<uint32_t>() : nullptr,
                                                   desc[big[b]].ctr_off, pre_bytes, lq_cap, cfg));
@@ -1561,10 +1584,12 @@ int connect_locked(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t* ou
     // (same bindings, same batch kind: nothing to copy)
     auto upload = [&](DevBuf& d, std::vector<uint8_t>& last, const void* src, size_t bytes, size_t min_bytes) -> int {
         const void* was = d.p;
-        HIPC(e, d.ensure(std::max(bytes, min_bytes)));
+        HIPC(e, grow(d, std::max(bytes, min_bytes)));
         const uint8_t* b = static_cast<const uint8_t*>(src);
         if (d.p == was && last.size() == bytes && (bytes == 0 || std::memcmp(last.data(), b, bytes) == 0))
             return CLS_OK;
+        const int qrc = conn_quiesce(e);                 // an earlier copy may still read `last`
+        if (qrc != CLS_OK) return qrc;
         last.assign(b, b + bytes);
         // from the engine's copy: it outlives the call (an unsynchronised
         // batch, sync = false, may still be copying when this returns)
@@ -1592,7 +1617,7 @@ int connect_locked(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t* ou
         // the call counters are zero between calls (the scatter launch clears
         // what it moves); cleared here only when (re)allocated
         const size_t had = e->s_cctr.bytes;
-        HIPC(e, e->s_cctr.ensure(size_t(n_ctr) * 8 * kConnCtrCopies));
+        HIPC(e, grow(e->s_cctr, size_t(n_ctr) * 8 * kConnCtrCopies));
         if (e->s_cctr.bytes != had || !e->cctr_zero)
             HIPC(e, hipMemsetAsync(e->s_cctr.p, 0, e->s_cctr.bytes, s));
         // zero again only once the scatter launch (which clears what it
@@ -1709,7 +1734,7 @@ int connect_locked(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t* ou
     const uint32_t nw = a.ctr16 ? (n_ctr + 1u) / 2u : n_ctr;
     a.ctr_rows = nullptr;
     if (cmode == 1 && n && !e->opts.conn_flush_atomic) {
-        HIPC(e, e->s_crows.ensure(size_t(grid) * nw * 4));
+        HIPC(e, grow(e->s_crows, size_t(grid) * nw * 4));
         a.ctr_rows = e->s_crows.as<uint32_t>();
     }
     HIPC(e, launch_connect(a, k16, lds_rules, cmode, int(grid), block, lds, s));
@@ -1743,10 +1768,14 @@ int connect_locked(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t* ou
         e->cctr_zero = true;            // n == 0: nothing was counted
     }
     if (!dev && n) HIPC(e, hipMemcpyAsync(out, o, n, hipMemcpyDeviceToHost, s));
-    // descriptor, pool and counter buffers are engine scratch: finish before
-    // they can be reused (and before the host vectors above go away); a
-    // batch of a multi-device engine synchronises all its devices at the end
-    if (sync || !dev) HIPC(e, hipStreamSynchronize(s));
+    // a host batch returns with its verdicts; a device batch is
+    // stream-ordered (conn_last: its scratch is reused only behind it)
+    if (sync || !dev) {
+        HIPC(e, hipStreamSynchronize(s));
+        e->conn_last = nullptr;
+    } else if (n) {
+        e->conn_last = s;
+    }
     return CLS_OK;
 }
 

@@ -206,6 +206,12 @@ struct cls_engine {
     // connection batch over unchanged bindings uploads nothing
     std::vector<uint8_t> up_desc, up_ifs, up_rules, up_tctr;
     DevBuf s_pool;
+    // A device connection batch is stream-ordered (connect_locked): the stream
+    // of the last one while it may still run, waited for before its scratch,
+    // plan or tables change (conn_quiesce); a batch on another stream waits
+    // for it on the GPU (conn_sync_ev)
+    hipStream_t conn_last = nullptr;
+    hipEvent_t conn_sync_ev = nullptr;
     // the 16-byte traffic generator's address pools as (hi, lo) pairs: the
     // host source of an unsynchronised upload (gen16_locked, sync = false)
     // outlives the call; gen_pending: such an upload may still be reading it
@@ -234,6 +240,18 @@ struct cls_engine {
     void* stage[2] = {nullptr, nullptr};
     hipEvent_t stage_ev[2] = {nullptr, nullptr};
 };
+
+// Wait for the last stream-ordered connection batch (cls_engine::conn_last).
+inline int conn_quiesce(cls_engine* e) {
+    if (!e->conn_last) return CLS_OK;
+    hipStream_t s = e->conn_last;
+    e->conn_last = nullptr;
+    if (hipStreamSynchronize(s) != hipSuccess) {
+        e->err = "hipStreamSynchronize of the last connection batch failed";
+        return CLS_E_HIP;
+    }
+    return CLS_OK;
+}
 
 // engine i of a multi-device engine (0: the primary itself)
 inline cls_engine* dev_engine(cls_engine* e, size_t i) { return i == 0 ? e : e->peers[i - 1]; }

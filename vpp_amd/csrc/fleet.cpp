@@ -382,6 +382,7 @@ int sync_peers(cls_engine* e) {
             }
         }
         if (dropped) {                  // no kept plan may hold a deleted table's buffers
+            (void)conn_quiesce(p);
             p->conn_plan = ConnPlan();
             p->up_plan = ~0ull;
         }
@@ -772,7 +773,8 @@ int cls_batch_connect(cls_engine* e, cls_batch* b, uint32_t flags) {
                                       false);
         if (rc != CLS_OK) return relay(e, s.d, rc);
     }
-    for (BatchShard& s : b->sh) HIPC(e, hipStreamSynchronize(s.d->stream));
+    // stream-ordered on every shard's device: cls_batch_wait, cls_batch_download
+    // and cls_conn_counters order behind it
     return CLS_OK;
 }
 
