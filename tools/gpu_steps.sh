@@ -62,6 +62,13 @@ for step in "$@"; do
         python3 tools/kstats.py $O/conn_${v}_$loc/run_kernel_stats.csv | grep -E "connect|pair"
       done
     done ;;
+  connx)
+    # connx:<locals>:<tag>[:key=value...]: a connection bench under library options, kernel stats
+    loc=${arg%%:*}; rest=${arg#*:}; t=${rest%%:*}; opts=""; [ "$rest" != "$t" ] && for o in $(echo ${rest#*:} | tr : ' '); do opts="$opts --opt $o"; done
+    (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/connx_${t}_$loc -o run --output-format csv -- python3 $R/tools/conn_bench.py --locals $loc --cpu-sample 0 --cpu-fast-sample 0 --opt debug_conn=1 $opts > $O/connx_${t}_$loc.json 2> $O/connx_${t}_$loc.err)
+    echo "-- $t, $loc local ACLs:$opts"; grep -m2 "connect: n 4194304" $O/connx_${t}_$loc.err || true
+    python3 tools/jl.py $O/connx_${t}_$loc.json hbm_resident hbm_resident_counted
+    python3 tools/kstats.py $O/connx_${t}_$loc/run_kernel_stats.csv | grep -E "connect|pair|rows" ;;
   connn)
     (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/connn_$arg -o run --output-format csv -- python3 $R/tools/conn_bench.py --locals 12 --n $arg --cpu-sample 0 > $O/connn_$arg.json 2> $O/connn_$arg.err)
     python3 tools/jl.py $O/connn_$arg.json hbm_resident hbm_resident_counted

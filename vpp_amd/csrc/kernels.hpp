@@ -287,7 +287,15 @@ struct ConnArgs {
                                  // SYN-ACK result << 2, batches that do not count)
     uint32_t bm_steps;           // bitmap forms: lower-bound steps of the largest interval table
     uint32_t job_lds;            // IPv4: LDS byte offset of the waves' job lists (512 B per wave)
+    uint32_t pf_lds;             // IPv4: LDS byte offset of the waves' field stages (two of kConnPfWave
+                                 // B per wave: the next iteration's fields, DMA'd from HBM); ~0u: none
 };
+// A wave's field stage (ConnArgs::pf_lds): the 64 connections of its next
+// iteration -- src_if, dst_if, src, dst (256 B each), sport, dport (128 B),
+// proto (64 B), then the large ACLs' early result words (kConnEarlyBlocks
+// blocks of 256 B: u8 results, or u16 SYN and SYN-ACK words)
+constexpr uint32_t kConnPfWave = 2048;
+constexpr uint32_t kConnPfEarly = 1344;
 // k16: 16-byte addresses; lds_rules: stage the pool; count: 0 none, 1 LDS
 // counters, 2 global (wave-aggregated) counters; grid: persistent workgroups
 // of `block` threads (512 or 1024); lds: dynamic LDS bytes (pool, LDS
