@@ -1683,11 +1683,17 @@ int connect_locked(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t* ou
             q.job_lds = uint32_t(job_at);
             q.lds = job_at + job_b;
         }
-        const size_t pf_at = (q.lds + 15) & ~size_t(15), pf_b = size_t(q.block / 64) * 2 * kConnPfWave;
-        if (pf_ok && q.meta_lds != 0xFFFFFFFFu && pf_at + pf_b <= lds_max &&
-            (q.per_cu == 1 || per_cu_of(pf_at + pf_b) == q.per_cu)) {
-            q.pf_lds = uint32_t(pf_at);
-            q.lds = pf_at + pf_b;
+        // (two stages per wave; option conn_prefetch=2 takes them also at the
+        // cost of a workgroup per CU -- the stages hide what the waves hid)
+        const size_t pf_at = (q.lds + 15) & ~size_t(15),
+                     pf_b = size_t(q.block / 64) * 2 * conn_pf_wave(uint32_t(big.size()), pre_bytes);
+        if (pf_ok && q.meta_lds != 0xFFFFFFFFu && pf_at + pf_b <= lds_max) {
+            const int pc = per_cu_of(pf_at + pf_b);
+            if (q.per_cu == 1 || pc == q.per_cu || (e->opts.conn_prefetch >= 2 && pc >= 2)) {
+                q.pf_lds = uint32_t(pf_at);
+                q.lds = pf_at + pf_b;
+                q.per_cu = std::min(q.per_cu, pc);
+            }
         }
         return q;
     };
@@ -1724,6 +1730,7 @@ int connect_locked(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t* ou
     a.meta_lds = plan.meta_lds;
     a.job_lds = plan.job_lds;
     a.pf_lds = plan.pf_lds;
+    a.pf_wave = conn_pf_wave(uint32_t(big.size()), pre_bytes);
     const int per_cu = plan.per_cu, block = plan.block;
     // Persistent grid: as many 512-thread workgroups per CU as the LDS
     // allows, at most three (the kernel's registers allow 24 waves per CU);

@@ -436,15 +436,17 @@ __device__ __forceinline__ bool mapped4(const uint4& a) { return (a.x | a.y) == 
 // memory (a.meta_lds == ~0u; uniform branch).  Staged, a connection's
 // interface and descriptor reads are LDS reads instead of dependent global
 // loads in front of every evaluation.
+template <bool kMeta = false>    // kMeta: the tables are in LDS (the kernel variant knows it)
 __device__ __forceinline__ IfAcls conn_if(const ConnArgs& a, uint32_t j) {
-    if (a.meta_lds != 0xFFFFFFFFu) {
+    if (kMeta || a.meta_lds != 0xFFFFFFFFu) {
         const v4u v = *lds128_t(a.meta_lds + a.n_desc * uint32_t(sizeof(ConnDesc)) + 16u * j);
         return IfAcls{int32_t(v.x), int32_t(v.y), int32_t(v.z), int32_t(v.w)};
     }
     return a.ifs[j];
 }
+template <bool kMeta = false>
 __device__ __forceinline__ ConnDesc conn_desc(const ConnArgs& a, uint32_t j) {
-    if (a.meta_lds != 0xFFFFFFFFu) {
+    if (kMeta || a.meta_lds != 0xFFFFFFFFu) {
         const uint32_t b = a.meta_lds + j * uint32_t(sizeof(ConnDesc));
         const v4u x = *lds128_t(b), y = *lds128_t(b + 16u);
         ConnDesc d;
@@ -601,8 +603,8 @@ __device__ __forceinline__ uint32_t conn_state(const uint32_t res[4], bool same,
 
 // kPf (IPv4): every wave DMAs the fields of its next iteration's 64
 // connections from HBM into one of its two LDS stages (a.pf_lds, 2 x
-// kConnPfWave bytes per wave; global_load_lds_dword, so no VGPR holds them
-// in flight) while it works on the current ones, and starts the iteration on
+// a.pf_wave bytes per wave; global_load_lds_dword, so no VGPR holds them in
+// flight) while it works on the current ones, and starts the iteration on
 // LDS reads instead of a round trip to HBM.  The next DMA is issued at the
 // top of an iteration, before anything is live in registers.  A wave whose
 // 64 connections are not all in the batch (the tail) loads them itself.
@@ -626,19 +628,25 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kCount == 
     const uint32_t n_iter = (n + nthreads - 1u) / nthreads;     // uniform trip count (ballots below)
     const uint32_t stride = uint32_t(a.pre_stride);
     // the wave's first connection of iteration `it`, and its field stage
-    const uint32_t wbase = blockIdx.x * blockDim.x + (threadIdx.x & ~63u);
-    const uint32_t pf0 = kPf ? __builtin_amdgcn_readfirstlane(a.pf_lds + (threadIdx.x >> 6) * (2u * kConnPfWave)) : 0u;
+    const uint32_t wbase = __builtin_amdgcn_readfirstlane(blockIdx.x * blockDim.x + (threadIdx.x & ~63u));
+    const uint32_t pf0 = kPf ? __builtin_amdgcn_readfirstlane(a.pf_lds + (threadIdx.x >> 6) * (2u * a.pf_wave)) : 0u;
+    const uint32_t early_b = a.pre_bytes == 1u ? 64u : 256u;   // a block's early words in the stage
     auto staged = [&](uint32_t it) { return wbase + it * nthreads + 64u <= n; };
     auto pf_issue = [&](uint32_t it) {
-        typedef __attribute__((address_space(3))) void* ldsp_t;
-        const uint32_t pf = pf0 + (it & 1u) * kConnPfWave;
+        const uint32_t pf = pf0 + (it & 1u) * a.pf_wave;
         // the lane's dword of an array: uniform base + 32-bit byte offset (the
         // lane term recomputed here, not held in a register across the loop)
         uint32_t l4;
         asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0\n\tv_lshlrev_b32 %0, 2, %0"
                      : "=v"(l4));
+        // (inline asm: the compiler, seeing an LDS-DMA, would drain it with
+        // vmcnt(0) before the iteration's own LDS reads, which it cannot prove
+        // apart from the other stage; the kernel waits for the stage itself)
         auto dma = [&](const void* base, uint32_t off, uint32_t to) {
-            __builtin_amdgcn_global_load_lds(reinterpret_cast<const char*>(base) + off, (ldsp_t)(to), 4, 0, 0);
+            asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dword %1, %2"
+                         :
+                         : "s"(to), "v"(off), "s"(base)
+                         : "memory", "m0");
         };
         const uint32_t b = wbase + it * nthreads;
         dma(a.src_if, 4u * b + l4, pf);
@@ -653,7 +661,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kCount == 
 #pragma unroll
         for (uint32_t k = 0; k < kConnEarlyBlocks; ++k)
             if (k < a.n_big) {
-                const uint32_t e = pf + kConnPfEarly + 256u * k;
+                const uint32_t e = pf + kConnPfEarly + early_b * k;
                 if (a.pre_bytes == 1u) {
                     const uint8_t* w = reinterpret_cast<const uint8_t*>(a.pre) + uint64_t(k) * stride;
                     if (l4 < 64u) dma(w, b + l4, e);
@@ -688,13 +696,12 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kCount == 
         for (uint32_t j = threadIdx.x; j < 4u * a.n_ifs; j += blockDim.x) *lctr_t(a.meta_lds + 4u * (nd + j)) = gi[j];
     }
     __syncthreads();
-    const uint64_t lt = (1ull << lane) - 1ull;
     const A* src = static_cast<const A*>(a.src);
     const A* dst = static_cast<const A*>(a.dst);
     // IPv4: this wave's job list in LDS, 64 entries of 8 B {owner lane | call
     // << 6 | descriptor << 8, port | protocol << 16}; a job's lane writes its
     // result word over the entry's first word
-    const uint32_t jq = a.job_lds + (threadIdx.x >> 6) * 512u;
+    const uint32_t jq = __builtin_amdgcn_readfirstlane(a.job_lds + (threadIdx.x >> 6) * 512u);
     for (uint32_t it = 0; it < n_iter; ++it) {
         const uint32_t i = it * nthreads + blockIdx.x * blockDim.x + threadIdx.x;
         const bool live = i < n;
@@ -704,7 +711,10 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kCount == 
         uint32_t si, dj, sp, dp, pr;
         A sa, da;
         // (u8 / u16 words, packed: one register per block)
-        const bool early = a.n_big == 0u || (a.n_big <= kConnEarlyBlocks && a.pre_bytes <= 2u);
+        // (kPf: the host takes that variant only with early words and staged
+        // tables, so no path of the loop loads from global memory -- a
+        // runtime branch to one would make the compiler drain the stage's DMA)
+        const bool early = kPf || a.n_big == 0u || (a.n_big <= kConnEarlyBlocks && a.pre_bytes <= 2u);
         uint32_t ew[kConnEarlyBlocks] = {};                    // [block]: SYN | SYN-ACK << (8 or 16)
         bool st = false;
         if constexpr (kPf) st = staged(it);
@@ -714,7 +724,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kCount == 
             __builtin_amdgcn_s_waitcnt(0x0F71);                // vmcnt(1)
             asm volatile("" ::: "memory");
             if (it + 1u < n_iter && staged(it + 1u)) pf_issue(it + 1u);
-            const uint32_t pf = pf0 + (it & 1u) * kConnPfWave;
+            const uint32_t pf = pf0 + (it & 1u) * a.pf_wave;
             si = *lds32_t(pf + 4u * lane);
             dj = *lds32_t(pf + 256u + 4u * lane);
             sa = A(*lds32_t(pf + 512u + 4u * lane));
@@ -725,7 +735,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kCount == 
 #pragma unroll
             for (uint32_t b = 0; b < kConnEarlyBlocks; ++b)
                 if (b < a.n_big) {
-                    const uint32_t e = pf + kConnPfEarly + 256u * b;
+                    const uint32_t e = pf + kConnPfEarly + early_b * b;
                     ew[b] = a.pre_bytes == 1u ? uint32_t(*lds8_t(e + lane))
                                               : uint32_t(*lds16_t(e + 2u * lane)) | uint32_t(*lds16_t(e + 128u + 2u * lane)) << 16;
                 }
@@ -737,29 +747,30 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kCount == 
             sp = *at(a.sport, ic);
             dp = *at(a.dport, ic);
             pr = *at(a.proto, ic);
+            if (early) {
+#pragma unroll
+                for (uint32_t b = 0; b < kConnEarlyBlocks; ++b)
+                    if (b < a.n_big) {
+                        if (a.pre_bytes == 1u) {
+                            ew[b] = reinterpret_cast<const uint8_t*>(a.pre)[uint64_t(b) * stride + ic];
+                        } else {
+                            const uint16_t* p16 = reinterpret_cast<const uint16_t*>(a.pre) + uint64_t(2u * b) * stride + ic;
+                            ew[b] = uint32_t(p16[0]) | uint32_t(p16[stride]) << 16;
+                        }
+                    }
+            }
             if constexpr (kPf) {
-                // nothing of this path left pending past the join: a use of
-                // these loads there would otherwise wait for the other
-                // path's DMA as well
+                // nothing of this path left pending past the join (or into
+                // the next iteration): a register it loads would otherwise be
+                // waited for with vmcnt(0) on the staged path too, draining
+                // the stage's DMA
                 __builtin_amdgcn_s_waitcnt(0x0F70);            // vmcnt(0)
                 asm volatile("" ::: "memory");
             }
         }
-        if (early && !st) {
-#pragma unroll
-            for (uint32_t b = 0; b < kConnEarlyBlocks; ++b)
-                if (b < a.n_big) {
-                    if (a.pre_bytes == 1u) {
-                        ew[b] = reinterpret_cast<const uint8_t*>(a.pre)[uint64_t(b) * stride + ic];
-                    } else {
-                        const uint16_t* p16 = reinterpret_cast<const uint16_t*>(a.pre) + uint64_t(2u * b) * stride + ic;
-                        ew[b] = uint32_t(p16[0]) | uint32_t(p16[stride]) << 16;
-                    }
-                }
-        }
         const bool ok = live && si < a.n_ifs && dj < a.n_ifs;   // unknown interface id: Failure
         // both lookups unconditional (an in-range index), the unknown case selected after
-        const IfAcls S0 = conn_if(a, ok ? si : 0u), D0 = conn_if(a, ok ? dj : 0u);
+        const IfAcls S0 = conn_if<kPf>(a, ok ? si : 0u), D0 = conn_if<kPf>(a, ok ? dj : 0u);
         const IfAcls S = ok ? S0 : IfAcls{-1, -1, -1, -1};
         const IfAcls Dif = ok ? D0 : IfAcls{-1, -1, -1, -1};
         const uint32_t p = pr <= 2u ? pr : 3u;
@@ -795,7 +806,8 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kCount == 
         for (int k = 0; k < 4; ++k) {
             job[k] = di[k] >= 0 && bi[k] < 0;
             m[k] = __ballot(job[k]);
-            jpos[k] = c[k] + uint32_t(__popcll(m[k] & lt));
+            // (the set bits of m[k] below this lane: mbcnt, no lane mask held in registers)
+            jpos[k] = c[k] + __builtin_amdgcn_mbcnt_hi(uint32_t(m[k] >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m[k]), 0u));
             c[k + 1] = c[k] + uint32_t(__popcll(m[k]));
         }
         const uint32_t nj = c[4];
@@ -820,7 +832,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kCount == 
                 const uint32_t o = act ? (e.x & 63u) : lane, kk = (e.x >> 6) & 3u;
                 const uint32_t xs = __shfl(uint32_t(sa), int(o)), xd = __shfl(uint32_t(da), int(o));
                 if (act) {
-                    const ConnDesc D = conn_desc(a, e.x >> 8);
+                    const ConnDesc D = conn_desc<kPf>(a, e.x >> 8);
                     const uint32_t port = e.y & 0xFFFFu, xp = e.y >> 16;
                     const uint32_t s1 = kk < 2u ? xs : xd, d1 = kk < 2u ? xd : xs;
                     uint32_t res, rule;
@@ -852,7 +864,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kCount == 
                 const int32_t d0 = __shfl(di[0], int(o)), d1 = __shfl(di[1], int(o));
                 const int32_t d2 = __shfl(di[2], int(o)), d3 = __shfl(di[3], int(o));
                 if (act) {
-                    const ConnDesc D = conn_desc(a, uint32_t(k == 0u ? d0 : k == 1u ? d1 : k == 2u ? d2 : d3));
+                    const ConnDesc D = conn_desc<kPf>(a, uint32_t(k == 0u ? d0 : k == 1u ? d1 : k == 2u ? d2 : d3));
                     const bool syn = k < 2u;
                     uint32_t res, rule;
                     if constexpr (!k16) {
@@ -899,7 +911,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kCount == 
                 if (made[k] && di[k] >= 0) {                    // nil ACLs are not counted
                     if (job[k]) {
                         key[k] = rj[k] >> 2;
-                    } else if (a.pre_rules) {                   // a large ACL: the word's counter index
+                    } else if (kPf || a.pre_rules) {            // a large ACL: the word's counter index
                         key[k] = w[k] >> 2;
                     } else {                                    // ... or its slot's rule
                         const ConnDesc D = conn_desc(a, uint32_t(di[k]));
