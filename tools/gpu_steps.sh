@@ -66,7 +66,7 @@ for step in "$@"; do
     # connx:<locals>:<tag>[:key=value...]: a connection bench under library options, kernel stats
     loc=${arg%%:*}; rest=${arg#*:}; t=${rest%%:*}; opts=""; [ "$rest" != "$t" ] && for o in $(echo ${rest#*:} | tr : ' '); do opts="$opts --opt $o"; done
     (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/connx_${t}_$loc -o run --output-format csv -- python3 $R/tools/conn_bench.py --locals $loc --cpu-sample 0 --cpu-fast-sample 0 --opt debug_conn=1 $opts > $O/connx_${t}_$loc.json 2> $O/connx_${t}_$loc.err)
-    echo "-- $t, $loc local ACLs:$opts"; grep -m2 "connect: n 4194304" $O/connx_${t}_$loc.err || true
+    echo "-- $t, $loc local ACLs:$opts"; awk '/connect: n 4194304/ && !/bitmaps 0 / && !seen[$0]++ && c++ < 4' $O/connx_${t}_$loc.err
     python3 tools/jl.py $O/connx_${t}_$loc.json hbm_resident hbm_resident_counted
     python3 tools/kstats.py $O/connx_${t}_$loc/run_kernel_stats.csv | grep -E "connect|pair|rows" ;;
   connn)

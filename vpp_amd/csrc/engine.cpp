@@ -1649,28 +1649,17 @@ int connect_locked(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t* ou
     // wave) on the same terms -- else the kernel's owner search and shuffles
     // (option conn_jobs=0: tests).  Counting with LDS counters and job
     // lists or 16-byte addresses, the kernel holds up to 96 VGPRs (kernels.hip
-    // connect_kernel): at most two 512-thread workgroups per CU.
+    // connect_kernel): at most two workgroups per CU.
     struct LdsPlan {
         size_t lds;
-        uint32_t meta_lds, job_lds, pf_lds;
+        uint32_t meta_lds, job_lds;
         int per_cu, block;
     };
-    // The waves' field stages (kPf, kernels.hip connect_kernel): IPv4 with
-    // every other load of the kernel's loop an LDS read -- the pool and the
-    // tables staged, the large ACLs' words early (at most kConnEarlyBlocks,
-    // u8 / u16), no global counters, no slot -> rule gather -- and arrays
-    // aligned for dword DMA; placed last, where it costs no workgroup per CU
-    // (option conn_prefetch=0: never).
-    const bool early_words = big.empty() || (big.size() <= kConnEarlyBlocks && pre_bytes <= 2u);
-    const bool pf_ok = e->opts.conn_prefetch && !k16 && n && lds_rules && cmode != 2 && early_words &&
-                       (!count || big.empty() || pre_rules) && aligned(sp, 4) && aligned(dp, 4) && aligned(pr, 4) &&
-                       aligned(sif, 4) && aligned(dif, 4) && aligned(src, 4) && aligned(dst, 4) &&
-                       (big.empty() || aligned(e->s_pre.p, 4));
     auto plan_of = [&](size_t ctr_b, bool jobs) {
         jobs = jobs && !k16 && e->opts.conn_jobs;
         const int cu_cap = cmode == 1 && (jobs || k16) ? 2 : 3;
         auto per_cu_of = [&](size_t b) { return b ? std::max(1, std::min(cu_cap, int(lds_max / b))) : cu_cap; };
-        LdsPlan q{lds_used + ctr_b, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0, 0};
+        LdsPlan q{lds_used + ctr_b, 0xFFFFFFFFu, 0xFFFFFFFFu, 0, 0};
         const size_t meta_at = (q.lds + 15) & ~size_t(15);
         if (meta_at + meta <= lds_max && per_cu_of(meta_at + meta) == per_cu_of(q.lds) && !(no_lds & 4)) {
             q.meta_lds = uint32_t(meta_at);
@@ -1682,18 +1671,6 @@ int connect_locked(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t* ou
         if (jobs && job_at + job_b <= lds_max && (q.per_cu == 1 || per_cu_of(job_at + job_b) == q.per_cu)) {
             q.job_lds = uint32_t(job_at);
             q.lds = job_at + job_b;
-        }
-        // (two stages per wave; option conn_prefetch=2 takes them also at the
-        // cost of a workgroup per CU -- the stages hide what the waves hid)
-        const size_t pf_at = (q.lds + 15) & ~size_t(15),
-                     pf_b = size_t(q.block / 64) * 2 * conn_pf_wave(uint32_t(big.size()), pre_bytes);
-        if (pf_ok && q.meta_lds != 0xFFFFFFFFu && pf_at + pf_b <= lds_max) {
-            const int pc = per_cu_of(pf_at + pf_b);
-            if (q.per_cu == 1 || pc == q.per_cu || (e->opts.conn_prefetch >= 2 && pc >= 2)) {
-                q.pf_lds = uint32_t(pf_at);
-                q.lds = pf_at + pf_b;
-                q.per_cu = std::min(q.per_cu, pc);
-            }
         }
         return q;
     };
@@ -1729,8 +1706,6 @@ int connect_locked(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t* ou
     size_t lds = plan.lds;
     a.meta_lds = plan.meta_lds;
     a.job_lds = plan.job_lds;
-    a.pf_lds = plan.pf_lds;
-    a.pf_wave = conn_pf_wave(uint32_t(big.size()), pre_bytes);
     const int per_cu = plan.per_cu, block = plan.block;
     // Persistent grid: as many 512-thread workgroups per CU as the LDS
     // allows, at most three (the kernel's registers allow 24 waves per CU);
@@ -1747,10 +1722,10 @@ int connect_locked(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t* ou
         size_t nbm = 0;
         for (const ConnDesc& d : desc) nbm += d.bm_off != 0xFFFFFFFFu;
         std::fprintf(stderr, "connect: n %llu desc %zu big %zu bitmaps %zu pool %zu lds_rules %d ctr %u cmode %d "
-                     "meta %s jobs %s prefetch %s lds %zu ctr16 %u per_cu %d block %d grid %llu bm_steps %u\n", (unsigned long long)n,
+                     "meta %s jobs %s lds %zu ctr16 %u per_cu %d block %d grid %llu bm_steps %u\n", (unsigned long long)n,
                      desc.size(), big.size(), nbm, pool.size(), int(lds_rules), n_ctr, cmode,
                      a.meta_lds != 0xFFFFFFFFu ? "lds" : "global", a.job_lds != 0xFFFFFFFFu ? "lds" : "shuffle",
-                     a.pf_lds != 0xFFFFFFFFu ? "lds" : "none", lds,
+                     lds,
                      a.ctr16, per_cu, block, (unsigned long long)grid, P.bm_steps);
     }
     // LDS counters leave the launch as one row per workgroup, summed into the

@@ -564,8 +564,10 @@ __device__ __forceinline__ uint32_t conn_bm(const ConnArgs& a, const ConnDesc& D
 // allows two or more, else one 1024-thread workgroup (16 waves rather than
 // the 8 of one 512-thread one); forcing 64 VGPRs spills to scratch.  The
 // LDS-counter variants with job lists or 16-byte addresses (kCount 1, kJobs
-// or k16) take up to 128 VGPRs (94: no spill, where 80 spilled 20 B) and at
-// most two workgroups per CU (the host's plan).
+// or k16) take up to 128 VGPRs (89: no spill, where 80 spilled 20 B) and at
+// most two 512-thread workgroups per CU (the host's plan; 640-thread ones,
+// 5 waves per SIMD, measured 125 against 88 us: the second workgroup finds
+// no SIMD with room for its third wave -- profiles/r06e_conn_tree_search_ab.txt).
 // kJobs (IPv4): the waves' job lists in LDS (a.job_lds); else the owner
 // search and shuffles (16-byte batches, and IPv4 launches whose LDS is
 // full: the job lists would displace LDS counters or bitmap forms)
@@ -601,25 +603,12 @@ __device__ __forceinline__ uint32_t conn_state(const uint32_t res[4], bool same,
     return v | uint32_t(made[0]) << 2 | uint32_t(made[1]) << 3 | uint32_t(made[2]) << 4 | uint32_t(made[3]) << 5;
 }
 
-// kPf (IPv4): every wave DMAs the fields of its next iteration's 64
-// connections from HBM into one of its two LDS stages (a.pf_lds, 2 x
-// a.pf_wave bytes per wave; global_load_lds_dword, so no VGPR holds them in
-// flight) while it works on the current ones, and starts the iteration on
-// LDS reads instead of a round trip to HBM.  The next DMA is issued at the
-// top of an iteration, before anything is live in registers.  A wave whose
-// 64 connections are not all in the batch (the tail) loads them itself.
-// The host takes this variant only where every other load of the loop is an
-// LDS read (pool and tables staged, the large ACLs' words early): its one
-// other VMEM operation is the verdict store, so vmcnt(1) at the top of an
-// iteration means the stage has landed (loads, stores and LDS-DMA retire in
-// issue order on the VM counter).
-template <bool k16, bool kLdsRules, int kCount, bool kJobs, bool kPf>
+template <bool k16, bool kLdsRules, int kCount, bool kJobs>
 __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kCount == 1 && (kJobs || k16) ? 4 : 6))) void connect_kernel(
     ConnArgs a) {
     typedef typename ConnT<k16>::A A;
     extern __shared__ uint4 smem[];
     typedef __attribute__((address_space(3))) uint32_t* lctr_t;
-    static_assert(!kPf || (!k16 && kLdsRules && kCount != 2), "prefetch: IPv4, LDS pool, no global counters");
     const uint32_t lane = __lane_id();
     // 32-bit connection indices (the host splits batches at 2^30): SGPR base
     // + 32-bit VGPR offset addressing, no 64-bit index arithmetic per load
@@ -627,53 +616,6 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kCount == 
     const uint32_t nthreads = gridDim.x * blockDim.x;
     const uint32_t n_iter = (n + nthreads - 1u) / nthreads;     // uniform trip count (ballots below)
     const uint32_t stride = uint32_t(a.pre_stride);
-    // the wave's first connection of iteration `it`, and its field stage
-    const uint32_t wbase = __builtin_amdgcn_readfirstlane(blockIdx.x * blockDim.x + (threadIdx.x & ~63u));
-    const uint32_t pf0 = kPf ? __builtin_amdgcn_readfirstlane(a.pf_lds + (threadIdx.x >> 6) * (2u * a.pf_wave)) : 0u;
-    const uint32_t early_b = a.pre_bytes == 1u ? 64u : 256u;   // a block's early words in the stage
-    auto staged = [&](uint32_t it) { return wbase + it * nthreads + 64u <= n; };
-    auto pf_issue = [&](uint32_t it) {
-        const uint32_t pf = pf0 + (it & 1u) * a.pf_wave;
-        // the lane's dword of an array: uniform base + 32-bit byte offset (the
-        // lane term recomputed here, not held in a register across the loop)
-        uint32_t l4;
-        asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0\n\tv_lshlrev_b32 %0, 2, %0"
-                     : "=v"(l4));
-        // (inline asm: the compiler, seeing an LDS-DMA, would drain it with
-        // vmcnt(0) before the iteration's own LDS reads, which it cannot prove
-        // apart from the other stage; the kernel waits for the stage itself)
-        auto dma = [&](const void* base, uint32_t off, uint32_t to) {
-            asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dword %1, %2"
-                         :
-                         : "s"(to), "v"(off), "s"(base)
-                         : "memory", "m0");
-        };
-        const uint32_t b = wbase + it * nthreads;
-        dma(a.src_if, 4u * b + l4, pf);
-        dma(a.dst_if, 4u * b + l4, pf + 256u);
-        dma(a.src, 4u * b + l4, pf + 512u);
-        dma(a.dst, 4u * b + l4, pf + 768u);
-        if (l4 < 128u) {
-            dma(a.sport, 2u * b + l4, pf + 1024u);
-            dma(a.dport, 2u * b + l4, pf + 1152u);
-        }
-        if (l4 < 64u) dma(a.proto, b + l4, pf + 1280u);
-#pragma unroll
-        for (uint32_t k = 0; k < kConnEarlyBlocks; ++k)
-            if (k < a.n_big) {
-                const uint32_t e = pf + kConnPfEarly + early_b * k;
-                if (a.pre_bytes == 1u) {
-                    const uint8_t* w = reinterpret_cast<const uint8_t*>(a.pre) + uint64_t(k) * stride;
-                    if (l4 < 64u) dma(w, b + l4, e);
-                } else if (l4 < 128u) {
-                    const uint8_t* w = reinterpret_cast<const uint8_t*>(a.pre) + uint64_t(4u * k) * stride;
-                    dma(w, 2u * b + l4, e);
-                    dma(w + 2u * stride, 2u * b + l4, e + 128u);
-                }
-            }
-    };
-    if constexpr (kPf)
-        if (staged(0)) pf_issue(0);                   // in flight during the staging below
     if constexpr (kLdsRules) lds_copy(smem, static_cast<const uint4*>(a.rules), a.rules_bytes / 16u);
     if constexpr (kCount == 1) {
         const uint32_t nw = a.ctr16 ? (a.n_ctr + 1u) / 2u : a.n_ctr;
@@ -711,35 +653,9 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kCount == 
         uint32_t si, dj, sp, dp, pr;
         A sa, da;
         // (u8 / u16 words, packed: one register per block)
-        // (kPf: the host takes that variant only with early words and staged
-        // tables, so no path of the loop loads from global memory -- a
-        // runtime branch to one would make the compiler drain the stage's DMA)
-        const bool early = kPf || a.n_big == 0u || (a.n_big <= kConnEarlyBlocks && a.pre_bytes <= 2u);
+        const bool early = a.n_big == 0u || (a.n_big <= kConnEarlyBlocks && a.pre_bytes <= 2u);
         uint32_t ew[kConnEarlyBlocks] = {};                    // [block]: SYN | SYN-ACK << (8 or 16)
-        bool st = false;
-        if constexpr (kPf) st = staged(it);
-        if (st) {
-            // this iteration's stage has landed (only the last verdict store
-            // may be younger); the next one goes into the other stage now
-            __builtin_amdgcn_s_waitcnt(0x0F71);                // vmcnt(1)
-            asm volatile("" ::: "memory");
-            if (it + 1u < n_iter && staged(it + 1u)) pf_issue(it + 1u);
-            const uint32_t pf = pf0 + (it & 1u) * a.pf_wave;
-            si = *lds32_t(pf + 4u * lane);
-            dj = *lds32_t(pf + 256u + 4u * lane);
-            sa = A(*lds32_t(pf + 512u + 4u * lane));
-            da = A(*lds32_t(pf + 768u + 4u * lane));
-            sp = *lds16_t(pf + 1024u + 2u * lane);
-            dp = *lds16_t(pf + 1152u + 2u * lane);
-            pr = *lds8_t(pf + 1280u + lane);
-#pragma unroll
-            for (uint32_t b = 0; b < kConnEarlyBlocks; ++b)
-                if (b < a.n_big) {
-                    const uint32_t e = pf + kConnPfEarly + early_b * b;
-                    ew[b] = a.pre_bytes == 1u ? uint32_t(*lds8_t(e + lane))
-                                              : uint32_t(*lds16_t(e + 2u * lane)) | uint32_t(*lds16_t(e + 128u + 2u * lane)) << 16;
-                }
-        } else {
+        {
             si = *at(a.src_if, ic);
             dj = *at(a.dst_if, ic);
             sa = *at(src, ic);
@@ -759,18 +675,10 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kCount == 
                         }
                     }
             }
-            if constexpr (kPf) {
-                // nothing of this path left pending past the join (or into
-                // the next iteration): a register it loads would otherwise be
-                // waited for with vmcnt(0) on the staged path too, draining
-                // the stage's DMA
-                __builtin_amdgcn_s_waitcnt(0x0F70);            // vmcnt(0)
-                asm volatile("" ::: "memory");
-            }
         }
         const bool ok = live && si < a.n_ifs && dj < a.n_ifs;   // unknown interface id: Failure
         // both lookups unconditional (an in-range index), the unknown case selected after
-        const IfAcls S0 = conn_if<kPf>(a, ok ? si : 0u), D0 = conn_if<kPf>(a, ok ? dj : 0u);
+        const IfAcls S0 = conn_if(a, ok ? si : 0u), D0 = conn_if(a, ok ? dj : 0u);
         const IfAcls S = ok ? S0 : IfAcls{-1, -1, -1, -1};
         const IfAcls Dif = ok ? D0 : IfAcls{-1, -1, -1, -1};
         const uint32_t p = pr <= 2u ? pr : 3u;
@@ -832,7 +740,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kCount == 
                 const uint32_t o = act ? (e.x & 63u) : lane, kk = (e.x >> 6) & 3u;
                 const uint32_t xs = __shfl(uint32_t(sa), int(o)), xd = __shfl(uint32_t(da), int(o));
                 if (act) {
-                    const ConnDesc D = conn_desc<kPf>(a, e.x >> 8);
+                    const ConnDesc D = conn_desc(a, e.x >> 8);
                     const uint32_t port = e.y & 0xFFFFu, xp = e.y >> 16;
                     const uint32_t s1 = kk < 2u ? xs : xd, d1 = kk < 2u ? xd : xs;
                     uint32_t res, rule;
@@ -864,7 +772,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kCount == 
                 const int32_t d0 = __shfl(di[0], int(o)), d1 = __shfl(di[1], int(o));
                 const int32_t d2 = __shfl(di[2], int(o)), d3 = __shfl(di[3], int(o));
                 if (act) {
-                    const ConnDesc D = conn_desc<kPf>(a, uint32_t(k == 0u ? d0 : k == 1u ? d1 : k == 2u ? d2 : d3));
+                    const ConnDesc D = conn_desc(a, uint32_t(k == 0u ? d0 : k == 1u ? d1 : k == 2u ? d2 : d3));
                     const bool syn = k < 2u;
                     uint32_t res, rule;
                     if constexpr (!k16) {
@@ -911,7 +819,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kCount == 
                 if (made[k] && di[k] >= 0) {                    // nil ACLs are not counted
                     if (job[k]) {
                         key[k] = rj[k] >> 2;
-                    } else if (kPf || a.pre_rules) {            // a large ACL: the word's counter index
+                    } else if (a.pre_rules) {            // a large ACL: the word's counter index
                         key[k] = w[k] >> 2;
                     } else {                                    // ... or its slot's rule
                         const ConnDesc D = conn_desc(a, uint32_t(di[k]));
@@ -1208,26 +1116,18 @@ hipError_t launch_connect(const ConnArgs& a, bool k16, bool lds_rules, int count
                           hipStream_t s) {
     if (a.n == 0) return hipSuccess;
     const bool jobs = a.job_lds != 0xFFFFFFFFu;
-    const bool pf = a.pf_lds != 0xFFFFFFFFu;
-    if (pf && (k16 || !lds_rules || count == 2)) return hipErrorInvalidValue;
-#define CONN_CASE(K16, L, C, J, P)                                                                         \
-    if (k16 == K16 && lds_rules == L && count == C && jobs == J && pf == P) {                              \
-        lds_attr<connect_kernel<K16, L, C, J, P>>();                                                       \
-        hipLaunchKernelGGL((connect_kernel<K16, L, C, J, P>), dim3(grid), dim3(block), lds, s, a);         \
+#define CONN_CASE(K16, L, C, J)                                                                            \
+    if (k16 == K16 && lds_rules == L && count == C && jobs == J) {                                         \
+        lds_attr<connect_kernel<K16, L, C, J>>();                                                          \
+        hipLaunchKernelGGL((connect_kernel<K16, L, C, J>), dim3(grid), dim3(block), lds, s, a);            \
         return hipGetLastError();                                                                          \
     }
-    CONN_CASE(false, false, 0, true, false) CONN_CASE(false, false, 1, true, false)
-    CONN_CASE(false, false, 2, true, false)
-    CONN_CASE(false, true, 0, true, false) CONN_CASE(false, true, 1, true, false) CONN_CASE(false, true, 2, true, false)
-    CONN_CASE(false, false, 0, false, false) CONN_CASE(false, false, 1, false, false)
-    CONN_CASE(false, false, 2, false, false)
-    CONN_CASE(false, true, 0, false, false) CONN_CASE(false, true, 1, false, false)
-    CONN_CASE(false, true, 2, false, false)
-    CONN_CASE(false, true, 0, true, true) CONN_CASE(false, true, 1, true, true)
-    CONN_CASE(false, true, 0, false, true) CONN_CASE(false, true, 1, false, true)
-    CONN_CASE(true, false, 0, false, false) CONN_CASE(true, false, 1, false, false)
-    CONN_CASE(true, false, 2, false, false)
-    CONN_CASE(true, true, 0, false, false) CONN_CASE(true, true, 1, false, false) CONN_CASE(true, true, 2, false, false)
+    CONN_CASE(false, false, 0, true) CONN_CASE(false, false, 1, true) CONN_CASE(false, false, 2, true)
+    CONN_CASE(false, true, 0, true) CONN_CASE(false, true, 1, true) CONN_CASE(false, true, 2, true)
+    CONN_CASE(false, false, 0, false) CONN_CASE(false, false, 1, false) CONN_CASE(false, false, 2, false)
+    CONN_CASE(false, true, 0, false) CONN_CASE(false, true, 1, false) CONN_CASE(false, true, 2, false)
+    CONN_CASE(true, false, 0, false) CONN_CASE(true, false, 1, false) CONN_CASE(true, false, 2, false)
+    CONN_CASE(true, true, 0, false) CONN_CASE(true, true, 1, false) CONN_CASE(true, true, 2, false)
 #undef CONN_CASE
     return hipErrorInvalidValue;
 }

@@ -287,18 +287,7 @@ struct ConnArgs {
                                  // SYN-ACK result << 2, batches that do not count)
     uint32_t bm_steps;           // bitmap forms: lower-bound steps of the largest interval table
     uint32_t job_lds;            // IPv4: LDS byte offset of the waves' job lists (512 B per wave)
-    uint32_t pf_lds;             // IPv4: LDS byte offset of the waves' field stages (two per wave, the
-                                 // next iteration's fields, DMA'd from HBM); ~0u: none
-    uint32_t pf_wave;            // bytes of one stage (conn_pf_wave)
 };
-// A wave's field stage (ConnArgs::pf_lds): the 64 connections of its next
-// iteration -- src_if, dst_if, src, dst (256 B each), sport, dport (128 B),
-// proto (64 B), then the large ACLs' early result words per block (u8
-// results: 64 B; u16 SYN and SYN-ACK words: 256 B)
-constexpr uint32_t kConnPfEarly = 1344;
-inline uint32_t conn_pf_wave(uint32_t n_big, uint32_t pre_bytes) {
-    return (kConnPfEarly + n_big * (pre_bytes == 1u ? 64u : 256u) + 63u) & ~63u;
-}
 // k16: 16-byte addresses; lds_rules: stage the pool; count: 0 none, 1 LDS
 // counters, 2 global (wave-aggregated) counters; grid: persistent workgroups
 // of `block` threads (512 or 1024); lds: dynamic LDS bytes (pool, LDS

@@ -43,8 +43,6 @@ struct Opts {
     int pair_lq = -1;           // pair launch: cap on the OTHER queue entries per wave in LDS
     int conn_no_lds = 0;        // bit 0 rules, bit 1 counters, bit 2 descriptors from global memory
     bool conn_jobs = true;      // the waves' LDS job lists (else owner search and shuffles)
-    int conn_prefetch = 1;      // IPv4: the next iteration's fields DMA'd into LDS stages (0 never,
-                                // 1 where they cost no workgroup per CU, 2 also where they do)
     int conn_plan = -1;         // counting LDS plan 0..3 = 32j 16j 32s 16s (-1: scored)
     bool conn_flush_atomic = false;  // LDS counters flushed by device atomics, not per-workgroup rows
     bool debug_conn = false;    // stderr: a connection launch's LDS plan
