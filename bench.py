@@ -64,6 +64,8 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="CPU baseline threads (default: every core this process may use)")
     ap.add_argument("--no-stream-floor", action="store_true", help="skip the live stream-floor measurement")
+    ap.add_argument("--opt", action="append", default=[],
+                    help="engine option key=value (cls_engine_set_option; A/B measurements)")
     ap.add_argument("--torch", action="store_true",
                     help="the torch harness instead of the product path: torch tensors and streams on the GPU, "
                          "counters merged by torch.distributed (the default, main_native, is the C ABI alone: "
@@ -76,6 +78,9 @@ def parse():
                     help="1 (the reported line): the classify kernels stamp their own start/end events "
                          "(hipExtLaunchKernel; the step period is start-to-start); diagnostics: 2 adds an "
                          "event record at each step boundary, 0 times nothing (wall time only)")
+    ap.add_argument("--event-every", type=int, default=4,
+                    help="native path: the timing events on every n-th step of the timed region (a timed "
+                         "launch costs the stream ~4 us: config 2 0.0437 against 0.0397 ms per step with none)")
     return ap.parse_args()
 
 
@@ -209,7 +214,7 @@ def main():
         n = -(-n_default // world)            # config 4: the fixed batch over the ranks
     else:
         n = n_default
-    eng = Engine(torch.cuda.current_device())
+    eng = Engine(torch.cuda.current_device(), options=dict(o.split("=", 1) for o in args.opt))
     table = eng.put_table("contiv/vpp-policy-GLOBAL", acl.rules)
     info = table.info()
     R = table.n_rules
@@ -370,7 +375,7 @@ def main():
             "dtype": "u32",
             "data": "synthetic (splitmix64 stream generated in HBM, seed %#x; rules rendered from a "
                     "synthetic 1000-pod policy set)" % spec["seed"],
-            "config": {"workload": wl,
+            "config": {"workload": wl, **({"options": args.opt} if args.opt else {}),
                        "rules": R, "packets_per_gpu": n,
                        "layout": "IPv4 SoA, 12 B/packet" if af == 4 else "16-byte address SoA, 36 B/packet",
                        "kernel": "classifier" if info["kernel"] == 1 else "linear",
@@ -455,7 +460,7 @@ def main_native(args, rank, world, local):
     strong = args.config == 4
     n = args.packets or (-(-n_default // world) if strong else n_default)
     af = spec.get("layout", 4)
-    eng = Engine(device)                       # one rank per GPU (RCCL: one rank per device)
+    eng = Engine(device, options=dict(o.split("=", 1) for o in args.opt))   # one rank per GPU (RCCL: one per device)
     if dist is not None and not shared:
         uid = [Engine.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
@@ -488,8 +493,9 @@ def main_native(args, rank, world, local):
     barrier()
     b.wait()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step(args.events >= 1)
+    every = max(1, args.event_every)
+    for j in range(args.steps):
+        step(args.events >= 1 and j % every == 0)
     t_submit = time.perf_counter() - t0
     b.wait()                                   # every kernel and the last all-reduce
     barrier()
@@ -509,7 +515,7 @@ def main_native(args, rank, world, local):
             np.save(os.path.join(args.dump, "counters.npy"), counters)
     avg_k = float(np.mean(kms)) if kms else float("nan")
     med_k = float(np.median(kms)) if kms else float("nan")
-    periods = list(np.diff(starts)) if len(starts) > 1 else []
+    periods = list(np.diff(starts) / every) if len(starts) > 1 else []      # timed steps `every` apart
     med_step = float(np.median(periods)) if periods else float("nan")
     # the stream floor over the batch's own device arrays
     shapes = []
@@ -570,7 +576,7 @@ def main_native(args, rank, world, local):
             "dtype": "u32",
             "data": "synthetic (splitmix64 stream generated in HBM, seed %#x; rules rendered from a "
                     "synthetic 1000-pod policy set)" % spec["seed"],
-            "config": {"workload": wl,
+            "config": {"workload": wl, **({"options": args.opt} if args.opt else {}),
                        "rules": R, "packets_per_gpu": n,
                        "layout": "IPv4 SoA, 12 B/packet" if af == 4 else "16-byte address SoA, 36 B/packet",
                        "kernel": "classifier" if info["kernel"] == 1 else "linear",
@@ -586,6 +592,7 @@ def main_native(args, rank, world, local):
             "counters_sum_ok": ok_sum,
             "settle_ms": round(settle_ms, 1),
             "step_ms_median": round(med_step, 4),
+            "timed_every": every,
             "host_submit_ms_per_step": round(t_submit * 1e3 / max(1, args.steps), 4),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),

@@ -171,3 +171,35 @@ def test_sharded_connection_batch_matches_oracle():
         assert np.array_equal(got, counts[name]), name
     b.close()
     multi.close()
+
+
+def _gpu_count():
+    import torch                            # counting devices does not initialise HIP on this image
+    return torch.cuda.device_count()
+
+
+@pytest.mark.skipif(_gpu_count() < 2, reason="needs two GPUs (distinct devices: an RCCL communicator)")
+def test_two_distinct_devices_all_reduce_counters():
+    """Two distinct devices: the engine builds an ncclCommInitAll
+    communicator (comm_info == (2, 0)), replicates the table, shards the
+    batch, and the RCCL all-reduce of the hit counters equals the oracle's,
+    as do the verdicts of both shards and a sharded connection batch."""
+    acl, spec, _ = workload.config(2)
+    n = (2 << 20) + 5
+    multi = Engine(devices=[0, 1])
+    assert multi.n_devices() == 2
+    assert multi.comm_info() == (2, 0), multi.comm_info()
+    t = multi.put_table("c2", acl.rules)
+    b = multi.batch(n)
+    b.gen_traffic(spec, 11)
+    c = multi.classify_batch(t, b)
+    tr = oracle.gen_traffic_v4(spec, 11, n)
+    ov, oc = _oracle(acl, tr)
+    assert np.array_equal(c, oc)
+    assert np.array_equal(b.download(_abi.BF_VERDICT), ov)
+    # async: counters of the last call, read later (the all-reduce on its side stream)
+    for _ in range(3):
+        assert multi.classify_batch(t, b, counters=False) is None
+    assert np.array_equal(b.counters(t.n_rules), oc)
+    b.close()
+    multi.close()

@@ -44,6 +44,14 @@ for step in "$@"; do
   bench)
     timeout -k 10 300 python bench.py --config $arg $B > $O/bench_c$arg.json 2> $O/bench_c$arg.err
     python3 tools/jl.py $O/bench_c$arg.json value ms_per_step step_ms_median roofline.kernel_ms_median roofline.stream_floor_ms roofline.frac ;;
+  benchk)
+    # benchk:<config>[:<tag>[:key=value...]]: the bench line under rocprofv3 kernel stats (no stream floor)
+    c=${arg%%:*}; rest=${arg#*:}; t=""; opts=""
+    if [ "$rest" != "$arg" ]; then t=_${rest%%:*}; [ "$rest" != "${rest%%:*}" ] && for o in $(echo ${rest#*:} | tr : ' '); do opts="$opts --opt $o"; done; fi
+    k=benchk_c$c$t
+    (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/$k -o run --output-format csv -- python3 $R/bench.py --config $c $B --no-stream-floor $opts > $O/$k.json 2> $O/$k.err)
+    echo "-- config $c$t:$opts"; python3 tools/jl.py $O/$k.json value ms_per_step step_ms_median roofline.kernel_ms_median
+    python3 tools/kstats.py $O/$k/run_kernel_stats.csv | grep -E "classify|finish|fold" ;;
   events)
     for ev in 2 1 0; do
       timeout -k 10 200 python bench.py --config $arg $B --events $ev > $O/ev_c${arg}_$ev.json 2> /dev/null

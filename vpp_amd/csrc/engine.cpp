@@ -556,7 +556,6 @@ static int scratch_of(cls_engine* e, Counters& c, uint32_t n_rules, hipStream_t 
         HIPC(e, q->out.ensure(size_t(n_rules + 1) * 8));
         // rows for the largest grid (cls_grid): never reallocated under pending work
         HIPC(e, q->part.ensure(size_t(e->n_cu) * (2048 / cls_block()) * std::max<uint32_t>(1, c.n_lctr) * 4));
-        HIPC(e, hipEventCreateWithFlags(&q->done, hipEventDisableTiming));
         p = std::move(q);
     }
     *out = p.get();
@@ -588,8 +587,8 @@ static CountOut count_out(Scratch* sc, uint64_t* counters_out, uint32_t flags) {
 
 // The finish launch of a classify chunk (kernels.hpp FinishArgs): fold the
 // workgroups' partials, and on the last chunk move every slot to its rule.
-static FinishArgs finish_args(const Counters& c, Scratch* sc, const Cls4Dev& cd, const CountOut& co,
-                              bool lds_resident, uint32_t rows, bool last) {
+static FinishArgs finish_args(const cls_engine* e, const Counters& c, Scratch* sc, const Cls4Dev& cd,
+                              const CountOut& co, bool lds_resident, uint32_t rows, bool last) {
     FinishArgs f;
     f.part = lds_resident ? sc->part.as<uint32_t>() : nullptr;
     f.rows = rows;
@@ -606,6 +605,11 @@ static FinishArgs finish_args(const Counters& c, Scratch* sc, const Cls4Dev& cd,
     f.other_map = c.d_other_map.as<uint32_t>();
     f.n_other = c.n_other;
     f.n_orules = c.n_orules;
+    // a tile's rows over several blocks where the tiles alone leave CUs idle
+    // (option fold_split=0: one block per tile)
+    const uint32_t tiles = (c.n_slots + 63u) / 64u;
+    if (last && f.part && tiles && e->opts.fold_split)
+        f.split = std::max(1u, std::min((rows + 63u) / 64u, uint32_t(e->n_cu) / tiles));
     return f;
 }
 
@@ -617,7 +621,6 @@ static int finish_counts(cls_engine* e, const Table& t, const Counters& c, Scrat
     const bool dev = flags & CLS_F_DEVICE;
     if (!remapped) {
         HIPC(e, launch_remap(sc->slot_val.as<unsigned long long>(), c.d_csr.as<uint2>(), c.n_slots, co.out, s));
-        HIPC(e, hipEventRecord(sc->done, s));        // (a finish launch stamps it itself)
     }
     if (!dev) {
         if (verdict_out && n) HIPC(e, hipMemcpyAsync(verdict_out, d_verdict, n, hipMemcpyDeviceToHost, s));
@@ -744,8 +747,8 @@ static int classify16_locked(cls_engine* e, std::shared_ptr<Table> t, const cls_
             HIPC(e, launch_classify16_cls(cd, fe, pc, vo, slot_val, q.lds_resident, lin, cfg));
             zeroed = true;
             cd.zero = nullptr;
-            HIPC(e, launch_finish16(finish_args(t->c16, sc, cd, co, q.lds_resident, uint32_t(cfg.grid), off + m >= n),
-                                    cd, cfg.other, fe, pc, vo, s, off + m >= n ? sc->done : nullptr));
+            HIPC(e, launch_finish16(finish_args(e, t->c16, sc, cd, co, q.lds_resident, uint32_t(cfg.grid), off + m >= n),
+                                    cd, cfg.other, fe, pc, vo, s));
             remapped = true;
         }
     }
@@ -845,9 +848,9 @@ int classify_locked(cls_engine* e, uint32_t table_id, const cls_pkt_soa* pk, uin
                 HIPC(e, launch_classify4_cls(cd, pc, vo, slot_val, t->lds_resident, vec, cfg));
                 zeroed = true;
                 cd.zero = nullptr;
-                FinishArgs fa = finish_args(t->c4, sc, cd, co, t->lds_resident, uint32_t(cfg.grid), off + m >= n);
+                FinishArgs fa = finish_args(e, t->c4, sc, cd, co, t->lds_resident, uint32_t(cfg.grid), off + m >= n);
                 fa.qmask = 1u;                      // the IPv4 launch's queue entries (run_n kMaskQ)
-                HIPC(e, launch_finish4(fa, cfg.other, pc, vo, s, off + m >= n ? sc->done : nullptr));
+                HIPC(e, launch_finish4(fa, cfg.other, pc, vo, s));
                 remapped = true;
             }
         } else {

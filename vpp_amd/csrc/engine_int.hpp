@@ -59,7 +59,10 @@ struct Scratch {
     DevBuf oq;                     // OTHER queue {fill per workgroup, segments of indices}
     DevBuf slot_val;               // u64 per slot: global-tier counters, folded partials
     DevBuf out;                    // u64 rule counters when the caller gives none on device
-    hipEvent_t done = nullptr;     // recorded after the call's last kernel
+    // (no completion event: the buffers are freed with hipFree, which
+    // synchronises the device first -- a done event stamped by every call's
+    // last launch cost the stream 2 us per call, config 2 0.0399 against
+    // 0.0379 ms per step, profiles/r06i_finish_event_ab.txt)
 };
 
 // Slot counters of one classifier image (or of the linear kernel alone):
@@ -74,13 +77,6 @@ struct Counters {
     DevBuf d_other_map;            // finish launch: compact rule index per OTHER slot, then those rules
     uint32_t n_other = 0, n_orules = 0;
     std::map<hipStream_t, std::unique_ptr<Scratch>> sc;
-    ~Counters() {
-        for (auto& kv : sc)
-            if (kv.second->done) {
-                (void)hipEventSynchronize(kv.second->done);   // device work may still read the buffers
-                (void)hipEventDestroy(kv.second->done);
-            }
-    }
 };
 
 // An event shared by the tables of one counting connection batch.

@@ -122,6 +122,11 @@ constexpr uint32_t kOtherLds = 4096;   // finish launch: LDS histogram of the OT
 // packets are counted straight into their rules, the tiles read only what
 // the classify launch wrote.
 constexpr uint32_t kFoldWaves = 16;
+// A tile's rows may be split over f.split blocks (the host's fold_split),
+// their sums added to the rules with device atomics: a few tiles each
+// walking every row of a many-workgroup launch wait one memory latency per
+// 64 rows.
+__device__ __forceinline__ uint32_t fold_split(const FinishArgs& f) { return f.remap && f.part ? max(f.split, 1u) : 1u; }
 template <typename Load>
 __device__ __forceinline__ void finish_body(const FinishArgs& f, const Cls4Dev& o, uint8_t* verdict,
                                             const Load& load) {
@@ -129,16 +134,19 @@ __device__ __forceinline__ void finish_body(const FinishArgs& f, const Cls4Dev& 
     __shared__ unsigned long long hot[kMaxHotRules];
     __shared__ uint32_t h[kOtherLds];
     const uint32_t span = f.remap ? f.n_slots : (f.part ? f.n_lctr : 0u);
-    const uint32_t ntile = (span + 63u) / 64u;
+    const uint32_t split = fold_split(f);
+    const uint32_t ntile = (span + 63u) / 64u * split;
     if (blockIdx.x < ntile) {
         const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-        const uint32_t i = blockIdx.x * 64u + lane;
+        const uint32_t piece = blockIdx.x % split;                 // this block's rows of the tile
+        const uint32_t i = blockIdx.x / split * 64u + lane;
         if (threadIdx.x < f.n_hot) hot[threadIdx.x] = 0ull;
         unsigned long long s64 = 0;
         if (f.part && i < f.n_lctr) {
-            const uint32_t n = f.n_lctr, rows = f.rows;
+            const uint32_t n = f.n_lctr, per = (f.rows + split - 1u) / split;
+            const uint32_t rows = min(f.rows, (piece + 1u) * per);
             const uint32_t* part = f.part;
-            uint32_t w = wave;
+            uint32_t w = piece * per + wave;
             for (; w + 3u * kFoldWaves < rows; w += 4u * kFoldWaves) {
                 const uint32_t a = part[size_t(w) * n + i], b = part[size_t(w + kFoldWaves) * n + i];
                 const uint32_t c = part[size_t(w + 2u * kFoldWaves) * n + i];
@@ -153,9 +161,11 @@ __device__ __forceinline__ void finish_body(const FinishArgs& f, const Cls4Dev& 
 #pragma unroll
             for (uint32_t k = 1; k < kFoldWaves; ++k) s64 += acc[k][lane];
             if (f.remap) {
-                const unsigned long long sv = f.slot_val[i];
-                if (sv) f.slot_val[i] = 0ull;
-                s64 += sv;
+                if (piece == 0u) {                   // the slot's global counter: one block
+                    const unsigned long long sv = f.slot_val[i];
+                    if (sv) f.slot_val[i] = 0ull;
+                    s64 += sv;
+                }
                 if (s64) {
                     const uint32_t e = f.slot_rule[i];
                     if (e & kHotRule) atomicAdd(&hot[e & ~kHotRule], s64);
@@ -1066,25 +1076,21 @@ hipError_t launch_remap(unsigned long long* slot_val, const uint2* csr, uint32_t
 
 static uint32_t finish_grid(const FinishArgs& f) {
     const uint32_t span = f.remap ? f.n_slots : (f.part ? f.n_lctr : 0u);
-    return (span + 63u) / 64u + (f.oq ? f.oq_rows : 0u);
+    return (span + 63u) / 64u * (f.remap && f.part ? std::max(f.split, 1u) : 1u) + (f.oq ? f.oq_rows : 0u);
 }
 
-hipError_t launch_finish4(const FinishArgs& f, const Cls4Dev& o, const Pkts4& p, uint8_t* verdict, hipStream_t s,
-                          hipEvent_t done) {
+hipError_t launch_finish4(const FinishArgs& f, const Cls4Dev& o, const Pkts4& p, uint8_t* verdict, hipStream_t s) {
     const uint32_t g = finish_grid(f);
-    if (g == 0) return done ? hipEventRecord(done, s) : hipSuccess;
-    if (done) hipExtLaunchKernelGGL(finish4_kernel, dim3(g), dim3(1024), 0u, s, nullptr, done, 0u, f, o, p, verdict);
-    else hipLaunchKernelGGL(finish4_kernel, dim3(g), dim3(1024), 0, s, f, o, p, verdict);
+    if (g == 0) return hipSuccess;
+    hipLaunchKernelGGL(finish4_kernel, dim3(g), dim3(1024), 0, s, f, o, p, verdict);
     return hipGetLastError();
 }
 
 hipError_t launch_finish16(const FinishArgs& f, const Cls4Dev& t, const Cls4Dev& o, const Fe16& fe, const Pkts16& p,
-                           uint8_t* verdict, hipStream_t s, hipEvent_t done) {
+                           uint8_t* verdict, hipStream_t s) {
     const uint32_t g = finish_grid(f);
-    if (g == 0) return done ? hipEventRecord(done, s) : hipSuccess;
-    if (done)
-        hipExtLaunchKernelGGL(finish16_kernel, dim3(g), dim3(1024), 0u, s, nullptr, done, 0u, f, t, o, fe, p, verdict);
-    else hipLaunchKernelGGL(finish16_kernel, dim3(g), dim3(1024), 0, s, f, t, o, fe, p, verdict);
+    if (g == 0) return hipSuccess;
+    hipLaunchKernelGGL(finish16_kernel, dim3(g), dim3(1024), 0, s, f, t, o, fe, p, verdict);
     return hipGetLastError();
 }
 

@@ -152,13 +152,13 @@ struct FinishArgs {
                                  // mask's bits (IPv4 launches: one entry per lane and wave step)
     const uint32_t* other_map;
     uint32_t n_other, n_orules;
+    uint32_t split = 1;          // blocks per tile of 64 slots, each folding a share of the rows
+                                 // (remap with partials only; the host's fold_split)
 };
 // finish4 / finish16: the OTHER packets' loads from the 4- / 16-byte batch
-// done (may be null): an event stamped when the launch completes
-hipError_t launch_finish4(const FinishArgs& f, const Cls4Dev& o, const Pkts4& p, uint8_t* verdict, hipStream_t s,
-                          hipEvent_t done = nullptr);
+hipError_t launch_finish4(const FinishArgs& f, const Cls4Dev& o, const Pkts4& p, uint8_t* verdict, hipStream_t s);
 hipError_t launch_finish16(const FinishArgs& f, const Cls4Dev& t, const Cls4Dev& o, const Fe16& fe, const Pkts16& p,
-                           uint8_t* verdict, hipStream_t s, hipEvent_t done = nullptr);
+                           uint8_t* verdict, hipStream_t s);
 // the classify kernels' packet stream without the lookups (stream floor);
 // exactly one of p4 / p16; p4 needs 16-B aligned src/dst, 8-B dport, 4-B
 // proto and verdict (variant bit 0: load and use instead of the next step's

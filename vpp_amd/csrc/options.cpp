@@ -62,6 +62,7 @@ bool opts_set(Opts& o, const char* key, const char* value, std::string& why) {
     OPT("other_cap", other_cap, uint32_t(x))
     OPT("wg_per_cu", wg_per_cu, i)
     OPT("debug_floor", debug_floor, b)
+    OPT("fold_split", fold_split, b)
     OPT("conn_bitmap", conn_bitmap, b)
     OPT("conn_pair", conn_pair, b)
     OPT("conn_pre_rules", conn_pre_rules, b)

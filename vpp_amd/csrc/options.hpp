@@ -32,6 +32,7 @@ struct Opts {
     uint32_t other_cap = 0;     // OTHER queue entries per workgroup (0: sized by the batch)
     int wg_per_cu = 0;          // classify workgroups per CU (0: by LDS)
     bool debug_floor = false;   // stderr: every stream shape's time
+    bool fold_split = true;     // finish launch: a slot tile's rows over several blocks when tiles are few
     // ---- connection batches (engine.cpp) ----------------------------------
     bool conn_bitmap = true;    // bitmap form of linear IPv4 ACLs
     bool conn_pair = true;      // both tuples of a large ACL in one launch (classify4_pair)
