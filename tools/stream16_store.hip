@@ -18,6 +18,9 @@
 //        fourth step (after that step's loads): a quarter of the store events
 //   P    the next step's loads issued before this step's stores and held in
 //        registers (one step ahead)
+//   W2 / W4 / W16  A with the stores of one wave step in 2 / 4 / 16 only (full
+//        lines, a half / quarter / sixteenth of the bytes): does the cost
+//        scale with the bytes written?
 // build: hipcc -O3 --offload-arch=gfx950 -o tools/stream16_store.bin tools/stream16_store.hip
 #include <hip/hip_runtime.h>
 
@@ -81,7 +84,8 @@ __global__ __launch_bounds__(1024) void k16(const uint4* S, const uint4* D, cons
     const uint32_t nsteps = n / 256u * 64u;
     const uint32_t g0 = blockIdx.x * blockDim.x + threadIdx.x;
     auto base_of = [&](uint32_t g) { return 4u * (g & ~63u); };
-    if constexpr (M == 0 || M == 1) {
+    if constexpr (M == 0 || M == 1 || M >= 6) {
+        constexpr uint32_t Q = M == 6 ? 2u : M == 7 ? 4u : 16u;
         for (uint32_t g = g0; g < nsteps; g += nthreads) {
             Step b;
             load(b, S, D, DP, PR, base_of(g), lane);
@@ -89,7 +93,10 @@ __global__ __launch_bounds__(1024) void k16(const uint4* S, const uint4* D, cons
 #pragma unroll
             for (int k = 0; k < 4; ++k) v[k] = mix(b.s[k], b.d[k], b.dp[k], b.pr[k]);
             if constexpr (M == 0) store4(V, base_of(g), lane, v);
-            else if ((v[0] ^ v[1] ^ v[2] ^ v[3]) == magic) V[base_of(g) + lane] = 1;   // never (magic > 3)
+            else if constexpr (M >= 6) {
+                if ((g / nthreads) % Q == 0u) store4(V, base_of(g), lane, v);    // wave-uniform
+                else if ((v[0] ^ v[1] ^ v[2] ^ v[3]) == magic) V[base_of(g) + lane] = 1;   // keeps the loads
+            } else if ((v[0] ^ v[1] ^ v[2] ^ v[3]) == magic) V[base_of(g) + lane] = 1;   // never (magic > 3)
         }
     } else if constexpr (M == 2 || M == 3) {
         uint32_t pv[4] = {0u, 0u, 0u, 0u}, pg = 0;
@@ -232,6 +239,9 @@ int main() {
         CK(hipMemset(v, 0, N));
         timed("P", [&] { k16<5><<<ncu, 1024, 16384>>>(src, dst, dp, pr, v, n, 7); });
         if (round == 0 && check("P")) return 1;
+        timed("W2", [&] { k16<6><<<ncu, 1024, 16384>>>(src, dst, dp, pr, v, n, 7); });
+        timed("W4", [&] { k16<7><<<ncu, 1024, 16384>>>(src, dst, dp, pr, v, n, 7); });
+        timed("W16", [&] { k16<8><<<ncu, 1024, 16384>>>(src, dst, dp, pr, v, n, 7); });
     }
     return 0;
 }
