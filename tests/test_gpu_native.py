@@ -203,3 +203,31 @@ def test_two_distinct_devices_all_reduce_counters():
     assert np.array_equal(b.counters(t.n_rules), oc)
     b.close()
     multi.close()
+
+
+@pytest.mark.skipif(_gpu_count() < 2, reason="needs two GPUs (distinct devices: peer table uploads)")
+def test_two_distinct_devices_connection_batch_counted():
+    """A counted connection batch sharded over two distinct devices: the
+    tables uploaded to the second GPU, both shards' verdicts and the
+    per-(ACL, rule) counters summed over the devices equal the oracle's."""
+    from test_gpu_connect_scale import build, oracle_connections, traffic
+    multi = Engine(devices=[0, 1])
+    ifs, bind, by_name, pool, spec = build(multi, seed=5, n_local=16, n_if=32)
+    n = 30011
+    rng = np.random.default_rng(13)
+    tr = traffic(5, n, pool, spec, 4)
+    si = rng.integers(0, len(ifs), n).astype(np.uint32)
+    di = np.where(rng.random(n) < 0.1, si, rng.integers(0, len(ifs), n)).astype(np.uint32)
+    ids = np.array([multi.if_id(x) for x in ifs], np.uint32)
+    b = multi.batch(n, conn=True)
+    for f, v in ((_abi.BF_SRC, tr["src"]), (_abi.BF_DST, tr["dst"]), (_abi.BF_SPORT, tr["sport"]),
+                 (_abi.BF_DPORT, tr["dport"]), (_abi.BF_PROTO, tr["proto"]), (_abi.BF_SRC_IF, ids[si]),
+                 (_abi.BF_DST_IF, ids[di])):
+        b.upload(f, v)
+    want, counts = oracle_connections(bind, by_name, ifs, si, di, tr, 4)
+    multi.connect_batch_b(b, count=True)
+    assert np.array_equal(b.download(_abi.BF_VERDICT), want)
+    for name in by_name:
+        assert np.array_equal(multi.conn_counters(name), counts[name]), name
+    b.close()
+    multi.close()

@@ -1660,7 +1660,8 @@ int connect_locked(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t* ou
     };
     auto plan_of = [&](size_t ctr_b, bool jobs) {
         jobs = jobs && !k16 && e->opts.conn_jobs;
-        const int cu_cap = cmode == 1 && (jobs || k16) ? 2 : 3;
+        const int cu_cap = std::min(cmode == 1 && (jobs || k16) ? 2 : 3,
+                                    e->opts.conn_wg_per_cu > 0 ? e->opts.conn_wg_per_cu : 3);
         auto per_cu_of = [&](size_t b) { return b ? std::max(1, std::min(cu_cap, int(lds_max / b))) : cu_cap; };
         LdsPlan q{lds_used + ctr_b, 0xFFFFFFFFu, 0xFFFFFFFFu, 0, 0};
         const size_t meta_at = (q.lds + 15) & ~size_t(15);

@@ -43,6 +43,7 @@ struct Opts {
     bool pair_other_global = false;  // pair launch: the OTHER image read from global memory
     int pair_lq = -1;           // pair launch: cap on the OTHER queue entries per wave in LDS
     int conn_no_lds = 0;        // bit 0 rules, bit 1 counters, bit 2 descriptors from global memory
+    int conn_wg_per_cu = 0;     // measurements: cap on the connection kernel's workgroups per CU (0: none)
     bool conn_jobs = true;      // the waves' LDS job lists (else owner search and shuffles)
     int conn_plan = -1;         // counting LDS plan 0..3 = 32j 16j 32s 16s (-1: scored)
     bool conn_flush_atomic = false;  // LDS counters flushed by device atomics, not per-workgroup rows
