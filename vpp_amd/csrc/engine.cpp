@@ -1650,9 +1650,9 @@ int connect_locked(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t* ou
     // interface tables after the pool and counters unless they would cost a
     // workgroup per CU, then (IPv4, `jobs`) the waves' job lists (512 B per
     // wave) on the same terms -- else the kernel's owner search and shuffles
-    // (option conn_jobs=0: tests).  Counting with LDS counters and job
-    // lists or 16-byte addresses, the kernel holds up to 96 VGPRs (kernels.hip
-    // connect_kernel): at most two workgroups per CU.
+    // (option conn_jobs=0: tests).  Counting with LDS counters and 16-byte
+    // addresses, the kernel holds up to 96 VGPRs (kernels.hip connect_kernel):
+    // at most two workgroups per CU.
     struct LdsPlan {
         size_t lds;
         uint32_t meta_lds, job_lds;
@@ -1660,8 +1660,7 @@ int connect_locked(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t* ou
     };
     auto plan_of = [&](size_t ctr_b, bool jobs) {
         jobs = jobs && !k16 && e->opts.conn_jobs;
-        const int cu_cap = std::min(cmode == 1 && (jobs || k16) ? 2 : 3,
-                                    e->opts.conn_wg_per_cu > 0 ? e->opts.conn_wg_per_cu : 3);
+        const int cu_cap = std::min(cmode == 1 && k16 ? 2 : 3, e->opts.conn_wg_per_cu > 0 ? e->opts.conn_wg_per_cu : 3);
         auto per_cu_of = [&](size_t b) { return b ? std::max(1, std::min(cu_cap, int(lds_max / b))) : cu_cap; };
         LdsPlan q{lds_used + ctr_b, 0xFFFFFFFFu, 0xFFFFFFFFu, 0, 0};
         const size_t meta_at = (q.lds + 15) & ~size_t(15);

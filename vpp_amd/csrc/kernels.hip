@@ -573,11 +573,13 @@ __device__ __forceinline__ uint32_t conn_bm(const ConnArgs& a, const ConnDesc& D
 // SIMD), so 24 waves fit a CU -- three 512-thread workgroups where the LDS
 // allows two or more, else one 1024-thread workgroup (16 waves rather than
 // the 8 of one 512-thread one); forcing 64 VGPRs spills to scratch.  The
-// LDS-counter variants with job lists or 16-byte addresses (kCount 1, kJobs
-// or k16) take up to 128 VGPRs (89: no spill, where 80 spilled 20 B) and at
-// most two 512-thread workgroups per CU (the host's plan; 640-thread ones,
-// 5 waves per SIMD, measured 125 against 88 us: the second workgroup finds
-// no SIMD with room for its third wave -- profiles/r06e_conn_tree_search_ab.txt).
+// 16-byte LDS-counter variants (kCount 1, k16) take up to 128 VGPRs (at 80
+// they spill) and at most two 512-thread workgroups per CU (the host's plan);
+// the IPv4 ones fit 80 since the job ranks came from mbcnt (round 6: 89 with
+// a lane mask held in registers), so they get the third workgroup wherever
+// the LDS allows it.  (640-thread workgroups, 5 waves per SIMD, measured 125
+// against 88 us: the second workgroup finds no SIMD with room for its third
+// wave -- profiles/r06e_conn_tree_search_ab.txt.)
 // kJobs (IPv4): the waves' job lists in LDS (a.job_lds); else the owner
 // search and shuffles (16-byte batches, and IPv4 launches whose LDS is
 // full: the job lists would displace LDS counters or bitmap forms)
@@ -614,7 +616,7 @@ __device__ __forceinline__ uint32_t conn_state(const uint32_t res[4], bool same,
 }
 
 template <bool k16, bool kLdsRules, int kCount, bool kJobs>
-__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kCount == 1 && (kJobs || k16) ? 4 : 6))) void connect_kernel(
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kCount == 1 && k16 ? 4 : 6))) void connect_kernel(
     ConnArgs a) {
     typedef typename ConnT<k16>::A A;
     extern __shared__ uint4 smem[];
