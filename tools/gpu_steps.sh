@@ -125,7 +125,7 @@ for v in vals:
 PY
     ;;
   sqconn)
-    SQ_KERNELS=connect_kernel,classify4_pair SQ_CMD="python3 $R/tools/conn_bench.py --locals $arg --count 1 --iters 2 --cpu-sample 0" bash tools/sq_profile.sh ${TAG}_conn$arg > /dev/null 2>&1
+    SQ_KERNELS=connect_kernel,classify4_pair SQ_CMD="python3 $R/tools/conn_bench.py --locals $arg --count 1 --iters 2 --cpu-sample 0 --cpu-fast-sample 0" bash tools/sq_profile.sh ${TAG}_conn$arg > /dev/null 2>&1
     cat gpurun_out/sq_${TAG}_conn$arg/summary.txt ;;
   pmc)
     bash tools/gpu_pmc.sh ${TAG}_pmc$arg $arg > /dev/null 2>&1
