@@ -627,6 +627,35 @@ func (en *Engine) ClassifyBatch(t *Table, src, dst []uint32, dport []uint16,
 	return verdict, counters, nil
 }
 
+// ClassifyBatchRules: each packet's ACLAction and the index of the rule at
+// which evalACL terminated (t.NRules: the default DENY) -- the matched rule
+// evalACL logs at Debug (aclengine_mock.go:651-654), for a whole batch; no
+// counters.
+func (en *Engine) ClassifyBatchRules(t *Table, src, dst []uint32, dport []uint16,
+	proto []aclengine.ProtocolType) ([]uint8, []uint32, error) {
+	n := len(src)
+	if len(dst) != n || len(dport) != n || len(proto) != n {
+		return nil, nil, errors.New("contivcls: packet arrays of different lengths")
+	}
+	verdict := make([]uint8, n)
+	rules := make([]uint32, n)
+	if n == 0 {
+		return verdict, rules, nil
+	}
+	pr := make([]uint8, n)
+	for i, p := range proto {
+		pr[i] = uint8(p)
+	}
+	en.Lock()
+	defer en.Unlock()
+	if rc := C.clsg_classify_rules_v4(en.e, C.uint32_t(t.ID), (*C.uint32_t)(&src[0]), (*C.uint32_t)(&dst[0]),
+		(*C.uint16_t)(&dport[0]), (*C.uint8_t)(&pr[0]), C.uint64_t(n), (*C.uint8_t)(&verdict[0]),
+		(*C.uint32_t)(&rules[0])); rc != C.CLS_OK {
+		return nil, nil, en.lastErr()
+	}
+	return verdict, rules, nil
+}
+
 // ClassifyBatchIP: the same for addresses of any family (net.IP; IPv4 and
 // IPv4-mapped packets match IPv4 networks only, as Go's IPNet.Contains).
 func (en *Engine) ClassifyBatchIP(t *Table, src, dst []net.IP, dport []uint16,

@@ -14,7 +14,8 @@
  *   DIR/pkt.bin    u64 n, then src4[n] dst4[n] (u32) dport[n] (u16) proto[n] (u8)
  *   DIR/conn.bin   u64 m, then si[m] di[m] (u32 indices into ifs.txt) src4[m]
  *                  dst4[m] (u32) sport[m] dport[m] (u16) proto[m] (u8)
- * writes DIR/out_*.bin: verdicts and counters of clsg_classify_v4, of
+ * writes DIR/out_*.bin: verdicts and counters of clsg_classify_v4 (and the
+ * verdicts and terminating rules of clsg_classify_rules_v4), of
  * clsg_classify_v16 (the same packets IPv4-mapped), of an engine-owned batch
  * filled through its pinned mirror (clsg_batch_mirror, cls_batch_upload,
  * cls_classify_batch, cls_batch_download), the ConnectionActions of
@@ -159,6 +160,13 @@ int main(int argc, char** argv) {
     if (rc != CLS_OK) die("clsg_classify_v4", e, rc);
     write_out("out_verdict.bin", verdict, n);
     write_out("out_counters.bin", ctr, (R + 1) * 8);
+    /* each packet's terminating rule (clsg_classify_rules_v4) */
+    uint32_t* rules = malloc(n ? 4 * n : 4);
+    rc = clsg_classify_rules_v4(e, tid, src, dst, dport, proto, n, verdict, rules);
+    if (rc != CLS_OK) die("clsg_classify_rules_v4", e, rc);
+    write_out("out_rverdict.bin", verdict, n);
+    write_out("out_rules.bin", rules, 4 * n);
+    free(rules);
 
     /* the same packets as IPv4-mapped 16-byte addresses (Go's To16) */
     uint8_t* s16 = calloc(n ? n : 1, 16);

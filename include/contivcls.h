@@ -42,7 +42,9 @@ extern "C" {
 /* 5: cls_engine_set_option (tuning / diagnostic switches; the library no
  *    longer reads the process environment); cls_compile_v4 / v16 take an
  *    option string; entry points restore the caller's current device; over
- *    distinct devices an engine without RCCL keeps host-summed counters. */
+ *    distinct devices an engine without RCCL keeps host-summed counters;
+ *    cls_classify_rules (the per-packet matched-rule trace); CLS_F_DEVICE
+ *    connection batches are stream-ordered. */
 #define CLS_ABI_VERSION 5
 
 /* ---- status codes ------------------------------------------------------ */
@@ -237,6 +239,18 @@ int cls_table_get_info(cls_engine* e, uint32_t table_id, cls_table_info* info);
 int cls_classify(cls_engine* e, uint32_t table_id, const cls_pkt_soa* pkts,
                  uint64_t n, uint8_t* verdict_out, uint64_t* counters_out,
                  uint32_t flags, void* stream);
+
+/* The per-packet trace of evalACL's matched rule (the reference logs it at
+ * Debug, aclengine_mock.go:651-654): verdict_out[i] as cls_classify (may be
+ * NULL) and rule_out[i] = the index k of the rule at which packet i's
+ * evaluation terminated, R for the default DENY (:667) -- the counter
+ * cls_classify adds the packet to.  No counters are touched.  Flags:
+ * CLS_F_DEVICE (device arrays, rule_out 4-byte aligned; stream-ordered),
+ * else host arrays and the call returns with the results.  Replaces, for a
+ * batch, the rule index evalACL computes and logs per call. */
+int cls_classify_rules(cls_engine* e, uint32_t table_id, const cls_pkt_soa* pkts,
+                       uint64_t n, uint8_t* verdict_out, uint32_t* rule_out,
+                       uint32_t flags, void* stream);
 
 /* Milliseconds of the last classify kernel (CLS_F_TIMING), measured with HIP
  * events on the launch stream.  Blocks until that kernel has finished. */

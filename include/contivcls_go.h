@@ -53,6 +53,20 @@ static inline int clsg_classify_v4(cls_engine* e, uint32_t table_id, const uint3
 
 /* cls_classify of a 16-byte batch (n x 16 network-order bytes per address;
  * IPv4 as IPv4-mapped, Go's net.IP.To16). */
+/* cls_classify_rules over an IPv4 batch: each packet's ACLAction and terminating rule. */
+static inline int clsg_classify_rules_v4(cls_engine* e, uint32_t table_id, const uint32_t* src4, const uint32_t* dst4,
+                                         const uint16_t* dport, const uint8_t* proto, uint64_t n, uint8_t* verdict,
+                                         uint32_t* rules) {
+    cls_pkt_soa p;
+    memset(&p, 0, sizeof p);
+    p.af = CLS_AF_V4;
+    p.src4 = src4;
+    p.dst4 = dst4;
+    p.dport = dport;
+    p.proto = proto;
+    return cls_classify_rules(e, table_id, &p, n, verdict, rules, 0, NULL);
+}
+
 static inline int clsg_classify_v16(cls_engine* e, uint32_t table_id, const uint8_t* src16, const uint8_t* dst16,
                                     const uint16_t* dport, const uint8_t* proto, uint64_t n, uint8_t* verdict,
                                     uint64_t* counters, uint32_t flags) {

@@ -84,6 +84,9 @@ def lib():
         L.orc_compile.restype = C.c_void_p
         L.orc_compile.argtypes = [C.POINTER(ClsRule), C.c_uint32]
         L.orc_ctable_free.argtypes = [C.c_void_p]
+        L.orc_classify_fast_hits.restype = C.c_int
+        L.orc_classify_fast_hits.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
+                                             C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_int]
         L.orc_classify_fast.restype = C.c_int
         L.orc_classify_fast.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
                                         C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_int]
@@ -238,6 +241,20 @@ class FastTable:
         if rc != 0:
             raise RuntimeError("orc_classify_fast rc=%d" % rc)
         return verdict, counters
+
+
+def classify_hits(crules, src, dst, dport, proto, af=4, nthreads=0):
+    """Each packet's ACLAction and terminating rule index (n: the default
+    DENY) on the fast port (orc_classify_fast_hits): (verdict, hits uint32)."""
+    t = FastTable(crules)
+    n = len(dport)
+    verdict = np.zeros(n, np.uint8)
+    hits = np.zeros(n, np.uint32)
+    rc = lib().orc_classify_fast_hits(t.h, af, _p(src), _p(dst), _p(np.ascontiguousarray(dport, np.uint16)),
+                                      _p(np.ascontiguousarray(proto, np.uint8)), n, _p(verdict), _p(hits), nthreads)
+    if rc != 0:
+        raise RuntimeError("orc_classify_fast_hits rc=%d" % rc)
+    return verdict, hits
 
 
 def connect_fast(tables, if_in, if_out, si, di, tr, af=4, nthreads=0):

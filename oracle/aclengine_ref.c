@@ -594,6 +594,29 @@ int orc_classify_fast(const orc_ctable* t, int af, const void* src, const void* 
     return 0;
 }
 
+/* Each packet's ACLAction and terminating rule index (n: the default DENY),
+ * as orc_eval_acl's *hit: the checker of cls_classify_rules. */
+int orc_classify_fast_hits(const orc_ctable* t, int af, const void* src, const void* dst,
+                           const uint16_t* dport, const uint8_t* proto, uint64_t n,
+                           uint8_t* verdict, uint32_t* hits, int nthreads) {
+#ifdef _OPENMP
+    if (nthreads <= 0) nthreads = omp_get_max_threads();
+#pragma omp parallel for schedule(static) num_threads(nthreads)
+#else
+    (void)nthreads;
+#endif
+    for (int64_t i = 0; i < (int64_t)n; i++) {
+        go_ip s, d;
+        load_ip(af, src, (uint64_t)i, s.b, &s.len);
+        load_ip(af, dst, (uint64_t)i, d.b, &d.len);
+        int32_t hit;
+        int a = fast_eval(t, &s, &d, proto[i], dport[i], &hit);
+        if (verdict) verdict[i] = (uint8_t)a;
+        hits[i] = (uint32_t)hit;
+    }
+    return 0;
+}
+
 /* ---------------------------------------------------------------------------
  * Fast CPU port of a batch of testConnection calls (the connection line's
  * CPU baseline): the ACLs pre-parsed (orc_compile), testConnection's order

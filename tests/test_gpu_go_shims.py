@@ -96,6 +96,9 @@ def test_go_shims_on_gpu(tmp_path):
         assert bad.size == 0, (v, bad[:8])
         np.testing.assert_array_equal(out(c, np.uint64), oc.astype(np.uint64), err_msg=c)
     assert oc.sum() == n
+    hv, hits = oracle.classify_hits(oracle.rules_to_c(acl.rules), tr["src"], tr["dst"], tr["dport"], tr["proto"])
+    assert np.array_equal(out("out_rverdict.bin", np.uint8), hv)
+    assert np.array_equal(out("out_rules.bin", np.uint32), hits)
     want, wcounts = oracle_connections(bind, by_name, ifs, si, di, ctr, 4)
     got = out("out_conn.bin", np.uint8)
     bad = np.nonzero(got != want)[0]

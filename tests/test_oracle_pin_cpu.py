@@ -82,3 +82,21 @@ def test_fast_connections_match_faithful(seed):
     want, _ = oracle_connections(bind, by_name, ifs, si, di, tr, 4)
     np.testing.assert_array_equal(got, want)
     assert len(set(want.tolist())) >= 3
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_fast_hits_match_literal_eval_acl(seed):
+    """orc_classify_fast_hits (the checker of cls_classify_rules) against
+    evalACL restated literally (orc_eval_acl, its *hit: the terminating rule,
+    n for the default DENY) packet by packet, on random IPv4 ACLs with
+    malformed rules and protocols > 2; their histogram is the counters."""
+    rules, pool = random_acl(seed * 11 + 3, [30, 150, 300][seed], 0.25)
+    tr = random_traffic(seed + 40, 600, pool, other_proto=True)
+    cr = oracle.rules_to_c(rules)
+    v, hits = oracle.classify_hits(cr, tr["src"], tr["dst"], tr["dport"], tr["proto"])
+    for i in range(len(v)):
+        a, h = oracle.eval_acl(cr, False, int(tr["src"][i]).to_bytes(4, "big"), int(tr["dst"][i]).to_bytes(4, "big"),
+                               int(tr["proto"][i]), int(tr["dport"][i]))
+        assert (int(v[i]), int(hits[i])) == (a, h), i
+    _, c = oracle.classify_faithful(cr, tr["src"], tr["dst"], tr["dport"], tr["proto"])
+    np.testing.assert_array_equal(np.bincount(hits, minlength=cr.n + 1), c)

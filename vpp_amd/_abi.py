@@ -46,7 +46,7 @@ R_ICMP, R_ICMP_CODE, R_ICMP_TYPE, R_ICMPV6, R_ACTIONS = 2048, 4096, 8192, 16384,
 
 # the exported symbols (checked by tests/test_abi.py against include/contivcls.h)
 SYMBOLS = ["cls_abi_version", "cls_engine_create", "cls_engine_destroy", "cls_last_error", "cls_engine_set_option",
-           "cls_table_put", "cls_table_del", "cls_table_get_info", "cls_classify",
+           "cls_table_put", "cls_table_del", "cls_table_get_info", "cls_classify", "cls_classify_rules",
            "cls_last_kernel_ms", "cls_kernel_times", "cls_kernel_starts", "cls_kernel_times_reset", "cls_acl_put", "cls_acl_del", "cls_acl_table", "cls_acl_counts",
            "cls_if_id",
            "cls_if_acls", "cls_connect_batch", "cls_gen_traffic_v4", "cls_compile_v4", "cls_image_kernel",
@@ -182,6 +182,7 @@ def bind(path: str, strict: bool = True):
         "cls_table_del": (C.c_int, [vp, u32]),
         "cls_table_get_info": (C.c_int, [vp, u32, C.POINTER(TableInfo)]),
         "cls_classify": (C.c_int, [vp, u32, C.POINTER(PktSoa), u64, vp, vp, u32, vp]),
+        "cls_classify_rules": (C.c_int, [vp, u32, C.POINTER(PktSoa), u64, vp, vp, u32, vp]),
         "cls_last_kernel_ms": (C.c_int, [vp, C.POINTER(C.c_float)]),
         "cls_kernel_times": (C.c_int, [vp, C.POINTER(C.c_float), u32, C.POINTER(u32)]),
         "cls_kernel_starts": (C.c_int, [vp, C.POINTER(C.c_float), u32, C.POINTER(u32)]),

@@ -760,6 +760,104 @@ static int classify16_locked(cls_engine* e, std::shared_ptr<Table> t, const cls_
     return finish_counts(e, *t, t->c16, sc, co, n, verdict_out, d_verdict, counters_out, flags, s, remapped);
 }
 
+// Each packet's ACLAction and terminating rule (the debug trace of
+// evalACL's matched rule, aclengine_mock.go:651-654): the classify kernels'
+// slot mode, then slot -> rule; tables without a classifier image run the
+// linear kernel.  No counters are touched.
+static int classify_rules_locked(cls_engine* e, uint32_t table_id, const cls_pkt_soa* pk, uint64_t n,
+                                 uint8_t* verdict_out, uint32_t* rule_out, uint32_t flags, void* stream) {
+    auto it = e->tables.find(table_id);
+    if (it == e->tables.end()) return fail(e, CLS_E_NOTFOUND, "no table %u", table_id);
+    const std::shared_ptr<Table> t = it->second;
+    const bool v16 = pk->af == CLS_AF_V16;
+    if (!v16 && pk->af != CLS_AF_V4) return fail(e, CLS_E_INVAL, "af must be CLS_AF_V4 or CLS_AF_V16");
+    if (n && (!pk->dport || !pk->proto || (v16 ? !pk->src16 || !pk->dst16 : !pk->src4 || !pk->dst4)))
+        return fail(e, CLS_E_INVAL, "missing packet arrays");
+    if (n && !rule_out) return fail(e, CLS_E_INVAL, "rule_out is NULL");
+    if (n > 0xFFFFFFFFull) return fail(e, CLS_E_INVAL, "batch above 2^32 packets");
+    const bool dev = flags & CLS_F_DEVICE;
+    const size_t ab = v16 ? 16 : 4;
+    const uint8_t* src = v16 ? pk->src16 : reinterpret_cast<const uint8_t*>(pk->src4);
+    const uint8_t* dst = v16 ? pk->dst16 : reinterpret_cast<const uint8_t*>(pk->dst4);
+    if (dev && n && (!aligned(rule_out, 4) || (v16 && (!aligned(src, 16) || !aligned(dst, 16))) ||
+                     (!v16 && (!aligned(src, 4) || !aligned(dst, 4))) || !aligned(pk->dport, 2)))
+        return fail(e, CLS_E_INVAL, "device arrays must be aligned to their element size");
+    HIPC(e, hipSetDevice(e->device));
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : e->stream;
+    const uint16_t* dp = pk->dport;
+    const uint8_t* pr = pk->proto;
+    uint8_t* d_verdict = verdict_out;
+    uint32_t* d_rule = rule_out;
+    if (!dev && n) {
+        HIPC(e, e->s_src.ensure(n * ab));
+        HIPC(e, e->s_dst.ensure(n * ab));
+        HIPC(e, e->s_dport.ensure(n * 2));
+        HIPC(e, e->s_proto.ensure(n));
+        HIPC(e, e->s_rule.ensure(n * 4));
+        HIPC(e, hipMemcpyAsync(e->s_src.p, src, n * ab, hipMemcpyHostToDevice, s));
+        HIPC(e, hipMemcpyAsync(e->s_dst.p, dst, n * ab, hipMemcpyHostToDevice, s));
+        HIPC(e, hipMemcpyAsync(e->s_dport.p, dp, n * 2, hipMemcpyHostToDevice, s));
+        HIPC(e, hipMemcpyAsync(e->s_proto.p, pr, n, hipMemcpyHostToDevice, s));
+        src = e->s_src.as<uint8_t>();
+        dst = e->s_dst.as<uint8_t>();
+        dp = e->s_dport.as<uint16_t>();
+        pr = e->s_proto.as<uint8_t>();
+        d_rule = e->s_rule.as<uint32_t>();
+        d_verdict = nullptr;
+        if (verdict_out) {
+            HIPC(e, e->s_verdict.ensure(n));
+            d_verdict = e->s_verdict.as<uint8_t>();
+        }
+    }
+    LaunchCfg cfg;
+    cfg.stream = s;
+    for (uint64_t off = 0; off < n; off += kClsChunk) {        // 32-bit packet offsets in the kernels
+        const uint64_t m = std::min<uint64_t>(kClsChunk, n - off);
+        uint8_t* vo = d_verdict ? d_verdict + off : nullptr;
+        uint32_t* ro = d_rule + off;
+        if (v16) {
+            const auto& q = t->p16;
+            const Cls4Image& ci = q.img.core;
+            const Cls4Dev cd = cls4_dev(ci, q.d_img, q.d_lin, uint32_t(q.lin.size()), t->n_rules);
+            cfg.other = cls4_dev(q.oimg, q.d_oimg, DevBuf(), 0, t->n_rules);
+            cfg.grid = cls_grid(e, true, q.lds_resident, ci.lds_bytes, m);
+            Pkts16 pc{reinterpret_cast<const uint4*>(src + 16 * off), reinterpret_cast<const uint4*>(dst + 16 * off),
+                      dp + off, pr + off, m, 0u};
+            if (ci.swap) std::swap(pc.src, pc.dst);          // destination-keyed image
+            HIPC(e, launch_classify16_slots(cd, fe16(q.img, q.d_src_search), pc, ro, q.lds_resident, cfg));
+            HIPC(e, launch_slot_rules(ro, q.d_slot_rule.as<uint32_t>(), uint32_t(m), vo, ro, s));
+        } else {
+            const uint32_t* s4 = reinterpret_cast<const uint32_t*>(src) + off;
+            const uint32_t* d4 = reinterpret_cast<const uint32_t*>(dst) + off;
+            const Pkts4 pc{s4, d4, dp + off, pr + off, m};
+            if (t->has_cls) {
+                cfg.other = cls4_dev(t->oimg, t->d_oimg, DevBuf(), 0, t->n_rules);
+                cfg.grid = cls_grid(e, true, t->lds_resident, t->img.lds_bytes, m);
+                HIPC(e, launch_classify4_slots(table_dev(*t), framed(t->img, pc), ro, t->lds_resident, cfg));
+                HIPC(e, launch_slot_rules(ro, t->d_slot_rule.as<uint32_t>(), uint32_t(m), vo, ro, s));
+            } else {
+                cfg.grid = cls_grid(e, false, false, 0, m);
+                HIPC(e, launch_classify4_linear(t->d_lin4.as<LinRule4>(), uint32_t(t->lin4.size()), t->n_rules, pc,
+                                                vo, nullptr, cfg, ro));
+            }
+        }
+    }
+    if (!dev && n) {
+        if (verdict_out) HIPC(e, hipMemcpyAsync(verdict_out, d_verdict, n, hipMemcpyDeviceToHost, s));
+        HIPC(e, hipMemcpyAsync(rule_out, d_rule, n * 4, hipMemcpyDeviceToHost, s));
+        HIPC(e, hipStreamSynchronize(s));
+    }
+    return CLS_OK;
+}
+
+int cls_classify_rules(cls_engine* e, uint32_t table_id, const cls_pkt_soa* pk, uint64_t n, uint8_t* verdict_out,
+                       uint32_t* rule_out, uint32_t flags, void* stream) {
+    if (!e || !pk) return CLS_E_INVAL;
+    std::lock_guard<std::mutex> g(e->mu);
+    const DeviceGuard dg;        // the caller's device again on return
+    return classify_rules_locked(e, table_id, pk, n, verdict_out, rule_out, flags, stream);
+}
+
 int cls_classify(cls_engine* e, uint32_t table_id, const cls_pkt_soa* pk, uint64_t n,
                  uint8_t* verdict_out, uint64_t* counters_out, uint32_t flags, void* stream) {
     if (!e || !pk) return CLS_E_INVAL;

@@ -191,6 +191,7 @@ struct cls_engine {
     DevBuf s_pq;                   // connection path: the pair launch's OTHER queue
     DevBuf s_rules, s_tctr, s_cctr;  // connection path: rule pool, table counter pointers, call counters
     DevBuf s_crows;                  // ... LDS counter rows of the workgroups
+    DevBuf s_rule;                   // cls_classify_rules of host arrays: the rule per packet
     bool cctr_zero = false;          // s_cctr cleared since its allocation (the scatter launch keeps it zero)
     // counting connection batches' scatter events (Table::conn_ev), reused
     // once no table holds them: one record per batch, not one per table

@@ -288,12 +288,14 @@ __global__ __launch_bounds__(1024) void fold_kernel(const uint32_t* __restrict__
     }
 }
 
+// rule_out (cls_classify_rules): each packet's terminating rule instead of
+// the counters.
 __global__ __launch_bounds__(kBlock) void classify4_linear(const LinRule4* __restrict__ rules,
                                                            uint32_t nr, uint32_t n_rules, Pkts4 p,
                                                            uint8_t* verdict,
-                                                           unsigned long long* gslot) {
+                                                           unsigned long long* gslot, uint32_t* rule_out) {
     __shared__ uint32_t lctr[kLinLdsCounters];
-    const bool lds = n_rules + 1 <= kLinLdsCounters;
+    const bool lds = n_rules + 1 <= kLinLdsCounters && !rule_out;
     if (lds) {
         for (uint32_t i = threadIdx.x; i <= n_rules; i += blockDim.x) lctr[i] = 0u;
         __syncthreads();
@@ -326,7 +328,8 @@ __global__ __launch_bounds__(kBlock) void classify4_linear(const LinRule4* __res
         }
         if (live) {
             if (verdict) verdict[i] = uint8_t(res);
-            if (lds) atomicAdd(&lctr[rule], 1u);
+            if (rule_out) rule_out[i] = rule;
+            else if (lds) atomicAdd(&lctr[rule], 1u);
             else atomicAdd(&gslot[rule], 1ull);
         }
     }
@@ -336,6 +339,19 @@ __global__ __launch_bounds__(kBlock) void classify4_linear(const LinRule4* __res
             const uint32_t v = lctr[i];
             if (v) atomicAdd(&gslot[i], (unsigned long long)v);
         }
+    }
+}
+
+// Slot-mode words -> each packet's ACLAction and terminating rule
+// (cls_classify_rules): word = result | slot << 2, slot_rule = the image's
+// slot -> rule map (the OTHER image's slots after the main image's); rule
+// may alias words (each element is read before it is written).
+__global__ __launch_bounds__(256) void slot_rules_kernel(const uint32_t* words, const uint32_t* __restrict__ slot_rule,
+                                                         uint32_t n, uint8_t* __restrict__ verdict, uint32_t* rule) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const uint32_t w = words[i];
+        if (verdict) verdict[i] = uint8_t(w & 3u);
+        rule[i] = slot_rule[w >> 2];
     }
 }
 
@@ -1053,9 +1069,17 @@ int cls_block() { return kClsBlock; }
 
 hipError_t launch_classify4_linear(const LinRule4* rules, uint32_t n_lin, uint32_t n_rules,
                                    const Pkts4& p, uint8_t* verdict, unsigned long long* gslot,
-                                   const LaunchCfg& cfg) {
+                                   const LaunchCfg& cfg, uint32_t* rule_out) {
     hipLaunchKernelGGL(classify4_linear, dim3(cfg.grid), dim3(kBlock), 0, cfg.stream, rules, n_lin,
-                       n_rules, p, verdict, gslot);
+                       n_rules, p, verdict, gslot, rule_out);
+    return hipGetLastError();
+}
+
+hipError_t launch_slot_rules(const uint32_t* words, const uint32_t* slot_rule, uint32_t n, uint8_t* verdict,
+                             uint32_t* rule, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const uint32_t grid = std::min<uint32_t>((n + 255u) / 256u, 8192u);
+    hipLaunchKernelGGL(slot_rules_kernel, dim3(grid), dim3(256), 0, s, words, slot_rule, n, verdict, rule);
     return hipGetLastError();
 }
 

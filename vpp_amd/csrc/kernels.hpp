@@ -110,9 +110,15 @@ hipError_t launch_classify4_cls(const Cls4Dev& t, const Pkts4& p, uint8_t* verdi
 hipError_t launch_classify16_cls(const Cls4Dev& t, const Fe16& fe, const Pkts16& p, uint8_t* verdict,
                                  unsigned long long* gslot, bool lds_resident, bool lin,
                                  const LaunchCfg& cfg);
+// rule_out (not null): each packet's terminating rule (R: the default DENY)
+// instead of counting into gslot
 hipError_t launch_classify4_linear(const LinRule4* rules, uint32_t n_lin, uint32_t n_rules,
                                    const Pkts4& p, uint8_t* verdict, unsigned long long* gslot,
-                                   const LaunchCfg& cfg);
+                                   const LaunchCfg& cfg, uint32_t* rule_out = nullptr);
+// slot-mode words (result | slot << 2) -> verdict (may be null) and
+// slot_rule[slot] per packet; rule may alias words
+hipError_t launch_slot_rules(const uint32_t* words, const uint32_t* slot_rule, uint32_t n, uint8_t* verdict,
+                             uint32_t* rule, hipStream_t s);
 // slot_val[i] += sum_w part[w * n + i], w < rows (the classify kernel's
 // partials); zero[0, n_zero) = 0 in the same launch (zero may be null)
 hipError_t launch_fold(const uint32_t* part, uint32_t rows, uint32_t n, unsigned long long* slot_val,

@@ -229,6 +229,43 @@ class Engine:
                                             flags, None))
         return v, c
 
+    def classify_rules(self, table: Table, src, dst, dport, proto, verdict=None, rules=None, stream=None):
+        """Each packet's ACLAction and terminating rule index (R: the default
+        DENY) -- cls_classify_rules, the batch form of the matched rule
+        evalACL logs; no counters.  numpy inputs: synchronous, returns
+        (verdict uint8[n], rules uint32[n]); torch device tensors: enqueued on
+        ``stream``, ``rules`` (int32[n]) and ``verdict`` (uint8[n], optional)
+        written and returned."""
+        n = int(len(dport))
+        dev = _is_torch(src)
+        v16 = (src.dim() if dev else np.ndim(src)) == 2
+
+        def soa(s_, d_, dp_, pr_):
+            if v16:
+                return _abi.PktSoa(_abi.AF_V16, None, None, _ptr(s_), _ptr(d_), None, _ptr(dp_), _ptr(pr_))
+            return _abi.PktSoa(_abi.AF_V4, _ptr(s_), _ptr(d_), None, None, None, _ptr(dp_), _ptr(pr_))
+        if dev:
+            import torch
+            if stream is None:
+                stream = torch.cuda.current_stream()
+            s = stream.cuda_stream if hasattr(stream, "cuda_stream") else stream
+            if rules is None:
+                rules = torch.empty(n, dtype=torch.int32, device=src.device)
+            pk = soa(src, dst, dport, proto)
+            self._check(_abi.lib().cls_classify_rules(self.h, table.id, C.byref(pk), n, _ptr(verdict),
+                                                      _ptr(rules), _abi.F_DEVICE, s))
+            return verdict, rules
+        adt = np.uint8 if v16 else np.uint32
+        src = np.ascontiguousarray(src, adt)
+        dst = np.ascontiguousarray(dst, adt)
+        dport = np.ascontiguousarray(dport, np.uint16)
+        proto = np.ascontiguousarray(proto, np.uint8)
+        v = np.zeros(n, np.uint8) if verdict is None else verdict
+        r = np.zeros(n, np.uint32) if rules is None else rules
+        pk = soa(src, dst, dport, proto)
+        self._check(_abi.lib().cls_classify_rules(self.h, table.id, C.byref(pk), n, _ptr(v), _ptr(r), 0, None))
+        return v, r
+
     def stream_floor(self, src, dst, dport, proto, verdict, reps: int = 10, stream=None) -> float:
         """Average ms of the classify kernel's packet stream alone (same loads,
         stores and grid, no lookups) over a device batch: the measured floor
