@@ -141,10 +141,12 @@ def main():
     # byte written) per HBM-resident batch, beside the stream floor of the
     # same arrays (cls_stream_floor_conn: the same reads and write, no
     # evaluation)
+    # (the product path: device batches through the C ABI, back to back)
     floor = eng.stream_floor_conn(*dargs, reps=20)
     roof = {"bound": "hbm", "bytes_per_connection": 22, "peak": 8000.0, "unit": "GB/s",
-            "achieved": round(22 * n / dev_dt / 1e9, 1), "frac": round(22 * n / dev_dt / 8e12, 4),
-            "stream_floor_ms": round(floor, 4), "frac_of_stream_floor": round(floor / (dev_dt * 1e3), 4)}
+            "achieved": round(22 * n / abi_piped / 1e9, 1), "frac": round(22 * n / abi_piped / 8e12, 4),
+            "stream_floor_ms": round(floor, 4), "frac_of_stream_floor": round(floor / (abi_piped * 1e3), 4),
+            "timed": "abi_pipelined_ms_per_batch"}
     k = a.cpu_sample
     t1 = time.perf_counter()
     want, _ = oracle_connections(bind, by_name, ifs, si[:k], di[:k], {f: v[:k] for f, v in tr.items()}, 4)
@@ -172,8 +174,12 @@ def main():
         assert np.array_equal(fast, out[:kf]), "the fast CPU port differs from the GPU verdicts"
     print(json.dumps({
         "metric": "connections classified per second (testConnection, up to 4 ACL evaluations each)",
-        "value": round(n / dt / 1e6, 3), "unit": "Mconn/s", "n": n, "ms_per_batch": round(dt * 1e3, 3),
-        "pcie_included": True, "global_rules": len(by_name["global"]), "local_acls": a.locals,
+        "value": round(n / abi_piped / 1e6, 3), "unit": "Mconn/s", "n": n,
+        "ms_per_batch": round(abi_piped * 1e3, 4),
+        "timed": "device batches through cls_connect_batch, back to back (HBM-resident, stream-ordered)",
+        "host_arrays": {"value": round(n / dt / 1e6, 3), "unit": "Mconn/s", "ms_per_batch": round(dt * 1e3, 3),
+                        "pcie_included": True},
+        "global_rules": len(by_name["global"]), "local_acls": a.locals,
         "other_proto": bool(a.other_proto), "hbm_resident_counted": counted,
         "hbm_resident": {"value": round(n / dev_dt / 1e6, 3), "unit": "Mconn/s",
                          "ms_per_batch": round(dev_dt * 1e3, 4), "abi_ms_per_batch": round(abi_dt * 1e3, 4),
