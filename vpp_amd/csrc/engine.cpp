@@ -1852,19 +1852,25 @@ int connect_locked(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t* ou
                                         s));
         }
         e->cctr_zero = true;
-        // cls_conn_counters waits for this batch's scatter, not the device
+        // cls_conn_counters waits for this batch's scatter, not the device:
+        // it reads on the engine's stream, so a batch on that stream needs no
+        // event (and every earlier batch is ordered before it, conn_last);
+        // one on another stream records one (an event per batch cost the
+        // stream ~5 us, profiles/r06u_conn_default_12_batches.txt)
         std::shared_ptr<SharedEvent> ev;
-        for (auto& x : e->conn_evs)
-            if (x.use_count() == 1) {
-                ev = x;
-                break;
+        if (s != e->stream) {
+            for (auto& x : e->conn_evs)
+                if (x.use_count() == 1) {
+                    ev = x;
+                    break;
+                }
+            if (!ev) {
+                ev = std::make_shared<SharedEvent>();
+                HIPC(e, hipEventCreateWithFlags(&ev->ev, hipEventDisableTiming));
+                e->conn_evs.push_back(ev);
             }
-        if (!ev) {
-            ev = std::make_shared<SharedEvent>();
-            HIPC(e, hipEventCreateWithFlags(&ev->ev, hipEventDisableTiming));
-            e->conn_evs.push_back(ev);
+            HIPC(e, hipEventRecord(ev->ev, s));
         }
-        HIPC(e, hipEventRecord(ev->ev, s));
         for (size_t j = 0; j < dtab.size(); ++j) dtab[j]->conn_ev = ev;
     } else if (cmode) {
         e->cctr_zero = true;            // n == 0: nothing was counted
