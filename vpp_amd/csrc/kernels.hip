@@ -734,18 +734,34 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kCount == 
         // job j of the wave is call k of owner lane o: the ballots of the four
         // calls give every job a rank; the jobs run 64 at a time, every lane
         // on one job
+        // The jobs of the calls with a linear ACL.  When they need more than
+        // one pass of the wave (more than 64), the calls that are never made
+        // are dropped first: the SYN calls' large-ACL results end the
+        // evaluation on DENY or FAILURE, and conn_state leaves calls 2 and 3
+        // unmade after a terminal call 0 or 1 whether or not call 1 itself
+        // was made (a REFLECT of call 0 on one interface skips all three);
+        // call 2's result is not used (a REFLECT of call 1 skips call 2 but
+        // not call 3).  At 64 local ACLs: 2.27 -> 1.98 passes per wave,
+        // connect_kernel 154 -> 135 us (profiles/r06y_conn_skip_ab.txt); at
+        // 12 one pass either way, and the test costs nothing there.
         bool job[4];
         uint64_t m[4];
         uint32_t c[5], jpos[4];
-        c[0] = 0;
+        auto pack = [&](bool skip) {
+            c[0] = 0;
+            bool ended = false;                                 // a large SYN result ended the evaluation
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            job[k] = di[k] >= 0 && bi[k] < 0;
-            m[k] = __ballot(job[k]);
-            // (the set bits of m[k] below this lane: mbcnt, no lane mask held in registers)
-            jpos[k] = c[k] + __builtin_amdgcn_mbcnt_hi(uint32_t(m[k] >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m[k]), 0u));
-            c[k + 1] = c[k] + uint32_t(__popcll(m[k]));
-        }
+            for (int k = 0; k < 4; ++k) {
+                job[k] = di[k] >= 0 && bi[k] < 0 && !ended;
+                if (skip) ended = ended || (k < 2 && bi[k] >= 0 && ((w[k] + 1u) & 3u) <= 1u);   // DENY 0, FAILURE 3
+                m[k] = __ballot(job[k]);
+                // (the set bits of m[k] below this lane: mbcnt, no lane mask held in registers)
+                jpos[k] = c[k] + __builtin_amdgcn_mbcnt_hi(uint32_t(m[k] >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m[k]), 0u));
+                c[k + 1] = c[k] + uint32_t(__popcll(m[k]));
+            }
+        };
+        pack(false);
+        if (c[4] > 64u) pack(true);                             // wave-uniform
         const uint32_t nj = c[4];
         uint32_t rj[4] = {0u, 0u, 0u, 0u};
         for (uint32_t j0 = 0; j0 < nj; j0 += 64u) {             // wave-uniform
