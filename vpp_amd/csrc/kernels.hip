@@ -631,17 +631,26 @@ __device__ __forceinline__ uint32_t conn_state(const uint32_t res[4], bool same,
     return v | uint32_t(made[0]) << 2 | uint32_t(made[1]) << 3 | uint32_t(made[2]) << 4 | uint32_t(made[3]) << 5;
 }
 
-// A connection launch's workgroup prologue: the rule pool, the LDS counters
-// (zeroed), testConnection's state table and the descriptor / interface
-// tables into LDS.
-template <bool kLdsRules, int kCount>
-__device__ __forceinline__ void conn_prologue(const ConnArgs& a, uint4* smem) {
+template <bool k16, bool kLdsRules, int kCount, bool kJobs>
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kCount == 1 && k16 ? 4 : 6))) void connect_kernel(
+    ConnArgs a) {
+    typedef typename ConnT<k16>::A A;
+    extern __shared__ uint4 smem[];
     typedef __attribute__((address_space(3))) uint32_t* lctr_t;
+    const uint32_t lane = __lane_id();
+    // 32-bit connection indices (the host splits batches at 2^30): SGPR base
+    // + 32-bit VGPR offset addressing, no 64-bit index arithmetic per load
+    const uint32_t n = uint32_t(a.n);
+    const uint32_t nthreads = gridDim.x * blockDim.x;
+    const uint32_t n_iter = (n + nthreads - 1u) / nthreads;     // uniform trip count (ballots below)
+    const uint32_t stride = uint32_t(a.pre_stride);
     if constexpr (kLdsRules) lds_copy(smem, static_cast<const uint4*>(a.rules), a.rules_bytes / 16u);
     if constexpr (kCount == 1) {
         const uint32_t nw = a.ctr16 ? (a.n_ctr + 1u) / 2u : a.n_ctr;
         for (uint32_t j = threadIdx.x; j < nw; j += blockDim.x) *lctr_t(a.ctr_lds + 4u * j) = 0u;
     }
+    // this workgroup's copy of the call counters
+    unsigned long long* const gctr = a.ctr + uint64_t(blockIdx.x % kConnCtrCopies) * a.n_ctr;
     // the state machine's table (kConnStateEntries bytes): entry res0 | res1
     // << 2 | res2 << 4 | res3 << 6 | same << 8 | !ok << 9
     for (uint32_t x = threadIdx.x; x < kConnStateEntries; x += blockDim.x) {
@@ -657,24 +666,6 @@ __device__ __forceinline__ void conn_prologue(const ConnArgs& a, uint4* smem) {
         for (uint32_t j = threadIdx.x; j < 4u * a.n_ifs; j += blockDim.x) *lctr_t(a.meta_lds + 4u * (nd + j)) = gi[j];
     }
     __syncthreads();
-}
-
-template <bool k16, bool kLdsRules, int kCount, bool kJobs>
-__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kCount == 1 && k16 ? 4 : 6))) void connect_kernel(
-    ConnArgs a) {
-    typedef typename ConnT<k16>::A A;
-    extern __shared__ uint4 smem[];
-    typedef __attribute__((address_space(3))) uint32_t* lctr_t;
-    const uint32_t lane = __lane_id();
-    // 32-bit connection indices (the host splits batches at 2^30): SGPR base
-    // + 32-bit VGPR offset addressing, no 64-bit index arithmetic per load
-    const uint32_t n = uint32_t(a.n);
-    const uint32_t nthreads = gridDim.x * blockDim.x;
-    const uint32_t n_iter = (n + nthreads - 1u) / nthreads;     // uniform trip count (ballots below)
-    const uint32_t stride = uint32_t(a.pre_stride);
-    conn_prologue<kLdsRules, kCount>(a, smem);
-    // this workgroup's copy of the call counters
-    unsigned long long* const gctr = a.ctr + uint64_t(blockIdx.x % kConnCtrCopies) * a.n_ctr;
     const A* src = static_cast<const A*>(a.src);
     const A* dst = static_cast<const A*>(a.dst);
     // IPv4: this wave's job list in LDS, 64 entries of 8 B {owner lane | call
