@@ -461,10 +461,22 @@ def main_native(args, rank, world, local):
     n = args.packets or (-(-n_default // world) if strong else n_default)
     af = spec.get("layout", 4)
     eng = Engine(device, options=dict(o.split("=", 1) for o in args.opt))   # one rank per GPU (RCCL: one per device)
+    comm_err = None
     if dist is not None and not shared:
         uid = [Engine.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
-        eng.comm_init(world, rank, uid[0])
+        try:
+            eng.comm_init(world, rank, uid[0])
+            ok = 1.0
+        except Exception as ex:                # (reported in the line; every rank takes the same path)
+            comm_err, ok = str(ex), 0.0
+        t = __import__("torch").tensor([ok], dtype=__import__("torch").float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        if t.item() < 1.0:                     # no RCCL group: counters summed over gloo after the steps
+            shared = True
+            comm_err = comm_err or "another rank's cls_comm_init failed"
+            eng.close()                        # (a rank whose init succeeded must not all-reduce alone)
+            eng = Engine(device, options=dict(o.split("=", 1) for o in args.opt))
     table = eng.put_table("contiv/vpp-policy-GLOBAL", acl.rules)
     info = table.info()
     R = table.n_rules
@@ -586,8 +598,10 @@ def main_native(args, rank, world, local):
                        "collective": ("counter all-reduce in the library: ncclAllReduce u64 sum over %d RCCL "
                                       "ranks (cls_comm_init), %d B, side stream overlapping the next step's "
                                       "classify" % (comm[0], (R + 1) * 8)) if comm[0] else
-                                     ("counters summed over gloo after the timed steps (%d ranks share a GPU: "
-                                      "RCCL needs one rank per device; rehearsal, not a scaling number)" % world)
+                                     ("counters summed over gloo after the timed steps (%s)" % (
+                                         "cls_comm_init failed: %s" % comm_err if comm_err else
+                                         "%d ranks share a GPU: RCCL needs one rank per device; rehearsal, "
+                                         "not a scaling number" % world))
                                      if shared else None},
             "counters_sum_ok": ok_sum,
             "settle_ms": round(settle_ms, 1),
