@@ -118,8 +118,8 @@ def oracle_connections(bind, by_name, ifs, si, di, tr, fam):
     return out, counts
 
 
-def _run(eng, seed, mode, fam, count, n=20000, n_local=64):
-    ifs, bind, by_name, pool, spec = build(eng, seed, fam=fam, n_local=n_local)
+def _run(eng, seed, mode, fam, count, n=20000, n_local=64, cfg=2):
+    ifs, bind, by_name, pool, spec = build(eng, seed, fam=fam, n_local=n_local, cfg=cfg)
     tr = traffic(seed, n, pool, spec, fam)
     rng = np.random.default_rng(seed)
     ids = np.array([eng.if_id(x) for x in ifs], np.uint32)
@@ -513,6 +513,24 @@ def test_counter_widths_and_flush_paths(flush, plan):
         _run(eng, 21, "device_auto", 4, count=True, n=20000, n_local=12)
     finally:
         eng.close()
+
+
+@pytest.mark.parametrize("wg768", [1, 0])
+def test_counted_768_thread_workgroups(wg768, capfd):
+    """The bench's counted plan (config-3 global ACL, 12 local ACLs, seed 0):
+    three 512-thread workgroups do not fit the LDS, two 768-thread ones do
+    (24 waves per CU, u16 counters, job lists); option conn_wg768=0 keeps the
+    512-thread shape.  Verdicts and per-(ACL, rule) counters against
+    orc_test_connection either way."""
+    from vpp_amd.engine import Engine
+    eng = Engine(options={"conn_wg768": wg768, "debug_conn": 1})
+    try:
+        # (>= kConnClsMinBatch connections: the global ACL on the classifier)
+        _run(eng, 0, "device_auto", 4, count=True, n=70000, n_local=12, cfg=3)
+    finally:
+        eng.close()
+    plans = [ln for ln in capfd.readouterr().err.splitlines() if ln.startswith("connect:") and "cmode 1" in ln]
+    assert plans and all(("block 768" in ln) == bool(wg768) for ln in plans), plans
 
 
 def test_pair_launch_partial_last_step_matches_linear():

@@ -1741,7 +1741,7 @@ int connect_locked(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t* ou
     // counters when they fit (else the kernel reads them from global memory).
     // Persistent grid: as many 512-thread workgroups per CU as the LDS
     // allows, at most three (the kernel's registers allow 24 waves per CU);
-    // where it allows only one, one 1024-thread workgroup.
+    // else two of 768 threads, two of 512 or one of 1024 (plan_of below).
     a.n_desc = uint32_t(desc.size());
     const size_t meta = desc.size() * sizeof(ConnDesc) + ifs.size() * sizeof(IfAcls);
     // The launch's LDS plan for counters of ctr_b bytes: the descriptor and
@@ -1756,22 +1756,36 @@ int connect_locked(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t* ou
         uint32_t meta_lds, job_lds;
         int per_cu, block;
     };
+    // Where three 512-thread workgroups do not fit but two 768-thread ones
+    // do (the shared part -- pool, counters, tables -- is paid per
+    // workgroup, the job lists per wave), the 768-thread shape keeps 24 waves
+    // per CU instead of 16 (option conn_wg768=0: the 512 / 1024 shapes only).
     auto plan_of = [&](size_t ctr_b, bool jobs) {
         jobs = jobs && !k16 && e->opts.conn_jobs;
         const int cu_cap = std::min(cmode == 1 && k16 ? 2 : 3, e->opts.conn_wg_per_cu > 0 ? e->opts.conn_wg_per_cu : 3);
-        auto per_cu_of = [&](size_t b) { return b ? std::max(1, std::min(cu_cap, int(lds_max / b))) : cu_cap; };
-        LdsPlan q{lds_used + ctr_b, 0xFFFFFFFFu, 0xFFFFFFFFu, 0, 0};
-        const size_t meta_at = (q.lds + 15) & ~size_t(15);
-        if (meta_at + meta <= lds_max && per_cu_of(meta_at + meta) == per_cu_of(q.lds) && !(no_lds & 4)) {
-            q.meta_lds = uint32_t(meta_at);
-            q.lds = meta_at + meta;
-        }
-        q.per_cu = per_cu_of(q.lds);
-        q.block = q.per_cu >= 2 ? 512 : 1024;
-        const size_t job_at = (q.lds + 15) & ~size_t(15), job_b = size_t(q.block / 64) * 512;
-        if (jobs && job_at + job_b <= lds_max && (q.per_cu == 1 || per_cu_of(job_at + job_b) == q.per_cu)) {
-            q.job_lds = uint32_t(job_at);
-            q.lds = job_at + job_b;
+        auto shape = [&](int cap, int block) {
+            auto per_cu_of = [&](size_t b) { return b ? std::max(1, std::min(cap, int(lds_max / b))) : cap; };
+            LdsPlan q{lds_used + ctr_b, 0xFFFFFFFFu, 0xFFFFFFFFu, 0, 0};
+            const size_t meta_at = (q.lds + 15) & ~size_t(15);
+            if (meta_at + meta <= lds_max && per_cu_of(meta_at + meta) == per_cu_of(q.lds) && !(no_lds & 4)) {
+                q.meta_lds = uint32_t(meta_at);
+                q.lds = meta_at + meta;
+            }
+            q.per_cu = per_cu_of(q.lds);
+            q.block = block ? block : q.per_cu >= 2 ? 512 : 1024;
+            const size_t job_at = (q.lds + 15) & ~size_t(15), job_b = size_t(q.block / 64) * 512;
+            if (jobs && job_at + job_b <= lds_max && (q.per_cu == 1 || per_cu_of(job_at + job_b) == q.per_cu)) {
+                q.job_lds = uint32_t(job_at);
+                q.lds = job_at + job_b;
+            }
+            return q;
+        };
+        // (job lists first, then waves per CU)
+        auto rank = [](const LdsPlan& p) { return (p.job_lds != 0xFFFFFFFFu ? 64 : 0) + p.per_cu * p.block / 64; };
+        const LdsPlan q = shape(cu_cap, 0);
+        if (cu_cap == 3 && e->opts.conn_wg768) {
+            const LdsPlan r = shape(2, 768);
+            if (r.per_cu == 2 && rank(r) > rank(q)) return r;
         }
         return q;
     };
@@ -1790,12 +1804,13 @@ int connect_locked(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t* ou
             if (c[pick].lds > lds_max) pick = -1;
         }
         if (pick < 0) {
-            // the job lists first, then workgroups per CU, then u16 (12 local
+            // the job lists first, then waves per CU, then u16 (12 local
             // ACLs, ms per counted batch: 16j 0.1367, 32j 0.1379, 32s 0.1468, 16s
             // 0.1571; 64: 16j 0.2289, 32 (no room for job lists) 0.2367, 16s
             // 0.2449 -- profiles/r05zh_conn_counted_plans.txt)
             auto score = [&](int k) {
-                return c[k].lds > lds_max ? -1 : (c[k].job_lds != 0xFFFFFFFFu ? 8 : 0) + 2 * c[k].per_cu + (k % 2 == 1);
+                return c[k].lds > lds_max ? -1 : (c[k].job_lds != 0xFFFFFFFFu ? 8 : 0) + c[k].per_cu * c[k].block / 256 +
+                                            (k % 2 == 1);
             };
             pick = 0;
             for (int k = 1; k < 4; ++k)

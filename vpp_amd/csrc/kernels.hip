@@ -587,8 +587,10 @@ __device__ __forceinline__ uint32_t conn_bm(const ConnArgs& a, const ConnDesc& D
 // global atomics.
 // Workgroup size (launch_connect): the kernel holds ~80 VGPRs (6 waves per
 // SIMD), so 24 waves fit a CU -- three 512-thread workgroups where the LDS
-// allows two or more, else one 1024-thread workgroup (16 waves rather than
-// the 8 of one 512-thread one); forcing 64 VGPRs spills to scratch.  The
+// allows, else two 768-thread ones where it allows those (the bench's
+// counted plan at 12 local ACLs: 88 -> 75 us, profiles/r06w768_*), else two
+// 512-thread ones or one 1024-thread workgroup (16 waves rather than the 8
+// of one 512-thread one); forcing 64 VGPRs spills to scratch.  The
 // 16-byte LDS-counter variants (kCount 1, k16) take up to 128 VGPRs (at 80
 // they spill) and at most two 512-thread workgroups per CU (the host's plan);
 // the IPv4 ones fit 80 since the job ranks came from mbcnt (round 6: 89 with

@@ -296,7 +296,7 @@ struct ConnArgs {
 };
 // k16: 16-byte addresses; lds_rules: stage the pool; count: 0 none, 1 LDS
 // counters, 2 global (wave-aggregated) counters; grid: persistent workgroups
-// of `block` threads (512 or 1024); lds: dynamic LDS bytes (pool, LDS
+// of `block` threads (512, 768 or 1024); lds: dynamic LDS bytes (pool, LDS
 // counters, a.meta_lds tables)
 hipError_t launch_connect(const ConnArgs& a, bool k16, bool lds_rules, int count, int grid, int block, size_t lds,
                           hipStream_t s);

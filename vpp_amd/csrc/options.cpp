@@ -72,6 +72,7 @@ bool opts_set(Opts& o, const char* key, const char* value, std::string& why) {
     OPT("conn_no_lds", conn_no_lds, i)
     OPT("conn_jobs", conn_jobs, b)
     OPT("conn_wg_per_cu", conn_wg_per_cu, i)
+    OPT("conn_wg768", conn_wg768, b)
     OPT("conn_flush_atomic", conn_flush_atomic, b)
     OPT("debug_conn", debug_conn, b)
     OPT("batch_layout", batch_layout, i)

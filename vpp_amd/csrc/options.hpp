@@ -45,6 +45,7 @@ struct Opts {
     int conn_no_lds = 0;        // bit 0 rules, bit 1 counters, bit 2 descriptors from global memory
     int conn_wg_per_cu = 0;     // measurements: cap on the connection kernel's workgroups per CU (0: none)
     bool conn_jobs = true;      // the waves' LDS job lists (else owner search and shuffles)
+    bool conn_wg768 = true;     // two 768-thread workgroups per CU where three 512-thread ones do not fit
     int conn_plan = -1;         // counting LDS plan 0..3 = 32j 16j 32s 16s (-1: scored)
     bool conn_flush_atomic = false;  // LDS counters flushed by device atomics, not per-workgroup rows
     bool debug_conn = false;    // stderr: a connection launch's LDS plan
