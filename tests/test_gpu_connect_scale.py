@@ -335,22 +335,31 @@ def test_device_plan_follows_binding_changes(count):
         eng.close()
 
 
-@pytest.mark.parametrize("opts", [{}, {"pair_other_global": 1}, {"pair_qcap": 3},
-                                  {"pair_other_global": 1, "pair_qcap": 0},
-                                  {"pair_lq": 0}, {"pair_lq": 2, "pair_qcap": 4},
-                                  {"pair_lq": 3}])
-def test_pair_launch_tail_and_other_protocols(opts):
+@pytest.mark.parametrize("opts,cfg", [({}, 2), ({"pair_other_global": 1}, 2), ({"pair_qcap": 3}, 2),
+                                      ({"pair_other_global": 1, "pair_qcap": 0}, 2),
+                                      ({"pair_lq": 0}, 2), ({"pair_lq": 2, "pair_qcap": 4}, 2),
+                                      ({"pair_lq": 3}, 2),
+                                      ({}, 3), ({"pair_other_late": 2}, 2), ({"pair_other_late": 2}, 3),
+                                      ({"pair_other_late": 2, "pair_qcap": 3}, 3),
+                                      ({"pair_other_late": 2, "pair_lq": 0}, 3), ({"pair_class": 0}, 3),
+                                      ({"pair_class": 0, "pair_other_late": 2}, 3),
+                                      ({"pair_other_global": 1}, 3)])
+def test_pair_launch_tail_and_other_protocols(opts, cfg, capfd):
     """classify4_pair (k4_pair.hip) on a batch of 4k + 3 connections with
     protocol-47 connections everywhere, the last three included (the scalar
-    tail's direct OTHER path): the OTHER image beside the main one in LDS or
-    read from global memory (o_at = 0), the OTHER queue roomy or nearly
+    tail's direct OTHER path): the OTHER image beside the main one in LDS,
+    read from global memory (o_at = 0), or staged over the main image for
+    the drain (o_late: the plan when it does not fit beside the main one;
+    option pair_other_late=2 forces it), the queued connections carrying
+    their source classes (the OTHER image's classes are the main image's)
+    or (option pair_class=0) searched again, the OTHER queue roomy or nearly
     full / empty so that connections overflow to in-place classification,
     its entries in LDS, in global memory (option pair_lq=0) or in both.
     Verdicts and counters against orc_test_connection."""
     from vpp_amd.engine import Engine
-    eng = Engine(options=opts)
+    eng = Engine(options=dict(opts, debug_conn=1))
     try:
-        ifs, bind, by_name, pool, spec = build(eng, 21, n_local=6, n_if=16)
+        ifs, bind, by_name, pool, spec = build(eng, 21, n_local=6, n_if=16, cfg=cfg)
         n = 4 * 4000 + 3
         tr = traffic(21, n, pool, spec, 4)
         rng = np.random.default_rng(21)
@@ -369,6 +378,14 @@ def test_pair_launch_tail_and_other_protocols(opts):
             assert np.array_equal(eng.conn_counters(name, reset=True), wcounts[name]), name
     finally:
         eng.close()
+    pairs = [ln for ln in capfd.readouterr().err.splitlines() if ln.startswith("pair:")]
+    assert pairs
+    if opts.get("pair_other_late") == 2:
+        assert all(" o_at 0 o_late 1 " in ln for ln in pairs), pairs
+    if opts.get("pair_class") == 0:
+        assert all(" cdiv 0" in ln for ln in pairs), pairs
+    else:
+        assert any(" cdiv 0" not in ln for ln in pairs), pairs
 
 
 def test_conn_counters_do_not_wait_for_other_streams():

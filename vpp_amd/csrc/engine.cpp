@@ -253,6 +253,8 @@ static int table_compile(cls_engine* e, const char* name, const cls_rule* rules,
         t->has_cls = true;
         t->kernel = 1;
         t->lds_resident = t->img.lds_ok && t->img.lds_bytes + kLdsReserved <= uint32_t(max_lds_bytes());
+        if (t->img.h_bounds == t->oimg.h_bounds && t->img.h_iclass == t->oimg.h_iclass && t->img.row_bytes)
+            t->pair_cdiv = uint32_t(((1ull << 32) + t->img.row_bytes - 1) / t->img.row_bytes);
         // the trie and wide cells exist only in LDS-resident images
         if (!cls_kernel_exists(t->img.mode, t->img.list_mode, t->lds_resident, false))
             return fail(e, CLS_E_INVAL, "no classify kernel for the compiled image (mode %u, list mode %u%s)",
@@ -288,6 +290,7 @@ std::shared_ptr<Table> table_clone_host(const Table& s) {
     t->has_cls = s.has_cls;
     t->img = s.img;
     t->oimg = s.oimg;
+    t->pair_cdiv = s.pair_cdiv;
     t->kernel = s.kernel;
     t->lds_resident = s.lds_resident;
     t->p16.ok = s.p16.ok;
@@ -1615,13 +1618,18 @@ int connect_locked(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t* ou
                     uint32_t o_at = (t.img.img_bytes + 15u) & ~15u;
                     // (+ 32: the queue fill word after the images)
                     if (o_at + t.oimg.img_bytes + 32u > uint32_t(max_lds_bytes())) o_at = 0;
-                    if (e->opts.pair_other_global) o_at = 0;   // tests: the global-memory OTHER path
+                    if (e->opts.pair_other_global || e->opts.pair_other_late == 2) o_at = 0;   // tests
+                    // else, when the OTHER image does not fit beside the main
+                    // one, staged over it for the drain (option
+                    // pair_other_late=0: read from global memory there)
+                    const bool o_late = !o_at && !e->opts.pair_other_global && e->opts.pair_other_late > 0 &&
+                                        t.oimg.img_bytes + 32u <= uint32_t(max_lds_bytes());
                     Cls4Dev od = cls4_dev(t.oimg, t.d_oimg, DevBuf(), 0, t.n_rules);
                     if (o_at) {
                         od.off_bounds += o_at; od.off_iclass += o_at; od.off_cells += o_at;
                         od.off_lists += o_at; od.off_tmpl += o_at;
                     }
-                    cfg.grid = cls_grid(e, true, true, o_at ? o_at + t.oimg.img_bytes : t.img.img_bytes, n);
+                    cfg.grid = cls_grid(e, true, true, pair_queue_lds(t.img.img_bytes, o_at, t.oimg.img_bytes, o_late), n);
                     // the OTHER queue, one segment per wave: its first entries
                     // in the LDS left after the images (one workgroup per CU
                     // either way), the rest in global memory
@@ -1629,14 +1637,19 @@ int connect_locked(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t* ou
                     // wave in all / in LDS, tests)
                     const uint32_t nwv = kPairBlock / 64;
                     const uint32_t qw = (pair_qcap(e, n, cfg.grid) + nwv - 1) / nwv;
-                    const uint32_t q_lds = ((o_at ? o_at + t.oimg.img_bytes : t.img.img_bytes) + 15u) & ~15u;
+                    const uint32_t q_lds = pair_queue_lds(t.img.img_bytes, o_at, t.oimg.img_bytes, o_late);
                     uint32_t lq_cap = std::min<uint32_t>(qw, (uint32_t(max_lds_bytes()) - q_lds) / 16u / nwv);
                     if (e->opts.pair_lq >= 0) lq_cap = std::min<uint32_t>(lq_cap, uint32_t(e->opts.pair_lq));
                     const uint32_t gq = qw - lq_cap;
                     HIPC(e, grow(e->s_pq, size_t(cfg.grid) * nwv * std::max<uint32_t>(1, gq) * 16));
+                    if (e->opts.debug_conn)      // diagnostics: where the OTHER image and queue live
+                        std::fprintf(stderr, "pair: img %u oimg %u o_at %u o_late %d lq %u gq %u cdiv %u\n",
+                                     t.img.img_bytes, t.oimg.img_bytes, o_at, int(o_late), lq_cap, gq,
+                                     e->opts.pair_class ? t.pair_cdiv : 0u);
                     HIPC(e, launch_classify4_pair(cd, od, o_at, syn, sp, pre, stride, e->s_pq.as<uint32_t>(), gq,
                                                   pre_rules ? t.d_slot_rule.as<uint32_t>() : nullptr,
-                                                  desc[big[b]].ctr_off, pre_bytes, lq_cap, cfg));
+                                                  desc[big[b]].ctr_off, pre_bytes, lq_cap, o_late,
+                                                  e->opts.pair_class ? t.pair_cdiv : 0u, cfg));
                 } else {
                     cfg.other = cls4_dev(t.oimg, t.d_oimg, DevBuf(), 0, t.n_rules);
                     cfg.grid = cls_grid(e, true, t.lds_resident, t.img.lds_bytes, n);

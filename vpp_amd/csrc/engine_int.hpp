@@ -103,6 +103,10 @@ struct Table {
     DevBuf d_img;
     Cls4Image oimg;            // protocols > 2 (compile.hpp Cls4Opts::other), read from global memory
     DevBuf d_oimg;
+    // the OTHER image's source classes are img's (same interval bounds and
+    // class numbering): the pair launch's queued connections carry their
+    // classes (ceil(2^32 / img.row_bytes); 0: the drain searches again)
+    uint32_t pair_cdiv = 0;
     int kernel = 0;            // 0 linear, 1 classifier
     bool lds_resident = false;
     // 16-byte layout (IPv6 / IPv4-mapped): classifier over 32-bit reps

@@ -10,13 +10,23 @@
 // stages the image once per workgroup and reads each connection's fields
 // once (13 B), writing 8 B.  The OTHER image (protocols > 2: networks alone
 // decide, evalACL's switch has no case) is staged beside the main image
-// when both fit LDS (no slot counters in this mode).  Those connections are
+// when both fit LDS (no slot counters in this mode), else staged over the
+// main image once every wave has left its main loop (o_late: the drain then
+// reads LDS, not a global-memory template scan -- 6.5 of 27.5 us at 4 Mi
+// connections, profiles/r06pab_pair_breakdown.txt).  Those connections are
 // queued with their fields (16-B entries in the wave's segment: first in the
 // LDS left after the images, then in global memory, its fill a wave-uniform
 // register) and classified on the OTHER image after the wave's main loop,
 // one per lane: the OTHER chain (interval search, candidate scan) then runs
 // once per 64 of them instead of once per wave step that holds any, and no
-// wave waits for the others (no workgroup barrier before the drain).
+// wave waits for the others (no workgroup barrier before the drain).  When
+// the OTHER image's source classes are the main image's (cdiv != 0: same
+// interval bounds and class numbering, checked by the host), an entry
+// carries the two tuples' classes, found by the main loop's lookups, and the
+// drain starts at the class row: its interval search -- 5.4 of the drain's
+// 6.5 us at 4 Mi connections -- is gone (profiles/r06pab_pair_breakdown.txt).
+// The OTHER image's candidates check no ports (evalACL has no case for
+// those protocols), so the entry does not carry them.
 #include "kernels_dev.hpp"
 
 namespace cls {
@@ -30,7 +40,8 @@ __global__ __launch_bounds__(kClsBlock) void classify4_pair(Cls4Dev t, Cls4Dev o
                                                             const uint16_t* sport, uint32_t* out, uint64_t stride,
                                                             uint32_t* oq, uint32_t gqw, uint32_t q_lds,
                                                             const uint32_t* slot_rule, uint32_t ctr_base,
-                                                            uint32_t wbytes, uint32_t lqw) {
+                                                            uint32_t wbytes, uint32_t lqw, uint32_t o_late,
+                                                            uint32_t cdiv) {
     extern __shared__ uint4 smem[];
     const uint32_t lane = __lane_id();
     const uint64_t lt = (1ull << lane) - 1ull;
@@ -44,7 +55,8 @@ __global__ __launch_bounds__(kClsBlock) void classify4_pair(Cls4Dev t, Cls4Dev o
     const uint32_t* PR = reinterpret_cast<const uint32_t*>(p.proto);
     uint4* OS = reinterpret_cast<uint4*>(out);
     uint4* OA = reinterpret_cast<uint4*>(out + stride);
-    // the wave's queue segment: {index, src, dst, dport | sport << 16}
+    // the wave's queue segment: {index, src, dst, dport | sport << 16} or
+    // (cdiv) {index, src, dst, SYN class | SYN-ACK class << 16}
     const uint32_t wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     const uint32_t lq = q_lds + 16u * lqw * (threadIdx.x >> 6);
     uint4* const GQ = reinterpret_cast<uint4*>(oq) + uint64_t(wave) * gqw;
@@ -93,11 +105,12 @@ __global__ __launch_bounds__(kClsBlock) void classify4_pair(Cls4Dev t, Cls4Dev o
     };
     // protocols > 2, both tuples of one connection -- SYN (s, d, dp) and
     // SYN-ACK (d, s, sp) -- on the OTHER image, their two chains interleaved:
-    // result | OTHER slot (after the main image's) << 2
-    auto other2 = [&](uint32_t s, uint32_t d, uint32_t dp, uint32_t sp, uint32_t& w0, uint32_t& w1) {
+    // result | OTHER slot (after the main image's) << 2.  lds: the OTHER
+    // image is in LDS (beside the main one, or staged late for the drain)
+    auto other2 = [&](uint32_t s, uint32_t d, uint32_t dp, uint32_t sp, uint32_t& w0, uint32_t& w1, bool lds) {
         const uint32_t s2[2] = {s, d}, d2[2] = {d, s}, p2[2] = {dp, sp}, z2[2] = {0u, 0u};
         uint32_t r2[2], k2[2];
-        if (o_at) classify_n<2, true, 0, 0, -1>(im, o, s2, d2, p2, z2, r2, k2);
+        if (lds) classify_n<2, true, 0, 0, -1>(im, o, s2, d2, p2, z2, r2, k2);
         else classify_n<2, false, 0, 0, -1>(og, o, s2, d2, p2, z2, r2, k2);
         w0 = r2[0] | (key(t.n_ctr + k2[0]) << 2);
         w1 = r2[1] | (key(t.n_ctr + k2[1]) << 2);
@@ -120,8 +133,8 @@ __global__ __launch_bounds__(kClsBlock) void classify4_pair(Cls4Dev t, Cls4Dev o
             p8[q] = dpa[q]; p8[4 + q] = spa[q];
             r8[q] = r; r8[4 + q] = r;
         }
-        uint32_t rv[8], k8[8];
-        classify_n<8, true, kMode, kList, kD>(im, t, s8, d8, p8, r8, rv, k8);
+        uint32_t rv[8], k8[8], row8[8];
+        classify_n<8, true, kMode, kList, kD>(im, t, s8, d8, p8, r8, rv, k8, &row8);
         uint32_t w0[4], w1[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -148,13 +161,17 @@ __global__ __launch_bounds__(kClsBlock) void classify4_pair(Cls4Dev t, Cls4Dev o
             for (int q = 0; q < 4; ++q)
                 if ((m[q] >> lane) & 1u) {
                     const uint32_t k = base + c[q] + uint32_t(__popcll(m[q] & lt));
-                    const uint4 ent = make_uint4(4u * g + uint32_t(q), s8[q], d8[q], p8[q] | (p8[4 + q] << 16));
+                    // (the class: the row's offset / row_bytes, by ceil(2^32 / row_bytes))
+                    const uint32_t w3 = cdiv ? __umulhi(row8[q] - t.off_cells, cdiv) |
+                                                   __umulhi(row8[4 + q] - t.off_cells, cdiv) << 16
+                                             : p8[q] | (p8[4 + q] << 16);
+                    const uint4 ent = make_uint4(4u * g + uint32_t(q), s8[q], d8[q], w3);
                     if (k < lqw)                // the LDS part of the segment
                         *lds128w_t(lq + 16u * k) = v4u{ent.x, ent.y, ent.z, ent.w};
                     else if (k - lqw < gqw)
                         GQ[k - lqw] = ent;
                     else    // the segment is full (a fixed size per wave): classify in place
-                        other2(s8[q], d8[q], p8[q], p8[4 + q], w0[q], w1[q]);
+                        other2(s8[q], d8[q], p8[q], p8[4 + q], w0[q], w1[q], o_at != 0u);
                 }
         }
         if (wbytes == 1u) {                             // both results of the 4 connections: 4 bytes
@@ -174,7 +191,7 @@ __global__ __launch_bounds__(kClsBlock) void classify4_pair(Cls4Dev t, Cls4Dev o
         const uint32_t s = p.src[i], d = p.dst[i], dp = p.dport[i], sp = sport[i], pr = p.proto[i];
         uint32_t w0, w1;
         if (pr > 2u) {
-            other2(s, d, dp, sp, w0, w1);
+            other2(s, d, dp, sp, w0, w1, o_at != 0u);
         } else {
             const uint32_t sa[1] = {s}, da[1] = {d}, dpa[1] = {dp}, spa[1] = {sp}, ra[1] = {pr};
             uint32_t r[1], k[1];
@@ -189,6 +206,11 @@ __global__ __launch_bounds__(kClsBlock) void classify4_pair(Cls4Dev t, Cls4Dev o
     // fields from the queue entry (no gather from the connection arrays); the
     // wave's own main-loop stores of the same words complete first
     __threadfence_block();
+    if (o_late) {                                       // uniform
+        __syncthreads();                                // every wave is done with the main image
+        lds_copy(smem, reinterpret_cast<const uint4*>(o.img), o.img_bytes / 16u);
+        __syncthreads();
+    }
     // lane 0's fill is current: the main loop's active lanes are a prefix
     const uint32_t nq = min(__builtin_amdgcn_readlane(wq, 0), lqw + gqw);
     for (uint32_t j = lane; j < nq; j += 64u) {
@@ -200,7 +222,17 @@ __global__ __launch_bounds__(kClsBlock) void classify4_pair(Cls4Dev t, Cls4Dev o
             e = GQ[j - lqw];
         }
         uint32_t w0, w1;
-        other2(e.y, e.z, e.w & 0xFFFFu, e.w >> 16, w0, w1);
+        if (cdiv) {                                     // uniform: from the class rows
+            const uint32_t r2[2] = {o.off_cells + (e.w & 0xFFFFu) * o.row_bytes, o.off_cells + (e.w >> 16) * o.row_bytes};
+            const uint32_t d2[2] = {e.z, e.y}, z2[2] = {0u, 0u};
+            uint32_t v2[2], k2[2];
+            if (o_at | o_late) classify_n<2, true, 3, 0, -1>(im, o, r2, d2, z2, z2, v2, k2);
+            else classify_n<2, false, 3, 0, -1>(og, o, r2, d2, z2, z2, v2, k2);
+            w0 = v2[0] | (key(t.n_ctr + k2[0]) << 2);
+            w1 = v2[1] | (key(t.n_ctr + k2[1]) << 2);
+        } else {
+            other2(e.y, e.z, e.w & 0xFFFFu, e.w >> 16, w0, w1, (o_at | o_late) != 0u);
+        }
         put(e.x, w0, w1);
     }
 }
@@ -208,12 +240,14 @@ __global__ __launch_bounds__(kClsBlock) void classify4_pair(Cls4Dev t, Cls4Dev o
 template <int kMode, int kList, int kD>
 void launch_pair_d(const Cls4Dev& t, const Cls4Dev& o, uint32_t o_at, const Pkts4& p, const uint16_t* sport,
                    uint32_t* out, uint64_t stride, uint32_t* oq, uint32_t oq_cap, const uint32_t* slot_rule,
-                   uint32_t ctr_base, uint32_t wbytes, uint32_t lq_cap, const LaunchCfg& cfg) {
-    const uint32_t q_lds = ((o_at ? o_at + o.img_bytes : t.img_bytes) + 15u) & ~15u;   // the waves' LDS segments
+                   uint32_t ctr_base, uint32_t wbytes, uint32_t lq_cap, bool o_late, uint32_t cdiv,
+                   const LaunchCfg& cfg) {
+    const uint32_t q_lds = pair_queue_lds(t.img_bytes, o_at, o.img_bytes, o_late);   // the waves' LDS segments
     const size_t lds = q_lds + size_t(lq_cap) * 16u * (kPairBlock / 64);
     lds_attr<classify4_pair<kMode, kList, kD>>();
     hipLaunchKernelGGL((classify4_pair<kMode, kList, kD>), dim3(cfg.grid), dim3(kClsBlock), lds, cfg.stream, t, o,
-                       o_at, p, sport, out, stride, oq, oq_cap, q_lds, slot_rule, ctr_base, wbytes, lq_cap);
+                       o_at, p, sport, out, stride, oq, oq_cap, q_lds, slot_rule, ctr_base, wbytes, lq_cap,
+                       o_late ? 1u : 0u, cdiv);
 }
 
 // sublist modes: the search depth as a template argument (the rendered
@@ -221,19 +255,21 @@ void launch_pair_d(const Cls4Dev& t, const Cls4Dev& o, uint32_t o_at, const Pkts
 template <int kMode, int kList>
 void launch_pair(const Cls4Dev& t, const Cls4Dev& o, uint32_t o_at, const Pkts4& p, const uint16_t* sport,
                  uint32_t* out, uint64_t stride, uint32_t* oq, uint32_t oq_cap, const uint32_t* slot_rule,
-                 uint32_t ctr_base, uint32_t wbytes, uint32_t lq_cap, const LaunchCfg& cfg) {
+                 uint32_t ctr_base, uint32_t wbytes, uint32_t lq_cap, bool o_late, uint32_t cdiv,
+                 const LaunchCfg& cfg) {
     if constexpr (kMode == 2 && (kList == 3 || kList == 4)) {
         switch (t.bv_steps) {
-        case 0: launch_pair_d<kMode, kList, 0>(t, o, o_at, p, sport, out, stride, oq, oq_cap, slot_rule, ctr_base, wbytes, lq_cap, cfg); return;
-        case 1: launch_pair_d<kMode, kList, 1>(t, o, o_at, p, sport, out, stride, oq, oq_cap, slot_rule, ctr_base, wbytes, lq_cap, cfg); return;
-        case 2: launch_pair_d<kMode, kList, 2>(t, o, o_at, p, sport, out, stride, oq, oq_cap, slot_rule, ctr_base, wbytes, lq_cap, cfg); return;
-        case 3: launch_pair_d<kMode, kList, 3>(t, o, o_at, p, sport, out, stride, oq, oq_cap, slot_rule, ctr_base, wbytes, lq_cap, cfg); return;
-        case 4: launch_pair_d<kMode, kList, 4>(t, o, o_at, p, sport, out, stride, oq, oq_cap, slot_rule, ctr_base, wbytes, lq_cap, cfg); return;
-        case 5: launch_pair_d<kMode, kList, 5>(t, o, o_at, p, sport, out, stride, oq, oq_cap, slot_rule, ctr_base, wbytes, lq_cap, cfg); return;
+        case 0: launch_pair_d<kMode, kList, 0>(t, o, o_at, p, sport, out, stride, oq, oq_cap, slot_rule, ctr_base, wbytes, lq_cap, o_late, cdiv, cfg); return;
+        case 1: launch_pair_d<kMode, kList, 1>(t, o, o_at, p, sport, out, stride, oq, oq_cap, slot_rule, ctr_base, wbytes, lq_cap, o_late, cdiv, cfg); return;
+        case 2: launch_pair_d<kMode, kList, 2>(t, o, o_at, p, sport, out, stride, oq, oq_cap, slot_rule, ctr_base, wbytes, lq_cap, o_late, cdiv, cfg); return;
+        case 3: launch_pair_d<kMode, kList, 3>(t, o, o_at, p, sport, out, stride, oq, oq_cap, slot_rule, ctr_base, wbytes, lq_cap, o_late, cdiv, cfg); return;
+        case 4: launch_pair_d<kMode, kList, 4>(t, o, o_at, p, sport, out, stride, oq, oq_cap, slot_rule, ctr_base, wbytes, lq_cap, o_late, cdiv, cfg); return;
+        case 5: launch_pair_d<kMode, kList, 5>(t, o, o_at, p, sport, out, stride, oq, oq_cap, slot_rule, ctr_base, wbytes, lq_cap, o_late, cdiv, cfg); return;
         default: break;
         }
     }
-    launch_pair_d<kMode, kList, -1>(t, o, o_at, p, sport, out, stride, oq, oq_cap, slot_rule, ctr_base, wbytes, lq_cap, cfg);
+    launch_pair_d<kMode, kList, -1>(t, o, o_at, p, sport, out, stride, oq, oq_cap, slot_rule, ctr_base, wbytes, lq_cap, o_late, cdiv,
+                                    cfg);
 }
 
 }  // namespace
@@ -241,11 +277,11 @@ void launch_pair(const Cls4Dev& t, const Cls4Dev& o, uint32_t o_at, const Pkts4&
 hipError_t launch_classify4_pair(const Cls4Dev& t, const Cls4Dev& o, uint32_t o_at, const Pkts4& p,
                                  const uint16_t* sport, uint32_t* out, uint64_t stride, uint32_t* oq,
                                  uint32_t oq_cap, const uint32_t* slot_rule, uint32_t ctr_base, uint32_t wbytes,
-                                 uint32_t lq_cap, const LaunchCfg& cfg) {
+                                 uint32_t lq_cap, bool o_late, uint32_t cdiv, const LaunchCfg& cfg) {
     if (!cls_dispatchable(t, true, false) || o.mode != 0 || o.list_mode != 0) return hipErrorInvalidValue;
     const int src = src_variant(t);
 #define PAIR_CASE(S, M, L) \
-    case 8 * S + L: launch_pair<M, L>(t, o, o_at, p, sport, out, stride, oq, oq_cap, slot_rule, ctr_base, wbytes, lq_cap, cfg); break;
+    case 8 * S + L: launch_pair<M, L>(t, o, o_at, p, sport, out, stride, oq, oq_cap, slot_rule, ctr_base, wbytes, lq_cap, o_late, cdiv, cfg); break;
     switch (8 * src + int(t.list_mode)) {
         PAIR_CASE(0, 0, 0) PAIR_CASE(0, 0, 1) PAIR_CASE(0, 0, 2) PAIR_CASE(0, 0, 3) PAIR_CASE(0, 0, 4)
         PAIR_CASE(0, 0, 5) PAIR_CASE(0, 0, 6)

@@ -184,10 +184,16 @@ hipError_t launch_classify16_slots(const Cls4Dev& t, const Fe16& fe, const Pkts1
 // out[i] = the SYN tuple (p.src, p.dst, p.dport) and out[stride + i] the
 // SYN-ACK tuple (p.dst, p.src, sport), result | slot << 2 each.  The OTHER
 // image (o, offsets rebased to LDS byte o_at) is staged beside the main one
-// when o_at != 0.  Connections of protocol > 2 go to the wave's queue
+// when o_at != 0; with o_late (o_at 0, offsets image-relative) it is staged
+// at LDS 0, over the main image, once every wave of the workgroup has left
+// its main loop.  Connections of protocol > 2 go to the wave's queue
 // segment -- lq_cap entries in the LDS after the images, then oq_cap in oq
 // (segment w of the grid's waves) -- and are classified on the OTHER image
-// after the wave's main loop, one per lane (in place when the segment is full).
+// after the wave's main loop, one per lane (in place when the segment is
+// full, from global memory unless the image sits beside the main one).
+// cdiv != 0 (ceil(2^32 / t.row_bytes)): the OTHER image's source classes are
+// t's, so a queued connection carries its two classes and the drain skips
+// the OTHER source search.
 // Needs 16-B aligned src / dst / out / out + stride, 8-B dport / sport, 4-B
 // proto; stride a multiple of 4.
 // slot_rule (may be null): write each word's counter index ctr_base +
@@ -199,7 +205,13 @@ hipError_t launch_classify16_slots(const Cls4Dev& t, const Fe16& fe, const Pkts1
 hipError_t launch_classify4_pair(const Cls4Dev& t, const Cls4Dev& o, uint32_t o_at, const Pkts4& p,
                                  const uint16_t* sport, uint32_t* out, uint64_t stride, uint32_t* oq,
                                  uint32_t oq_cap, const uint32_t* slot_rule, uint32_t ctr_base, uint32_t wbytes,
-                                 uint32_t lq_cap, const LaunchCfg& cfg);
+                                 uint32_t lq_cap, bool o_late, uint32_t cdiv, const LaunchCfg& cfg);
+// LDS byte offset of the pair launch's queue segments: after the main image,
+// the OTHER image beside it (o_at != 0), or the larger of the two (o_late)
+inline uint32_t pair_queue_lds(uint32_t img_bytes, uint32_t o_at, uint32_t o_bytes, bool o_late) {
+    const uint32_t end = o_at ? o_at + o_bytes : o_late && o_bytes > img_bytes ? o_bytes : img_bytes;
+    return (end + 15u) & ~15u;
+}
 // The OTHER queue segment of one pair-launch workgroup (kPairBlock threads)
 // that holds every connection its lanes visit, 4 per lane per step, in 16-B
 // entries; the engine caps the segment (oq_cap entries; the overflow is

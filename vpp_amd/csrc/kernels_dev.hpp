@@ -274,11 +274,15 @@ __device__ __forceinline__ void src_row(const Img<kLds>& im, const Cls4Dev& t,
 // First match of N packets (protocols 0-2) against their cells' candidate
 // lists: verdict (ACLAction) and the terminating counter slot (0 = default
 // DENY, aclengine_mock.go:667).
+// row_out (optional): the packets' class rows (byte address of the row of
+// cells), for a caller that classifies some of them again on the OTHER
+// image, whose classes are the same (k4_pair.hip)
 template <int N, bool kLds, int kMode, int kList, int kD>
 __device__ __forceinline__ void classify_n(const Img<kLds>& im, const Cls4Dev& t,
                                            const uint32_t (&src)[N], const uint32_t (&dst)[N],
                                            const uint32_t (&dport)[N], const uint32_t (&proto)[N],
-                                           uint32_t (&res)[N], uint32_t (&slot)[N]) {
+                                           uint32_t (&res)[N], uint32_t (&slot)[N],
+                                           uint32_t (*row_out)[N] = nullptr) {
     // list modes 5, 6: 4, 3 with the wide cells in global memory (t.gcells)
     constexpr bool kWide = kList >= 5;
     constexpr int kPort = kList == 5 ? 4 : kList == 6 ? 3 : kList;
@@ -306,6 +310,10 @@ __device__ __forceinline__ void classify_n(const Img<kLds>& im, const Cls4Dev& t
     }
     uint32_t row[N];
     src_row<N, kLds, kMode>(im, t, src, row);
+    if (row_out) {
+#pragma unroll
+        for (int q = 0; q < N; ++q) (*row_out)[q] = row[q];
+    }
 
     if constexpr (kList >= 3) {
         // Port-filtered sublists.  cell = {pointer table word address | counter

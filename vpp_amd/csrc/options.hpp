@@ -41,6 +41,9 @@ struct Opts {
     uint32_t pair_qcap = 0;     // pair launch: OTHER queue entries per wave (0: sized by the batch)
     bool pair_qcap_set = false;
     bool pair_other_global = false;  // pair launch: the OTHER image read from global memory
+    int pair_other_late = 1;    // pair launch: the OTHER image staged over the main one for the drain when
+                                // it does not fit beside it (2: always -- tests; 0: never)
+    bool pair_class = true;     // pair launch: queued OTHER connections carry their source classes
     int pair_lq = -1;           // pair launch: cap on the OTHER queue entries per wave in LDS
     int conn_no_lds = 0;        // bit 0 rules, bit 1 counters, bit 2 descriptors from global memory
     int conn_wg_per_cu = 0;     // measurements: cap on the connection kernel's workgroups per CU (0: none)
