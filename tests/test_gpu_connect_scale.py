@@ -335,19 +335,26 @@ def test_device_plan_follows_binding_changes(count):
         eng.close()
 
 
-@pytest.mark.parametrize("opts,cfg", [({}, 2), ({"pair_other_global": 1}, 2), ({"pair_qcap": 3}, 2),
-                                      ({"pair_other_global": 1, "pair_qcap": 0}, 2),
-                                      ({"pair_lq": 0}, 2), ({"pair_lq": 2, "pair_qcap": 4}, 2),
-                                      ({"pair_lq": 3}, 2),
-                                      ({}, 3), ({"pair_other_late": 2}, 2), ({"pair_other_late": 2}, 3),
-                                      ({"pair_other_late": 2, "pair_qcap": 3}, 3),
-                                      ({"pair_other_late": 2, "pair_lq": 0}, 3), ({"pair_class": 0}, 3),
-                                      ({"pair_class": 0, "pair_other_late": 2}, 3),
-                                      ({"pair_other_global": 1}, 3)])
+_Q = {"pair_o4": 0}      # the OTHER queue path, not the four-cell pair image
+
+
+@pytest.mark.parametrize("opts,cfg", [({}, 2), ({}, 3), ({"conn_pre_rules": 0}, 3), ({"pair_map_lds": 0}, 3),
+                                      (_Q, 2), (dict(_Q, pair_other_global=1), 2), (dict(_Q, pair_qcap=3), 2),
+                                      (dict(_Q, pair_other_global=1, pair_qcap=0), 2),
+                                      (dict(_Q, pair_lq=0), 2), (dict(_Q, pair_lq=2, pair_qcap=4), 2),
+                                      (dict(_Q, pair_lq=3), 2),
+                                      (_Q, 3), (dict(_Q, pair_other_late=2), 2), (dict(_Q, pair_other_late=2), 3),
+                                      (dict(_Q, pair_other_late=2, pair_qcap=3), 3),
+                                      (dict(_Q, pair_other_late=2, pair_lq=0), 3), (dict(_Q, pair_class=0), 3),
+                                      (dict(_Q, pair_class=0, pair_other_late=2), 3),
+                                      (dict(_Q, pair_other_global=1), 3)])
 def test_pair_launch_tail_and_other_protocols(opts, cfg, capfd):
     """classify4_pair (k4_pair.hip) on a batch of 4k + 3 connections with
     protocol-47 connections everywhere, the last three included (the scalar
-    tail's direct OTHER path): the OTHER image beside the main one in LDS,
+    tail): on the pair image (four cells per class, protocols > 2 with the
+    others: the default where it fits and the batch does not count by slot),
+    or with the OTHER queue (option pair_o4=0, or a counting batch without
+    counter-index words): the OTHER image beside the main one in LDS,
     read from global memory (o_at = 0), or staged over the main image for
     the drain (o_late: the plan when it does not fit beside the main one;
     option pair_other_late=2 forces it), the queued connections carrying
@@ -378,8 +385,15 @@ def test_pair_launch_tail_and_other_protocols(opts, cfg, capfd):
             assert np.array_equal(eng.conn_counters(name, reset=True), wcounts[name]), name
     finally:
         eng.close()
-    pairs = [ln for ln in capfd.readouterr().err.splitlines() if ln.startswith("pair:")]
-    assert pairs
+    lines = [ln for ln in capfd.readouterr().err.splitlines() if ln.startswith("pair:")]
+    pimg = [ln for ln in lines if ln.startswith("pair: pimg")]
+    pairs = [ln for ln in lines if " o_at " in ln]
+    if opts.get("pair_o4", 1) and opts.get("conn_pre_rules", 1):
+        assert pimg, lines
+        # (counting: the slot -> rule map staged in LDS unless pair_map_lds=0)
+        assert any((" map 0 " in ln) == (opts.get("pair_map_lds") == 0) for ln in pimg), pimg
+        return
+    assert pairs and not pimg, lines
     if opts.get("pair_other_late") == 2:
         assert all(" o_at 0 o_late 1 " in ln for ln in pairs), pairs
     if opts.get("pair_class") == 0:

@@ -809,7 +809,8 @@ static bool build_cls4_one(const std::vector<SemRule>& sem, uint32_t n_rules, Cl
     std::unordered_map<std::vector<uint16_t>, uint32_t, VecHash> list_id;
     std::vector<uint16_t> lists;
     // cells per class: TCP, UDP, ICMP (the main image), or OTHER alone
-    const uint32_t pr0 = opt && opt->other ? uint32_t(P_OTHER) : 0u, ncell = opt && opt->other ? 1u : 3u;
+    const uint32_t pr0 = opt && opt->other ? uint32_t(P_OTHER) : 0u;
+    const uint32_t ncell = opt && opt->other ? 1u : opt && opt->with_other ? 4u : 3u;
     img.n_cells = ncell;
     std::vector<uint32_t> cells(size_t(n_classes) * ncell * 2);
     img.ctr_rule.assign(1, n_rules);  // slot 0: default DENY
@@ -1901,6 +1902,14 @@ bool build_other4(const std::vector<SemRule>& sem, uint32_t n_rules, Cls4Image& 
     Cls4Opts opt;
     opt.other = true;
     return build_cls4_one(sem, n_rules, img, why, &opt);
+}
+
+bool build_pair4(const std::vector<SemRule>& sem, uint32_t n_rules, bool swap, Cls4Image& img, std::string& why) {
+    Cls4Opts opt;
+    opt.with_other = true;
+    if (!build_cls4_one(swap ? swap_sides(sem) : sem, n_rules, img, why, &opt)) return false;
+    img.swap = swap ? 1 : 0;
+    return true;
 }
 
 bool build_cls16(const std::vector<SemRule>& sem, uint32_t n_rules, Cls16Image& img, std::string& why) {

@@ -213,11 +213,18 @@ struct Cls4Opts {
     // and template scan, read from global memory by the few lanes holding
     // such a packet (kernels.hip run_n).  Its slots follow the main image's.
     bool other = false;
+    // The pair launch's image (k4_pair.hip): a fourth cell per class for
+    // protocols > 2 beside TCP, UDP and ICMP, so a connection batch
+    // classifies those connections with the others -- no OTHER queue, no
+    // second image.  Its slots are its own (ctr_rule).
+    bool with_other = false;
 };
 
 // The OTHER image of a rule set (in the main image's orientation: pass the
 // swapped rules for a destination-keyed one).
 bool build_other4(const std::vector<SemRule>& sem, uint32_t n_rules, Cls4Image& img, std::string& why);
+// The pair launch's image of `sem` in the orientation `swap` (Cls4Opts::with_other)
+bool build_pair4(const std::vector<SemRule>& sem, uint32_t n_rules, bool swap, Cls4Image& img, std::string& why);
 
 uint32_t lds_budget();
 bool place_counters(Cls4Image& img, uint32_t budget, bool partial);

@@ -260,6 +260,7 @@ static int table_compile(cls_engine* e, const char* name, const cls_rule* rules,
             return fail(e, CLS_E_INVAL, "no classify kernel for the compiled image (mode %u, list mode %u%s)",
                         t->img.mode, t->img.list_mode, t->lds_resident ? "" : ", global memory");
     }
+    if (t->has_cls && t->lds_resident) t->sem4 = std::make_shared<const std::vector<SemRule>>(sem);
     // 16-byte layout: both families' reductions over one rep space
     auto& q = t->p16;
     std::vector<SemRule> s16;
@@ -291,6 +292,7 @@ std::shared_ptr<Table> table_clone_host(const Table& s) {
     t->img = s.img;
     t->oimg = s.oimg;
     t->pair_cdiv = s.pair_cdiv;
+    t->sem4 = s.sem4;                   // (the pair image is built per device, at first use)
     t->kernel = s.kernel;
     t->lds_resident = s.lds_resident;
     t->p16.ok = s.p16.ok;
@@ -524,6 +526,39 @@ static Cls4Dev cls4_dev(const Cls4Image& im, const DevBuf& d_img, const DevBuf& 
 // The v4 classifier of a table (its kernel never reads the linear rules:
 // every protocol has a cell).
 static Cls4Dev table_dev(const Table& t) { return cls4_dev(t.img, t.d_img, DevBuf(), 0, t.n_rules); }
+
+// The pair launch's image of a table (Table::pimg), built and uploaded at
+// its first use; false when the table has none.
+static bool pair_image(cls_engine* e, Table& t) {
+    if (t.pimg_state == 0) {
+        t.pimg_state = -1;
+        std::string why;
+        const CompileScope scope(e->opts);
+        if (t.sem4 && build_pair4(*t.sem4, t.n_rules, t.img.swap != 0, t.pimg, why) && t.pimg.gcells.empty() &&
+            t.pimg.img_bytes + 32u <= uint32_t(max_lds_bytes()) &&
+            cls_kernel_exists(t.pimg.mode, t.pimg.list_mode, true, false) &&
+            upload(e, t.d_pimg, t.pimg) == CLS_OK) {
+            const std::vector<uint32_t>& m = t.pimg.ctr_rule;
+            if (t.d_pslot_rule.ensure(std::max<size_t>(1, m.size()) * 4) == hipSuccess &&
+                (m.empty() || hipMemcpy(t.d_pslot_rule.p, m.data(), m.size() * 4, hipMemcpyHostToDevice) == hipSuccess))
+                t.pimg_state = 1;
+            // ... and as u16 for the launch to stage in LDS beside the image
+            t.pslot16_n16 = 0;
+            if (t.pimg_state > 0 && t.n_rules < 0xFFFFu && !m.empty()) {
+                std::vector<uint16_t> m16((m.size() + 7) & ~size_t(7), 0);
+                for (size_t i = 0; i < m.size(); ++i) m16[i] = uint16_t(m[i]);
+                if (t.d_pslot16.ensure(m16.size() * 2) == hipSuccess &&
+                    hipMemcpy(t.d_pslot16.p, m16.data(), m16.size() * 2, hipMemcpyHostToDevice) == hipSuccess)
+                    t.pslot16_n16 = uint32_t(m16.size() / 8);
+            }
+        }
+        if (t.pimg_state < 0) {
+            t.pimg = Cls4Image();
+            (void)hipGetLastError();
+        }
+    }
+    return t.pimg_state > 0;
+}
 
 // Packets in an image's frame: src and dst exchanged for a destination-keyed one.
 static Pkts4 framed(const Cls4Image& im, const Pkts4& p) {
@@ -1614,7 +1649,32 @@ int connect_locked(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t* ou
                 // Both tuples in one launch when the image is LDS-resident and
                 // the arrays allow 16-B loads; the OTHER image beside the main
                 // one when both fit (no slot counters in this mode)
-                if (pair_ok(t)) {
+                if (pair_ok(t) && e->opts.pair_o4 && (!count || pre_rules) && pair_image(e, t)) {
+                    // the pair image: protocols > 2 in the main loop with the
+                    // others -- no OTHER queue, drain or second image (its
+                    // slots are its own: counting takes the counter-index
+                    // words; option pair_o4=0: the OTHER queue below)
+                    const Cls4Dev pd = cls4_dev(t.pimg, t.d_pimg, DevBuf(), 0, t.n_rules);
+                    // counting: the slot -> rule map in LDS after the image when
+                    // it fits (else each word's rule is a global gather)
+                    PairMap sm;
+                    sm.srl = (t.pimg.img_bytes + 15u) & ~15u;
+                    if (pre_rules && t.pslot16_n16 && e->opts.pair_map_lds &&
+                        sm.srl + 16u * t.pslot16_n16 + 32u <= uint32_t(max_lds_bytes())) {
+                        sm.map = t.d_pslot16.as<uint16_t>();
+                        sm.n16 = t.pslot16_n16;
+                    } else {
+                        sm.srl = 0;
+                    }
+                    cfg.grid = cls_grid(e, true, true, sm.srl ? sm.srl + 16u * sm.n16 : t.pimg.img_bytes, n);
+                    if (e->opts.debug_conn)
+                        std::fprintf(stderr, "pair: pimg %u mode %u list mode %u map %u (img %u oimg %u)\n",
+                                     t.pimg.img_bytes, t.pimg.mode, t.pimg.list_mode, 16u * sm.n16, t.img.img_bytes,
+                                     t.oimg.img_bytes);
+                    HIPC(e, launch_classify4_pair(pd, pd, 0, framed(t.pimg, Pkts4{s4, d4, dp, pr, n}), sp, pre, stride,
+                                                  nullptr, 0, pre_rules ? t.d_pslot_rule.as<uint32_t>() : nullptr,
+                                                  desc[big[b]].ctr_off, pre_bytes, 0, false, 0u, true, sm, cfg));
+                } else if (pair_ok(t)) {
                     uint32_t o_at = (t.img.img_bytes + 15u) & ~15u;
                     // (+ 32: the queue fill word after the images)
                     if (o_at + t.oimg.img_bytes + 32u > uint32_t(max_lds_bytes())) o_at = 0;
@@ -1649,7 +1709,7 @@ int connect_locked(cls_engine* e, const cls_conn_soa* c, uint64_t n, uint8_t* ou
                     HIPC(e, launch_classify4_pair(cd, od, o_at, syn, sp, pre, stride, e->s_pq.as<uint32_t>(), gq,
                                                   pre_rules ? t.d_slot_rule.as<uint32_t>() : nullptr,
                                                   desc[big[b]].ctr_off, pre_bytes, lq_cap, o_late,
-                                                  e->opts.pair_class ? t.pair_cdiv : 0u, cfg));
+                                                  e->opts.pair_class ? t.pair_cdiv : 0u, false, PairMap{}, cfg));
                 } else {
                     cfg.other = cls4_dev(t.oimg, t.d_oimg, DevBuf(), 0, t.n_rules);
                     cfg.grid = cls_grid(e, true, t.lds_resident, t.img.lds_bytes, n);

@@ -107,6 +107,16 @@ struct Table {
     // class numbering): the pair launch's queued connections carry their
     // classes (ceil(2^32 / img.row_bytes); 0: the drain searches again)
     uint32_t pair_cdiv = 0;
+    // The pair launch's image (compile.hpp Cls4Opts::with_other: a fourth
+    // cell per class for protocols > 2), built from sem4 at the table's
+    // first connection batch that takes the pair launch: pimg_state 0 not
+    // yet, 1 built and uploaded, -1 none (too large for LDS, no kernel)
+    std::shared_ptr<const std::vector<SemRule>> sem4;
+    int pimg_state = 0;
+    Cls4Image pimg;
+    DevBuf d_pimg, d_pslot_rule;
+    DevBuf d_pslot16;           // the slot -> rule map as u16 (rules < 65535), 16-B padded; n16 units
+    uint32_t pslot16_n16 = 0;
     int kernel = 0;            // 0 linear, 1 classifier
     bool lds_resident = false;
     // 16-byte layout (IPv6 / IPv4-mapped): classifier over 32-bit reps

@@ -35,13 +35,17 @@ namespace {
 
 static_assert(kClsBlock == kPairBlock, "pair_queue_words sizes the queue for this block");
 
-template <int kMode, int kList, int kD>
+// kO4: t is the pair image (four cells per class, compile.hpp
+// Cls4Opts::with_other): every connection is classified in the main loop,
+// no OTHER queue and no drain (o, o_at, the queue and cdiv unused)
+template <int kMode, int kList, int kD, bool kO4>
 __global__ __launch_bounds__(kClsBlock) void classify4_pair(Cls4Dev t, Cls4Dev o, uint32_t o_at, Pkts4 p,
                                                             const uint16_t* sport, uint32_t* out, uint64_t stride,
                                                             uint32_t* oq, uint32_t gqw, uint32_t q_lds,
                                                             const uint32_t* slot_rule, uint32_t ctr_base,
                                                             uint32_t wbytes, uint32_t lqw, uint32_t o_late,
-                                                            uint32_t cdiv) {
+                                                            uint32_t cdiv, const uint16_t* slot16, uint32_t srl,
+                                                            uint32_t srl_n) {
     extern __shared__ uint4 smem[];
     const uint32_t lane = __lane_id();
     const uint64_t lt = (1ull << lane) - 1ull;
@@ -82,13 +86,19 @@ __global__ __launch_bounds__(kClsBlock) void classify4_pair(Cls4Dev t, Cls4Dev o
     if (tid < nsteps) fetch(tid, nx);
     // both images in one round of loads (a second round is a second memory
     // latency before the first step)
-    lds_copy2(smem, reinterpret_cast<const uint4*>(t.img), t.img_bytes / 16u, o_at / 16u,
-              reinterpret_cast<const uint4*>(o.img), o_at ? o.img_bytes / 16u : 0u);
+    // (srl: the slot -> rule map as u16 at LDS byte srl, srl_n 16-B units;
+    // it takes the OTHER image's place -- the pair image has none)
+    lds_copy2(smem, reinterpret_cast<const uint4*>(t.img), t.img_bytes / 16u, srl ? srl / 16u : o_at / 16u,
+              srl ? reinterpret_cast<const uint4*>(slot16) : reinterpret_cast<const uint4*>(o.img),
+              srl ? srl_n : o_at ? o.img_bytes / 16u : 0u);
     __syncthreads();
     const Img<true> im{nullptr};
     const Img<false> og{reinterpret_cast<const uint8_t*>(o.img)};
     // a word's payload: the slot, or (counting) its counter index
-    auto key = [&](uint32_t slot) { return slot_rule ? ctr_base + slot_rule[slot] : slot; };
+    // (from the LDS copy of the map when there is one)
+    auto key = [&](uint32_t slot) {
+        return srl ? ctr_base + *lds16_t(srl + 2u * slot) : slot_rule ? ctr_base + slot_rule[slot] : slot;
+    };
     // one connection's two words: u32, u16 (wbytes 2: the host keeps the
     // counter indices below 2^14), or (wbytes 1) its two results in one byte
     uint16_t* const out16 = reinterpret_cast<uint16_t*>(out);
@@ -134,7 +144,7 @@ __global__ __launch_bounds__(kClsBlock) void classify4_pair(Cls4Dev t, Cls4Dev o
             r8[q] = r; r8[4 + q] = r;
         }
         uint32_t rv[8], k8[8], row8[8];
-        classify_n<8, true, kMode, kList, kD>(im, t, s8, d8, p8, r8, rv, k8, &row8);
+        classify_n<8, true, kMode, kList, kD, kO4 ? 4 : 3>(im, t, s8, d8, p8, r8, rv, k8, kO4 ? nullptr : &row8);
         uint32_t w0[4], w1[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -144,7 +154,7 @@ __global__ __launch_bounds__(kClsBlock) void classify4_pair(Cls4Dev t, Cls4Dev o
         // Some protocol byte > 2 (SWAR, as classify4_cls): those connections
         // go to the wave's queue segment; their words above are overwritten
         // after the main loop
-        const bool oth = ((pr | ((pr & 0x7F7F7F7Fu) + 0x7D7D7D7Du)) & 0x80808080u) != 0u;
+        const bool oth = !kO4 && ((pr | ((pr & 0x7F7F7F7Fu) + 0x7D7D7D7Du)) & 0x80808080u) != 0u;
         if (__any(oth)) {
             wq = __builtin_amdgcn_readfirstlane(wq);     // (lanes done with the loop keep stale copies)
             uint64_t m[4];
@@ -190,18 +200,19 @@ __global__ __launch_bounds__(kClsBlock) void classify4_pair(Cls4Dev t, Cls4Dev o
     for (uint32_t i = nsteps * 4u + tid; i < uint32_t(p.n); i += nthreads) {
         const uint32_t s = p.src[i], d = p.dst[i], dp = p.dport[i], sp = sport[i], pr = p.proto[i];
         uint32_t w0, w1;
-        if (pr > 2u) {
+        if (!kO4 && pr > 2u) {
             other2(s, d, dp, sp, w0, w1, o_at != 0u);
         } else {
             const uint32_t sa[1] = {s}, da[1] = {d}, dpa[1] = {dp}, spa[1] = {sp}, ra[1] = {pr};
             uint32_t r[1], k[1];
-            classify_n<1, true, kMode, kList, -1>(im, t, sa, da, dpa, ra, r, k);
+            classify_n<1, true, kMode, kList, -1, kO4 ? 4 : 3>(im, t, sa, da, dpa, ra, r, k);
             w0 = r[0] | (key(k[0]) << 2);
-            classify_n<1, true, kMode, kList, -1>(im, t, da, sa, spa, ra, r, k);
+            classify_n<1, true, kMode, kList, -1, kO4 ? 4 : 3>(im, t, da, sa, spa, ra, r, k);
             w1 = r[0] | (key(k[0]) << 2);
         }
         put(i, w0, w1);
     }
+    if constexpr (kO4) return;
     // the wave's queued connections of protocol > 2, one per lane, their
     // fields from the queue entry (no gather from the connection arrays); the
     // wave's own main-loop stores of the same words complete first
@@ -237,39 +248,40 @@ __global__ __launch_bounds__(kClsBlock) void classify4_pair(Cls4Dev t, Cls4Dev o
     }
 }
 
-template <int kMode, int kList, int kD>
+template <int kMode, int kList, int kD, bool kO4>
 void launch_pair_d(const Cls4Dev& t, const Cls4Dev& o, uint32_t o_at, const Pkts4& p, const uint16_t* sport,
                    uint32_t* out, uint64_t stride, uint32_t* oq, uint32_t oq_cap, const uint32_t* slot_rule,
                    uint32_t ctr_base, uint32_t wbytes, uint32_t lq_cap, bool o_late, uint32_t cdiv,
-                   const LaunchCfg& cfg) {
+                   const PairMap& sm, const LaunchCfg& cfg) {
     const uint32_t q_lds = pair_queue_lds(t.img_bytes, o_at, o.img_bytes, o_late);   // the waves' LDS segments
-    const size_t lds = q_lds + size_t(lq_cap) * 16u * (kPairBlock / 64);
-    lds_attr<classify4_pair<kMode, kList, kD>>();
-    hipLaunchKernelGGL((classify4_pair<kMode, kList, kD>), dim3(cfg.grid), dim3(kClsBlock), lds, cfg.stream, t, o,
+    const size_t lds = std::max<size_t>(q_lds + size_t(lq_cap) * 16u * (kPairBlock / 64),
+                                        sm.srl ? sm.srl + 16u * sm.n16 : 0u);
+    lds_attr<classify4_pair<kMode, kList, kD, kO4>>();
+    hipLaunchKernelGGL((classify4_pair<kMode, kList, kD, kO4>), dim3(cfg.grid), dim3(kClsBlock), lds, cfg.stream, t, o,
                        o_at, p, sport, out, stride, oq, oq_cap, q_lds, slot_rule, ctr_base, wbytes, lq_cap,
-                       o_late ? 1u : 0u, cdiv);
+                       o_late ? 1u : 0u, cdiv, sm.map, sm.srl, sm.n16);
 }
 
 // sublist modes: the search depth as a template argument (the rendered
 // global tables' one-length hash, as the hot classify kernel)
-template <int kMode, int kList>
+template <int kMode, int kList, bool kO4>
 void launch_pair(const Cls4Dev& t, const Cls4Dev& o, uint32_t o_at, const Pkts4& p, const uint16_t* sport,
                  uint32_t* out, uint64_t stride, uint32_t* oq, uint32_t oq_cap, const uint32_t* slot_rule,
                  uint32_t ctr_base, uint32_t wbytes, uint32_t lq_cap, bool o_late, uint32_t cdiv,
-                 const LaunchCfg& cfg) {
+                 const PairMap& sm, const LaunchCfg& cfg) {
     if constexpr (kMode == 2 && (kList == 3 || kList == 4)) {
         switch (t.bv_steps) {
-        case 0: launch_pair_d<kMode, kList, 0>(t, o, o_at, p, sport, out, stride, oq, oq_cap, slot_rule, ctr_base, wbytes, lq_cap, o_late, cdiv, cfg); return;
-        case 1: launch_pair_d<kMode, kList, 1>(t, o, o_at, p, sport, out, stride, oq, oq_cap, slot_rule, ctr_base, wbytes, lq_cap, o_late, cdiv, cfg); return;
-        case 2: launch_pair_d<kMode, kList, 2>(t, o, o_at, p, sport, out, stride, oq, oq_cap, slot_rule, ctr_base, wbytes, lq_cap, o_late, cdiv, cfg); return;
-        case 3: launch_pair_d<kMode, kList, 3>(t, o, o_at, p, sport, out, stride, oq, oq_cap, slot_rule, ctr_base, wbytes, lq_cap, o_late, cdiv, cfg); return;
-        case 4: launch_pair_d<kMode, kList, 4>(t, o, o_at, p, sport, out, stride, oq, oq_cap, slot_rule, ctr_base, wbytes, lq_cap, o_late, cdiv, cfg); return;
-        case 5: launch_pair_d<kMode, kList, 5>(t, o, o_at, p, sport, out, stride, oq, oq_cap, slot_rule, ctr_base, wbytes, lq_cap, o_late, cdiv, cfg); return;
+        case 0: launch_pair_d<kMode, kList, 0, kO4>(t, o, o_at, p, sport, out, stride, oq, oq_cap, slot_rule, ctr_base, wbytes, lq_cap, o_late, cdiv, sm, cfg); return;
+        case 1: launch_pair_d<kMode, kList, 1, kO4>(t, o, o_at, p, sport, out, stride, oq, oq_cap, slot_rule, ctr_base, wbytes, lq_cap, o_late, cdiv, sm, cfg); return;
+        case 2: launch_pair_d<kMode, kList, 2, kO4>(t, o, o_at, p, sport, out, stride, oq, oq_cap, slot_rule, ctr_base, wbytes, lq_cap, o_late, cdiv, sm, cfg); return;
+        case 3: launch_pair_d<kMode, kList, 3, kO4>(t, o, o_at, p, sport, out, stride, oq, oq_cap, slot_rule, ctr_base, wbytes, lq_cap, o_late, cdiv, sm, cfg); return;
+        case 4: launch_pair_d<kMode, kList, 4, kO4>(t, o, o_at, p, sport, out, stride, oq, oq_cap, slot_rule, ctr_base, wbytes, lq_cap, o_late, cdiv, sm, cfg); return;
+        case 5: launch_pair_d<kMode, kList, 5, kO4>(t, o, o_at, p, sport, out, stride, oq, oq_cap, slot_rule, ctr_base, wbytes, lq_cap, o_late, cdiv, sm, cfg); return;
         default: break;
         }
     }
-    launch_pair_d<kMode, kList, -1>(t, o, o_at, p, sport, out, stride, oq, oq_cap, slot_rule, ctr_base, wbytes, lq_cap, o_late, cdiv,
-                                    cfg);
+    launch_pair_d<kMode, kList, -1, kO4>(t, o, o_at, p, sport, out, stride, oq, oq_cap, slot_rule, ctr_base, wbytes, lq_cap, o_late, cdiv,
+                                    sm, cfg);
 }
 
 }  // namespace
@@ -277,11 +289,15 @@ void launch_pair(const Cls4Dev& t, const Cls4Dev& o, uint32_t o_at, const Pkts4&
 hipError_t launch_classify4_pair(const Cls4Dev& t, const Cls4Dev& o, uint32_t o_at, const Pkts4& p,
                                  const uint16_t* sport, uint32_t* out, uint64_t stride, uint32_t* oq,
                                  uint32_t oq_cap, const uint32_t* slot_rule, uint32_t ctr_base, uint32_t wbytes,
-                                 uint32_t lq_cap, bool o_late, uint32_t cdiv, const LaunchCfg& cfg) {
-    if (!cls_dispatchable(t, true, false) || o.mode != 0 || o.list_mode != 0) return hipErrorInvalidValue;
+                                 uint32_t lq_cap, bool o_late, uint32_t cdiv, bool o4, const PairMap& sm,
+                                 const LaunchCfg& cfg) {
+    if (!cls_dispatchable(t, true, false) || (!o4 && (o.mode != 0 || o.list_mode != 0))) return hipErrorInvalidValue;
     const int src = src_variant(t);
 #define PAIR_CASE(S, M, L) \
-    case 8 * S + L: launch_pair<M, L>(t, o, o_at, p, sport, out, stride, oq, oq_cap, slot_rule, ctr_base, wbytes, lq_cap, o_late, cdiv, cfg); break;
+    case 8 * S + L: \
+        if (o4) launch_pair<M, L, true>(t, o, 0u, p, sport, out, stride, oq, oq_cap, slot_rule, ctr_base, wbytes, lq_cap, false, 0u, sm, cfg); \
+        else launch_pair<M, L, false>(t, o, o_at, p, sport, out, stride, oq, oq_cap, slot_rule, ctr_base, wbytes, lq_cap, o_late, cdiv, PairMap{}, cfg); \
+        break;
     switch (8 * src + int(t.list_mode)) {
         PAIR_CASE(0, 0, 0) PAIR_CASE(0, 0, 1) PAIR_CASE(0, 0, 2) PAIR_CASE(0, 0, 3) PAIR_CASE(0, 0, 4)
         PAIR_CASE(0, 0, 5) PAIR_CASE(0, 0, 6)

@@ -180,6 +180,12 @@ hipError_t launch_classify4_slots(const Cls4Dev& t, const Pkts4& p, uint32_t* ou
                                   const LaunchCfg& cfg);
 hipError_t launch_classify16_slots(const Cls4Dev& t, const Fe16& fe, const Pkts16& p, uint32_t* out,
                                    bool lds_resident, const LaunchCfg& cfg);
+// The pair image's slot -> rule map as u16 (map, n16 16-B units), staged at
+// LDS byte srl after the image (0: none; the launch reads slot_rule)
+struct PairMap {
+    const uint16_t* map = nullptr;
+    uint32_t srl = 0, n16 = 0;
+};
 // Both tuples of a connection batch in one launch (LDS-resident IPv4 image):
 // out[i] = the SYN tuple (p.src, p.dst, p.dport) and out[stride + i] the
 // SYN-ACK tuple (p.dst, p.src, sport), result | slot << 2 each.  The OTHER
@@ -193,7 +199,9 @@ hipError_t launch_classify16_slots(const Cls4Dev& t, const Fe16& fe, const Pkts1
 // full, from global memory unless the image sits beside the main one).
 // cdiv != 0 (ceil(2^32 / t.row_bytes)): the OTHER image's source classes are
 // t's, so a queued connection carries its two classes and the drain skips
-// the OTHER source search.
+// the OTHER source search.  o4: t is the pair image (compile.hpp
+// Cls4Opts::with_other, four cells per class): protocols > 2 are classified
+// with the others -- no queue, no OTHER image, slots of t's own.
 // Needs 16-B aligned src / dst / out / out + stride, 8-B dport / sport, 4-B
 // proto; stride a multiple of 4.
 // slot_rule (may be null): write each word's counter index ctr_base +
@@ -205,7 +213,8 @@ hipError_t launch_classify16_slots(const Cls4Dev& t, const Fe16& fe, const Pkts1
 hipError_t launch_classify4_pair(const Cls4Dev& t, const Cls4Dev& o, uint32_t o_at, const Pkts4& p,
                                  const uint16_t* sport, uint32_t* out, uint64_t stride, uint32_t* oq,
                                  uint32_t oq_cap, const uint32_t* slot_rule, uint32_t ctr_base, uint32_t wbytes,
-                                 uint32_t lq_cap, bool o_late, uint32_t cdiv, const LaunchCfg& cfg);
+                                 uint32_t lq_cap, bool o_late, uint32_t cdiv, bool o4, const PairMap& sm,
+                                 const LaunchCfg& cfg);
 // LDS byte offset of the pair launch's queue segments: after the main image,
 // the OTHER image beside it (o_at != 0), or the larger of the two (o_late)
 inline uint32_t pair_queue_lds(uint32_t img_bytes, uint32_t o_at, uint32_t o_bytes, bool o_late) {

@@ -276,8 +276,11 @@ __device__ __forceinline__ void src_row(const Img<kLds>& im, const Cls4Dev& t,
 // DENY, aclengine_mock.go:667).
 // row_out (optional): the packets' class rows (byte address of the row of
 // cells), for a caller that classifies some of them again on the OTHER
-// image, whose classes are the same (k4_pair.hip)
-template <int N, bool kLds, int kMode, int kList, int kD>
+// image, whose classes are the same (k4_pair.hip).  kCells: cells per class
+// row -- 3 (TCP, UDP, ICMP; protocols > 2 go to the OTHER image), or 4 (the
+// pair launch's image, compile.hpp Cls4Opts::with_other: the fourth cell for
+// protocols > 2).
+template <int N, bool kLds, int kMode, int kList, int kD, int kCells = 3>
 __device__ __forceinline__ void classify_n(const Img<kLds>& im, const Cls4Dev& t,
                                            const uint32_t (&src)[N], const uint32_t (&dst)[N],
                                            const uint32_t (&dport)[N], const uint32_t (&proto)[N],
@@ -332,7 +335,7 @@ __device__ __forceinline__ void classify_n(const Img<kLds>& im, const Cls4Dev& t
             uint2 wc[N];
 #pragma unroll
             for (int q = 0; q < N; ++q)
-                wc[q] = *reinterpret_cast<const uint2*>(t.gcells + row[q] + 8u * min(proto[q], 2u));
+                wc[q] = *reinterpret_cast<const uint2*>(t.gcells + row[q] + 8u * min(proto[q], uint32_t(kCells - 1)));
 #pragma unroll
             for (int q = 0; q < N; ++q) {
                 cell[q] = wc[q].y;
@@ -340,7 +343,7 @@ __device__ __forceinline__ void classify_n(const Img<kLds>& im, const Cls4Dev& t
             }
         } else {
 #pragma unroll
-            for (int q = 0; q < N; ++q) cell[q] = im.u32(row[q] + 4u * min(proto[q], 2u));
+            for (int q = 0; q < N; ++q) cell[q] = im.u32(row[q] + 4u * min(proto[q], uint32_t(kCells - 1)));
 #pragma unroll
             for (int q = 0; q < N; ++q) st[q] = im.u32(((cell[q] & 0x3FFFu) << 2) + pc[q]);
         }
@@ -384,7 +387,7 @@ __device__ __forceinline__ void classify_n(const Img<kLds>& im, const Cls4Dev& t
         uint32_t cb[N], ad[N], ap[N], rlo[N], rhi[N], md[N], mp[N];
 #pragma unroll
         for (int q = 0; q < N; ++q) {
-            const uint32_t cell = im.u32(row[q] + 4u * min(proto[q], 2u));
+            const uint32_t cell = im.u32(row[q] + 4u * min(proto[q], uint32_t(kCells - 1)));
             cb[q] = cell >> 16;
             ad[q] = (cell & 0xFFFFu) * 8u;
             ap[q] = ad[q] + (8u << S);
@@ -438,7 +441,7 @@ __device__ __forceinline__ void classify_n(const Img<kLds>& im, const Cls4Dev& t
         bool act[N];
 #pragma unroll
         for (int q = 0; q < N; ++q) {
-            const uint2 cell = im.u64(row[q] + 8u * min(proto[q], 2u));
+            const uint2 cell = im.u64(row[q] + 8u * min(proto[q], uint32_t(kCells - 1)));
             start[q] = cell.x & 0xFFFFu;
             len[q] = cell.x >> 16;
             cb[q] = cell.y;

@@ -69,6 +69,8 @@ bool opts_set(Opts& o, const char* key, const char* value, std::string& why) {
     OPT("conn_pre_narrow", conn_pre_narrow, b)
     OPT("pair_other_global", pair_other_global, b)
     OPT("pair_other_late", pair_other_late, i)
+    OPT("pair_o4", pair_o4, b)
+    OPT("pair_map_lds", pair_map_lds, b)
     OPT("pair_class", pair_class, b)
     OPT("pair_lq", pair_lq, i)
     OPT("conn_no_lds", conn_no_lds, i)

@@ -43,6 +43,8 @@ struct Opts {
     bool pair_other_global = false;  // pair launch: the OTHER image read from global memory
     int pair_other_late = 1;    // pair launch: the OTHER image staged over the main one for the drain when
                                 // it does not fit beside it (2: always -- tests; 0: never)
+    bool pair_o4 = true;        // pair launch: the four-cell pair image where it fits (else the OTHER queue)
+    bool pair_map_lds = true;   // pair image, counting: the slot -> rule map staged in LDS
     bool pair_class = true;     // pair launch: queued OTHER connections carry their source classes
     int pair_lq = -1;           // pair launch: cap on the OTHER queue entries per wave in LDS
     int conn_no_lds = 0;        // bit 0 rules, bit 1 counters, bit 2 descriptors from global memory
