@@ -141,7 +141,7 @@ class Image:
         """Bit-vector lists: per list, masks of the entries covering the dst
         interval and the port interval; first match = lowest common bit."""
         img = np.frombuffer(self._img, np.uint32)
-        pr = np.minimum(proto, 2).astype(np.int64)
+        pr = np.minimum(proto, self.ncell - 1).astype(np.int64)
         cells1 = np.frombuffer(self._img, np.uint32, count=self.h.n_classes * self.ncell,
                                offset=self.h.off_cells)
         cell = cells1[cls * self.ncell + pr]
@@ -210,7 +210,7 @@ class Image:
         entries {start - 1, state}, a probe of step i reads 8 << i bytes on and
         moves the state when start - 1 < dst; outcome = result | (j + 1) << 2."""
         img = np.frombuffer(self._img, np.uint32).astype(np.int64)
-        pr = np.minimum(proto, 2).astype(np.int64)
+        pr = np.minimum(proto, self.ncell - 1).astype(np.int64)
         pc4 = self._port_class4(dport)                # class x 4
         if self.h.list_mode >= 5:
             # wide cells (list modes 5, 6) in global memory: {pointer table byte address, counter base}
@@ -281,7 +281,7 @@ class Image:
             return self._classify_bv3(cls, src, dst, dport, proto, counters)
         if self.h.list_mode >= 1:
             return self._classify_bv(cls, src, dst, dport, proto, counters)
-        pr = np.minimum(proto, 2).astype(np.int64)
+        pr = np.minimum(proto, self.ncell - 1).astype(np.int64)
         cell = self.cells[cls * self.ncell + pr]
         start = (cell[:, 0] & 0xFFFF).astype(np.int64)
         ln = (cell[:, 0] >> 16).astype(np.int64)

@@ -2248,6 +2248,13 @@ int cls_compile_v4(const cls_rule* rules, uint32_t n, void* blob, uint64_t cap, 
     std::vector<LinRule4> lin = linear4(sem);
     Cls4Image img, oimg;
     const bool has = sem.size() > 8 && build_pair(sem, n, img, oimg, why);
+    if (has && o.pair4) {
+        // (option pair4: the connection pair launch's four-cell image, in the
+        // main image's orientation, instead -- CPU tests of that compile)
+        Cls4Image pimg;
+        if (!build_pair4(sem, n, img.swap != 0, pimg, why)) return CLS_E_INVAL;
+        return write_blob(&pimg, lin, n, 0x434C5334u, nullptr, 0, blob, cap, need, nullptr, 0, nullptr);
+    }
     return write_blob(has ? &img : nullptr, lin, n, 0x434C5334u, nullptr, 0, blob, cap, need, nullptr, 0,
                       has ? &oimg : nullptr);
 }

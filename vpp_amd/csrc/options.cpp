@@ -59,6 +59,7 @@ bool opts_set(Opts& o, const char* key, const char* value, std::string& why) {
     OPT("v16_src_search", v16_src_search, i)
     OPT("v16_src_trie", v16_src_trie, i)
     OPT("debug_modes", debug_modes, b)
+    OPT("pair4", pair4, b)
     OPT("other_cap", other_cap, uint32_t(x))
     OPT("wg_per_cu", wg_per_cu, i)
     OPT("debug_floor", debug_floor, b)

@@ -28,6 +28,7 @@ struct Opts {
     int v16_src_trie = -1;      // 16-byte front end: 1 the source trie, 0 never
     int orient = -1;            // 0 source-keyed, 1 destination-keyed (-1: the better one)
     bool debug_modes = false;   // stderr: why a list mode was refused
+    bool pair4 = false;         // cls_compile_v4: the connection pair launch's four-cell image (tests)
     // ---- classify launches (engine.cpp) -----------------------------------
     uint32_t other_cap = 0;     // OTHER queue entries per workgroup (0: sized by the batch)
     int wg_per_cu = 0;          // classify workgroups per CU (0: by LDS)
