@@ -8,25 +8,30 @@
 // evaluated here for both tuples of every connection; the connection kernel
 // then reads the two result words instead of scanning the ACL.  One launch
 // stages the image once per workgroup and reads each connection's fields
-// once (13 B), writing 8 B.  The OTHER image (protocols > 2: networks alone
-// decide, evalACL's switch has no case) is staged beside the main image
-// when both fit LDS (no slot counters in this mode), else staged over the
-// main image once every wave has left its main loop (o_late: the drain then
-// reads LDS, not a global-memory template scan -- 6.5 of 27.5 us at 4 Mi
-// connections, profiles/r06pab_pair_breakdown.txt).  Those connections are
-// queued with their fields (16-B entries in the wave's segment: first in the
-// LDS left after the images, then in global memory, its fill a wave-uniform
-// register) and classified on the OTHER image after the wave's main loop,
-// one per lane: the OTHER chain (interval search, candidate scan) then runs
-// once per 64 of them instead of once per wave step that holds any, and no
-// wave waits for the others (no workgroup barrier before the drain).  When
-// the OTHER image's source classes are the main image's (cdiv != 0: same
-// interval bounds and class numbering, checked by the host), an entry
-// carries the two tuples' classes, found by the main loop's lookups, and the
-// drain starts at the class row: its interval search -- 5.4 of the drain's
-// 6.5 us at 4 Mi connections -- is gone (profiles/r06pab_pair_breakdown.txt).
-// The OTHER image's candidates check no ports (evalACL has no case for
-// those protocols), so the entry does not carry them.
+// once (13 B), writing 1 B (the two results) or two counter-index words.
+//
+// The default image (kO4) is the table's pair image: a fourth cell per
+// source class for protocols > 2 (networks alone decide, evalACL's switch
+// has no case for them), so every connection takes the main loop's eight
+// interleaved chains.  That replaced the path below, whose OTHER queue
+// upkeep and end-of-launch drain were 3.1 and 6.7 of its 27.4 us at 4 Mi
+// connections (profiles/r06pab_pair_breakdown.txt; 17.6-18.4 us on the pair
+// image, profiles/r06o4_pair_image_ab.txt).
+//
+// The OTHER-queue path (the main image plus the OTHER image; tables whose
+// pair image does not fit LDS, batches counting by slot): the OTHER image is
+// staged beside the main image when both fit LDS, else over the main image
+// once every wave has left its main loop (o_late; global memory before:
+// 30.4 against 28.5 us when forced on config 3).  Connections of protocol
+// > 2 are queued with their fields (16-B entries in the wave's segment:
+// first in the LDS left after the images, then in global memory, its fill a
+// wave-uniform register) and classified on the OTHER image after the wave's
+// main loop, one per lane.  When the OTHER image's source classes are the
+// main image's (cdiv != 0: same interval bounds and class numbering, checked
+// by the host), an entry carries the two tuples' classes, found by the main
+// loop's lookups, and the drain starts at the class row (27.3 -> 26.3 us).
+// The OTHER image's candidates check no ports, so the entry does not carry
+// them.
 #include "kernels_dev.hpp"
 
 namespace cls {
