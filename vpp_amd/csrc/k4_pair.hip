@@ -105,14 +105,13 @@ __global__ __launch_bounds__(kClsBlock) void classify4_pair(Cls4Dev t, Cls4Dev o
         return srl ? ctr_base + *lds16_t(srl + 2u * slot) : slot_rule ? ctr_base + slot_rule[slot] : slot;
     };
     // one connection's two words: u32, u16 (wbytes 2: the host keeps the
-    // counter indices below 2^14), or (wbytes 1) its two results in one byte
-    uint16_t* const out16 = reinterpret_cast<uint16_t*>(out);
+    // counter indices below 2^14; both in one u32), or (wbytes 1) its two
+    // results in one byte
     auto put = [&](uint32_t i, uint32_t w0, uint32_t w1) {
         if (wbytes == 1u) {
             reinterpret_cast<uint8_t*>(out)[i] = uint8_t((w0 & 3u) | (w1 & 3u) << 2);
         } else if (wbytes == 2u) {
-            out16[i] = uint16_t(w0);
-            out16[stride + i] = uint16_t(w1);
+            out[i] = (w0 & 0xFFFFu) | w1 << 16;
         } else {
             out[i] = w0;
             out[stride + i] = w1;
@@ -194,9 +193,8 @@ __global__ __launch_bounds__(kClsBlock) void classify4_pair(Cls4Dev t, Cls4Dev o
 #pragma unroll
             for (int q = 0; q < 4; ++q) v |= ((w0[q] & 3u) | (w1[q] & 3u) << 2) << (8 * q);
             reinterpret_cast<uint32_t*>(out)[g] = v;
-        } else if (wbytes == 2u) {                      // 4 u16 words per tuple: 8 bytes each
-            reinterpret_cast<uint2*>(out16)[g] = make_uint2(w0[0] | w0[1] << 16, w0[2] | w0[3] << 16);
-            reinterpret_cast<uint2*>(out16 + stride)[g] = make_uint2(w1[0] | w1[1] << 16, w1[2] | w1[3] << 16);
+        } else if (wbytes == 2u) {                      // SYN | SYN-ACK << 16 per connection: 16 bytes
+            OS[g] = make_uint4(w0[0] | w1[0] << 16, w0[1] | w1[1] << 16, w0[2] | w1[2] << 16, w0[3] | w1[3] << 16);
         } else {
             OS[g] = make_uint4(w0[0], w0[1], w0[2], w0[3]);
             OA[g] = make_uint4(w1[0], w1[1], w1[2], w1[3]);

@@ -697,12 +697,8 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kCount == 
 #pragma unroll
                 for (uint32_t b = 0; b < kConnEarlyBlocks; ++b)
                     if (b < a.n_big) {
-                        if (a.pre_bytes == 1u) {
-                            ew[b] = reinterpret_cast<const uint8_t*>(a.pre)[uint64_t(b) * stride + ic];
-                        } else {
-                            const uint16_t* p16 = reinterpret_cast<const uint16_t*>(a.pre) + uint64_t(2u * b) * stride + ic;
-                            ew[b] = uint32_t(p16[0]) | uint32_t(p16[stride]) << 16;
-                        }
+                        if (a.pre_bytes == 1u) ew[b] = reinterpret_cast<const uint8_t*>(a.pre)[uint64_t(b) * stride + ic];
+                        else ew[b] = a.pre[uint64_t(b) * stride + ic];      // SYN | SYN-ACK << 16
                     }
             }
         }
@@ -727,9 +723,8 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kCount == 
                        ? uint32_t(*(bi[k] >= 0 ? reinterpret_cast<const uint8_t*>(a.pre) + uint64_t(uint32_t(bi[k])) * stride + ic
                                                : reinterpret_cast<const uint8_t*>(a.src_if) + ic)) >> (2 * (k >> 1))
                    : a.pre_bytes == 2u
-                       ? uint32_t(*(bi[k] >= 0 ? reinterpret_cast<const uint16_t*>(a.pre) +
-                                                     (uint64_t(2u * uint32_t(bi[k]) + uint32_t(k >> 1)) * stride + ic)
-                                               : reinterpret_cast<const uint16_t*>(a.src_if) + ic))
+                       ? (*(bi[k] >= 0 ? a.pre + uint64_t(uint32_t(bi[k])) * stride + ic : at(a.src_if, ic)) >>
+                          (16u * uint32_t(k >> 1))) & 0xFFFFu
                        : *(bi[k] >= 0 ? a.pre + (uint64_t(2u * uint32_t(bi[k]) + uint32_t(k >> 1)) * stride + ic)
                                       : at(a.src_if, ic));
         // ---- the jobs of the wave, packed ----

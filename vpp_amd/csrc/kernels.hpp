@@ -207,7 +207,8 @@ struct PairMap {
 // slot_rule (may be null): write each word's counter index ctr_base +
 // slot_rule[slot] in place of the slot (counting connection batches).
 // wbytes: 4 -- u32 words (SYN at out[i], SYN-ACK at out[stride + i]); 2 --
-// u16 words at the same element offsets (counter indices < 2^14); 1 -- only
+// u16 words (counter indices < 2^14), the two in one u32 at out[i] (SYN |
+// SYN-ACK << 16: one load for the connection kernel); 1 -- only
 // the two ACLActions, one byte per connection (SYN result | SYN-ACK result
 // << 2) at byte i (batches that do not count)
 hipError_t launch_classify4_pair(const Cls4Dev& t, const Cls4Dev& o, uint32_t o_at, const Pkts4& p,
@@ -308,8 +309,9 @@ struct ConnArgs {
     uint32_t n_big;              // blocks at pre (the large ACLs); <= kConnEarlyBlocks: every block's
                                  // words loaded with the connection's fields, before the interfaces
     uint32_t pre_rules;          // the words carry counter indices (descriptor base + rule), not slots
-    uint32_t pre_bytes;          // the words' width: 4; 2 (u16 counter-index words, block b at
-                                 // (uint16_t*) pre + 2 b pre_stride); 1 (block b is one byte per
+    uint32_t pre_bytes;          // the words' width: 4; 2 (u16 counter-index words, both tuples'
+                                 // in one u32 per connection, SYN | SYN-ACK << 16, block b at
+                                 // pre + b pre_stride); 1 (block b is one byte per
                                  // connection at (uint8_t*) pre + b pre_stride: SYN result |
                                  // SYN-ACK result << 2, batches that do not count)
     uint32_t bm_steps;           // bitmap forms: lower-bound steps of the largest interval table
